@@ -1,0 +1,221 @@
+#!/usr/bin/env python3
+"""Headline benchmark: Ray-SD + SVAO AO frames on MI355X (BASELINE.json metric
+"Mrays/s + AO frames/s, 1080p 1/4-res Ray-SD").
+
+A step = one AO frame of the reference's SVAO::execute span (SVAO.cpp:327-455: clear
+ray intervals, "AO 1", StochasticDepthMapRT, "AO 2") over the configs[1] workload:
+Sun Temple stand-in (~0.6 M triangles, seed 2), 1920x1080 visible + 64-px guard band
+(2048x1208 frame buffer), 1/4-res SD map (768x558 texels incl. the 128-texel SD guard),
+N = 4, MAX_COUNT = 8.  Inputs (BVH, G-buffer) are resident in HBM before timing.
+
+  value            = SD rays dispatched per frame * frames / timed wall  (Mrays/s, whole job)
+  ao_frames_per_s  = frames / timed wall
+  sd_kernel_mrays  = SD rays / SD-kernel time (HIP events around the trace launch)
+
+Multi-GPU (torchrun, one rank per GPU): the frame is sharded by screen band.  Every
+rank holds the replicated BVH and G-buffer, runs pass 1 over the whole frame (exact
+ray intervals, no all-reduce), traces its band of SD rows, all-gathers the SD map,
+runs pass 2 on its band of AO rows and all-gathers the AO image (RCCL over xGMI).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+PKG = ROOT / "ray-traced-stochastic-depth-map_amd"
+for p in (str(ROOT), str(PKG)):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8 TB/s (spec)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="suntemple_1080p_q")
+    ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0,
+                    help="target wall time of the bounded CPU-oracle sample (0 disables)")
+    ap.add_argument("--pmc-csv", default=None, help="rocprofv3 --pmc counter_collection.csv for roofline.traffic")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+
+    from rsd.frame import CONFIGS, FrameConfig, Renderer
+    from rsd.scenes import make_scene
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    kw, scene_name = CONFIGS[args.config]
+    cfg = FrameConfig(**kw)
+    scene = make_scene(scene_name)
+    r = Renderer(scene, cfg, device=local)
+    r.gbuffer()
+    torch.cuda.synchronize()
+
+    # instrumented trace (not timed): traversal counters for the roofline bytes
+    r.clear_intervals()
+    r.pass1()
+    cnt = r.sd_trace(counters=True)
+    torch.cuda.synchronize()
+
+    stream = torch.cuda.current_stream()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+
+    def frame(i=None):
+        r.clear_intervals()
+        r.pass1()
+        if i is not None:
+            ev[i][0].record(stream)
+        r.sd_trace()
+        if i is not None:
+            ev[i][1].record(stream)
+        r.pass2()
+
+    for _ in range(args.warmup):
+        frame()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        frame(i)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([wall], device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        wall = float(t.item())
+
+    sd_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    rays = r.sd_rays
+    N = cfg.sd_samples
+    # B_ray = 16 (linearZ bilinear) + 8 (rayMin+rayMax) + 4N (store) + 64 n_node + 48 n_tri
+    alg_bytes = rays * (16 + 8 + 4 * N) + 64 * cnt.nodes_visited + 48 * cnt.tris_tested
+    achieved = alg_bytes / (sd_ms * 1e-3) / 1e9
+    traffic = None
+    if args.pmc_csv and Path(args.pmc_csv).exists():
+        traffic = pmc_traffic(args.pmc_csv, "sd_trace_kernel")
+
+    if rank != 0:
+        if dist:
+            dist.destroy_process_group()
+        return
+
+    cpu = None
+    if args.cpu_baseline_seconds > 0 and world == 1:
+        cpu = cpu_baseline(r, scene, args.cpu_baseline_seconds)
+
+    frames_per_s = args.steps / wall
+    value = rays * frames_per_s / 1e6 * 1.0
+    line = {
+        "metric": "Mrays/s + AO frames/s, 1080p 1/4-res Ray-SD, 1/2/4/8 MI355X",
+        "value": round(value, 3),
+        "unit": "Mrays/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(wall / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (seeded procedural stand-in scene; no reference assets in the container)",
+        "config": {"workload": args.config, "scene": scene_name, "triangles": scene.triangle_count,
+                   "frame_buffer": [cfg.fb_w, cfg.fb_h], "visible": [cfg.visible_w, cfg.visible_h],
+                   "sd_map": [r.sd_w, r.sd_h], "sd_samples": N, "max_count": cfg.max_count,
+                   "stoch_map_divisor": cfg.divisor, "parallelism": f"screen-band x{world}"},
+        "ao_frames_per_s": round(frames_per_s, 2),
+        "sd_kernel_ms": round(sd_ms, 4),
+        "sd_kernel_mrays_per_s": round(rays / (sd_ms * 1e-3) / 1e6, 2),
+        "active_rays": int(cnt.rays_active),
+        "traversal": {"nodes_per_ray": round(cnt.nodes_visited / rays, 3),
+                      "tris_per_ray": round(cnt.tris_tested / rays, 3),
+                      "nodes_per_active_ray": round(cnt.nodes_visited / max(cnt.rays_active, 1), 2),
+                      "tris_per_active_ray": round(cnt.tris_tested / max(cnt.rays_active, 1), 2)},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     "kernel": "sd_trace_kernel", "alg_bytes_per_launch": int(alg_bytes)},
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(line))
+    if dist:
+        dist.destroy_process_group()
+
+
+def pmc_traffic(csv_path, kernel_substr):
+    """HBM bytes per launch from a rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE csv (KB units; FETCH_SIZE
+    doubled on gfx950 per MI355X_MICROARCH.md §HBM)."""
+    import csv
+    per = {}
+    with open(csv_path) as f:
+        for row in csv.DictReader(f):
+            if kernel_substr not in row.get("Kernel_Name", ""):
+                continue
+            name, val = row.get("Counter_Name"), float(row.get("Counter_Value", 0))
+            per.setdefault(name, []).append(val)
+    if not per:
+        return None
+    fetch = sum(per.get("FETCH_SIZE", [0])) / max(len(per.get("FETCH_SIZE", [1])), 1)
+    write = sum(per.get("WRITE_SIZE", [0])) / max(len(per.get("WRITE_SIZE", [1])), 1)
+    return int((2 * fetch + write) * 1024)
+
+
+def cpu_baseline(r, scene, target_s):
+    """The CPU oracle (kind 'port') on a bounded sample of SD rows of the same frame."""
+    import numpy as np
+
+    from oracle import oracle as O
+    sys.path.insert(0, str(ROOT / "tests"))
+    from helpers import to_oracle
+
+    g = r.numpy()
+    cores = min(os.cpu_count() or 1, 16)
+    osc = O.Scene(scene.positions, scene.indices, scene.flags)
+    cam, sdp = to_oracle(r.cam, O.Camera), to_oracle(r.sdp, O.SDParams)
+    # rows in the middle of the map hold the most active rays: sample there
+    mid = r.sd_h // 2
+    rows = 8
+    t0 = time.perf_counter()
+    O.sd_trace(osc, cam, sdp, g["depth"], g["ray_min"], g["ray_max"], r.sd_w, r.sd_h, rows=(mid, mid + rows),
+               threads=cores)
+    dt = time.perf_counter() - t0
+    rows = int(min(r.sd_h, max(8, rows * target_s / max(dt, 1e-3))))
+    y0 = max(0, mid - rows // 2)
+    y1 = min(r.sd_h, y0 + rows)
+    t0 = time.perf_counter()
+    sd, stats = O.sd_trace(osc, cam, sdp, g["depth"], g["ray_min"], g["ray_max"], r.sd_w, r.sd_h, rows=(y0, y1),
+                           threads=cores)
+    dt = time.perf_counter() - t0
+    n = (y1 - y0) * r.sd_w
+    # the sample's share of the GPU result must be bit-identical (the baseline computes the same thing)
+    same = bool(np.array_equal(sd[:, y0:y1].view(np.uint32), g["sd"][:, y0:y1].view(np.uint32)))
+    return {"value": round(n / dt / 1e6, 4), "unit": "Mrays/s", "cores": cores, "kind": "port",
+            "sample": f"SD rows {y0}-{y1} of {r.sd_h} ({n} rays, {int(stats[0])} active), oracle pthreads",
+            "seconds": round(dt, 2), "bit_identical_to_gpu": same}
+
+
+if __name__ == "__main__":
+    main()

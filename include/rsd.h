@@ -1,0 +1,187 @@
+/*
+ * rsd.h -- C ABI of librsd, the MI355X-native Ray-SD + SVAO hot path.
+ *
+ * This is the drop-in boundary.  In the reference the hot path is reached through
+ * Falcor's plugin ABI (Plugin.cpp:56-91 dlopen + registerPlugin) and the RenderPass
+ * virtuals (RenderPass.h:119-259); each pass's execute() records DXR / compute
+ * dispatches.  librsd exports those dispatches as plain C entry points: device
+ * pointers, sizes and a HIP stream, no C++ or torch types.  The C++ RenderPass
+ * mirror (csrc/host/) and the Python graph front end (falcor/) call exactly these.
+ *
+ * Conventions:
+ *   - every entry point returns rsd_status; never throws across the ABI;
+ *     rsd_last_error() gives a thread-local message for the last failure;
+ *   - the caller owns every d_* buffer (device memory);
+ *   - compute entry points are asynchronous and ordered on the given stream
+ *     (rsd_stream = hipStream_t; NULL = the legacy default stream);
+ *   - one rsd_device per GPU per host thread; scenes are bound to a device.
+ */
+#ifndef RSD_H
+#define RSD_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RSD_ABI_VERSION 1
+
+typedef enum {
+    RSD_OK = 0,
+    RSD_ERR_INVALID_ARG = 1,
+    RSD_ERR_UNSUPPORTED = 2,
+    RSD_ERR_HIP = 3,
+    RSD_ERR_OUT_OF_MEMORY = 4,
+    RSD_ERR_NO_DEVICE = 5,
+} rsd_status;
+
+typedef struct rsd_device rsd_device;
+typedef struct rsd_scene rsd_scene;
+typedef void* rsd_stream; /* hipStream_t */
+
+/* Scene ingest (replaces Scene::initGeomDesc/buildBlas/buildTlas, Scene.cpp:2688-2830,
+ * 3091, 3628-3739).  A world-space triangle soup; triangle_flags per triangle:
+ *   bit0 double-sided (TriangleFacingCullDisable, Scene.cpp:3452)
+ *   bit1 front face clockwise (TriangleFrontCounterClockwise, Scene.cpp:3451)
+ *   bit2 alpha-masked material (AlphaMode::Mask; alpha test not yet supported)
+ * Primitive id = triangle index in this array.                                        */
+#define RSD_TRI_DOUBLE_SIDED 1u
+#define RSD_TRI_FRONT_CW 2u
+#define RSD_TRI_ALPHA_MASK 4u
+
+typedef struct {
+    const float* positions;   /* float3[vertex_count] (host) */
+    uint32_t vertex_count;
+    const uint32_t* indices;  /* uint32[3 * triangle_count] (host) */
+    uint32_t triangle_count;
+    const uint32_t* triangle_flags; /* uint32[triangle_count] or NULL (all 0) */
+} rsd_scene_desc;
+
+typedef struct {
+    uint32_t triangle_count;
+    uint32_t node_count;      /* BVH2 inner nodes (64 B each) */
+    uint32_t max_depth;
+    uint32_t leaf_count;
+    double sah_cost;
+    double build_ms;
+    uint64_t device_bytes;
+} rsd_scene_info;
+
+/* Camera data mirror (CameraData.slang:35-68 subset), 32 floats. */
+typedef struct {
+    float posW[3];  float nearZ;
+    float U[3];     float farZ;
+    float V[3];     float focalLength;
+    float W[3];     float frameHeight;
+    float frameWidth; float jitterX; float jitterY; float aspectRatio;
+    float viewMat[16]; /* row-major */
+} rsd_camera;
+
+/* StochasticDepthMapRT Properties -> shader defines (StochasticDepthMapRT.cpp:262-276) */
+typedef enum { RSD_SD_DEFAULT = 0, RSD_SD_COVERAGE_MASK = 1, RSD_SD_RESERVOIR_SAMPLING = 2, RSD_SD_KBUFFER = 3 } rsd_sd_impl;
+typedef enum { RSD_CULL_NONE = 0, RSD_CULL_BACK = 1, RSD_CULL_FRONT = 2 } rsd_cull_mode;
+
+typedef struct {
+    uint32_t sample_count;   /* SampleCount N: 1, 2, 4, 8 (reference) or 16 (extension) */
+    uint32_t implementation; /* rsd_sd_impl (ReservoirSampling is raster-only -> unsupported) */
+    uint32_t max_count;      /* MaxCount (MAX_COUNT) */
+    int32_t guard_band;      /* GuardBand (GUARD_BAND), SD texels */
+    uint32_t jitter;         /* Jitter (SD_JITTER) */
+    uint32_t normalize;      /* normalize (NORMALIZE) */
+    uint32_t ray_interval;   /* RayInterval (USE_RAY_INTERVAL) */
+    uint32_t cull_mode;      /* CullMode (CULL_MODE_RAY_FLAG) */
+    uint32_t alpha_test;     /* AlphaTest (USE_ALPHA_TEST); opaque scenes only for now */
+    float alpha;             /* Alpha (ALPHA), coverage-mask implementation */
+} rsd_sd_params;
+
+/* VAOData.slang:33-45 mirror */
+typedef struct {
+    float noiseScale[2];
+    float resolution[2];
+    float lowResolution[2];
+    float invResolution[2];
+    float radius;
+    float exponent;
+    float thickness;
+    int32_t sdGuard;
+    float ssRadiusCutoff;
+    float ssMaxRadius;
+} rsd_vao_data;
+
+/* SVAO compile-time defines (SVAO.cpp:221-237) + the per-frame guardBand */
+typedef struct {
+    uint32_t num_directions;       /* NUM_DIRECTIONS (8) */
+    uint32_t sd_samples;           /* MSAA_SAMPLES = SD N */
+    uint32_t secondary_depth_mode; /* DepthMode: 0 SingleDepth, 2 StochasticDepth */
+    uint32_t ray_interval;         /* USE_RAY_INTERVAL */
+    uint32_t sd_jitter;            /* SD_JITTER */
+    uint32_t guard_band;           /* dict["guardBand"] from the GuardBand pass */
+} rsd_svao_params;
+
+/* Traversal counters of the last instrumented trace (roofline bytes) */
+typedef struct {
+    uint64_t rays_dispatched;
+    uint64_t rays_active;     /* TMin <= TMax after the ray interval */
+    uint64_t nodes_visited;   /* 64-B BVH2 nodes fetched */
+    uint64_t tris_tested;     /* 48-B triangle records fetched */
+    uint64_t hits_delivered;  /* any-hit invocations (sorted stream) */
+} rsd_counters;
+
+/* --- library / device ------------------------------------------------------------ */
+uint32_t rsd_abi_version(void);
+const char* rsd_last_error(void);
+rsd_status rsd_device_open(int hip_device, rsd_device** out);
+void rsd_device_close(rsd_device* dev);
+
+/* --- scene (BVH2 build on the host, upload to HBM) --------------------------------- */
+rsd_status rsd_scene_upload(rsd_device* dev, const rsd_scene_desc* desc, rsd_scene** out);
+rsd_status rsd_scene_info_get(const rsd_scene* scene, rsd_scene_info* out);
+void rsd_scene_release(rsd_scene* scene);
+
+/* --- host helpers (no GPU work) ---------------------------------------------------- */
+/* Camera::calculateCameraParameters (Camera.cpp:99-185), preserveHeight = true */
+rsd_status rsd_camera_look_at(const float pos[3], const float target[3], const float up[3],
+                              float focal_length, float frame_height, float aspect_ratio,
+                              float near_z, float far_z, float focal_distance, rsd_camera* out);
+/* SVAO::compile / getStochMapSize / getExtraGuardBand (SVAO.cpp:143-150, 700-723):
+ * fb_w x fb_h frame buffer, divisor, SD guard band in full-res pixels (mStochMapGuardBand). */
+rsd_status rsd_svao_make_vao_data(uint32_t fb_w, uint32_t fb_h, uint32_t divisor, int32_t sd_guard_px,
+                                  float radius, float exponent, float thickness,
+                                  rsd_vao_data* out, uint32_t* sd_w, uint32_t* sd_h);
+
+/* --- GPU passes (stream-ordered, asynchronous) ------------------------------------- */
+/* Primary visibility (GBufferRaster -> LinearizeDepth -> CompressNormals):
+ * linear view depth (R32F) and view-space octahedral 2x8 face normal (R16Uint). */
+rsd_status rsd_gbuffer(rsd_scene* scene, const rsd_camera* cam, uint32_t width, uint32_t height,
+                       uint32_t cull_mode, float* d_linear_z, uint16_t* d_normals, rsd_stream stream);
+
+/* StochasticDepthMapRT::execute (StochasticDepthMapRT.cpp:231-331) + rayGen/anyHit
+ * (StochasticDepthMapRT.rt.slang:39-105).  d_sd_out layout = Texture2DArray:
+ * [layer][y][x][ch], ch = min(N,4), layers = ceil(N/4).  d_ray_min / d_ray_max may be
+ * NULL (no interval).  If `counters` is non-NULL, an instrumented kernel fills it
+ * (synchronises the stream). */
+rsd_status rsd_sd_trace(rsd_scene* scene, const rsd_camera* cam, const rsd_sd_params* params,
+                        const float* d_linear_z, uint32_t z_w, uint32_t z_h,
+                        const uint32_t* d_ray_min, const uint32_t* d_ray_max,
+                        float* d_sd_out, uint32_t sd_w, uint32_t sd_h,
+                        rsd_counters* counters, rsd_stream stream);
+
+/* SVAO.cpp:330-341: rayMax <- 0, rayMin <- asuint(FLT_MAX) */
+rsd_status rsd_svao_clear_intervals(uint32_t* d_ray_min, uint32_t* d_ray_max, uint32_t count, rsd_stream stream);
+
+/* "AO 1": SVAORaster.ps.slang:29-122, dispatched as SVAO.cpp:344-350 */
+rsd_status rsd_svao_pass1(const rsd_camera* cam, const rsd_vao_data* vao, const rsd_svao_params* params,
+                          const float* d_depth, const uint16_t* d_normals, uint32_t width, uint32_t height,
+                          uint8_t* d_ao, uint8_t* d_stencil, uint32_t* d_ray_min, uint32_t* d_ray_max,
+                          uint32_t sd_w, uint32_t sd_h, rsd_stream stream);
+
+/* "AO 2": SVAORaster2.ps.slang:48-65 / calcAO2 (Common.slang:523-663), SVAO.cpp:450-454 */
+rsd_status rsd_svao_pass2(const rsd_camera* cam, const rsd_vao_data* vao, const rsd_svao_params* params,
+                          const float* d_depth, const uint16_t* d_normals, uint32_t width, uint32_t height,
+                          const uint8_t* d_stencil, const float* d_sd, uint32_t sd_w, uint32_t sd_h,
+                          uint8_t* d_ao, rsd_stream stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RSD_H */

@@ -1,0 +1,223 @@
+"""ctypes front end of the CPU oracle (oracle/rsd_oracle.c).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg -- never by the product package.  Inputs are
+numpy arrays and plain Python values; outputs are numpy arrays.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+from pathlib import Path
+
+import numpy as np
+
+_HERE = Path(__file__).resolve().parent
+_LIB_PATH = _HERE / "_build" / "librsd_oracle.so"
+
+
+def build(quiet: bool = True) -> Path:
+    subprocess.run(["make", "-C", str(_HERE)], check=True,
+                   stdout=subprocess.DEVNULL if quiet else None)
+    return _LIB_PATH
+
+
+class Camera(C.Structure):
+    _fields_ = [("posW", C.c_float * 3), ("nearZ", C.c_float),
+                ("U", C.c_float * 3), ("farZ", C.c_float),
+                ("V", C.c_float * 3), ("focalLength", C.c_float),
+                ("W", C.c_float * 3), ("frameHeight", C.c_float),
+                ("frameWidth", C.c_float), ("jitterX", C.c_float), ("jitterY", C.c_float),
+                ("aspectRatio", C.c_float), ("viewMat", C.c_float * 16)]
+
+
+class SDParams(C.Structure):
+    _fields_ = [("sample_count", C.c_uint32), ("implementation", C.c_uint32), ("max_count", C.c_uint32),
+                ("guard_band", C.c_int32), ("jitter", C.c_uint32), ("normalize", C.c_uint32),
+                ("ray_interval", C.c_uint32), ("cull_mode", C.c_uint32), ("alpha_test", C.c_uint32),
+                ("alpha", C.c_float)]
+
+
+class VAOData(C.Structure):
+    _fields_ = [("noiseScale", C.c_float * 2), ("resolution", C.c_float * 2),
+                ("lowResolution", C.c_float * 2), ("invResolution", C.c_float * 2),
+                ("radius", C.c_float), ("exponent", C.c_float), ("thickness", C.c_float),
+                ("sdGuard", C.c_int32), ("ssRadiusCutoff", C.c_float), ("ssMaxRadius", C.c_float)]
+
+
+class SVAOParams(C.Structure):
+    _fields_ = [("num_directions", C.c_uint32), ("sd_samples", C.c_uint32),
+                ("secondary_depth_mode", C.c_uint32), ("ray_interval", C.c_uint32),
+                ("sd_jitter", C.c_uint32), ("guard_band", C.c_uint32)]
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not _LIB_PATH.exists():
+            build()
+        L = C.CDLL(str(_LIB_PATH))
+        vp, u32, i32, f32 = C.c_void_p, C.c_uint32, C.c_int, C.c_float
+        L.ocpu_scene_create.restype = vp
+        L.ocpu_scene_create.argtypes = [vp, u32, vp, u32, vp]
+        L.ocpu_scene_destroy.argtypes = [vp]
+        L.ocpu_scene_node_count.restype = u32
+        L.ocpu_scene_node_count.argtypes = [vp]
+        L.ocpu_camera_look_at.argtypes = [vp, vp, vp, f32, f32, f32, f32, f32, f32, vp]
+        L.ocpu_gbuffer.argtypes = [vp, vp, u32, u32, u32, vp, vp, i32]
+        L.ocpu_sd_trace.argtypes = [vp, vp, vp, vp, u32, u32, vp, vp, vp, u32, u32, u32, u32, i32, vp]
+        L.ocpu_sd_ray.argtypes = [vp, vp, vp, u32, u32, vp, vp, u32, u32, u32, u32, vp, vp, vp, vp]
+        L.ocpu_svao_clear.argtypes = [vp, vp, u32]
+        L.ocpu_svao_pass1.argtypes = [vp, vp, vp, vp, vp, u32, u32, vp, vp, vp, vp, u32, u32]
+        L.ocpu_svao_pass2.argtypes = [vp, vp, vp, vp, vp, u32, u32, vp, vp, u32, u32, vp, i32]
+        L.ocpu_hash.restype = f32
+        L.ocpu_hash.argtypes = [f32, f32]
+        L.ocpu_jitter.argtypes = [u32, u32, vp, vp]
+        L.ocpu_stratified_lut.argtypes = [i32, vp, vp]
+        L.ocpu_noise_texture.argtypes = [vp]
+        L.ocpu_sample_radius.restype = f32
+        L.ocpu_sample_radius.argtypes = [u32, u32]
+        L.ocpu_encode_normal_2x8.restype = u32
+        L.ocpu_encode_normal_2x8.argtypes = [vp]
+        L.ocpu_decode_normal_2x8.argtypes = [u32, vp]
+        L.ocpu_intersect.restype = i32
+        L.ocpu_intersect.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp]
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    return a.ctypes.data_as(C.c_void_p) if a is not None else None
+
+
+def _threads(n):
+    return int(n) if n else (os.cpu_count() or 1)
+
+
+class Scene:
+    def __init__(self, positions, indices, flags=None):
+        self.positions = np.ascontiguousarray(positions, np.float32)
+        self.indices = np.ascontiguousarray(indices, np.uint32)
+        self.flags = np.ascontiguousarray(flags if flags is not None else np.zeros(len(self.indices)), np.uint32)
+        self.h = lib().ocpu_scene_create(_p(self.positions), len(self.positions), _p(self.indices),
+                                         len(self.indices), _p(self.flags))
+
+    @property
+    def node_count(self):
+        return lib().ocpu_scene_node_count(self.h)
+
+    def __del__(self):
+        if getattr(self, "h", None) and _lib is not None:
+            _lib.ocpu_scene_destroy(self.h)
+            self.h = None
+
+
+def camera_look_at(pos, target, up, focal_length=21.0, frame_height=24.0, aspect=16 / 9, near=0.1, far=1000.0,
+                   focal_distance=10000.0) -> Camera:
+    cam = Camera()
+    f3 = lambda v: np.ascontiguousarray(v, np.float32)
+    p, t, u = f3(pos), f3(target), f3(up)
+    lib().ocpu_camera_look_at(_p(p), _p(t), _p(u), focal_length, frame_height, aspect, near, far, focal_distance,
+                              C.byref(cam))
+    return cam
+
+
+def gbuffer(scene: Scene, cam: Camera, W, H, cull_mode=1, threads=None):
+    z = np.zeros((H, W), np.float32)
+    n = np.zeros((H, W), np.uint16)
+    lib().ocpu_gbuffer(scene.h, C.byref(cam), W, H, cull_mode, _p(z), _p(n), _threads(threads))
+    return z, n
+
+
+def sd_trace(scene: Scene, cam: Camera, params: SDParams, linearZ, rayMin, rayMax, sdW, sdH,
+             rows=None, threads=None):
+    N = params.sample_count
+    ch, layers = min(N, 4), (N + 3) // 4
+    sd = np.zeros((layers, sdH, sdW, ch), np.float32)
+    r0, r1 = rows if rows else (0, sdH)
+    stats = np.zeros(2, np.uint64)
+    lz = np.ascontiguousarray(linearZ, np.float32)
+    lib().ocpu_sd_trace(scene.h, C.byref(cam), C.byref(params), _p(lz), lz.shape[1], lz.shape[0],
+                        _p(rayMin), _p(rayMax), _p(sd), sdW, sdH, r0, r1, _threads(threads), _p(stats))
+    return sd, stats
+
+
+def sd_ray(cam: Camera, params: SDParams, linearZ, rayMin, rayMax, sdW, sdH, x, y):
+    out = np.zeros(6, np.float32)
+    tmin, tmax, cosT = C.c_float(), C.c_float(), C.c_float()
+    lz = np.ascontiguousarray(linearZ, np.float32)
+    lib().ocpu_sd_ray(C.byref(cam), C.byref(params), _p(lz), lz.shape[1], lz.shape[0], _p(rayMin), _p(rayMax),
+                      sdW, sdH, x, y, _p(out), C.byref(tmin), C.byref(tmax), C.byref(cosT))
+    return out[:3], out[3:], tmin.value, tmax.value, cosT.value
+
+
+def svao_pass1(cam, vao: VAOData, p: SVAOParams, depth, normals, sdW, sdH):
+    H, W = depth.shape
+    ao = np.zeros((H, W), np.uint8)
+    st = np.zeros((H, W), np.uint8)
+    rmin = np.zeros((sdH, sdW), np.uint32)
+    rmax = np.zeros((sdH, sdW), np.uint32)
+    lib().ocpu_svao_clear(_p(rmin), _p(rmax), sdW * sdH)
+    lib().ocpu_svao_pass1(C.byref(cam), C.byref(vao), C.byref(p), _p(depth), _p(normals), W, H,
+                          _p(ao), _p(st), _p(rmin), _p(rmax), sdW, sdH)
+    return ao, st, rmin, rmax
+
+
+def svao_pass2(cam, vao: VAOData, p: SVAOParams, depth, normals, stencil, sd, ao, threads=None):
+    H, W = depth.shape
+    ao = np.array(ao, np.uint8, copy=True)
+    sdH, sdW = sd.shape[1], sd.shape[2]
+    sdc = np.ascontiguousarray(sd, np.float32)
+    lib().ocpu_svao_pass2(C.byref(cam), C.byref(vao), C.byref(p), _p(depth), _p(normals), W, H,
+                          _p(stencil), _p(sdc), sdW, sdH, _p(ao), _threads(threads))
+    return ao
+
+
+def hash2(x, y):
+    return lib().ocpu_hash(float(x), float(y))
+
+
+def jitter(x, y):
+    a, b = C.c_float(), C.c_float()
+    lib().ocpu_jitter(x, y, C.byref(a), C.byref(b))
+    return a.value, b.value
+
+
+def stratified_lut(n):
+    idx = np.zeros(n + 1, np.int32)
+    lut = np.zeros(1 << n, np.uint32)
+    lib().ocpu_stratified_lut(n, _p(idx), _p(lut))
+    return idx, lut
+
+
+def noise_texture():
+    out = np.zeros(16, np.uint8)
+    lib().ocpu_noise_texture(_p(out))
+    return out
+
+
+def sample_radius(nd, i):
+    return lib().ocpu_sample_radius(nd, i)
+
+
+def encode_normal(n):
+    a = np.ascontiguousarray(n, np.float32)
+    return lib().ocpu_encode_normal_2x8(_p(a))
+
+
+def decode_normal(packed):
+    out = np.zeros(3, np.float32)
+    lib().ocpu_decode_normal_2x8(int(packed), _p(out))
+    return out
+
+
+def intersect(o, d, v0, v1, v2):
+    f = lambda v: np.ascontiguousarray(v, np.float32)
+    t, u, v, det = C.c_float(), C.c_float(), C.c_float(), C.c_float()
+    hit = lib().ocpu_intersect(_p(f(o)), _p(f(d)), _p(f(v0)), _p(f(v1)), _p(f(v2)),
+                               C.byref(t), C.byref(u), C.byref(v), C.byref(det))
+    return bool(hit), t.value, u.value, v.value, det.value

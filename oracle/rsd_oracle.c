@@ -1,0 +1,1120 @@
+/*
+ * rsd_oracle.c -- CPU ORACLE (test infrastructure only; see rsd_oracle.h).
+ *
+ * Scalar C restatement of the Ray-SD + SVAO reference shaders.  Compile with
+ * -ffp-contract=off: every float expression below is evaluated operation by
+ * operation, in the order written, like the product kernels.
+ *
+ * Numerics contract shared with the product (DESIGN.md "Numerics"):
+ *  - float ops are IEEE binary32, round-to-nearest, no contraction;
+ *  - normalize(v) = v * (1 / sqrt(dot(v,v)))  (Falcor VectorMath.h:1731 rsqrt form);
+ *  - sin/cos/pow of a float argument = (float)libm(double)  ("accurate" transcendental;
+ *    HLSL leaves the precision of sin/pow implementation-defined);
+ *  - bilinear filtering uses 8 fractional sub-texel bits (D3D11_SUBTEXEL_FRACTIONAL_BIT_COUNT);
+ *  - any-hit calls arrive in ascending (t, primitive id) order, at most once per triangle.
+ */
+#include "rsd_oracle.h"
+#include <math.h>
+#include <float.h>
+#include <stdlib.h>
+#include <string.h>
+#include <pthread.h>
+
+#define O_FLT_MAX 3.402823466e+38f
+
+/* ------------------------------------------------------------------ vector helpers */
+static inline float o_dot(const float a[3], const float b[3]) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+static inline void o_cross(const float a[3], const float b[3], float r[3])
+{
+    r[0] = a[1] * b[2] - a[2] * b[1];
+    r[1] = a[2] * b[0] - a[0] * b[2];
+    r[2] = a[0] * b[1] - a[1] * b[0];
+}
+static inline void o_normalize(const float v[3], float r[3])
+{
+    float inv = 1.0f / sqrtf(o_dot(v, v));
+    r[0] = v[0] * inv; r[1] = v[1] * inv; r[2] = v[2] * inv;
+}
+static inline float o_len(const float v[3]) { return sqrtf(o_dot(v, v)); }
+/* HLSL saturate/min/max: a NaN operand yields the other operand (saturate(NaN) = 0) */
+static inline float o_saturate(float x) { return !(x > 0.0f) ? 0.0f : (x > 1.0f ? 1.0f : x); }
+static inline float o_sin(float x) { return (float)sin((double)x); }
+static inline float o_cos(float x) { return (float)cos((double)x); }
+static inline float o_pow(float x, float y) { return (float)pow((double)x, (double)y); }
+static inline float o_max(float a, float b) { return fmaxf(a, b); }
+static inline float o_min(float a, float b) { return fminf(a, b); }
+static inline uint32_t o_asuint(float f) { uint32_t u; memcpy(&u, &f, 4); return u; }
+static inline float o_asfloat(uint32_t u) { float f; memcpy(&f, &u, 4); return f; }
+
+/* R8Unorm store: saturate, round to nearest (D3D FLOAT->UNORM); NaN -> 0 */
+static inline uint8_t o_unorm8(float x)
+{
+    if (x != x) return 0;
+    x = o_saturate(x);
+    return (uint8_t)floorf(x * 255.0f + 0.5f);
+}
+static inline float o_unorm8_to_float(uint8_t c) { return (float)c / 255.0f; }
+
+/* ------------------------------------------------------------------ constant tables */
+/* Jitter.slangh:20 -- sobol 2d jitter table, indexed (y%4)*4 + x%4 */
+static const float k_jitter[16][2] = {
+    {0.6483604982495308f, 0.914070401340723f},   {0.7279119342565536f, 0.1037941575050354f},
+    {0.48886989802122116f, 0.699178121984005f},  {0.3848271369934082f, 0.25951504334807396f},
+    {0.1555836834013462f, 0.8020274639129639f},  {0.2205628715455532f, 0.2412630058825016f},
+    {0.9962188489735126f, 0.5846633277833462f},  {0.8776040785014629f, 0.3954884633421898f},
+    {0.9271227307617664f, 0.831196017563343f},   {0.9490576796233654f, 0.14202157780528069f},
+    {0.20916065946221352f, 0.5476771481335163f}, {0.16468944773077965f, 0.4869129806756973f},
+    {0.43544455617666245f, 0.9515445046126842f}, {0.44085410237312317f, 0.011881716549396515f},
+    {0.7173641100525856f, 0.6695209294557571f},  {0.6563677340745926f, 0.35924511030316353f},
+};
+
+/* SVAO/Common.slang:53 -- VAO sample radii for NUM_DIRECTIONS = 8 */
+static const float k_radius8[8] = {0.917883f, 0.564429f, 0.734504f, 0.359545f,
+                                   0.820004f, 0.470149f, 0.650919f, 0.205215f};
+
+/* Jitter.slangh:27-50 randomJitter */
+void ocpu_jitter(uint32_t x, uint32_t y, float* jx, float* jy)
+{
+    uint32_t idx = (y % 4u) * 4u + (x % 4u);
+    *jx = k_jitter[idx][0];
+    *jy = k_jitter[idx][1];
+}
+
+float ocpu_sample_radius(uint32_t num_directions, uint32_t i)
+{
+    if (num_directions == 8 && i < 8) return k_radius8[i];
+    return 0.0f;
+}
+
+/* SVAO.cpp:663-688 genNoiseTexture: 4x4 Bayer dither -> R8Unorm bytes */
+void ocpu_noise_texture(uint8_t out[16])
+{
+    static const float dither[16] = {0.0f, 8.0f, 2.0f, 10.0f, 12.0f, 4.0f, 14.0f, 6.0f,
+                                     3.0f, 11.0f, 1.0f, 9.0f, 15.0f, 7.0f, 13.0f, 5.0f};
+    for (int i = 0; i < 16; ++i) out[i] = (uint8_t)(dither[i] / 16.0f * 255.0f);
+}
+
+/* StochasticDepthMapRT.cpp:79-124: binomial-ordered popcount look-up table */
+static int o_binomial(int n, int k)
+{
+    int C[64];
+    memset(C, 0, sizeof(C));
+    C[0] = 1;
+    for (int i = 1; i <= n; i++)
+        for (int j = (i < k ? i : k); j > 0; j--) C[j] = C[j] + C[j - 1];
+    return C[k];
+}
+void ocpu_stratified_lut(int n, int32_t* indices, uint32_t* lut)
+{
+    uint32_t maxEntries = 1u << n;
+    indices[0] = 0;
+    for (int i = 1; i <= n; i++) indices[i] = o_binomial(n, i - 1) + indices[i - 1];
+    int32_t cur[33];
+    for (int i = 0; i <= n; i++) cur[i] = indices[i];
+    lut[0] = 0;
+    for (uint32_t i = 1; i < maxEntries; i++) {
+        int pc = __builtin_popcount(i);
+        lut[cur[pc]] = i;
+        cur[pc]++;
+    }
+}
+
+/* Common.slangh:36-39 -- hash from "Improved Alpha Testing Using Hashed Sampling" */
+float ocpu_hash(float x, float y)
+{
+    float a = 17.0f * x + 0.1f * y;
+    float b = 13.0f * y + x;
+    float r = 1.0e4f * o_sin(a) * (0.1f + fabsf(o_sin(b)));
+    return r - floorf(r); /* frac */
+}
+
+/* ------------------------------------------------------------------ normal packing */
+/* FormatConversion.slang:49-53 */
+static int o_float_to_snorm8(float v)
+{
+    v = (v != v) ? 0.0f : o_min(o_max(v, -1.0f), 1.0f);
+    return (int)truncf(v * 127.0f + (v >= 0.0f ? 0.5f : -0.5f));
+}
+/* MathHelpers.slang:156-159 */
+static void o_oct_wrap(const float v[2], float r[2])
+{
+    r[0] = (1.0f - fabsf(v[1])) * (v[0] >= 0.0f ? 1.0f : -1.0f);
+    r[1] = (1.0f - fabsf(v[0])) * (v[1] >= 0.0f ? 1.0f : -1.0f);
+}
+/* PackedFormats.slang:35-39 + MathHelpers.slang:166-172 + FormatConversion.slang:91-95 */
+uint32_t ocpu_encode_normal_2x8(const float n[3])
+{
+    float s = 1.0f / (fabsf(n[0]) + fabsf(n[1]) + fabsf(n[2]));
+    float p[2] = {n[0] * s, n[1] * s};
+    if (n[2] < 0.0f) {
+        float w[2];
+        o_oct_wrap(p, w);
+        p[0] = w[0]; p[1] = w[1];
+    }
+    return ((uint32_t)o_float_to_snorm8(p[0]) & 0xffu) | (((uint32_t)o_float_to_snorm8(p[1]) << 8) & 0xff00u);
+}
+/* PackedFormats.slang:44-48 + FormatConversion.slang:81-86 + MathHelpers.slang:186-191 */
+void ocpu_decode_normal_2x8(uint32_t packed, float out[3])
+{
+    int bx = (int)(int8_t)(uint8_t)(packed & 0xffu);
+    int by = (int)(int8_t)(uint8_t)((packed >> 8) & 0xffu);
+    float p[2] = {o_max((float)bx / 127.0f, -1.0f), o_max((float)by / 127.0f, -1.0f)};
+    float n[3] = {p[0], p[1], 1.0f - fabsf(p[0]) - fabsf(p[1])};
+    if (n[2] < 0.0f) {
+        float w[2];
+        o_oct_wrap(n, w);
+        n[0] = w[0]; n[1] = w[1];
+    }
+    o_normalize(n, out);
+}
+
+/* ------------------------------------------------------------------ camera */
+/* Camera.cpp:99-185 (calculateCameraParameters), MatrixMath.h:686-712 (RightHanded look-at),
+ * FalcorMath.h:123-126 (focalLengthToFovY).  preserveHeight = true. */
+void ocpu_camera_look_at(const float pos[3], const float target[3], const float up[3],
+                         float focalLength, float frameHeight, float aspectRatio,
+                         float nearZ, float farZ, float focalDistance, ocam* c)
+{
+    memset(c, 0, sizeof(*c));
+    for (int i = 0; i < 3; ++i) c->posW[i] = pos[i];
+    c->nearZ = nearZ;
+    c->farZ = farZ;
+    c->focalLength = focalLength;
+    c->frameHeight = frameHeight;
+    c->aspectRatio = aspectRatio;
+    c->frameWidth = frameHeight * aspectRatio;
+    float fovY = focalLength == 0.0f ? 0.0f : 2.0f * atanf(0.5f * frameHeight / focalLength);
+
+    /* view matrix */
+    float emc[3] = {pos[0] - target[0], pos[1] - target[1], pos[2] - target[2]};
+    float f[3], r[3], u[3], t[3];
+    o_normalize(emc, f);
+    o_cross(up, f, t);
+    o_normalize(t, r);
+    o_cross(f, r, u);
+    float* m = c->viewMat;
+    for (int i = 0; i < 16; ++i) m[i] = 0.0f;
+    m[0] = r[0]; m[1] = r[1]; m[2] = r[2]; m[3] = -o_dot(r, pos);
+    m[4] = u[0]; m[5] = u[1]; m[6] = u[2]; m[7] = -o_dot(u, pos);
+    m[8] = f[0]; m[9] = f[1]; m[10] = f[2]; m[11] = -o_dot(f, pos);
+    m[15] = 1.0f;
+
+    /* ray tracing basis */
+    float tmp[3] = {target[0] - pos[0], target[1] - pos[1], target[2] - pos[2]};
+    float w[3];
+    o_normalize(tmp, w);
+    for (int i = 0; i < 3; ++i) c->W[i] = w[i] * focalDistance;
+    float cu[3], cv[3];
+    o_cross(c->W, up, tmp);
+    o_normalize(tmp, cu);
+    o_cross(cu, c->W, tmp);
+    o_normalize(tmp, cv);
+    float ulen = focalDistance * tanf(fovY * 0.5f) * aspectRatio;
+    float vlen = focalDistance * tanf(fovY * 0.5f);
+    for (int i = 0; i < 3; ++i) { c->U[i] = cu[i] * ulen; c->V[i] = cv[i] * vlen; }
+}
+
+/* Camera.slang:73-90 computeNonNormalizedRayDirPinhole: p in [0,1] screen space */
+static void o_ray_dir(const ocam* c, float px, float py, float out[3])
+{
+    float ndcx = 2.0f * px + -1.0f;
+    float ndcy = -2.0f * py + 1.0f;
+    for (int i = 0; i < 3; ++i) out[i] = ndcx * c->U[i] + ndcy * c->V[i] + c->W[i];
+}
+
+/* ------------------------------------------------------------------ textures */
+/* Linear filtering of an R32F texture at uv, D3D conventions, 8 sub-texel bits.
+ * wrap = 1: AddressMode::Wrap (Falcor Sampler default, StochasticDepthMapRT S sampler)
+ * wrap = 0: AddressMode::Clamp (SVAO gTextureSampler, SVAO.cpp:76). */
+static inline int o_addr(int i, int n, int wrap)
+{
+    if (wrap) { i %= n; return i < 0 ? i + n : i; }
+    return i < 0 ? 0 : (i >= n ? n - 1 : i);
+}
+static float o_bilinear(const float* tex, int W, int H, float u, float v, int wrap)
+{
+    float x = u * (float)W - 0.5f;
+    float y = v * (float)H - 0.5f;
+    float fx0 = floorf(x), fy0 = floorf(y);
+    float qx = floorf((x - fx0) * 256.0f + 0.5f);
+    float qy = floorf((y - fy0) * 256.0f + 0.5f);
+    int ix = (int)fx0, iy = (int)fy0;
+    if (qx >= 256.0f) { ix += 1; qx = 0.0f; }
+    if (qy >= 256.0f) { iy += 1; qy = 0.0f; }
+    float wx = qx * (1.0f / 256.0f), wy = qy * (1.0f / 256.0f);
+    int x0 = o_addr(ix, W, wrap), x1 = o_addr(ix + 1, W, wrap);
+    int y0 = o_addr(iy, H, wrap), y1 = o_addr(iy + 1, H, wrap);
+    float t00 = tex[(size_t)y0 * W + x0], t10 = tex[(size_t)y0 * W + x1];
+    float t01 = tex[(size_t)y1 * W + x0], t11 = tex[(size_t)y1 * W + x1];
+    float r0 = t00 * (1.0f - wx) + t10 * wx;
+    float r1 = t01 * (1.0f - wx) + t11 * wx;
+    return r0 * (1.0f - wy) + r1 * wy;
+}
+
+/* ------------------------------------------------------------------ intersection */
+/* Pre-computed per-ray data of the watertight test (IntersectionHelpers.slang:114-133) */
+typedef struct {
+    float o[3], d[3];
+    int kx, ky, kz;
+    float Sx, Sy, Sz;
+} oray;
+
+static void o_ray_setup(oray* r, const float o[3], const float d[3])
+{
+    for (int i = 0; i < 3; ++i) { r->o[i] = o[i]; r->d[i] = d[i]; }
+    float ax = fabsf(d[0]), ay = fabsf(d[1]), az = fabsf(d[2]);
+    int axis = 0;
+    if (ay > ax && ay > az) axis = 1;
+    if (az > ax && az > ay) axis = 2;
+    r->kz = axis;
+    r->kx = (axis + 1) % 3;
+    r->ky = (r->kx + 1) % 3;
+    if (d[r->kz] < 0.0f) { int s = r->kx; r->kx = r->ky; r->ky = s; }
+    r->Sx = d[r->kx] / d[r->kz];
+    r->Sy = d[r->ky] / d[r->kz];
+    r->Sz = 1.0f / d[r->kz];
+}
+
+/* IntersectionHelpers.slang:109-180.  Returns 1 on hit, t, DXR barycentrics (V,W)/det, det */
+static int o_intersect_tri(const oray* r, const float v0[3], const float v1[3], const float v2[3],
+                           float* t, float* bu, float* bv, float* detOut)
+{
+    float A[3], B[3], C[3];
+    for (int i = 0; i < 3; ++i) { A[i] = v0[i] - r->o[i]; B[i] = v1[i] - r->o[i]; C[i] = v2[i] - r->o[i]; }
+    const int kx = r->kx, ky = r->ky, kz = r->kz;
+    float Ax = A[kx] - r->Sx * A[kz];
+    float Ay = A[ky] - r->Sy * A[kz];
+    float Bx = B[kx] - r->Sx * B[kz];
+    float By = B[ky] - r->Sy * B[kz];
+    float Cx = C[kx] - r->Sx * C[kz];
+    float Cy = C[ky] - r->Sy * C[kz];
+    float U = Cx * By - Cy * Bx;
+    float V = Ax * Cy - Ay * Cx;
+    float W = Bx * Ay - By * Ax;
+    if (U == 0.0f || V == 0.0f || W == 0.0f) {
+        double CxBy = (double)Cx * (double)By, CyBx = (double)Cy * (double)Bx;
+        U = (float)(CxBy - CyBx);
+        double AxCy = (double)Ax * (double)Cy, AyCx = (double)Ay * (double)Cx;
+        V = (float)(AxCy - AyCx);
+        double BxAy = (double)Bx * (double)Ay, ByAx = (double)By * (double)Ax;
+        W = (float)(BxAy - ByAx);
+    }
+    if ((U < 0.0f || V < 0.0f || W < 0.0f) && (U > 0.0f || V > 0.0f || W > 0.0f)) return 0;
+    float det = U + V + W;
+    if (det == 0.0f) return 0;
+    float Az = r->Sz * A[kz], Bz = r->Sz * B[kz], Cz = r->Sz * C[kz];
+    float T = U * Az + V * Bz + W * Cz;
+    float rcpDet = 1.0f / det;
+    *t = T * rcpDet;
+    *bu = V * rcpDet;
+    *bv = W * rcpDet;
+    *detOut = det;
+    return 1;
+}
+
+int ocpu_intersect(const float o[3], const float d[3], const float v0[3], const float v1[3],
+                   const float v2[3], float* t, float* u, float* v, float* det)
+{
+    oray r;
+    o_ray_setup(&r, o, d);
+    return o_intersect_tri(&r, v0, v1, v2, t, u, v, det);
+}
+
+/* Culling (RtAccelerationStructure instance flags, Scene.cpp:3446-3452; ray flags
+ * CULL_BACK/FRONT_FACING_TRIANGLES).  det > 0 <=> vertices counter-clockwise seen from
+ * the ray origin (right-handed), which is Falcor's front face unless frontFaceCW. */
+static int o_culled(float det, uint32_t flags, uint32_t cull_mode)
+{
+    if (cull_mode == 0 || (flags & 1u)) return 0;
+    int front = (det > 0.0f) != ((flags & 2u) != 0);
+    return cull_mode == 1 ? !front : front;
+}
+
+/* ------------------------------------------------------------------ oracle BVH (object median) */
+typedef struct { float lo[3], hi[3]; uint32_t left, right, first, count; } onode;
+
+struct oscene {
+    uint32_t nt;
+    float* tri;        /* nt * 9 floats (v0,v1,v2), original primitive order */
+    uint32_t* flags;   /* nt */
+    uint32_t* order;   /* leaf order -> primitive id */
+    onode* nodes;
+    uint32_t nnodes;
+};
+
+static float* g_cent; /* centroid array used by the select routine */
+
+static void o_bounds(const oscene* s, const uint32_t* idx, uint32_t n, float lo[3], float hi[3])
+{
+    for (int k = 0; k < 3; ++k) { lo[k] = FLT_MAX; hi[k] = -FLT_MAX; }
+    for (uint32_t i = 0; i < n; ++i) {
+        const float* v = s->tri + (size_t)idx[i] * 9;
+        for (int j = 0; j < 3; ++j)
+            for (int k = 0; k < 3; ++k) {
+                if (v[j * 3 + k] < lo[k]) lo[k] = v[j * 3 + k];
+                if (v[j * 3 + k] > hi[k]) hi[k] = v[j * 3 + k];
+            }
+    }
+}
+
+/* 3-way-partition quickselect: afterwards idx[k] holds the k-th smallest centroid along
+ * `axis`, smaller ones before it and larger ones after it. */
+static void o_select(uint32_t* idx, uint32_t n, uint32_t k, int axis)
+{
+    uint32_t lo = 0, hi = n;
+    while (hi - lo > 1) {
+        float a = g_cent[(size_t)idx[lo] * 3 + axis];
+        float b = g_cent[(size_t)idx[(lo + hi) / 2] * 3 + axis];
+        float c = g_cent[(size_t)idx[hi - 1] * 3 + axis];
+        float pivot = a < b ? (b < c ? b : (a < c ? c : a)) : (a < c ? a : (b < c ? c : b));
+        uint32_t lt = lo, i = lo, gt = hi;
+        while (i < gt) {
+            float v = g_cent[(size_t)idx[i] * 3 + axis];
+            if (v < pivot) { uint32_t t = idx[lt]; idx[lt] = idx[i]; idx[i] = t; lt++; i++; }
+            else if (v > pivot) { gt--; uint32_t t = idx[gt]; idx[gt] = idx[i]; idx[i] = t; }
+            else i++;
+        }
+        if (k < lt) hi = lt;
+        else if (k >= gt) lo = gt;
+        else return;
+    }
+}
+
+static uint32_t o_build(oscene* s, uint32_t* idx, uint32_t first, uint32_t n)
+{
+    uint32_t me = s->nnodes++;
+    onode* nd = &s->nodes[me];
+    o_bounds(s, idx + first, n, nd->lo, nd->hi);
+    if (n <= 4) {
+        nd->left = nd->right = 0;
+        nd->first = first;
+        nd->count = n;
+        return me;
+    }
+    float clo[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, chi[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+    for (uint32_t i = 0; i < n; ++i)
+        for (int k = 0; k < 3; ++k) {
+            float c = g_cent[(size_t)idx[first + i] * 3 + k];
+            if (c < clo[k]) clo[k] = c;
+            if (c > chi[k]) chi[k] = c;
+        }
+    int axis = 0;
+    float ext = chi[0] - clo[0];
+    if (chi[1] - clo[1] > ext) { axis = 1; ext = chi[1] - clo[1]; }
+    if (chi[2] - clo[2] > ext) axis = 2;
+    uint32_t half = n / 2;
+    o_select(idx + first, n, half, axis);
+    uint32_t l = o_build(s, idx, first, half);
+    uint32_t r = o_build(s, idx, first + half, n - half);
+    nd = &s->nodes[me];
+    nd->left = l;
+    nd->right = r;
+    nd->count = 0;
+    return me;
+}
+
+oscene* ocpu_scene_create(const float* pos, uint32_t nv, const uint32_t* ind, uint32_t nt, const uint32_t* flags)
+{
+    (void)nv;
+    oscene* s = (oscene*)calloc(1, sizeof(oscene));
+    s->nt = nt;
+    s->tri = (float*)malloc(sizeof(float) * 9 * (size_t)(nt ? nt : 1));
+    s->flags = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)(nt ? nt : 1));
+    s->order = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)(nt ? nt : 1));
+    g_cent = (float*)malloc(sizeof(float) * 3 * (size_t)(nt ? nt : 1));
+    for (uint32_t i = 0; i < nt; ++i) {
+        for (int j = 0; j < 3; ++j)
+            for (int k = 0; k < 3; ++k) s->tri[(size_t)i * 9 + j * 3 + k] = pos[(size_t)ind[(size_t)i * 3 + j] * 3 + k];
+        s->flags[i] = flags ? flags[i] : 0u;
+        s->order[i] = i;
+        for (int k = 0; k < 3; ++k) {
+            const float* v = s->tri + (size_t)i * 9;
+            g_cent[(size_t)i * 3 + k] = (v[k] + v[3 + k] + v[6 + k]) * (1.0f / 3.0f);
+        }
+    }
+    s->nodes = (onode*)calloc(2 * (size_t)(nt ? nt : 1) + 1, sizeof(onode));
+    if (nt) o_build(s, s->order, 0, nt);
+    free(g_cent);
+    g_cent = NULL;
+    return s;
+}
+
+void ocpu_scene_destroy(oscene* s)
+{
+    if (!s) return;
+    free(s->tri); free(s->flags); free(s->order); free(s->nodes); free(s);
+}
+uint32_t ocpu_scene_node_count(const oscene* s) { return s->nnodes; }
+
+/* Conservative slab test in double precision with a relative margin: a node is
+ * skipped only when it certainly holds no triangle hit with t in [tmin, tmax]. */
+static int o_box(const oray* r, const onode* n, double tmin, double tmax)
+{
+    double t0 = -INFINITY, t1 = INFINITY;
+    for (int k = 0; k < 3; ++k) {
+        double o = r->o[k], d = r->d[k];
+        if (d == 0.0) {
+            if (o < n->lo[k] || o > n->hi[k]) return 0;
+            continue;
+        }
+        double a = (n->lo[k] - o) / d, b = (n->hi[k] - o) / d;
+        if (a > b) { double t = a; a = b; b = t; }
+        if (a > t0) t0 = a;
+        if (b < t1) t1 = b;
+    }
+    double m = 1e-5 * (fabs(t0) + fabs(t1)) + 1e-30;
+    t0 -= m; t1 += m;
+    if (t0 < tmin) t0 = tmin;
+    if (t1 > tmax) t1 = tmax;
+    return t0 <= t1;
+}
+
+/* ------------------------------------------------------------------ hit collection */
+typedef struct { float t, u, v; uint32_t prim; } ohit;
+
+typedef struct {
+    ohit* h;
+    uint32_t n, cap;
+    uint32_t limit; /* keep only the `limit` smallest (t,prim); 0 = keep all */
+} ohits;
+
+static inline int o_key_less(float ta, uint32_t pa, float tb, uint32_t pb)
+{
+    return ta < tb || (ta == tb && pa < pb);
+}
+
+static void o_hits_push(ohits* hs, ohit x)
+{
+    if (hs->limit && hs->n == hs->limit) {
+        ohit* last = &hs->h[hs->n - 1];
+        if (!o_key_less(x.t, x.prim, last->t, last->prim)) return;
+        hs->n--; /* drop the largest */
+    }
+    if (hs->n == hs->cap) {
+        hs->cap = hs->cap ? hs->cap * 2 : 16;
+        hs->h = (ohit*)realloc(hs->h, sizeof(ohit) * hs->cap);
+    }
+    /* insertion keeps the list sorted by (t, prim) */
+    uint32_t i = hs->n++;
+    while (i > 0 && o_key_less(x.t, x.prim, hs->h[i - 1].t, hs->h[i - 1].prim)) {
+        hs->h[i] = hs->h[i - 1];
+        i--;
+    }
+    hs->h[i] = x;
+}
+
+/* all hits with TMin <= t <= TMax, culling applied, ascending (t, prim) order */
+static void o_collect(const oscene* s, const oray* r, float TMin, float TMax, uint32_t cull, ohits* hs)
+{
+    if (!s->nt || !(TMin <= TMax)) return;
+    uint32_t stack[128];
+    int sp = 0;
+    stack[sp++] = 0;
+    while (sp) {
+        const onode* n = &s->nodes[stack[--sp]];
+        float bound = TMax;
+        if (hs->limit && hs->n == hs->limit && hs->h[hs->n - 1].t < bound) bound = hs->h[hs->n - 1].t;
+        if (!o_box(r, n, TMin, bound)) continue;
+        if (n->count) {
+            for (uint32_t i = 0; i < n->count; ++i) {
+                uint32_t prim = s->order[n->first + i];
+                const float* v = s->tri + (size_t)prim * 9;
+                float t, u, vv, det;
+                if (!o_intersect_tri(r, v, v + 3, v + 6, &t, &u, &vv, &det)) continue;
+                if (!(t >= TMin && t <= TMax)) continue;
+                if (o_culled(det, s->flags[prim], cull)) continue;
+                ohit x = {t, u, vv, prim};
+                o_hits_push(hs, x);
+            }
+        } else {
+            stack[sp++] = n->left;
+            stack[sp++] = n->right;
+        }
+    }
+}
+
+/* ------------------------------------------------------------------ G-buffer */
+typedef struct {
+    const oscene* s; const ocam* c; uint32_t W, H, cull;
+    float* z; uint16_t* n;
+    uint32_t y0, y1;
+} ogb_job;
+
+static void* o_gbuffer_rows(void* arg)
+{
+    ogb_job* j = (ogb_job*)arg;
+    const ocam* c = j->c;
+    float wn[3];
+    o_normalize(c->W, wn);
+    for (uint32_t y = j->y0; y < j->y1; ++y)
+        for (uint32_t x = 0; x < j->W; ++x) {
+            /* Camera.slang:46-59 computeRayPinhole (camera jitter applied) */
+            float px = ((float)x + 0.5f) / (float)j->W + -c->jitterX;
+            float py = ((float)y + 0.5f) / (float)j->H + c->jitterY;
+            float dn[3], d[3];
+            o_ray_dir(c, px, py, dn);
+            o_normalize(dn, d);
+            float invCos = 1.0f / o_dot(wn, d);
+            float tmin = c->nearZ * invCos, tmax = c->farZ * invCos;
+            oray r;
+            o_ray_setup(&r, c->posW, d);
+            ohits hs = {0};
+            hs.limit = 1;
+            o_collect(j->s, &r, tmin, tmax, j->cull, &hs);
+            size_t o = (size_t)y * j->W + x;
+            if (hs.n == 0) {
+                j->z[o] = c->farZ;
+                j->n[o] = 0;
+            } else {
+                j->z[o] = hs.h[0].t * o_dot(wn, d);
+                const float* v = j->s->tri + (size_t)hs.h[0].prim * 9;
+                float e1[3] = {v[3] - v[0], v[4] - v[1], v[5] - v[2]};
+                float e2[3] = {v[6] - v[0], v[7] - v[1], v[8] - v[2]};
+                float cr[3], nw[3], nv[3];
+                o_cross(e1, e2, cr);
+                o_normalize(cr, nw);
+                const float* m = c->viewMat;
+                for (int k = 0; k < 3; ++k) nv[k] = m[k * 4 + 0] * nw[0] + m[k * 4 + 1] * nw[1] + m[k * 4 + 2] * nw[2];
+                j->n[o] = (uint16_t)ocpu_encode_normal_2x8(nv);
+            }
+            free(hs.h);
+        }
+    return NULL;
+}
+
+static void o_run_rows(void* (*fn)(void*), void* jobs, size_t jobsz, uint32_t y0, uint32_t y1, int nthreads,
+                       void (*setrows)(void*, uint32_t, uint32_t))
+{
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 256) nthreads = 256;
+    pthread_t th[256];
+    uint32_t rows = y1 - y0;
+    for (int i = 0; i < nthreads; ++i) {
+        void* job = (char*)jobs + jobsz * i;
+        setrows(job, y0 + (uint32_t)((uint64_t)rows * i / nthreads), y0 + (uint32_t)((uint64_t)rows * (i + 1) / nthreads));
+        pthread_create(&th[i], NULL, fn, job);
+    }
+    for (int i = 0; i < nthreads; ++i) pthread_join(th[i], NULL);
+}
+
+static void o_gb_setrows(void* j, uint32_t a, uint32_t b) { ((ogb_job*)j)->y0 = a; ((ogb_job*)j)->y1 = b; }
+
+void ocpu_gbuffer(const oscene* s, const ocam* cam, uint32_t W, uint32_t H, uint32_t cull,
+                  float* linearZ, uint16_t* normals, int nthreads)
+{
+    if (nthreads < 1) nthreads = 1;
+    ogb_job* jobs = (ogb_job*)calloc((size_t)nthreads, sizeof(ogb_job));
+    for (int i = 0; i < nthreads; ++i) {
+        jobs[i].s = s; jobs[i].c = cam; jobs[i].W = W; jobs[i].H = H; jobs[i].cull = cull;
+        jobs[i].z = linearZ; jobs[i].n = normals;
+    }
+    o_run_rows(o_gbuffer_rows, jobs, sizeof(ogb_job), 0, H, nthreads, o_gb_setrows);
+    free(jobs);
+}
+
+/* ------------------------------------------------------------------ SD trace */
+/* initRayDesc, Common.slangh:65-92 (+ Camera.slang:46-90).  Returns TMin/TMax, the
+ * normalized jittered direction d and cosT = dot(normalize(cameraW), d). */
+static void o_sd_ray(const ocam* c, const osd_params* p, const float* z, uint32_t zW, uint32_t zH,
+                     const uint32_t* rmin, const uint32_t* rmax, uint32_t sdW, uint32_t sdH,
+                     uint32_t x, uint32_t y, float d[3], float* TMinOut, float* TMaxOut, float* cosTOut)
+{
+    const int G = p->guard_band;
+    const int dimx = (int)sdW - 2 * G, dimy = (int)sdH - 2 * G;
+    float wn[3];
+    o_normalize(c->W, wn);
+    int sx = (int)x - G, sy = (int)y - G;
+    float pcx = ((float)sx + 0.5f) / (float)dimx + -c->jitterX;
+    float pcy = ((float)sy + 0.5f) / (float)dimy + c->jitterY;
+    float dn[3], dc[3];
+    o_ray_dir(c, pcx, pcy, dn);
+    o_normalize(dn, dc);
+    float invCos = 1.0f / o_dot(wn, dc);
+    float TMax = c->farZ * invCos; /* computeRayPinhole tMax (pixel centre) */
+    float jx = 0.5f, jy = 0.5f;
+    if (p->jitter) ocpu_jitter(x, y, &jx, &jy);
+    float pjx = ((float)sx + jx) / (float)dimx;
+    float pjy = ((float)sy + jy) / (float)dimy;
+    o_ray_dir(c, pjx, pjy, dn);
+    o_normalize(dn, d);
+    float eps = 0.1f * c->nearZ;
+    float depth = 0.0f;
+    if (sx >= 0 && sy >= 0 && sx < dimx && sy < dimy)
+        depth = o_bilinear(z, (int)zW, (int)zH, ((float)sx + 0.5f) / (float)dimx,
+                           ((float)sy + 0.5f) / (float)dimy, 1);
+    float cosT = o_dot(wn, d);
+    float TMin = depth / cosT + eps;
+    if (p->ray_interval) {
+        size_t o = (size_t)y * sdW + x;
+        uint32_t iMin = rmin ? rmin[o] : 0u;
+        if (iMin != 0u) TMin = o_max(o_asfloat(iMin), TMin);
+        uint32_t iMax = rmax ? rmax[o] : 0u;
+        if (iMax != 0u) TMax = o_min(o_asfloat(iMax), TMax);
+    }
+    *TMinOut = TMin; *TMaxOut = TMax; *cosTOut = cosT;
+}
+
+void ocpu_sd_ray(const ocam* c, const osd_params* p, const float* z, uint32_t zW, uint32_t zH,
+                 const uint32_t* rmin, const uint32_t* rmax, uint32_t sdW, uint32_t sdH, uint32_t x, uint32_t y,
+                 float out[6] /* o.xyz, d.xyz */, float* tmin, float* tmax, float* cosT)
+{
+    float d[3];
+    o_sd_ray(c, p, z, zW, zH, rmin, rmax, sdW, sdH, x, y, d, tmin, tmax, cosT);
+    for (int i = 0; i < 3; ++i) { out[i] = c->posW[i]; out[3 + i] = d[i]; }
+}
+
+typedef struct {
+    const oscene* s; const ocam* c; const osd_params* p;
+    const float* z; uint32_t zW, zH;
+    const uint32_t* rmin; const uint32_t* rmax;
+    float* sd; uint32_t sdW, sdH;
+    uint32_t y0, y1;
+    uint64_t active, hits;
+} osd_job;
+
+static void* o_sd_rows(void* arg)
+{
+    osd_job* j = (osd_job*)arg;
+    const ocam* c = j->c;
+    const osd_params* p = j->p;
+    const uint32_t N = p->sample_count;
+    const float DEFAULT = p->normalize ? 1.0f : 3.40282347e+37f; /* Common.slangh:16 */
+    const uint32_t ch = N < 4 ? N : 4, layers = (N + 3) / 4;
+
+    int32_t lutIdx[33];
+    uint32_t* lut = NULL;
+    if (p->implementation == 1) {
+        lut = (uint32_t*)malloc(sizeof(uint32_t) << N);
+        ocpu_stratified_lut((int)N, lutIdx, lut);
+    }
+
+    for (uint32_t y = j->y0; y < j->y1; ++y)
+        for (uint32_t x = 0; x < j->sdW; ++x) {
+            float d[3], TMin, TMax, cosT;
+            o_sd_ray(c, p, j->z, j->zW, j->zH, j->rmin, j->rmax, j->sdW, j->sdH, x, y, d, &TMin, &TMax, &cosT);
+
+            /* ---- rayGen payload init, StochasticDepthMapRT.rt.slang:74-80 ---- */
+            float depths[16];
+            for (uint32_t i = 0; i < N; ++i) depths[i] = DEFAULT;
+            uint32_t count = 0;
+
+            if (TMin <= TMax) {
+                j->active++;
+                oray r;
+                o_ray_setup(&r, c->posW, d);
+                ohits hs = {0};
+                /* Default / KBuffer always commit by the MAX_COUNT-th hit */
+                hs.limit = (p->implementation == 1) ? 0u : (p->max_count ? p->max_count : 1u);
+                o_collect(j->s, &r, TMin, TMax, p->cull_mode, &hs);
+                /* ---- anyHit -> algorithm, Common.slangh:102-254, ascending (t, prim) ---- */
+                for (uint32_t k = 0; k < hs.n; ++k) {
+                    j->hits++;
+                    float rng = ocpu_hash(hs.h[k].u, hs.h[k].v);
+                    float t = hs.h[k].t * cosT; /* RayToViewDepth */
+                    if (p->normalize) t = o_saturate((t - c->nearZ) / (c->farZ - c->nearZ));
+                    int commit;
+                    if (p->implementation == 1) { /* CoverageMask */
+                        int R = (int)floorf(p->alpha * (float)N + rng);
+                        uint32_t mask = 0;
+                        if (R >= (int)N) mask = 0xffffu;
+                        else if (R != 0) {
+                            float rng2 = ocpu_hash(rng, t); /* hash3D(float3(bary, t)) */
+                            float a = (float)lutIdx[R], b = (float)lutIdx[R + 1];
+                            int index = (int)(a + rng2 * (b - a));
+                            mask = lut[index];
+                        }
+                        float maxT = 0.0f;
+                        for (uint32_t i = 0; i < N; ++i) {
+                            if (mask & (1u << i))
+                                if (t < depths[i]) depths[i] = t;
+                            maxT = o_max(maxT, depths[i]);
+                        }
+                        commit = !(t < maxT);
+                    } else if (p->implementation == 3) { /* KBuffer */
+                        if (t >= depths[N - 1]) { commit = 1; }
+                        else {
+                            count++;
+                            float rayT = t;
+                            for (uint32_t i = 0; i < N; ++i)
+                                if (t < depths[i]) { float tmp = depths[i]; depths[i] = t; t = tmp; }
+                            commit = (depths[N - 1] == rayT) ? 1 : (count >= p->max_count);
+                        }
+                    } else { /* Default: reservoir */
+                        uint32_t slot = count++;
+                        if (count > N) slot = (uint32_t)(rng * (float)count);
+                        if (slot < N && !(depths[slot] <= t)) depths[slot] = t; /* opaque: alpha test passes */
+                        commit = count >= p->max_count;
+                    }
+                    if (commit) break; /* committed hit: TMax = t, stream ends */
+                }
+                free(hs.h);
+            }
+
+            /* ---- store, StochasticDepthMapRT.rt.slang:90-104 ---- */
+            for (uint32_t l = 0; l < layers; ++l)
+                for (uint32_t k = 0; k < ch; ++k) {
+                    size_t o = (((size_t)l * j->sdH + y) * j->sdW + x) * ch + k;
+                    j->sd[o] = depths[l * 4 + k];
+                }
+        }
+    free(lut);
+    return NULL;
+}
+
+static void o_sd_setrows(void* j, uint32_t a, uint32_t b) { ((osd_job*)j)->y0 = a; ((osd_job*)j)->y1 = b; }
+
+void ocpu_sd_trace(const oscene* s, const ocam* cam, const osd_params* p,
+                   const float* linearZ, uint32_t zW, uint32_t zH,
+                   const uint32_t* rayMin, const uint32_t* rayMax,
+                   float* sd, uint32_t sdW, uint32_t sdH,
+                   uint32_t row0, uint32_t row1, int nthreads, uint64_t* stats)
+{
+    if (nthreads < 1) nthreads = 1;
+    osd_job* jobs = (osd_job*)calloc((size_t)nthreads, sizeof(osd_job));
+    for (int i = 0; i < nthreads; ++i) {
+        jobs[i].s = s; jobs[i].c = cam; jobs[i].p = p;
+        jobs[i].z = linearZ; jobs[i].zW = zW; jobs[i].zH = zH;
+        jobs[i].rmin = rayMin; jobs[i].rmax = rayMax;
+        jobs[i].sd = sd; jobs[i].sdW = sdW; jobs[i].sdH = sdH;
+    }
+    if (row1 > sdH) row1 = sdH;
+    o_run_rows(o_sd_rows, jobs, sizeof(osd_job), row0, row1, nthreads, o_sd_setrows);
+    if (stats) {
+        stats[0] = stats[1] = 0;
+        for (int i = 0; i < nthreads; ++i) { stats[0] += jobs[i].active; stats[1] += jobs[i].hits; }
+    }
+    free(jobs);
+}
+
+/* ------------------------------------------------------------------ SVAO */
+typedef struct {
+    const ocam* c; const ovao* d; const osvao_params* p;
+    const float* depth; const uint16_t* normals; uint32_t W, H;
+    float sinNoise[16], cosNoise[16];
+    float sinDir[8], cosDir[8];
+} octx;
+
+typedef struct {
+    float posV[3]; float posVLength;
+    float normal[3], tangent[3], bitangent[3], normalO[3], normalV[3];
+    float radiusInPixels, radius;
+} obasic;
+
+typedef struct {
+    float sphereStart, sphereEnd, pdf;
+    int isInScreen;
+    float samplePosUV[2], rasterSamplePosUV[2];
+    float visibility, objectSpaceZ;
+    float initialSamplePosLength, radius;
+    float initialSamplePosV[3];
+    float screenSpaceRadius;
+} osample;
+
+static void o_ctx_init(octx* x, const ocam* c, const ovao* d, const osvao_params* p,
+                       const float* depth, const uint16_t* normals, uint32_t W, uint32_t H)
+{
+    x->c = c; x->d = d; x->p = p; x->depth = depth; x->normals = normals; x->W = W; x->H = H;
+    uint8_t noise[16];
+    ocpu_noise_texture(noise);
+    for (int i = 0; i < 16; ++i) {
+        float rr = o_unorm8_to_float(noise[i]) * 2.0f * 3.141f; /* Common.slang:311 */
+        x->sinNoise[i] = o_sin(rr);
+        x->cosNoise[i] = o_cos(rr);
+    }
+    for (int i = 0; i < 8; ++i) {
+        float a = ((float)i / 8.0f) * 2.0f * 3.141f; /* Common.slang:357 */
+        x->sinDir[i] = o_sin(a);
+        x->cosDir[i] = o_cos(a);
+    }
+}
+
+/* Common.slang:139-144 */
+static void o_uv_to_view(const octx* x, float u, float v, float z, float out[3])
+{
+    float ndcx = u * 2.0f - 1.0f, ndcy = (1.0f - v) * 2.0f - 1.0f;
+    float isx = 0.5f * (x->c->frameWidth / x->c->focalLength);
+    float isy = 0.5f * (x->c->frameHeight / x->c->focalLength);
+    out[0] = ndcx * z * isx;
+    out[1] = ndcy * z * isy;
+    out[2] = -z;
+}
+/* Common.slang:148-153 */
+static void o_view_to_uv(const octx* x, const float p[3], float uv[2])
+{
+    float isx = 0.5f * (x->c->frameWidth / x->c->focalLength);
+    float isy = 0.5f * (x->c->frameHeight / x->c->focalLength);
+    float ndcx = p[0] / (isx * p[2]), ndcy = p[1] / (isy * p[2]);
+    uv[0] = ndcx * -0.5f + 0.5f;
+    uv[1] = ndcy * 0.5f + 0.5f;
+}
+
+static float o_depth_sample(const octx* x, float u, float v)
+{
+    return o_bilinear(x->depth, (int)x->W, (int)x->H, u, v, 0);
+}
+
+/* Common.slang:285-324 BasicAOData::Init */
+static int o_basic_init(const octx* x, float u, float v, obasic* b)
+{
+    const ovao* d = x->d;
+    float z = o_depth_sample(x, u, v);
+    /* GetAORadiusInPixels, Common.slang:247-261 */
+    float rux = (d->radius * x->c->focalLength) / (x->c->frameWidth * z);
+    float ruy = (d->radius * x->c->focalLength) / (x->c->frameHeight * z);
+    float a = rux * d->resolution[0], bb = ruy * d->resolution[1];
+    b->radiusInPixels = a + 0.5f * (bb - a); /* lerp(a, b, 0.5) */
+    b->radius = d->radius;
+    float maxRadius = d->ssMaxRadius;
+    if (b->radiusInPixels > maxRadius) {
+        b->radius = b->radius / b->radiusInPixels * maxRadius;
+        b->radiusInPixels = maxRadius;
+    }
+    if (b->radiusInPixels < 0.5f) return 0;
+    o_uv_to_view(x, u, v, z, b->posV);
+    b->posVLength = o_len(b->posV);
+    /* loadNormal, Common.slang:98-103: integer load at uint2(texC * resolution) */
+    uint32_t ix = (uint32_t)(u * d->resolution[0]), iy = (uint32_t)(v * d->resolution[1]);
+    uint32_t packed = (ix < x->W && iy < x->H) ? x->normals[(size_t)iy * x->W + ix] : 0u;
+    ocpu_decode_normal_2x8(packed, b->normalV);
+    if (o_dot(b->posV, b->normalV) > 0.0f)
+        for (int k = 0; k < 3; ++k) b->normalV[k] = -b->normalV[k];
+    /* noise: point sampler, wrap, 4x4 texture at texC * noiseScale */
+    float nu = u * d->noiseScale[0], nv = v * d->noiseScale[1];
+    int ni = ((int)floorf(nu * 4.0f)) & 3, nj = ((int)floorf(nv * 4.0f)) & 3;
+    float rd[3] = {x->sinNoise[nj * 4 + ni], x->cosNoise[nj * 4 + ni], 0.0f};
+    float il = 1.0f / b->posVLength; (void)il;
+    for (int k = 0; k < 3; ++k) b->normal[k] = -b->posV[k] / b->posVLength;
+    float t[3];
+    o_cross(b->normal, rd, t);
+    o_normalize(t, b->bitangent);
+    o_cross(b->bitangent, b->normal, b->tangent);
+    b->normalO[0] = o_dot(b->normalV, b->tangent);
+    b->normalO[1] = o_dot(b->normalV, b->bitangent);
+    b->normalO[2] = o_dot(b->normalV, b->normal);
+    return 1;
+}
+
+/* Common.slang:170-174 */
+static float o_make_nonzero(float v, float eps)
+{
+    float a = o_max(fabsf(v), eps);
+    return v >= 0.0f ? a : -a;
+}
+
+/* Common.slang:354-399 SampleAOData::Init (VAO kernel) */
+static int o_sample_init(const octx* x, float u, float v, const obasic* b, uint32_t i, osample* s)
+{
+    const ovao* d = x->d;
+    s->radius = k_radius8[i] * b->radius;
+    float dir[2] = {s->radius * x->sinDir[i], s->radius * x->cosDir[i]};
+    float sphereHeight = sqrtf(b->radius * b->radius - s->radius * s->radius);
+    s->pdf = 2.0f * sphereHeight;
+    s->sphereStart = sphereHeight;
+    s->sphereEnd = -sphereHeight;
+    float zi = -(dir[0] * b->normalO[0] + dir[1] * b->normalO[1]) / o_make_nonzero(b->normalO[2], 0.0001f);
+    float zc = o_min(o_max(zi, -sphereHeight), sphereHeight);
+    s->sphereEnd = zc;
+    if ((s->sphereStart - s->sphereEnd) / (2.0f * sphereHeight) <= 0.1f) return 0;
+    for (int k = 0; k < 3; ++k) s->initialSamplePosV[k] = b->posV[k] + b->tangent[k] * dir[0] + b->bitangent[k] * dir[1];
+    s->initialSamplePosLength = o_len(s->initialSamplePosV);
+    o_view_to_uv(x, s->initialSamplePosV, s->samplePosUV);
+    s->visibility = 0.0f;
+    s->objectSpaceZ = 0.0f;
+    float dd[2] = {(u - s->samplePosUV[0]) * d->resolution[0], (v - s->samplePosUV[1]) * d->resolution[1]};
+    s->screenSpaceRadius = sqrtf(dd[0] * dd[0] + dd[1] * dd[1]);
+    float su = o_saturate(s->samplePosUV[0]), sv = o_saturate(s->samplePosUV[1]);
+    s->isInScreen = (s->samplePosUV[0] == su) && (s->samplePosUV[1] == sv);
+    /* getSnappedUV, Common.slang:116-120 */
+    s->rasterSamplePosUV[0] = (floorf(su * d->resolution[0]) + 0.5f) / d->resolution[0];
+    s->rasterSamplePosUV[1] = (floorf(sv * d->resolution[1]) + 0.5f) / d->resolution[1];
+    return 1;
+}
+
+/* Common.slang:180-196 */
+static float o_calc_visibility(const ovao* d, float oz, float ss, float se, float pdf, float radius)
+{
+    float sphere = o_max(ss - o_max(se, oz), 0.0f) / pdf;
+    float halo = o_saturate((oz - (1.0f + d->thickness) * radius) / ss) * (ss - se) / pdf;
+    return sphere + halo;
+}
+
+/* Common.slang:463-483 addSample (VAO) */
+static void o_add_sample(const octx* x, const obasic* b, osample* s, const float spV[3], int init)
+{
+    float diff[3] = {spV[0] - b->posV[0], spV[1] - b->posV[1], spV[2] - b->posV[2]};
+    float oz = o_dot(diff, b->normal);
+    s->objectSpaceZ = init ? oz : o_min(s->objectSpaceZ, oz);
+    float vis = o_calc_visibility(x->d, oz, s->sphereStart, s->sphereEnd, s->pdf, b->radius);
+    s->visibility = init ? vis : o_min(s->visibility, vis);
+}
+
+/* Common.slang:492-496 evalPrimaryVisibility */
+static void o_eval_primary(const octx* x, const obasic* b, osample* s)
+{
+    float z = o_depth_sample(x, s->rasterSamplePosUV[0], s->rasterSamplePosUV[1]);
+    float spV[3];
+    o_uv_to_view(x, s->rasterSamplePosUV[0], s->rasterSamplePosUV[1], z, spV);
+    o_add_sample(x, b, s, spV, 1);
+}
+
+/* Common.slang:164-168 UVToSDPixel */
+static void o_uv_to_sd_pixel(const ovao* d, const float uv[2], int out[2])
+{
+    for (int k = 0; k < 2; ++k) {
+        int px = (int)floorf(uv[k] * d->lowResolution[k]) + d->sdGuard;
+        int hi = (int)d->lowResolution[k] + d->sdGuard * 2 - 1;
+        out[k] = px < 0 ? 0 : (px > hi ? hi : px);
+    }
+}
+
+void ocpu_svao_clear(uint32_t* rayMin, uint32_t* rayMax, uint32_t n)
+{
+    /* SVAO.cpp:334-340 */
+    for (uint32_t i = 0; i < n; ++i) { rayMax[i] = 0u; rayMin[i] = o_asuint(FLT_MAX); }
+}
+
+/* SVAORaster.ps.slang:29-122 */
+void ocpu_svao_pass1(const ocam* cam, const ovao* d, const osvao_params* p,
+                     const float* depth, const uint16_t* normals, uint32_t W, uint32_t H,
+                     uint8_t* ao, uint8_t* stencil, uint32_t* rayMin, uint32_t* rayMax,
+                     uint32_t sdW, uint32_t sdH)
+{
+    octx x;
+    o_ctx_init(&x, cam, d, p, depth, normals, W, H);
+    const uint32_t g = p->guard_band;
+    /* SVAO.cpp:347-350: dispatch roundup32(dims - 2 guardBand); the 2x2 group interleave
+     * (SVAORaster.ps.slang:36) is a bijection of that range, so iterate it directly. */
+    uint32_t nx = ((W - 2 * g) + 31u) / 32u * 32u, ny = ((H - 2 * g) + 31u) / 32u * 32u;
+    for (uint32_t oy = 0; oy < ny; ++oy)
+        for (uint32_t ox = 0; ox < nx; ++ox) {
+            uint32_t px = ox + g, py = oy + g;
+            float u = ((float)px + 0.5f) * d->invResolution[0];
+            float v = ((float)py + 0.5f) * d->invResolution[1];
+            float aoOut = 0.0f;
+            uint32_t st = 0;
+            obasic b;
+            if (!o_basic_init(&x, u, v, &b)) {
+                aoOut = 1.0f;
+            } else {
+                for (uint32_t i = 0; i < 8; ++i) {
+                    osample s;
+                    if (!o_sample_init(&x, u, v, &b, i, &s)) continue;
+                    /* isSamePixel, Common.slang:129-134 */
+                    if (fabsf(u - s.rasterSamplePosUV[0]) < d->invResolution[0] * 0.9f &&
+                        fabsf(v - s.rasterSamplePosUV[1]) < d->invResolution[1] * 0.9f) {
+                        aoOut += (s.sphereStart - s.sphereEnd) / s.pdf;
+                        continue;
+                    }
+                    o_eval_primary(&x, &b, &s);
+                    aoOut += s.visibility;
+                    int forceRay = 0;
+                    if (!s.isInScreen && d->sdGuard > 0) {
+                        forceRay = 1;
+                        s.objectSpaceZ = O_FLT_MAX;
+                    }
+                    /* requireRay (VAO), Common.slang:455-461 with CONST_RADIUS (Common.slang:37) */
+                    float constRadius = (1.0f + d->thickness) * b.radius - s.sphereStart;
+                    int req = s.objectSpaceZ > s.sphereStart + constRadius && s.screenSpaceRadius > d->ssRadiusCutoff;
+                    if (req || forceRay) {
+                        st |= 1u << i;
+                        if (p->secondary_depth_mode == 2) {
+                            int pix[2];
+                            o_uv_to_sd_pixel(d, s.samplePosUV, pix);
+                            size_t o = (size_t)pix[1] * sdW + pix[0];
+                            if (p->ray_interval) {
+                                float osMin = o_min(s.objectSpaceZ, b.radius + d->thickness * b.radius + s.sphereStart);
+                                uint32_t rmin = o_asuint(o_max(b.posVLength - osMin, 0.0f));
+                                uint32_t rmax = o_asuint(o_max(b.posVLength - s.sphereEnd, 0.0f));
+                                if (rmin < rayMin[o]) rayMin[o] = rmin;
+                                if (rmax > rayMax[o]) rayMax[o] = rmax;
+                            } else {
+                                rayMax[o] = 1u;
+                            }
+                        }
+                    }
+                }
+                aoOut *= 1.0f / 8.0f;
+                aoOut *= 2.0f;
+                if (p->secondary_depth_mode == 0 || st == 0) aoOut = o_pow(aoOut, d->exponent);
+            }
+            if (px < W && py < H) {
+                ao[(size_t)py * W + px] = o_unorm8(aoOut);
+                stencil[(size_t)py * W + px] = (uint8_t)st;
+            }
+        }
+    (void)sdH;
+}
+
+/* SVAORaster2.ps.slang:48-65 -> calcAO2 (Common.slang:523-663), stochastic branch */
+typedef struct {
+    const octx* x; const uint8_t* stencil; const float* sd; uint32_t sdW, sdH; uint8_t* ao;
+    uint32_t y0, y1;
+} op2_job;
+
+static void* o_pass2_rows(void* arg)
+{
+    op2_job* j = (op2_job*)arg;
+    const octx* x = j->x;
+    const ovao* d = x->d;
+    const uint32_t g = x->p->guard_band, W = x->W, N = x->p->sd_samples;
+    const uint32_t ch = N < 4 ? N : 4;
+    const float depthRange = x->c->farZ - x->c->nearZ, depthOffset = x->c->nearZ;
+    for (uint32_t py = j->y0; py < j->y1; ++py)
+        for (uint32_t px = g; px < W - g; ++px) {
+            size_t o = (size_t)py * W + px;
+            uint32_t mask = j->stencil[o];
+            if (mask == 0) continue;
+            float u = ((float)px + 0.5f) * d->invResolution[0];
+            float v = ((float)py + 0.5f) * d->invResolution[1];
+            obasic b;
+            o_basic_init(x, u, v, &b);
+            float vis = 0.0f;
+            for (uint32_t i = 0; i < 8; ++i) {
+                if (!(mask & (1u << i))) continue;
+                osample s;
+                o_sample_init(x, u, v, &b, i, &s);
+                o_eval_primary(x, &b, &s);
+                vis -= s.visibility;
+                int pc[2];
+                o_uv_to_sd_pixel(d, s.samplePosUV, pc);
+                float jx = 0.5f, jy = 0.5f;
+                if (x->p->sd_jitter) ocpu_jitter((uint32_t)pc[0], (uint32_t)pc[1], &jx, &jy);
+                float su = ((float)(pc[0] - d->sdGuard) + jx) / d->lowResolution[0];
+                float sv = ((float)(pc[1] - d->sdGuard) + jy) / d->lowResolution[1];
+                if (!s.isInScreen) { s.visibility = 1.0f; s.objectSpaceZ = O_FLT_MAX; } /* resetSample */
+                for (uint32_t k = 0; k < N; ++k) {
+                    size_t so = ((((size_t)(k / 4) * j->sdH) + (size_t)pc[1]) * j->sdW + (size_t)pc[0]) * ch + (k % 4);
+                    float lz = j->sd[so] * depthRange + depthOffset;
+                    float spV[3];
+                    o_uv_to_view(x, su, sv, lz, spV);
+                    o_add_sample(x, &b, &s, spV, 0);
+                }
+                vis += s.visibility;
+            }
+            vis *= 1.0f / 8.0f;
+            vis *= 2.0f;
+            vis += o_unorm8_to_float(j->ao[o]);
+            vis = o_pow(vis, d->exponent);
+            j->ao[o] = o_unorm8(vis);
+        }
+    return NULL;
+}
+
+static void o_p2_setrows(void* j, uint32_t a, uint32_t b) { ((op2_job*)j)->y0 = a; ((op2_job*)j)->y1 = b; }
+
+void ocpu_svao_pass2(const ocam* cam, const ovao* d, const osvao_params* p,
+                     const float* depth, const uint16_t* normals, uint32_t W, uint32_t H,
+                     const uint8_t* stencil, const float* sd, uint32_t sdW, uint32_t sdH,
+                     uint8_t* ao, int nthreads)
+{
+    octx x;
+    o_ctx_init(&x, cam, d, p, depth, normals, W, H);
+    if (nthreads < 1) nthreads = 1;
+    op2_job* jobs = (op2_job*)calloc((size_t)nthreads, sizeof(op2_job));
+    for (int i = 0; i < nthreads; ++i) {
+        jobs[i].x = &x; jobs[i].stencil = stencil; jobs[i].sd = sd;
+        jobs[i].sdW = sdW; jobs[i].sdH = sdH; jobs[i].ao = ao;
+    }
+    o_run_rows(o_pass2_rows, jobs, sizeof(op2_job), p->guard_band, H - p->guard_band, nthreads, o_p2_setrows);
+    free(jobs);
+}

@@ -1,0 +1,206 @@
+// rsd_host.cpp -- librsd host entry points: errors, devices, scene upload (BVH build +
+// HBM residency), camera and SVAO constant derivation.  No GPU work besides copies.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <thread>
+
+#include "rsd_internal.h"
+
+namespace rsd {
+namespace {
+thread_local std::string g_last_error;
+}
+void set_error(const std::string& msg) { g_last_error = msg; }
+rsd_status hip_fail(hipError_t e, const char* what) {
+    g_last_error = std::string(what) + ": " + hipGetErrorString(e);
+    return e == hipErrorOutOfMemory ? RSD_ERR_OUT_OF_MEMORY : RSD_ERR_HIP;
+}
+}  // namespace rsd
+
+using rsd::set_error;
+
+extern "C" uint32_t rsd_abi_version(void) { return RSD_ABI_VERSION; }
+
+extern "C" const char* rsd_last_error(void) { return rsd::g_last_error.c_str(); }
+
+extern "C" rsd_status rsd_device_open(int hip_device, rsd_device** out) {
+    if (!out) {
+        set_error("rsd_device_open: out is null");
+        return RSD_ERR_INVALID_ARG;
+    }
+    *out = nullptr;
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess || n == 0) {
+        set_error("rsd_device_open: no HIP device available");
+        return RSD_ERR_NO_DEVICE;
+    }
+    if (hip_device < 0 || hip_device >= n) {
+        set_error("rsd_device_open: device index out of range");
+        return RSD_ERR_INVALID_ARG;
+    }
+    RSD_HIP(hipSetDevice(hip_device));
+    hipDeviceProp_t prop;
+    RSD_HIP(hipGetDeviceProperties(&prop, hip_device));
+    auto* d = new rsd_device;
+    d->hip_device = hip_device;
+    d->cu_count = prop.multiProcessorCount;
+    *out = d;
+    return RSD_OK;
+}
+
+extern "C" void rsd_device_close(rsd_device* dev) { delete dev; }
+
+extern "C" rsd_status rsd_scene_upload(rsd_device* dev, const rsd_scene_desc* desc, rsd_scene** out) {
+    if (!dev || !desc || !out || (desc->triangle_count && (!desc->positions || !desc->indices))) {
+        set_error("rsd_scene_upload: null argument");
+        return RSD_ERR_INVALID_ARG;
+    }
+    *out = nullptr;
+    for (uint64_t i = 0; i < 3ull * desc->triangle_count; ++i)
+        if (desc->indices[i] >= desc->vertex_count) {
+            set_error("rsd_scene_upload: index out of range of vertex_count");
+            return RSD_ERR_INVALID_ARG;
+        }
+    if (desc->triangle_count >= (1u << 30)) {
+        set_error("rsd_scene_upload: too many triangles");
+        return RSD_ERR_UNSUPPORTED;
+    }
+    RSD_HIP(hipSetDevice(dev->hip_device));
+    unsigned threads = std::max(1u, std::thread::hardware_concurrency());
+    threads = std::min(threads, 16u);
+    rsd::FlatBvh bvh = rsd::build_bvh(desc->positions, desc->vertex_count, desc->indices, desc->triangle_count,
+                                      desc->triangle_flags, threads);
+    auto* s = new rsd_scene;
+    s->dev = dev;
+    s->triangle_count = desc->triangle_count;
+    s->node_count = (uint32_t)(bvh.nodes.size() / 16);
+    s->stats = bvh.stats;
+    const size_t nb = bvh.nodes.size() * sizeof(float), tb = std::max<size_t>(bvh.tris.size(), 12) * sizeof(float);
+    hipError_t e = hipMalloc(&s->d_nodes, nb);
+    if (e == hipSuccess) e = hipMalloc(&s->d_tris, tb);
+    if (e == hipSuccess) e = hipMalloc(&s->d_counters, 8 * sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipMemcpy(s->d_nodes, bvh.nodes.data(), nb, hipMemcpyHostToDevice);
+    if (e == hipSuccess && !bvh.tris.empty())
+        e = hipMemcpy(s->d_tris, bvh.tris.data(), bvh.tris.size() * sizeof(float), hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        rsd_status st = rsd::hip_fail(e, "rsd_scene_upload");
+        (void)hipFree(s->d_nodes);
+        (void)hipFree(s->d_tris);
+        (void)hipFree(s->d_counters);
+        delete s;
+        return st;
+    }
+    s->device_bytes = nb + tb;
+    *out = s;
+    return RSD_OK;
+}
+
+extern "C" rsd_status rsd_scene_info_get(const rsd_scene* s, rsd_scene_info* out) {
+    if (!s || !out) {
+        set_error("rsd_scene_info_get: null argument");
+        return RSD_ERR_INVALID_ARG;
+    }
+    out->triangle_count = s->triangle_count;
+    out->node_count = s->node_count;
+    out->max_depth = s->stats.max_depth;
+    out->leaf_count = s->stats.leaves;
+    out->sah_cost = s->stats.sah_cost;
+    out->build_ms = s->stats.build_ms;
+    out->device_bytes = s->device_bytes;
+    return RSD_OK;
+}
+
+extern "C" void rsd_scene_release(rsd_scene* s) {
+    if (!s) return;
+    (void)hipSetDevice(s->dev->hip_device);
+    (void)hipFree(s->d_nodes);
+    (void)hipFree(s->d_tris);
+    (void)hipFree(s->d_counters);
+    delete s;
+}
+
+// ---- Camera::calculateCameraParameters, Camera.cpp:99-185 (preserveHeight), with
+//      MatrixMath.h:686-712 (RightHanded look-at) and VectorMath.h:1731 normalize.
+namespace {
+struct v3 { float x, y, z; };
+inline float dot3(v3 a, v3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+inline v3 cross3(v3 a, v3 b) { return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x}; }
+inline v3 norm3(v3 v) {
+    float inv = 1.0f / std::sqrt(dot3(v, v));
+    return {v.x * inv, v.y * inv, v.z * inv};
+}
+}  // namespace
+
+extern "C" rsd_status rsd_camera_look_at(const float pos[3], const float target[3], const float up[3],
+                                         float focal_length, float frame_height, float aspect_ratio, float near_z,
+                                         float far_z, float focal_distance, rsd_camera* c) {
+    if (!pos || !target || !up || !c) {
+        set_error("rsd_camera_look_at: null argument");
+        return RSD_ERR_INVALID_ARG;
+    }
+    std::memset(c, 0, sizeof(*c));
+    const v3 P{pos[0], pos[1], pos[2]}, T{target[0], target[1], target[2]}, Up{up[0], up[1], up[2]};
+    for (int i = 0; i < 3; ++i) c->posW[i] = pos[i];
+    c->nearZ = near_z;
+    c->farZ = far_z;
+    c->focalLength = focal_length;
+    c->frameHeight = frame_height;
+    c->aspectRatio = aspect_ratio;
+    c->frameWidth = frame_height * aspect_ratio;
+    const float fovY = focal_length == 0.0f ? 0.0f : 2.0f * std::atan(0.5f * frame_height / focal_length);
+    const v3 f = norm3({P.x - T.x, P.y - T.y, P.z - T.z});
+    const v3 r = norm3(cross3(Up, f));
+    const v3 u = cross3(f, r);
+    float* m = c->viewMat;
+    m[0] = r.x; m[1] = r.y; m[2] = r.z; m[3] = -dot3(r, P);
+    m[4] = u.x; m[5] = u.y; m[6] = u.z; m[7] = -dot3(u, P);
+    m[8] = f.x; m[9] = f.y; m[10] = f.z; m[11] = -dot3(f, P);
+    m[15] = 1.0f;
+    const v3 w = norm3({T.x - P.x, T.y - P.y, T.z - P.z});
+    const v3 W{w.x * focal_distance, w.y * focal_distance, w.z * focal_distance};
+    const v3 cu = norm3(cross3(W, Up));
+    const v3 cv = norm3(cross3(cu, W));
+    const float ulen = focal_distance * std::tan(fovY * 0.5f) * aspect_ratio;
+    const float vlen = focal_distance * std::tan(fovY * 0.5f);
+    c->W[0] = W.x; c->W[1] = W.y; c->W[2] = W.z;
+    c->U[0] = cu.x * ulen; c->U[1] = cu.y * ulen; c->U[2] = cu.z * ulen;
+    c->V[0] = cv.x * vlen; c->V[1] = cv.y * vlen; c->V[2] = cv.z * vlen;
+    return RSD_OK;
+}
+
+// SVAO::compile (SVAO.cpp:143-150), getStochMapSize (:700-716), getExtraGuardBand (:718-723)
+extern "C" rsd_status rsd_svao_make_vao_data(uint32_t fb_w, uint32_t fb_h, uint32_t divisor, int32_t sd_guard_px,
+                                             float radius, float exponent, float thickness, rsd_vao_data* out,
+                                             uint32_t* sd_w, uint32_t* sd_h) {
+    if (!out || fb_w == 0 || fb_h == 0 || divisor == 0 || sd_guard_px < 0) {
+        set_error("rsd_svao_make_vao_data: invalid argument");
+        return RSD_ERR_INVALID_ARG;
+    }
+    rsd_vao_data d{};
+    d.resolution[0] = (float)fb_w;
+    d.resolution[1] = (float)fb_h;
+    d.invResolution[0] = 1.0f / d.resolution[0];
+    d.invResolution[1] = 1.0f / d.resolution[1];
+    d.sdGuard = sd_guard_px / (int32_t)divisor;
+    const uint32_t lw = divisor > 1 ? (fb_w + divisor - 1) / divisor : fb_w;
+    const uint32_t lh = divisor > 1 ? (fb_h + divisor - 1) / divisor : fb_h;
+    d.lowResolution[0] = (float)lw;
+    d.lowResolution[1] = (float)lh;
+    d.noiseScale[0] = d.resolution[0] / 4.0f;
+    d.noiseScale[1] = d.resolution[1] / 4.0f;
+    d.radius = radius;
+    d.exponent = exponent;
+    d.thickness = thickness;
+    d.ssRadiusCutoff = 6.0f;   // VAOData.slang:43
+    d.ssMaxRadius = 512.0f;    // VAOData.slang:44
+    *out = d;
+    if (sd_w) *sd_w = lw + 2u * (uint32_t)d.sdGuard;
+    if (sd_h) *sd_h = lh + 2u * (uint32_t)d.sdGuard;
+    return RSD_OK;
+}

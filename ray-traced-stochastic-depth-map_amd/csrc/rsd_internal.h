@@ -1,0 +1,35 @@
+// rsd_internal.h -- librsd private state shared by the host entry points and the launchers.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <string>
+
+#include "../../include/rsd.h"
+#include "bvh_build.h"
+
+struct rsd_device {
+    int hip_device = 0;
+    int cu_count = 0;
+};
+
+struct rsd_scene {
+    rsd_device* dev = nullptr;
+    float4* d_nodes = nullptr;   // 4 x float4 per inner node
+    float4* d_tris = nullptr;    // 3 x float4 per triangle record
+    uint32_t triangle_count = 0;
+    uint32_t node_count = 0;
+    rsd::BvhStats stats;
+    uint64_t device_bytes = 0;
+    unsigned long long* d_counters = nullptr;  // 5 x u64 scratch for instrumented traces
+};
+
+namespace rsd {
+void set_error(const std::string& msg);
+rsd_status hip_fail(hipError_t e, const char* what);
+}  // namespace rsd
+
+#define RSD_HIP(call)                                                   \
+    do {                                                                \
+        hipError_t e_ = (call);                                         \
+        if (e_ != hipSuccess) return rsd::hip_fail(e_, #call);          \
+    } while (0)

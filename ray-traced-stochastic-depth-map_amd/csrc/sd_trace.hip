@@ -1,0 +1,615 @@
+// sd_trace.hip -- the Ray-SD hot path on gfx950: BVH2 k-nearest any-hit traversal
+// that fills the stochastic depth map, plus the primary-visibility (G-buffer) kernel
+// built on the same traversal.
+//
+// Reference: StochasticDepthMapRT.rt.slang:39-105 (rayGen / anyHit),
+//            Common.slangh:65-92 (initRayDesc), :102-254 (algorithm),
+//            IntersectionHelpers.slang:109-180 (watertight triangle test),
+//            Camera.slang:46-90 (pinhole rays).
+//
+// Any-hit order.  DXR calls any-hit in an unspecified order.  Here the
+// any-hit stream is CANONICAL: ascending (t, primitive id), each triangle at most once.
+// The Default reservoir and the KBuffer commit no later than the MAX_COUNT-th hit and a
+// commit ends the stream (TMax = t), so the result only depends on the MAX_COUNT nearest
+// hits: each lane keeps a sorted k-list of the k nearest (t, prim) keys in VGPRs, prunes
+// the traversal with the k-th key exactly like a DXR commit shrinks TMax, and runs the
+// reference algorithm over the sorted list afterwards.  The coverage-mask variant (no
+// count bound) continues in chunks of k keys after the last one processed.  The result is
+// independent of the BVH and of the traversal order -- the property the CPU oracle checks.
+//
+// Kernel shape: one lane per SD texel, one 64-lane wave per 8x8 texel tile (coherent
+// primary rays), node stack in LDS (16 entries / lane) with a private overflow.  Nodes are
+// 64-B {child boxes, refs} records fetched as 4 x 16-B loads; triangles 48-B records.
+#include <algorithm>
+#include <vector>
+
+#include "rsd_device.h"
+#include "rsd_internal.h"
+
+namespace rsd {
+
+constexpr int kTile = 8;               // 8x8 texels per wave
+constexpr int kBlock = kTile * kTile;  // 64 threads
+constexpr int kLdsStack = 16;
+constexpr int kStackTotal = 64;        // >= kBvhMaxDepth + 2
+
+struct RayCtx {
+    f3 o, d;
+    int kx, ky, kz;
+    float Sx, Sy, Sz;
+    f3 invd, oinvd;
+};
+
+__device__ __forceinline__ float comp(f3 v, int k) { return k == 0 ? v.x : (k == 1 ? v.y : v.z); }
+
+__device__ __forceinline__ void ray_setup(RayCtx& r, f3 o, f3 d) {
+    r.o = o;
+    r.d = d;
+    float ax = fabsf(d.x), ay = fabsf(d.y), az = fabsf(d.z);
+    int axis = 0;
+    if (ay > ax && ay > az) axis = 1;
+    if (az > ax && az > ay) axis = 2;
+    r.kz = axis;
+    r.kx = axis == 2 ? 0 : axis + 1;
+    r.ky = r.kx == 2 ? 0 : r.kx + 1;
+    if (comp(d, r.kz) < 0.0f) { int s = r.kx; r.kx = r.ky; r.ky = s; }
+    float dz = comp(d, r.kz);
+    r.Sx = comp(d, r.kx) / dz;
+    r.Sy = comp(d, r.ky) / dz;
+    r.Sz = 1.0f / dz;
+    // box test reciprocal: avoid 0 * inf = NaN for axis-parallel rays
+    auto safe = [](float v) { return fabsf(v) > 1e-20f ? v : copysignf(1e-20f, v); };
+    r.invd = mk(1.0f / safe(d.x), 1.0f / safe(d.y), 1.0f / safe(d.z));
+    r.oinvd = mk(o.x * r.invd.x, o.y * r.invd.y, o.z * r.invd.z);
+}
+
+// IntersectionHelpers.slang:109-180 -- bit-identical to the oracle (no contraction).
+__device__ __forceinline__ bool intersect_tri(const RayCtx& r, float4 a, float4 b, float4 c, float& t, float& bu,
+                                              float& bv, float& detOut) {
+    f3 A = mk(a.x - r.o.x, a.y - r.o.y, a.z - r.o.z);
+    f3 B = mk(b.x - r.o.x, b.y - r.o.y, b.z - r.o.z);
+    f3 C = mk(c.x - r.o.x, c.y - r.o.y, c.z - r.o.z);
+    const float Akz = comp(A, r.kz), Bkz = comp(B, r.kz), Ckz = comp(C, r.kz);
+    const float Ax = comp(A, r.kx) - r.Sx * Akz;
+    const float Ay = comp(A, r.ky) - r.Sy * Akz;
+    const float Bx = comp(B, r.kx) - r.Sx * Bkz;
+    const float By = comp(B, r.ky) - r.Sy * Bkz;
+    const float Cx = comp(C, r.kx) - r.Sx * Ckz;
+    const float Cy = comp(C, r.ky) - r.Sy * Ckz;
+    float U = Cx * By - Cy * Bx;
+    float V = Ax * Cy - Ay * Cx;
+    float W = Bx * Ay - By * Ax;
+    if (U == 0.0f || V == 0.0f || W == 0.0f) {
+        double CxBy = (double)Cx * (double)By, CyBx = (double)Cy * (double)Bx;
+        U = (float)(CxBy - CyBx);
+        double AxCy = (double)Ax * (double)Cy, AyCx = (double)Ay * (double)Cx;
+        V = (float)(AxCy - AyCx);
+        double BxAy = (double)Bx * (double)Ay, ByAx = (double)By * (double)Ax;
+        W = (float)(BxAy - ByAx);
+    }
+    if ((U < 0.0f || V < 0.0f || W < 0.0f) && (U > 0.0f || V > 0.0f || W > 0.0f)) return false;
+    const float det = U + V + W;
+    if (det == 0.0f) return false;
+    const float Az = r.Sz * Akz, Bz = r.Sz * Bkz, Cz = r.Sz * Ckz;
+    const float T = U * Az + V * Bz + W * Cz;
+    const float rcpDet = 1.0f / det;
+    t = T * rcpDet;
+    bu = V * rcpDet;
+    bv = W * rcpDet;
+    detOut = det;
+    return true;
+}
+
+// det > 0 <=> counter-clockwise seen from the ray origin = Falcor front face (unless
+// the mesh is frontFaceCW); double-sided disables culling (Scene.cpp:3446-3452).
+__device__ __forceinline__ bool culled(float det, uint32_t flags, uint32_t cull) {
+    if (cull == 0u || (flags & 1u)) return false;
+    const bool front = (det > 0.0f) != ((flags & 2u) != 0u);
+    return cull == 1u ? !front : front;
+}
+
+// Conservative slab test: entry/exit widened by a relative 1e-5 so that a node is skipped
+// only if it cannot hold a reported hit in [tlo, thi].
+__device__ __forceinline__ bool box_hit(const RayCtx& r, float lox, float hix, float loy, float hiy, float loz,
+                                        float hiz, float tlo, float thi, float& tnear) {
+    float x0 = fmaf(lox, r.invd.x, -r.oinvd.x), x1 = fmaf(hix, r.invd.x, -r.oinvd.x);
+    float y0 = fmaf(loy, r.invd.y, -r.oinvd.y), y1 = fmaf(hiy, r.invd.y, -r.oinvd.y);
+    float z0 = fmaf(loz, r.invd.z, -r.oinvd.z), z1 = fmaf(hiz, r.invd.z, -r.oinvd.z);
+    float tn = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fminf(z0, z1));
+    float tf = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fmaxf(z0, z1));
+    float m = 1e-5f * (fabsf(tn) + fabsf(tf));
+    tn -= m;
+    tf += m;
+    tnear = tn;
+    return fmaxf(tn, tlo) <= fminf(tf, thi);
+}
+
+__device__ __forceinline__ bool key_less(float ta, uint32_t pa, float tb, uint32_t pb) {
+    return ta < tb || (ta == tb && pa < pb);
+}
+
+template <int K>
+struct KList {
+    float t[K];
+    uint32_t p[K];
+    uint32_t l[K];
+    __device__ __forceinline__ void clear() {
+#pragma unroll
+        for (int j = 0; j < K; ++j) { t[j] = INFINITY; p[j] = 0xffffffffu; l[j] = 0u; }
+    }
+    // insert keeping ascending (t, prim) order; the largest key falls off the end
+    __device__ __forceinline__ void insert(float nt, uint32_t np, uint32_t nl) {
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            const bool lt = key_less(nt, np, t[j], p[j]);
+            const float tt = t[j];
+            const uint32_t pp = p[j], ll = l[j];
+            t[j] = lt ? nt : tt;
+            p[j] = lt ? np : pp;
+            l[j] = lt ? nl : ll;
+            nt = lt ? tt : nt;
+            np = lt ? pp : np;
+            nl = lt ? ll : nl;
+        }
+    }
+};
+
+struct TraceStats {
+    uint32_t nodes, tris;
+};
+
+// Collects the K smallest keys (t, prim) with tmin <= t <= tmax, key > (lbT, lbP) when
+// useLB, culling applied.  Returns the number of keys found (<= K).
+template <int K>
+__device__ __forceinline__ int trace_knearest(const float4* __restrict__ nodes, const float4* __restrict__ tris,
+                                              const RayCtx& r, float tmin, float tmax, uint32_t cull, bool useLB,
+                                              float lbT, uint32_t lbP, KList<K>& kl, uint32_t* __restrict__ lds,
+                                              TraceStats& st) {
+    kl.clear();
+    uint32_t spill[kStackTotal - kLdsStack];
+    int sp = 0;
+    int found = 0;
+    uint32_t node = 0;
+    const float tlo = useLB ? fmaxf(tmin, lbT) : tmin;
+    while (true) {
+        const float4 n0 = nodes[4 * node + 0];
+        const float4 n1 = nodes[4 * node + 1];
+        const float4 n2 = nodes[4 * node + 2];
+        const uint4 n3 = reinterpret_cast<const uint4*>(nodes)[4 * node + 3];
+        st.nodes++;
+        const float thi = fminf(tmax, kl.t[K - 1]);
+        float tn0, tn1;
+        bool h0 = box_hit(r, n0.x, n0.y, n0.z, n0.w, n2.x, n2.y, tlo, thi, tn0);
+        bool h1 = box_hit(r, n1.x, n1.y, n1.z, n1.w, n2.z, n2.w, tlo, thi, tn1);
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            const bool hc = c == 0 ? h0 : h1;
+            const uint32_t cnt = c == 0 ? n3.z : n3.w;
+            if (hc && cnt > 0u) {
+                const uint32_t first = c == 0 ? n3.x : n3.y;
+                for (uint32_t i = first; i < first + cnt; ++i) {
+                    const float4 a = tris[3 * i + 0];
+                    const float4 b = tris[3 * i + 1];
+                    const float4 cc = tris[3 * i + 2];
+                    st.tris++;
+                    float t, bu, bv, det;
+                    if (!intersect_tri(r, a, b, cc, t, bu, bv, det)) continue;
+                    if (!(t >= tmin && t <= tmax)) continue;
+                    const uint32_t prim = __float_as_uint(a.w);
+                    if (culled(det, __float_as_uint(b.w), cull)) continue;
+                    if (useLB && !key_less(lbT, lbP, t, prim)) continue;
+                    if (!key_less(t, prim, kl.t[K - 1], kl.p[K - 1])) continue;
+                    kl.insert(t, prim, i);
+                    found = found < K ? found + 1 : K;
+                }
+                if (c == 0) h0 = false; else h1 = false;
+            }
+        }
+        if (h0 && h1) {
+            const bool nearIs0 = tn0 <= tn1;
+            const uint32_t nearN = nearIs0 ? n3.x : n3.y;
+            const uint32_t farN = nearIs0 ? n3.y : n3.x;
+            if (sp < kLdsStack) lds[sp * kBlock] = farN;
+            else spill[sp - kLdsStack] = farN;
+            ++sp;
+            node = nearN;
+        } else if (h0) {
+            node = n3.x;
+        } else if (h1) {
+            node = n3.y;
+        } else {
+            if (sp == 0) break;
+            --sp;
+            node = sp < kLdsStack ? lds[sp * kBlock] : spill[sp - kLdsStack];
+        }
+    }
+    return found;
+}
+
+// ------------------------------------------------------------------------------------
+// SD map kernel
+// ------------------------------------------------------------------------------------
+struct SDArgs {
+    const float4* nodes;
+    const float4* tris;
+    rsd_camera cam;
+    const float* linearZ;
+    int zW, zH;
+    const uint32_t* rayMin;
+    const uint32_t* rayMax;
+    float* sd;
+    int sdW, sdH;
+    int guard;
+    uint32_t impl, maxCount, jitter, normalize, rayInterval, cull;
+    float alpha;
+    const int32_t* lutIdx;  // coverage mask: stratified indices [N+1]
+    const uint32_t* lut;    // coverage mask: look-up table [2^N]
+    unsigned long long* counters;
+};
+
+__device__ __forceinline__ f3 cam_dir(const rsd_camera& c, float px, float py) {
+    const float ndcx = 2.0f * px + -1.0f;
+    const float ndcy = -2.0f * py + 1.0f;
+    return mk(ndcx * c.U[0] + ndcy * c.V[0] + c.W[0], ndcx * c.U[1] + ndcy * c.V[1] + c.W[1],
+              ndcx * c.U[2] + ndcy * c.V[2] + c.W[2]);
+}
+
+template <int K, int N>
+__global__ void __launch_bounds__(kBlock) sd_trace_kernel(SDArgs a) {
+    __shared__ uint32_t sstack[kLdsStack * kBlock];
+    const int lane = threadIdx.x;
+    const int x = blockIdx.x * kTile + (lane & (kTile - 1));
+    const int y = blockIdx.y * kTile + (lane / kTile);
+    const bool inside = x < a.sdW && y < a.sdH;
+    const rsd_camera& c = a.cam;
+    const float DEFAULT = a.normalize ? 1.0f : 3.40282347e+37f;  // Common.slangh:16
+
+    float depths[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) depths[i] = DEFAULT;
+    TraceStats st{0u, 0u};
+    uint32_t active = 0, hitsDelivered = 0;
+
+    if (inside) {
+        // ---- initRayDesc, Common.slangh:65-92
+        const int dimx = a.sdW - 2 * a.guard, dimy = a.sdH - 2 * a.guard;
+        const int sx = x - a.guard, sy = y - a.guard;
+        const f3 wn = normalize(mk(c.W[0], c.W[1], c.W[2]));
+        const f3 dc = normalize(cam_dir(c, ((float)sx + 0.5f) / (float)dimx + -c.jitterX,
+                                        ((float)sy + 0.5f) / (float)dimy + c.jitterY));
+        const float invCos = 1.0f / dot(wn, dc);
+        float TMax = c.farZ * invCos;
+        float jx, jy;
+        sd_jitter((uint32_t)x, (uint32_t)y, a.jitter != 0u, jx, jy);
+        const f3 d = normalize(cam_dir(c, ((float)sx + jx) / (float)dimx, ((float)sy + jy) / (float)dimy));
+        const float eps = 0.1f * c.nearZ;
+        float depth = 0.0f;
+        if (sx >= 0 && sy >= 0 && sx < dimx && sy < dimy)
+            depth = tex_bilinear(a.linearZ, a.zW, a.zH, ((float)sx + 0.5f) / (float)dimx,
+                                 ((float)sy + 0.5f) / (float)dimy, true);
+        const float cosT = dot(wn, d);
+        float TMin = depth / cosT + eps;
+        if (a.rayInterval) {
+            const size_t o = (size_t)y * a.sdW + x;
+            const uint32_t iMin = a.rayMin ? a.rayMin[o] : 0u;
+            if (iMin != 0u) TMin = hmax(asfloat(iMin), TMin);
+            const uint32_t iMax = a.rayMax ? a.rayMax[o] : 0u;
+            if (iMax != 0u) TMax = hmin(asfloat(iMax), TMax);
+        }
+
+        if (TMin <= TMax) {
+            active = 1;
+            RayCtx r;
+            ray_setup(r, mk(c.posW[0], c.posW[1], c.posW[2]), d);
+            KList<K> kl;
+            uint32_t count = 0;
+            bool commit = false, useLB = false;
+            float lbT = 0.0f;
+            uint32_t lbP = 0u;
+            while (!commit) {
+                const int found = trace_knearest<K>(a.nodes, a.tris, r, TMin, TMax, a.cull, useLB, lbT, lbP, kl,
+                                                    &sstack[lane], st);
+                // ---- anyHit -> algorithm (Common.slangh:102-254), ascending (t, prim)
+#pragma unroll
+                for (int j = 0; j < K; ++j) {
+                    if (commit || j >= found) continue;
+                    // barycentrics of the j-th hit: re-run the identical test on its record
+                    const uint32_t ti = kl.l[j];
+                    float t, bu, bv, det;
+                    intersect_tri(r, a.tris[3 * ti], a.tris[3 * ti + 1], a.tris[3 * ti + 2], t, bu, bv, det);
+                    hitsDelivered++;
+                    const float rng = sd_hash(bu, bv);
+                    float z = t * cosT;  // RayToViewDepth
+                    if (a.normalize) z = saturate((z - c.nearZ) / (c.farZ - c.nearZ));
+                    if (a.impl == 1u) {  // CoverageMask, Common.slangh:117-131, 189-209
+                        const int R = (int)floorf(a.alpha * (float)N + rng);
+                        uint32_t mask = 0u;
+                        if (R >= N) mask = 0xffffu;
+                        else if (R != 0) {
+                            const float rng2 = sd_hash(rng, z);  // hash3D(float3(bary, t))
+                            const float lo = (float)a.lutIdx[R], hi = (float)a.lutIdx[R + 1];
+                            mask = a.lut[(int)(lo + rng2 * (hi - lo))];
+                        }
+                        float maxT = 0.0f;
+#pragma unroll
+                        for (int i = 0; i < N; ++i) {
+                            if ((mask & (1u << i)) && z < depths[i]) depths[i] = z;
+                            maxT = hmax(maxT, depths[i]);
+                        }
+                        commit = !(z < maxT);
+                    } else if (a.impl == 3u) {  // KBuffer, Common.slangh:132-135, 211-232
+                        if (z >= depths[N - 1]) {
+                            commit = true;
+                        } else {
+                            count++;
+                            const float rayT = z;
+#pragma unroll
+                            for (int i = 0; i < N; ++i)
+                                if (z < depths[i]) { const float tmp = depths[i]; depths[i] = z; z = tmp; }
+                            commit = (depths[N - 1] == rayT) || count >= a.maxCount;
+                        }
+                    } else {  // Default reservoir, Common.slangh:136-153, 234-247
+                        uint32_t slot = count++;
+                        if (count > (uint32_t)N) slot = (uint32_t)(rng * (float)count);
+#pragma unroll
+                        for (int i = 0; i < N; ++i)
+                            if ((uint32_t)i == slot && !(depths[i] <= z)) depths[i] = z;
+                        commit = count >= a.maxCount;
+                    }
+                }
+                if (found < K) break;  // stream exhausted
+                useLB = true;
+                lbT = kl.t[K - 1];
+                lbP = kl.p[K - 1];
+            }
+        }
+
+        // ---- store, StochasticDepthMapRT.rt.slang:90-104 (Texture2DArray layout)
+        const size_t plane = (size_t)a.sdW * a.sdH;
+        const size_t o = (size_t)y * a.sdW + x;
+        if constexpr (N == 1) {
+            a.sd[o] = depths[0];
+        } else if constexpr (N == 2) {
+            reinterpret_cast<float2*>(a.sd)[o] = make_float2(depths[0], depths[1]);
+        } else {
+#pragma unroll
+            for (int l = 0; l < N / 4; ++l)
+                reinterpret_cast<float4*>(a.sd)[l * plane + o] =
+                    make_float4(depths[4 * l], depths[4 * l + 1], depths[4 * l + 2], depths[4 * l + 3]);
+        }
+    }
+    if (a.counters) {
+        atomicAdd(&a.counters[0], (unsigned long long)(inside ? 1u : 0u));
+        atomicAdd(&a.counters[1], (unsigned long long)active);
+        atomicAdd(&a.counters[2], (unsigned long long)st.nodes);
+        atomicAdd(&a.counters[3], (unsigned long long)st.tris);
+        atomicAdd(&a.counters[4], (unsigned long long)hitsDelivered);
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// Primary visibility: closest (t, prim) hit in [near/cos, far/cos] (Camera.slang:46-59),
+// linear depth = t * cos (LinearizeDepth), view-space face normal packed 2x8
+// (CompressNormals.ps.slang, viewSpace + use16Bit).  Miss: depth = farZ, normal = 0.
+// ------------------------------------------------------------------------------------
+struct GBArgs {
+    const float4* nodes;
+    const float4* tris;
+    rsd_camera cam;
+    int W, H;
+    uint32_t cull;
+    float* z;
+    uint16_t* n;
+};
+
+__global__ void __launch_bounds__(kBlock) gbuffer_kernel(GBArgs a) {
+    __shared__ uint32_t sstack[kLdsStack * kBlock];
+    const int lane = threadIdx.x;
+    const int x = blockIdx.x * kTile + (lane & (kTile - 1));
+    const int y = blockIdx.y * kTile + (lane / kTile);
+    if (x >= a.W || y >= a.H) return;
+    const rsd_camera& c = a.cam;
+    const f3 wn = normalize(mk(c.W[0], c.W[1], c.W[2]));
+    const f3 d = normalize(cam_dir(c, ((float)x + 0.5f) / (float)a.W + -c.jitterX,
+                                   ((float)y + 0.5f) / (float)a.H + c.jitterY));
+    const float cosT = dot(wn, d);
+    const float invCos = 1.0f / cosT;
+    RayCtx r;
+    ray_setup(r, mk(c.posW[0], c.posW[1], c.posW[2]), d);
+    KList<1> kl;
+    TraceStats st{0u, 0u};
+    const int found = trace_knearest<1>(a.nodes, a.tris, r, c.nearZ * invCos, c.farZ * invCos, a.cull, false, 0.0f,
+                                        0u, kl, &sstack[lane], st);
+    const size_t o = (size_t)y * a.W + x;
+    if (!found) {
+        a.z[o] = c.farZ;
+        a.n[o] = 0;
+        return;
+    }
+    a.z[o] = kl.t[0] * cosT;
+    const uint32_t ti = kl.l[0];
+    const float4 v0 = a.tris[3 * ti], v1 = a.tris[3 * ti + 1], v2 = a.tris[3 * ti + 2];
+    const f3 e1 = mk(v1.x - v0.x, v1.y - v0.y, v1.z - v0.z);
+    const f3 e2 = mk(v2.x - v0.x, v2.y - v0.y, v2.z - v0.z);
+    const f3 nw = normalize(cross(e1, e2));
+    const float* m = c.viewMat;
+    const f3 nv = mk(m[0] * nw.x + m[1] * nw.y + m[2] * nw.z, m[4] * nw.x + m[5] * nw.y + m[6] * nw.z,
+                     m[8] * nw.x + m[9] * nw.y + m[10] * nw.z);
+    a.n[o] = (uint16_t)encode_normal_2x8(nv);
+}
+
+// ------------------------------------------------------------------------------------
+// launchers
+// ------------------------------------------------------------------------------------
+template <int K>
+static hipError_t launch_sd_k(const SDArgs& a, uint32_t N, dim3 grid, hipStream_t s) {
+    switch (N) {
+        case 1: hipLaunchKernelGGL((sd_trace_kernel<K, 1>), grid, dim3(kBlock), 0, s, a); break;
+        case 2: hipLaunchKernelGGL((sd_trace_kernel<K, 2>), grid, dim3(kBlock), 0, s, a); break;
+        case 4: hipLaunchKernelGGL((sd_trace_kernel<K, 4>), grid, dim3(kBlock), 0, s, a); break;
+        case 8: hipLaunchKernelGGL((sd_trace_kernel<K, 8>), grid, dim3(kBlock), 0, s, a); break;
+        case 16: hipLaunchKernelGGL((sd_trace_kernel<K, 16>), grid, dim3(kBlock), 0, s, a); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+}  // namespace rsd
+
+using namespace rsd;
+
+namespace {
+struct LutCache {
+    int n = -1;
+    int32_t* d_idx = nullptr;
+    uint32_t* d_lut = nullptr;
+};
+thread_local LutCache g_lut[17];
+
+rsd_status ensure_lut(uint32_t N, const int32_t** idx, const uint32_t** lut) {
+    LutCache& c = g_lut[N];
+    if (c.n != (int)N) {
+        // StochasticDepthMapRT.cpp:79-124 generateStratifiedLookupTable
+        std::vector<int32_t> ind(N + 1);
+        std::vector<uint32_t> tab(1u << N);
+        auto binom = [](int n, int k) {
+            std::vector<int> C(k + 1, 0);
+            C[0] = 1;
+            for (int i = 1; i <= n; i++)
+                for (int j = std::min(i, k); j > 0; j--) C[j] = C[j] + C[j - 1];
+            return C[k];
+        };
+        ind[0] = 0;
+        for (uint32_t i = 1; i <= N; i++) ind[i] = binom((int)N, (int)i - 1) + ind[i - 1];
+        std::vector<int32_t> cur(ind);
+        tab[0] = 0;
+        for (uint32_t i = 1; i < (1u << N); i++) {
+            int pc = __builtin_popcount(i);
+            tab[cur[pc]] = i;
+            cur[pc]++;
+        }
+        RSD_HIP(hipMalloc(&c.d_idx, sizeof(int32_t) * ind.size()));
+        RSD_HIP(hipMalloc(&c.d_lut, sizeof(uint32_t) * tab.size()));
+        RSD_HIP(hipMemcpy(c.d_idx, ind.data(), sizeof(int32_t) * ind.size(), hipMemcpyHostToDevice));
+        RSD_HIP(hipMemcpy(c.d_lut, tab.data(), sizeof(uint32_t) * tab.size(), hipMemcpyHostToDevice));
+        c.n = (int)N;
+    }
+    *idx = c.d_idx;
+    *lut = c.d_lut;
+    return RSD_OK;
+}
+}  // namespace
+
+extern "C" rsd_status rsd_sd_trace(rsd_scene* scene, const rsd_camera* cam, const rsd_sd_params* p,
+                                   const float* d_linear_z, uint32_t z_w, uint32_t z_h, const uint32_t* d_ray_min,
+                                   const uint32_t* d_ray_max, float* d_sd_out, uint32_t sd_w, uint32_t sd_h,
+                                   rsd_counters* counters, rsd_stream stream) {
+    if (!scene || !cam || !p || !d_linear_z || !d_sd_out || sd_w == 0 || sd_h == 0 || z_w == 0 || z_h == 0) {
+        set_error("rsd_sd_trace: null argument or empty extent");
+        return RSD_ERR_INVALID_ARG;
+    }
+    const uint32_t N = p->sample_count;
+    if (N != 1 && N != 2 && N != 4 && N != 8 && N != 16) {
+        // StochasticDepthMapRT.cpp:190 throws for other N; 16 is the documented extension
+        set_error("rsd_sd_trace: SampleCount must be 1, 2, 4, 8 or 16");
+        return RSD_ERR_UNSUPPORTED;
+    }
+    if (p->implementation == RSD_SD_RESERVOIR_SAMPLING || p->implementation > RSD_SD_KBUFFER) {
+        set_error("rsd_sd_trace: ReservoirSampling is a raster-only implementation");
+        return RSD_ERR_UNSUPPORTED;
+    }
+    if (p->max_count == 0 && p->implementation != RSD_SD_COVERAGE_MASK) {
+        set_error("rsd_sd_trace: MaxCount must be >= 1");
+        return RSD_ERR_INVALID_ARG;
+    }
+    if (2 * p->guard_band >= (int32_t)sd_w || 2 * p->guard_band >= (int32_t)sd_h || p->guard_band < 0) {
+        set_error("rsd_sd_trace: GuardBand leaves no interior");
+        return RSD_ERR_INVALID_ARG;
+    }
+    if (scene->triangle_count == 0) {
+        // no geometry: every texel keeps DEFAULT_DEPTH
+        const float def = p->normalize ? 1.0f : 3.40282347e+37f;
+        std::vector<float> h((size_t)sd_w * sd_h * (N < 4 ? N : 4) * ((N + 3) / 4), def);
+        RSD_HIP(hipMemcpyAsync(d_sd_out, h.data(), h.size() * sizeof(float), hipMemcpyHostToDevice, (hipStream_t)stream));
+        RSD_HIP(hipStreamSynchronize((hipStream_t)stream));
+        if (counters) *counters = rsd_counters{(uint64_t)sd_w * sd_h, 0, 0, 0, 0};
+        return RSD_OK;
+    }
+    SDArgs a;
+    a.nodes = scene->d_nodes;
+    a.tris = scene->d_tris;
+    a.cam = *cam;
+    a.linearZ = d_linear_z;
+    a.zW = (int)z_w;
+    a.zH = (int)z_h;
+    a.rayMin = d_ray_min;
+    a.rayMax = d_ray_max;
+    a.sd = d_sd_out;
+    a.sdW = (int)sd_w;
+    a.sdH = (int)sd_h;
+    a.guard = p->guard_band;
+    a.impl = p->implementation;
+    a.maxCount = p->max_count;
+    a.jitter = p->jitter;
+    a.normalize = p->normalize;
+    a.rayInterval = p->ray_interval;
+    a.cull = p->cull_mode;
+    a.alpha = p->alpha;
+    a.lutIdx = nullptr;
+    a.lut = nullptr;
+    a.counters = nullptr;
+    if (p->implementation == RSD_SD_COVERAGE_MASK) {
+        rsd_status s = ensure_lut(N, &a.lutIdx, &a.lut);
+        if (s != RSD_OK) return s;
+    }
+    hipStream_t s = (hipStream_t)stream;
+    if (counters) {
+        RSD_HIP(hipMemsetAsync(scene->d_counters, 0, 5 * sizeof(unsigned long long), s));
+        a.counters = scene->d_counters;
+    }
+    dim3 grid((sd_w + kTile - 1) / kTile, (sd_h + kTile - 1) / kTile);
+    // k = the MAX_COUNT nearest keys decide Default and KBuffer; coverage mask streams chunks
+    const uint32_t need = p->implementation == RSD_SD_COVERAGE_MASK ? 8u : p->max_count;
+    hipError_t e;
+    if (need <= 4) e = launch_sd_k<4>(a, N, grid, s);
+    else if (need <= 8) e = launch_sd_k<8>(a, N, grid, s);
+    else e = launch_sd_k<16>(a, N, grid, s);
+    if (e != hipSuccess) return hip_fail(e, "sd_trace_kernel launch");
+    if (counters) {
+        unsigned long long h[5];
+        RSD_HIP(hipMemcpyAsync(h, scene->d_counters, sizeof(h), hipMemcpyDeviceToHost, s));
+        RSD_HIP(hipStreamSynchronize(s));
+        counters->rays_dispatched = h[0];
+        counters->rays_active = h[1];
+        counters->nodes_visited = h[2];
+        counters->tris_tested = h[3];
+        counters->hits_delivered = h[4];
+    }
+    return RSD_OK;
+}
+
+extern "C" rsd_status rsd_gbuffer(rsd_scene* scene, const rsd_camera* cam, uint32_t width, uint32_t height,
+                                  uint32_t cull_mode, float* d_linear_z, uint16_t* d_normals, rsd_stream stream) {
+    if (!scene || !cam || !d_linear_z || !d_normals || width == 0 || height == 0) {
+        set_error("rsd_gbuffer: null argument or empty extent");
+        return RSD_ERR_INVALID_ARG;
+    }
+    if (cull_mode > 2) {
+        set_error("rsd_gbuffer: cull_mode must be 0, 1 or 2");
+        return RSD_ERR_INVALID_ARG;
+    }
+    hipStream_t s = (hipStream_t)stream;
+    if (scene->triangle_count == 0) {
+        std::vector<float> z((size_t)width * height, cam->farZ);
+        RSD_HIP(hipMemcpyAsync(d_linear_z, z.data(), z.size() * 4, hipMemcpyHostToDevice, s));
+        RSD_HIP(hipMemsetAsync(d_normals, 0, (size_t)width * height * 2, s));
+        RSD_HIP(hipStreamSynchronize(s));
+        return RSD_OK;
+    }
+    GBArgs a{scene->d_nodes, scene->d_tris, *cam, (int)width, (int)height, cull_mode, d_linear_z, d_normals};
+    dim3 grid((width + kTile - 1) / kTile, (height + kTile - 1) / kTile);
+    hipLaunchKernelGGL(gbuffer_kernel, grid, dim3(kBlock), 0, s, a);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return hip_fail(e, "gbuffer_kernel launch");
+    return RSD_OK;
+}

@@ -1,0 +1,130 @@
+"""ctypes binding of librsd's C ABI (include/rsd.h).
+
+This is the binding a Python host (Falcor's scripting layer, a test, the bench)
+uses; it mirrors the header one to one.  There is no fallback: if librsd.so is
+missing or a call fails, a RuntimeError is raised with rsd_last_error().
+"""
+from __future__ import annotations
+
+import ctypes as C
+from pathlib import Path
+
+PKG_DIR = Path(__file__).resolve().parents[1]
+LIB_PATH = PKG_DIR / "librsd.so"
+
+RSD_OK = 0
+STATUS_NAMES = {0: "RSD_OK", 1: "RSD_ERR_INVALID_ARG", 2: "RSD_ERR_UNSUPPORTED", 3: "RSD_ERR_HIP",
+                4: "RSD_ERR_OUT_OF_MEMORY", 5: "RSD_ERR_NO_DEVICE"}
+
+TRI_DOUBLE_SIDED = 1
+TRI_FRONT_CW = 2
+TRI_ALPHA_MASK = 4
+
+SD_DEFAULT, SD_COVERAGE_MASK, SD_RESERVOIR_SAMPLING, SD_KBUFFER = 0, 1, 2, 3
+CULL_NONE, CULL_BACK, CULL_FRONT = 0, 1, 2
+
+
+class SceneDesc(C.Structure):
+    _fields_ = [("positions", C.c_void_p), ("vertex_count", C.c_uint32), ("indices", C.c_void_p),
+                ("triangle_count", C.c_uint32), ("triangle_flags", C.c_void_p)]
+
+
+class SceneInfo(C.Structure):
+    _fields_ = [("triangle_count", C.c_uint32), ("node_count", C.c_uint32), ("max_depth", C.c_uint32),
+                ("leaf_count", C.c_uint32), ("sah_cost", C.c_double), ("build_ms", C.c_double),
+                ("device_bytes", C.c_uint64)]
+
+
+class Camera(C.Structure):
+    _fields_ = [("posW", C.c_float * 3), ("nearZ", C.c_float),
+                ("U", C.c_float * 3), ("farZ", C.c_float),
+                ("V", C.c_float * 3), ("focalLength", C.c_float),
+                ("W", C.c_float * 3), ("frameHeight", C.c_float),
+                ("frameWidth", C.c_float), ("jitterX", C.c_float), ("jitterY", C.c_float),
+                ("aspectRatio", C.c_float), ("viewMat", C.c_float * 16)]
+
+
+class SDParams(C.Structure):
+    _fields_ = [("sample_count", C.c_uint32), ("implementation", C.c_uint32), ("max_count", C.c_uint32),
+                ("guard_band", C.c_int32), ("jitter", C.c_uint32), ("normalize", C.c_uint32),
+                ("ray_interval", C.c_uint32), ("cull_mode", C.c_uint32), ("alpha_test", C.c_uint32),
+                ("alpha", C.c_float)]
+
+
+class VAOData(C.Structure):
+    _fields_ = [("noiseScale", C.c_float * 2), ("resolution", C.c_float * 2),
+                ("lowResolution", C.c_float * 2), ("invResolution", C.c_float * 2),
+                ("radius", C.c_float), ("exponent", C.c_float), ("thickness", C.c_float),
+                ("sdGuard", C.c_int32), ("ssRadiusCutoff", C.c_float), ("ssMaxRadius", C.c_float)]
+
+
+class SVAOParams(C.Structure):
+    _fields_ = [("num_directions", C.c_uint32), ("sd_samples", C.c_uint32),
+                ("secondary_depth_mode", C.c_uint32), ("ray_interval", C.c_uint32),
+                ("sd_jitter", C.c_uint32), ("guard_band", C.c_uint32)]
+
+
+class Counters(C.Structure):
+    _fields_ = [("rays_dispatched", C.c_uint64), ("rays_active", C.c_uint64), ("nodes_visited", C.c_uint64),
+                ("tris_tested", C.c_uint64), ("hits_delivered", C.c_uint64)]
+
+
+# every symbol include/rsd.h declares (checked by tests/test_abi.py)
+EXPORTS = ["rsd_abi_version", "rsd_last_error", "rsd_device_open", "rsd_device_close", "rsd_scene_upload",
+           "rsd_scene_info_get", "rsd_scene_release", "rsd_camera_look_at", "rsd_svao_make_vao_data",
+           "rsd_gbuffer", "rsd_sd_trace", "rsd_svao_clear_intervals", "rsd_svao_pass1", "rsd_svao_pass2"]
+
+_lib = None
+
+
+def lib():
+    """Load librsd.so (in-tree).  Raises if it has not been built."""
+    global _lib
+    if _lib is None:
+        if not LIB_PATH.exists():
+            raise RuntimeError(f"librsd.so not found at {LIB_PATH}: build it with `make -C {PKG_DIR}` "
+                               "(or __graft_entry__.build()); there is no CPU fallback")
+        L = C.CDLL(str(LIB_PATH))
+        vp, u32, i32, f32, st = C.c_void_p, C.c_uint32, C.c_int32, C.c_float, C.c_int
+        L.rsd_abi_version.restype = u32
+        L.rsd_last_error.restype = C.c_char_p
+        L.rsd_device_open.restype = st
+        L.rsd_device_open.argtypes = [C.c_int, C.POINTER(vp)]
+        L.rsd_device_close.argtypes = [vp]
+        L.rsd_scene_upload.restype = st
+        L.rsd_scene_upload.argtypes = [vp, C.POINTER(SceneDesc), C.POINTER(vp)]
+        L.rsd_scene_info_get.restype = st
+        L.rsd_scene_info_get.argtypes = [vp, C.POINTER(SceneInfo)]
+        L.rsd_scene_release.argtypes = [vp]
+        L.rsd_camera_look_at.restype = st
+        L.rsd_camera_look_at.argtypes = [vp, vp, vp, f32, f32, f32, f32, f32, f32, C.POINTER(Camera)]
+        L.rsd_svao_make_vao_data.restype = st
+        L.rsd_svao_make_vao_data.argtypes = [u32, u32, u32, i32, f32, f32, f32, C.POINTER(VAOData),
+                                             C.POINTER(u32), C.POINTER(u32)]
+        L.rsd_gbuffer.restype = st
+        L.rsd_gbuffer.argtypes = [vp, C.POINTER(Camera), u32, u32, u32, vp, vp, vp]
+        L.rsd_sd_trace.restype = st
+        L.rsd_sd_trace.argtypes = [vp, C.POINTER(Camera), C.POINTER(SDParams), vp, u32, u32, vp, vp, vp, u32, u32,
+                                   C.POINTER(Counters), vp]
+        L.rsd_svao_clear_intervals.restype = st
+        L.rsd_svao_clear_intervals.argtypes = [vp, vp, u32, vp]
+        L.rsd_svao_pass1.restype = st
+        L.rsd_svao_pass1.argtypes = [C.POINTER(Camera), C.POINTER(VAOData), C.POINTER(SVAOParams), vp, vp, u32, u32,
+                                     vp, vp, vp, vp, u32, u32, vp]
+        L.rsd_svao_pass2.restype = st
+        L.rsd_svao_pass2.argtypes = [C.POINTER(Camera), C.POINTER(VAOData), C.POINTER(SVAOParams), vp, vp, u32, u32,
+                                     vp, vp, u32, u32, vp, vp]
+        _lib = L
+    return _lib
+
+
+class RsdError(RuntimeError):
+    def __init__(self, status, where):
+        msg = lib().rsd_last_error().decode(errors="replace")
+        super().__init__(f"{where}: {STATUS_NAMES.get(status, status)}: {msg}")
+        self.status = status
+
+
+def check(status, where):
+    if status != RSD_OK:
+        raise RsdError(status, where)

@@ -1,0 +1,215 @@
+"""Frame-level driver of the Ray-SD + SVAO hot path on one GPU.
+
+`Renderer` owns one rsd_device, one uploaded scene and the device buffers of one
+frame, and issues exactly the dispatch sequence of SVAO::execute (SVAO.cpp:192-456):
+
+    clear ray intervals  ->  "AO 1" (pass 1)  ->  StochasticDepthMapRT (SD trace)
+    ->  "AO 2" (pass 2)
+
+The G-buffer (linear depth + packed view-space normals) is produced once by the
+primary-visibility kernel; it is an input of the hot path, not part of it
+(AO frame time excludes the G-buffer and the BVH build).
+
+Device memory comes from torch (plumbing only); every compute step is a librsd
+C-ABI call on torch's current HIP stream.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import dataclasses
+
+import numpy as np
+
+from . import abi
+from .scenes import Scene
+
+
+@dataclasses.dataclass
+class FrameConfig:
+    """One BASELINE config: visible size + GuardBand, SD divisor, SD samples, SVAO knobs.
+
+    Defaults follow scripts/SVAO.py:10-12 (guardBand 64, radius 0.2, stochMapDivisor 4)
+    and SVAO.h:90-126 (N = 4, MAX_COUNT = 8, jitter, ray interval, back-face culling,
+    512-px SD guard band, 8 AO directions)."""
+    visible_w: int = 1920
+    visible_h: int = 1080
+    guard_band: int = 64
+    divisor: int = 4
+    sd_samples: int = 4
+    max_count: int = 8
+    implementation: int = abi.SD_DEFAULT
+    jitter: bool = True
+    ray_interval: bool = True
+    cull_mode: int = abi.CULL_BACK
+    radius: float = 0.2
+    exponent: float = 2.0
+    thickness: float = 0.0
+    sd_guard_px: int = 512
+    num_directions: int = 8
+    focal_length: float = 21.0
+    frame_height: float = 24.0
+    near: float = 0.1
+    far: float = 1000.0
+
+    @property
+    def fb_w(self):
+        return self.visible_w + 2 * self.guard_band
+
+    @property
+    def fb_h(self):
+        return self.visible_h + 2 * self.guard_band
+
+
+CONFIGS = {
+    # BASELINE.json configs[1..4] (configs[0] is the CPU-only plumbing case, see tests)
+    "suntemple_1080p_q": (dict(visible_w=1920, visible_h=1080, divisor=4, sd_samples=4), "suntemple"),
+    "bistro_1080p_full": (dict(visible_w=1920, visible_h=1080, divisor=1, sd_samples=8), "bistro_exterior"),
+    "emerald_4k_q": (dict(visible_w=3840, visible_h=2160, divisor=4, sd_samples=4), "emerald_square"),
+    "bistro_4k_full_n16": (dict(visible_w=3840, visible_h=2160, divisor=1, sd_samples=16, max_count=16),
+                           "bistro_exterior"),
+}
+
+
+def make_camera(scene: Scene, cfg: FrameConfig) -> abi.Camera:
+    cam = abi.Camera()
+    f3 = lambda v: (C.c_float * 3)(*[float(x) for x in v])
+    aspect = np.float32(cfg.fb_w) / np.float32(cfg.fb_h)
+    abi.check(abi.lib().rsd_camera_look_at(f3(scene.camera["pos"]), f3(scene.camera["target"]), f3(scene.camera["up"]),
+                                           cfg.focal_length, cfg.frame_height, float(aspect), cfg.near, cfg.far,
+                                           10000.0, C.byref(cam)), "rsd_camera_look_at")
+    return cam
+
+
+def make_vao(cfg: FrameConfig):
+    vao = abi.VAOData()
+    w, h = C.c_uint32(), C.c_uint32()
+    abi.check(abi.lib().rsd_svao_make_vao_data(cfg.fb_w, cfg.fb_h, cfg.divisor, cfg.sd_guard_px, cfg.radius,
+                                               cfg.exponent, cfg.thickness, C.byref(vao), C.byref(w), C.byref(h)),
+              "rsd_svao_make_vao_data")
+    return vao, w.value, h.value
+
+
+def sd_params(cfg: FrameConfig, sd_guard: int) -> abi.SDParams:
+    # SVAO::compile builds the nested SD pass with these Properties (SVAO.cpp:158-183)
+    return abi.SDParams(cfg.sd_samples, cfg.implementation, cfg.max_count, sd_guard, int(cfg.jitter), 1,
+                        int(cfg.ray_interval), cfg.cull_mode, 0, float(np.float32(1.5 / cfg.sd_samples)))
+
+
+def svao_params(cfg: FrameConfig) -> abi.SVAOParams:
+    return abi.SVAOParams(cfg.num_directions, cfg.sd_samples, 2, int(cfg.ray_interval), int(cfg.jitter),
+                          cfg.guard_band)
+
+
+class Device:
+    def __init__(self, index: int = 0):
+        h = C.c_void_p()
+        abi.check(abi.lib().rsd_device_open(index, C.byref(h)), "rsd_device_open")
+        self.h = h
+        self.index = index
+
+    def close(self):
+        if self.h:
+            abi.lib().rsd_device_close(self.h)
+            self.h = None
+
+
+class GpuScene:
+    def __init__(self, dev: Device, scene: Scene):
+        desc = abi.SceneDesc(scene.positions.ctypes.data, scene.positions.shape[0], scene.indices.ctypes.data,
+                             scene.indices.shape[0], scene.flags.ctypes.data)
+        h = C.c_void_p()
+        abi.check(abi.lib().rsd_scene_upload(dev.h, C.byref(desc), C.byref(h)), "rsd_scene_upload")
+        self.h = h
+        self.info = abi.SceneInfo()
+        abi.check(abi.lib().rsd_scene_info_get(h, C.byref(self.info)), "rsd_scene_info_get")
+
+    def release(self):
+        if self.h:
+            abi.lib().rsd_scene_release(self.h)
+            self.h = None
+
+
+def _ptr(t):
+    return C.c_void_p(t.data_ptr()) if t is not None else None
+
+
+class Renderer:
+    """Owns the frame buffers of one config on one GPU and runs the hot path."""
+
+    def __init__(self, scene: Scene, cfg: FrameConfig, device: int = 0, gpu_scene: GpuScene | None = None,
+                 dev: Device | None = None):
+        import torch
+        self.torch = torch
+        self.cfg = cfg
+        self.scene = scene
+        self.dev = dev or Device(device)
+        torch.cuda.set_device(self.dev.index)
+        self.gscene = gpu_scene or GpuScene(self.dev, scene)
+        self.cam = make_camera(scene, cfg)
+        self.vao, self.sd_w, self.sd_h = make_vao(cfg)
+        self.sdp = sd_params(cfg, self.vao.sdGuard)
+        self.svp = svao_params(cfg)
+        W, H, N = cfg.fb_w, cfg.fb_h, cfg.sd_samples
+        dv = torch.device("cuda", self.dev.index)
+        self.depth = torch.empty((H, W), dtype=torch.float32, device=dv)
+        self.normals = torch.empty((H, W), dtype=torch.int16, device=dv)
+        self.ao = torch.zeros((H, W), dtype=torch.uint8, device=dv)  # SVAO.cpp:307 clears on first use
+        self.stencil = torch.zeros((H, W), dtype=torch.uint8, device=dv)
+        self.ray_min = torch.empty((self.sd_h, self.sd_w), dtype=torch.int32, device=dv)
+        self.ray_max = torch.empty((self.sd_h, self.sd_w), dtype=torch.int32, device=dv)
+        self.sd = torch.empty(((N + 3) // 4, self.sd_h, self.sd_w, min(N, 4)), dtype=torch.float32, device=dv)
+
+    @property
+    def stream(self):
+        return C.c_void_p(self.torch.cuda.current_stream().cuda_stream)
+
+    @property
+    def sd_rays(self) -> int:
+        return self.sd_w * self.sd_h
+
+    def gbuffer(self):
+        abi.check(abi.lib().rsd_gbuffer(self.gscene.h, C.byref(self.cam), self.cfg.fb_w, self.cfg.fb_h,
+                                        self.cfg.cull_mode, _ptr(self.depth), _ptr(self.normals), self.stream),
+                  "rsd_gbuffer")
+
+    def clear_intervals(self):
+        abi.check(abi.lib().rsd_svao_clear_intervals(_ptr(self.ray_min), _ptr(self.ray_max), self.sd_w * self.sd_h,
+                                                     self.stream), "rsd_svao_clear_intervals")
+
+    def pass1(self):
+        abi.check(abi.lib().rsd_svao_pass1(C.byref(self.cam), C.byref(self.vao), C.byref(self.svp), _ptr(self.depth),
+                                           _ptr(self.normals), self.cfg.fb_w, self.cfg.fb_h, _ptr(self.ao),
+                                           _ptr(self.stencil), _ptr(self.ray_min), _ptr(self.ray_max), self.sd_w,
+                                           self.sd_h, self.stream), "rsd_svao_pass1")
+
+    def sd_trace(self, counters: bool = False):
+        cnt = abi.Counters() if counters else None
+        abi.check(abi.lib().rsd_sd_trace(self.gscene.h, C.byref(self.cam), C.byref(self.sdp), _ptr(self.depth),
+                                         self.cfg.fb_w, self.cfg.fb_h, _ptr(self.ray_min), _ptr(self.ray_max),
+                                         _ptr(self.sd), self.sd_w, self.sd_h,
+                                         C.byref(cnt) if cnt is not None else None, self.stream), "rsd_sd_trace")
+        return cnt
+
+    def pass2(self):
+        abi.check(abi.lib().rsd_svao_pass2(C.byref(self.cam), C.byref(self.vao), C.byref(self.svp), _ptr(self.depth),
+                                           _ptr(self.normals), self.cfg.fb_w, self.cfg.fb_h, _ptr(self.stencil),
+                                           _ptr(self.sd), self.sd_w, self.sd_h, _ptr(self.ao), self.stream),
+                  "rsd_svao_pass2")
+
+    def frame(self):
+        """One AO frame: the span of the reference's "AO 1" + "AORefine" profile scopes."""
+        self.clear_intervals()
+        self.pass1()
+        self.sd_trace()
+        self.pass2()
+
+    def numpy(self):
+        t = self.torch
+        t.cuda.synchronize()
+        return dict(depth=self.depth.cpu().numpy(), normals=self.normals.cpu().numpy().view(np.uint16),
+                    ao=self.ao.cpu().numpy(), stencil=self.stencil.cpu().numpy(),
+                    ray_min=self.ray_min.cpu().numpy().view(np.uint32),
+                    ray_max=self.ray_max.cpu().numpy().view(np.uint32), sd=self.sd.cpu().numpy())
+
+    def close(self):
+        self.gscene.release()

@@ -1,0 +1,201 @@
+"""CPU tests of the oracle itself: intersection / culling conventions, normal packing,
+and the any-hit-stream semantics of the SD trace against a brute-force restatement
+(every triangle tested, hits sorted by (t, prim), algorithm replayed in numpy float32)."""
+import math
+
+import numpy as np
+import pytest
+
+from helpers import oracle_vao
+
+F = np.float32
+
+
+def test_watertight_facing_convention(oracle):
+    # ray down -z onto a triangle that is counter-clockwise seen from the origin
+    o, d = [0.25, 0.25, 10.0], [0.0, 0.0, -1.0]
+    v0, v1, v2 = [0, 0, 0], [1, 0, 0], [0, 1, 0]
+    hit, t, u, v, det = oracle.intersect(o, d, v0, v1, v2)
+    assert hit and t == 10.0 and det > 0
+    assert (u, v) == (0.25, 0.25)  # DXR barycentrics = weights of v1, v2
+    hit, t, u, v, det = oracle.intersect(o, d, v0, v2, v1)
+    assert hit and det < 0
+    assert not oracle.intersect([2.0, 2.0, 10.0], d, v0, v1, v2)[0]
+
+
+def test_watertight_shared_edge(oracle):
+    # rays through the diagonal shared by two triangles of a quad never fall through
+    rng = np.random.default_rng(5)
+    a, b, c, e = [0, 0, 0], [1, 0, 0], [1, 1, 0], [0, 1, 0]
+    for s in rng.random(500):
+        p = [float(F(s)), float(F(s)), 3.0]
+        h1 = oracle.intersect(p, [0, 0, -1], a, b, c)[0]
+        h2 = oracle.intersect(p, [0, 0, -1], a, c, e)[0]
+        assert h1 or h2
+
+
+def test_normal_packing_roundtrip(oracle):
+    rng = np.random.default_rng(1)
+    for n in rng.normal(size=(300, 3)):
+        n = (n / np.linalg.norm(n)).astype(np.float32)
+        d = oracle.decode_normal(oracle.encode_normal(n))
+        assert np.linalg.norm(d - n) < 0.03
+    assert oracle.encode_normal([0, 0, 1]) == 0
+    assert oracle.encode_normal([1, 0, 0]) == 127
+    assert oracle.encode_normal([0, 1, 0]) == 127 << 8
+    assert np.allclose(oracle.decode_normal(0), [0, 0, 1])
+
+
+def _layered_scene(n_planes=12, seed=3, jitter=0.0):
+    """Stacked, slightly tilted quads in front of the camera (many hits per ray)."""
+    rng = np.random.default_rng(seed)
+    pos, ind = [], []
+    for k in range(n_planes):
+        z = -2.0 - 0.7 * k + jitter * rng.random()
+        tilt = 0.05 * rng.standard_normal()
+        q = np.array([[-3, -3, z], [3, -3, z + tilt], [3, 3, z + 2 * tilt], [-3, 3, z + tilt]], np.float32)
+        base = len(pos) * 4
+        pos.append(q)
+        # alternate winding so that back-face culling removes some planes
+        if k % 3 == 2:
+            ind += [[base, base + 2, base + 1], [base, base + 3, base + 2]]
+        else:
+            ind += [[base, base + 1, base + 2], [base, base + 2, base + 3]]
+    return np.concatenate(pos), np.array(ind, np.uint32)
+
+
+def _replay(hits, N, impl, max_count, cosT, near, far, alpha):
+    """Common.slangh:102-254 over the sorted hit stream, numpy float32."""
+    depths = [F(1.0)] * N
+    count = 0
+    idx = lut = None
+    if impl == 1:
+        idx = [sum(math.comb(N, j) for j in range(i)) for i in range(N + 1)]
+        lut = [0] + sorted(range(1, 1 << N), key=lambda m: (bin(m).count("1"), m))
+    for t, u, v in hits:
+        rng = F(hash_(u, v))
+        z = F(F(t) * F(cosT))
+        z = F(min(max(F(F(z - F(near)) / F(F(far) - F(near))), F(0)), F(1)))
+        if impl == 1:
+            R = int(math.floor(F(F(F(alpha) * F(N)) + rng)))
+            mask = 0
+            if R >= N:
+                mask = 0xFFFF
+            elif R != 0:
+                r2 = F(hash_(rng, z))
+                lo, hi = F(idx[R]), F(idx[R + 1])
+                mask = lut[int(F(lo + F(r2 * F(hi - lo))))]
+            maxT = F(0)
+            for i in range(N):
+                if (mask >> i) & 1 and z < depths[i]:
+                    depths[i] = z
+                maxT = max(maxT, depths[i])
+            if not z < maxT:
+                break
+        elif impl == 3:
+            if z >= depths[N - 1]:
+                break
+            count += 1
+            rayT = z
+            for i in range(N):
+                if z < depths[i]:
+                    depths[i], z = z, depths[i]
+            if depths[N - 1] == rayT or count >= max_count:
+                break
+        else:
+            slot = count
+            count += 1
+            if count > N:
+                slot = int(F(rng * F(count)))
+            if slot < N and not depths[slot] <= z:
+                depths[slot] = z
+            if count >= max_count:
+                break
+    return depths
+
+
+hash_ = None
+
+
+@pytest.mark.parametrize("impl,N,max_count,cull", [(0, 4, 8, 1), (0, 1, 1, 1), (0, 8, 8, 0), (0, 2, 5, 2),
+                                                   (3, 4, 8, 1), (3, 2, 3, 0), (1, 4, 8, 1), (1, 8, 8, 0),
+                                                   (0, 16, 16, 0)])
+def test_sd_trace_equals_bruteforce_sorted_stream(oracle, impl, N, max_count, cull):
+    global hash_
+    hash_ = oracle.hash2
+    pos, ind = _layered_scene()
+    flags = np.zeros(len(ind), np.uint32)
+    flags[::5] = 1  # some double-sided triangles
+    sc = oracle.Scene(pos, ind, flags)
+    W = H = 12
+    cam = oracle.camera_look_at([0.1, 0.2, 1.0], [0.0, 0.0, -5.0], [0, 1, 0], aspect=1.0)
+    lz = np.zeros((H, W), np.float32)  # TMin = 0.1 * near
+    p = oracle.SDParams(N, impl, max_count, 0, 1, 1, 0, cull, 0, float(F(1.5 / N)))
+    sd, stats = oracle.sd_trace(sc, cam, p, lz, None, None, W, H, threads=2)
+    tris = pos[ind]
+    for y in range(H):
+        for x in range(W):
+            o, d, tmin, tmax, cosT = oracle.sd_ray(cam, p, lz, None, None, W, H, x, y)
+            hits = []
+            for prim, (v0, v1, v2) in enumerate(tris):
+                hit, t, u, v, det = oracle.intersect(o, d, v0, v1, v2)
+                if not hit or not (tmin <= t <= tmax):
+                    continue
+                if cull and not flags[prim] & 1:
+                    front = det > 0
+                    if (cull == 1 and not front) or (cull == 2 and front):
+                        continue
+                hits.append((t, prim, u, v))
+            hits.sort(key=lambda h: (h[0], h[1]))
+            want = _replay([(t, u, v) for t, _, u, v in hits], N, impl, max_count, cosT, cam.nearZ, cam.farZ,
+                           float(F(1.5 / N)))
+            got = [sd[k // 4, y, x, k % 4] for k in range(N)] if N >= 4 else list(sd[0, y, x, :N])
+            assert [F(g) for g in got] == want, (x, y, hits[:10])
+
+
+def test_sd_result_depends_only_on_max_count_nearest_hits(oracle):
+    """Default reservoir commits at the MAX_COUNT-th hit: planes behind it are irrelevant."""
+    pos, ind = _layered_scene(n_planes=14)
+    W = H = 16
+    cam = oracle.camera_look_at([0.0, 0.0, 1.0], [0.0, 0.0, -5.0], [0, 1, 0], aspect=1.0)
+    lz = np.zeros((H, W), np.float32)
+    p = oracle.SDParams(4, 0, 8, 0, 1, 1, 0, 0, 0, 0.375)
+    full, _ = oracle.sd_trace(oracle.Scene(pos, ind), cam, p, lz, None, None, W, H)
+    # keep the 8 nearest planes (16 triangles) only
+    cut, _ = oracle.sd_trace(oracle.Scene(pos, ind[:16]), cam, p, lz, None, None, W, H)
+    assert np.array_equal(full, cut)
+
+
+def test_sd_empty_interval_keeps_default_depth(oracle):
+    pos, ind = _layered_scene()
+    sc = oracle.Scene(pos, ind)
+    W = H = 8
+    cam = oracle.camera_look_at([0.0, 0.0, 1.0], [0.0, 0.0, -5.0], [0, 1, 0], aspect=1.0)
+    lz = np.zeros((H, W), np.float32)
+    rmin = np.full((H, W), np.float32(3.4028235e38).view(np.uint32), np.uint32)  # cleared (SVAO.cpp:339)
+    rmax = np.zeros((H, W), np.uint32)
+    p = oracle.SDParams(4, 0, 8, 0, 1, 1, 1, 1, 0, 0.375)
+    sd, stats = oracle.sd_trace(sc, cam, p, lz, rmin, rmax, W, H)
+    assert stats[0] == 0 and np.all(sd == 1.0)
+
+
+def test_svao_pass1_interval_invariants(oracle):
+    from rsd.scenes import make_scene
+    s = make_scene("arcade_tiny")
+    sc = oracle.Scene(s.positions, s.indices, s.flags)
+    g, vis = 16, (96, 64)
+    W, H = vis[0] + 2 * g, vis[1] + 2 * g
+    cam = oracle.camera_look_at(s.camera["pos"], s.camera["target"], s.camera["up"], aspect=float(F(W) / F(H)))
+    z, n = oracle.gbuffer(sc, cam, W, H)
+    vao, sdW, sdH = oracle_vao(oracle, W, H, 2, sd_guard_px=64, radius=1.5)
+    p = oracle.SVAOParams(8, 4, 2, 1, 1, g)
+    ao, st, rmin, rmax = oracle.svao_pass1(cam, vao, p, z, n, sdW, sdH)
+    touched = rmax != 0
+    assert touched.any() and (st != 0).any()
+    assert np.all(rmin[~touched] == np.float32(3.4028235e38).view(np.uint32))
+    assert np.all(rmin[touched].view(np.float32) <= rmax[touched].view(np.float32))
+    # pass 2 only rewrites stencilled pixels
+    N = 4
+    sd = np.ones((1, sdH, sdW, N), np.float32)
+    ao2 = oracle.svao_pass2(cam, vao, p, z, n, st, sd, ao)
+    assert np.array_equal(ao2[st == 0], ao[st == 0])
