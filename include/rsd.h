@@ -59,7 +59,7 @@ typedef struct {
 
 typedef struct {
     uint32_t triangle_count;
-    uint32_t node_count;      /* BVH2 inner nodes (64 B each) */
+    uint32_t node_count;      /* 4-wide BVH nodes (128 B each) */
     uint32_t max_depth;
     uint32_t leaf_count;
     double sah_cost;
@@ -122,9 +122,10 @@ typedef struct {
 typedef struct {
     uint64_t rays_dispatched;
     uint64_t rays_active;     /* TMin <= TMax after the ray interval */
-    uint64_t nodes_visited;   /* 64-B BVH2 nodes fetched */
+    uint64_t nodes_visited;   /* 128-B 4-wide BVH nodes fetched */
     uint64_t tris_tested;     /* 48-B triangle records fetched */
     uint64_t hits_delivered;  /* any-hit invocations (sorted stream) */
+    uint64_t max_nodes_per_ray; /* longest traversal (latency tail of the launch) */
 } rsd_counters;
 
 /* --- library / device ------------------------------------------------------------ */
@@ -180,6 +181,26 @@ rsd_status rsd_svao_pass2(const rsd_camera* cam, const rsd_vao_data* vao, const 
                           const float* d_depth, const uint16_t* d_normals, uint32_t width, uint32_t height,
                           const uint8_t* d_stencil, const float* d_sd, uint32_t sd_w, uint32_t sd_h,
                           uint8_t* d_ao, rsd_stream stream);
+
+/* --- screen-band sharding (multi-GPU) ----------------------------------
+ * Band b of B owns: pass-1/pass-2 rows whose 32-row group g (counted from the first
+ * visible row, SVAORaster.ps.slang:36 interleave) has g % B == b, and SD-map 8-row tile
+ * rows t with t % B == b.  The union over b = 0..B-1 is exactly the full-frame call;
+ * the functions above are band 0 of 1.  Interleaving balances sky vs. geometry. */
+rsd_status rsd_sd_trace_band(rsd_scene* scene, const rsd_camera* cam, const rsd_sd_params* params,
+                             const float* d_linear_z, uint32_t z_w, uint32_t z_h,
+                             const uint32_t* d_ray_min, const uint32_t* d_ray_max,
+                             float* d_sd_out, uint32_t sd_w, uint32_t sd_h,
+                             uint32_t band_index, uint32_t band_count, rsd_counters* counters, rsd_stream stream);
+rsd_status rsd_svao_pass1_band(const rsd_camera* cam, const rsd_vao_data* vao, const rsd_svao_params* params,
+                               const float* d_depth, const uint16_t* d_normals, uint32_t width, uint32_t height,
+                               uint8_t* d_ao, uint8_t* d_stencil, uint32_t* d_ray_min, uint32_t* d_ray_max,
+                               uint32_t sd_w, uint32_t sd_h, uint32_t band_index, uint32_t band_count,
+                               rsd_stream stream);
+rsd_status rsd_svao_pass2_band(const rsd_camera* cam, const rsd_vao_data* vao, const rsd_svao_params* params,
+                               const float* d_depth, const uint16_t* d_normals, uint32_t width, uint32_t height,
+                               const uint8_t* d_stencil, const float* d_sd, uint32_t sd_w, uint32_t sd_h,
+                               uint8_t* d_ao, uint32_t band_index, uint32_t band_count, rsd_stream stream);
 
 #ifdef __cplusplus
 }

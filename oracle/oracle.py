@@ -72,6 +72,9 @@ def lib():
         L.ocpu_sd_trace.argtypes = [vp, vp, vp, vp, u32, u32, vp, vp, vp, u32, u32, u32, u32, i32, vp]
         L.ocpu_sd_ray.argtypes = [vp, vp, vp, u32, u32, vp, vp, u32, u32, u32, u32, vp, vp, vp, vp]
         L.ocpu_svao_clear.argtypes = [vp, vp, u32]
+        L.ocpu_sd_trace_band.argtypes = [vp, vp, vp, vp, u32, u32, vp, vp, vp, u32, u32, u32, u32, u32, u32, i32, vp]
+        L.ocpu_svao_pass1_band.argtypes = [vp, vp, vp, vp, vp, u32, u32, vp, vp, vp, vp, u32, u32, u32, u32]
+        L.ocpu_svao_pass2_band.argtypes = [vp, vp, vp, vp, vp, u32, u32, vp, vp, u32, u32, vp, u32, u32, i32]
         L.ocpu_svao_pass1.argtypes = [vp, vp, vp, vp, vp, u32, u32, vp, vp, vp, vp, u32, u32]
         L.ocpu_svao_pass2.argtypes = [vp, vp, vp, vp, vp, u32, u32, vp, vp, u32, u32, vp, i32]
         L.ocpu_hash.restype = f32
@@ -221,3 +224,31 @@ def intersect(o, d, v0, v1, v2):
     hit = lib().ocpu_intersect(_p(f(o)), _p(f(d)), _p(f(v0)), _p(f(v1)), _p(f(v2)),
                                C.byref(t), C.byref(u), C.byref(v), C.byref(det))
     return bool(hit), t.value, u.value, v.value, det.value
+
+
+# ---- in-place, screen-band variants (used by the multi-process sharding tests)
+def svao_clear(rmin, rmax):
+    lib().ocpu_svao_clear(_p(rmin), _p(rmax), rmin.size)
+
+
+def svao_pass1_into(cam, vao, p, depth, normals, ao, st, rmin, rmax, band=(0, 1)):
+    H, W = depth.shape
+    sdH, sdW = rmin.shape
+    lib().ocpu_svao_pass1_band(C.byref(cam), C.byref(vao), C.byref(p), _p(depth), _p(normals), W, H, _p(ao), _p(st),
+                               _p(rmin), _p(rmax), sdW, sdH, band[0], band[1])
+
+
+def sd_trace_into(scene, cam, params, linearZ, rmin, rmax, sd, band=(0, 1), threads=None):
+    sdH, sdW = sd.shape[1], sd.shape[2]
+    stats = np.zeros(2, np.uint64)
+    lib().ocpu_sd_trace_band(scene.h, C.byref(cam), C.byref(params), _p(linearZ), linearZ.shape[1], linearZ.shape[0],
+                             _p(rmin), _p(rmax), _p(sd), sdW, sdH, 0, sdH, band[0], band[1], _threads(threads),
+                             _p(stats))
+    return stats
+
+
+def svao_pass2_into(cam, vao, p, depth, normals, stencil, sd, ao, band=(0, 1), threads=None):
+    H, W = depth.shape
+    sdH, sdW = sd.shape[1], sd.shape[2]
+    lib().ocpu_svao_pass2_band(C.byref(cam), C.byref(vao), C.byref(p), _p(depth), _p(normals), W, H, _p(stencil),
+                               _p(sd), sdW, sdH, _p(ao), band[0], band[1], _threads(threads))

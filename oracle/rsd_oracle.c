@@ -669,6 +669,7 @@ typedef struct {
     const uint32_t* rmin; const uint32_t* rmax;
     float* sd; uint32_t sdW, sdH;
     uint32_t y0, y1;
+    uint32_t bi, bc; /* band: 8-row tile rows t with t % bc == bi */
     uint64_t active, hits;
 } osd_job;
 
@@ -690,6 +691,7 @@ static void* o_sd_rows(void* arg)
 
     for (uint32_t y = j->y0; y < j->y1; ++y)
         for (uint32_t x = 0; x < j->sdW; ++x) {
+            if ((y / 8u) % j->bc != j->bi) break;
             float d[3], TMin, TMax, cosT;
             o_sd_ray(c, p, j->z, j->zW, j->zH, j->rmin, j->rmax, j->sdW, j->sdH, x, y, d, &TMin, &TMax, &cosT);
 
@@ -769,6 +771,16 @@ void ocpu_sd_trace(const oscene* s, const ocam* cam, const osd_params* p,
                    float* sd, uint32_t sdW, uint32_t sdH,
                    uint32_t row0, uint32_t row1, int nthreads, uint64_t* stats)
 {
+    ocpu_sd_trace_band(s, cam, p, linearZ, zW, zH, rayMin, rayMax, sd, sdW, sdH, row0, row1, 0, 1, nthreads, stats);
+}
+
+void ocpu_sd_trace_band(const oscene* s, const ocam* cam, const osd_params* p,
+                        const float* linearZ, uint32_t zW, uint32_t zH,
+                        const uint32_t* rayMin, const uint32_t* rayMax,
+                        float* sd, uint32_t sdW, uint32_t sdH,
+                        uint32_t row0, uint32_t row1, uint32_t band_index, uint32_t band_count,
+                        int nthreads, uint64_t* stats)
+{
     if (nthreads < 1) nthreads = 1;
     osd_job* jobs = (osd_job*)calloc((size_t)nthreads, sizeof(osd_job));
     for (int i = 0; i < nthreads; ++i) {
@@ -776,6 +788,7 @@ void ocpu_sd_trace(const oscene* s, const ocam* cam, const osd_params* p,
         jobs[i].z = linearZ; jobs[i].zW = zW; jobs[i].zH = zH;
         jobs[i].rmin = rayMin; jobs[i].rmax = rayMax;
         jobs[i].sd = sd; jobs[i].sdW = sdW; jobs[i].sdH = sdH;
+        jobs[i].bi = band_index; jobs[i].bc = band_count ? band_count : 1;
     }
     if (row1 > sdH) row1 = sdH;
     o_run_rows(o_sd_rows, jobs, sizeof(osd_job), row0, row1, nthreads, o_sd_setrows);
@@ -979,6 +992,15 @@ void ocpu_svao_pass1(const ocam* cam, const ovao* d, const osvao_params* p,
                      uint8_t* ao, uint8_t* stencil, uint32_t* rayMin, uint32_t* rayMax,
                      uint32_t sdW, uint32_t sdH)
 {
+    ocpu_svao_pass1_band(cam, d, p, depth, normals, W, H, ao, stencil, rayMin, rayMax, sdW, sdH, 0, 1);
+}
+
+void ocpu_svao_pass1_band(const ocam* cam, const ovao* d, const osvao_params* p,
+                          const float* depth, const uint16_t* normals, uint32_t W, uint32_t H,
+                          uint8_t* ao, uint8_t* stencil, uint32_t* rayMin, uint32_t* rayMax,
+                          uint32_t sdW, uint32_t sdH, uint32_t band_index, uint32_t band_count)
+{
+    if (!band_count) band_count = 1;
     octx x;
     o_ctx_init(&x, cam, d, p, depth, normals, W, H);
     const uint32_t g = p->guard_band;
@@ -987,6 +1009,7 @@ void ocpu_svao_pass1(const ocam* cam, const ovao* d, const osvao_params* p,
     uint32_t nx = ((W - 2 * g) + 31u) / 32u * 32u, ny = ((H - 2 * g) + 31u) / 32u * 32u;
     for (uint32_t oy = 0; oy < ny; ++oy)
         for (uint32_t ox = 0; ox < nx; ++ox) {
+            if ((oy / 32u) % band_count != band_index) break;
             uint32_t px = ox + g, py = oy + g;
             float u = ((float)px + 0.5f) * d->invResolution[0];
             float v = ((float)py + 0.5f) * d->invResolution[1];
@@ -1049,6 +1072,7 @@ void ocpu_svao_pass1(const ocam* cam, const ovao* d, const osvao_params* p,
 typedef struct {
     const octx* x; const uint8_t* stencil; const float* sd; uint32_t sdW, sdH; uint8_t* ao;
     uint32_t y0, y1;
+    uint32_t bi, bc; /* band: 32-row groups of visible rows */
 } op2_job;
 
 static void* o_pass2_rows(void* arg)
@@ -1061,6 +1085,7 @@ static void* o_pass2_rows(void* arg)
     const float depthRange = x->c->farZ - x->c->nearZ, depthOffset = x->c->nearZ;
     for (uint32_t py = j->y0; py < j->y1; ++py)
         for (uint32_t px = g; px < W - g; ++px) {
+            if (((py - g) / 32u) % j->bc != j->bi) break;
             size_t o = (size_t)py * W + px;
             uint32_t mask = j->stencil[o];
             if (mask == 0) continue;
@@ -1107,6 +1132,14 @@ void ocpu_svao_pass2(const ocam* cam, const ovao* d, const osvao_params* p,
                      const uint8_t* stencil, const float* sd, uint32_t sdW, uint32_t sdH,
                      uint8_t* ao, int nthreads)
 {
+    ocpu_svao_pass2_band(cam, d, p, depth, normals, W, H, stencil, sd, sdW, sdH, ao, 0, 1, nthreads);
+}
+
+void ocpu_svao_pass2_band(const ocam* cam, const ovao* d, const osvao_params* p,
+                          const float* depth, const uint16_t* normals, uint32_t W, uint32_t H,
+                          const uint8_t* stencil, const float* sd, uint32_t sdW, uint32_t sdH,
+                          uint8_t* ao, uint32_t band_index, uint32_t band_count, int nthreads)
+{
     octx x;
     o_ctx_init(&x, cam, d, p, depth, normals, W, H);
     if (nthreads < 1) nthreads = 1;
@@ -1114,6 +1147,7 @@ void ocpu_svao_pass2(const ocam* cam, const ovao* d, const osvao_params* p,
     for (int i = 0; i < nthreads; ++i) {
         jobs[i].x = &x; jobs[i].stencil = stencil; jobs[i].sd = sd;
         jobs[i].sdW = sdW; jobs[i].sdH = sdH; jobs[i].ao = ao;
+        jobs[i].bi = band_index; jobs[i].bc = band_count ? band_count : 1;
     }
     o_run_rows(o_pass2_rows, jobs, sizeof(op2_job), p->guard_band, H - p->guard_band, nthreads, o_p2_setrows);
     free(jobs);

@@ -124,6 +124,22 @@ void ocpu_svao_pass2(const ocam* cam, const ovao* d, const osvao_params* p,
                      const uint8_t* stencil, const float* sd, uint32_t sdW, uint32_t sdH,
                      uint8_t* ao, int nthreads);
 
+/* screen-band variants (multi-GPU sharding, same band rules as rsd.h) */
+void ocpu_sd_trace_band(const oscene* s, const ocam* cam, const osd_params* p,
+                        const float* linearZ, uint32_t zW, uint32_t zH,
+                        const uint32_t* rayMin, const uint32_t* rayMax,
+                        float* sd, uint32_t sdW, uint32_t sdH,
+                        uint32_t row0, uint32_t row1, uint32_t band_index, uint32_t band_count,
+                        int nthreads, uint64_t* stats);
+void ocpu_svao_pass1_band(const ocam* cam, const ovao* d, const osvao_params* p,
+                          const float* depth, const uint16_t* normals, uint32_t W, uint32_t H,
+                          uint8_t* ao, uint8_t* stencil, uint32_t* rayMin, uint32_t* rayMax,
+                          uint32_t sdW, uint32_t sdH, uint32_t band_index, uint32_t band_count);
+void ocpu_svao_pass2_band(const ocam* cam, const ovao* d, const osvao_params* p,
+                          const float* depth, const uint16_t* normals, uint32_t W, uint32_t H,
+                          const uint8_t* stencil, const float* sd, uint32_t sdW, uint32_t sdH,
+                          uint8_t* ao, uint32_t band_index, uint32_t band_count, int nthreads);
+
 /* constant tables / helpers exposed for golden-vector tests */
 float ocpu_hash(float x, float y);
 void ocpu_jitter(uint32_t x, uint32_t y, float* jx, float* jy);

@@ -6,6 +6,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstring>
+#include <functional>
 #include <limits>
 #include <thread>
 
@@ -192,31 +193,9 @@ FlatBvh build_bvh(const float* pos, uint32_t nv, const uint32_t* ind, uint32_t n
     else nodes[root].count = 0;
     const uint32_t ntmp = b.next.load();
 
-    // ---- flatten: each inner node stores both children's boxes; leaves are not nodes
-    // DFS order keeps a parent and its near subtree close together in memory.
-    std::vector<uint32_t> innerIndex(ntmp, 0xffffffffu);
-    std::vector<uint32_t> dfs;
-    dfs.reserve(ntmp);
-    std::vector<uint32_t> stack;
+    // ---- collapse the binary tree into 4-wide nodes and flatten (DFS order keeps a node
+    // and its nearest subtree close in memory).  Each wide node stores all child boxes.
     out.tris.reserve(12 * (size_t)nt);
-    uint32_t ninner = 0;
-    // a root that is itself a leaf becomes an inner node with one (leaf) child
-    const bool rootLeaf = nodes[root].left < 0;
-    if (!rootLeaf) {
-        stack.push_back(root);
-        while (!stack.empty()) {
-            uint32_t n = stack.back();
-            stack.pop_back();
-            innerIndex[n] = ninner++;
-            dfs.push_back(n);
-            // push right first so the left subtree is laid out next
-            for (int32_t c : {nodes[n].right, nodes[n].left})
-                if (nodes[c].left >= 0) stack.push_back((uint32_t)c);
-        }
-    } else {
-        ninner = 1;
-    }
-    out.nodes.assign(16 * (size_t)ninner, 0.0f);
     auto emit_tris = [&](const TNode& leaf) -> uint32_t {
         uint32_t first = (uint32_t)(out.tris.size() / 12);
         for (uint32_t k = 0; k < leaf.count; ++k) {
@@ -234,32 +213,54 @@ FlatBvh build_bvh(const float* pos, uint32_t nv, const uint32_t* ind, uint32_t n
     };
     auto down = [](float v) { return std::nextafter(std::nextafter(v, -INFINITY), -INFINITY); };
     auto up = [](float v) { return std::nextafter(std::nextafter(v, INFINITY), INFINITY); };
-    auto set_child = [&](float* nd, int slot, const TNode* c) {
-        float lo[3], hi[3];
-        uint32_t ref = 0xffffffffu, cnt = 0;
-        if (c && (c->count > 0 || c->left >= 0)) {
-            for (int k = 0; k < 3; ++k) { lo[k] = down(c->box.lo[k]); hi[k] = up(c->box.hi[k]); }
-            if (c->left >= 0) { ref = innerIndex[&*c - &nodes[0]]; cnt = 0; }
-            else { ref = emit_tris(*c); cnt = c->count; }
+    uint32_t nwide = 0;
+    // recursive: returns the wide-node index of binary node `n` (an inner node, or the root)
+    std::function<uint32_t(uint32_t)> build_wide = [&](uint32_t n) -> uint32_t {
+        const uint32_t me = nwide++;
+        out.nodes.resize(32 * (size_t)nwide, 0.0f);
+        uint32_t ch[kBvhWidth];
+        int nc = 0;
+        if (nodes[n].left < 0) {
+            if (nodes[n].count) ch[nc++] = n;  // a leaf root: one leaf child
         } else {
-            for (int k = 0; k < 3; ++k) { lo[k] = INFINITY; hi[k] = -INFINITY; }
+            ch[nc++] = (uint32_t)nodes[n].left;
+            ch[nc++] = (uint32_t)nodes[n].right;
+            while (nc < (int)kBvhWidth) {  // open the largest inner child
+                int best = -1;
+                double ba = -1.0;
+                for (int i = 0; i < nc; ++i)
+                    if (nodes[ch[i]].left >= 0 && nodes[ch[i]].box.area() > ba) { ba = nodes[ch[i]].box.area(); best = i; }
+                if (best < 0) break;
+                const uint32_t c = ch[best];
+                ch[best] = (uint32_t)nodes[c].left;
+                ch[nc++] = (uint32_t)nodes[c].right;
+            }
         }
-        if (slot == 0) { nd[0] = lo[0]; nd[1] = hi[0]; nd[2] = lo[1]; nd[3] = hi[1]; nd[8] = lo[2]; nd[9] = hi[2]; }
-        else { nd[4] = lo[0]; nd[5] = hi[0]; nd[6] = lo[1]; nd[7] = hi[1]; nd[10] = lo[2]; nd[11] = hi[2]; }
-        nd[12 + slot] = bits_as_float(ref);
-        nd[14 + slot] = bits_as_float(cnt);
+        uint32_t ref[kBvhWidth], cnt[kBvhWidth];
+        float lo[kBvhWidth][3], hi[kBvhWidth][3];
+        for (uint32_t i = 0; i < kBvhWidth; ++i) {
+            ref[i] = 0xffffffffu;
+            cnt[i] = 0;
+            for (int k = 0; k < 3; ++k) lo[i][k] = hi[i][k] = 0.0f;
+        }
+        for (int i = 0; i < nc; ++i) {
+            const TNode& c = nodes[ch[i]];
+            for (int k = 0; k < 3; ++k) { lo[i][k] = down(c.box.lo[k]); hi[i][k] = up(c.box.hi[k]); }
+            if (c.left >= 0) { ref[i] = build_wide(ch[i]); cnt[i] = 0; }
+            else { ref[i] = emit_tris(c); cnt[i] = c.count; }
+        }
+        float* nd = &out.nodes[32 * (size_t)me];
+        for (uint32_t i = 0; i < kBvhWidth; ++i) {
+            nd[0 + i] = lo[i][0];  nd[4 + i] = hi[i][0];
+            nd[8 + i] = lo[i][1];  nd[12 + i] = hi[i][1];
+            nd[16 + i] = lo[i][2]; nd[20 + i] = hi[i][2];
+            nd[24 + i] = bits_as_float(ref[i]);
+            nd[28 + i] = bits_as_float(cnt[i]);
+        }
+        return me;
     };
-    if (rootLeaf) {
-        set_child(&out.nodes[0], 0, nt ? &nodes[root] : nullptr);
-        set_child(&out.nodes[0], 1, nullptr);
-    } else {
-        for (uint32_t i = 0; i < ninner; ++i) {
-            const TNode& n = nodes[dfs[i]];
-            float* nd = &out.nodes[16 * (size_t)i];
-            set_child(nd, 0, &nodes[n.left]);
-            set_child(nd, 1, &nodes[n.right]);
-        }
-    }
+    build_wide(root);
+    const uint32_t ninner = nwide;
 
     // statistics
     double rootArea = std::max(nodes[root].box.area(), 1e-30), sah = 0.0;

@@ -4,15 +4,15 @@
 // a binned-SAH binary BVH over the world-space triangle soup, flattened into the
 // layout the HIP traversal kernels read from HBM:
 //
-//   node (64 B) = 4 x 16 B:  {c0.lo.x, c0.hi.x, c0.lo.y, c0.hi.y}
-//                            {c1.lo.x, c1.hi.x, c1.lo.y, c1.hi.y}
-//                            {c0.lo.z, c0.hi.z, c1.lo.z, c1.hi.z}
-//                            {c0.ref,  c1.ref,  c0.cnt,  c1.cnt }   (uint32)
-//     cnt > 0: leaf child, ref = first triangle record, cnt triangles
-//     cnt = 0: inner child, ref = node index (0xffffffff + empty box: no child)
+//   4-wide node (128 B) = 8 x 16 B, structure-of-arrays over the 4 children:
+//       {lo.x[4]} {hi.x[4]} {lo.y[4]} {hi.y[4]} {lo.z[4]} {hi.z[4]} {ref[4]} {cnt[4]}
+//     cnt > 0: leaf child, ref = first triangle record, cnt (<= 4) triangles
+//     cnt = 0: inner child, ref = node index;  ref = 0xffffffff: empty slot
 //   triangle record (48 B) = {v0.xyz, prim id}, {v1.xyz, flags}, {v2.xyz, 0}
 //
-// Both child boxes live in the parent, so one 64-B fetch tests two children.
+// The binary SAH tree is collapsed into 4-wide nodes (open the largest inner child
+// until 4 children): one 128-B fetch tests 4 children, halving the dependent-load
+// chain of a traversal -- the SD trace is latency-bound.
 #pragma once
 #include <cstdint>
 #include <vector>
@@ -28,13 +28,14 @@ struct BvhStats {
 };
 
 struct FlatBvh {
-    std::vector<float> nodes;   // 16 floats per inner node (the last 4 are uint32 bits)
+    std::vector<float> nodes;   // 32 floats per wide node (the last 8 are uint32 bits)
     std::vector<float> tris;    // 12 floats per triangle record
     BvhStats stats;
 };
 
 constexpr uint32_t kBvhMaxDepth = 60;   // traversal stack is 64 entries
 constexpr uint32_t kBvhMaxLeaf = 4;
+constexpr uint32_t kBvhWidth = 4;
 
 // positions: float3[nv]; indices: uint32[3*nt]; flags: uint32[nt] or nullptr
 FlatBvh build_bvh(const float* positions, uint32_t nv, const uint32_t* indices, uint32_t nt,

@@ -79,24 +79,30 @@ extern "C" rsd_status rsd_scene_upload(rsd_device* dev, const rsd_scene_desc* de
     auto* s = new rsd_scene;
     s->dev = dev;
     s->triangle_count = desc->triangle_count;
-    s->node_count = (uint32_t)(bvh.nodes.size() / 16);
+    s->node_count = (uint32_t)(bvh.nodes.size() / 32);
     s->stats = bvh.stats;
-    const size_t nb = bvh.nodes.size() * sizeof(float), tb = std::max<size_t>(bvh.tris.size(), 12) * sizeof(float);
-    hipError_t e = hipMalloc(&s->d_nodes, nb);
-    if (e == hipSuccess) e = hipMalloc(&s->d_tris, tb);
+    // one allocation: wide nodes, then triangle records, then 12 x 16 B of padding so a
+    // traversal step may always fetch 192 B (DESIGN.md "BVH layout in HBM")
+    const size_t nb = bvh.nodes.size() * sizeof(float), tb = bvh.tris.size() * sizeof(float);
+    const size_t total = nb + tb + 12 * 16;
+    s->tri_offset = (uint32_t)(bvh.nodes.size() / 4);
+    hipError_t e = hipMalloc(&s->d_nodes, total);
     if (e == hipSuccess) e = hipMalloc(&s->d_counters, 8 * sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipMalloc(&s->d_qctl, 4 * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMemset(s->d_nodes, 0, total);
     if (e == hipSuccess) e = hipMemcpy(s->d_nodes, bvh.nodes.data(), nb, hipMemcpyHostToDevice);
-    if (e == hipSuccess && !bvh.tris.empty())
-        e = hipMemcpy(s->d_tris, bvh.tris.data(), bvh.tris.size() * sizeof(float), hipMemcpyHostToDevice);
+    if (e == hipSuccess && tb)
+        e = hipMemcpy(reinterpret_cast<char*>(s->d_nodes) + nb, bvh.tris.data(), tb, hipMemcpyHostToDevice);
     if (e != hipSuccess) {
         rsd_status st = rsd::hip_fail(e, "rsd_scene_upload");
         (void)hipFree(s->d_nodes);
-        (void)hipFree(s->d_tris);
         (void)hipFree(s->d_counters);
+        (void)hipFree(s->d_qctl);
         delete s;
         return st;
     }
-    s->device_bytes = nb + tb;
+    s->d_tris = s->d_nodes + s->tri_offset;
+    s->device_bytes = total;
     *out = s;
     return RSD_OK;
 }
@@ -120,8 +126,9 @@ extern "C" void rsd_scene_release(rsd_scene* s) {
     if (!s) return;
     (void)hipSetDevice(s->dev->hip_device);
     (void)hipFree(s->d_nodes);
-    (void)hipFree(s->d_tris);
     (void)hipFree(s->d_counters);
+    (void)hipFree(s->d_qctl);
+    (void)hipFree(s->d_queue);
     delete s;
 }
 

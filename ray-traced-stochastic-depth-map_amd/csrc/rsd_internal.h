@@ -14,13 +14,17 @@ struct rsd_device {
 
 struct rsd_scene {
     rsd_device* dev = nullptr;
-    float4* d_nodes = nullptr;   // 4 x float4 per inner node
-    float4* d_tris = nullptr;    // 3 x float4 per triangle record
+    float4* d_nodes = nullptr;   // one allocation: 8 x float4 per wide node, then
+    float4* d_tris = nullptr;    //   3 x float4 per triangle record (d_tris = d_nodes + tri_offset)
+    uint32_t tri_offset = 0;     // in float4 units
     uint32_t triangle_count = 0;
     uint32_t node_count = 0;
     rsd::BvhStats stats;
     uint64_t device_bytes = 0;
-    unsigned long long* d_counters = nullptr;  // 5 x u64 scratch for instrumented traces
+    unsigned long long* d_counters = nullptr;  // 8 x u64 scratch for instrumented traces
+    uint32_t* d_qctl = nullptr;    // live-ray queue {count, head}
+    uint32_t* d_queue = nullptr;   // live-ray queue (SD texel indices), grow-only
+    size_t queue_cap = 0;
 };
 
 namespace rsd {

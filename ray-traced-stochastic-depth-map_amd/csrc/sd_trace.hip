@@ -19,7 +19,8 @@
 //
 // Kernel shape: one lane per SD texel, one 64-lane wave per 8x8 texel tile (coherent
 // primary rays), node stack in LDS (16 entries / lane) with a private overflow.  Nodes are
-// 64-B {child boxes, refs} records fetched as 4 x 16-B loads; triangles 48-B records.
+// 4-wide 128-B {child boxes, refs} records fetched as 8 x 16-B loads; triangles are 48-B
+// records, a whole leaf (<= 4) fetched before it is tested.
 #include <algorithm>
 #include <vector>
 
@@ -31,7 +32,7 @@ namespace rsd {
 constexpr int kTile = 8;               // 8x8 texels per wave
 constexpr int kBlock = kTile * kTile;  // 64 threads
 constexpr int kLdsStack = 16;
-constexpr int kStackTotal = 64;        // >= kBvhMaxDepth + 2
+constexpr int kStackTotal = 96;        // 4-wide: <= 3 pushes per level, <= 30 levels
 
 struct RayCtx {
     f3 o, d;
@@ -158,70 +159,114 @@ struct TraceStats {
     uint32_t nodes, tris;
 };
 
+__device__ __forceinline__ void cswap(float& ta, uint32_t& ra, float& tb, uint32_t& rb) {
+    const bool s = tb < ta;
+    const float t = ta;
+    const uint32_t r = ra;
+    ta = s ? tb : ta;
+    ra = s ? rb : ra;
+    tb = s ? t : tb;
+    rb = s ? r : rb;
+}
+
+// Work items of the traversal: one 32-bit word.  bit31 = leaf, bits 29-30 = leaf triangle
+// count - 1, bits 0-28 = offset in 16-B units from the BVH base (wide nodes and triangle
+// records share one allocation).  Every step fetches 12 x 16 B at the item's offset -- a
+// 128-B node (+ 64 B ignored) or a whole leaf of <= 4 48-B triangle records -- with the
+// same instructions, so a wave whose lanes mix node steps and leaf steps still pays ONE
+// memory latency per step.  The SD trace is latency-bound (few active rays, long tails).
+constexpr uint32_t kLeafBit = 0x80000000u;
+constexpr uint32_t kOffMask = 0x1fffffffu;
+constexpr uint32_t kNoItem = 0xffffffffu;
+
 // Collects the K smallest keys (t, prim) with tmin <= t <= tmax, key > (lbT, lbP) when
-// useLB, culling applied.  Returns the number of keys found (<= K).
+// useLB, culling applied.  Returns the number of keys found (<= K).  Children are visited
+// nearest-first; the others go to a per-lane LDS stack with their entry distance, and a
+// popped item is dropped without a fetch once the k-th key is nearer than its box.
 template <int K>
-__device__ __forceinline__ int trace_knearest(const float4* __restrict__ nodes, const float4* __restrict__ tris,
-                                              const RayCtx& r, float tmin, float tmax, uint32_t cull, bool useLB,
-                                              float lbT, uint32_t lbP, KList<K>& kl, uint32_t* __restrict__ lds,
-                                              TraceStats& st) {
+__device__ __forceinline__ int trace_knearest(const float4* __restrict__ bvh, uint32_t triOff, const RayCtx& r,
+                                              float tmin, float tmax, uint32_t cull, bool useLB, float lbT,
+                                              uint32_t lbP, KList<K>& kl, uint32_t* __restrict__ ldsItem,
+                                              float* __restrict__ ldsT, TraceStats& st) {
     kl.clear();
-    uint32_t spill[kStackTotal - kLdsStack];
+    uint32_t spillItem[kStackTotal - kLdsStack];
+    float spillT[kStackTotal - kLdsStack];
     int sp = 0;
     int found = 0;
-    uint32_t node = 0;
+    uint32_t item = 0;  // root node
     const float tlo = useLB ? fmaxf(tmin, lbT) : tmin;
     while (true) {
-        const float4 n0 = nodes[4 * node + 0];
-        const float4 n1 = nodes[4 * node + 1];
-        const float4 n2 = nodes[4 * node + 2];
-        const uint4 n3 = reinterpret_cast<const uint4*>(nodes)[4 * node + 3];
-        st.nodes++;
-        const float thi = fminf(tmax, kl.t[K - 1]);
-        float tn0, tn1;
-        bool h0 = box_hit(r, n0.x, n0.y, n0.z, n0.w, n2.x, n2.y, tlo, thi, tn0);
-        bool h1 = box_hit(r, n1.x, n1.y, n1.z, n1.w, n2.z, n2.w, tlo, thi, tn1);
+        const float4* p = bvh + (item & kOffMask);
+        float4 q[12];
 #pragma unroll
-        for (int c = 0; c < 2; ++c) {
-            const bool hc = c == 0 ? h0 : h1;
-            const uint32_t cnt = c == 0 ? n3.z : n3.w;
-            if (hc && cnt > 0u) {
-                const uint32_t first = c == 0 ? n3.x : n3.y;
-                for (uint32_t i = first; i < first + cnt; ++i) {
-                    const float4 a = tris[3 * i + 0];
-                    const float4 b = tris[3 * i + 1];
-                    const float4 cc = tris[3 * i + 2];
-                    st.tris++;
-                    float t, bu, bv, det;
-                    if (!intersect_tri(r, a, b, cc, t, bu, bv, det)) continue;
-                    if (!(t >= tmin && t <= tmax)) continue;
-                    const uint32_t prim = __float_as_uint(a.w);
-                    if (culled(det, __float_as_uint(b.w), cull)) continue;
-                    if (useLB && !key_less(lbT, lbP, t, prim)) continue;
-                    if (!key_less(t, prim, kl.t[K - 1], kl.p[K - 1])) continue;
-                    kl.insert(t, prim, i);
-                    found = found < K ? found + 1 : K;
-                }
-                if (c == 0) h0 = false; else h1 = false;
+        for (int j = 0; j < 12; ++j) q[j] = p[j];
+        uint32_t next = kNoItem;
+        if (item & kLeafBit) {
+            const uint32_t cnt = ((item >> 29) & 3u) + 1u;
+            const uint32_t first = ((item & kOffMask) - triOff) / 3u;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                if ((uint32_t)j >= cnt) continue;
+                st.tris++;
+                float t, bu, bv, det;
+                if (!intersect_tri(r, q[3 * j], q[3 * j + 1], q[3 * j + 2], t, bu, bv, det)) continue;
+                if (!(t >= tmin && t <= tmax)) continue;
+                const uint32_t prim = __float_as_uint(q[3 * j].w);
+                if (culled(det, __float_as_uint(q[3 * j + 1].w), cull)) continue;
+                if (useLB && !key_less(lbT, lbP, t, prim)) continue;
+                if (!key_less(t, prim, kl.t[K - 1], kl.p[K - 1])) continue;
+                kl.insert(t, prim, first + (uint32_t)j);
+                found = found < K ? found + 1 : K;
             }
-        }
-        if (h0 && h1) {
-            const bool nearIs0 = tn0 <= tn1;
-            const uint32_t nearN = nearIs0 ? n3.x : n3.y;
-            const uint32_t farN = nearIs0 ? n3.y : n3.x;
-            if (sp < kLdsStack) lds[sp * kBlock] = farN;
-            else spill[sp - kLdsStack] = farN;
-            ++sp;
-            node = nearN;
-        } else if (h0) {
-            node = n3.x;
-        } else if (h1) {
-            node = n3.y;
         } else {
-            if (sp == 0) break;
-            --sp;
-            node = sp < kLdsStack ? lds[sp * kBlock] : spill[sp - kLdsStack];
+            st.nodes++;
+            const float thi = fminf(tmax, kl.t[K - 1]);
+            const uint4 rf = make_uint4(__float_as_uint(q[6].x), __float_as_uint(q[6].y), __float_as_uint(q[6].z),
+                                        __float_as_uint(q[6].w));
+            const uint4 ct = make_uint4(__float_as_uint(q[7].x), __float_as_uint(q[7].y), __float_as_uint(q[7].z),
+                                        __float_as_uint(q[7].w));
+            float k0, k1, k2, k3;
+            bool h0 = rf.x != kNoItem && box_hit(r, q[0].x, q[1].x, q[2].x, q[3].x, q[4].x, q[5].x, tlo, thi, k0);
+            bool h1 = rf.y != kNoItem && box_hit(r, q[0].y, q[1].y, q[2].y, q[3].y, q[4].y, q[5].y, tlo, thi, k1);
+            bool h2 = rf.z != kNoItem && box_hit(r, q[0].z, q[1].z, q[2].z, q[3].z, q[4].z, q[5].z, tlo, thi, k2);
+            bool h3 = rf.w != kNoItem && box_hit(r, q[0].w, q[1].w, q[2].w, q[3].w, q[4].w, q[5].w, tlo, thi, k3);
+            auto mkitem = [&](uint32_t ref, uint32_t cnt) {
+                return cnt ? (kLeafBit | ((cnt - 1u) << 29) | (triOff + 3u * ref)) : 8u * ref;
+            };
+            uint32_t c0 = h0 ? mkitem(rf.x, ct.x) : kNoItem, c1 = h1 ? mkitem(rf.y, ct.y) : kNoItem;
+            uint32_t c2 = h2 ? mkitem(rf.z, ct.z) : kNoItem, c3 = h3 ? mkitem(rf.w, ct.w) : kNoItem;
+            k0 = h0 ? k0 : INFINITY;
+            k1 = h1 ? k1 : INFINITY;
+            k2 = h2 ? k2 : INFINITY;
+            k3 = h3 ? k3 : INFINITY;
+            cswap(k0, c0, k1, c1);
+            cswap(k2, c2, k3, c3);
+            cswap(k0, c0, k2, c2);
+            cswap(k1, c1, k3, c3);
+            cswap(k1, c1, k2, c2);
+#define RSD_PUSH(c, k)                                                 \
+    if ((c) != kNoItem) {                                              \
+        if (sp < kLdsStack) { ldsItem[sp * kBlock] = (c); ldsT[sp * kBlock] = (k); } \
+        else { spillItem[sp - kLdsStack] = (c); spillT[sp - kLdsStack] = (k); }      \
+        ++sp;                                                          \
+    }
+            RSD_PUSH(c3, k3)
+            RSD_PUSH(c2, k2)
+            RSD_PUSH(c1, k1)
+#undef RSD_PUSH
+            next = c0;
         }
+        if (next == kNoItem) {
+            const float thi = fminf(tmax, kl.t[K - 1]);
+            while (sp > 0) {
+                --sp;
+                const uint32_t it = sp < kLdsStack ? ldsItem[sp * kBlock] : spillItem[sp - kLdsStack];
+                const float tt = sp < kLdsStack ? ldsT[sp * kBlock] : spillT[sp - kLdsStack];
+                if (tt <= thi) { next = it; break; }
+            }
+            if (next == kNoItem) break;
+        }
+        item = next;
     }
     return found;
 }
@@ -230,8 +275,9 @@ __device__ __forceinline__ int trace_knearest(const float4* __restrict__ nodes, 
 // SD map kernel
 // ------------------------------------------------------------------------------------
 struct SDArgs {
-    const float4* nodes;
-    const float4* tris;
+    const float4* nodes;  // BVH base (wide nodes, then triangle records)
+    const float4* tris;   // = nodes + triOff
+    uint32_t triOff;
     rsd_camera cam;
     const float* linearZ;
     int zW, zH;
@@ -245,6 +291,7 @@ struct SDArgs {
     const int32_t* lutIdx;  // coverage mask: stratified indices [N+1]
     const uint32_t* lut;    // coverage mask: look-up table [2^N]
     unsigned long long* counters;
+    int bandIndex, bandCount;  // screen-band sharding: 8-row tile rows t with t % count == index
 };
 
 __device__ __forceinline__ f3 cam_dir(const rsd_camera& c, float px, float py) {
@@ -254,136 +301,198 @@ __device__ __forceinline__ f3 cam_dir(const rsd_camera& c, float px, float py) {
               ndcx * c.U[2] + ndcy * c.V[2] + c.W[2]);
 }
 
-template <int K, int N>
-__global__ void __launch_bounds__(kBlock) sd_trace_kernel(SDArgs a) {
-    __shared__ uint32_t sstack[kLdsStack * kBlock];
-    const int lane = threadIdx.x;
-    const int x = blockIdx.x * kTile + (lane & (kTile - 1));
-    const int y = blockIdx.y * kTile + (lane / kTile);
-    const bool inside = x < a.sdW && y < a.sdH;
+// initRayDesc, Common.slangh:65-92 (with Camera.slang:46-90).  Returns true if the ray
+// interval is non-empty (TMin <= TMax): only those rays reach TraceRay.
+__device__ __forceinline__ bool sd_ray(const SDArgs& a, int x, int y, f3& d, float& TMin, float& TMax, float& cosT) {
     const rsd_camera& c = a.cam;
-    const float DEFAULT = a.normalize ? 1.0f : 3.40282347e+37f;  // Common.slangh:16
+    const int dimx = a.sdW - 2 * a.guard, dimy = a.sdH - 2 * a.guard;
+    const int sx = x - a.guard, sy = y - a.guard;
+    const f3 wn = normalize(mk(c.W[0], c.W[1], c.W[2]));
+    const f3 dc = normalize(cam_dir(c, ((float)sx + 0.5f) / (float)dimx + -c.jitterX,
+                                    ((float)sy + 0.5f) / (float)dimy + c.jitterY));
+    const float invCos = 1.0f / dot(wn, dc);
+    TMax = c.farZ * invCos;  // computeRayPinhole tMax (pixel centre)
+    float jx, jy;
+    sd_jitter((uint32_t)x, (uint32_t)y, a.jitter != 0u, jx, jy);
+    d = normalize(cam_dir(c, ((float)sx + jx) / (float)dimx, ((float)sy + jy) / (float)dimy));
+    const float eps = 0.1f * c.nearZ;
+    float depth = 0.0f;
+    if (sx >= 0 && sy >= 0 && sx < dimx && sy < dimy)
+        depth = tex_bilinear(a.linearZ, a.zW, a.zH, ((float)sx + 0.5f) / (float)dimx, ((float)sy + 0.5f) / (float)dimy,
+                             true);
+    cosT = dot(wn, d);
+    TMin = depth / cosT + eps;
+    if (a.rayInterval) {
+        const size_t o = (size_t)y * a.sdW + x;
+        const uint32_t iMin = a.rayMin ? a.rayMin[o] : 0u;
+        if (iMin != 0u) TMin = hmax(asfloat(iMin), TMin);
+        const uint32_t iMax = a.rayMax ? a.rayMax[o] : 0u;
+        if (iMax != 0u) TMax = hmin(asfloat(iMax), TMax);
+    }
+    return TMin <= TMax;
+}
 
-    float depths[N];
+// store, StochasticDepthMapRT.rt.slang:90-104 (Texture2DArray layout [layer][y][x][ch])
+template <int N>
+__device__ __forceinline__ void sd_store(const SDArgs& a, int x, int y, const float (&depths)[N]) {
+    const size_t plane = (size_t)a.sdW * a.sdH;
+    const size_t o = (size_t)y * a.sdW + x;
+    if constexpr (N == 1) {
+        a.sd[o] = depths[0];
+    } else if constexpr (N == 2) {
+        reinterpret_cast<float2*>(a.sd)[o] = make_float2(depths[0], depths[1]);
+    } else {
 #pragma unroll
-    for (int i = 0; i < N; ++i) depths[i] = DEFAULT;
-    TraceStats st{0u, 0u};
-    uint32_t active = 0, hitsDelivered = 0;
+        for (int l = 0; l < N / 4; ++l)
+            reinterpret_cast<float4*>(a.sd)[l * plane + o] =
+                make_float4(depths[4 * l], depths[4 * l + 1], depths[4 * l + 2], depths[4 * l + 3]);
+    }
+}
 
-    if (inside) {
-        // ---- initRayDesc, Common.slangh:65-92
-        const int dimx = a.sdW - 2 * a.guard, dimy = a.sdH - 2 * a.guard;
-        const int sx = x - a.guard, sy = y - a.guard;
-        const f3 wn = normalize(mk(c.W[0], c.W[1], c.W[2]));
-        const f3 dc = normalize(cam_dir(c, ((float)sx + 0.5f) / (float)dimx + -c.jitterX,
-                                        ((float)sy + 0.5f) / (float)dimy + c.jitterY));
-        const float invCos = 1.0f / dot(wn, dc);
-        float TMax = c.farZ * invCos;
-        float jx, jy;
-        sd_jitter((uint32_t)x, (uint32_t)y, a.jitter != 0u, jx, jy);
-        const f3 d = normalize(cam_dir(c, ((float)sx + jx) / (float)dimx, ((float)sy + jy) / (float)dimy));
-        const float eps = 0.1f * c.nearZ;
-        float depth = 0.0f;
-        if (sx >= 0 && sy >= 0 && sx < dimx && sy < dimy)
-            depth = tex_bilinear(a.linearZ, a.zW, a.zH, ((float)sx + 0.5f) / (float)dimx,
-                                 ((float)sy + 0.5f) / (float)dimy, true);
-        const float cosT = dot(wn, d);
-        float TMin = depth / cosT + eps;
-        if (a.rayInterval) {
-            const size_t o = (size_t)y * a.sdW + x;
-            const uint32_t iMin = a.rayMin ? a.rayMin[o] : 0u;
-            if (iMin != 0u) TMin = hmax(asfloat(iMin), TMin);
-            const uint32_t iMax = a.rayMax ? a.rayMax[o] : 0u;
-            if (iMax != 0u) TMax = hmin(asfloat(iMax), TMax);
-        }
-
-        if (TMin <= TMax) {
-            active = 1;
-            RayCtx r;
-            ray_setup(r, mk(c.posW[0], c.posW[1], c.posW[2]), d);
-            KList<K> kl;
-            uint32_t count = 0;
-            bool commit = false, useLB = false;
-            float lbT = 0.0f;
-            uint32_t lbP = 0u;
-            while (!commit) {
-                const int found = trace_knearest<K>(a.nodes, a.tris, r, TMin, TMax, a.cull, useLB, lbT, lbP, kl,
-                                                    &sstack[lane], st);
-                // ---- anyHit -> algorithm (Common.slangh:102-254), ascending (t, prim)
+// TraceRay + anyHit -> algorithm (Common.slangh:102-254) over the canonical hit stream.
+template <int K, int N>
+__device__ __forceinline__ void sd_resolve(const SDArgs& a, f3 d, float TMin, float TMax, float cosT, float (&depths)[N],
+                                           uint32_t* lds, float* ldsT, TraceStats& st, uint32_t& hitsDelivered) {
+    const rsd_camera& c = a.cam;
+    RayCtx r;
+    ray_setup(r, mk(c.posW[0], c.posW[1], c.posW[2]), d);
+    KList<K> kl;
+    uint32_t count = 0;
+    bool commit = false, useLB = false;
+    float lbT = 0.0f;
+    uint32_t lbP = 0u;
+    while (!commit) {
+        const int found = trace_knearest<K>(a.nodes, a.triOff, r, TMin, TMax, a.cull, useLB, lbT, lbP, kl, lds, ldsT,
+                                            st);
 #pragma unroll
-                for (int j = 0; j < K; ++j) {
-                    if (commit || j >= found) continue;
-                    // barycentrics of the j-th hit: re-run the identical test on its record
-                    const uint32_t ti = kl.l[j];
-                    float t, bu, bv, det;
-                    intersect_tri(r, a.tris[3 * ti], a.tris[3 * ti + 1], a.tris[3 * ti + 2], t, bu, bv, det);
-                    hitsDelivered++;
-                    const float rng = sd_hash(bu, bv);
-                    float z = t * cosT;  // RayToViewDepth
-                    if (a.normalize) z = saturate((z - c.nearZ) / (c.farZ - c.nearZ));
-                    if (a.impl == 1u) {  // CoverageMask, Common.slangh:117-131, 189-209
-                        const int R = (int)floorf(a.alpha * (float)N + rng);
-                        uint32_t mask = 0u;
-                        if (R >= N) mask = 0xffffu;
-                        else if (R != 0) {
-                            const float rng2 = sd_hash(rng, z);  // hash3D(float3(bary, t))
-                            const float lo = (float)a.lutIdx[R], hi = (float)a.lutIdx[R + 1];
-                            mask = a.lut[(int)(lo + rng2 * (hi - lo))];
-                        }
-                        float maxT = 0.0f;
-#pragma unroll
-                        for (int i = 0; i < N; ++i) {
-                            if ((mask & (1u << i)) && z < depths[i]) depths[i] = z;
-                            maxT = hmax(maxT, depths[i]);
-                        }
-                        commit = !(z < maxT);
-                    } else if (a.impl == 3u) {  // KBuffer, Common.slangh:132-135, 211-232
-                        if (z >= depths[N - 1]) {
-                            commit = true;
-                        } else {
-                            count++;
-                            const float rayT = z;
-#pragma unroll
-                            for (int i = 0; i < N; ++i)
-                                if (z < depths[i]) { const float tmp = depths[i]; depths[i] = z; z = tmp; }
-                            commit = (depths[N - 1] == rayT) || count >= a.maxCount;
-                        }
-                    } else {  // Default reservoir, Common.slangh:136-153, 234-247
-                        uint32_t slot = count++;
-                        if (count > (uint32_t)N) slot = (uint32_t)(rng * (float)count);
-#pragma unroll
-                        for (int i = 0; i < N; ++i)
-                            if ((uint32_t)i == slot && !(depths[i] <= z)) depths[i] = z;
-                        commit = count >= a.maxCount;
-                    }
+        for (int j = 0; j < K; ++j) {
+            if (commit || j >= found) continue;
+            // barycentrics of the j-th hit: re-run the identical test on its record
+            const uint32_t ti = kl.l[j];
+            float t, bu, bv, det;
+            intersect_tri(r, a.tris[3 * ti], a.tris[3 * ti + 1], a.tris[3 * ti + 2], t, bu, bv, det);
+            hitsDelivered++;
+            const float rng = sd_hash(bu, bv);
+            float z = t * cosT;  // RayToViewDepth
+            if (a.normalize) z = saturate((z - c.nearZ) / (c.farZ - c.nearZ));
+            if (a.impl == 1u) {  // CoverageMask, Common.slangh:117-131, 189-209
+                const int R = (int)floorf(a.alpha * (float)N + rng);
+                uint32_t mask = 0u;
+                if (R >= N) mask = 0xffffu;
+                else if (R != 0) {
+                    const float rng2 = sd_hash(rng, z);  // hash3D(float3(bary, t))
+                    const float lo = (float)a.lutIdx[R], hi = (float)a.lutIdx[R + 1];
+                    mask = a.lut[(int)(lo + rng2 * (hi - lo))];
                 }
-                if (found < K) break;  // stream exhausted
-                useLB = true;
-                lbT = kl.t[K - 1];
-                lbP = kl.p[K - 1];
+                float maxT = 0.0f;
+#pragma unroll
+                for (int i = 0; i < N; ++i) {
+                    if ((mask & (1u << i)) && z < depths[i]) depths[i] = z;
+                    maxT = hmax(maxT, depths[i]);
+                }
+                commit = !(z < maxT);
+            } else if (a.impl == 3u) {  // KBuffer, Common.slangh:132-135, 211-232
+                if (z >= depths[N - 1]) {
+                    commit = true;
+                } else {
+                    count++;
+                    const float rayT = z;
+#pragma unroll
+                    for (int i = 0; i < N; ++i)
+                        if (z < depths[i]) { const float tmp = depths[i]; depths[i] = z; z = tmp; }
+                    commit = (depths[N - 1] == rayT) || count >= a.maxCount;
+                }
+            } else {  // Default reservoir, Common.slangh:136-153, 234-247
+                uint32_t slot = count++;
+                if (count > (uint32_t)N) slot = (uint32_t)(rng * (float)count);
+#pragma unroll
+                for (int i = 0; i < N; ++i)
+                    if ((uint32_t)i == slot && !(depths[i] <= z)) depths[i] = z;
+                commit = count >= a.maxCount;
             }
         }
+        if (found < K) break;  // stream exhausted
+        useLB = true;
+        lbT = kl.t[K - 1];
+        lbP = kl.p[K - 1];
+    }
+}
 
-        // ---- store, StochasticDepthMapRT.rt.slang:90-104 (Texture2DArray layout)
-        const size_t plane = (size_t)a.sdW * a.sdH;
-        const size_t o = (size_t)y * a.sdW + x;
-        if constexpr (N == 1) {
-            a.sd[o] = depths[0];
-        } else if constexpr (N == 2) {
-            reinterpret_cast<float2*>(a.sd)[o] = make_float2(depths[0], depths[1]);
-        } else {
+// Phase 1 (rayGen up to TraceRay): one lane per SD texel of the band.  Rays whose interval
+// is empty keep DEFAULT_DEPTH and are written here; the others are appended to a compact
+// queue (one atomic per wave) so that phase 2 runs full waves of live rays only.
+template <int N>
+__global__ void __launch_bounds__(kBlock) sd_setup_kernel(SDArgs a, uint32_t* __restrict__ queue,
+                                                          uint32_t* __restrict__ qctl) {
+    const int lane = threadIdx.x;
+    const int x = blockIdx.x * kTile + (lane & (kTile - 1));
+    const int y = ((int)blockIdx.y * a.bandCount + a.bandIndex) * kTile + (lane / kTile);
+    const bool inside = x < a.sdW && y < a.sdH;
+    bool live = false;
+    if (inside) {
+        f3 d;
+        float TMin, TMax, cosT;
+        live = sd_ray(a, x, y, d, TMin, TMax, cosT);
+        if (!live) {
+            float depths[N];
+            const float DEFAULT = a.normalize ? 1.0f : 3.40282347e+37f;  // Common.slangh:16
 #pragma unroll
-            for (int l = 0; l < N / 4; ++l)
-                reinterpret_cast<float4*>(a.sd)[l * plane + o] =
-                    make_float4(depths[4 * l], depths[4 * l + 1], depths[4 * l + 2], depths[4 * l + 3]);
+            for (int i = 0; i < N; ++i) depths[i] = DEFAULT;
+            sd_store<N>(a, x, y, depths);
         }
     }
+    const unsigned long long m = __ballot(live);
+    const uint32_t n = (uint32_t)__popcll(m);
+    uint32_t base = 0;
+    if (lane == 0 && n) base = atomicAdd(&qctl[0], n);
+    base = __shfl(base, 0);
+    if (live) queue[base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = (uint32_t)y * (uint32_t)a.sdW + x;
+    const unsigned long long in = __ballot(inside);
+    if (a.counters && lane == 0) atomicAdd(&a.counters[0], (unsigned long long)__popcll(in));
+}
+
+// Phase 2: persistent waves pull 64 live rays at a time from the queue until it drains
+// (every wave reaches the exit: the head only grows and the count is fixed).  The first
+// chunk of each wave is static (blockIdx), later ones come from one atomic head that
+// starts after the static range -- a wave with no static chunk exits without an atomic
+// (one head word serialises ~90 dequeues/us, MI355X_MICROARCH.md "dequeue").
+template <int K, int N>
+__global__ void __launch_bounds__(kBlock) sd_trace_queue_kernel(SDArgs a, const uint32_t* __restrict__ queue,
+                                                                uint32_t* __restrict__ qctl) {
+    __shared__ uint32_t sstack[kLdsStack * kBlock];
+    __shared__ float sstackT[kLdsStack * kBlock];
+    const int lane = threadIdx.x;
+    const uint32_t count = __hip_atomic_load(&qctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    TraceStats st{0u, 0u};
+    uint32_t active = 0, hitsDelivered = 0, maxNodes = 0;
+    uint32_t base = blockIdx.x * (uint32_t)kBlock;
+    while (base < count) {
+        const uint32_t qi = base + (uint32_t)lane;
+        if (qi < count) {
+            const uint32_t idx = queue[qi];
+            const int x = (int)(idx % (uint32_t)a.sdW), y = (int)(idx / (uint32_t)a.sdW);
+            f3 d;
+            float TMin, TMax, cosT;
+            sd_ray(a, x, y, d, TMin, TMax, cosT);
+            float depths[N];
+            const float DEFAULT = a.normalize ? 1.0f : 3.40282347e+37f;
+#pragma unroll
+            for (int i = 0; i < N; ++i) depths[i] = DEFAULT;
+            const uint32_t n0 = st.nodes;
+            sd_resolve<K, N>(a, d, TMin, TMax, cosT, depths, &sstack[lane], &sstackT[lane], st, hitsDelivered);
+            maxNodes = max(maxNodes, st.nodes - n0);
+            active++;
+            sd_store<N>(a, x, y, depths);
+        }
+        if (lane == 0) base = gridDim.x * (uint32_t)kBlock + atomicAdd(&qctl[1], (uint32_t)kBlock);
+        base = __shfl(base, 0);
+    }
     if (a.counters) {
-        atomicAdd(&a.counters[0], (unsigned long long)(inside ? 1u : 0u));
         atomicAdd(&a.counters[1], (unsigned long long)active);
         atomicAdd(&a.counters[2], (unsigned long long)st.nodes);
         atomicAdd(&a.counters[3], (unsigned long long)st.tris);
         atomicAdd(&a.counters[4], (unsigned long long)hitsDelivered);
+        atomicMax(&a.counters[5], (unsigned long long)maxNodes);
     }
 }
 
@@ -395,6 +504,7 @@ __global__ void __launch_bounds__(kBlock) sd_trace_kernel(SDArgs a) {
 struct GBArgs {
     const float4* nodes;
     const float4* tris;
+    uint32_t triOff;
     rsd_camera cam;
     int W, H;
     uint32_t cull;
@@ -404,6 +514,7 @@ struct GBArgs {
 
 __global__ void __launch_bounds__(kBlock) gbuffer_kernel(GBArgs a) {
     __shared__ uint32_t sstack[kLdsStack * kBlock];
+    __shared__ float sstackT[kLdsStack * kBlock];
     const int lane = threadIdx.x;
     const int x = blockIdx.x * kTile + (lane & (kTile - 1));
     const int y = blockIdx.y * kTile + (lane / kTile);
@@ -418,8 +529,8 @@ __global__ void __launch_bounds__(kBlock) gbuffer_kernel(GBArgs a) {
     ray_setup(r, mk(c.posW[0], c.posW[1], c.posW[2]), d);
     KList<1> kl;
     TraceStats st{0u, 0u};
-    const int found = trace_knearest<1>(a.nodes, a.tris, r, c.nearZ * invCos, c.farZ * invCos, a.cull, false, 0.0f,
-                                        0u, kl, &sstack[lane], st);
+    const int found = trace_knearest<1>(a.nodes, a.triOff, r, c.nearZ * invCos, c.farZ * invCos, a.cull, false,
+                                        0.0f, 0u, kl, &sstack[lane], &sstackT[lane], st);
     const size_t o = (size_t)y * a.W + x;
     if (!found) {
         a.z[o] = c.farZ;
@@ -441,17 +552,27 @@ __global__ void __launch_bounds__(kBlock) gbuffer_kernel(GBArgs a) {
 // ------------------------------------------------------------------------------------
 // launchers
 // ------------------------------------------------------------------------------------
+template <int K, int N>
+static hipError_t launch_sd_kn(const SDArgs& a, dim3 grid, uint32_t persistentBlocks, uint32_t* queue, uint32_t* qctl,
+                               hipStream_t s) {
+    hipLaunchKernelGGL((sd_setup_kernel<N>), grid, dim3(kBlock), 0, s, a, queue, qctl);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((sd_trace_queue_kernel<K, N>), dim3(persistentBlocks), dim3(kBlock), 0, s, a, queue, qctl);
+    return hipGetLastError();
+}
+
 template <int K>
-static hipError_t launch_sd_k(const SDArgs& a, uint32_t N, dim3 grid, hipStream_t s) {
+static hipError_t launch_sd_k(const SDArgs& a, uint32_t N, dim3 grid, uint32_t pb, uint32_t* q, uint32_t* qc,
+                              hipStream_t s) {
     switch (N) {
-        case 1: hipLaunchKernelGGL((sd_trace_kernel<K, 1>), grid, dim3(kBlock), 0, s, a); break;
-        case 2: hipLaunchKernelGGL((sd_trace_kernel<K, 2>), grid, dim3(kBlock), 0, s, a); break;
-        case 4: hipLaunchKernelGGL((sd_trace_kernel<K, 4>), grid, dim3(kBlock), 0, s, a); break;
-        case 8: hipLaunchKernelGGL((sd_trace_kernel<K, 8>), grid, dim3(kBlock), 0, s, a); break;
-        case 16: hipLaunchKernelGGL((sd_trace_kernel<K, 16>), grid, dim3(kBlock), 0, s, a); break;
+        case 1: return launch_sd_kn<K, 1>(a, grid, pb, q, qc, s);
+        case 2: return launch_sd_kn<K, 2>(a, grid, pb, q, qc, s);
+        case 4: return launch_sd_kn<K, 4>(a, grid, pb, q, qc, s);
+        case 8: return launch_sd_kn<K, 8>(a, grid, pb, q, qc, s);
+        case 16: return launch_sd_kn<K, 16>(a, grid, pb, q, qc, s);
         default: return hipErrorInvalidValue;
     }
-    return hipGetLastError();
 }
 
 }  // namespace rsd
@@ -500,10 +621,15 @@ rsd_status ensure_lut(uint32_t N, const int32_t** idx, const uint32_t** lut) {
 }
 }  // namespace
 
-extern "C" rsd_status rsd_sd_trace(rsd_scene* scene, const rsd_camera* cam, const rsd_sd_params* p,
-                                   const float* d_linear_z, uint32_t z_w, uint32_t z_h, const uint32_t* d_ray_min,
-                                   const uint32_t* d_ray_max, float* d_sd_out, uint32_t sd_w, uint32_t sd_h,
-                                   rsd_counters* counters, rsd_stream stream) {
+extern "C" rsd_status rsd_sd_trace_band(rsd_scene* scene, const rsd_camera* cam, const rsd_sd_params* p,
+                                        const float* d_linear_z, uint32_t z_w, uint32_t z_h,
+                                        const uint32_t* d_ray_min, const uint32_t* d_ray_max, float* d_sd_out,
+                                        uint32_t sd_w, uint32_t sd_h, uint32_t band_index, uint32_t band_count,
+                                        rsd_counters* counters, rsd_stream stream) {
+    if (band_count == 0 || band_index >= band_count) {
+        set_error("rsd_sd_trace_band: band_index must be < band_count");
+        return RSD_ERR_INVALID_ARG;
+    }
     if (!scene || !cam || !p || !d_linear_z || !d_sd_out || sd_w == 0 || sd_h == 0 || z_w == 0 || z_h == 0) {
         set_error("rsd_sd_trace: null argument or empty extent");
         return RSD_ERR_INVALID_ARG;
@@ -532,12 +658,13 @@ extern "C" rsd_status rsd_sd_trace(rsd_scene* scene, const rsd_camera* cam, cons
         std::vector<float> h((size_t)sd_w * sd_h * (N < 4 ? N : 4) * ((N + 3) / 4), def);
         RSD_HIP(hipMemcpyAsync(d_sd_out, h.data(), h.size() * sizeof(float), hipMemcpyHostToDevice, (hipStream_t)stream));
         RSD_HIP(hipStreamSynchronize((hipStream_t)stream));
-        if (counters) *counters = rsd_counters{(uint64_t)sd_w * sd_h, 0, 0, 0, 0};
+        if (counters) *counters = rsd_counters{(uint64_t)sd_w * sd_h, 0, 0, 0, 0, 0};
         return RSD_OK;
     }
     SDArgs a;
     a.nodes = scene->d_nodes;
     a.tris = scene->d_tris;
+    a.triOff = scene->tri_offset;
     a.cam = *cam;
     a.linearZ = d_linear_z;
     a.zW = (int)z_w;
@@ -558,25 +685,41 @@ extern "C" rsd_status rsd_sd_trace(rsd_scene* scene, const rsd_camera* cam, cons
     a.lutIdx = nullptr;
     a.lut = nullptr;
     a.counters = nullptr;
+    a.bandIndex = (int)band_index;
+    a.bandCount = (int)band_count;
     if (p->implementation == RSD_SD_COVERAGE_MASK) {
         rsd_status s = ensure_lut(N, &a.lutIdx, &a.lut);
         if (s != RSD_OK) return s;
     }
     hipStream_t s = (hipStream_t)stream;
     if (counters) {
-        RSD_HIP(hipMemsetAsync(scene->d_counters, 0, 5 * sizeof(unsigned long long), s));
+        RSD_HIP(hipMemsetAsync(scene->d_counters, 0, 6 * sizeof(unsigned long long), s));
         a.counters = scene->d_counters;
     }
-    dim3 grid((sd_w + kTile - 1) / kTile, (sd_h + kTile - 1) / kTile);
+    const uint32_t tiles = (sd_h + kTile - 1) / kTile;
+    const uint32_t bandTiles = tiles > band_index ? (tiles - band_index + band_count - 1) / band_count : 0u;
+    dim3 grid((sd_w + kTile - 1) / kTile, bandTiles);
     // k = the MAX_COUNT nearest keys decide Default and KBuffer; coverage mask streams chunks
     const uint32_t need = p->implementation == RSD_SD_COVERAGE_MASK ? 8u : p->max_count;
-    hipError_t e;
-    if (need <= 4) e = launch_sd_k<4>(a, N, grid, s);
-    else if (need <= 8) e = launch_sd_k<8>(a, N, grid, s);
-    else e = launch_sd_k<16>(a, N, grid, s);
+    // live-ray queue workspace (grow-only; the first call of a larger map allocates)
+    const size_t need_q = (size_t)sd_w * sd_h;
+    if (scene->queue_cap < need_q) {
+        RSD_HIP(hipStreamSynchronize(s));
+        (void)hipFree(scene->d_queue);
+        scene->d_queue = nullptr;
+        RSD_HIP(hipMalloc(&scene->d_queue, need_q * sizeof(uint32_t)));
+        scene->queue_cap = need_q;
+    }
+    RSD_HIP(hipMemsetAsync(scene->d_qctl, 0, 2 * sizeof(uint32_t), s));
+    const uint32_t pb = (uint32_t)std::max(1, scene->dev->cu_count) * 8u;
+    hipError_t e = hipSuccess;
+    if (bandTiles == 0) {}
+    else if (need <= 4) e = launch_sd_k<4>(a, N, grid, pb, scene->d_queue, scene->d_qctl, s);
+    else if (need <= 8) e = launch_sd_k<8>(a, N, grid, pb, scene->d_queue, scene->d_qctl, s);
+    else e = launch_sd_k<16>(a, N, grid, pb, scene->d_queue, scene->d_qctl, s);
     if (e != hipSuccess) return hip_fail(e, "sd_trace_kernel launch");
     if (counters) {
-        unsigned long long h[5];
+        unsigned long long h[6];
         RSD_HIP(hipMemcpyAsync(h, scene->d_counters, sizeof(h), hipMemcpyDeviceToHost, s));
         RSD_HIP(hipStreamSynchronize(s));
         counters->rays_dispatched = h[0];
@@ -584,8 +727,17 @@ extern "C" rsd_status rsd_sd_trace(rsd_scene* scene, const rsd_camera* cam, cons
         counters->nodes_visited = h[2];
         counters->tris_tested = h[3];
         counters->hits_delivered = h[4];
+        counters->max_nodes_per_ray = h[5];
     }
     return RSD_OK;
+}
+
+extern "C" rsd_status rsd_sd_trace(rsd_scene* scene, const rsd_camera* cam, const rsd_sd_params* p,
+                                   const float* d_linear_z, uint32_t z_w, uint32_t z_h, const uint32_t* d_ray_min,
+                                   const uint32_t* d_ray_max, float* d_sd_out, uint32_t sd_w, uint32_t sd_h,
+                                   rsd_counters* counters, rsd_stream stream) {
+    return rsd_sd_trace_band(scene, cam, p, d_linear_z, z_w, z_h, d_ray_min, d_ray_max, d_sd_out, sd_w, sd_h, 0, 1,
+                             counters, stream);
 }
 
 extern "C" rsd_status rsd_gbuffer(rsd_scene* scene, const rsd_camera* cam, uint32_t width, uint32_t height,
@@ -606,7 +758,7 @@ extern "C" rsd_status rsd_gbuffer(rsd_scene* scene, const rsd_camera* cam, uint3
         RSD_HIP(hipStreamSynchronize(s));
         return RSD_OK;
     }
-    GBArgs a{scene->d_nodes, scene->d_tris, *cam, (int)width, (int)height, cull_mode, d_linear_z, d_normals};
+    GBArgs a{scene->d_nodes, scene->d_tris, scene->tri_offset, *cam, (int)width, (int)height, cull_mode, d_linear_z, d_normals};
     dim3 grid((width + kTile - 1) / kTile, (height + kTile - 1) / kTile);
     hipLaunchKernelGGL(gbuffer_kernel, grid, dim3(kBlock), 0, s, a);
     hipError_t e = hipGetLastError();

@@ -37,6 +37,7 @@ struct SvaoArgs {
     const float* sd;
     int sdW, sdH;
     uint32_t guard, secondary, rayInterval, sdJitter, N;
+    uint32_t bandIndex, bandCount;  // 32-row groups g (offset space) with g % count == index
 };
 
 struct Basic {
@@ -175,7 +176,7 @@ __global__ void clear_intervals_kernel(uint32_t* rmin, uint32_t* rmax, uint32_t 
 // SVAORaster.ps.slang:29-122, [numthreads(16,16,1)] with the 2x2 group interleave
 __global__ void __launch_bounds__(256) svao_pass1_kernel(SvaoArgs a) {
     const uint32_t ox = (blockIdx.x / 2u) * 32u + 2u * threadIdx.x + (blockIdx.x % 2u);
-    const uint32_t oy = (blockIdx.y / 2u) * 32u + 2u * threadIdx.y + (blockIdx.y % 2u);
+    const uint32_t oy = ((blockIdx.y / 2u) * a.bandCount + a.bandIndex) * 32u + 2u * threadIdx.y + (blockIdx.y % 2u);
     const uint32_t px = ox + a.guard, py = oy + a.guard;
     const rsd_vao_data& d = a.d;
     const float u = ((float)px + 0.5f) * d.invResolution[0];
@@ -234,7 +235,7 @@ __global__ void __launch_bounds__(256) svao_pass1_kernel(SvaoArgs a) {
 template <int N>
 __global__ void __launch_bounds__(256) svao_pass2_kernel(SvaoArgs a) {
     const uint32_t px = blockIdx.x * 16u + threadIdx.x + a.guard;
-    const uint32_t py = blockIdx.y * 16u + threadIdx.y + a.guard;
+    const uint32_t py = ((blockIdx.y / 2u) * a.bandCount + a.bandIndex) * 32u + (blockIdx.y % 2u) * 16u + threadIdx.y + a.guard;
     if (px >= (uint32_t)a.W - a.guard || py >= (uint32_t)a.H - a.guard) return;
     const size_t o = (size_t)py * a.W + px;
     uint32_t mask = a.stencil[o];
@@ -344,11 +345,22 @@ extern "C" rsd_status rsd_svao_clear_intervals(uint32_t* d_ray_min, uint32_t* d_
     return e == hipSuccess ? RSD_OK : hip_fail(e, "clear_intervals_kernel launch");
 }
 
-extern "C" rsd_status rsd_svao_pass1(const rsd_camera* cam, const rsd_vao_data* vao, const rsd_svao_params* p,
-                                     const float* d_depth, const uint16_t* d_normals, uint32_t W, uint32_t H,
-                                     uint8_t* d_ao, uint8_t* d_stencil, uint32_t* d_ray_min, uint32_t* d_ray_max,
-                                     uint32_t sd_w, uint32_t sd_h, rsd_stream stream) {
-    rsd_status st = check_common(cam, vao, p, d_depth, d_normals, W, H, "rsd_svao_pass1");
+static rsd_status check_band(uint32_t index, uint32_t count, const char* who) {
+    if (count == 0 || index >= count) {
+        set_error(std::string(who) + ": band_index must be < band_count");
+        return RSD_ERR_INVALID_ARG;
+    }
+    return RSD_OK;
+}
+
+extern "C" rsd_status rsd_svao_pass1_band(const rsd_camera* cam, const rsd_vao_data* vao, const rsd_svao_params* p,
+                                          const float* d_depth, const uint16_t* d_normals, uint32_t W, uint32_t H,
+                                          uint8_t* d_ao, uint8_t* d_stencil, uint32_t* d_ray_min, uint32_t* d_ray_max,
+                                          uint32_t sd_w, uint32_t sd_h, uint32_t band_index, uint32_t band_count,
+                                          rsd_stream stream) {
+    rsd_status st = check_band(band_index, band_count, "rsd_svao_pass1_band");
+    if (st != RSD_OK) return st;
+    st = check_common(cam, vao, p, d_depth, d_normals, W, H, "rsd_svao_pass1");
     if (st != RSD_OK) return st;
     if (!d_ao || !d_stencil || (p->secondary_depth_mode == 2 && (!d_ray_min || !d_ray_max || !sd_w || !sd_h))) {
         set_error("rsd_svao_pass1: null output buffer");
@@ -381,16 +393,23 @@ extern "C" rsd_status rsd_svao_pass1(const rsd_camera* cam, const rsd_vao_data* 
     a.N = p->sd_samples;
     // SVAO.cpp:347-350: nThreads = roundup32(dims - 2 guardBand), 16x16 groups
     const uint32_t nx = (W - 2 * p->guard_band + 31u) / 32u * 32u, ny = (H - 2 * p->guard_band + 31u) / 32u * 32u;
-    hipLaunchKernelGGL(svao_pass1_kernel, dim3(nx / 16, ny / 16), dim3(16, 16), 0, (hipStream_t)stream, a);
+    const uint32_t groups = ny / 32u;
+    const uint32_t bandGroups = groups > band_index ? (groups - band_index + band_count - 1) / band_count : 0u;
+    a.bandIndex = band_index;
+    a.bandCount = band_count;
+    if (bandGroups == 0) return RSD_OK;
+    hipLaunchKernelGGL(svao_pass1_kernel, dim3(nx / 16, 2 * bandGroups), dim3(16, 16), 0, (hipStream_t)stream, a);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? RSD_OK : hip_fail(e, "svao_pass1_kernel launch");
 }
 
-extern "C" rsd_status rsd_svao_pass2(const rsd_camera* cam, const rsd_vao_data* vao, const rsd_svao_params* p,
-                                     const float* d_depth, const uint16_t* d_normals, uint32_t W, uint32_t H,
-                                     const uint8_t* d_stencil, const float* d_sd, uint32_t sd_w, uint32_t sd_h,
-                                     uint8_t* d_ao, rsd_stream stream) {
-    rsd_status st = check_common(cam, vao, p, d_depth, d_normals, W, H, "rsd_svao_pass2");
+extern "C" rsd_status rsd_svao_pass2_band(const rsd_camera* cam, const rsd_vao_data* vao, const rsd_svao_params* p,
+                                          const float* d_depth, const uint16_t* d_normals, uint32_t W, uint32_t H,
+                                          const uint8_t* d_stencil, const float* d_sd, uint32_t sd_w, uint32_t sd_h,
+                                          uint8_t* d_ao, uint32_t band_index, uint32_t band_count, rsd_stream stream) {
+    rsd_status st = check_band(band_index, band_count, "rsd_svao_pass2_band");
+    if (st != RSD_OK) return st;
+    st = check_common(cam, vao, p, d_depth, d_normals, W, H, "rsd_svao_pass2");
     if (st != RSD_OK) return st;
     if (!d_stencil || !d_sd || !d_ao || !sd_w || !sd_h) {
         set_error("rsd_svao_pass2: null buffer");
@@ -420,7 +439,12 @@ extern "C" rsd_status rsd_svao_pass2(const rsd_camera* cam, const rsd_vao_data* 
     a.sdJitter = p->sd_jitter;
     a.N = N;
     const uint32_t vw = W - 2 * p->guard_band, vh = H - 2 * p->guard_band;
-    dim3 grid((vw + 15) / 16, (vh + 15) / 16), block(16, 16);
+    const uint32_t groups = (vh + 31u) / 32u;
+    const uint32_t bandGroups = groups > band_index ? (groups - band_index + band_count - 1) / band_count : 0u;
+    a.bandIndex = band_index;
+    a.bandCount = band_count;
+    if (bandGroups == 0) return RSD_OK;
+    dim3 grid((vw + 15) / 16, 2 * bandGroups), block(16, 16);
     hipStream_t s = (hipStream_t)stream;
     switch (N) {
         case 1: hipLaunchKernelGGL(svao_pass2_kernel<1>, grid, block, 0, s, a); break;
@@ -431,4 +455,19 @@ extern "C" rsd_status rsd_svao_pass2(const rsd_camera* cam, const rsd_vao_data* 
     }
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? RSD_OK : hip_fail(e, "svao_pass2_kernel launch");
+}
+
+extern "C" rsd_status rsd_svao_pass1(const rsd_camera* cam, const rsd_vao_data* vao, const rsd_svao_params* p,
+                                     const float* d_depth, const uint16_t* d_normals, uint32_t W, uint32_t H,
+                                     uint8_t* d_ao, uint8_t* d_stencil, uint32_t* d_ray_min, uint32_t* d_ray_max,
+                                     uint32_t sd_w, uint32_t sd_h, rsd_stream stream) {
+    return rsd_svao_pass1_band(cam, vao, p, d_depth, d_normals, W, H, d_ao, d_stencil, d_ray_min, d_ray_max, sd_w,
+                               sd_h, 0, 1, stream);
+}
+
+extern "C" rsd_status rsd_svao_pass2(const rsd_camera* cam, const rsd_vao_data* vao, const rsd_svao_params* p,
+                                     const float* d_depth, const uint16_t* d_normals, uint32_t W, uint32_t H,
+                                     const uint8_t* d_stencil, const float* d_sd, uint32_t sd_w, uint32_t sd_h,
+                                     uint8_t* d_ao, rsd_stream stream) {
+    return rsd_svao_pass2_band(cam, vao, p, d_depth, d_normals, W, H, d_stencil, d_sd, sd_w, sd_h, d_ao, 0, 1, stream);
 }

@@ -66,13 +66,14 @@ class SVAOParams(C.Structure):
 
 class Counters(C.Structure):
     _fields_ = [("rays_dispatched", C.c_uint64), ("rays_active", C.c_uint64), ("nodes_visited", C.c_uint64),
-                ("tris_tested", C.c_uint64), ("hits_delivered", C.c_uint64)]
+                ("tris_tested", C.c_uint64), ("hits_delivered", C.c_uint64), ("max_nodes_per_ray", C.c_uint64)]
 
 
 # every symbol include/rsd.h declares (checked by tests/test_abi.py)
 EXPORTS = ["rsd_abi_version", "rsd_last_error", "rsd_device_open", "rsd_device_close", "rsd_scene_upload",
            "rsd_scene_info_get", "rsd_scene_release", "rsd_camera_look_at", "rsd_svao_make_vao_data",
-           "rsd_gbuffer", "rsd_sd_trace", "rsd_svao_clear_intervals", "rsd_svao_pass1", "rsd_svao_pass2"]
+           "rsd_gbuffer", "rsd_sd_trace", "rsd_svao_clear_intervals", "rsd_svao_pass1", "rsd_svao_pass2",
+           "rsd_sd_trace_band", "rsd_svao_pass1_band", "rsd_svao_pass2_band"]
 
 _lib = None
 
@@ -114,6 +115,15 @@ def lib():
         L.rsd_svao_pass2.restype = st
         L.rsd_svao_pass2.argtypes = [C.POINTER(Camera), C.POINTER(VAOData), C.POINTER(SVAOParams), vp, vp, u32, u32,
                                      vp, vp, u32, u32, vp, vp]
+        L.rsd_sd_trace_band.restype = st
+        L.rsd_sd_trace_band.argtypes = [vp, C.POINTER(Camera), C.POINTER(SDParams), vp, u32, u32, vp, vp, vp, u32,
+                                        u32, u32, u32, C.POINTER(Counters), vp]
+        L.rsd_svao_pass1_band.restype = st
+        L.rsd_svao_pass1_band.argtypes = [C.POINTER(Camera), C.POINTER(VAOData), C.POINTER(SVAOParams), vp, vp, u32,
+                                          u32, vp, vp, vp, vp, u32, u32, u32, u32, vp]
+        L.rsd_svao_pass2_band.restype = st
+        L.rsd_svao_pass2_band.argtypes = [C.POINTER(Camera), C.POINTER(VAOData), C.POINTER(SVAOParams), vp, vp, u32,
+                                          u32, vp, vp, u32, u32, vp, u32, u32, vp]
         _lib = L
     return _lib
 

@@ -176,25 +176,27 @@ class Renderer:
         abi.check(abi.lib().rsd_svao_clear_intervals(_ptr(self.ray_min), _ptr(self.ray_max), self.sd_w * self.sd_h,
                                                      self.stream), "rsd_svao_clear_intervals")
 
-    def pass1(self):
-        abi.check(abi.lib().rsd_svao_pass1(C.byref(self.cam), C.byref(self.vao), C.byref(self.svp), _ptr(self.depth),
-                                           _ptr(self.normals), self.cfg.fb_w, self.cfg.fb_h, _ptr(self.ao),
-                                           _ptr(self.stencil), _ptr(self.ray_min), _ptr(self.ray_max), self.sd_w,
-                                           self.sd_h, self.stream), "rsd_svao_pass1")
+    def pass1(self, band=(0, 1)):
+        abi.check(abi.lib().rsd_svao_pass1_band(C.byref(self.cam), C.byref(self.vao), C.byref(self.svp),
+                                                _ptr(self.depth), _ptr(self.normals), self.cfg.fb_w, self.cfg.fb_h,
+                                                _ptr(self.ao), _ptr(self.stencil), _ptr(self.ray_min),
+                                                _ptr(self.ray_max), self.sd_w, self.sd_h, band[0], band[1],
+                                                self.stream), "rsd_svao_pass1_band")
 
-    def sd_trace(self, counters: bool = False):
+    def sd_trace(self, counters: bool = False, band=(0, 1)):
         cnt = abi.Counters() if counters else None
-        abi.check(abi.lib().rsd_sd_trace(self.gscene.h, C.byref(self.cam), C.byref(self.sdp), _ptr(self.depth),
-                                         self.cfg.fb_w, self.cfg.fb_h, _ptr(self.ray_min), _ptr(self.ray_max),
-                                         _ptr(self.sd), self.sd_w, self.sd_h,
-                                         C.byref(cnt) if cnt is not None else None, self.stream), "rsd_sd_trace")
+        abi.check(abi.lib().rsd_sd_trace_band(self.gscene.h, C.byref(self.cam), C.byref(self.sdp), _ptr(self.depth),
+                                              self.cfg.fb_w, self.cfg.fb_h, _ptr(self.ray_min), _ptr(self.ray_max),
+                                              _ptr(self.sd), self.sd_w, self.sd_h, band[0], band[1],
+                                              C.byref(cnt) if cnt is not None else None, self.stream),
+                  "rsd_sd_trace_band")
         return cnt
 
-    def pass2(self):
-        abi.check(abi.lib().rsd_svao_pass2(C.byref(self.cam), C.byref(self.vao), C.byref(self.svp), _ptr(self.depth),
-                                           _ptr(self.normals), self.cfg.fb_w, self.cfg.fb_h, _ptr(self.stencil),
-                                           _ptr(self.sd), self.sd_w, self.sd_h, _ptr(self.ao), self.stream),
-                  "rsd_svao_pass2")
+    def pass2(self, band=(0, 1)):
+        abi.check(abi.lib().rsd_svao_pass2_band(C.byref(self.cam), C.byref(self.vao), C.byref(self.svp),
+                                                _ptr(self.depth), _ptr(self.normals), self.cfg.fb_w, self.cfg.fb_h,
+                                                _ptr(self.stencil), _ptr(self.sd), self.sd_w, self.sd_h,
+                                                _ptr(self.ao), band[0], band[1], self.stream), "rsd_svao_pass2_band")
 
     def frame(self):
         """One AO frame: the span of the reference's "AO 1" + "AORefine" profile scopes."""

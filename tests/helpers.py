@@ -38,7 +38,9 @@ def oracle_frame(O, oscene, cam, vao, sdp, svp, fb_w, fb_h, sd_w, sd_h, threads=
     return dict(depth=z, normals=n, ao1=ao1, stencil=st, ray_min=rmin, ray_max=rmax, sd=sd, ao=ao2, stats=stats)
 
 
-def small_frame_config(visible=(160, 96), guard=16, divisor=2, N=4, max_count=8, impl=0):
+def small_frame_config(visible=(160, 96), guard=16, divisor=2, N=4, max_count=8, impl=0, radius=1.0):
+    """A small frame; the AO radius is scaled up so that, at this resolution, the sample
+    radius exceeds ssRadiusCutoff (6 px) and pass 1 actually requests SD rays."""
     from rsd.frame import FrameConfig
     return FrameConfig(visible_w=visible[0], visible_h=visible[1], guard_band=guard, divisor=divisor,
-                       sd_samples=N, max_count=max_count, implementation=impl, sd_guard_px=64)
+                       sd_samples=N, max_count=max_count, implementation=impl, sd_guard_px=64, radius=radius)

@@ -1,0 +1,34 @@
+"""Diagnostic timings of the SD trace kernel under controlled inputs (GPU box)."""
+import sys, time
+from pathlib import Path
+ROOT = Path(__file__).resolve().parents[1]
+sys.path[:0] = [str(ROOT), str(ROOT / "ray-traced-stochastic-depth-map_amd")]
+import torch
+from rsd.frame import CONFIGS, FrameConfig, Renderer
+from rsd.scenes import make_scene
+
+def timeit(fn, n=20):
+    fn(); torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(n): fn()
+    e.record(); torch.cuda.synchronize()
+    return s.elapsed_time(e) / n
+
+name = sys.argv[1] if len(sys.argv) > 1 else "suntemple_1080p_q"
+kw, sc = CONFIGS[name]
+r = Renderer(make_scene(sc), FrameConfig(**kw))
+r.gbuffer(); torch.cuda.synchronize()
+print("gbuffer ms", timeit(r.gbuffer, 5))
+r.clear_intervals()
+print("sd all-inactive ms", timeit(r.sd_trace))
+r.clear_intervals(); r.pass1()
+print("pass1 ms", timeit(lambda: (r.clear_intervals(), r.pass1())))
+c = r.sd_trace(counters=True)
+print("counters", c.rays_dispatched, c.rays_active, c.nodes_visited, c.tris_tested, c.hits_delivered, "max", c.max_nodes_per_ray)
+print("sd normal ms", timeit(r.sd_trace))
+print("pass2 ms", timeit(r.pass2))
+r.sdp.ray_interval = 0
+c = r.sd_trace(counters=True)
+print("no-interval counters", c.rays_active, c.nodes_visited, c.tris_tested, c.hits_delivered, "max", c.max_nodes_per_ray)
+print("sd no-interval ms", timeit(r.sd_trace, 5))
