@@ -12,10 +12,11 @@ N = 4, MAX_COUNT = 8.  Inputs (BVH, G-buffer) are resident in HBM before timing.
   ao_frames_per_s  = frames / timed wall
   sd_kernel_mrays  = SD rays / SD-kernel time (HIP events around the trace launch)
 
-Multi-GPU (torchrun, one rank per GPU): the frame is sharded by screen band.  Every
-rank holds the replicated BVH and G-buffer, runs pass 1 over the whole frame (exact
-ray intervals, no all-reduce), traces its band of SD rows, all-gathers the SD map,
-runs pass 2 on its band of AO rows and all-gathers the AO image (RCCL over xGMI).
+Multi-GPU (torchrun, one rank per GPU): the frame is sharded by screen band (rsd/shard.py).
+Every rank holds the replicated BVH and G-buffer, runs pass 1 on its band of rows, all-
+reduces the ray-interval maps (MIN/MAX), traces its band of SD tile rows, all-gathers the
+SD map, runs pass 2 on its band and all-gathers the AO image (RCCL over xGMI).  Strong
+scaling: the whole job renders the same frame size whatever N is.
 """
 from __future__ import annotations
 
@@ -71,24 +72,20 @@ def main():
     r.gbuffer()
     torch.cuda.synchronize()
 
-    # instrumented trace (not timed): traversal counters for the roofline bytes
+    # instrumented full-frame trace (not timed): traversal counters for the roofline bytes
     r.clear_intervals()
     r.pass1()
     cnt = r.sd_trace(counters=True)
     torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
 
-    stream = torch.cuda.current_stream()
+    from rsd.shard import BandFrame
+    bf = BandFrame(r, rank, world)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
 
     def frame(i=None):
-        r.clear_intervals()
-        r.pass1()
-        if i is not None:
-            ev[i][0].record(stream)
-        r.sd_trace()
-        if i is not None:
-            ev[i][1].record(stream)
-        r.pass2()
+        bf.frame(sd_events=ev[i] if i is not None else None)
 
     for _ in range(args.warmup):
         frame()

@@ -126,6 +126,10 @@ typedef struct {
     uint64_t tris_tested;     /* 48-B triangle records fetched */
     uint64_t hits_delivered;  /* any-hit invocations (sorted stream) */
     uint64_t max_nodes_per_ray; /* longest traversal (latency tail of the launch) */
+    uint64_t max_steps_per_ray; /* node + leaf steps of the longest traversal */
+    uint64_t sum_ray_clocks;    /* shader clocks (s_memtime) spent in live rays */
+    uint64_t max_ray_clocks;    /* the slowest live ray */
+    uint64_t leaves_visited;    /* leaf steps (<= 4 triangle records each) */
 } rsd_counters;
 
 /* --- library / device ------------------------------------------------------------ */

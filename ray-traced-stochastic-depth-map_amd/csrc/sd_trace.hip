@@ -156,7 +156,7 @@ struct KList {
 };
 
 struct TraceStats {
-    uint32_t nodes, tris;
+    uint32_t nodes, tris, leaves;
 };
 
 __device__ __forceinline__ void cswap(float& ta, uint32_t& ra, float& tb, uint32_t& rb) {
@@ -349,10 +349,145 @@ __device__ __forceinline__ void sd_store(const SDArgs& a, int x, int y, const fl
     }
 }
 
-// TraceRay + anyHit -> algorithm (Common.slangh:102-254) over the canonical hit stream.
+// ------------------------------------------------------------------------------------
+// Quad-cooperative traversal (the SD trace).  A live SD ray is latency-bound: few rays,
+// long dependent chains (MI355X: one wave alone issues a VALU op every ~4 cycles).  So
+// each ray is walked by a QUAD of 4 lanes: in a node step lane q fetches and tests child
+// q (the node is SoA, so the quad's 8 loads of 4 B are 16-B coalesced rows); in a leaf
+// step lane q tests triangle q.  The 4 child keys are sorted across the quad with
+// __shfl_xor compare-exchanges, the nearest is taken and the rest go to the ray's LDS
+// stack.  Every lane keeps an identical copy of the ray's k-list; accepted hits are
+// broadcast one by one and inserted by all 4 lanes.  A wave walks 16 rays.
+// ------------------------------------------------------------------------------------
+constexpr int kQuadRays = kBlock / 4;   // rays per wave
+constexpr int kQuadStack = 96;          // per-ray LDS stack depth (4-wide: <= 3 per level)
+
+// Quad-local exchange through DPP quad_perm (a VALU modifier: no LDS round trip, unlike
+// __shfl / ds_bpermute).  CTRL = quad_perm(p0,p1,p2,p3) = p0 | p1<<2 | p2<<4 | p3<<6.
+constexpr int kDppXor1 = 0xB1, kDppXor2 = 0x4E, kDppXor3 = 0x1B;
+template <int CTRL>
+__device__ __forceinline__ uint32_t dppu(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, true);
+}
+template <int CTRL>
+__device__ __forceinline__ float dppf(float v) {
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, true));
+}
+template <int L>  // value of quad lane L, in every lane of the quad
+__device__ __forceinline__ float qbcf(float v) { return dppf<L * 0x55>(v); }
+template <int L>
+__device__ __forceinline__ uint32_t qbcu(uint32_t v) { return dppu<L * 0x55>(v); }
+__device__ __forceinline__ float qself(float v, int j) {
+    const float b0 = qbcf<0>(v), b1 = qbcf<1>(v), b2 = qbcf<2>(v), b3 = qbcf<3>(v);
+    return j == 0 ? b0 : (j == 1 ? b1 : (j == 2 ? b2 : b3));
+}
+__device__ __forceinline__ uint32_t qselu(uint32_t v, int j) {
+    const uint32_t b0 = qbcu<0>(v), b1 = qbcu<1>(v), b2 = qbcu<2>(v), b3 = qbcu<3>(v);
+    return j == 0 ? b0 : (j == 1 ? b1 : (j == 2 ? b2 : b3));
+}
+
+template <int CTRL>
+__device__ __forceinline__ void quad_cx(float& k, uint32_t& it, bool low) {
+    const float ok = dppf<CTRL>(k);
+    const uint32_t oi = dppu<CTRL>(it);
+    const bool takeOther = low ? (ok < k) : (k < ok);
+    k = takeOther ? ok : k;
+    it = takeOther ? oi : it;
+}
+
+template <int K>
+__device__ __forceinline__ int trace_knearest_quad(const float4* __restrict__ bvh, uint32_t triOff, const RayCtx& r,
+                                                   float tmin, float tmax, uint32_t cull, bool useLB, float lbT,
+                                                   uint32_t lbP, KList<K>& kl, uint32_t* __restrict__ sItem,
+                                                   float* __restrict__ sT, int q, int quadBase, TraceStats& st) {
+    kl.clear();
+    int sp = 0, found = 0;
+    uint32_t item = 0;
+    const float tlo = useLB ? fmaxf(tmin, lbT) : tmin;
+    const float* bf = reinterpret_cast<const float*>(bvh);
+    while (true) {
+        const uint32_t off = item & kOffMask;
+        uint32_t next = kNoItem;
+        if (item & kLeafBit) {
+            st.leaves++;
+            const uint32_t cnt = ((item >> 29) & 3u) + 1u;
+            bool acc = false;
+            float t = 0.0f;
+            uint32_t prim = 0u;
+            if ((uint32_t)q < cnt) {
+                const float4* tp = bvh + off + 3u * (uint32_t)q;
+                const float4 va = tp[0], vb = tp[1], vc = tp[2];
+                st.tris++;
+                float bu, bv, det;
+                if (intersect_tri(r, va, vb, vc, t, bu, bv, det) && t >= tmin && t <= tmax) {
+                    prim = __float_as_uint(va.w);
+                    acc = !culled(det, __float_as_uint(vb.w), cull) && (!useLB || key_less(lbT, lbP, t, prim)) &&
+                          key_less(t, prim, kl.t[K - 1], kl.p[K - 1]);
+                }
+            }
+            uint32_t m = (uint32_t)(__ballot(acc) >> quadBase) & 0xfu;
+            const uint32_t first = (off - triOff) / 3u;
+            while (m) {
+                const int j = __ffs(m) - 1;
+                m &= m - 1u;
+                const float tj = qself(t, j);
+                const uint32_t pj = qselu(prim, j);
+                if (key_less(tj, pj, kl.t[K - 1], kl.p[K - 1])) {
+                    kl.insert(tj, pj, first + (uint32_t)j);
+                    found = found < K ? found + 1 : K;
+                }
+            }
+        } else {
+            st.nodes++;
+            const float thi = fminf(tmax, kl.t[K - 1]);
+            const float* nb = bf + 4u * off;
+            const float lox = nb[q], hix = nb[4 + q], loy = nb[8 + q], hiy = nb[12 + q], loz = nb[16 + q],
+                        hiz = nb[20 + q];
+            const uint32_t ref = __float_as_uint(nb[24 + q]), cnt = __float_as_uint(nb[28 + q]);
+            float tn;
+            const bool hit = ref != kNoItem && box_hit(r, lox, hix, loy, hiy, loz, hiz, tlo, thi, tn);
+            float k = hit ? tn : INFINITY;
+            uint32_t it = hit ? (cnt ? (kLeafBit | ((cnt - 1u) << 29) | (triOff + 3u * ref)) : 8u * ref) : kNoItem;
+            const int m = __popc((uint32_t)(__ballot(hit) >> quadBase) & 0xfu);
+            // sorting network (0,1)(2,3) (0,2)(1,3) (1,2) across the quad
+            quad_cx<kDppXor1>(k, it, (q & 1) == 0);
+            quad_cx<kDppXor2>(k, it, (q & 2) == 0);
+            {
+                const float ok = dppf<kDppXor3>(k);
+                const uint32_t oi = dppu<kDppXor3>(it);
+                const bool mid = q == 1 || q == 2;
+                const bool takeOther = mid && ((q == 1) ? (ok < k) : (k < ok));
+                k = takeOther ? ok : k;
+                it = takeOther ? oi : it;
+            }
+            next = qbcu<0>(it);
+            if (q >= 1 && q < m) {
+                const int slot = sp + (m - 1 - q);  // farthest deepest
+                sItem[slot * kQuadRays] = it;
+                sT[slot * kQuadRays] = k;
+            }
+            sp += m > 0 ? m - 1 : 0;
+        }
+        if (next == kNoItem) {
+            const float thi = fminf(tmax, kl.t[K - 1]);
+            while (sp > 0) {
+                --sp;
+                const float tt = sT[sp * kQuadRays];
+                if (tt <= thi) { next = sItem[sp * kQuadRays]; break; }
+            }
+            if (next == kNoItem) break;
+        }
+        item = next;
+    }
+    return found;
+}
+
+// TraceRay + anyHit -> algorithm (Common.slangh:102-254) over the canonical hit stream,
+// for the ray of this quad.  All 4 lanes end with identical depths.
 template <int K, int N>
 __device__ __forceinline__ void sd_resolve(const SDArgs& a, f3 d, float TMin, float TMax, float cosT, float (&depths)[N],
-                                           uint32_t* lds, float* ldsT, TraceStats& st, uint32_t& hitsDelivered) {
+                                           uint32_t* sItem, float* sT, int q, int quadBase, TraceStats& st,
+                                           uint32_t& hitsDelivered) {
     const rsd_camera& c = a.cam;
     RayCtx r;
     ray_setup(r, mk(c.posW[0], c.posW[1], c.posW[2]), d);
@@ -361,20 +496,37 @@ __device__ __forceinline__ void sd_resolve(const SDArgs& a, f3 d, float TMin, fl
     bool commit = false, useLB = false;
     float lbT = 0.0f;
     uint32_t lbP = 0u;
+    constexpr int J = (K + 3) / 4;  // hits per lane in the epilogue
     while (!commit) {
-        const int found = trace_knearest<K>(a.nodes, a.triOff, r, TMin, TMax, a.cull, useLB, lbT, lbP, kl, lds, ldsT,
-                                            st);
+        const int found = trace_knearest_quad<K>(a.nodes, a.triOff, r, TMin, TMax, a.cull, useLB, lbT, lbP, kl, sItem,
+                                                 sT, q, quadBase, st);
+        // barycentrics + hash of hit j are computed by lane j % 4 (re-running the identical
+        // triangle test on the hit's record), then shared with the quad
+        float rngL[J], zL[J];
+#pragma unroll
+        for (int i = 0; i < J; ++i) {
+            const int j = 4 * i + q;
+            rngL[i] = 0.0f;
+            zL[i] = 0.0f;
+            uint32_t ti = 0u;
+#pragma unroll
+            for (int jj = 0; jj < K; ++jj)
+                if (jj == j) ti = kl.l[jj];
+            if (j < found) {
+                float t, bu, bv, det;
+                intersect_tri(r, a.tris[3 * ti], a.tris[3 * ti + 1], a.tris[3 * ti + 2], t, bu, bv, det);
+                rngL[i] = sd_hash(bu, bv);
+                float z = t * cosT;  // RayToViewDepth
+                if (a.normalize) z = saturate((z - c.nearZ) / (c.farZ - c.nearZ));
+                zL[i] = z;
+            }
+        }
 #pragma unroll
         for (int j = 0; j < K; ++j) {
+            const float rng = qself(rngL[j / 4], j % 4);
+            float z = qself(zL[j / 4], j % 4);
             if (commit || j >= found) continue;
-            // barycentrics of the j-th hit: re-run the identical test on its record
-            const uint32_t ti = kl.l[j];
-            float t, bu, bv, det;
-            intersect_tri(r, a.tris[3 * ti], a.tris[3 * ti + 1], a.tris[3 * ti + 2], t, bu, bv, det);
             hitsDelivered++;
-            const float rng = sd_hash(bu, bv);
-            float z = t * cosT;  // RayToViewDepth
-            if (a.normalize) z = saturate((z - c.nearZ) / (c.farZ - c.nearZ));
             if (a.impl == 1u) {  // CoverageMask, Common.slangh:117-131, 189-209
                 const int R = (int)floorf(a.alpha * (float)N + rng);
                 uint32_t mask = 0u;
@@ -451,23 +603,25 @@ __global__ void __launch_bounds__(kBlock) sd_setup_kernel(SDArgs a, uint32_t* __
     if (a.counters && lane == 0) atomicAdd(&a.counters[0], (unsigned long long)__popcll(in));
 }
 
-// Phase 2: persistent waves pull 64 live rays at a time from the queue until it drains
-// (every wave reaches the exit: the head only grows and the count is fixed).  The first
-// chunk of each wave is static (blockIdx), later ones come from one atomic head that
-// starts after the static range -- a wave with no static chunk exits without an atomic
-// (one head word serialises ~90 dequeues/us, MI355X_MICROARCH.md "dequeue").
+// Phase 2: persistent waves pull 16 live rays (one per quad) at a time from the queue
+// until it drains (every wave reaches the exit: the head only grows, the count is fixed).
+// The first chunk of each wave is static (blockIdx); later ones come from one atomic head
+// that starts after the static range, so a wave with no static chunk exits without an
+// atomic (one head word serialises ~90 dequeues/us, MI355X_MICROARCH.md "dequeue").
 template <int K, int N>
 __global__ void __launch_bounds__(kBlock) sd_trace_queue_kernel(SDArgs a, const uint32_t* __restrict__ queue,
                                                                 uint32_t* __restrict__ qctl) {
-    __shared__ uint32_t sstack[kLdsStack * kBlock];
-    __shared__ float sstackT[kLdsStack * kBlock];
+    __shared__ uint32_t sItem[kQuadStack * kQuadRays];
+    __shared__ float sT[kQuadStack * kQuadRays];
     const int lane = threadIdx.x;
+    const int q = lane & 3, quad = lane >> 2, quadBase = lane & ~3;
     const uint32_t count = __hip_atomic_load(&qctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    TraceStats st{0u, 0u};
-    uint32_t active = 0, hitsDelivered = 0, maxNodes = 0;
-    uint32_t base = blockIdx.x * (uint32_t)kBlock;
+    TraceStats st{0u, 0u, 0u};
+    uint32_t active = 0, hitsDelivered = 0, maxNodes = 0, maxSteps = 0;
+    unsigned long long sumCycles = 0, maxCycles = 0;
+    uint32_t base = blockIdx.x * (uint32_t)kQuadRays;
     while (base < count) {
-        const uint32_t qi = base + (uint32_t)lane;
+        const uint32_t qi = base + (uint32_t)quad;
         if (qi < count) {
             const uint32_t idx = queue[qi];
             const int x = (int)(idx % (uint32_t)a.sdW), y = (int)(idx / (uint32_t)a.sdW);
@@ -478,21 +632,36 @@ __global__ void __launch_bounds__(kBlock) sd_trace_queue_kernel(SDArgs a, const 
             const float DEFAULT = a.normalize ? 1.0f : 3.40282347e+37f;
 #pragma unroll
             for (int i = 0; i < N; ++i) depths[i] = DEFAULT;
-            const uint32_t n0 = st.nodes;
-            sd_resolve<K, N>(a, d, TMin, TMax, cosT, depths, &sstack[lane], &sstackT[lane], st, hitsDelivered);
-            maxNodes = max(maxNodes, st.nodes - n0);
-            active++;
-            sd_store<N>(a, x, y, depths);
+            const uint32_t n0 = st.nodes, l0 = st.leaves;
+            const unsigned long long c0 = a.counters ? __builtin_amdgcn_s_memtime() : 0ull;
+            sd_resolve<K, N>(a, d, TMin, TMax, cosT, depths, &sItem[quad], &sT[quad], q, quadBase, st,
+                             hitsDelivered);
+            if (q == 0) {
+                if (a.counters) {
+                    const unsigned long long dc = __builtin_amdgcn_s_memtime() - c0;
+                    sumCycles += dc;
+                    maxCycles = dc > maxCycles ? dc : maxCycles;
+                }
+                maxNodes = max(maxNodes, st.nodes - n0);
+                maxSteps = max(maxSteps, st.nodes - n0 + st.leaves - l0);
+                active++;
+                sd_store<N>(a, x, y, depths);
+            }
         }
-        if (lane == 0) base = gridDim.x * (uint32_t)kBlock + atomicAdd(&qctl[1], (uint32_t)kBlock);
+        if (lane == 0) base = gridDim.x * (uint32_t)kQuadRays + atomicAdd(&qctl[1], (uint32_t)kQuadRays);
         base = __shfl(base, 0);
     }
     if (a.counters) {
+        if (q != 0) hitsDelivered = 0;
         atomicAdd(&a.counters[1], (unsigned long long)active);
-        atomicAdd(&a.counters[2], (unsigned long long)st.nodes);
+        atomicAdd(&a.counters[2], (unsigned long long)(q == 0 ? st.nodes : 0u));
         atomicAdd(&a.counters[3], (unsigned long long)st.tris);
         atomicAdd(&a.counters[4], (unsigned long long)hitsDelivered);
         atomicMax(&a.counters[5], (unsigned long long)maxNodes);
+        atomicMax(&a.counters[6], (unsigned long long)maxSteps);
+        atomicAdd(&a.counters[7], sumCycles);
+        atomicMax(&a.counters[8], maxCycles);
+        atomicAdd(&a.counters[9], (unsigned long long)(q == 0 ? st.leaves : 0u));
     }
 }
 
@@ -528,7 +697,7 @@ __global__ void __launch_bounds__(kBlock) gbuffer_kernel(GBArgs a) {
     RayCtx r;
     ray_setup(r, mk(c.posW[0], c.posW[1], c.posW[2]), d);
     KList<1> kl;
-    TraceStats st{0u, 0u};
+    TraceStats st{0u, 0u, 0u};
     const int found = trace_knearest<1>(a.nodes, a.triOff, r, c.nearZ * invCos, c.farZ * invCos, a.cull, false,
                                         0.0f, 0u, kl, &sstack[lane], &sstackT[lane], st);
     const size_t o = (size_t)y * a.W + x;
@@ -658,7 +827,7 @@ extern "C" rsd_status rsd_sd_trace_band(rsd_scene* scene, const rsd_camera* cam,
         std::vector<float> h((size_t)sd_w * sd_h * (N < 4 ? N : 4) * ((N + 3) / 4), def);
         RSD_HIP(hipMemcpyAsync(d_sd_out, h.data(), h.size() * sizeof(float), hipMemcpyHostToDevice, (hipStream_t)stream));
         RSD_HIP(hipStreamSynchronize((hipStream_t)stream));
-        if (counters) *counters = rsd_counters{(uint64_t)sd_w * sd_h, 0, 0, 0, 0, 0};
+        if (counters) { *counters = rsd_counters{}; counters->rays_dispatched = (uint64_t)sd_w * sd_h; }
         return RSD_OK;
     }
     SDArgs a;
@@ -693,7 +862,7 @@ extern "C" rsd_status rsd_sd_trace_band(rsd_scene* scene, const rsd_camera* cam,
     }
     hipStream_t s = (hipStream_t)stream;
     if (counters) {
-        RSD_HIP(hipMemsetAsync(scene->d_counters, 0, 6 * sizeof(unsigned long long), s));
+        RSD_HIP(hipMemsetAsync(scene->d_counters, 0, 10 * sizeof(unsigned long long), s));
         a.counters = scene->d_counters;
     }
     const uint32_t tiles = (sd_h + kTile - 1) / kTile;
@@ -719,7 +888,7 @@ extern "C" rsd_status rsd_sd_trace_band(rsd_scene* scene, const rsd_camera* cam,
     else e = launch_sd_k<16>(a, N, grid, pb, scene->d_queue, scene->d_qctl, s);
     if (e != hipSuccess) return hip_fail(e, "sd_trace_kernel launch");
     if (counters) {
-        unsigned long long h[6];
+        unsigned long long h[10];
         RSD_HIP(hipMemcpyAsync(h, scene->d_counters, sizeof(h), hipMemcpyDeviceToHost, s));
         RSD_HIP(hipStreamSynchronize(s));
         counters->rays_dispatched = h[0];
@@ -728,6 +897,10 @@ extern "C" rsd_status rsd_sd_trace_band(rsd_scene* scene, const rsd_camera* cam,
         counters->tris_tested = h[3];
         counters->hits_delivered = h[4];
         counters->max_nodes_per_ray = h[5];
+        counters->max_steps_per_ray = h[6];
+        counters->sum_ray_clocks = h[7];
+        counters->max_ray_clocks = h[8];
+        counters->leaves_visited = h[9];
     }
     return RSD_OK;
 }

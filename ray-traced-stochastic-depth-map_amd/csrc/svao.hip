@@ -38,6 +38,7 @@ struct SvaoArgs {
     int sdW, sdH;
     uint32_t guard, secondary, rayInterval, sdJitter, N;
     uint32_t bandIndex, bandCount;  // 32-row groups g (offset space) with g % count == index
+    float isx, isy;  // imageScale (Common.slang:142), hoisted: 0.5 * (frameW / focal), same bits
 };
 
 struct Basic {
@@ -57,15 +58,11 @@ struct Sample {
 
 __device__ __forceinline__ f3 uv_to_view(const SvaoArgs& a, float u, float v, float z) {
     const float ndcx = u * 2.0f - 1.0f, ndcy = (1.0f - v) * 2.0f - 1.0f;
-    const float isx = 0.5f * (a.cam.frameWidth / a.cam.focalLength);
-    const float isy = 0.5f * (a.cam.frameHeight / a.cam.focalLength);
-    return mk(ndcx * z * isx, ndcy * z * isy, -z);
+    return mk(ndcx * z * a.isx, ndcy * z * a.isy, -z);
 }
 
 __device__ __forceinline__ void view_to_uv(const SvaoArgs& a, f3 p, float& u, float& v) {
-    const float isx = 0.5f * (a.cam.frameWidth / a.cam.focalLength);
-    const float isy = 0.5f * (a.cam.frameHeight / a.cam.focalLength);
-    const float ndcx = p.x / (isx * p.z), ndcy = p.y / (isy * p.z);
+    const float ndcx = p.x / (a.isx * p.z), ndcy = p.y / (a.isy * p.z);
     u = ndcx * -0.5f + 0.5f;
     v = ndcy * 0.5f + 0.5f;
 }
@@ -291,6 +288,12 @@ __global__ void __launch_bounds__(256) svao_pass2_kernel(SvaoArgs a) {
     a.ao[o] = unorm8(vis);
 }
 
+static void fill_scale(SvaoArgs& a) {
+    // Common.slang:142/150 imageScale, evaluated once on the host (IEEE float, same bits)
+    a.isx = 0.5f * (a.cam.frameWidth / a.cam.focalLength);
+    a.isy = 0.5f * (a.cam.frameHeight / a.cam.focalLength);
+}
+
 static void fill_consts(SvaoConsts& k) {
     // SVAO.cpp:670-684 -> R8Unorm noise; Common.slang:311-312 randRotation, :357 alpha
     static const float dither[16] = {0.0f, 8.0f, 2.0f, 10.0f, 12.0f, 4.0f, 14.0f, 6.0f,
@@ -376,6 +379,7 @@ extern "C" rsd_status rsd_svao_pass1_band(const rsd_camera* cam, const rsd_vao_d
     a.cam = *cam;
     a.d = *vao;
     fill_consts(a.k);
+    fill_scale(a);
     a.depth = d_depth;
     a.normals = d_normals;
     a.W = (int)W;
@@ -424,6 +428,7 @@ extern "C" rsd_status rsd_svao_pass2_band(const rsd_camera* cam, const rsd_vao_d
     a.cam = *cam;
     a.d = *vao;
     fill_consts(a.k);
+    fill_scale(a);
     a.depth = d_depth;
     a.normals = d_normals;
     a.W = (int)W;

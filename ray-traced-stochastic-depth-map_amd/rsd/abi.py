@@ -66,7 +66,9 @@ class SVAOParams(C.Structure):
 
 class Counters(C.Structure):
     _fields_ = [("rays_dispatched", C.c_uint64), ("rays_active", C.c_uint64), ("nodes_visited", C.c_uint64),
-                ("tris_tested", C.c_uint64), ("hits_delivered", C.c_uint64), ("max_nodes_per_ray", C.c_uint64)]
+                ("tris_tested", C.c_uint64), ("hits_delivered", C.c_uint64), ("max_nodes_per_ray", C.c_uint64),
+                ("max_steps_per_ray", C.c_uint64), ("sum_ray_clocks", C.c_uint64), ("max_ray_clocks", C.c_uint64),
+                ("leaves_visited", C.c_uint64)]
 
 
 # every symbol include/rsd.h declares (checked by tests/test_abi.py)

@@ -1,0 +1,112 @@
+"""Multi-process screen-band sharding (rsd/shard.py) over gloo on the CPU.
+
+The GPU backend of BandFrame is librsd (bench.py, tests/test_gpu_parity.py); here the same
+orchestration runs with the CPU oracle as backend in world_size 2 and 3 processes, and the
+gathered frame must be bit-identical to a single-process oracle frame."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from helpers import oracle_vao, small_frame_config
+
+
+class OracleBackend:
+    """BandFrame backend on the CPU oracle; numpy buffers shared with torch tensors."""
+
+    def __init__(self, O, scene, cfg):
+        self.O, self.cfg = O, cfg
+        self.osc = O.Scene(scene.positions, scene.indices, scene.flags)
+        W, H = cfg.fb_w, cfg.fb_h
+        aspect = float(np.float32(W) / np.float32(H))
+        self.cam = O.camera_look_at(scene.camera["pos"], scene.camera["target"], scene.camera["up"], aspect=aspect)
+        self.vao, self.sd_w, self.sd_h = oracle_vao(O, W, H, cfg.divisor, cfg.sd_guard_px, cfg.radius)
+        N = cfg.sd_samples
+        self.sdp = O.SDParams(N, cfg.implementation, cfg.max_count, self.vao.sdGuard, 1, 1, 1, cfg.cull_mode, 0,
+                              float(np.float32(1.5 / N)))
+        self.svp = O.SVAOParams(8, N, 2, 1, 1, cfg.guard_band)
+        self.z, self.n = O.gbuffer(self.osc, self.cam, W, H, cfg.cull_mode, threads=2)
+        self.np_ao = np.zeros((H, W), np.uint8)
+        self.np_st = np.zeros((H, W), np.uint8)
+        self.np_rmin = np.zeros((self.sd_h, self.sd_w), np.uint32)
+        self.np_rmax = np.zeros((self.sd_h, self.sd_w), np.uint32)
+        self.np_sd = np.zeros(((N + 3) // 4, self.sd_h, self.sd_w, min(N, 4)), np.float32)
+        self.ao = torch.from_numpy(self.np_ao)
+        self.stencil = torch.from_numpy(self.np_st)
+        self.ray_min = torch.from_numpy(self.np_rmin.view(np.int32))
+        self.ray_max = torch.from_numpy(self.np_rmax.view(np.int32))
+        self.sd = torch.from_numpy(self.np_sd)
+
+    def clear_intervals(self):
+        self.O.svao_clear(self.np_rmin, self.np_rmax)
+
+    def pass1(self, band=(0, 1)):
+        self.O.svao_pass1_into(self.cam, self.vao, self.svp, self.z, self.n, self.np_ao, self.np_st, self.np_rmin,
+                               self.np_rmax, band)
+
+    def sd_trace(self, band=(0, 1)):
+        self.O.sd_trace_into(self.osc, self.cam, self.sdp, self.z, self.np_rmin, self.np_rmax, self.np_sd, band,
+                             threads=2)
+
+    def pass2(self, band=(0, 1)):
+        self.O.svao_pass2_into(self.cam, self.vao, self.svp, self.z, self.n, self.np_st, self.np_sd, self.np_ao, band,
+                               threads=2)
+
+
+def _cfg():
+    return small_frame_config(visible=(192, 104), guard=16, divisor=2, N=4)
+
+
+def _worker(rank, world, port, out_dir):
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parents[1]
+    for p in (str(root), str(root / "ray-traced-stochastic-depth-map_amd"), str(root / "tests")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    import torch.distributed as dist
+
+    from oracle import oracle as O
+    from rsd.scenes import make_scene
+    from rsd.shard import BandFrame
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    be = OracleBackend(O, make_scene("arcade_tiny"), _cfg())
+    BandFrame(be, rank, world).frame()
+    np.save(os.path.join(out_dir, f"ao_{rank}.npy"), be.np_ao)
+    np.save(os.path.join(out_dir, f"sd_{rank}.npy"), be.np_sd)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_band_sharded_frame_equals_single_process(oracle, tmp_path, world):
+    from rsd.scenes import make_scene
+    from rsd.shard import BandFrame
+    ref = OracleBackend(oracle, make_scene("arcade_tiny"), _cfg())
+    BandFrame(ref, 0, 1).frame()
+    assert (ref.np_st != 0).any()
+    mp.start_processes(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True,
+                       start_method="spawn")
+    for r in range(world):
+        assert np.array_equal(np.load(tmp_path / f"ao_{r}.npy"), ref.np_ao), f"rank {r} AO"
+        assert np.array_equal(np.load(tmp_path / f"sd_{r}.npy").view(np.uint32), ref.np_sd.view(np.uint32)), \
+            f"rank {r} SD map"
+
+
+def test_band_rows_partition():
+    from rsd.shard import band_rows
+    for world in (1, 2, 3, 8):
+        rows = [band_rows(1144, 32, 64, r, world) for r in range(world)]
+        allr = torch.cat(rows).sort().values
+        assert torch.equal(allr, torch.arange(64, 64 + 1144))

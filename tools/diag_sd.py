@@ -26,6 +26,8 @@ r.clear_intervals(); r.pass1()
 print("pass1 ms", timeit(lambda: (r.clear_intervals(), r.pass1())))
 c = r.sd_trace(counters=True)
 print("counters", c.rays_dispatched, c.rays_active, c.nodes_visited, c.tris_tested, c.hits_delivered, "max", c.max_nodes_per_ray)
+print("steps: max", c.max_steps_per_ray, "leaves", c.leaves_visited, "avg clocks/ray", c.sum_ray_clocks / max(c.rays_active, 1),
+      "max clocks", c.max_ray_clocks, "clocks/step avg", c.sum_ray_clocks / max(c.nodes_visited + c.leaves_visited, 1))
 print("sd normal ms", timeit(r.sd_trace))
 print("pass2 ms", timeit(r.pass2))
 r.sdp.ray_interval = 0
