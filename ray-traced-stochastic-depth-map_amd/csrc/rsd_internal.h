@@ -22,7 +22,7 @@ struct rsd_scene {
     rsd::BvhStats stats;
     uint64_t device_bytes = 0;
     unsigned long long* d_counters = nullptr;  // 8 x u64 scratch for instrumented traces
-    uint32_t* d_qctl = nullptr;    // live-ray queue {count, head}
+    uint32_t* d_qctl = nullptr;    // live-ray queue {count[32], head[32]}
     uint32_t* d_queue = nullptr;   // live-ray queue (SD texel indices), grow-only
     size_t queue_cap = 0;
 };

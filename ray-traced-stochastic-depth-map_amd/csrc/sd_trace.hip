@@ -30,6 +30,7 @@
 namespace rsd {
 
 constexpr int kTile = 8;               // 8x8 texels per wave
+constexpr uint32_t kQueueParts = 32;   // live-ray queue partitions (counter sharding)
 constexpr int kBlock = kTile * kTile;  // 64 threads
 constexpr int kLdsStack = 16;
 constexpr int kStackTotal = 96;        // 4-wide: <= 3 pushes per level, <= 30 levels
@@ -291,6 +292,7 @@ struct SDArgs {
     const int32_t* lutIdx;  // coverage mask: stratified indices [N+1]
     const uint32_t* lut;    // coverage mask: look-up table [2^N]
     unsigned long long* counters;
+    uint32_t partCap;  // live-ray queue: capacity of one partition
     int bandIndex, bandCount;  // screen-band sharding: 8-row tile rows t with t % count == index
 };
 
@@ -595,10 +597,16 @@ __global__ void __launch_bounds__(kBlock) sd_setup_kernel(SDArgs a, uint32_t* __
     }
     const unsigned long long m = __ballot(live);
     const uint32_t n = (uint32_t)__popcll(m);
+    // the queue is split in kQueueParts partitions (block b -> partition b % kQueueParts), each
+    // with its own counter: one counter word serialises ~90 atomics/us.
+    const uint32_t lin = blockIdx.y * gridDim.x + blockIdx.x;
+    const uint32_t part = lin % kQueueParts;
     uint32_t base = 0;
-    if (lane == 0 && n) base = atomicAdd(&qctl[0], n);
+    if (lane == 0 && n) base = atomicAdd(&qctl[part], n);
     base = __shfl(base, 0);
-    if (live) queue[base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = (uint32_t)y * (uint32_t)a.sdW + x;
+    if (live)
+        queue[part * a.partCap + base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] =
+            (uint32_t)y * (uint32_t)a.sdW + x;
     const unsigned long long in = __ballot(inside);
     if (a.counters && lane == 0) atomicAdd(&a.counters[0], (unsigned long long)__popcll(in));
 }
@@ -615,15 +623,18 @@ __global__ void __launch_bounds__(kBlock) sd_trace_queue_kernel(SDArgs a, const 
     __shared__ float sT[kQuadStack * kQuadRays];
     const int lane = threadIdx.x;
     const int q = lane & 3, quad = lane >> 2, quadBase = lane & ~3;
-    const uint32_t count = __hip_atomic_load(&qctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // wave w serves partition w % kQueueParts (gridDim.x is a multiple of kQueueParts)
+    const uint32_t part = blockIdx.x % kQueueParts, wavesPerPart = gridDim.x / kQueueParts;
+    const uint32_t count = __hip_atomic_load(&qctl[part], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t* pq = queue + part * a.partCap;
     TraceStats st{0u, 0u, 0u};
     uint32_t active = 0, hitsDelivered = 0, maxNodes = 0, maxSteps = 0;
     unsigned long long sumCycles = 0, maxCycles = 0;
-    uint32_t base = blockIdx.x * (uint32_t)kQuadRays;
+    uint32_t base = (blockIdx.x / kQueueParts) * (uint32_t)kQuadRays;
     while (base < count) {
         const uint32_t qi = base + (uint32_t)quad;
         if (qi < count) {
-            const uint32_t idx = queue[qi];
+            const uint32_t idx = pq[qi];
             const int x = (int)(idx % (uint32_t)a.sdW), y = (int)(idx / (uint32_t)a.sdW);
             f3 d;
             float TMin, TMax, cosT;
@@ -648,7 +659,8 @@ __global__ void __launch_bounds__(kBlock) sd_trace_queue_kernel(SDArgs a, const 
                 sd_store<N>(a, x, y, depths);
             }
         }
-        if (lane == 0) base = gridDim.x * (uint32_t)kQuadRays + atomicAdd(&qctl[1], (uint32_t)kQuadRays);
+        if (lane == 0)
+            base = wavesPerPart * (uint32_t)kQuadRays + atomicAdd(&qctl[kQueueParts + part], (uint32_t)kQuadRays);
         base = __shfl(base, 0);
     }
     if (a.counters) {
@@ -871,7 +883,7 @@ extern "C" rsd_status rsd_sd_trace_band(rsd_scene* scene, const rsd_camera* cam,
     // k = the MAX_COUNT nearest keys decide Default and KBuffer; coverage mask streams chunks
     const uint32_t need = p->implementation == RSD_SD_COVERAGE_MASK ? 8u : p->max_count;
     // live-ray queue workspace (grow-only; the first call of a larger map allocates)
-    const size_t need_q = (size_t)sd_w * sd_h;
+    const size_t need_q = ((size_t)(sd_w + kTile - 1) / kTile * ((sd_h + kTile - 1) / kTile) + kQueueParts) * kBlock;
     if (scene->queue_cap < need_q) {
         RSD_HIP(hipStreamSynchronize(s));
         (void)hipFree(scene->d_queue);
@@ -879,8 +891,10 @@ extern "C" rsd_status rsd_sd_trace_band(rsd_scene* scene, const rsd_camera* cam,
         RSD_HIP(hipMalloc(&scene->d_queue, need_q * sizeof(uint32_t)));
         scene->queue_cap = need_q;
     }
-    RSD_HIP(hipMemsetAsync(scene->d_qctl, 0, 2 * sizeof(uint32_t), s));
-    const uint32_t pb = (uint32_t)std::max(1, scene->dev->cu_count) * 8u;
+    RSD_HIP(hipMemsetAsync(scene->d_qctl, 0, 2 * kQueueParts * sizeof(uint32_t), s));
+    const uint32_t setupBlocks = grid.x * grid.y;
+    a.partCap = (setupBlocks + kQueueParts - 1) / kQueueParts * (uint32_t)kBlock;
+    const uint32_t pb = ((uint32_t)std::max(1, scene->dev->cu_count) * 8u + kQueueParts - 1) / kQueueParts * kQueueParts;
     hipError_t e = hipSuccess;
     if (bandTiles == 0) {}
     else if (need <= 4) e = launch_sd_k<4>(a, N, grid, pb, scene->d_queue, scene->d_qctl, s);

@@ -172,8 +172,9 @@ __global__ void clear_intervals_kernel(uint32_t* rmin, uint32_t* rmax, uint32_t 
 
 // SVAORaster.ps.slang:29-122, [numthreads(16,16,1)] with the 2x2 group interleave
 __global__ void __launch_bounds__(256) svao_pass1_kernel(SvaoArgs a) {
-    const uint32_t ox = (blockIdx.x / 2u) * 32u + 2u * threadIdx.x + (blockIdx.x % 2u);
-    const uint32_t oy = ((blockIdx.y / 2u) * a.bandCount + a.bandIndex) * 32u + 2u * threadIdx.y + (blockIdx.y % 2u);
+    const uint32_t bx = blockIdx.x, by = blockIdx.y;
+    const uint32_t ox = (bx / 2u) * 32u + 2u * threadIdx.x + (bx % 2u);
+    const uint32_t oy = ((by / 2u) * a.bandCount + a.bandIndex) * 32u + 2u * threadIdx.y + (by % 2u);
     const uint32_t px = ox + a.guard, py = oy + a.guard;
     const rsd_vao_data& d = a.d;
     const float u = ((float)px + 0.5f) * d.invResolution[0];
@@ -231,8 +232,9 @@ __global__ void __launch_bounds__(256) svao_pass1_kernel(SvaoArgs a) {
 // SVAORaster2.ps.slang:48-65 -> calcAO2 (Common.slang:523-597), stochastic-depth branch
 template <int N>
 __global__ void __launch_bounds__(256) svao_pass2_kernel(SvaoArgs a) {
-    const uint32_t px = blockIdx.x * 16u + threadIdx.x + a.guard;
-    const uint32_t py = ((blockIdx.y / 2u) * a.bandCount + a.bandIndex) * 32u + (blockIdx.y % 2u) * 16u + threadIdx.y + a.guard;
+    const uint32_t bx = blockIdx.x, by = blockIdx.y;
+    const uint32_t px = bx * 16u + threadIdx.x + a.guard;
+    const uint32_t py = ((by / 2u) * a.bandCount + a.bandIndex) * 32u + (by % 2u) * 16u + threadIdx.y + a.guard;
     if (px >= (uint32_t)a.W - a.guard || py >= (uint32_t)a.H - a.guard) return;
     const size_t o = (size_t)py * a.W + px;
     uint32_t mask = a.stencil[o];
