@@ -91,10 +91,20 @@ __device__ __forceinline__ float tex_bilinear(const float* __restrict__ tex, int
     if (qx >= 256.0f) { ix += 1; qx = 0.0f; }
     if (qy >= 256.0f) { iy += 1; qy = 0.0f; }
     float wx = qx * (1.0f / 256.0f), wy = qy * (1.0f / 256.0f);
-    int x0 = tex_addr(ix, W, wrap), x1 = tex_addr(ix + 1, W, wrap);
-    int y0 = tex_addr(iy, H, wrap), y1 = tex_addr(iy + 1, H, wrap);
-    float t00 = tex[(size_t)y0 * W + x0], t10 = tex[(size_t)y0 * W + x1];
-    float t01 = tex[(size_t)y1 * W + x0], t11 = tex[(size_t)y1 * W + x1];
+    int x0 = tex_addr(ix, W, wrap), y0 = tex_addr(iy, H, wrap);
+    const float t00 = tex[(size_t)y0 * W + x0];
+    // Zero weights: t*(1-0) + t'*0 == t exactly for finite t' (depth texels are finite,
+    // DESIGN.md "Numerics"), so the taps with zero weight are not fetched.  Pixel-centre
+    // samples (SVAO Init / primary visibility) need 1 fetch instead of 4.
+    if (qx == 0.0f && qy == 0.0f) return t00;
+    int x1 = tex_addr(ix + 1, W, wrap), y1 = tex_addr(iy + 1, H, wrap);
+    if (qy == 0.0f) {
+        const float t10 = tex[(size_t)y0 * W + x1];
+        return t00 * (1.0f - wx) + t10 * wx;
+    }
+    const float t01 = tex[(size_t)y1 * W + x0];
+    if (qx == 0.0f) return t00 * (1.0f - wy) + t01 * wy;
+    const float t10 = tex[(size_t)y0 * W + x1], t11 = tex[(size_t)y1 * W + x1];
     float r0 = t00 * (1.0f - wx) + t10 * wx;
     float r1 = t01 * (1.0f - wx) + t11 * wx;
     return r0 * (1.0f - wy) + r1 * wy;
