@@ -34,6 +34,7 @@ for p in (str(ROOT), str(PKG)):
         sys.path.insert(0, p)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8 TB/s (spec)
+SD_KERNELS = ("sd_setup_kernel", "sd_trace_queue_kernel")  # the two launches of one rsd_sd_trace
 
 
 def parse():
@@ -44,7 +45,9 @@ def parse():
     ap.add_argument("--config", default="suntemple_1080p_q")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0,
                     help="target wall time of the bounded CPU-oracle sample (0 disables)")
-    ap.add_argument("--pmc-csv", default=None, help="rocprofv3 --pmc counter_collection.csv for roofline.traffic")
+    ap.add_argument("--pmc-csv", nargs="*", default=None,
+                    help="rocprofv3 --pmc counter_collection.csv file(s) with FETCH_SIZE / WRITE_SIZE for "
+                         "roofline.traffic (default: the committed profiles/round1 passes)")
     return ap.parse_args()
 
 
@@ -113,9 +116,9 @@ def main():
     # librsd's nodes are 4-wide (128 B per visit = two of SURVEY's 64-B BVH2 nodes)
     alg_bytes = rays * (16 + 8 + 4 * N) + 128 * cnt.nodes_visited + 48 * cnt.tris_tested
     achieved = alg_bytes / (sd_ms * 1e-3) / 1e9
-    traffic = None
-    if args.pmc_csv and Path(args.pmc_csv).exists():
-        traffic = pmc_traffic(args.pmc_csv, "sd_trace_kernel")
+    pmc = args.pmc_csv if args.pmc_csv is not None else [str(ROOT / "profiles" / "round1" / f)
+                                                          for f in ("pmc_fetch_size.csv", "pmc_write_size.csv")]
+    traffic = pmc_traffic([p for p in pmc if Path(p).exists()], SD_KERNELS)
 
     if rank != 0:
         if dist:
@@ -155,7 +158,9 @@ def main():
                       "tris_per_active_ray": round(cnt.tris_tested / max(cnt.rays_active, 1), 2)},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "kernel": "sd_trace_kernel", "alg_bytes_per_launch": int(alg_bytes)},
+                     "kernel": "+".join(SD_KERNELS), "alg_bytes_per_launch": int(alg_bytes),
+                     "traffic_source": ", ".join(str(Path(p).relative_to(ROOT)) if Path(p).is_relative_to(ROOT)
+                                                 else p for p in pmc if Path(p).exists()) or None},
         "cpu_baseline": cpu,
     }
     print(json.dumps(line))
@@ -163,22 +168,25 @@ def main():
         dist.destroy_process_group()
 
 
-def pmc_traffic(csv_path, kernel_substr):
-    """HBM bytes per launch from a rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE csv (KB units; FETCH_SIZE
-    doubled on gfx950 per MI355X_MICROARCH.md §HBM)."""
+def pmc_traffic(csv_paths, kernel_substrs):
+    """HBM bytes of one SD pass from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (KB units;
+    FETCH_SIZE doubled on gfx950 per MI355X_MICROARCH.md §HBM): per kernel, the mean over its
+    launches; summed over the kernels of the pass."""
     import csv
-    per = {}
-    with open(csv_path) as f:
-        for row in csv.DictReader(f):
-            if kernel_substr not in row.get("Kernel_Name", ""):
-                continue
-            name, val = row.get("Counter_Name"), float(row.get("Counter_Value", 0))
-            per.setdefault(name, []).append(val)
+    if not csv_paths:
+        return None
+    per = {}  # (kernel, counter) -> values
+    for path in csv_paths:
+        with open(path) as f:
+            for row in csv.DictReader(f):
+                k = next((s for s in kernel_substrs if s in row.get("Kernel_Name", "")), None)
+                if k is None:
+                    continue
+                per.setdefault((k, row.get("Counter_Name")), []).append(float(row.get("Counter_Value", 0)))
     if not per:
         return None
-    fetch = sum(per.get("FETCH_SIZE", [0])) / max(len(per.get("FETCH_SIZE", [1])), 1)
-    write = sum(per.get("WRITE_SIZE", [0])) / max(len(per.get("WRITE_SIZE", [1])), 1)
-    return int((2 * fetch + write) * 1024)
+    mean = lambda k, c: (sum(per[(k, c)]) / len(per[(k, c)])) if (k, c) in per else 0.0  # noqa: E731
+    return int(sum(2 * mean(k, "FETCH_SIZE") + mean(k, "WRITE_SIZE") for k in kernel_substrs) * 1024)
 
 
 def cpu_baseline(r, scene, target_s):

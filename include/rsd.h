@@ -160,6 +160,17 @@ rsd_status rsd_svao_make_vao_data(uint32_t fb_w, uint32_t fb_h, uint32_t divisor
 rsd_status rsd_gbuffer(rsd_scene* scene, const rsd_camera* cam, uint32_t width, uint32_t height,
                        uint32_t cull_mode, float* d_linear_z, uint16_t* d_normals, rsd_stream stream);
 
+/* The raster-style G-buffer of scripts/SVAO.py, for the render-graph host:
+ * GBufferRaster.depth (non-linear [0,1] depth, R32F) + GBufferRaster.faceNormalW (RGBA32F),
+ * LinearizeDepth (Linearize.ps.slang) and CompressNormals (CompressNormals.ps.slang,
+ * view space, 2x8 octahedral). */
+rsd_status rsd_gbuffer_raster(rsd_scene* scene, const rsd_camera* cam, uint32_t width, uint32_t height,
+                              uint32_t cull_mode, float* d_depth, float* d_normal_w, rsd_stream stream);
+rsd_status rsd_linearize_depth(const float* d_depth, float* d_linear_z, uint32_t count, float near_z, float far_z,
+                               rsd_stream stream);
+rsd_status rsd_compress_normals(const float* d_normal_w, uint16_t* d_packed, uint32_t count,
+                                const rsd_camera* cam, rsd_stream stream);
+
 /* StochasticDepthMapRT::execute (StochasticDepthMapRT.cpp:231-331) + rayGen/anyHit
  * (StochasticDepthMapRT.rt.slang:39-105).  d_sd_out layout = Texture2DArray:
  * [layer][y][x][ch], ch = min(N,4), layers = ceil(N/4).  d_ray_min / d_ray_max may be

@@ -1,0 +1,82 @@
+/* rsd_graph.h -- C ABI of the librsd render-graph host (csrc/host/graph.h).
+ *
+ * This is the surface a graph script binds (Falcor's Python RenderGraph API,
+ * RenderGraph.cpp / RenderGraphScripting): scripts/SVAO*.py call
+ *   RenderGraph(name)              -> rsd_graph_create        (RenderGraph.cpp:55 create)
+ *   g.create_pass(n, type, dict)   -> rsd_graph_create_pass   (RenderGraph.cpp:101 createPass)
+ *   g.add_edge(src, dst)           -> rsd_graph_add_edge      (RenderGraph.cpp:249 addEdge)
+ *   g.mark_output(name)            -> rsd_graph_mark_output   (RenderGraph.cpp:525 markOutput)
+ * and the application drives it with
+ *   setScene / compile / execute / getOutput / setInput
+ *                                  -> rsd_graph_set_scene / _compile / _execute / _get_output / _set_input
+ *                                     (RenderGraph.cpp:158, 336, 420, 470, 444)
+ * Pass types come from the plugin registry (Plugin.cpp:45-91): built-ins (GuardBand,
+ * GBufferRaster, LinearizeDepth, CompressNormals, StochasticDepthMapRT, SVAO), then
+ * dlopen("<plugin dir>/<Type>.so") with extern "C" registerPlugin, else a no-op stub.
+ * Properties travel as a flat JSON object ({"radius": 0.2, "cull": "Back", ...}).
+ *
+ * Every call returns rsd_status and never throws; rsd_last_error() has the message.
+ */
+#ifndef RSD_GRAPH_H
+#define RSD_GRAPH_H
+#include <stddef.h>
+#include <stdint.h>
+
+#include "rsd.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct rsd_graph rsd_graph;
+
+/* resource formats of graph textures (graph.h Format) */
+typedef enum {
+    RSD_FMT_R32F = 0, RSD_FMT_RG32F = 1, RSD_FMT_RGBA32F = 2, RSD_FMT_R16U = 3,
+    RSD_FMT_R8U = 4, RSD_FMT_R8UNORM = 5, RSD_FMT_R32U = 6, RSD_FMT_UNKNOWN = 7
+} rsd_format;
+
+typedef struct {
+    void* ptr;        /* device pointer, [layer][y][x][texel] */
+    uint32_t width, height, layers;
+    uint32_t format;  /* rsd_format */
+    uint64_t bytes;
+} rsd_texture;
+
+rsd_status rsd_graph_create(const char* name, rsd_graph** out);
+void rsd_graph_destroy(rsd_graph* g);
+rsd_status rsd_graph_create_pass(rsd_graph* g, const char* pass_name, const char* type, const char* props_json);
+rsd_status rsd_graph_add_edge(rsd_graph* g, const char* src, const char* dst);
+rsd_status rsd_graph_mark_output(rsd_graph* g, const char* name);
+/* scene + camera of the frame; call again with a new camera each frame (the camera is copied) */
+rsd_status rsd_graph_set_scene(rsd_graph* g, rsd_scene* scene, const rsd_camera* cam);
+/* external input bound to "pass.field" (caller-owned device memory) */
+rsd_status rsd_graph_set_input(rsd_graph* g, const char* name, const rsd_texture* tex);
+rsd_status rsd_graph_compile(rsd_graph* g, uint32_t width, uint32_t height, rsd_stream stream);
+rsd_status rsd_graph_execute(rsd_graph* g, rsd_stream stream);
+/* compile without device work: culling, execution order and the resource table only
+ * (RenderGraphCompiler.cpp:48-172); lets a script be validated on a host without a GPU */
+rsd_status rsd_graph_plan(rsd_graph* g, uint32_t width, uint32_t height);
+/* resource table of the last plan/compile: "pass.field width height layers format\n" lines */
+rsd_status rsd_graph_resources(const rsd_graph* g, char* buf, size_t cap, size_t* needed);
+/* "pass.field" of a compiled graph (graph-owned memory, valid until the next compile) */
+rsd_status rsd_graph_get_output(rsd_graph* g, const char* name, rsd_texture* out);
+/* device-to-device (or to host) copy of a graph resource, exactly its size in bytes */
+rsd_status rsd_graph_copy_output(rsd_graph* g, const char* name, void* dst, uint64_t bytes, rsd_stream stream);
+/* pass names in execution order, '\n'-separated; *needed receives the full length + 1 */
+rsd_status rsd_graph_execution_order(const rsd_graph* g, char* buf, size_t cap, size_t* needed);
+/* per-pass GPU time (ms) of the last execute, in execution order (synchronises the stream) */
+rsd_status rsd_graph_pass_times(rsd_graph* g, float* ms, uint32_t cap, uint32_t* count);
+/* graph dictionary entry (RenderData::getDictionary), e.g. "guardBand" */
+rsd_status rsd_graph_get_dict_int(const rsd_graph* g, const char* key, int64_t* out);
+rsd_status rsd_graph_pass_count(const rsd_graph* g, uint32_t* passes, uint32_t* edges);
+
+/* plugin registry */
+rsd_status rsd_plugin_set_dir(const char* dir);
+/* registered pass types, '\n'-separated */
+rsd_status rsd_plugin_types(char* buf, size_t cap, size_t* needed);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RSD_GRAPH_H */

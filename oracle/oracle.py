@@ -69,6 +69,9 @@ def lib():
         L.ocpu_scene_node_count.argtypes = [vp]
         L.ocpu_camera_look_at.argtypes = [vp, vp, vp, f32, f32, f32, f32, f32, f32, vp]
         L.ocpu_gbuffer.argtypes = [vp, vp, u32, u32, u32, vp, vp, i32]
+        L.ocpu_gbuffer_raster.argtypes = [vp, vp, u32, u32, u32, vp, vp, i32]
+        L.ocpu_linearize_depth.argtypes = [vp, vp, C.c_size_t, f32, f32]
+        L.ocpu_compress_normals.argtypes = [vp, vp, C.c_size_t, vp]
         L.ocpu_sd_trace.argtypes = [vp, vp, vp, vp, u32, u32, vp, vp, vp, u32, u32, u32, u32, i32, vp]
         L.ocpu_sd_ray.argtypes = [vp, vp, vp, u32, u32, vp, vp, u32, u32, u32, u32, vp, vp, vp, vp]
         L.ocpu_svao_clear.argtypes = [vp, vp, u32]
@@ -134,6 +137,28 @@ def gbuffer(scene: Scene, cam: Camera, W, H, cull_mode=1, threads=None):
     n = np.zeros((H, W), np.uint16)
     lib().ocpu_gbuffer(scene.h, C.byref(cam), W, H, cull_mode, _p(z), _p(n), _threads(threads))
     return z, n
+
+
+def gbuffer_raster(scene: Scene, cam: Camera, W, H, cull_mode=1, threads=None):
+    """GBufferRaster.depth (non-linear) and .faceNormalW (H, W, 4) -- the raster G-buffer."""
+    d = np.zeros((H, W), np.float32)
+    nw = np.zeros((H, W, 4), np.float32)
+    lib().ocpu_gbuffer_raster(scene.h, C.byref(cam), W, H, cull_mode, _p(d), _p(nw), _threads(threads))
+    return d, nw
+
+
+def linearize_depth(depth, near, far):
+    d = np.ascontiguousarray(depth, np.float32)
+    z = np.zeros_like(d)
+    lib().ocpu_linearize_depth(_p(d), _p(z), d.size, near, far)
+    return z
+
+
+def compress_normals(normal_w, cam: Camera):
+    nw = np.ascontiguousarray(normal_w, np.float32)
+    out = np.zeros(nw.shape[:-1], np.uint16)
+    lib().ocpu_compress_normals(_p(nw), _p(out), out.size, C.byref(cam))
+    return out
 
 
 def sd_trace(scene: Scene, cam: Camera, params: SDParams, linearZ, rayMin, rayMax, sdW, sdH,

@@ -537,6 +537,7 @@ static void o_collect(const oscene* s, const oray* r, float TMin, float TMax, ui
 typedef struct {
     const oscene* s; const ocam* c; uint32_t W, H, cull;
     float* z; uint16_t* n;
+    float* nw; /* raster mode (GBufferRaster): z = non-linear depth, nw = RGBA32F world face normal */
     uint32_t y0, y1;
 } ogb_job;
 
@@ -563,16 +564,31 @@ static void* o_gbuffer_rows(void* arg)
             o_collect(j->s, &r, tmin, tmax, j->cull, &hs);
             size_t o = (size_t)y * j->W + x;
             if (hs.n == 0) {
-                j->z[o] = c->farZ;
-                j->n[o] = 0;
+                if (j->nw) { /* cleared depth buffer / zero normal */
+                    j->z[o] = 1.0f;
+                    for (int k = 0; k < 4; ++k) j->nw[o * 4 + k] = 0.0f;
+                } else {
+                    j->z[o] = c->farZ;
+                    j->n[o] = 0;
+                }
             } else {
-                j->z[o] = hs.h[0].t * o_dot(wn, d);
+                const float zlin = hs.h[0].t * o_dot(wn, d);
                 const float* v = j->s->tri + (size_t)hs.h[0].prim * 9;
                 float e1[3] = {v[3] - v[0], v[4] - v[1], v[5] - v[2]};
                 float e2[3] = {v[6] - v[0], v[7] - v[1], v[8] - v[2]};
                 float cr[3], nw[3], nv[3];
                 o_cross(e1, e2, cr);
                 o_normalize(cr, nw);
+                if (j->nw) {
+                    /* D3D [0,1] depth of the right-handed perspective projection
+                     * (Camera.cpp:164 perspective(), depth range [0,1]): far (z - near) / (z (far - near)) */
+                    j->z[o] = c->farZ * (zlin - c->nearZ) / (zlin * (c->farZ - c->nearZ));
+                    j->nw[o * 4 + 0] = nw[0]; j->nw[o * 4 + 1] = nw[1]; j->nw[o * 4 + 2] = nw[2];
+                    j->nw[o * 4 + 3] = 0.0f;
+                    free(hs.h);
+                    continue;
+                }
+                j->z[o] = zlin;
                 const float* m = c->viewMat;
                 for (int k = 0; k < 3; ++k) nv[k] = m[k * 4 + 0] * nw[0] + m[k * 4 + 1] * nw[1] + m[k * 4 + 2] * nw[2];
                 j->n[o] = (uint16_t)ocpu_encode_normal_2x8(nv);
@@ -610,6 +626,37 @@ void ocpu_gbuffer(const oscene* s, const ocam* cam, uint32_t W, uint32_t H, uint
     }
     o_run_rows(o_gbuffer_rows, jobs, sizeof(ogb_job), 0, H, nthreads, o_gb_setrows);
     free(jobs);
+}
+
+void ocpu_gbuffer_raster(const oscene* s, const ocam* cam, uint32_t W, uint32_t H, uint32_t cull,
+                         float* depth, float* normalW, int nthreads)
+{
+    if (nthreads < 1) nthreads = 1;
+    ogb_job* jobs = (ogb_job*)calloc((size_t)nthreads, sizeof(ogb_job));
+    for (int i = 0; i < nthreads; ++i) {
+        jobs[i].s = s; jobs[i].c = cam; jobs[i].W = W; jobs[i].H = H; jobs[i].cull = cull;
+        jobs[i].z = depth; jobs[i].nw = normalW;
+    }
+    o_run_rows(o_gbuffer_rows, jobs, sizeof(ogb_job), 0, H, nthreads, o_gb_setrows);
+    free(jobs);
+}
+
+/* LinearizeDepth/Linearize.ps.slang:11-16 */
+void ocpu_linearize_depth(const float* d, float* z, size_t n, float zn, float zf)
+{
+    for (size_t i = 0; i < n; ++i) z[i] = zn * zf / (zf + d[i] * (zn - zf));
+}
+
+/* CompressNormals/CompressNormals.ps.slang:11-23 (viewSpace, use16Bit) */
+void ocpu_compress_normals(const float* nw, uint16_t* out, size_t n, const ocam* c)
+{
+    const float* m = c->viewMat;
+    for (size_t i = 0; i < n; ++i) {
+        const float* v = nw + i * 4;
+        float nv[3];
+        for (int k = 0; k < 3; ++k) nv[k] = m[k * 4 + 0] * v[0] + m[k * 4 + 1] * v[1] + m[k * 4 + 2] * v[2];
+        out[i] = (uint16_t)ocpu_encode_normal_2x8(nv);
+    }
 }
 
 /* ------------------------------------------------------------------ SD trace */

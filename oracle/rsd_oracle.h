@@ -29,6 +29,7 @@
  */
 #ifndef RSD_ORACLE_H
 #define RSD_ORACLE_H
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -99,6 +100,11 @@ void ocpu_camera_look_at(const float pos[3], const float target[3], const float 
 /* primary visibility: linear view depth (R32F) + view-space octahedral 2x8 normal (R16Uint) */
 void ocpu_gbuffer(const oscene* s, const ocam* cam, uint32_t W, uint32_t H, uint32_t cull_mode,
                   float* linearZ, uint16_t* normals, int nthreads);
+/* GBufferRaster.depth (non-linear [0,1], cleared 1) + faceNormalW (RGBA32F, cleared 0) */
+void ocpu_gbuffer_raster(const oscene* s, const ocam* cam, uint32_t W, uint32_t H, uint32_t cull_mode,
+                         float* depth, float* normalW, int nthreads);
+void ocpu_linearize_depth(const float* d, float* z, size_t n, float near_z, float far_z);
+void ocpu_compress_normals(const float* normalW, uint16_t* out, size_t n, const ocam* cam);
 
 /* SD trace for rows [row0,row1) of the SD map.  sd layout: [layer][y][x][ch],
  * ch = min(N,4), layers = ceil(N/4).  rayMin/rayMax may be NULL.

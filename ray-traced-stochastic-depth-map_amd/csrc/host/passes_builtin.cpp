@@ -1,0 +1,393 @@
+// passes_builtin.cpp -- the render passes of the SVAO graph that librsd implements, behind
+// the RenderPass interface of graph.h:
+//
+//   GuardBand             GuardBand.cpp:38-64        dict["guardBand"]
+//   GBufferRaster         GBufferRaster.cpp:86-230   depth + faceNormalW (rsd_gbuffer_raster)
+//   LinearizeDepth        LinearizeDepth.cpp:73-96   rsd_linearize_depth
+//   CompressNormals       CompressNormals.cpp:70-96  rsd_compress_normals (viewSpace, 16 bit)
+//   StochasticDepthMapRT  StochasticDepthMapRT.cpp   rsd_sd_trace            (the hot path)
+//   SVAO                  SVAO.cpp                   rsd_svao_* + a nested "Stochastic Depth"
+//                                                    graph holding StochasticDepthMapRT
+//
+// Every other pass type of the reference scripts (ToneMapper, TAA, CrossBilateralBlur, ...)
+// is outside the hot path; it resolves to a stub that declares whatever fields
+// the script connects and does no work, so the scripts build and run unchanged.
+#include <cmath>
+#include <cstdio>
+
+#include "graph.h"
+
+namespace rsd::host {
+namespace {
+
+void check(rsd_status st, const char* what) {
+    if (st != RSD_OK) throw std::runtime_error(std::string(what) + ": " + rsd_last_error());
+}
+
+// Falcor enums arrive from the scripts as their names ('Back', 'StochasticDepth', ...) or as numbers
+uint32_t enumProp(const Properties& p, const std::string& key, std::initializer_list<const char*> names,
+                  uint32_t def) {
+    if (!p.has(key)) return def;
+    auto& v = p.items().at(key);
+    if (auto s = std::get_if<std::string>(&v)) {
+        uint32_t i = 0;
+        for (const char* n : names) {
+            if (*s == n) return i;
+            ++i;
+        }
+        throw std::runtime_error("property '" + key + "': unknown value '" + *s + "'");
+    }
+    return (uint32_t)p.getInt(key, def);
+}
+
+const std::initializer_list<const char*> kCullNames = {"None", "Front", "Back"};  // RasterizerState::CullMode
+uint32_t toRsdCull(uint32_t falcorCull) {  // Falcor None/Front/Back -> RSD_CULL_NONE/FRONT/BACK
+    return falcorCull == 0 ? RSD_CULL_NONE : falcorCull == 1 ? RSD_CULL_FRONT : RSD_CULL_BACK;
+}
+const std::initializer_list<const char*> kDepthModeNames = {"SingleDepth", "DualDepth", "StochasticDepth",
+                                                            "Raytraced"};  // VAO/DepthMode.h
+const std::initializer_list<const char*> kImplNames = {"Default", "CoverageMask", "ReservoirSampling",
+                                                       "KBuffer"};  // StochasticDepthImplementation.h
+
+const SceneRef* requireScene(const SceneRef* s, const std::string& who) {
+    if (!s || !s->scene) throw std::runtime_error(who + ": no scene set");
+    return s;
+}
+
+// ------------------------------------------------------------------------------ stubs
+class StubPass : public RenderPass {
+public:
+    explicit StubPass(const Properties& p) { props_ = p; }
+    Reflection reflect(const CompileData&) override { return {}; }
+    void execute(Context&, const RenderData&) override {}
+    bool acceptsAnyField() const override { return true; }
+};
+
+// ------------------------------------------------------------------------------ GuardBand
+class GuardBandPass : public RenderPass {
+public:
+    explicit GuardBandPass(const Properties& p) {
+        props_ = p;
+        guard_ = (int)p.getInt("guardBand", 64);  // GuardBand.h:54
+    }
+    Reflection reflect(const CompileData&) override { return {}; }
+    void execute(Context&, const RenderData& rd) override {
+        // GuardBand.cpp:58-63 (the float2 uv bounds are not used by the hot path)
+        rd.getDictionary()["guardBand"] = (int64_t)guard_;
+    }
+
+private:
+    int guard_;
+};
+
+// ------------------------------------------------------------------------------ GBufferRaster
+class GBufferRasterPass : public RenderPass {
+public:
+    explicit GBufferRasterPass(const Properties& p) {
+        props_ = p;
+        // GBufferRaster.cpp:184: cull = forceCullMode ? cull : Back
+        const bool force = p.getBool("forceCullMode", false);
+        cull_ = force ? toRsdCull(enumProp(p, "cull", kCullNames, 2)) : RSD_CULL_BACK;
+    }
+    Reflection reflect(const CompileData&) override {
+        Reflection r;
+        r.addOutput("depth", "Depth buffer (D32 non-linear, R32F here)").format = Format::R32Float;
+        r.addOutput("faceNormalW", "Face normal in world space").format = Format::RGBA32Float;
+        return r;
+    }
+    void setScene(Context&, const SceneRef* s) override { scene_ = s; }
+    void execute(Context& ctx, const RenderData& rd) override {
+        if (!scene_) return;  // GBufferRaster.cpp:157 no scene -> outputs stay cleared
+        Texture* d = rd["depth"];
+        Texture* n = rd["faceNormalW"];
+        check(rsd_gbuffer_raster(scene_->scene, &scene_->camera, d->width, d->height, cull_, (float*)d->ptr,
+                                 (float*)n->ptr, ctx.stream),
+              "GBufferRaster");
+    }
+    // further channels (posW, normW, mvec, ...) feed passes outside the hot path
+    bool acceptsAnyField() const override { return true; }
+
+private:
+    const SceneRef* scene_ = nullptr;
+    uint32_t cull_;
+};
+
+// ------------------------------------------------------------------------------ LinearizeDepth
+class LinearizeDepthPass : public RenderPass {
+public:
+    explicit LinearizeDepthPass(const Properties& p) {
+        props_ = p;
+        const std::string fmt = p.getString("depthFormat", "R32Float");
+        if (fmt != "R32Float") throw Unsupported("LinearizeDepth: only depthFormat R32Float is implemented");
+    }
+    Reflection reflect(const CompileData&) override {
+        Reflection r;
+        r.addInput("depth", "non-linear depth").format = Format::R32Float;
+        r.addOutput("linearDepth", "linear view-depth").format = Format::R32Float;
+        return r;
+    }
+    void setScene(Context&, const SceneRef* s) override { scene_ = s; }
+    void execute(Context& ctx, const RenderData& rd) override {
+        if (!scene_) return;
+        Texture* in = rd["depth"];
+        Texture* out = rd["linearDepth"];
+        if (in->format != Format::R32Float || in->width != out->width || in->height != out->height)
+            throw std::runtime_error("LinearizeDepth: input must be R32Float at the output size");
+        check(rsd_linearize_depth((const float*)in->ptr, (float*)out->ptr, out->width * out->height,
+                                  scene_->camera.nearZ, scene_->camera.farZ, ctx.stream),
+              "LinearizeDepth");
+    }
+
+private:
+    const SceneRef* scene_ = nullptr;
+};
+
+// ------------------------------------------------------------------------------ CompressNormals
+class CompressNormalsPass : public RenderPass {
+public:
+    explicit CompressNormalsPass(const Properties& p) {
+        props_ = p;
+        if (!p.getBool("viewSpace", true) || !p.getBool("use16Bit", true))
+            throw Unsupported("CompressNormals: only viewSpace = True, use16Bit = True is implemented");
+    }
+    Reflection reflect(const CompileData&) override {
+        Reflection r;
+        r.addInput("normalW", "World Space Normals").format = Format::RGBA32Float;
+        r.addOutput("normalOut", "Compressed Normals (Octa mapping)").format = Format::R16Uint;
+        return r;
+    }
+    void setScene(Context&, const SceneRef* s) override { scene_ = s; }
+    void execute(Context& ctx, const RenderData& rd) override {
+        if (!scene_) return;
+        Texture* in = rd["normalW"];
+        Texture* out = rd["normalOut"];
+        if (in->format != Format::RGBA32Float || in->width != out->width || in->height != out->height)
+            throw std::runtime_error("CompressNormals: input must be RGBA32Float at the output size");
+        check(rsd_compress_normals((const float*)in->ptr, (uint16_t*)out->ptr, out->width * out->height,
+                                   &scene_->camera, ctx.stream),
+              "CompressNormals");
+    }
+
+private:
+    const SceneRef* scene_ = nullptr;
+};
+
+// ------------------------------------------------------------------------------ StochasticDepthMapRT
+// StochasticDepthMapRT.cpp:135-155 Properties, :190-216 reflect, :231-331 execute.
+class StochasticDepthMapRTPass : public RenderPass {
+public:
+    explicit StochasticDepthMapRTPass(const Properties& p) {
+        props_ = p;
+        prm_.sample_count = (uint32_t)p.getInt("SampleCount", 4);
+        prm_.cull_mode = toRsdCull(enumProp(p, "CullMode", kCullNames, 2));
+        prm_.normalize = p.getBool("normalize", true);
+        prm_.alpha_test = p.getBool("AlphaTest", true);
+        prm_.jitter = p.getBool("Jitter", false);
+        prm_.implementation = enumProp(p, "Implementation", kImplNames, 0);
+        prm_.alpha = (float)p.getFloat("Alpha", 0.2);
+        prm_.ray_interval = p.getBool("RayInterval", true);
+        prm_.guard_band = (int32_t)p.getInt("GuardBand", 0);
+        prm_.max_count = (uint32_t)p.getInt("MaxCount", 8);
+        if (p.getBool("StoreNormals", false))  // StochasticDepthMapRT.cpp:198-203
+            throw Unsupported("StochasticDepthMapRT: Storing normals is not supported yet");
+        if (p.getBool("useRayPipeline", true) == false)
+            throw Unsupported("StochasticDepthMapRT: the raster variant is not part of librsd");
+    }
+    Reflection reflect(const CompileData&) override {
+        const uint32_t N = prm_.sample_count;
+        Reflection r;
+        r.addInput("linearZ", "non-linear (primary) depth map").format = Format::R32Float;
+        auto& st = r.addInput("stencilMask", "(optional) stencil-mask");
+        st.format = Format::R8Uint;
+        st.optional = true;
+        r.addInput("rayMin", "min ray T distance for depth values").optional = true;
+        r.addInput("rayMax", "max ray T distance for depth values").optional = true;
+        auto& o = r.addOutput("stochasticDepth", "stochastic depths in [0,1]");
+        // [layer][y][x][min(N,4)] f32 (the reference stores 16-bit floats for N <= 4 with Use16Bit)
+        o.format = N == 1 ? Format::R32Float : N == 2 ? Format::RG32Float : Format::RGBA32Float;
+        o.layers = (N + 3) / 4;
+        return r;
+    }
+    void setScene(Context&, const SceneRef* s) override { scene_ = s; }
+    void execute(Context& ctx, const RenderData& rd) override {
+        if (!scene_) return;  // StochasticDepthMapRT.cpp:233
+        Texture* z = rd["linearZ"];
+        Texture* sd = rd["stochasticDepth"];
+        Texture* rmin = rd["rayMin"];
+        Texture* rmax = rd["rayMax"];
+        auto& dict = rd.getDictionary();
+        auto it = dict.find("SD_CLEAR");
+        if (it != dict.end() && std::holds_alternative<bool>(it->second) && std::get<bool>(it->second))
+            if (hipMemsetAsync(sd->ptr, 0, sd->bytes(), ctx.stream) != hipSuccess)
+                throw std::runtime_error("StochasticDepthMapRT: clear failed");
+        check(rsd_sd_trace(scene_->scene, &scene_->camera, &prm_, (const float*)z->ptr, z->width, z->height,
+                           rmin ? (const uint32_t*)rmin->ptr : nullptr, rmax ? (const uint32_t*)rmax->ptr : nullptr,
+                           (float*)sd->ptr, sd->width, sd->height, nullptr, ctx.stream),
+              "StochasticDepthMapRT");
+    }
+    const rsd_sd_params& params() const { return prm_; }
+
+private:
+    const SceneRef* scene_ = nullptr;
+    rsd_sd_params prm_{};
+};
+
+// ------------------------------------------------------------------------------ SVAO
+// SVAO.cpp:73-100 Properties, :117-140 reflect, :143-190 compile (nested SD graph),
+// :192-455 execute.  Members the reference sets only from its GUI (SVAO.h:90-126) are
+// accepted as extra Properties with the same defaults: stochSamples, stochMaxCount,
+// stochGuardBand, stochJitter, rayInterval, cullMode, sampleCount, stochImplementation.
+class SVAOPass : public RenderPass {
+public:
+    explicit SVAOPass(const Properties& p) {
+        props_ = p;
+        radius_ = (float)p.getFloat("radius", 1.0);
+        exponent_ = (float)p.getFloat("exponent", 1.0);
+        thickness_ = (float)p.getFloat("thickness", 0.0);
+        primary_ = enumProp(p, "primaryDepthMode", kDepthModeNames, 0);
+        secondary_ = enumProp(p, "secondaryDepthMode", kDepthModeNames, 2);
+        divisor_ = (uint32_t)p.getInt("stochMapDivisor", 1);
+        dualAo_ = p.getBool("dualAO", false);
+        alphaTest_ = p.getBool("alphaTest", true);
+        samples_ = (uint32_t)p.getInt("stochSamples", 4);
+        maxCount_ = (uint32_t)p.getInt("stochMaxCount", 8);
+        guardPx_ = (int32_t)p.getInt("stochGuardBand", 512);
+        jitter_ = p.getBool("stochJitter", true);
+        rayInterval_ = p.getBool("rayInterval", true);
+        cull_ = toRsdCull(enumProp(p, "cullMode", kCullNames, 2));
+        directions_ = (uint32_t)p.getInt("sampleCount", 8);
+        impl_ = enumProp(p, "stochImplementation", kImplNames, 0);
+    }
+    void checkSupported() const {
+        if (primary_ != 0) throw Unsupported("SVAO: primaryDepthMode other than SingleDepth is not implemented");
+        if (secondary_ != 0 && secondary_ != 2)
+            throw Unsupported("SVAO: secondaryDepthMode DualDepth/Raytraced is not implemented (SURVEY 8(f))");
+        if (dualAo_) throw Unsupported("SVAO: dualAO is not implemented");
+    }
+    void sdSize(uint32_t w, uint32_t h, rsd_vao_data* vao, uint32_t* sw, uint32_t* sh) const {
+        check(rsd_svao_make_vao_data(w, h, divisor_, guardPx_, radius_, exponent_, thickness_, vao, sw, sh), "SVAO");
+    }
+    Reflection reflect(const CompileData& cd) override {
+        checkSupported();  // reported when the graph is planned, before any device work
+        rsd_vao_data vao;
+        uint32_t sw = 1, sh = 1;
+        if (cd.defaultWidth && cd.defaultHeight) sdSize(cd.defaultWidth, cd.defaultHeight, &vao, &sw, &sh);
+        Reflection r;
+        auto opt = [&](const char* n, const char* d) { r.addInput(n, d).optional = true; };
+        opt("gbufferDepth", "Non-Linear Depth from the G-Buffer");
+        r.addInput("depth", "Linear Depth-buffer").format = Format::R32Float;
+        opt("depth2", "Linear Depth-buffer of second layer");
+        r.addInput("normals", "View space normals, 2x8 octahedral").format = Format::R16Uint;
+        opt("color", "Color for pixel importance");
+        r.addOutput("ao", "Ambient Occlusion").format = Format::R8Unorm;
+        // NUM_DIRECTIONS = 8 -> R8Uint (SVAO.cpp:132-135)
+        r.addOutput("stencil", "Stencil Bitmask for primary / secondary ao").format = Format::R8Uint;
+        for (const char* n : {"internalRayMin", "internalRayMax"}) {
+            auto& f = r.addOutput(n, n[8] == 'M' && n[10] == 'n' ? "internal ray min" : "internal ray max");
+            f.format = Format::R32Uint;  // R32Int in the reference; the bit patterns are non-negative floats
+            f.width = sw;
+            f.height = sh;
+        }
+        return r;
+    }
+    void setScene(Context& ctx, const SceneRef* s) override {
+        scene_ = s;
+        if (sdGraph_) sdGraph_->setScene(ctx, s);
+    }
+    void compile(Context& ctx, const CompileData& cd) override {
+        checkSupported();
+        width_ = cd.defaultWidth;
+        height_ = cd.defaultHeight;
+        sdSize(width_, height_, &vao_, &sdW_, &sdH_);
+        svp_ = rsd_svao_params{directions_, samples_, secondary_, (uint32_t)rayInterval_, (uint32_t)jitter_, 0};
+        sdGraph_.reset();
+        if (secondary_ != 2) return;
+        // SVAO.cpp:157-189: the nested "Stochastic Depth" graph
+        Properties sd;
+        sd.set("SampleCount", (int64_t)samples_);
+        sd.set("AlphaTest", alphaTest_);
+        sd.set("Implementation", (int64_t)impl_);
+        sd.set("Alpha", (double)(float)(1.5 / samples_));
+        sd.set("RayInterval", rayInterval_);
+        sd.set("CullMode", std::string(cull_ == RSD_CULL_NONE ? "None" : cull_ == RSD_CULL_FRONT ? "Front" : "Back"));
+        sd.set("normalize", true);
+        sd.set("StoreNormals", false);
+        sd.set("Jitter", jitter_);
+        sd.set("GuardBand", (int64_t)vao_.sdGuard);
+        sd.set("MaxCount", (int64_t)maxCount_);
+        sdGraph_ = std::make_unique<RenderGraph>("Stochastic Depth");
+        sdGraph_->createPass("StochasticDepthMap", "StochasticDepthMapRT", sd);
+        sdGraph_->markOutput("StochasticDepthMap.stochasticDepth");
+        sdGraph_->setScene(ctx, scene_);
+        sdGraph_->compile(ctx, sdW_, sdH_);
+    }
+    void execute(Context& ctx, const RenderData& rd) override {
+        if (!scene_) return;  // SVAO.cpp:194
+        const SceneRef* s = requireScene(scene_, "SVAO");
+        Texture* depth = rd["depth"];
+        Texture* normals = rd["normals"];
+        Texture* ao = rd["ao"];
+        Texture* stencil = rd["stencil"];
+        Texture* rmin = rd["internalRayMin"];
+        Texture* rmax = rd["internalRayMax"];
+        if (depth->width != width_ || depth->height != height_ || normals->width != width_ ||
+            normals->height != height_ || depth->format != Format::R32Float || normals->format != Format::R16Uint)
+            throw std::runtime_error("SVAO: depth (R32Float) and normals (R16Uint) must match the frame size");
+        // SVAO.cpp:326: the guard band comes from the GuardBand pass through the dictionary
+        auto& dict = rd.getDictionary();
+        int64_t guard = 0;
+        if (auto it = dict.find("guardBand"); it != dict.end() && std::holds_alternative<int64_t>(it->second))
+            guard = std::get<int64_t>(it->second);
+        svp_.guard_band = (uint32_t)guard;
+        if (secondary_ == 2)  // SVAO.cpp:330-341
+            check(rsd_svao_clear_intervals((uint32_t*)rmin->ptr, (uint32_t*)rmax->ptr, sdW_ * sdH_, ctx.stream),
+                  "SVAO clear");
+        check(rsd_svao_pass1(&s->camera, &vao_, &svp_, (const float*)depth->ptr, (const uint16_t*)normals->ptr,
+                             width_, height_, (uint8_t*)ao->ptr, (uint8_t*)stencil->ptr, (uint32_t*)rmin->ptr,
+                             (uint32_t*)rmax->ptr, sdW_, sdH_, ctx.stream),
+              "SVAO AO 1");
+        if (secondary_ == 0) return;  // SVAO.cpp:355
+        // SVAO.cpp:364-390: the nested graph traces the stochastic depth map
+        sdGraph_->setInput("StochasticDepthMap.linearZ", depth);
+        sdGraph_->setInput("StochasticDepthMap.rayMin", rmin);
+        sdGraph_->setInput("StochasticDepthMap.rayMax", rmax);
+        sdGraph_->dictionary()["SD_CLEAR"] = false;
+        sdGraph_->execute(ctx);
+        Texture* sd = sdGraph_->getOutput("StochasticDepthMap.stochasticDepth");
+        check(rsd_svao_pass2(&s->camera, &vao_, &svp_, (const float*)depth->ptr, (const uint16_t*)normals->ptr,
+                             width_, height_, (const uint8_t*)stencil->ptr, (const float*)sd->ptr, sdW_, sdH_,
+                             (uint8_t*)ao->ptr, ctx.stream),
+              "SVAO AO 2");
+    }
+    RenderGraph* stochasticDepthGraph() { return sdGraph_.get(); }
+
+private:
+    const SceneRef* scene_ = nullptr;
+    float radius_, exponent_, thickness_;
+    uint32_t primary_, secondary_, divisor_, samples_, maxCount_, cull_, directions_, impl_;
+    int32_t guardPx_;
+    bool dualAo_, alphaTest_, jitter_, rayInterval_;
+    uint32_t width_ = 0, height_ = 0, sdW_ = 0, sdH_ = 0;
+    rsd_vao_data vao_{};
+    rsd_svao_params svp_{};
+    std::unique_ptr<RenderGraph> sdGraph_;
+};
+
+template <class T>
+PluginRegistry::Factory factory() {
+    return [](const Properties& p) { return std::unique_ptr<RenderPass>(new T(p)); };
+}
+
+}  // namespace
+
+void registerBuiltinPasses(PluginRegistry& r) {
+    r.registerClass("__Stub", "pass outside the librsd hot path (no work)", factory<StubPass>());
+    r.registerClass("GuardBand", "guard band size into the graph dictionary", factory<GuardBandPass>());
+    r.registerClass("GBufferRaster", "depth + face normal G-buffer", factory<GBufferRasterPass>());
+    r.registerClass("LinearizeDepth", "non-linear -> linear view depth", factory<LinearizeDepthPass>());
+    r.registerClass("CompressNormals", "view-space 2x8 octahedral normals", factory<CompressNormalsPass>());
+    r.registerClass("StochasticDepthMapRT", "ray-traced stochastic depth map", factory<StochasticDepthMapRTPass>());
+    r.registerClass("SVAO", "stochastic-depth volumetric ambient occlusion", factory<SVAOPass>());
+}
+
+}  // namespace rsd::host

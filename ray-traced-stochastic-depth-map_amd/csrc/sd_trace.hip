@@ -691,6 +691,7 @@ struct GBArgs {
     uint32_t cull;
     float* z;
     uint16_t* n;
+    float4* nw;  // raster mode: world face normal (RGBA32F); z then holds non-linear depth
 };
 
 __global__ void __launch_bounds__(kBlock) gbuffer_kernel(GBArgs a) {
@@ -714,16 +715,28 @@ __global__ void __launch_bounds__(kBlock) gbuffer_kernel(GBArgs a) {
                                         0.0f, 0u, kl, &sstack[lane], &sstackT[lane], st);
     const size_t o = (size_t)y * a.W + x;
     if (!found) {
-        a.z[o] = c.farZ;
-        a.n[o] = 0;
+        if (a.nw) {
+            a.z[o] = 1.0f;  // cleared depth
+            a.nw[o] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        } else {
+            a.z[o] = c.farZ;
+            a.n[o] = 0;
+        }
         return;
     }
-    a.z[o] = kl.t[0] * cosT;
+    const float zlin = kl.t[0] * cosT;
     const uint32_t ti = kl.l[0];
     const float4 v0 = a.tris[3 * ti], v1 = a.tris[3 * ti + 1], v2 = a.tris[3 * ti + 2];
     const f3 e1 = mk(v1.x - v0.x, v1.y - v0.y, v1.z - v0.z);
     const f3 e2 = mk(v2.x - v0.x, v2.y - v0.y, v2.z - v0.z);
     const f3 nw = normalize(cross(e1, e2));
+    if (a.nw) {
+        // D3D-style [0,1] depth of a right-handed perspective: far (z - near) / (z (far - near))
+        a.z[o] = c.farZ * (zlin - c.nearZ) / (zlin * (c.farZ - c.nearZ));
+        a.nw[o] = make_float4(nw.x, nw.y, nw.z, 0.0f);
+        return;
+    }
+    a.z[o] = zlin;
     const float* m = c.viewMat;
     const f3 nv = mk(m[0] * nw.x + m[1] * nw.y + m[2] * nw.z, m[4] * nw.x + m[5] * nw.y + m[6] * nw.z,
                      m[8] * nw.x + m[9] * nw.y + m[10] * nw.z);
@@ -945,10 +958,33 @@ extern "C" rsd_status rsd_gbuffer(rsd_scene* scene, const rsd_camera* cam, uint3
         RSD_HIP(hipStreamSynchronize(s));
         return RSD_OK;
     }
-    GBArgs a{scene->d_nodes, scene->d_tris, scene->tri_offset, *cam, (int)width, (int)height, cull_mode, d_linear_z, d_normals};
+    GBArgs a{scene->d_nodes, scene->d_tris, scene->tri_offset, *cam, (int)width, (int)height, cull_mode, d_linear_z,
+             d_normals, nullptr};
     dim3 grid((width + kTile - 1) / kTile, (height + kTile - 1) / kTile);
     hipLaunchKernelGGL(gbuffer_kernel, grid, dim3(kBlock), 0, s, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(e, "gbuffer_kernel launch");
     return RSD_OK;
+}
+
+extern "C" rsd_status rsd_gbuffer_raster(rsd_scene* scene, const rsd_camera* cam, uint32_t width, uint32_t height,
+                                         uint32_t cull_mode, float* d_depth, float* d_normal_w, rsd_stream stream) {
+    if (!scene || !cam || !d_depth || !d_normal_w || width == 0 || height == 0 || cull_mode > 2) {
+        set_error("rsd_gbuffer_raster: invalid argument");
+        return RSD_ERR_INVALID_ARG;
+    }
+    hipStream_t s = (hipStream_t)stream;
+    if (scene->triangle_count == 0) {
+        std::vector<float> z((size_t)width * height, 1.0f);
+        RSD_HIP(hipMemcpyAsync(d_depth, z.data(), z.size() * 4, hipMemcpyHostToDevice, s));
+        RSD_HIP(hipMemsetAsync(d_normal_w, 0, (size_t)width * height * 16, s));
+        RSD_HIP(hipStreamSynchronize(s));
+        return RSD_OK;
+    }
+    GBArgs a{scene->d_nodes, scene->d_tris, scene->tri_offset, *cam, (int)width, (int)height, cull_mode, d_depth,
+             nullptr, reinterpret_cast<float4*>(d_normal_w)};
+    dim3 grid((width + kTile - 1) / kTile, (height + kTile - 1) / kTile);
+    hipLaunchKernelGGL(gbuffer_kernel, grid, dim3(kBlock), 0, s, a);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? RSD_OK : hip_fail(e, "gbuffer_kernel launch");
 }

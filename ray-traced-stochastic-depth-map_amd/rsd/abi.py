@@ -75,7 +75,22 @@ class Counters(C.Structure):
 EXPORTS = ["rsd_abi_version", "rsd_last_error", "rsd_device_open", "rsd_device_close", "rsd_scene_upload",
            "rsd_scene_info_get", "rsd_scene_release", "rsd_camera_look_at", "rsd_svao_make_vao_data",
            "rsd_gbuffer", "rsd_sd_trace", "rsd_svao_clear_intervals", "rsd_svao_pass1", "rsd_svao_pass2",
-           "rsd_sd_trace_band", "rsd_svao_pass1_band", "rsd_svao_pass2_band"]
+           "rsd_sd_trace_band", "rsd_svao_pass1_band", "rsd_svao_pass2_band", "rsd_gbuffer_raster",
+           "rsd_linearize_depth", "rsd_compress_normals"]
+
+# every symbol include/rsd_graph.h declares
+GRAPH_EXPORTS = ["rsd_graph_create", "rsd_graph_destroy", "rsd_graph_create_pass", "rsd_graph_add_edge",
+                 "rsd_graph_mark_output", "rsd_graph_set_scene", "rsd_graph_set_input", "rsd_graph_compile",
+                 "rsd_graph_execute", "rsd_graph_plan", "rsd_graph_resources", "rsd_graph_get_output",
+                 "rsd_graph_copy_output", "rsd_graph_execution_order", "rsd_graph_pass_times",
+                 "rsd_graph_get_dict_int", "rsd_graph_pass_count", "rsd_plugin_set_dir", "rsd_plugin_types"]
+
+FMT_R32F, FMT_RG32F, FMT_RGBA32F, FMT_R16U, FMT_R8U, FMT_R8UNORM, FMT_R32U, FMT_UNKNOWN = range(8)
+
+
+class Texture(C.Structure):
+    _fields_ = [("ptr", C.c_void_p), ("width", C.c_uint32), ("height", C.c_uint32), ("layers", C.c_uint32),
+                ("format", C.c_uint32), ("bytes", C.c_uint64)]
 
 _lib = None
 
@@ -87,7 +102,7 @@ def lib():
         if not LIB_PATH.exists():
             raise RuntimeError(f"librsd.so not found at {LIB_PATH}: build it with `make -C {PKG_DIR}` "
                                "(or __graft_entry__.build()); there is no CPU fallback")
-        L = C.CDLL(str(LIB_PATH))
+        L = C.CDLL(str(LIB_PATH), mode=C.RTLD_GLOBAL)  # global: render-pass plugins resolve the host's symbols
         vp, u32, i32, f32, st = C.c_void_p, C.c_uint32, C.c_int32, C.c_float, C.c_int
         L.rsd_abi_version.restype = u32
         L.rsd_last_error.restype = C.c_char_p
@@ -126,6 +141,38 @@ def lib():
         L.rsd_svao_pass2_band.restype = st
         L.rsd_svao_pass2_band.argtypes = [C.POINTER(Camera), C.POINTER(VAOData), C.POINTER(SVAOParams), vp, vp, u32,
                                           u32, vp, vp, u32, u32, vp, u32, u32, vp]
+        L.rsd_gbuffer_raster.restype = st
+        L.rsd_gbuffer_raster.argtypes = [vp, C.POINTER(Camera), u32, u32, u32, vp, vp, vp]
+        L.rsd_linearize_depth.restype = st
+        L.rsd_linearize_depth.argtypes = [vp, vp, u32, f32, f32, vp]
+        L.rsd_compress_normals.restype = st
+        L.rsd_compress_normals.argtypes = [vp, vp, u32, C.POINTER(Camera), vp]
+        cs, sz, tp = C.c_char_p, C.c_size_t, C.POINTER(Texture)
+        for name, args in {
+            "rsd_graph_create": [cs, C.POINTER(vp)],
+            "rsd_graph_create_pass": [vp, cs, cs, cs],
+            "rsd_graph_add_edge": [vp, cs, cs],
+            "rsd_graph_mark_output": [vp, cs],
+            "rsd_graph_set_scene": [vp, vp, C.POINTER(Camera)],
+            "rsd_graph_set_input": [vp, cs, tp],
+            "rsd_graph_compile": [vp, u32, u32, vp],
+            "rsd_graph_execute": [vp, vp],
+            "rsd_graph_plan": [vp, u32, u32],
+            "rsd_graph_resources": [vp, vp, sz, C.POINTER(sz)],
+            "rsd_graph_get_output": [vp, cs, tp],
+            "rsd_graph_copy_output": [vp, cs, vp, C.c_uint64, vp],
+            "rsd_graph_execution_order": [vp, vp, sz, C.POINTER(sz)],
+            "rsd_graph_pass_times": [vp, C.POINTER(f32), u32, C.POINTER(u32)],
+            "rsd_graph_get_dict_int": [vp, cs, C.POINTER(C.c_int64)],
+            "rsd_graph_pass_count": [vp, C.POINTER(u32), C.POINTER(u32)],
+            "rsd_plugin_set_dir": [cs],
+            "rsd_plugin_types": [vp, sz, C.POINTER(sz)],
+        }.items():
+            fn = getattr(L, name)
+            fn.restype = st
+            fn.argtypes = args
+        L.rsd_graph_destroy.restype = None
+        L.rsd_graph_destroy.argtypes = [vp]
         _lib = L
     return _lib
 

@@ -46,8 +46,8 @@ def test_library_exports_every_header_symbol(abi):
 def test_struct_layouts_match_header(abi, tmp_path):
     structs = {"rsd_scene_desc": abi.SceneDesc, "rsd_scene_info": abi.SceneInfo, "rsd_camera": abi.Camera,
                "rsd_sd_params": abi.SDParams, "rsd_vao_data": abi.VAOData, "rsd_svao_params": abi.SVAOParams,
-               "rsd_counters": abi.Counters}
-    src = "#include <stdio.h>\n#include \"rsd.h\"\nint main(void){\n"
+               "rsd_counters": abi.Counters, "rsd_texture": abi.Texture}
+    src = "#include <stdio.h>\n#include \"rsd_graph.h\"\nint main(void){\n"
     for name in structs:
         src += f'printf("%zu\\n", sizeof({name}));\n'
     src += "return 0;}\n"

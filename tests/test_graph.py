@@ -1,0 +1,177 @@
+"""The render-graph host (include/rsd_graph.h, csrc/host/) on the CPU: script loading,
+the plugin registry, graph planning (culling, execution order, resource table) and error
+behaviour.  No device work: graphs are planned, not compiled (rsd_graph_plan)."""
+import os
+import subprocess
+from pathlib import Path
+
+import pytest
+
+from conftest import PKG as PKG_DIR, ROOT
+
+rsdgraph = pytest.importorskip("rsd.graph")
+from rsd import abi  # noqa: E402
+
+SCRIPT = ROOT / "tests" / "graphs" / "svao_hotpath.py"
+REF_SCRIPTS = Path("/root/reference/scripts")
+FB = (192, 128)  # visible 160 x 96 + 2 x 16 guard band
+
+
+def hotpath():
+    return rsdgraph.load_script(SCRIPT)["SVAOHotPath"]
+
+
+def test_builtin_pass_types():
+    assert {"GuardBand", "GBufferRaster", "LinearizeDepth", "CompressNormals", "StochasticDepthMapRT",
+            "SVAO"} <= set(rsdgraph.plugin_types())
+
+
+def test_script_load_and_plan():
+    g = hotpath()
+    assert g.counts() == (7, 8)
+    g.plan(*FB)
+    # the ToneMapper stub feeds no output and is culled (RenderGraphCompiler.cpp:121-172)
+    assert g.execution_order() == ["GuardBand", "GBufferRaster", "LinearizeDepth", "CompressNormals", "SVAO",
+                                   "Blur"]
+    res = g.resources()
+    assert res["GBufferRaster.depth"] == (FB[0], FB[1], 1, "R32Float")
+    assert res["GBufferRaster.faceNormalW"] == (FB[0], FB[1], 1, "RGBA32Float")
+    assert res["LinearizeDepth.linearDepth"] == (FB[0], FB[1], 1, "R32Float")
+    assert res["CompressNormals.normalOut"] == (FB[0], FB[1], 1, "R16Uint")
+    assert res["SVAO.ao"] == (FB[0], FB[1], 1, "R8Unorm")
+    assert res["SVAO.stencil"] == (FB[0], FB[1], 1, "R8Uint")
+    # SD map = ceil(fb / divisor) + 2 * (64 px guard / divisor)   (SVAO.cpp:700-723)
+    sd = ((FB[0] + 1) // 2 + 64, (FB[1] + 1) // 2 + 64)
+    assert res["SVAO.internalRayMin"] == (sd[0], sd[1], 1, "R32Uint")
+    assert res["SVAO.internalRayMax"] == (sd[0], sd[1], 1, "R32Uint")
+    # a stub output takes the format the consumer does not constrain: RGBA32F
+    assert res["Blur.colorOut"][3] == "RGBA32Float"
+    assert "Unused.dst" not in res
+
+
+def test_script_as_code_through_falcor_module():
+    ns = {}
+    exec(compile(SCRIPT.read_text(), str(SCRIPT), "exec"), ns)  # our own script
+    g = ns["SVAOHotPath"]
+    assert g.counts() == (7, 8)
+    assert type(g).__module__ == "rsd.graph"
+
+
+@pytest.mark.skipif(not REF_SCRIPTS.is_dir(), reason="reference scripts not present (GPU box)")
+@pytest.mark.parametrize("name", ["SVAO.py", "SVAO_small.py", "SVAO_debugsd.py"])
+def test_reference_svao_scripts_plan(name):
+    """The reference's SVAO graphs load unchanged (read, not executed) and plan."""
+    graphs = rsdgraph.load_script(REF_SCRIPTS / name)
+    g = graphs["SVAO"]
+    g.plan(1920 + 128, 1080 + 128)
+    order = g.execution_order()
+    for p in ("GuardBand", "GBufferRaster", "LinearizeDepth", "CompressNormals", "SVAO"):
+        assert p in order
+    assert order.index("GuardBand") < order.index("GBufferRaster") < order.index("LinearizeDepth") < \
+        order.index("SVAO")
+    assert order.index("CompressNormals") < order.index("SVAO")
+    res = g.resources()
+    assert res["SVAO.internalRayMax"][:2] == (768, 558)  # 1080p, divisor 4, 512 px SD guard band
+
+
+@pytest.mark.skipif(not REF_SCRIPTS.is_dir(), reason="reference scripts not present (GPU box)")
+@pytest.mark.parametrize("name", ["SVAO_depth.py", "SAVO_record.py"])
+def test_reference_raytraced_svao_is_reported_unsupported(name):
+    g = next(iter(rsdgraph.load_script(REF_SCRIPTS / name).values()))
+    with pytest.raises(abi.RsdError) as e:
+        g.plan(1920 + 128, 1080 + 128)
+    assert e.value.status == 2 and "not implemented" in str(e.value)
+
+
+def test_graph_errors():
+    g = rsdgraph.RenderGraph("errors")
+    g.create_pass("A", "LinearizeDepth", {})
+    with pytest.raises(abi.RsdError, match="exists"):
+        g.create_pass("A", "LinearizeDepth", {})
+    with pytest.raises(abi.RsdError, match="unknown pass"):
+        g.add_edge("A.linearDepth", "B.depth")
+    with pytest.raises(abi.RsdError, match="pass.field"):
+        g.mark_output("A")
+    # required input not connected
+    g.mark_output("A.linearDepth")
+    with pytest.raises(abi.RsdError, match="required input 'A.depth'"):
+        g.plan(64, 64)
+    # edges to a field a built-in pass does not declare
+    g.create_pass("B", "LinearizeDepth", {})
+    g.add_edge("B.linearDepth", "A.notAField")
+    with pytest.raises(abi.RsdError, match="no input 'notAField'"):
+        g.plan(64, 64)
+
+
+def test_graph_cycle():
+    g = rsdgraph.RenderGraph("cycle")
+    g.create_pass("A", "Foo", {})
+    g.create_pass("B", "Foo", {})
+    g.add_edge("A.x", "B.y")
+    g.add_edge("B.z", "A.w")
+    g.mark_output("B.z")
+    with pytest.raises(abi.RsdError, match="cycle"):
+        g.plan(8, 8)
+
+
+def test_property_errors():
+    g = rsdgraph.RenderGraph("props")
+    with pytest.raises(abi.RsdError, match="unknown value 'Sideways'"):
+        g.create_pass("G", "GBufferRaster", {"forceCullMode": True, "cull": "Sideways"})
+    with pytest.raises(abi.RsdError) as e:
+        g.create_pass("S", "StochasticDepthMapRT", {"StoreNormals": True})
+    assert e.value.status == 2  # StochasticDepthMapRT.cpp:198-203 throws for StoreNormals
+    with pytest.raises(abi.RsdError, match="not a number"):
+        g.create_pass("T", "StochasticDepthMapRT", {"SampleCount": "four"})
+    with pytest.raises(abi.RsdError) as e:
+        g.create_pass("C", "CompressNormals", {"use16Bit": False})
+    assert e.value.status == 2
+
+
+def test_sd_pass_reflection():
+    for n, fmt, layers in [(1, "R32Float", 1), (2, "RG32Float", 1), (4, "RGBA32Float", 1), (8, "RGBA32Float", 2),
+                           (16, "RGBA32Float", 4)]:
+        g = rsdgraph.RenderGraph("sd")
+        g.create_pass("SD", "StochasticDepthMapRT", {"SampleCount": n})
+        g.create_pass("Z", "Source", {})
+        g.add_edge("Z.z", "SD.linearZ")
+        g.mark_output("SD.stochasticDepth")
+        g.plan(100, 60)
+        assert g.resources()["SD.stochasticDepth"] == (100, 60, layers, fmt)
+        # the producer of linearZ (a stub) takes the consumer's declared format
+        assert g.resources()["Z.z"][3] == "R32Float"
+
+
+def test_plugin_dlopen(tmp_path):
+    """A pass type unknown to librsd is loaded from <plugin dir>/<Type>.so."""
+    so = tmp_path / "ConstantDepth.so"
+    cmd = ["g++", "-O1", "-std=c++17", "-shared", "-fPIC", "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include",
+           f"-I{PKG_DIR / 'csrc' / 'host'}", str(ROOT / "tests" / "plugins" / "ConstantDepth.cpp"), "-o", str(so)]
+    subprocess.run(cmd, check=True, timeout=300)
+    assert "ConstantDepth" not in rsdgraph.plugin_types()
+    rsdgraph.set_plugin_dir(tmp_path)
+    try:
+        g = rsdgraph.RenderGraph("plugin")
+        g.create_pass("C", "ConstantDepth", {"value": 0.5})
+        g.create_pass("L", "LinearizeDepth", {})
+        g.add_edge("C.depth", "L.depth")
+        g.mark_output("L.linearDepth")
+        g.plan(32, 16)
+        assert g.execution_order() == ["C", "L"]
+        assert g.resources()["C.depth"] == (32, 16, 1, "R32Float")
+        assert "ConstantDepth" in rsdgraph.plugin_types()
+    finally:
+        rsdgraph.set_plugin_dir("")
+
+
+def test_graph_header_exports():
+    """include/rsd_graph.h declares exactly abi.GRAPH_EXPORTS and librsd exports them."""
+    import re
+    hdr = (ROOT / "include" / "rsd_graph.h").read_text()
+    declared = set(re.findall(r"^(?:rsd_status|void)\s+(rsd_\w+)\(", hdr, re.M))
+    assert declared == set(abi.GRAPH_EXPORTS)
+    out = subprocess.run(["nm", "-D", "--defined-only", str(abi.LIB_PATH)], capture_output=True, text=True,
+                         check=True).stdout
+    exported = set(re.findall(r" T (rsd_\w+)$", out, re.M))
+    assert set(abi.GRAPH_EXPORTS) <= exported
+    assert os.path.getsize(abi.LIB_PATH) > 0

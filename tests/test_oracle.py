@@ -199,3 +199,24 @@ def test_svao_pass1_interval_invariants(oracle):
     sd = np.ones((1, sdH, sdW, N), np.float32)
     ao2 = oracle.svao_pass2(cam, vao, p, z, n, st, sd, ao)
     assert np.array_equal(ao2[st == 0], ao[st == 0])
+
+
+def test_raster_gbuffer_chain_matches_linear_gbuffer(oracle):
+    """GBufferRaster.depth -> LinearizeDepth and .faceNormalW -> CompressNormals restate the
+    same closest hits as the direct linear G-buffer: identical misses, normals bit-equal,
+    depth equal up to the float round trip through the non-linear depth."""
+    from rsd.scenes import make_scene
+    s = make_scene("arcade_tiny")
+    os_ = oracle.Scene(s.positions, s.indices, s.flags)
+    cam = oracle.camera_look_at([0, 1.7, 3.0], [0, 1.2, -2.0], [0, 1, 0], aspect=96 / 64)
+    z, n = oracle.gbuffer(os_, cam, 96, 64, 1)
+    d, nw = oracle.gbuffer_raster(os_, cam, 96, 64, 1)
+    miss = d == 1.0
+    assert miss.sum() < miss.size and np.all(nw[miss] == 0)
+    assert np.all(z[miss] == np.float32(cam.farZ))
+    np.testing.assert_array_equal(oracle.compress_normals(nw, cam)[~miss], n[~miss])
+    zl = oracle.linearize_depth(d, cam.nearZ, cam.farZ)
+    np.testing.assert_allclose(zl[~miss], z[~miss], rtol=2e-3)
+    # Linearize.ps.slang formula, evaluated in float32 by numpy
+    zn, zf = np.float32(cam.nearZ), np.float32(cam.farZ)
+    np.testing.assert_array_equal(zl, zn * zf / (zf + d * (zn - zf)))
