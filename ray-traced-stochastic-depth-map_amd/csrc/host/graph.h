@@ -167,6 +167,7 @@ public:
     void setScene(Context& ctx, const SceneRef* scene);
     // allocate = false plans only (culling, order, resource table) -- no device calls
     void compile(Context& ctx, uint32_t width, uint32_t height, bool allocate = true);
+    bool isCompiled() const { return compiled_; }
     void execute(Context& ctx);
     Texture* getOutput(const std::string& name);
     Dictionary& dictionary() { return dict_; }

@@ -241,8 +241,8 @@ class SVAOPass : public RenderPass {
 public:
     explicit SVAOPass(const Properties& p) {
         props_ = p;
-        radius_ = (float)p.getFloat("radius", 1.0);
-        exponent_ = (float)p.getFloat("exponent", 1.0);
+        radius_ = (float)p.getFloat("radius", 0.5);      // VAOData.slang:39
+        exponent_ = (float)p.getFloat("exponent", 2.0);  // VAOData.slang:40
         thickness_ = (float)p.getFloat("thickness", 0.0);
         primary_ = enumProp(p, "primaryDepthMode", kDepthModeNames, 0);
         secondary_ = enumProp(p, "secondaryDepthMode", kDepthModeNames, 2);
@@ -319,7 +319,8 @@ public:
         sdGraph_->createPass("StochasticDepthMap", "StochasticDepthMapRT", sd);
         sdGraph_->markOutput("StochasticDepthMap.stochasticDepth");
         sdGraph_->setScene(ctx, scene_);
-        sdGraph_->compile(ctx, sdW_, sdH_);
+        // compiled at the first execute, once its inputs are bound (RenderGraph::execute
+        // compiles on demand in the reference, RenderGraph.cpp:420-430)
     }
     void execute(Context& ctx, const RenderData& rd) override {
         if (!scene_) return;  // SVAO.cpp:194
@@ -352,6 +353,7 @@ public:
         sdGraph_->setInput("StochasticDepthMap.rayMin", rmin);
         sdGraph_->setInput("StochasticDepthMap.rayMax", rmax);
         sdGraph_->dictionary()["SD_CLEAR"] = false;
+        if (!sdGraph_->isCompiled()) sdGraph_->compile(ctx, sdW_, sdH_);
         sdGraph_->execute(ctx);
         Texture* sd = sdGraph_->getOutput("StochasticDepthMap.stochasticDepth");
         check(rsd_svao_pass2(&s->camera, &vao_, &svp_, (const float*)depth->ptr, (const uint16_t*)normals->ptr,

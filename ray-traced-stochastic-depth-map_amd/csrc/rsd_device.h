@@ -38,7 +38,12 @@ __device__ __forceinline__ float saturate(float x) { return !(x > 0.0f) ? 0.0f :
 __device__ __forceinline__ float hmax(float a, float b) { return fmaxf(a, b); }
 __device__ __forceinline__ float hmin(float a, float b) { return fminf(a, b); }
 __device__ __forceinline__ float acc_sin(float x) { return (float)sin((double)x); }
-__device__ __forceinline__ float acc_pow(float x, float y) { return (float)pow((double)x, (double)y); }
+__device__ __forceinline__ float acc_pow(float x, float y) {
+    // y == 2 (the SVAO default exponent, VAOData.slang:40): x * x is exact in double (48-bit
+    // product), so the correctly rounded pow rounds to the binary32 product x * x.
+    if (y == 2.0f) return x * x;
+    return (float)pow((double)x, (double)y);
+}
 
 // R8Unorm store: saturate, round to nearest; NaN -> 0
 __device__ __forceinline__ uint8_t unorm8(float x) {

@@ -24,6 +24,14 @@ r.clear_intervals()
 print("sd all-inactive ms", timeit(r.sd_trace))
 r.clear_intervals(); r.pass1()
 print("pass1 ms", timeit(lambda: (r.clear_intervals(), r.pass1())))
+r.svp.secondary_depth_mode = 0
+print("pass1 (SingleDepth: no interval atomics) ms", timeit(r.pass1))
+r.svp.secondary_depth_mode = 2
+r.clear_intervals(); r.pass1()
+st = r.stencil.cpu().numpy()
+import numpy as np
+print("stencil: pixels with mask", int((st != 0).sum()), "of", st.size, "directions set", int(np.unpackbits(st).sum()))
+print("touched SD texels", int((r.ray_max.cpu().numpy() != 0).sum()), "of", r.sd_w * r.sd_h)
 c = r.sd_trace(counters=True)
 print("counters", c.rays_dispatched, c.rays_active, c.nodes_visited, c.tris_tested, c.hits_delivered, "max", c.max_nodes_per_ray)
 print("steps: max", c.max_steps_per_ray, "leaves", c.leaves_visited, "avg clocks/ray", c.sum_ray_clocks / max(c.rays_active, 1),
