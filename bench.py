@@ -34,7 +34,7 @@ for p in (str(ROOT), str(PKG)):
         sys.path.insert(0, p)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8 TB/s (spec)
-SD_KERNELS = ("sd_setup_kernel", "sd_trace_queue_kernel")  # the two launches of one rsd_sd_trace
+SD_KERNELS = ("sd_setup_kernel", "sd_trace_row_kernel", "sd_resolve_row_kernel", "sd_trace_queue_kernel")  # launches of one rsd_sd_trace
 
 
 def parse():
@@ -158,7 +158,8 @@ def main():
                       "tris_per_active_ray": round(cnt.tris_tested / max(cnt.rays_active, 1), 2)},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "kernel": "+".join(SD_KERNELS), "alg_bytes_per_launch": int(alg_bytes),
+                     "kernel": "rsd_sd_trace = sd_setup_kernel + sd_trace_row_kernel (+ sd_resolve_row_kernel)",
+                     "alg_bytes_per_launch": int(alg_bytes),
                      "traffic_source": ", ".join(str(Path(p).relative_to(ROOT)) if Path(p).is_relative_to(ROOT)
                                                  else p for p in pmc if Path(p).exists()) or None},
         "cpu_baseline": cpu,
@@ -173,14 +174,16 @@ def pmc_traffic(csv_paths, kernel_substrs):
     FETCH_SIZE doubled on gfx950 per MI355X_MICROARCH.md §HBM): per kernel, the mean over its
     launches; summed over the kernels of the pass."""
     import csv
+    import re
     if not csv_paths:
         return None
     per = {}  # (kernel, counter) -> values
     for path in csv_paths:
         with open(path) as f:
             for row in csv.DictReader(f):
-                k = next((s for s in kernel_substrs if s in row.get("Kernel_Name", "")), None)
-                if k is None:
+                name = row.get("Kernel_Name", "")
+                k = next((s for s in kernel_substrs if s in name), None)
+                if k is None or re.search(r", (true|false), true>", name):  # skip the instrumented launch
                     continue
                 per.setdefault((k, row.get("Counter_Name")), []).append(float(row.get("Counter_Value", 0)))
     if not per:

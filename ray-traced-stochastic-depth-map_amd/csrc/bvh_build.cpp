@@ -215,8 +215,10 @@ FlatBvh build_bvh(const float* pos, uint32_t nv, const uint32_t* ind, uint32_t n
     auto up = [](float v) { return std::nextafter(std::nextafter(v, INFINITY), INFINITY); };
     uint32_t nwide = 0;
     // recursive: returns the wide-node index of binary node `n` (an inner node, or the root)
-    std::function<uint32_t(uint32_t)> build_wide = [&](uint32_t n) -> uint32_t {
+    uint32_t wideDepth = 0;
+    std::function<uint32_t(uint32_t, uint32_t)> build_wide = [&](uint32_t n, uint32_t level) -> uint32_t {
         const uint32_t me = nwide++;
+        wideDepth = std::max(wideDepth, level);
         out.nodes.resize(32 * (size_t)nwide, 0.0f);
         uint32_t ch[kBvhWidth];
         int nc = 0;
@@ -246,7 +248,7 @@ FlatBvh build_bvh(const float* pos, uint32_t nv, const uint32_t* ind, uint32_t n
         for (int i = 0; i < nc; ++i) {
             const TNode& c = nodes[ch[i]];
             for (int k = 0; k < 3; ++k) { lo[i][k] = down(c.box.lo[k]); hi[i][k] = up(c.box.hi[k]); }
-            if (c.left >= 0) { ref[i] = build_wide(ch[i]); cnt[i] = 0; }
+            if (c.left >= 0) { ref[i] = build_wide(ch[i], level + 1); cnt[i] = 0; }
             else { ref[i] = emit_tris(c); cnt[i] = c.count; }
         }
         float* nd = &out.nodes[32 * (size_t)me];
@@ -259,7 +261,7 @@ FlatBvh build_bvh(const float* pos, uint32_t nv, const uint32_t* ind, uint32_t n
         }
         return me;
     };
-    build_wide(root);
+    build_wide(root, 1);
     const uint32_t ninner = nwide;
 
     // statistics
@@ -274,6 +276,7 @@ FlatBvh build_bvh(const float* pos, uint32_t nv, const uint32_t* ind, uint32_t n
     out.stats.inner_nodes = ninner;
     out.stats.leaves = leaves;
     out.stats.max_depth = b.maxDepth.load();
+    out.stats.wide_depth = wideDepth;
     out.stats.sah_cost = sah;
     out.stats.build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     return out;

@@ -22,7 +22,8 @@ namespace rsd {
 struct BvhStats {
     uint32_t inner_nodes = 0;
     uint32_t leaves = 0;
-    uint32_t max_depth = 0;
+    uint32_t max_depth = 0;   // binary SAH tree
+    uint32_t wide_depth = 0;  // inner 4-wide nodes on the longest root-to-leaf path (the root counts 1)
     double sah_cost = 0.0;
     double build_ms = 0.0;
 };

@@ -23,8 +23,8 @@ struct rsd_scene {
     uint64_t device_bytes = 0;
     unsigned long long* d_counters = nullptr;  // 8 x u64 scratch for instrumented traces
     uint32_t* d_qctl = nullptr;    // live-ray queue {count[32], head[32]}
-    uint32_t* d_queue = nullptr;   // live-ray queue (SD texel indices), grow-only
-    size_t queue_cap = 0;
+    void* d_queue = nullptr;       // SD-trace workspace (live-ray records + K-key slots), grow-only
+    size_t queue_cap = 0;          // bytes
 };
 
 namespace rsd {

@@ -22,6 +22,9 @@
 // 4-wide 128-B {child boxes, refs} records fetched as 8 x 16-B loads; triangles are 48-B
 // records, a whole leaf (<= 4) fetched before it is tested.
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <string>
 #include <vector>
 
 #include "rsd_device.h"
@@ -294,6 +297,7 @@ struct SDArgs {
     unsigned long long* counters;
     uint32_t partCap;  // live-ray queue: capacity of one partition
     int bandIndex, bandCount;  // screen-band sharding: 8-row tile rows t with t % count == index
+    int poolSoft;      // row traversal: above this many pooled items a row pops one item per step
 };
 
 __device__ __forceinline__ f3 cam_dir(const rsd_camera& c, float px, float py) {
@@ -572,20 +576,32 @@ __device__ __forceinline__ void sd_resolve(const SDArgs& a, f3 d, float TMin, fl
     }
 }
 
+// A live ray in the queue: 2 x 16 B {dir.xyz, TMin} {TMax, cosT, texel, 0}
+__device__ __forceinline__ void ray_rec_load(const float4* __restrict__ q, uint32_t slot, f3& d, float& TMin,
+                                             float& TMax, float& cosT, uint32_t& texel) {
+    const float4 r0 = q[2u * slot], r1 = q[2u * slot + 1u];
+    d = mk(r0.x, r0.y, r0.z);
+    TMin = r0.w;
+    TMax = r1.x;
+    cosT = r1.y;
+    texel = __float_as_uint(r1.z);
+}
+
 // Phase 1 (rayGen up to TraceRay): one lane per SD texel of the band.  Rays whose interval
 // is empty keep DEFAULT_DEPTH and are written here; the others are appended to a compact
-// queue (one atomic per wave) so that phase 2 runs full waves of live rays only.
+// queue of ray records (one atomic per wave) so that phase 2 runs full waves of live rays
+// and starts traversing without recomputing the ray.
 template <int N>
-__global__ void __launch_bounds__(kBlock) sd_setup_kernel(SDArgs a, uint32_t* __restrict__ queue,
+__global__ void __launch_bounds__(kBlock) sd_setup_kernel(SDArgs a, float4* __restrict__ queue,
                                                           uint32_t* __restrict__ qctl) {
     const int lane = threadIdx.x;
     const int x = blockIdx.x * kTile + (lane & (kTile - 1));
     const int y = ((int)blockIdx.y * a.bandCount + a.bandIndex) * kTile + (lane / kTile);
     const bool inside = x < a.sdW && y < a.sdH;
     bool live = false;
+    f3 d = mk(0.0f, 0.0f, 0.0f);
+    float TMin = 0.0f, TMax = 0.0f, cosT = 0.0f;
     if (inside) {
-        f3 d;
-        float TMin, TMax, cosT;
         live = sd_ray(a, x, y, d, TMin, TMax, cosT);
         if (!live) {
             float depths[N];
@@ -604,9 +620,11 @@ __global__ void __launch_bounds__(kBlock) sd_setup_kernel(SDArgs a, uint32_t* __
     uint32_t base = 0;
     if (lane == 0 && n) base = atomicAdd(&qctl[part], n);
     base = __shfl(base, 0);
-    if (live)
-        queue[part * a.partCap + base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] =
-            (uint32_t)y * (uint32_t)a.sdW + x;
+    if (live) {
+        const uint32_t slot = part * a.partCap + base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+        queue[2u * slot] = make_float4(d.x, d.y, d.z, TMin);
+        queue[2u * slot + 1u] = make_float4(TMax, cosT, __uint_as_float((uint32_t)y * (uint32_t)a.sdW + x), 0.0f);
+    }
     const unsigned long long in = __ballot(inside);
     if (a.counters && lane == 0) atomicAdd(&a.counters[0], (unsigned long long)__popcll(in));
 }
@@ -617,7 +635,7 @@ __global__ void __launch_bounds__(kBlock) sd_setup_kernel(SDArgs a, uint32_t* __
 // that starts after the static range, so a wave with no static chunk exits without an
 // atomic (one head word serialises ~90 dequeues/us, MI355X_MICROARCH.md "dequeue").
 template <int K, int N>
-__global__ void __launch_bounds__(kBlock) sd_trace_queue_kernel(SDArgs a, const uint32_t* __restrict__ queue,
+__global__ void __launch_bounds__(kBlock) sd_trace_queue_kernel(SDArgs a, const float4* __restrict__ queue,
                                                                 uint32_t* __restrict__ qctl) {
     __shared__ uint32_t sItem[kQuadStack * kQuadRays];
     __shared__ float sT[kQuadStack * kQuadRays];
@@ -626,7 +644,7 @@ __global__ void __launch_bounds__(kBlock) sd_trace_queue_kernel(SDArgs a, const 
     // wave w serves partition w % kQueueParts (gridDim.x is a multiple of kQueueParts)
     const uint32_t part = blockIdx.x % kQueueParts, wavesPerPart = gridDim.x / kQueueParts;
     const uint32_t count = __hip_atomic_load(&qctl[part], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const uint32_t* pq = queue + part * a.partCap;
+    const uint32_t slot0 = part * a.partCap;
     TraceStats st{0u, 0u, 0u};
     uint32_t active = 0, hitsDelivered = 0, maxNodes = 0, maxSteps = 0;
     unsigned long long sumCycles = 0, maxCycles = 0;
@@ -634,11 +652,11 @@ __global__ void __launch_bounds__(kBlock) sd_trace_queue_kernel(SDArgs a, const 
     while (base < count) {
         const uint32_t qi = base + (uint32_t)quad;
         if (qi < count) {
-            const uint32_t idx = pq[qi];
-            const int x = (int)(idx % (uint32_t)a.sdW), y = (int)(idx / (uint32_t)a.sdW);
             f3 d;
             float TMin, TMax, cosT;
-            sd_ray(a, x, y, d, TMin, TMax, cosT);
+            uint32_t idx;
+            ray_rec_load(queue, slot0 + qi, d, TMin, TMax, cosT, idx);
+            const int x = (int)(idx % (uint32_t)a.sdW), y = (int)(idx / (uint32_t)a.sdW);
             float depths[N];
             const float DEFAULT = a.normalize ? 1.0f : 3.40282347e+37f;
 #pragma unroll
@@ -675,6 +693,456 @@ __global__ void __launch_bounds__(kBlock) sd_trace_queue_kernel(SDArgs a, const 
         atomicMax(&a.counters[8], maxCycles);
         atomicAdd(&a.counters[9], (unsigned long long)(q == 0 ? st.leaves : 0u));
     }
+}
+
+// ------------------------------------------------------------------------------------
+// Row-parallel traversal (the default SD trace).  The quad walk above is depth-first: its
+// critical path is every node and leaf the ray visits, one dependent fetch after the other
+// (the slowest live ray of a 1080p/4 frame visits ~130 items, and the launch lasts as long
+// as that ray).  Here a ray is walked by a ROW of 16 lanes (a quarter wave): each step, up
+// to 16 work items (4-wide nodes or leaves) taken from the top of the ray's LDS pool are
+// processed at once, one per lane, and their surviving children are pushed back, nearest on
+// top.  The critical path becomes ~ the tree depth plus (visited items / 16).
+// The ray's k-list is sorted ACROSS the row (lane j holds key j, up to 16 keys): inserting a
+// hit is one ballot and three shuffles.  Pruning is the depth-first walk's: an item is
+// dropped once the K-th key is nearer than its box, which only depends on keys found, so the
+// K nearest keys -- and the SD texel -- do not depend on the visiting order.
+// Pool bound: a row pops 16 items per step while the pool holds <= poolSoft items and one
+// item (a depth-first step, +3 items per level at most) above, so the pool never exceeds
+// poolSoft + 48 + 3 * (wide tree depth) <= kPoolCap (poolSoft is derived from the depth).
+// A wave walks 4 rays; every row refills from the live-ray queue on its own.
+// ------------------------------------------------------------------------------------
+constexpr int kPoolCap = 256;  // work items per ray (LDS: rays per wave x 256 x 8 B)
+
+template <int ROW>
+__device__ __forceinline__ uint32_t row_bits(bool p, int base) {
+    return (uint32_t)(__ballot(p) >> base) & ((1u << ROW) - 1u);
+}
+
+// insert key (nt, np, nl) into the row-distributed sorted list (lane j holds key j); the
+// largest key falls off the last lane
+template <int ROW>
+__device__ __forceinline__ void row_insert(float& kt, uint32_t& kp, uint32_t& kl, float nt, uint32_t np, uint32_t nlSrc,
+                                           int srcL, int l, int base) {
+    const uint32_t nl = __shfl(nlSrc, base + srcL);  // the new key's triangle record, from its lane
+    const int pos = __popc(row_bits<ROW>(key_less(kt, kp, nt, np), base));
+    const int src = base + (l > 0 ? l - 1 : 0);
+    const float st = __shfl(kt, src);
+    const uint32_t sp = __shfl(kp, src), sl = __shfl(kl, src);
+    if (l == pos) {
+        kt = nt; kp = np; kl = nl;
+    } else if (l > pos) {
+        kt = st; kp = sp; kl = sl;
+    }
+}
+
+// exclusive prefix sum (and total) of v in [0, 7] over the lanes of a row
+template <int ROW>
+__device__ __forceinline__ int row_prefix(int v, int l, int base, int& total) {
+    const uint32_t below = (1u << l) - 1u;
+    int pre = 0;
+    total = 0;
+#pragma unroll
+    for (int b = 0; b < 3; ++b) {
+        const uint32_t m = row_bits<ROW>((v >> b) & 1, base);
+        pre += __popc(m & below) << b;
+        total += __popc(m) << b;
+    }
+    return pre;
+}
+
+// anyHit -> algorithm (Common.slangh:102-254) over `found` keys in ascending (t, prim) order;
+// lane j of the row holds key j's hash `rng` and normalized view depth `z`.  Every lane of
+// the row ends with the same depths / cnt / commit.
+template <int K, int N>
+__device__ __forceinline__ bool sd_algorithm_row(const SDArgs& a, float rng, float z, int found, int base,
+                                                 float (&depths)[N], uint32_t& cnt, uint32_t& delivered) {
+    bool commit = false;
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+        const float rj = __shfl(rng, base + j);
+        float zj = __shfl(z, base + j);
+        if (commit || j >= found) continue;
+        delivered++;
+        if (a.impl == 1u) {  // CoverageMask, Common.slangh:117-131, 189-209
+            const int R = (int)floorf(a.alpha * (float)N + rj);
+            uint32_t mask = 0u;
+            if (R >= N) mask = 0xffffu;
+            else if (R != 0) {
+                const float rng2 = sd_hash(rj, zj);  // hash3D(float3(bary, t))
+                const float lo = (float)a.lutIdx[R], hi = (float)a.lutIdx[R + 1];
+                mask = a.lut[(int)(lo + rng2 * (hi - lo))];
+            }
+            float maxT = 0.0f;
+#pragma unroll
+            for (int i = 0; i < N; ++i) {
+                if ((mask & (1u << i)) && zj < depths[i]) depths[i] = zj;
+                maxT = hmax(maxT, depths[i]);
+            }
+            commit = !(zj < maxT);
+        } else if (a.impl == 3u) {  // KBuffer, Common.slangh:132-135, 211-232
+            if (zj >= depths[N - 1]) {
+                commit = true;
+            } else {
+                cnt++;
+                const float rayT = zj;
+#pragma unroll
+                for (int i = 0; i < N; ++i)
+                    if (zj < depths[i]) { const float tmp = depths[i]; depths[i] = zj; zj = tmp; }
+                commit = (depths[N - 1] == rayT) || cnt >= a.maxCount;
+            }
+        } else {  // Default reservoir, Common.slangh:136-153, 234-247
+            uint32_t slot = cnt++;
+            if (cnt > (uint32_t)N) slot = (uint32_t)(rj * (float)cnt);
+#pragma unroll
+            for (int i = 0; i < N; ++i)
+                if ((uint32_t)i == slot && !(depths[i] <= zj)) depths[i] = zj;
+            commit = cnt >= a.maxCount;
+        }
+    }
+    return commit;
+}
+
+// hash + normalized view depth of the hit (t, triangle record tri) -- the barycentrics come
+// from re-running the identical triangle test (Common.slangh:110-115)
+__device__ __forceinline__ void sd_hit_terms(const SDArgs& a, const RayCtx& r, float cosT, uint32_t tri, float& rng,
+                                             float& z) {
+    float t, bu, bv, det;
+    intersect_tri(r, a.tris[3 * tri], a.tris[3 * tri + 1], a.tris[3 * tri + 2], t, bu, bv, det);
+    rng = sd_hash(bu, bv);
+    z = t * cosT;  // RayToViewDepth
+    if (a.normalize) z = saturate((z - a.cam.nearZ) / (a.cam.farZ - a.cam.nearZ));
+}
+
+// ROW lanes per ray (8 or 16, >= K: lane j of the row holds key j), 64 / ROW rays per wave.
+// SPLIT: the walk only collects the K nearest keys and writes them to `keys` (one K-key slot
+// per queue slot); sd_resolve_row_kernel runs the algorithm.  Valid when one chunk of K keys
+// always decides the texel: Default / KBuffer with MaxCount <= K.  Otherwise the algorithm
+// runs here and the walk continues after the K-th key while it has not committed.
+template <int K, int N, int ROW, bool SPLIT, bool CNT>
+__global__ void __launch_bounds__(kBlock) sd_trace_row_kernel(SDArgs a, const float4* __restrict__ queue,
+                                                              uint32_t* __restrict__ qctl, uint2* __restrict__ keys) {
+    static_assert(K <= ROW, "one key per lane");
+    constexpr int kRow = ROW, kRowRays = kBlock / ROW;
+    __shared__ uint32_t sItem[kRowRays * kPoolCap];
+    __shared__ float sT[kRowRays * kPoolCap];
+    const int lane = threadIdx.x;
+    const int l = lane & (kRow - 1), base = lane & ~(kRow - 1), row = lane / kRow;
+    uint32_t* pItem = sItem + row * kPoolCap;
+    float* pT = sT + row * kPoolCap;
+    const uint32_t part = blockIdx.x % kQueueParts, wavesPerPart = gridDim.x / kQueueParts;
+    const uint32_t count = __hip_atomic_load(&qctl[part], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t slot0 = part * a.partCap;
+    const rsd_camera& c = a.cam;
+    const float DEFAULT = a.normalize ? 1.0f : 3.40282347e+37f;  // Common.slangh:16
+    const int soft = a.poolSoft;
+    uint32_t slot = 0;  // queue slot of the row's ray
+
+    // ---- per-row state (the same value in the 16 lanes of a row unless noted)
+    constexpr int kFetch = 0, kTrace = 1, kExit = 2;
+    int phase = kFetch;
+    bool first = true;
+    int x = 0, y = 0;
+    RayCtx r;
+    float TMin = 0.0f, TMax = 0.0f, cosT = 0.0f;
+    float depths[N];
+    uint32_t cnt = 0;     // algorithm count (Common.slangh:137)
+    bool useLB = false;   // coverage mask / MaxCount > K: keys after (lbT, lbP) only
+    float lbT = 0.0f;
+    uint32_t lbP = 0u;
+    int pool = 0;         // items in this ray's LDS pool
+    uint32_t item = kNoItem;  // per lane: the work item of this step
+    float kt = INFINITY;  // per lane: key l of the row's sorted k-list
+    uint32_t kp = kNoItem, kl = 0u;
+    // ---- statistics (counters build)
+    TraceStats st{0u, 0u, 0u};
+    uint32_t active = 0, hitsDelivered = 0, maxSteps = 0, raySteps = 0, maxNodes = 0, rayNodes = 0;
+    unsigned long long sumCycles = 0, maxCycles = 0, c0 = 0;
+
+    unsigned long long tFetch = 0, tStep = 0, tResolve = 0, nStep = 0, nLoop = 0, tS0 = 0, tS1 = 0;
+    while (__ballot(phase != kExit) != 0ull) {
+        if constexpr (CNT) { tS0 = __builtin_amdgcn_s_memtime(); nLoop += lane == 0; }
+        const bool fetching = phase == kFetch;
+        if (phase == kFetch) {
+            uint32_t qi;
+            if (first) {
+                qi = (blockIdx.x / kQueueParts) * (uint32_t)kRowRays + (uint32_t)row;  // static first ray
+                first = false;
+            } else {
+                uint32_t h = 0;
+                if (l == 0) h = atomicAdd(&qctl[kQueueParts + part], 1u);
+                qi = wavesPerPart * (uint32_t)kRowRays + __shfl(h, base);
+            }
+            if (qi >= count) {
+                phase = kExit;
+            } else {
+                slot = slot0 + qi;
+                f3 d;
+                uint32_t idx;
+                ray_rec_load(queue, slot, d, TMin, TMax, cosT, idx);
+                x = (int)(idx % (uint32_t)a.sdW);
+                y = (int)(idx / (uint32_t)a.sdW);
+                ray_setup(r, mk(c.posW[0], c.posW[1], c.posW[2]), d);
+#pragma unroll
+                for (int i = 0; i < N; ++i) depths[i] = DEFAULT;
+                cnt = 0u;
+                useLB = false;
+                pool = 0;
+                item = l == 0 ? 0u : kNoItem;  // the root node
+                kt = INFINITY; kp = kNoItem; kl = 0u;
+                phase = kTrace;
+                if constexpr (CNT) {
+                    active += l == 0;
+                    raySteps = 0;
+                    rayNodes = 0;
+                    c0 = __builtin_amdgcn_s_memtime();
+                }
+            }
+        }
+        if constexpr (CNT) {
+            tS1 = __builtin_amdgcn_s_memtime();
+            if (fetching && l == 0) tFetch += tS1 - tS0;
+        }
+        if (phase != kTrace) continue;
+
+        // ---- one traversal step of this row
+        const float tlo = useLB ? fmaxf(TMin, lbT) : TMin;
+        float kthT = __shfl(kt, base + K - 1);
+        uint32_t kthP = __shfl(kp, base + K - 1);
+        float thi = fminf(TMax, kthT);
+        float ck[4];
+        uint32_t ci[4];
+        int nc = 0;
+        // one 128-B fetch: a 4-wide node, or triangle records 0-1 (+ 2/3 of record 2) of a
+        // leaf; records 2-3 of a larger leaf are re-read below (same or next cache line)
+        const float4* p = a.nodes + (item & kOffMask);
+        float4 q[8];
+        if (item != kNoItem) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) q[j] = p[j];
+        }
+        const bool isLeaf = item != kNoItem && (item & kLeafBit);
+        if (item != kNoItem && !isLeaf) {
+            st.nodes++;
+            rayNodes++;
+            const uint32_t rf[4] = {__float_as_uint(q[6].x), __float_as_uint(q[6].y), __float_as_uint(q[6].z),
+                                    __float_as_uint(q[6].w)};
+            const uint32_t cn[4] = {__float_as_uint(q[7].x), __float_as_uint(q[7].y), __float_as_uint(q[7].z),
+                                    __float_as_uint(q[7].w)};
+            const float lox[4] = {q[0].x, q[0].y, q[0].z, q[0].w}, hix[4] = {q[1].x, q[1].y, q[1].z, q[1].w};
+            const float loy[4] = {q[2].x, q[2].y, q[2].z, q[2].w}, hiy[4] = {q[3].x, q[3].y, q[3].z, q[3].w};
+            const float loz[4] = {q[4].x, q[4].y, q[4].z, q[4].w}, hiz[4] = {q[5].x, q[5].y, q[5].z, q[5].w};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                float tn;
+                const bool h = rf[j] != kNoItem && box_hit(r, lox[j], hix[j], loy[j], hiy[j], loz[j], hiz[j], tlo,
+                                                          thi, tn);
+                ck[j] = h ? tn : INFINITY;
+                ci[j] = h ? (cn[j] ? (kLeafBit | ((cn[j] - 1u) << 29) | (a.triOff + 3u * rf[j])) : 8u * rf[j])
+                          : kNoItem;
+                nc += h;
+            }
+            // ascending entry distance; misses (INF) sort last
+            cswap(ck[0], ci[0], ck[1], ci[1]);
+            cswap(ck[2], ci[2], ck[3], ci[3]);
+            cswap(ck[0], ci[0], ck[2], ci[2]);
+            cswap(ck[1], ci[1], ck[3], ci[3]);
+            cswap(ck[1], ci[1], ck[2], ci[2]);
+        }
+        // ---- leaves: triangle j of every leaf lane, then the row merges the accepted hits
+        //      into its k-list (one insert each) before triangle j + 1
+        const uint32_t lc = isLeaf ? ((item >> 29) & 3u) + 1u : 0u;
+        const uint32_t firstTri = ((item & kOffMask) - a.triOff) / 3u;
+        if (isLeaf) st.leaves++;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            if (row_bits<ROW>((uint32_t)j < lc, base) == 0u) break;
+            bool acc = false;
+            float t = 0.0f;
+            uint32_t prim = 0u;
+            if ((uint32_t)j < lc) {
+                st.tris++;
+                const float4 v0 = j < 2 ? q[3 * j] : (j == 2 ? q[6] : p[9]);
+                const float4 v1 = j < 2 ? q[3 * j + 1] : (j == 2 ? q[7] : p[10]);
+                const float4 v2 = j < 2 ? q[3 * j + 2] : p[3 * j + 2];
+                float bu, bv, det;
+                if (intersect_tri(r, v0, v1, v2, t, bu, bv, det) && t >= TMin && t <= TMax) {
+                    prim = __float_as_uint(v0.w);
+                    acc = !culled(det, __float_as_uint(v1.w), a.cull) && (!useLB || key_less(lbT, lbP, t, prim)) &&
+                          key_less(t, prim, kthT, kthP);
+                }
+            }
+            for (uint32_t m = row_bits<ROW>(acc, base); m; m &= m - 1u) {
+                const int srcLane = base + __ffs(m) - 1;
+                const float bt = __shfl(t, srcLane);
+                const uint32_t bp = __shfl(prim, srcLane);
+                if (key_less(bt, bp, kthT, kthP)) {
+                    row_insert<ROW>(kt, kp, kl, bt, bp, firstTri + (uint32_t)j, srcLane - base, l, base);
+                    kthT = __shfl(kt, base + K - 1);
+                    kthP = __shfl(kp, base + K - 1);
+                }
+            }
+        }
+        thi = fminf(TMax, kthT);
+        // ---- push the surviving children, nearest on top
+        int keep = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) keep += (j < nc && ck[j] <= thi) ? 1 : 0;  // ck ascending: a prefix
+        int total;
+        const int pre = row_prefix<ROW>(keep, l, base, total);
+        if (pool + total > kPoolCap) {  // unreachable by the pool bound; never write out of range
+            if (a.counters && l == 0) atomicAdd(&a.counters[10], 1ull);  // always checked
+            keep = max(0, min(keep, kPoolCap - pool - pre));
+            total = kPoolCap - pool;
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            if (j < keep) {
+                const int slot = pool + pre + (keep - 1 - j);
+                pItem[slot] = ci[j];
+                pT[slot] = ck[j];
+            }
+        }
+        pool += total;
+        __builtin_amdgcn_wave_barrier();  // LDS pushes above before the pops below (one wave)
+        // ---- pop the next items
+        const int take = min(pool, pool <= soft ? kRow : 1);
+        item = kNoItem;
+        if (l < take) {
+            const uint32_t it = pItem[pool - 1 - l];
+            const float tt = pT[pool - 1 - l];
+            item = tt <= thi ? it : kNoItem;
+        }
+        pool -= take;
+        __builtin_amdgcn_wave_barrier();
+        if constexpr (CNT) {
+            raySteps++;
+            const unsigned long long t2 = __builtin_amdgcn_s_memtime();
+            if (l == 0) { tStep += t2 - tS1; nStep++; }
+            tS1 = t2;
+        }
+        if (pool > 0 || row_bits<ROW>(item != kNoItem, base) != 0u) continue;
+
+        // ---- traversal done
+        if constexpr (SPLIT) {
+            // the K nearest keys of the ray -> sd_resolve_row_kernel
+            if (l < K) keys[(size_t)slot * K + l] = make_uint2(__float_as_uint(kt), kp == kNoItem ? kNoItem : kl);
+            phase = kFetch;
+            if constexpr (CNT) {
+                uint32_t n = rayNodes;
+#pragma unroll
+                for (int o = ROW / 2; o >= 1; o >>= 1) n += __shfl_xor(n, o);
+                maxNodes = max(maxNodes, n);
+                maxSteps = max(maxSteps, raySteps);
+                const unsigned long long t3 = __builtin_amdgcn_s_memtime();
+                if (l == 0) {
+                    tResolve += t3 - tS1;
+                    sumCycles += t3 - c0;
+                    maxCycles = t3 - c0 > maxCycles ? t3 - c0 : maxCycles;
+                }
+            }
+            continue;
+        }
+        // TraceRay + anyHit -> algorithm (Common.slangh:102-254) over the found keys, in
+        // ascending (t, prim) order; lane j prepares key j
+        const int found = min(K, __popc(row_bits<ROW>(kp != kNoItem, base)));
+        float rng = 0.0f, z = 0.0f;
+        if (l < found) sd_hit_terms(a, r, cosT, kl, rng, z);
+        uint32_t delivered = 0;
+        const bool commit = sd_algorithm_row<K, N>(a, rng, z, found, base, depths, cnt, delivered);
+        if (l == 0) hitsDelivered += delivered;
+        if (CNT && l == 0) tResolve += __builtin_amdgcn_s_memtime() - tS1;
+        if (!commit && found == K) {
+            // the stream continues after the K-th key: trace the next chunk of K keys
+            useLB = true;
+            lbT = __shfl(kt, base + K - 1);
+            lbP = __shfl(kp, base + K - 1);
+            pool = 0;
+            item = l == 0 ? 0u : kNoItem;
+            kt = INFINITY; kp = kNoItem; kl = 0u;
+            continue;
+        }
+        if (l == 0) sd_store<N>(a, x, y, depths);
+        phase = kFetch;
+        if constexpr (CNT) {
+            // per-ray totals: row sums of the lanes' node counts
+            uint32_t n = rayNodes;
+#pragma unroll
+            for (int o = ROW / 2; o >= 1; o >>= 1) n += __shfl_xor(n, o);
+            maxNodes = max(maxNodes, n);
+            maxSteps = max(maxSteps, raySteps);
+            const unsigned long long dc = __builtin_amdgcn_s_memtime() - c0;
+            if (l == 0) {
+                sumCycles += dc;
+                maxCycles = dc > maxCycles ? dc : maxCycles;
+            }
+        }
+    }
+    if constexpr (CNT) {
+        atomicAdd(&a.counters[1], (unsigned long long)active);
+        atomicAdd(&a.counters[2], (unsigned long long)st.nodes);
+        atomicAdd(&a.counters[3], (unsigned long long)st.tris);
+        atomicAdd(&a.counters[4], (unsigned long long)hitsDelivered);
+        atomicMax(&a.counters[5], (unsigned long long)maxNodes);
+        atomicMax(&a.counters[6], (unsigned long long)maxSteps);
+        atomicAdd(&a.counters[7], sumCycles);
+        atomicMax(&a.counters[8], maxCycles);
+        atomicAdd(&a.counters[9], (unsigned long long)st.leaves);
+        atomicAdd(&a.counters[11], tFetch);
+        atomicAdd(&a.counters[12], tStep);
+        atomicAdd(&a.counters[13], tResolve);
+        atomicAdd(&a.counters[14], nStep);
+        atomicAdd(&a.counters[15], nLoop);
+    }
+}
+
+// Phase 3 of the split trace: anyHit -> algorithm over the K nearest keys of every live ray
+// (one row of ROW lanes per ray, lane j prepares key j), then the SD texel store
+// (StochasticDepthMapRT.rt.slang:90-104).  Persistent rows stride over the queue partitions.
+template <int K, int N, int ROW>
+__global__ void __launch_bounds__(kBlock) sd_resolve_row_kernel(SDArgs a, const float4* __restrict__ queue,
+                                                                const uint32_t* __restrict__ qctl,
+                                                                const uint2* __restrict__ keys) {
+    constexpr int kRowRays = kBlock / ROW;
+    const int lane = threadIdx.x;
+    const int l = lane & (ROW - 1), base = lane & ~(ROW - 1), row = lane / ROW;
+    const uint32_t rows = gridDim.x * (uint32_t)kRowRays, me = blockIdx.x * (uint32_t)kRowRays + (uint32_t)row;
+    const rsd_camera& c = a.cam;
+    const float DEFAULT = a.normalize ? 1.0f : 3.40282347e+37f;  // Common.slangh:16
+    uint32_t delivered = 0;
+    // live ray g of the frame = partition part, entry g - (rays in partitions < part)
+    uint32_t part = 0, partStart = 0, partCount = qctl[0];
+    for (uint32_t g = me;; g += rows) {
+        while (part < kQueueParts && g >= partStart + partCount) {
+            partStart += partCount;
+            if (++part < kQueueParts) partCount = qctl[part];
+        }
+        if (part >= kQueueParts) break;
+        {
+            const uint32_t slot = part * a.partCap + (g - partStart);
+            f3 d;
+            float TMin, TMax, cosT;
+            uint32_t idx;
+            ray_rec_load(queue, slot, d, TMin, TMax, cosT, idx);
+            RayCtx r;
+            ray_setup(r, mk(c.posW[0], c.posW[1], c.posW[2]), d);
+            float rng = 0.0f, z = 0.0f;
+            bool valid = false;
+            if (l < K) {
+                const uint2 k = keys[(size_t)slot * K + l];
+                valid = k.y != kNoItem;
+                if (valid) sd_hit_terms(a, r, cosT, k.y, rng, z);
+            }
+            const int found = __popc(row_bits<ROW>(valid, base));  // keys are sorted: a prefix
+            float depths[N];
+#pragma unroll
+            for (int i = 0; i < N; ++i) depths[i] = DEFAULT;
+            uint32_t cnt = 0;
+            sd_algorithm_row<K, N>(a, rng, z, found, base, depths, cnt, delivered);
+            if (l == 0) sd_store<N>(a, (int)(idx % (uint32_t)a.sdW), (int)(idx / (uint32_t)a.sdW), depths);
+        }
+    }
+    if (a.counters && l == 0 && delivered) atomicAdd(&a.counters[4], (unsigned long long)delivered);
 }
 
 // ------------------------------------------------------------------------------------
@@ -746,25 +1214,39 @@ __global__ void __launch_bounds__(kBlock) gbuffer_kernel(GBArgs a) {
 // ------------------------------------------------------------------------------------
 // launchers
 // ------------------------------------------------------------------------------------
+// walk: 0 = quad (depth-first), 1 = row walk + in-kernel algorithm, 2 = split (row walk ->
+// keys -> resolve kernel)
 template <int K, int N>
-static hipError_t launch_sd_kn(const SDArgs& a, dim3 grid, uint32_t persistentBlocks, uint32_t* queue, uint32_t* qctl,
-                               hipStream_t s) {
+static hipError_t launch_sd_kn(const SDArgs& a, dim3 grid, uint32_t persistentBlocks, float4* queue, uint32_t* qctl,
+                               uint2* keys, int walk, hipStream_t s) {
+    constexpr int ROW = K <= 8 ? 8 : 16;
     hipLaunchKernelGGL((sd_setup_kernel<N>), grid, dim3(kBlock), 0, s, a, queue, qctl);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((sd_trace_queue_kernel<K, N>), dim3(persistentBlocks), dim3(kBlock), 0, s, a, queue, qctl);
+    const dim3 pg(persistentBlocks), wb(kBlock);
+    if (walk == 2) {
+        if (a.counters) hipLaunchKernelGGL((sd_trace_row_kernel<K, N, ROW, true, true>), pg, wb, 0, s, a, queue, qctl, keys);
+        else hipLaunchKernelGGL((sd_trace_row_kernel<K, N, ROW, true, false>), pg, wb, 0, s, a, queue, qctl, keys);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        hipLaunchKernelGGL((sd_resolve_row_kernel<K, N, ROW>), pg, wb, 0, s, a, queue, qctl, keys);
+    } else if (walk == 1) {
+        if (a.counters) hipLaunchKernelGGL((sd_trace_row_kernel<K, N, ROW, false, true>), pg, wb, 0, s, a, queue, qctl, keys);
+        else hipLaunchKernelGGL((sd_trace_row_kernel<K, N, ROW, false, false>), pg, wb, 0, s, a, queue, qctl, keys);
+    } else {
+        hipLaunchKernelGGL((sd_trace_queue_kernel<K, N>), dim3(persistentBlocks), dim3(kBlock), 0, s, a, queue, qctl);
+    }
     return hipGetLastError();
 }
 
 template <int K>
-static hipError_t launch_sd_k(const SDArgs& a, uint32_t N, dim3 grid, uint32_t pb, uint32_t* q, uint32_t* qc,
-                              hipStream_t s) {
+static hipError_t launch_sd_k(const SDArgs& a, uint32_t N, dim3 grid, uint32_t pb, float4* q, uint32_t* qc, uint2* keys,
+                              int walk, hipStream_t s) {
     switch (N) {
-        case 1: return launch_sd_kn<K, 1>(a, grid, pb, q, qc, s);
-        case 2: return launch_sd_kn<K, 2>(a, grid, pb, q, qc, s);
-        case 4: return launch_sd_kn<K, 4>(a, grid, pb, q, qc, s);
-        case 8: return launch_sd_kn<K, 8>(a, grid, pb, q, qc, s);
-        case 16: return launch_sd_kn<K, 16>(a, grid, pb, q, qc, s);
+        case 1: return launch_sd_kn<K, 1>(a, grid, pb, q, qc, keys, walk, s);
+        case 2: return launch_sd_kn<K, 2>(a, grid, pb, q, qc, keys, walk, s);
+        case 4: return launch_sd_kn<K, 4>(a, grid, pb, q, qc, keys, walk, s);
+        case 8: return launch_sd_kn<K, 8>(a, grid, pb, q, qc, keys, walk, s);
+        case 16: return launch_sd_kn<K, 16>(a, grid, pb, q, qc, keys, walk, s);
         default: return hipErrorInvalidValue;
     }
 }
@@ -887,7 +1369,7 @@ extern "C" rsd_status rsd_sd_trace_band(rsd_scene* scene, const rsd_camera* cam,
     }
     hipStream_t s = (hipStream_t)stream;
     if (counters) {
-        RSD_HIP(hipMemsetAsync(scene->d_counters, 0, 10 * sizeof(unsigned long long), s));
+        RSD_HIP(hipMemsetAsync(scene->d_counters, 0, 16 * sizeof(unsigned long long), s));
         a.counters = scene->d_counters;
     }
     const uint32_t tiles = (sd_h + kTile - 1) / kTile;
@@ -897,25 +1379,48 @@ extern "C" rsd_status rsd_sd_trace_band(rsd_scene* scene, const rsd_camera* cam,
     const uint32_t need = p->implementation == RSD_SD_COVERAGE_MASK ? 8u : p->max_count;
     // live-ray queue workspace (grow-only; the first call of a larger map allocates)
     const size_t need_q = ((size_t)(sd_w + kTile - 1) / kTile * ((sd_h + kTile - 1) / kTile) + kQueueParts) * kBlock;
-    if (scene->queue_cap < need_q) {
+    const uint32_t K = need <= 4 ? 4u : (need <= 8 ? 8u : 16u);
+    // split walk (trace -> keys -> resolve) when one chunk of K keys decides every texel
+    const bool split = p->implementation != RSD_SD_COVERAGE_MASK && p->max_count <= K;
+    const size_t queueBytes = need_q * 32, keyBytes = split ? need_q * K * sizeof(uint2) : 0;
+    if (scene->queue_cap < queueBytes + keyBytes) {
         RSD_HIP(hipStreamSynchronize(s));
         (void)hipFree(scene->d_queue);
         scene->d_queue = nullptr;
-        RSD_HIP(hipMalloc(&scene->d_queue, need_q * sizeof(uint32_t)));
-        scene->queue_cap = need_q;
+        RSD_HIP(hipMalloc(&scene->d_queue, queueBytes + keyBytes));
+        scene->queue_cap = queueBytes + keyBytes;
     }
+    float4* queue = reinterpret_cast<float4*>(scene->d_queue);
+    uint2* keys = reinterpret_cast<uint2*>(reinterpret_cast<char*>(scene->d_queue) + queueBytes);
     RSD_HIP(hipMemsetAsync(scene->d_qctl, 0, 2 * kQueueParts * sizeof(uint32_t), s));
     const uint32_t setupBlocks = grid.x * grid.y;
     a.partCap = (setupBlocks + kQueueParts - 1) / kQueueParts * (uint32_t)kBlock;
-    const uint32_t pb = ((uint32_t)std::max(1, scene->dev->cu_count) * 8u + kQueueParts - 1) / kQueueParts * kQueueParts;
+    // traversal walk: row-parallel (default) unless the tree is too deep for its LDS pool
+    // bound (kPoolCap >= poolSoft + 48 + 3 * depth), or RSD_TRACE_WALK=quad asks for the
+    // depth-first quad walk (A/B measurements)
+    const int depth = (int)std::max(1u, scene->stats.wide_depth);
+    a.poolSoft = std::min(kPoolCap - 48 - 3 * depth, 160);
+    static const char* walkEnv = std::getenv("RSD_TRACE_WALK");
+    const std::string walkName = walkEnv ? walkEnv : "";
+    const bool rowWalk = a.poolSoft >= 16 && walkName != "quad";
+    // default: the split row walk (trace -> keys -> resolve) where one chunk of K keys decides
+    // every texel, else the fused row walk; RSD_TRACE_WALK=fused|quad for A/B runs
+    const int walk = !rowWalk ? 0 : (split && walkName != "fused") ? 2 : 1;
+    // persistent waves: 8 per CU.  At 1080p/4 every row gets one of the ~22 K live rays in its
+    // static first slot and the launch lasts as long as the slowest ray; 16 waves per CU (the
+    // split walk holds < 128 VGPRs) measured no faster (tools/sd_time.py sweep)
+    static const char* wpcEnv = std::getenv("RSD_TRACE_WAVES_PER_CU");  // experiments only
+    const uint32_t wavesPerCu = wpcEnv ? (uint32_t)std::max(1, std::atoi(wpcEnv)) : 8u;
+    const uint32_t pb = ((uint32_t)std::max(1, scene->dev->cu_count) * wavesPerCu + kQueueParts - 1) / kQueueParts *
+                        kQueueParts;
     hipError_t e = hipSuccess;
     if (bandTiles == 0) {}
-    else if (need <= 4) e = launch_sd_k<4>(a, N, grid, pb, scene->d_queue, scene->d_qctl, s);
-    else if (need <= 8) e = launch_sd_k<8>(a, N, grid, pb, scene->d_queue, scene->d_qctl, s);
-    else e = launch_sd_k<16>(a, N, grid, pb, scene->d_queue, scene->d_qctl, s);
+    else if (K == 4) e = launch_sd_k<4>(a, N, grid, pb, queue, scene->d_qctl, keys, walk, s);
+    else if (K == 8) e = launch_sd_k<8>(a, N, grid, pb, queue, scene->d_qctl, keys, walk, s);
+    else e = launch_sd_k<16>(a, N, grid, pb, queue, scene->d_qctl, keys, walk, s);
     if (e != hipSuccess) return hip_fail(e, "sd_trace_kernel launch");
     if (counters) {
-        unsigned long long h[10];
+        unsigned long long h[16];
         RSD_HIP(hipMemcpyAsync(h, scene->d_counters, sizeof(h), hipMemcpyDeviceToHost, s));
         RSD_HIP(hipStreamSynchronize(s));
         counters->rays_dispatched = h[0];
@@ -928,6 +1433,13 @@ extern "C" rsd_status rsd_sd_trace_band(rsd_scene* scene, const rsd_camera* cam,
         counters->sum_ray_clocks = h[7];
         counters->max_ray_clocks = h[8];
         counters->leaves_visited = h[9];
+        if (const char* dbg = std::getenv("RSD_TRACE_PHASES"))
+            if (*dbg) std::fprintf(stderr, "[rsd] row walk phase clocks: fetch %llu step %llu resolve %llu steps %llu loops %llu\n",
+                                   h[11], h[12], h[13], h[14], h[15]);
+        if (h[10]) {  // the pool bound was violated: results of this trace are not reliable
+            set_error("rsd_sd_trace: traversal pool overflow (BVH deeper than the row walk supports)");
+            return RSD_ERR_HIP;
+        }
     }
     return RSD_OK;
 }
