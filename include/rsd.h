@@ -112,7 +112,7 @@ typedef struct {
 typedef struct {
     uint32_t num_directions;       /* NUM_DIRECTIONS (8) */
     uint32_t sd_samples;           /* MSAA_SAMPLES = SD N */
-    uint32_t secondary_depth_mode; /* DepthMode: 0 SingleDepth, 2 StochasticDepth */
+    uint32_t secondary_depth_mode; /* DepthMode: 0 SingleDepth, 2 StochasticDepth, 3 Raytraced */
     uint32_t ray_interval;         /* USE_RAY_INTERVAL */
     uint32_t sd_jitter;            /* SD_JITTER */
     uint32_t guard_band;           /* dict["guardBand"] from the GuardBand pass */
@@ -197,6 +197,18 @@ rsd_status rsd_svao_pass2(const rsd_camera* cam, const rsd_vao_data* vao, const 
                           const uint8_t* d_stencil, const float* d_sd, uint32_t sd_w, uint32_t sd_h,
                           uint8_t* d_ao, rsd_stream stream);
 
+/* "AO 2" in SecondaryDepthMode::Raytraced (the ground-truth AO of
+ * scripts/SVAO_depth.py and SAVO_record.py): calcAO2 DEPTH_MODE_RAYTRACING (Common.slang:598-651)
+ * with aoAnyHit (:679-718) over the canonical ascending hit stream.  Replaces the RayQuery
+ * compute pass (SVAORaster2.ps.slang:9-65, SVAO.cpp:432-455; ray_pipeline = 0: visible pixels)
+ * and the ray pipeline (Ray.rt.slang, SVAO.cpp:408-431; ray_pipeline = 1: the rayGen grid covers
+ * the frame from the guard band to the right/bottom edge).  Pass 1 must have run with
+ * secondary_depth_mode = 3.  cull_mode: SVAO's CULL_MODE_RAY_FLAG (rsd_cull_mode). */
+rsd_status rsd_svao_pass2_raytraced(rsd_scene* scene, const rsd_camera* cam, const rsd_vao_data* vao,
+                                    const rsd_svao_params* params, const float* d_depth, const uint16_t* d_normals,
+                                    uint32_t width, uint32_t height, const uint8_t* d_stencil, uint8_t* d_ao,
+                                    uint32_t cull_mode, uint32_t ray_pipeline, rsd_stream stream);
+
 /* --- screen-band sharding (multi-GPU) ----------------------------------
  * Band b of B owns: pass-1/pass-2 rows whose 32-row group g (counted from the first
  * visible row, SVAORaster.ps.slang:36 interleave) has g % B == b, and SD-map 8-row tile
@@ -216,6 +228,13 @@ rsd_status rsd_svao_pass2_band(const rsd_camera* cam, const rsd_vao_data* vao, c
                                const float* d_depth, const uint16_t* d_normals, uint32_t width, uint32_t height,
                                const uint8_t* d_stencil, const float* d_sd, uint32_t sd_w, uint32_t sd_h,
                                uint8_t* d_ao, uint32_t band_index, uint32_t band_count, rsd_stream stream);
+
+rsd_status rsd_svao_pass2_raytraced_band(rsd_scene* scene, const rsd_camera* cam, const rsd_vao_data* vao,
+                                         const rsd_svao_params* params, const float* d_depth,
+                                         const uint16_t* d_normals, uint32_t width, uint32_t height,
+                                         const uint8_t* d_stencil, uint8_t* d_ao, uint32_t cull_mode,
+                                         uint32_t ray_pipeline, uint32_t band_index, uint32_t band_count,
+                                         rsd_stream stream);
 
 #ifdef __cplusplus
 }

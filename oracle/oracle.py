@@ -80,6 +80,7 @@ def lib():
         L.ocpu_svao_pass2_band.argtypes = [vp, vp, vp, vp, vp, u32, u32, vp, vp, u32, u32, vp, u32, u32, i32]
         L.ocpu_svao_pass1.argtypes = [vp, vp, vp, vp, vp, u32, u32, vp, vp, vp, vp, u32, u32]
         L.ocpu_svao_pass2.argtypes = [vp, vp, vp, vp, vp, u32, u32, vp, vp, u32, u32, vp, i32]
+        L.ocpu_svao_pass2_rt_band.argtypes = [vp, vp, vp, vp, vp, vp, u32, u32, vp, vp, u32, u32, u32, u32, i32]
         L.ocpu_hash.restype = f32
         L.ocpu_hash.argtypes = [f32, f32]
         L.ocpu_jitter.argtypes = [u32, u32, vp, vp]
@@ -202,6 +203,17 @@ def svao_pass2(cam, vao: VAOData, p: SVAOParams, depth, normals, stencil, sd, ao
     sdc = np.ascontiguousarray(sd, np.float32)
     lib().ocpu_svao_pass2(C.byref(cam), C.byref(vao), C.byref(p), _p(depth), _p(normals), W, H,
                           _p(stencil), _p(sdc), sdW, sdH, _p(ao), _threads(threads))
+    return ao
+
+
+def svao_pass2_raytraced(scene: Scene, cam, vao: VAOData, p: SVAOParams, depth, normals, stencil, ao, cull=1,
+                         ray_pipeline=0, band=(0, 1), threads=None):
+    """SVAO "AO 2" in the Raytraced secondary mode; returns the updated AO image."""
+    H, W = depth.shape
+    ao = np.array(ao, np.uint8, copy=True)
+    lib().ocpu_svao_pass2_rt_band(scene.h, C.byref(cam), C.byref(vao), C.byref(p), _p(depth), _p(normals), W, H,
+                                  _p(np.ascontiguousarray(stencil, np.uint8)), _p(ao), cull, ray_pipeline, band[0],
+                                  band[1], _threads(threads))
     return ao
 
 

@@ -470,7 +470,7 @@ static int o_box(const oray* r, const onode* n, double tmin, double tmax)
 }
 
 /* ------------------------------------------------------------------ hit collection */
-typedef struct { float t, u, v; uint32_t prim; } ohit;
+typedef struct { float t, u, v; uint32_t prim; float det; } ohit;
 
 typedef struct {
     ohit* h;
@@ -523,7 +523,7 @@ static void o_collect(const oscene* s, const oray* r, float TMin, float TMax, ui
                 if (!o_intersect_tri(r, v, v + 3, v + 6, &t, &u, &vv, &det)) continue;
                 if (!(t >= TMin && t <= TMax)) continue;
                 if (o_culled(det, s->flags[prim], cull)) continue;
-                ohit x = {t, u, vv, prim};
+                ohit x = {t, u, vv, prim, det};
                 o_hits_push(hs, x);
             }
         } else {
@@ -1075,9 +1075,10 @@ void ocpu_svao_pass1_band(const ocam* cam, const ovao* d, const osvao_params* p,
                         aoOut += (s.sphereStart - s.sphereEnd) / s.pdf;
                         continue;
                     }
+                    /* SVAORaster.ps.slang:62-66: Raytraced mode with TRACE_OUT_OF_SCREEN (SVAO.h:104) */
+                    int forceRay = p->secondary_depth_mode == 3 && !s.isInScreen;
                     o_eval_primary(&x, &b, &s);
                     aoOut += s.visibility;
-                    int forceRay = 0;
                     if (!s.isInScreen && d->sdGuard > 0) {
                         forceRay = 1;
                         s.objectSpaceZ = O_FLT_MAX;
@@ -1197,5 +1198,123 @@ void ocpu_svao_pass2_band(const ocam* cam, const ovao* d, const osvao_params* p,
         jobs[i].bi = band_index; jobs[i].bc = band_count ? band_count : 1;
     }
     o_run_rows(o_pass2_rows, jobs, sizeof(op2_job), p->guard_band, H - p->guard_band, nthreads, o_p2_setrows);
+    free(jobs);
+}
+
+/* ------------------------------------------------------------------ SVAO pass 2, Raytraced */
+/* calcAO2 DEPTH_MODE_RAYTRACING (Common.slang:598-651), traceAORay (SVAORaster2.ps.slang:9-46,
+ * Ray.rt.slang:46-58) and aoAnyHit (Common.slang:679-718, VAO kernel), replayed literally over
+ * the canonical any-hit stream: every hit in [TMin, TMax] (culling applied) in ascending
+ * (t, prim) order, TMax shrinking on a commit. */
+typedef struct {
+    const oscene* s; const octx* x; const uint8_t* stencil; uint8_t* ao;
+    uint32_t cull, rayPipeline;
+    float invView[9];
+    uint32_t y0, y1, bi, bc;
+} ort_job;
+
+static void* o_pass2_rt_rows(void* arg)
+{
+    ort_job* j = (ort_job*)arg;
+    const octx* x = j->x;
+    const ovao* d = x->d;
+    const ocam* c = x->c;
+    const uint32_t g = x->p->guard_band, W = x->W, H = x->H;
+    const uint32_t xEnd = j->rayPipeline ? W : W - g; /* SVAO.cpp:429-430 vs :452-453 */
+    (void)H;
+    for (uint32_t py = j->y0; py < j->y1; ++py)
+        for (uint32_t px = g; px < xEnd; ++px) {
+            if (((py - g) / 32u) % j->bc != j->bi) break;
+            size_t o = (size_t)py * W + px;
+            uint32_t mask = j->stencil[o];
+            if (mask == 0) continue;
+            float u = ((float)px + 0.5f) * d->invResolution[0];
+            float v = ((float)py + 0.5f) * d->invResolution[1];
+            obasic b;
+            o_basic_init(x, u, v, &b);
+            float vis = 0.0f;
+            for (uint32_t i = 0; i < 8; ++i) {
+                if (!(mask & (1u << i))) continue;
+                osample s;
+                o_sample_init(x, u, v, &b, i, &s);
+                o_eval_primary(x, &b, &s);
+                vis -= s.visibility;
+                /* getSnappedUV(samplePosUV): Common.slang:116-125, no clamp */
+                float suv[2] = {(floorf(s.samplePosUV[0] * d->resolution[0]) + 0.5f) / d->resolution[0],
+                                (floorf(s.samplePosUV[1] * d->resolution[1]) + 0.5f) / d->resolution[1]};
+                float pv[3], dv[3], dw[3];
+                o_uv_to_view(x, suv[0], suv[1], 1.0f, pv);
+                o_normalize(pv, dv);
+                for (int k = 0; k < 3; ++k)
+                    dw[k] = j->invView[k * 3 + 0] * dv[0] + j->invView[k * 3 + 1] * dv[1] + j->invView[k * 3 + 2] * dv[2];
+                const float L = s.initialSamplePosLength, pl = b.posVLength;
+                /* RayData init, Common.slang:614-620 */
+                float halo = (pl - s.sphereStart - b.radius - d->thickness * b.radius) * L / pl;
+                float inside = (pl - s.sphereEnd) * L / pl;
+                const float tCRS = (pl - b.radius - d->thickness * b.radius) * L / pl;
+                const float tSS = (pl - s.sphereStart) * L / pl;
+                float TMin = o_max(halo, 0.0f), TMax = inside;
+                if (!s.isInScreen) { s.visibility = 1.0f; s.objectSpaceZ = O_FLT_MAX; } /* resetSample */
+                const float eps = b.radius * 0.01f;
+                if (s.isInScreen) TMin = o_max(TMin, (pl - s.objectSpaceZ) * L / pl + eps);
+                if (TMin <= TMax) {
+                    oray r;
+                    o_ray_setup(&r, c->posW, dw);
+                    ohits hs = {0};
+                    o_collect(j->s, &r, TMin, TMax, j->cull, &hs);
+                    for (uint32_t k = 0; k < hs.n; ++k) {
+                        const float t = hs.h[k].t;
+                        if (t > TMax) break;          /* beyond a committed hit */
+                        if (t < halo) continue;       /* SVAORaster2.ps.slang:27-28 */
+                        const uint32_t fl = j->s->flags[hs.h[k].prim];
+                        const int front = (hs.h[k].det > 0.0f) != ((fl & 2u) != 0u);
+                        if (!(front || (fl & 1u) || (fl & 4u))) continue; /* Common.slang:695-697 */
+                        if (t <= tSS) {
+                            halo = o_max(halo, t);
+                            if (t >= tCRS) break;     /* AO_HIT_ACCEPT_AND_END */
+                        } else {
+                            inside = o_min(inside, t); /* AO_HIT_ACCEPT: commit */
+                            TMax = t;
+                        }
+                    }
+                    free(hs.h);
+                }
+                /* Common.slang:641-644 */
+                float sphereVis = o_calc_visibility(d, pl - inside * pl / L, s.sphereStart, s.sphereEnd, s.pdf, b.radius);
+                float haloVis = o_saturate((pl - halo * pl / L - (1.0f + d->thickness) * b.radius) / s.sphereStart) *
+                                (s.sphereStart - s.sphereEnd) / s.pdf;
+                s.visibility = o_min(s.visibility, o_min(sphereVis, haloVis));
+                vis += s.visibility;
+            }
+            vis *= 1.0f / 8.0f;
+            vis *= 2.0f;
+            vis += o_unorm8_to_float(j->ao[o]);
+            vis = o_pow(vis, d->exponent);
+            j->ao[o] = o_unorm8(vis);
+        }
+    return NULL;
+}
+
+static void o_rt_setrows(void* j, uint32_t a, uint32_t b) { ((ort_job*)j)->y0 = a; ((ort_job*)j)->y1 = b; }
+
+void ocpu_svao_pass2_rt_band(const oscene* sc, const ocam* cam, const ovao* d, const osvao_params* p,
+                             const float* depth, const uint16_t* normals, uint32_t W, uint32_t H,
+                             const uint8_t* stencil, uint8_t* ao, uint32_t cull, uint32_t ray_pipeline,
+                             uint32_t band_index, uint32_t band_count, int nthreads)
+{
+    octx x;
+    o_ctx_init(&x, cam, d, p, depth, normals, W, H);
+    if (nthreads < 1) nthreads = 1;
+    ort_job* jobs = (ort_job*)calloc((size_t)nthreads, sizeof(ort_job));
+    for (int i = 0; i < nthreads; ++i) {
+        jobs[i].s = sc; jobs[i].x = &x; jobs[i].stencil = stencil; jobs[i].ao = ao;
+        jobs[i].cull = cull; jobs[i].rayPipeline = ray_pipeline;
+        /* float3x3(inverse(viewMat)) = transpose of the view rotation (rigid view matrix) */
+        for (int r = 0; r < 3; ++r)
+            for (int k = 0; k < 3; ++k) jobs[i].invView[r * 3 + k] = cam->viewMat[k * 4 + r];
+        jobs[i].bi = band_index; jobs[i].bc = band_count ? band_count : 1;
+    }
+    const uint32_t g = p->guard_band, yEnd = ray_pipeline ? H : H - g;
+    o_run_rows(o_pass2_rt_rows, jobs, sizeof(ort_job), g, yEnd, nthreads, o_rt_setrows);
     free(jobs);
 }

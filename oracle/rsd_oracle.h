@@ -158,6 +158,12 @@ void ocpu_decode_normal_2x8(uint32_t packed, float out[3]);
 int ocpu_intersect(const float o[3], const float d[3], const float v0[3], const float v1[3],
                    const float v2[3], float* t, float* u, float* v, float* det);
 
+/* SVAO pass 2 in SecondaryDepthMode::Raytraced (Common.slang:598-651, aoAnyHit :679-718) */
+void ocpu_svao_pass2_rt_band(const oscene* sc, const ocam* cam, const ovao* d, const osvao_params* p,
+                             const float* depth, const uint16_t* normals, uint32_t W, uint32_t H,
+                             const uint8_t* stencil, uint8_t* ao, uint32_t cull, uint32_t ray_pipeline,
+                             uint32_t band_index, uint32_t band_count, int nthreads);
+
 #ifdef __cplusplus
 }
 #endif

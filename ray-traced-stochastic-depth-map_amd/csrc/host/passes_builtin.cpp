@@ -257,15 +257,18 @@ public:
         cull_ = toRsdCull(enumProp(p, "cullMode", kCullNames, 2));
         directions_ = (uint32_t)p.getInt("sampleCount", 8);
         impl_ = enumProp(p, "stochImplementation", kImplNames, 0);
+        rayPipeline_ = p.getBool("rayPipeline", true);  // SVAO.h:101
     }
     void checkSupported() const {
         if (primary_ != 0) throw Unsupported("SVAO: primaryDepthMode other than SingleDepth is not implemented");
-        if (secondary_ != 0 && secondary_ != 2)
-            throw Unsupported("SVAO: secondaryDepthMode DualDepth/Raytraced is not implemented (SURVEY 8(f))");
+        if (secondary_ == 1) throw Unsupported("SVAO: secondaryDepthMode DualDepth is not implemented (SURVEY 8(f))");
         if (dualAo_) throw Unsupported("SVAO: dualAO is not implemented");
     }
     void sdSize(uint32_t w, uint32_t h, rsd_vao_data* vao, uint32_t* sw, uint32_t* sh) const {
-        check(rsd_svao_make_vao_data(w, h, divisor_, guardPx_, radius_, exponent_, thickness_, vao, sw, sh), "SVAO");
+        // getExtraGuardBand (SVAO.cpp:718-723): only the StochasticDepth mode has an SD guard band
+        check(rsd_svao_make_vao_data(w, h, divisor_, secondary_ == 2 ? guardPx_ : 0, radius_, exponent_, thickness_, vao,
+                                     sw, sh),
+              "SVAO");
     }
     Reflection reflect(const CompileData& cd) override {
         checkSupported();  // reported when the graph is planned, before any device work
@@ -348,6 +351,13 @@ public:
                              (uint32_t*)rmax->ptr, sdW_, sdH_, ctx.stream),
               "SVAO AO 1");
         if (secondary_ == 0) return;  // SVAO.cpp:355
+        if (secondary_ == 3) {  // SVAO.cpp:408-455: refine by tracing the scene
+            check(rsd_svao_pass2_raytraced(s->scene, &s->camera, &vao_, &svp_, (const float*)depth->ptr,
+                                           (const uint16_t*)normals->ptr, width_, height_, (const uint8_t*)stencil->ptr,
+                                           (uint8_t*)ao->ptr, cull_, rayPipeline_ ? 1u : 0u, ctx.stream),
+                  "SVAO AO 2 (raytraced)");
+            return;
+        }
         // SVAO.cpp:364-390: the nested graph traces the stochastic depth map
         sdGraph_->setInput("StochasticDepthMap.linearZ", depth);
         sdGraph_->setInput("StochasticDepthMap.rayMin", rmin);
@@ -368,7 +378,7 @@ private:
     float radius_, exponent_, thickness_;
     uint32_t primary_, secondary_, divisor_, samples_, maxCount_, cull_, directions_, impl_;
     int32_t guardPx_;
-    bool dualAo_, alphaTest_, jitter_, rayInterval_;
+    bool dualAo_, alphaTest_, jitter_, rayInterval_, rayPipeline_;
     uint32_t width_ = 0, height_ = 0, sdW_ = 0, sdH_ = 0;
     rsd_vao_data vao_{};
     rsd_svao_params svp_{};

@@ -1,0 +1,210 @@
+// svao_math.h -- SVAO per-pixel math shared by the "AO 1" / "AO 2" kernels (svao.hip) and the
+// Raytraced secondary mode (svao_rt.hip).
+//
+// Reference: SVAO/Common.slang:98-496 (BasicAOData, SampleAOData, visibility terms, UV/view
+// conversions), SVAO.cpp:663-688 (noise texture).  Numerics contract: rsd_device.h.
+#pragma once
+#include <cmath>
+#include <string>
+
+#include "rsd_device.h"
+#include "rsd_internal.h"
+
+namespace rsd {
+
+struct SvaoConsts {
+    float sinNoise[16], cosNoise[16];
+    float sinDir[8], cosDir[8];
+    float sampleRadius[8];
+};
+
+struct SvaoArgs {
+    rsd_camera cam;
+    rsd_vao_data d;
+    SvaoConsts k;
+    const float* depth;
+    const uint16_t* normals;
+    int W, H;
+    uint8_t* ao;
+    uint8_t* stencil;
+    uint32_t* rayMin;
+    uint32_t* rayMax;
+    const float* sd;
+    int sdW, sdH;
+    uint32_t guard, secondary, rayInterval, sdJitter, N;
+    uint32_t bandIndex, bandCount;  // 32-row groups g (offset space) with g % count == index
+    float isx, isy;  // imageScale (Common.slang:142), hoisted: 0.5 * (frameW / focal), same bits
+};
+
+struct Basic {
+    f3 posV;
+    float posVLength;
+    f3 normal, tangent, bitangent, normalO, normalV;
+    float radiusInPixels, radius;
+};
+
+struct Sample {
+    float sphereStart, sphereEnd, pdf;
+    bool isInScreen;
+    float su, sv;  // samplePosUV
+    float ru, rv;  // rasterSamplePosUV
+    float visibility, objectSpaceZ;
+    f3 ip;  // initialSamplePosV (the Raytraced mode needs its length)
+};
+
+__device__ __forceinline__ f3 uv_to_view(const SvaoArgs& a, float u, float v, float z) {
+    const float ndcx = u * 2.0f - 1.0f, ndcy = (1.0f - v) * 2.0f - 1.0f;
+    return mk(ndcx * z * a.isx, ndcy * z * a.isy, -z);
+}
+
+__device__ __forceinline__ void view_to_uv(const SvaoArgs& a, f3 p, float& u, float& v) {
+    const float ndcx = p.x / (a.isx * p.z), ndcy = p.y / (a.isy * p.z);
+    u = ndcx * -0.5f + 0.5f;
+    v = ndcy * 0.5f + 0.5f;
+}
+
+__device__ __forceinline__ float depth_sample(const SvaoArgs& a, float u, float v) {
+    return tex_bilinear(a.depth, a.W, a.H, u, v, false);  // gTextureSampler: linear, clamp
+}
+
+// Common.slang:285-324
+__device__ __forceinline__ bool basic_init(const SvaoArgs& a, float u, float v, Basic& b) {
+    const rsd_vao_data& d = a.d;
+    const float z = depth_sample(a, u, v);
+    const float rux = (d.radius * a.cam.focalLength) / (a.cam.frameWidth * z);
+    const float ruy = (d.radius * a.cam.focalLength) / (a.cam.frameHeight * z);
+    const float pa = rux * d.resolution[0], pb = ruy * d.resolution[1];
+    b.radiusInPixels = pa + 0.5f * (pb - pa);
+    b.radius = d.radius;
+    const float maxRadius = d.ssMaxRadius;
+    if (b.radiusInPixels > maxRadius) {
+        b.radius = b.radius / b.radiusInPixels * maxRadius;
+        b.radiusInPixels = maxRadius;
+    }
+    if (b.radiusInPixels < 0.5f) return false;
+    b.posV = uv_to_view(a, u, v, z);
+    b.posVLength = length(b.posV);
+    const uint32_t ix = (uint32_t)(u * d.resolution[0]), iy = (uint32_t)(v * d.resolution[1]);
+    const uint32_t packed = (ix < (uint32_t)a.W && iy < (uint32_t)a.H) ? a.normals[(size_t)iy * a.W + ix] : 0u;
+    b.normalV = decode_normal_2x8(packed);
+    if (dot(b.posV, b.normalV) > 0.0f) b.normalV = -b.normalV;
+    const float nu = u * d.noiseScale[0], nv = v * d.noiseScale[1];
+    const int ni = ((int)floorf(nu * 4.0f)) & 3, nj = ((int)floorf(nv * 4.0f)) & 3;
+    const f3 rd = mk(a.k.sinNoise[nj * 4 + ni], a.k.cosNoise[nj * 4 + ni], 0.0f);
+    b.normal = mk(-b.posV.x / b.posVLength, -b.posV.y / b.posVLength, -b.posV.z / b.posVLength);
+    b.bitangent = normalize(cross(b.normal, rd));
+    b.tangent = cross(b.bitangent, b.normal);
+    b.normalO = mk(dot(b.normalV, b.tangent), dot(b.normalV, b.bitangent), dot(b.normalV, b.normal));
+    return true;
+}
+
+__device__ __forceinline__ float make_nonzero(float v, float eps) {
+    const float av = hmax(fabsf(v), eps);
+    return v >= 0.0f ? av : -av;
+}
+
+// Common.slang:354-399 (VAO kernel)
+__device__ __forceinline__ bool sample_init(const SvaoArgs& a, float u, float v, const Basic& b, int i, Sample& s,
+                                            float& screenSpaceRadius) {
+    const rsd_vao_data& d = a.d;
+    const float radius = a.k.sampleRadius[i] * b.radius;
+    const float dx = radius * a.k.sinDir[i], dy = radius * a.k.cosDir[i];
+    const float sphereHeight = sqrtf(b.radius * b.radius - radius * radius);
+    s.pdf = 2.0f * sphereHeight;
+    s.sphereStart = sphereHeight;
+    const float zi = -(dx * b.normalO.x + dy * b.normalO.y) / make_nonzero(b.normalO.z, 0.0001f);
+    s.sphereEnd = hmin(hmax(zi, -sphereHeight), sphereHeight);
+    if ((s.sphereStart - s.sphereEnd) / (2.0f * sphereHeight) <= 0.1f) return false;
+    const f3 ip = b.posV + b.tangent * dx + b.bitangent * dy;
+    s.ip = ip;
+    view_to_uv(a, ip, s.su, s.sv);
+    s.visibility = 0.0f;
+    s.objectSpaceZ = 0.0f;
+    const float ex = (u - s.su) * d.resolution[0], ey = (v - s.sv) * d.resolution[1];
+    screenSpaceRadius = sqrtf(ex * ex + ey * ey);
+    const float cu = saturate(s.su), cv = saturate(s.sv);
+    s.isInScreen = (s.su == cu) && (s.sv == cv);
+    s.ru = (floorf(cu * d.resolution[0]) + 0.5f) / d.resolution[0];
+    s.rv = (floorf(cv * d.resolution[1]) + 0.5f) / d.resolution[1];
+    return true;
+}
+
+// Common.slang:180-184 calcHaloVisibility (HALO_RADIUS = sphereStart, Common.slang:38)
+__device__ __forceinline__ float calc_halo_visibility(const rsd_vao_data& d, float oz, float ss, float se, float pdf,
+                                                      float radius) {
+    return saturate((oz - (1.0f + d.thickness) * radius) / ss) * (ss - se) / pdf;
+}
+
+// Common.slang:180-196
+__device__ __forceinline__ float calc_visibility(const rsd_vao_data& d, float oz, float ss, float se, float pdf,
+                                                 float radius) {
+    const float sphere = hmax(ss - hmax(se, oz), 0.0f) / pdf;
+    const float halo = saturate((oz - (1.0f + d.thickness) * radius) / ss) * (ss - se) / pdf;
+    return sphere + halo;
+}
+
+// Common.slang:463-483
+__device__ __forceinline__ void add_sample(const SvaoArgs& a, const Basic& b, Sample& s, f3 spV, bool init) {
+    const float oz = dot(spV - b.posV, b.normal);
+    s.objectSpaceZ = init ? oz : hmin(s.objectSpaceZ, oz);
+    const float vis = calc_visibility(a.d, oz, s.sphereStart, s.sphereEnd, s.pdf, b.radius);
+    s.visibility = init ? vis : hmin(s.visibility, vis);
+}
+
+// Common.slang:492-496
+__device__ __forceinline__ void eval_primary(const SvaoArgs& a, const Basic& b, Sample& s) {
+    const float z = depth_sample(a, s.ru, s.rv);
+    add_sample(a, b, s, uv_to_view(a, s.ru, s.rv, z), true);
+}
+
+// Common.slang:164-168
+__device__ __forceinline__ int uv_to_sd(float uv, float low, int guard) {
+    const int p = (int)floorf(uv * low) + guard;
+    const int hi = (int)low + guard * 2 - 1;
+    return p < 0 ? 0 : (p > hi ? hi : p);
+}
+
+inline void fill_scale(SvaoArgs& a) {
+    // Common.slang:142/150 imageScale, evaluated once on the host (IEEE float, same bits)
+    a.isx = 0.5f * (a.cam.frameWidth / a.cam.focalLength);
+    a.isy = 0.5f * (a.cam.frameHeight / a.cam.focalLength);
+}
+
+inline void fill_consts(SvaoConsts& k) {
+    // SVAO.cpp:670-684 -> R8Unorm noise; Common.slang:311-312 randRotation, :357 alpha
+    static const float dither[16] = {0.0f, 8.0f, 2.0f, 10.0f, 12.0f, 4.0f, 14.0f, 6.0f,
+                                     3.0f, 11.0f, 1.0f, 9.0f, 15.0f, 7.0f, 13.0f, 5.0f};
+    for (int i = 0; i < 16; ++i) {
+        const uint8_t byte = (uint8_t)(dither[i] / 16.0f * 255.0f);
+        const float rr = (float)byte / 255.0f * 2.0f * 3.141f;
+        k.sinNoise[i] = (float)std::sin((double)rr);
+        k.cosNoise[i] = (float)std::cos((double)rr);
+    }
+    static const float radius8[8] = {0.917883f, 0.564429f, 0.734504f, 0.359545f,
+                                     0.820004f, 0.470149f, 0.650919f, 0.205215f};  // Common.slang:53
+    for (int i = 0; i < 8; ++i) {
+        const float al = ((float)i / 8.0f) * 2.0f * 3.141f;
+        k.sinDir[i] = (float)std::sin((double)al);
+        k.cosDir[i] = (float)std::cos((double)al);
+        k.sampleRadius[i] = radius8[i];
+    }
+}
+
+inline rsd_status check_common(const rsd_camera* cam, const rsd_vao_data* vao, const rsd_svao_params* p,
+                               const float* depth, const uint16_t* normals, uint32_t W, uint32_t H, const char* who) {
+    if (!cam || !vao || !p || !depth || !normals || W == 0 || H == 0) {
+        set_error(std::string(who) + ": null argument or empty extent");
+        return RSD_ERR_INVALID_ARG;
+    }
+    if (p->num_directions != 8) {
+        set_error(std::string(who) + ": only NUM_DIRECTIONS = 8 (the SVAO default) is implemented");
+        return RSD_ERR_UNSUPPORTED;
+    }
+    if (2 * p->guard_band >= W || 2 * p->guard_band >= H) {
+        set_error(std::string(who) + ": guard band leaves no visible region");
+        return RSD_ERR_INVALID_ARG;
+    }
+    return RSD_OK;
+}
+
+}  // namespace rsd

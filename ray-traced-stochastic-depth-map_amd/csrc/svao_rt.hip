@@ -1,0 +1,262 @@
+// svao_rt.hip -- SVAO "AO 2" in SecondaryDepthMode::Raytraced (the ground-truth AO of
+// scripts/SVAO_depth.py / SAVO_record.py): every stencilled direction is
+// refined by tracing the scene instead of reading the stochastic depth map.
+//
+// Reference: calcAO2 DEPTH_MODE_RAYTRACING (SVAO/Common.slang:598-651), traceAORay
+// (SVAORaster2.ps.slang:9-46 RayQuery, Ray.rt.slang:46-58 TraceRay) and aoAnyHit
+// (Common.slang:679-718, VAO kernel); dispatch SVAO.cpp:408-455.
+//
+// Any-hit order.  As for the SD trace, the hit stream is canonical: ascending t, each
+// triangle once.  aoAnyHit over that stream (accepted = front face, or double-sided, or
+// alpha-masked; culled triangles never arrive):
+//     t <= tSphereStart:  halo = max(halo, t); end the query if t >= tConstRadiusStart
+//     t >  tSphereStart:  inside = min(inside, t); commit (TMax = t) -- nothing nearer follows
+// The query therefore ends at the first accepted hit A with term(A) = (A > tSphereStart ||
+// A >= tConstRadiusStart), a predicate monotone in t, and every accepted hit before A is
+// a halo update.  So the result is:  halo = max(halo0, B, A if A <= tSphereStart),
+// inside = A if A > tSphereStart else inside0, with A the nearest terminating and B the
+// farthest non-terminating accepted hit in [TMin, TMax] -- which one traversal with the
+// upper bound min(TMax, A) collects in any order.  (The RayQuery's "t < halo: skip" test
+// never fires in ascending order: TMin >= halo0.)  The CPU oracle replays the ascending
+// stream literally (oracle/rsd_oracle.c ocpu_svao_pass2_rt_band).
+#include <cfloat>
+
+#include "bvh_traverse.h"
+#include "rsd_device.h"
+#include "rsd_internal.h"
+#include "svao_math.h"
+
+namespace rsd {
+
+struct RtArgs {
+    SvaoArgs s;
+    const float4* nodes;  // BVH base (wide nodes, then triangle records)
+    uint32_t triOff;
+    uint32_t cull;
+    uint32_t rayPipeline;  // 1: ray-pipeline dispatch extent (SVAO.cpp:429-430), 0: compute (:452-453)
+    float invView[9];      // float3x3(inverse(viewMat)), row-major
+};
+
+// The aoAnyHit stream of one AO ray reduced to (A, B), see the file header.
+__device__ __forceinline__ void trace_ao(const float4* __restrict__ bvh, uint32_t triOff, const RayCtx& r, float tmin,
+                                         float tmax, uint32_t cull, float tCRS, float tSS, float& A, float& B,
+                                         uint32_t* __restrict__ ldsItem, float* __restrict__ ldsT) {
+    A = INFINITY;
+    B = -INFINITY;
+    uint32_t spillItem[kStackTotal - kLdsStack];
+    float spillT[kStackTotal - kLdsStack];
+    int sp = 0;
+    uint32_t item = 0;  // root node
+    while (true) {
+        const float4* p = bvh + (item & kOffMask);
+        float4 q[12];
+#pragma unroll
+        for (int j = 0; j < 12; ++j) q[j] = p[j];
+        uint32_t next = kNoItem;
+        const float thi = fminf(tmax, A);
+        if (item & kLeafBit) {
+            const uint32_t cnt = ((item >> 29) & 3u) + 1u;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                if ((uint32_t)j >= cnt) continue;
+                float t, bu, bv, det;
+                if (!intersect_tri(r, q[3 * j], q[3 * j + 1], q[3 * j + 2], t, bu, bv, det)) continue;
+                if (!(t >= tmin && t <= thi)) continue;
+                const uint32_t flags = __float_as_uint(q[3 * j + 1].w);
+                if (culled(det, flags, cull)) continue;
+                // aoAnyHit: frontFace || isDoubleSided || isAlphaTested (Common.slang:695-697)
+                const bool front = (det > 0.0f) != ((flags & RSD_TRI_FRONT_CW) != 0u);
+                if (!(front || (flags & (RSD_TRI_DOUBLE_SIDED | RSD_TRI_ALPHA_MASK)))) continue;
+                if (t > tSS || t >= tCRS) A = fminf(A, t);
+                else B = fmaxf(B, t);
+            }
+        } else {
+            const uint4 rf = make_uint4(__float_as_uint(q[6].x), __float_as_uint(q[6].y), __float_as_uint(q[6].z),
+                                        __float_as_uint(q[6].w));
+            const uint4 ct = make_uint4(__float_as_uint(q[7].x), __float_as_uint(q[7].y), __float_as_uint(q[7].z),
+                                        __float_as_uint(q[7].w));
+            float k0, k1, k2, k3;
+            bool h0 = rf.x != kNoItem && box_hit(r, q[0].x, q[1].x, q[2].x, q[3].x, q[4].x, q[5].x, tmin, thi, k0);
+            bool h1 = rf.y != kNoItem && box_hit(r, q[0].y, q[1].y, q[2].y, q[3].y, q[4].y, q[5].y, tmin, thi, k1);
+            bool h2 = rf.z != kNoItem && box_hit(r, q[0].z, q[1].z, q[2].z, q[3].z, q[4].z, q[5].z, tmin, thi, k2);
+            bool h3 = rf.w != kNoItem && box_hit(r, q[0].w, q[1].w, q[2].w, q[3].w, q[4].w, q[5].w, tmin, thi, k3);
+            auto mkitem = [&](uint32_t ref, uint32_t cnt) {
+                return cnt ? (kLeafBit | ((cnt - 1u) << 29) | (triOff + 3u * ref)) : 8u * ref;
+            };
+            uint32_t c0 = h0 ? mkitem(rf.x, ct.x) : kNoItem, c1 = h1 ? mkitem(rf.y, ct.y) : kNoItem;
+            uint32_t c2 = h2 ? mkitem(rf.z, ct.z) : kNoItem, c3 = h3 ? mkitem(rf.w, ct.w) : kNoItem;
+            k0 = h0 ? k0 : INFINITY;
+            k1 = h1 ? k1 : INFINITY;
+            k2 = h2 ? k2 : INFINITY;
+            k3 = h3 ? k3 : INFINITY;
+            cswap(k0, c0, k1, c1);
+            cswap(k2, c2, k3, c3);
+            cswap(k0, c0, k2, c2);
+            cswap(k1, c1, k3, c3);
+            cswap(k1, c1, k2, c2);
+#define RSD_PUSH(c, k)                                                                  \
+    if ((c) != kNoItem) {                                                               \
+        if (sp < kLdsStack) { ldsItem[sp * 64] = (c); ldsT[sp * 64] = (k); }            \
+        else { spillItem[sp - kLdsStack] = (c); spillT[sp - kLdsStack] = (k); }         \
+        ++sp;                                                                           \
+    }
+            RSD_PUSH(c3, k3)
+            RSD_PUSH(c2, k2)
+            RSD_PUSH(c1, k1)
+#undef RSD_PUSH
+            next = c0;
+        }
+        if (next == kNoItem) {
+            const float hi = fminf(tmax, A);
+            while (sp > 0) {
+                --sp;
+                const uint32_t it = sp < kLdsStack ? ldsItem[sp * 64] : spillItem[sp - kLdsStack];
+                const float tt = sp < kLdsStack ? ldsT[sp * 64] : spillT[sp - kLdsStack];
+                if (tt <= hi) { next = it; break; }
+            }
+            if (next == kNoItem) break;
+        }
+        item = next;
+    }
+}
+
+// SVAORaster2.ps.slang:48-65 / Ray.rt.slang:60-75 -> calcAO2 (Common.slang:523-663), Raytraced
+// branch.  8 x 8 pixels per 64-lane workgroup; one lane walks the AO rays of its pixel.
+__global__ void __launch_bounds__(64) svao_pass2_rt_kernel(RtArgs ra) {
+    __shared__ uint32_t sItem[kLdsStack * 64];
+    __shared__ float sT[kLdsStack * 64];
+    const SvaoArgs& a = ra.s;
+    const rsd_vao_data& d = a.d;
+    const uint32_t lane = threadIdx.x;
+    // band: 8-row tiles of the 32-row groups g (counted from the first visible row) with
+    // g % bandCount == bandIndex
+    const uint32_t by = blockIdx.y;
+    const uint32_t tileRow = ((by / 4u) * a.bandCount + a.bandIndex) * 4u + by % 4u;
+    const uint32_t px = a.guard + blockIdx.x * 8u + lane % 8u;
+    const uint32_t py = a.guard + tileRow * 8u + lane / 8u;
+    const uint32_t xEnd = ra.rayPipeline ? (uint32_t)a.W : (uint32_t)a.W - a.guard;
+    const uint32_t yEnd = ra.rayPipeline ? (uint32_t)a.H : (uint32_t)a.H - a.guard;
+    if (px >= xEnd || py >= yEnd) return;
+    const size_t o = (size_t)py * a.W + px;
+    const uint32_t mask = a.stencil[o];
+    if (mask == 0u) return;
+    const float u = ((float)px + 0.5f) * d.invResolution[0];
+    const float v = ((float)py + 0.5f) * d.invResolution[1];
+    Basic b;
+    basic_init(a, u, v, b);
+    const f3 camPos = mk(a.cam.posW[0], a.cam.posW[1], a.cam.posW[2]);
+    const float* M = ra.invView;
+    float vis = 0.0f;
+#pragma unroll 1
+    for (int i = 0; i < 8; ++i) {
+        if (!(mask & (1u << i))) continue;
+        Sample s;
+        float ssr;
+        sample_init(a, u, v, b, i, s, ssr);
+        eval_primary(a, b, s);
+        vis -= s.visibility;
+        // getSnappedUV (Common.slang:116-125), not clamped: rays may leave the screen
+        const float su = (floorf(s.su * d.resolution[0]) + 0.5f) / d.resolution[0];
+        const float sv = (floorf(s.sv * d.resolution[1]) + 0.5f) / d.resolution[1];
+        const f3 dv = normalize(uv_to_view(a, su, sv, 1.0f));
+        const f3 dw = mk(M[0] * dv.x + M[1] * dv.y + M[2] * dv.z, M[3] * dv.x + M[4] * dv.y + M[5] * dv.z,
+                         M[6] * dv.x + M[7] * dv.y + M[8] * dv.z);
+        const float initLen = length(s.ip);
+        const float pl = b.posVLength;
+        const float tHalo0 = (pl - s.sphereStart - b.radius - d.thickness * b.radius) * initLen / pl;
+        const float tInside0 = (pl - s.sphereEnd) * initLen / pl;
+        const float tCRS = (pl - b.radius - d.thickness * b.radius) * initLen / pl;
+        const float tSS = (pl - s.sphereStart) * initLen / pl;
+        float TMin = hmax(tHalo0, 0.0f);
+        const float TMax = tInside0;
+        if (!s.isInScreen) { s.visibility = 1.0f; s.objectSpaceZ = 3.402823466e+38f; }  // resetSample
+        const float eps = b.radius * 0.01f;
+        if (s.isInScreen) TMin = hmax(TMin, (pl - s.objectSpaceZ) * initLen / pl + eps);
+        float halo = tHalo0, inside = tInside0;
+        if (TMin <= TMax) {
+            RayCtx r;
+            ray_setup(r, camPos, dw);
+            float A, B;
+            trace_ao(ra.nodes, ra.triOff, r, TMin, TMax, ra.cull, tCRS, tSS, A, B, &sItem[lane], &sT[lane]);
+            if (B != -INFINITY) halo = hmax(halo, B);
+            if (A != INFINITY) {
+                if (A <= tSS) halo = hmax(halo, A);
+                else inside = hmin(inside, A);
+            }
+        }
+        const float sphereVis = calc_visibility(d, pl - inside * pl / initLen, s.sphereStart, s.sphereEnd, s.pdf,
+                                                b.radius);
+        const float haloVis = calc_halo_visibility(d, pl - halo * pl / initLen, s.sphereStart, s.sphereEnd, s.pdf,
+                                                   b.radius);
+        s.visibility = hmin(s.visibility, hmin(sphereVis, haloVis));
+        vis += s.visibility;
+    }
+    vis *= 1.0f / 8.0f;
+    vis *= 2.0f;
+    vis += unorm8_to_float(a.ao[o]);
+    vis = acc_pow(vis, d.exponent);
+    a.ao[o] = unorm8(vis);
+}
+
+}  // namespace rsd
+
+using namespace rsd;
+
+extern "C" rsd_status rsd_svao_pass2_raytraced_band(rsd_scene* scene, const rsd_camera* cam, const rsd_vao_data* vao,
+                                                    const rsd_svao_params* p, const float* d_depth,
+                                                    const uint16_t* d_normals, uint32_t W, uint32_t H,
+                                                    const uint8_t* d_stencil, uint8_t* d_ao, uint32_t cull_mode,
+                                                    uint32_t ray_pipeline, uint32_t band_index, uint32_t band_count,
+                                                    rsd_stream stream) {
+    if (band_count == 0 || band_index >= band_count) {
+        set_error("rsd_svao_pass2_raytraced_band: band_index must be < band_count");
+        return RSD_ERR_INVALID_ARG;
+    }
+    rsd_status st = check_common(cam, vao, p, d_depth, d_normals, W, H, "rsd_svao_pass2_raytraced");
+    if (st != RSD_OK) return st;
+    if (!scene || !d_stencil || !d_ao || cull_mode > 2) {
+        set_error("rsd_svao_pass2_raytraced: null argument or bad cull mode");
+        return RSD_ERR_INVALID_ARG;
+    }
+    RtArgs ra{};
+    SvaoArgs& a = ra.s;
+    a.cam = *cam;
+    a.d = *vao;
+    fill_consts(a.k);
+    fill_scale(a);
+    a.depth = d_depth;
+    a.normals = d_normals;
+    a.W = (int)W;
+    a.H = (int)H;
+    a.ao = d_ao;
+    a.stencil = const_cast<uint8_t*>(d_stencil);
+    a.guard = p->guard_band;
+    a.secondary = 3u;
+    a.bandIndex = band_index;
+    a.bandCount = band_count;
+    ra.nodes = scene->d_nodes;
+    ra.triOff = scene->tri_offset;
+    ra.cull = cull_mode;
+    ra.rayPipeline = ray_pipeline ? 1u : 0u;
+    // float3x3(inverse(viewMat)): the view matrix is a rotation + translation, so the rotation
+    // part of its inverse is the transpose (exact; Falcor's general inverse rounds it)
+    for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c) ra.invView[r * 3 + c] = cam->viewMat[c * 4 + r];
+    const uint32_t xEnd = ra.rayPipeline ? W : W - p->guard_band, yEnd = ra.rayPipeline ? H : H - p->guard_band;
+    const uint32_t tilesX = (xEnd - p->guard_band + 7u) / 8u;
+    const uint32_t groups = (yEnd - p->guard_band + 31u) / 32u;
+    const uint32_t bandGroups = groups > band_index ? (groups - band_index + band_count - 1) / band_count : 0u;
+    if (bandGroups == 0 || tilesX == 0) return RSD_OK;
+    hipLaunchKernelGGL(svao_pass2_rt_kernel, dim3(tilesX, 4 * bandGroups), dim3(64), 0, (hipStream_t)stream, ra);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? RSD_OK : hip_fail(e, "svao_pass2_rt_kernel launch");
+}
+
+extern "C" rsd_status rsd_svao_pass2_raytraced(rsd_scene* scene, const rsd_camera* cam, const rsd_vao_data* vao,
+                                               const rsd_svao_params* p, const float* d_depth,
+                                               const uint16_t* d_normals, uint32_t W, uint32_t H,
+                                               const uint8_t* d_stencil, uint8_t* d_ao, uint32_t cull_mode,
+                                               uint32_t ray_pipeline, rsd_stream stream) {
+    return rsd_svao_pass2_raytraced_band(scene, cam, vao, p, d_depth, d_normals, W, H, d_stencil, d_ao, cull_mode,
+                                         ray_pipeline, 0, 1, stream);
+}

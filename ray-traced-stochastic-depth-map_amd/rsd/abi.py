@@ -21,6 +21,7 @@ TRI_FRONT_CW = 2
 TRI_ALPHA_MASK = 4
 
 SD_DEFAULT, SD_COVERAGE_MASK, SD_RESERVOIR_SAMPLING, SD_KBUFFER = 0, 1, 2, 3
+DEPTH_SINGLE, DEPTH_DUAL, DEPTH_STOCHASTIC, DEPTH_RAYTRACED = 0, 1, 2, 3  # VAO/DepthMode.h
 CULL_NONE, CULL_BACK, CULL_FRONT = 0, 1, 2
 
 
@@ -76,7 +77,7 @@ EXPORTS = ["rsd_abi_version", "rsd_last_error", "rsd_device_open", "rsd_device_c
            "rsd_scene_info_get", "rsd_scene_release", "rsd_camera_look_at", "rsd_svao_make_vao_data",
            "rsd_gbuffer", "rsd_sd_trace", "rsd_svao_clear_intervals", "rsd_svao_pass1", "rsd_svao_pass2",
            "rsd_sd_trace_band", "rsd_svao_pass1_band", "rsd_svao_pass2_band", "rsd_gbuffer_raster",
-           "rsd_linearize_depth", "rsd_compress_normals"]
+           "rsd_linearize_depth", "rsd_compress_normals", "rsd_svao_pass2_raytraced", "rsd_svao_pass2_raytraced_band"]
 
 # every symbol include/rsd_graph.h declares
 GRAPH_EXPORTS = ["rsd_graph_create", "rsd_graph_destroy", "rsd_graph_create_pass", "rsd_graph_add_edge",
@@ -141,6 +142,12 @@ def lib():
         L.rsd_svao_pass2_band.restype = st
         L.rsd_svao_pass2_band.argtypes = [C.POINTER(Camera), C.POINTER(VAOData), C.POINTER(SVAOParams), vp, vp, u32,
                                           u32, vp, vp, u32, u32, vp, u32, u32, vp]
+        L.rsd_svao_pass2_raytraced.restype = st
+        L.rsd_svao_pass2_raytraced.argtypes = [vp, C.POINTER(Camera), C.POINTER(VAOData), C.POINTER(SVAOParams), vp, vp,
+                                               u32, u32, vp, vp, u32, u32, vp]
+        L.rsd_svao_pass2_raytraced_band.restype = st
+        L.rsd_svao_pass2_raytraced_band.argtypes = [vp, C.POINTER(Camera), C.POINTER(VAOData), C.POINTER(SVAOParams),
+                                                    vp, vp, u32, u32, vp, vp, u32, u32, u32, u32, vp]
         L.rsd_gbuffer_raster.restype = st
         L.rsd_gbuffer_raster.argtypes = [vp, C.POINTER(Camera), u32, u32, u32, vp, vp, vp]
         L.rsd_linearize_depth.restype = st

@@ -43,6 +43,8 @@ class FrameConfig:
     cull_mode: int = abi.CULL_BACK
     radius: float = 0.2
     exponent: float = 2.0
+    secondary: int = abi.DEPTH_STOCHASTIC  # SVAO secondaryDepthMode: 0 Single, 2 StochasticDepth, 3 Raytraced
+    ray_pipeline: bool = True              # SVAO rayPipeline (SVAO.h:101): pass-2 extent in Raytraced mode
     thickness: float = 0.0
     sd_guard_px: int = 512
     num_directions: int = 8
@@ -83,7 +85,9 @@ def make_camera(scene: Scene, cfg: FrameConfig) -> abi.Camera:
 def make_vao(cfg: FrameConfig):
     vao = abi.VAOData()
     w, h = C.c_uint32(), C.c_uint32()
-    abi.check(abi.lib().rsd_svao_make_vao_data(cfg.fb_w, cfg.fb_h, cfg.divisor, cfg.sd_guard_px, cfg.radius,
+    # getExtraGuardBand (SVAO.cpp:718-723): the SD guard band exists in StochasticDepth mode only
+    guard = cfg.sd_guard_px if cfg.secondary == abi.DEPTH_STOCHASTIC else 0
+    abi.check(abi.lib().rsd_svao_make_vao_data(cfg.fb_w, cfg.fb_h, cfg.divisor, guard, cfg.radius,
                                                cfg.exponent, cfg.thickness, C.byref(vao), C.byref(w), C.byref(h)),
               "rsd_svao_make_vao_data")
     return vao, w.value, h.value
@@ -96,7 +100,7 @@ def sd_params(cfg: FrameConfig, sd_guard: int) -> abi.SDParams:
 
 
 def svao_params(cfg: FrameConfig) -> abi.SVAOParams:
-    return abi.SVAOParams(cfg.num_directions, cfg.sd_samples, 2, int(cfg.ray_interval), int(cfg.jitter),
+    return abi.SVAOParams(cfg.num_directions, cfg.sd_samples, cfg.secondary, int(cfg.ray_interval), int(cfg.jitter),
                           cfg.guard_band)
 
 
@@ -198,12 +202,25 @@ class Renderer:
                                                 _ptr(self.stencil), _ptr(self.sd), self.sd_w, self.sd_h,
                                                 _ptr(self.ao), band[0], band[1], self.stream), "rsd_svao_pass2_band")
 
+    def pass2_raytraced(self, band=(0, 1)):
+        abi.check(abi.lib().rsd_svao_pass2_raytraced_band(self.gscene.h, C.byref(self.cam), C.byref(self.vao),
+                                                          C.byref(self.svp), _ptr(self.depth), _ptr(self.normals),
+                                                          self.cfg.fb_w, self.cfg.fb_h, _ptr(self.stencil),
+                                                          _ptr(self.ao), self.cfg.cull_mode, int(self.cfg.ray_pipeline),
+                                                          band[0], band[1], self.stream),
+                  "rsd_svao_pass2_raytraced_band")
+
     def frame(self):
-        """One AO frame: the span of the reference's "AO 1" + "AORefine" profile scopes."""
-        self.clear_intervals()
+        """One AO frame: the span of the reference's "AO 1" + "AORefine" profile scopes
+        (SVAO.cpp:327-455) for the configured secondary depth mode."""
+        if self.cfg.secondary == abi.DEPTH_STOCHASTIC:
+            self.clear_intervals()
         self.pass1()
-        self.sd_trace()
-        self.pass2()
+        if self.cfg.secondary == abi.DEPTH_STOCHASTIC:
+            self.sd_trace()
+            self.pass2()
+        elif self.cfg.secondary == abi.DEPTH_RAYTRACED:
+            self.pass2_raytraced()
 
     def numpy(self):
         t = self.torch

@@ -189,3 +189,45 @@ def test_band_union_equals_full_frame(device, oracle, world):
     for k in ("ao", "stencil", "ray_min", "ray_max"):
         assert np.array_equal(g[k], full[k]), k
     assert bits_equal(g["sd"], full["sd"])
+
+
+@pytest.mark.parametrize("ray_pipeline,cull", [(1, 1), (0, 1), (1, 0), (0, 2)])
+def test_raytraced_svao_parity(device, oracle, ray_pipeline, cull):
+    """SVAO secondaryDepthMode Raytraced: pass 1 with TRACE_OUT_OF_SCREEN
+    and the aoAnyHit pass 2, both extents (rayPipeline), all cull modes."""
+    from rsd import abi
+    cfg = small_frame_config(visible=(160, 96), guard=16, divisor=1)
+    cfg.secondary = abi.DEPTH_RAYTRACED
+    cfg.ray_pipeline = bool(ray_pipeline)
+    cfg.cull_mode = cull
+    r, osc = renderer("arcade_tiny", cfg, device, oracle)
+    r.gbuffer()
+    r.frame()
+    g = r.numpy()
+    cam, vao, sdp, svp = oracle_structs(r, oracle)
+    assert vao.sdGuard == 0
+    z, n = oracle.gbuffer(osc, cam, cfg.fb_w, cfg.fb_h, cull)
+    ao1, st, _, _ = oracle.svao_pass1(cam, vao, svp, z, n, r.sd_w, r.sd_h)
+    assert np.array_equal(g["stencil"], st)
+    assert (st != 0).sum() > 100, "no refined directions: the test frame is degenerate"
+    ao = oracle.svao_pass2_raytraced(osc, cam, vao, svp, z, n, st, ao1, cull=cull, ray_pipeline=ray_pipeline)
+    assert np.array_equal(g["ao"], ao)
+    assert not np.array_equal(ao, ao1)  # the refinement changed something
+
+
+def test_raytraced_band_union_equals_full_frame(device, oracle):
+    from rsd import abi
+    cfg = small_frame_config(visible=(160, 96), guard=16, divisor=1)
+    cfg.secondary = abi.DEPTH_RAYTRACED
+    r, osc = renderer("arcade_tiny", cfg, device, oracle)
+    r.gbuffer()
+    r.frame()
+    full = r.numpy()
+    r.ao.zero_()
+    r.stencil.zero_()
+    for b in range(3):
+        r.pass1(band=(b, 3))
+    for b in range(3):
+        r.pass2_raytraced(band=(b, 3))
+    g = r.numpy()
+    assert np.array_equal(g["stencil"], full["stencil"]) and np.array_equal(g["ao"], full["ao"])

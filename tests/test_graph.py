@@ -75,12 +75,22 @@ def test_reference_svao_scripts_plan(name):
 
 
 @pytest.mark.skipif(not REF_SCRIPTS.is_dir(), reason="reference scripts not present (GPU box)")
-@pytest.mark.parametrize("name", ["SVAO_depth.py", "SAVO_record.py"])
-def test_reference_raytraced_svao_is_reported_unsupported(name):
-    g = next(iter(rsdgraph.load_script(REF_SCRIPTS / name).values()))
+def test_reference_raytraced_svao_script_plans():
+    """SAVO_record.py: two SVAO passes in the Raytraced secondary mode."""
+    g = next(iter(rsdgraph.load_script(REF_SCRIPTS / "SAVO_record.py").values()))
+    g.plan(1920 + 128, 1080 + 128)
+    order = g.execution_order()
+    assert "SVAO" in order and "SVAO_ref" in order
+    # no SD guard band outside the StochasticDepth mode (SVAO.cpp:718-723): divisor 1 -> frame size
+    assert g.resources()["SVAO.internalRayMax"][:2] == (2048, 1208)
+
+
+@pytest.mark.skipif(not REF_SCRIPTS.is_dir(), reason="reference scripts not present (GPU box)")
+def test_reference_dual_depth_svao_is_reported_unsupported():
+    g = next(iter(rsdgraph.load_script(REF_SCRIPTS / "SVAO_depth.py").values()))
     with pytest.raises(abi.RsdError) as e:
         g.plan(1920 + 128, 1080 + 128)
-    assert e.value.status == 2 and "not implemented" in str(e.value)
+    assert e.value.status == 2 and "primaryDepthMode" in str(e.value)  # SVAO primaryDepthMode DualDepth
 
 
 def test_graph_errors():

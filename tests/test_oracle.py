@@ -220,3 +220,26 @@ def test_raster_gbuffer_chain_matches_linear_gbuffer(oracle):
     # Linearize.ps.slang formula, evaluated in float32 by numpy
     zn, zf = np.float32(cam.nearZ), np.float32(cam.farZ)
     np.testing.assert_array_equal(zl, zn * zf / (zf + d * (zn - zf)))
+
+
+def test_raytraced_ao_independent_of_bvh(oracle):
+    """The Raytraced pass 2 depends on hit distances only: permuting the triangles (another
+    BVH, other primitive ids) leaves the AO image bit-identical; the refinement is not a no-op."""
+    from rsd.scenes import make_scene
+    s = make_scene("arcade_tiny")
+    g, vis = 16, (96, 64)
+    W, H = vis[0] + 2 * g, vis[1] + 2 * g
+    cam = oracle.camera_look_at(s.camera["pos"], s.camera["target"], s.camera["up"], aspect=float(F(W) / F(H)))
+    sc = oracle.Scene(s.positions, s.indices, s.flags)
+    z, n = oracle.gbuffer(sc, cam, W, H)
+    vao, sdW, sdH = oracle_vao(oracle, W, H, 1, sd_guard_px=0, radius=1.5)
+    p = oracle.SVAOParams(8, 4, 3, 1, 1, g)
+    ao1, st, _, _ = oracle.svao_pass1(cam, vao, p, z, n, sdW, sdH)
+    assert (st != 0).sum() > 50
+    ao = oracle.svao_pass2_raytraced(sc, cam, vao, p, z, n, st, ao1)
+    perm = np.random.default_rng(7).permutation(len(s.indices))
+    sc2 = oracle.Scene(s.positions, s.indices[perm], s.flags[perm])
+    ao2 = oracle.svao_pass2_raytraced(sc2, cam, vao, p, z, n, st, ao1)
+    assert np.array_equal(ao, ao2)
+    assert not np.array_equal(ao, ao1)
+    assert np.array_equal(ao[st == 0], ao1[st == 0])
