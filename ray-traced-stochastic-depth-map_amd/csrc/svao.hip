@@ -11,6 +11,7 @@
 // the only per-pixel libm call left is pow() in finalize (SVAO Common.slang:326-330).
 #include <cfloat>
 #include <cmath>
+#include <vector>
 
 #include "rsd_device.h"
 #include "rsd_internal.h"
@@ -45,8 +46,8 @@ __global__ void __launch_bounds__(256) svao_pass1_kernel(SvaoArgs a) {
 #pragma unroll 1
         for (int i = 0; i < 8; ++i) {
             Sample s;
-            float ssr;
-            if (!sample_init(a, u, v, b, i, s, ssr)) continue;
+            bool ssrAbove;
+            if (!sample_init(a, u, v, b, i, s, ssrAbove)) continue;
             if (fabsf(u - s.ru) < d.invResolution[0] * 0.9f && fabsf(v - s.rv) < d.invResolution[1] * 0.9f) {
                 ao += (s.sphereStart - s.sphereEnd) / s.pdf;  // isSamePixel
                 continue;
@@ -60,7 +61,7 @@ __global__ void __launch_bounds__(256) svao_pass1_kernel(SvaoArgs a) {
                 s.objectSpaceZ = 3.402823466e+38f;
             }
             const float constRadius = (1.0f + d.thickness) * b.radius - s.sphereStart;
-            const bool req = s.objectSpaceZ > s.sphereStart + constRadius && ssr > d.ssRadiusCutoff;
+            const bool req = s.objectSpaceZ > s.sphereStart + constRadius && ssrAbove;
             if (req || forceRay) {
                 st |= 1u << i;
                 if (a.secondary == 2u) {
@@ -109,8 +110,8 @@ __global__ void __launch_bounds__(256) svao_pass2_kernel(SvaoArgs a) {
     for (int i = 0; i < 8; ++i) {
         if (!(mask & (1u << i))) continue;
         Sample s;
-        float ssr;
-        sample_init(a, u, v, b, i, s, ssr);
+        bool ssrAbove;
+        sample_init(a, u, v, b, i, s, ssrAbove);
         eval_primary(a, b, s);
         vis -= s.visibility;
         const int cx = uv_to_sd(s.su, d.lowResolution[0], d.sdGuard);
@@ -148,6 +149,36 @@ __global__ void __launch_bounds__(256) svao_pass2_kernel(SvaoArgs a) {
     a.ao[o] = unorm8(vis);
 }
 
+}  // namespace rsd
+
+namespace rsd {
+namespace {
+struct SnapCache {
+    int w = -1, h = -1;
+    float* d = nullptr;
+};
+thread_local SnapCache g_snap;
+}  // namespace
+
+rsd_status snap_tables(const rsd_vao_data& vd, const float** u, const float** v) {
+    const int w = (int)vd.resolution[0], h = (int)vd.resolution[1];
+    SnapCache& c = g_snap;
+    if (c.w != w || c.h != h) {
+        std::vector<float> t((size_t)w + 1 + (size_t)h + 1);
+        for (int k = 0; k <= w; ++k) t[k] = ((float)k + 0.5f) / vd.resolution[0];
+        for (int k = 0; k <= h; ++k) t[(size_t)w + 1 + k] = ((float)k + 0.5f) / vd.resolution[1];
+        (void)hipFree(c.d);
+        c.d = nullptr;
+        c.w = c.h = -1;
+        RSD_HIP(hipMalloc(&c.d, t.size() * sizeof(float)));
+        RSD_HIP(hipMemcpy(c.d, t.data(), t.size() * sizeof(float), hipMemcpyHostToDevice));
+        c.w = w;
+        c.h = h;
+    }
+    *u = c.d;
+    *v = c.d + w + 1;
+    return RSD_OK;
+}
 }  // namespace rsd
 
 using namespace rsd;
@@ -195,7 +226,11 @@ extern "C" rsd_status rsd_svao_pass1_band(const rsd_camera* cam, const rsd_vao_d
     SvaoArgs a{};
     a.cam = *cam;
     a.d = *vao;
-    fill_consts(a.k);
+    fill_consts(a.k, a.d);
+    {
+        rsd_status ts = snap_tables(a.d, &a.snapU, &a.snapV);
+        if (ts != RSD_OK) return ts;
+    }
     fill_scale(a);
     a.depth = d_depth;
     a.normals = d_normals;
@@ -244,7 +279,11 @@ extern "C" rsd_status rsd_svao_pass2_band(const rsd_camera* cam, const rsd_vao_d
     SvaoArgs a{};
     a.cam = *cam;
     a.d = *vao;
-    fill_consts(a.k);
+    fill_consts(a.k, a.d);
+    {
+        rsd_status ts = snap_tables(a.d, &a.snapU, &a.snapV);
+        if (ts != RSD_OK) return ts;
+    }
     fill_scale(a);
     a.depth = d_depth;
     a.normals = d_normals;

@@ -16,6 +16,11 @@ struct SvaoConsts {
     float sinNoise[16], cosNoise[16];
     float sinDir[8], cosDir[8];
     float sampleRadius[8];
+    // SampleAOData::Init terms that only depend on the AO radius (Common.slang:358-363),
+    // evaluated on the host with the device's float operations for radius == VAOData.radius
+    // (every pixel whose screen radius is not clamped to ssMaxRadius)
+    float dirRadius[8], dirDx[8], dirDy[8], dirHeight[8];
+    float ssrMin2;  // smallest float x with sqrtf(x) > ssRadiusCutoff: sqrtf(x) > c <=> x >= ssrMin2
 };
 
 struct SvaoArgs {
@@ -34,6 +39,8 @@ struct SvaoArgs {
     uint32_t guard, secondary, rayInterval, sdJitter, N;
     uint32_t bandIndex, bandCount;  // 32-row groups g (offset space) with g % count == index
     float isx, isy;  // imageScale (Common.slang:142), hoisted: 0.5 * (frameW / focal), same bits
+    const float* snapU;  // getSnappedUV: snapU[k] = (k + 0.5f) / resolution.x for k in [0, resolution.x]
+    const float* snapV;  //               snapV[k] = (k + 0.5f) / resolution.y
 };
 
 struct Basic {
@@ -104,12 +111,22 @@ __device__ __forceinline__ float make_nonzero(float v, float eps) {
 }
 
 // Common.slang:354-399 (VAO kernel)
+// ssrAbove = (screenSpaceRadius > ssRadiusCutoff), decided on the squared radius (no sqrt)
 __device__ __forceinline__ bool sample_init(const SvaoArgs& a, float u, float v, const Basic& b, int i, Sample& s,
-                                            float& screenSpaceRadius) {
+                                            bool& ssrAbove) {
     const rsd_vao_data& d = a.d;
-    const float radius = a.k.sampleRadius[i] * b.radius;
-    const float dx = radius * a.k.sinDir[i], dy = radius * a.k.cosDir[i];
-    const float sphereHeight = sqrtf(b.radius * b.radius - radius * radius);
+    float radius, dx, dy, sphereHeight;
+    if (b.radius == d.radius) {  // the host-evaluated terms (same operations, same bits)
+        radius = a.k.dirRadius[i];
+        dx = a.k.dirDx[i];
+        dy = a.k.dirDy[i];
+        sphereHeight = a.k.dirHeight[i];
+    } else {
+        radius = a.k.sampleRadius[i] * b.radius;
+        dx = radius * a.k.sinDir[i];
+        dy = radius * a.k.cosDir[i];
+        sphereHeight = sqrtf(b.radius * b.radius - radius * radius);
+    }
     s.pdf = 2.0f * sphereHeight;
     s.sphereStart = sphereHeight;
     const float zi = -(dx * b.normalO.x + dy * b.normalO.y) / make_nonzero(b.normalO.z, 0.0001f);
@@ -121,11 +138,12 @@ __device__ __forceinline__ bool sample_init(const SvaoArgs& a, float u, float v,
     s.visibility = 0.0f;
     s.objectSpaceZ = 0.0f;
     const float ex = (u - s.su) * d.resolution[0], ey = (v - s.sv) * d.resolution[1];
-    screenSpaceRadius = sqrtf(ex * ex + ey * ey);
+    ssrAbove = ex * ex + ey * ey >= a.k.ssrMin2;
     const float cu = saturate(s.su), cv = saturate(s.sv);
     s.isInScreen = (s.su == cu) && (s.sv == cv);
-    s.ru = (floorf(cu * d.resolution[0]) + 0.5f) / d.resolution[0];
-    s.rv = (floorf(cv * d.resolution[1]) + 0.5f) / d.resolution[1];
+    // getSnappedUV (Common.slang:116-120): (floor(uv * res) + 0.5) / res from the host table
+    s.ru = a.snapU[(int)floorf(cu * d.resolution[0])];
+    s.rv = a.snapV[(int)floorf(cv * d.resolution[1])];
     return true;
 }
 
@@ -170,7 +188,7 @@ inline void fill_scale(SvaoArgs& a) {
     a.isy = 0.5f * (a.cam.frameHeight / a.cam.focalLength);
 }
 
-inline void fill_consts(SvaoConsts& k) {
+inline void fill_consts(SvaoConsts& k, const rsd_vao_data& d) {
     // SVAO.cpp:670-684 -> R8Unorm noise; Common.slang:311-312 randRotation, :357 alpha
     static const float dither[16] = {0.0f, 8.0f, 2.0f, 10.0f, 12.0f, 4.0f, 14.0f, 6.0f,
                                      3.0f, 11.0f, 1.0f, 9.0f, 15.0f, 7.0f, 13.0f, 5.0f};
@@ -187,8 +205,22 @@ inline void fill_consts(SvaoConsts& k) {
         k.sinDir[i] = (float)std::sin((double)al);
         k.cosDir[i] = (float)std::cos((double)al);
         k.sampleRadius[i] = radius8[i];
+        // Common.slang:358-361 at radius = VAOData.radius (float ops as on the device)
+        k.dirRadius[i] = k.sampleRadius[i] * d.radius;
+        k.dirDx[i] = k.dirRadius[i] * k.sinDir[i];
+        k.dirDy[i] = k.dirRadius[i] * k.cosDir[i];
+        k.dirHeight[i] = std::sqrt(d.radius * d.radius - k.dirRadius[i] * k.dirRadius[i]);
     }
+    // sqrtf is correctly rounded and monotone: the least x with sqrtf(x) > c
+    const float c = d.ssRadiusCutoff;
+    float x = (float)((double)c * (double)c);
+    while (x > 0.0f && std::sqrt(std::nextafter(x, 0.0f)) > c) x = std::nextafter(x, 0.0f);
+    while (!(std::sqrt(x) > c)) x = std::nextafter(x, INFINITY);
+    k.ssrMin2 = x;
 }
+
+// getSnappedUV tables for a frame size (device copies cached per thread, grow-only)
+rsd_status snap_tables(const rsd_vao_data& d, const float** u, const float** v);
 
 inline rsd_status check_common(const rsd_camera* cam, const rsd_vao_data* vao, const rsd_svao_params* p,
                                const float* depth, const uint16_t* normals, uint32_t W, uint32_t H, const char* who) {

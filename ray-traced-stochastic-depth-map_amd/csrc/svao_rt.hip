@@ -151,8 +151,8 @@ __global__ void __launch_bounds__(64) svao_pass2_rt_kernel(RtArgs ra) {
     for (int i = 0; i < 8; ++i) {
         if (!(mask & (1u << i))) continue;
         Sample s;
-        float ssr;
-        sample_init(a, u, v, b, i, s, ssr);
+        bool ssrAbove;
+        sample_init(a, u, v, b, i, s, ssrAbove);
         eval_primary(a, b, s);
         vis -= s.visibility;
         // getSnappedUV (Common.slang:116-125), not clamped: rays may leave the screen
@@ -222,7 +222,11 @@ extern "C" rsd_status rsd_svao_pass2_raytraced_band(rsd_scene* scene, const rsd_
     SvaoArgs& a = ra.s;
     a.cam = *cam;
     a.d = *vao;
-    fill_consts(a.k);
+    fill_consts(a.k, a.d);
+    {
+        rsd_status ts = snap_tables(a.d, &a.snapU, &a.snapV);
+        if (ts != RSD_OK) return ts;
+    }
     fill_scale(a);
     a.depth = d_depth;
     a.normals = d_normals;
