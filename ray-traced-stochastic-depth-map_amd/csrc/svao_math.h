@@ -111,6 +111,15 @@ __device__ __forceinline__ float make_nonzero(float v, float eps) {
 }
 
 // Common.slang:354-399 (VAO kernel)
+// RN(n / D) <= 0.1f for n >= 0, D >= 0 (Common.slang:378), without the division: 0.1f has an odd
+// significand, so RN(q) <= 0.1f <=> q < M = 0.1f + ulp(0.1f) / 2 (a tie rounds up, to even), and
+// for D > 0 q < M <=> n < M * D, a product of 25- and 24-bit significands: exact in double.
+// D = 0 gives +inf / NaN in the reference (never <= 0.1): n < 0 is false here as well.
+__device__ __forceinline__ bool ratio_le_tenth(float n, float D) {
+    constexpr double M = (double)0.1f + 0x1p-28;
+    return (double)n < M * (double)D;
+}
+
 // ssrAbove = (screenSpaceRadius > ssRadiusCutoff), decided on the squared radius (no sqrt)
 __device__ __forceinline__ bool sample_init(const SvaoArgs& a, float u, float v, const Basic& b, int i, Sample& s,
                                             bool& ssrAbove) {
@@ -131,7 +140,7 @@ __device__ __forceinline__ bool sample_init(const SvaoArgs& a, float u, float v,
     s.sphereStart = sphereHeight;
     const float zi = -(dx * b.normalO.x + dy * b.normalO.y) / make_nonzero(b.normalO.z, 0.0001f);
     s.sphereEnd = hmin(hmax(zi, -sphereHeight), sphereHeight);
-    if ((s.sphereStart - s.sphereEnd) / (2.0f * sphereHeight) <= 0.1f) return false;
+    if (ratio_le_tenth(s.sphereStart - s.sphereEnd, 2.0f * sphereHeight)) return false;
     const f3 ip = b.posV + b.tangent * dx + b.bitangent * dy;
     s.ip = ip;
     view_to_uv(a, ip, s.su, s.sv);
@@ -157,7 +166,10 @@ __device__ __forceinline__ float calc_halo_visibility(const rsd_vao_data& d, flo
 __device__ __forceinline__ float calc_visibility(const rsd_vao_data& d, float oz, float ss, float se, float pdf,
                                                  float radius) {
     const float sphere = hmax(ss - hmax(se, oz), 0.0f) / pdf;
-    const float halo = saturate((oz - (1.0f + d.thickness) * radius) / ss) * (ss - se) / pdf;
+    // saturate(x / ss) with ss > 0 is +0 for x <= 0 (and for NaN), so the halo term is then
+    // exactly +0 * (ss - se) / pdf = +0: its two divisions are skipped
+    const float x = oz - (1.0f + d.thickness) * radius;
+    const float halo = x > 0.0f ? saturate(x / ss) * (ss - se) / pdf : 0.0f;
     return sphere + halo;
 }
 
