@@ -135,11 +135,27 @@ __global__ void __launch_bounds__(256) svao_pass2_kernel(SvaoArgs a) {
             }
         }
         if (!s.isInScreen) { s.visibility = 1.0f; s.objectSpaceZ = 3.402823466e+38f; }  // resetSample
+        // addSample x N (Common.slang:583-596): visibility = min over k of sphere_k + halo_k.
+        // Where halo_k is exactly +0 the term is RN(y_k / pdf), monotone in y_k, so those k
+        // share ONE division of their least numerator (the result is the same float).
+        float ymin = INFINITY;
+        bool plain = false;
 #pragma unroll
         for (int k = 0; k < N; ++k) {
             const float lz = dep[k] * depthRange + depthOffset;
-            add_sample(a, b, s, uv_to_view(a, su, sv, lz), false);
+            const float oz = dot(uv_to_view(a, su, sv, lz) - b.posV, b.normal);
+            s.objectSpaceZ = hmin(s.objectSpaceZ, oz);
+            const float y = hmax(s.sphereStart - hmax(s.sphereEnd, oz), 0.0f);
+            const float x = oz - (1.0f + d.thickness) * b.radius;
+            if (x > 0.0f) {
+                const float halo = saturate(x / s.sphereStart) * (s.sphereStart - s.sphereEnd) / s.pdf;
+                s.visibility = hmin(s.visibility, y / s.pdf + halo);
+            } else {
+                ymin = hmin(ymin, y);
+                plain = true;
+            }
         }
+        if (plain) s.visibility = hmin(s.visibility, ymin / s.pdf);
         vis += s.visibility;
     }
     vis *= 1.0f / 8.0f;
