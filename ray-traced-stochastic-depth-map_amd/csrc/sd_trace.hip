@@ -976,7 +976,12 @@ static hipError_t launch_sd_kn(const SDArgs& a, dim3 grid, uint32_t persistentBl
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const dim3 pg(persistentBlocks), wb(kBlock);
-    if (walk == 2) {
+    static const char* row16Env = std::getenv("RSD_TRACE_ROW16");  // experiments: 16 lanes per ray
+    if (walk == 2 && row16Env && *row16Env == '1' && !a.counters) {
+        hipLaunchKernelGGL((sd_trace_row_kernel<K, N, 16, true, false>), pg, wb, 0, s, a, queue, qctl, keys);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        hipLaunchKernelGGL((sd_resolve_row_kernel<K, N, 16>), pg, wb, 0, s, a, queue, qctl, keys);
+    } else if (walk == 2) {
         if (a.counters) hipLaunchKernelGGL((sd_trace_row_kernel<K, N, ROW, true, true>), pg, wb, 0, s, a, queue, qctl, keys);
         else hipLaunchKernelGGL((sd_trace_row_kernel<K, N, ROW, true, false>), pg, wb, 0, s, a, queue, qctl, keys);
         if ((e = hipGetLastError()) != hipSuccess) return e;
@@ -1154,7 +1159,13 @@ extern "C" rsd_status rsd_sd_trace_band(rsd_scene* scene, const rsd_camera* cam,
     a.poolSoft = std::min(kPoolCap - 48 - 3 * depth, 160);
     static const char* walkEnv = std::getenv("RSD_TRACE_WALK");
     const std::string walkName = walkEnv ? walkEnv : "";
-    const bool rowWalk = a.poolSoft >= 16 && walkName != "quad";
+    // The row walk wins when few rays are live (the launch is the slowest ray's chain); with
+    // more SD texels the live rays fill the machine and the quad walk's lane utilisation wins
+    // (rsd_sd_trace, row vs quad: 1080p/4 0.43 M texels 92 vs 133 us; 4K/4 1.0 M texels 443 vs
+    // 327 us; 1080p full 6.9 M texels 688 vs 294 us -- DESIGN.md section 4)
+    const uint64_t bandTexels = (uint64_t)sd_w * sd_h / band_count;
+    const bool rowWalk = a.poolSoft >= 16 && walkName != "quad" &&
+                         (walkName == "fused" || walkName == "split" || bandTexels <= 600000u);
     // default: the split row walk (trace -> keys -> resolve) where one chunk of K keys decides
     // every texel, else the fused row walk; RSD_TRACE_WALK=fused|quad for A/B runs
     const int walk = !rowWalk ? 0 : (split && walkName != "fused") ? 2 : 1;
