@@ -56,28 +56,70 @@ struct SDArgs {
     uint32_t partCap;  // live-ray queue: capacity of one partition
     int bandIndex, bandCount;  // screen-band sharding: 8-row tile rows t with t % count == index
     int poolSoft;      // row traversal: above this many pooled items a row pops one item per step
+    const float* rayTab;  // per-column / per-row ray terms (ray_table_kernel), see sd_ray
 };
+
+// Per-column and per-row terms of initRayDesc, evaluated once per frame size with exactly the
+// operations sd_ray used to evaluate per texel (so the bits are unchanged):
+//   [0, W)        cx[x]  = (sx + 0.5) / dimx + -jitterX      (pixel-centre dir, TMax)
+//   [W, 2W)       u0[x]  = (sx + 0.5) / dimx                 (linearZ sample)
+//   [2W, 6W)      jx[r][x] = (sx + jitterPos[r][x % 4].x) / dimx, r = y % 4
+//   [6W, 6W+H)    cy[y]  = (sy + 0.5) / dimy + jitterY
+//   [.., +H)      v0[y]  = (sy + 0.5) / dimy
+//   [.., +4H)     jy[r][y] = (sy + jitterPos[y % 4][r].y) / dimy, r = x % 4
+//   [.., +3)      normalize(camera W)
+__global__ void ray_table_kernel(float* __restrict__ tab, int W, int H, int guard, uint32_t jitter, float jitterX,
+                                 float jitterY, f3 camW) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const int dimx = W - 2 * guard, dimy = H - 2 * guard;
+    if (i < W) {
+        const int sx = i - guard;
+        tab[i] = ((float)sx + 0.5f) / (float)dimx + -jitterX;
+        tab[W + i] = ((float)sx + 0.5f) / (float)dimx;
+        for (int r = 0; r < 4; ++r) {
+            float jx, jy;
+            sd_jitter((uint32_t)i, (uint32_t)r, jitter != 0u, jx, jy);
+            tab[2 * W + r * W + i] = ((float)sx + jx) / (float)dimx;
+        }
+    }
+    if (i < H) {
+        const int sy = i - guard;
+        float* t = tab + 6 * W;
+        t[i] = ((float)sy + 0.5f) / (float)dimy + jitterY;
+        t[H + i] = ((float)sy + 0.5f) / (float)dimy;
+        for (int r = 0; r < 4; ++r) {
+            float jx, jy;
+            sd_jitter((uint32_t)r, (uint32_t)i, jitter != 0u, jx, jy);
+            t[2 * H + r * H + i] = ((float)sy + jy) / (float)dimy;
+        }
+    }
+    if (i == 0) {
+        const f3 wn = normalize(camW);
+        float* t = tab + 6 * W + 6 * H;
+        t[0] = wn.x;
+        t[1] = wn.y;
+        t[2] = wn.z;
+    }
+}
 
 
 // initRayDesc, Common.slangh:65-92 (with Camera.slang:46-90).  Returns true if the ray
 // interval is non-empty (TMin <= TMax): only those rays reach TraceRay.
 __device__ __forceinline__ bool sd_ray(const SDArgs& a, int x, int y, f3& d, float& TMin, float& TMax, float& cosT) {
     const rsd_camera& c = a.cam;
-    const int dimx = a.sdW - 2 * a.guard, dimy = a.sdH - 2 * a.guard;
+    const int W = a.sdW, H = a.sdH;
+    const int dimx = W - 2 * a.guard, dimy = H - 2 * a.guard;
     const int sx = x - a.guard, sy = y - a.guard;
-    const f3 wn = normalize(mk(c.W[0], c.W[1], c.W[2]));
-    const f3 dc = normalize(cam_dir(c, ((float)sx + 0.5f) / (float)dimx + -c.jitterX,
-                                    ((float)sy + 0.5f) / (float)dimy + c.jitterY));
+    const float* t = a.rayTab;  // ray_table_kernel
+    const float* ty = t + 6 * W;
+    const f3 wn = mk(ty[6 * H], ty[6 * H + 1], ty[6 * H + 2]);  // normalize(camera W)
+    const f3 dc = normalize(cam_dir(c, t[x], ty[y]));
     const float invCos = 1.0f / dot(wn, dc);
     TMax = c.farZ * invCos;  // computeRayPinhole tMax (pixel centre)
-    float jx, jy;
-    sd_jitter((uint32_t)x, (uint32_t)y, a.jitter != 0u, jx, jy);
-    d = normalize(cam_dir(c, ((float)sx + jx) / (float)dimx, ((float)sy + jy) / (float)dimy));
+    d = normalize(cam_dir(c, t[2 * W + (y & 3) * W + x], ty[2 * H + (x & 3) * H + y]));  // SD jitter
     const float eps = 0.1f * c.nearZ;
     float depth = 0.0f;
-    if (sx >= 0 && sy >= 0 && sx < dimx && sy < dimy)
-        depth = tex_bilinear(a.linearZ, a.zW, a.zH, ((float)sx + 0.5f) / (float)dimx, ((float)sy + 0.5f) / (float)dimy,
-                             true);
+    if (sx >= 0 && sy >= 0 && sx < dimx && sy < dimy) depth = tex_bilinear(a.linearZ, a.zW, a.zH, t[W + x], ty[H + y], true);
     cosT = dot(wn, d);
     TMin = depth / cosT + eps;
     if (a.rayInterval) {
@@ -1020,6 +1062,25 @@ struct LutCache {
 };
 thread_local LutCache g_lut[17];
 
+struct RayTabCache {
+    int w = -1, h = -1, guard = 0;
+    uint32_t jitter = 0;
+    float jx = 0.0f, jy = 0.0f;
+    float camW[3] = {0.0f, 0.0f, 0.0f};
+    int device = -1;
+    float* d = nullptr;
+    size_t cap = 0;
+    bool same(const RayTabCache& k) const {
+        return w == k.w && h == k.h && guard == k.guard && jitter == k.jitter && jx == k.jx && jy == k.jy &&
+               camW[0] == k.camW[0] && camW[1] == k.camW[1] && camW[2] == k.camW[2] && device == k.device;
+    }
+    void setKey(const RayTabCache& k) {
+        w = k.w; h = k.h; guard = k.guard; jitter = k.jitter; jx = k.jx; jy = k.jy;
+        camW[0] = k.camW[0]; camW[1] = k.camW[1]; camW[2] = k.camW[2]; device = k.device;
+    }
+};
+thread_local RayTabCache g_raytab;
+
 rsd_status ensure_lut(uint32_t N, const int32_t** idx, const uint32_t** lut) {
     LutCache& c = g_lut[N];
     if (c.n != (int)N) {
@@ -1125,6 +1186,30 @@ extern "C" rsd_status rsd_sd_trace_band(rsd_scene* scene, const rsd_camera* cam,
         if (s != RSD_OK) return s;
     }
     hipStream_t s = (hipStream_t)stream;
+    {
+        // per-frame-size ray terms (recomputed when the SD map size, guard band or jitter change)
+        RayTabCache& rt = g_raytab;
+        const RayTabCache key{(int)sd_w, (int)sd_h, p->guard_band, p->jitter, cam->jitterX, cam->jitterY,
+                              {cam->W[0], cam->W[1], cam->W[2]}, scene->dev->hip_device};
+        const size_t need = (6 * (size_t)sd_w + 6 * (size_t)sd_h + 3) * sizeof(float);
+        if (!rt.same(key) || rt.cap < need) {
+            if (rt.cap < need) {
+                RSD_HIP(hipStreamSynchronize(s));
+                (void)hipFree(rt.d);
+                rt.d = nullptr;
+                rt.cap = 0;
+                RSD_HIP(hipMalloc(&rt.d, need));
+                rt.cap = need;
+            }
+            const int n = (int)std::max(sd_w, sd_h);
+            hipLaunchKernelGGL(ray_table_kernel, dim3((n + 255) / 256), dim3(256), 0, s, rt.d, (int)sd_w, (int)sd_h,
+                               p->guard_band, p->jitter, cam->jitterX, cam->jitterY, f3{cam->W[0], cam->W[1], cam->W[2]});
+            hipError_t te = hipGetLastError();
+            if (te != hipSuccess) return hip_fail(te, "ray_table_kernel launch");
+            rt.setKey(key);
+        }
+        a.rayTab = rt.d;
+    }
     if (counters) {
         RSD_HIP(hipMemsetAsync(scene->d_counters, 0, 16 * sizeof(unsigned long long), s));
         a.counters = scene->d_counters;
