@@ -1,0 +1,56 @@
+"""GPU parity at the BASELINE configs' full sizes (configs[2..4]: 1080p full-res N = 8 on a
+2.8 M-triangle scene, 4K 1/4-res on 10 M triangles, 4K full-res N = 16).
+
+The oracle cannot replay a whole 4K frame in seconds, so each stage is checked on the GPU's
+own inputs (the stages are deterministic functions of them): pass 1 over the full frame,
+the SD trace on a spread of 8-row tile rows through the whole map, and pass 2 over the full
+frame.  Bit-exact, like test_gpu_parity.py.  (configs[1] is checked bit-for-bit over its
+whole SD map by every bench.py run: cpu_baseline.bit_identical_to_gpu.)"""
+import numpy as np
+import pytest
+
+from helpers import to_oracle
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("config", ["bistro_1080p_full", "emerald_4k_q", "bistro_4k_full_n16"])
+def test_fullsize_config_parity(oracle, config):
+    import torch
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    from rsd.frame import CONFIGS, FrameConfig, Renderer
+    from rsd.scenes import make_scene
+    kw, scene_name = CONFIGS[config]
+    scene = make_scene(scene_name)
+    cfg = FrameConfig(**kw)
+    r = Renderer(scene, cfg)
+    r.gbuffer()
+    r.frame()
+    g = r.numpy()
+    cam, vao = to_oracle(r.cam, oracle.Camera), to_oracle(r.vao, oracle.VAOData)
+    sdp, svp = to_oracle(r.sdp, oracle.SDParams), to_oracle(r.svp, oracle.SVAOParams)
+
+    # pass 1 ("AO 1") over the whole frame, on the GPU's G-buffer
+    ao1, st, rmin, rmax = oracle.svao_pass1(cam, vao, svp, g["depth"], g["normals"], r.sd_w, r.sd_h)
+    assert np.array_equal(g["stencil"], st)
+    assert np.array_equal(g["ray_min"], rmin) and np.array_equal(g["ray_max"], rmax)
+    assert (rmax != 0).sum() > 1000, "no SD rays requested: degenerate frame"
+
+    # SD trace: 8-row tile rows spread through the map (every `step`-th tile row)
+    osc = oracle.Scene(scene.positions, scene.indices, scene.flags)
+    tiles = (r.sd_h + 7) // 8
+    step = max(1, tiles // 12)
+    checked = 0
+    for t in range(0, tiles, step):
+        y0, y1 = 8 * t, min(8 * t + 8, r.sd_h)
+        sd, _ = oracle.sd_trace(osc, cam, sdp, g["depth"], rmin, rmax, r.sd_w, r.sd_h, rows=(y0, y1))
+        assert np.array_equal(sd[:, y0:y1].view(np.uint32), g["sd"][:, y0:y1].view(np.uint32)), (config, y0)
+        checked += (rmax[y0:y1] != 0).sum()
+    assert checked > 0
+
+    # pass 2 ("AO 2") over the whole frame, on the GPU's SD map
+    ao = oracle.svao_pass2(cam, vao, svp, g["depth"], g["normals"], st, g["sd"], ao1)
+    gv = slice(cfg.guard_band, cfg.fb_h - cfg.guard_band), slice(cfg.guard_band, cfg.fb_w - cfg.guard_band)
+    assert np.array_equal(g["ao"][gv], ao[gv])
+    r.close()
