@@ -43,7 +43,7 @@ typedef void* rsd_stream; /* hipStream_t */
  * 3091, 3628-3739).  A world-space triangle soup; triangle_flags per triangle:
  *   bit0 double-sided (TriangleFacingCullDisable, Scene.cpp:3452)
  *   bit1 front face clockwise (TriangleFrontCounterClockwise, Scene.cpp:3451)
- *   bit2 alpha-masked material (AlphaMode::Mask; alpha test not yet supported)
+ *   bit2 alpha-masked material (AlphaMode::Mask): alpha-tested, see rsd_scene_upload_alpha
  * Primitive id = triangle index in this array.                                        */
 #define RSD_TRI_DOUBLE_SIDED 1u
 #define RSD_TRI_FRONT_CW 2u
@@ -66,6 +66,32 @@ typedef struct {
     double build_ms;
     uint64_t device_bytes;
 } rsd_scene_info;
+
+/* Alpha-masked materials (MaterialFactory.slang:124-151, AlphaTest.slang:54-84,
+ * StandardMaterial.slang:128-132): the opacity of a triangle flagged RSD_TRI_ALPHA_MASK is the
+ * alpha of its material's base-colour texture at the interpolated texture coordinate (or the
+ * material's constant alpha); the hit is alpha-tested away when opacity < alpha_threshold
+ * (the threshold is stored as float16 like MaterialHeader, MaterialData.slang:99).
+ * Textures are R8 (alpha only), row-major, mip 0; librsd builds the 2x2 box-filter mip chain.
+ * Sampling: trilinear, wrap, 8 sub-texel / LOD-fraction bits (DESIGN.md "Alpha test"). */
+#define RSD_NO_TEXTURE 0xffffffffu
+typedef struct {
+    uint32_t width, height;
+    const uint8_t* alpha; /* width * height texels (host) */
+} rsd_alpha_texture;
+typedef struct {
+    float alpha_threshold; /* MaterialHeader alpha threshold (default 0.5) */
+    float alpha;           /* constant alpha (baseColor.a) when texture == RSD_NO_TEXTURE */
+    uint32_t texture;      /* index into rsd_alpha_desc.textures or RSD_NO_TEXTURE */
+} rsd_material;
+typedef struct {
+    const float* texcoords;            /* float2[vertex_count] (indexed like the positions) */
+    const uint32_t* triangle_material; /* uint32[triangle_count] */
+    const rsd_material* materials;
+    uint32_t material_count;
+    const rsd_alpha_texture* textures;
+    uint32_t texture_count;
+} rsd_alpha_desc;
 
 /* Camera data mirror (CameraData.slang:35-68 subset), 32 floats. */
 typedef struct {
@@ -90,7 +116,7 @@ typedef struct {
     uint32_t normalize;      /* normalize (NORMALIZE) */
     uint32_t ray_interval;   /* RayInterval (USE_RAY_INTERVAL) */
     uint32_t cull_mode;      /* CullMode (CULL_MODE_RAY_FLAG) */
-    uint32_t alpha_test;     /* AlphaTest (USE_ALPHA_TEST); opaque scenes only for now */
+    uint32_t alpha_test;     /* AlphaTest (USE_ALPHA_TEST) */
     float alpha;             /* Alpha (ALPHA), coverage-mask implementation */
 } rsd_sd_params;
 
@@ -140,10 +166,20 @@ void rsd_device_close(rsd_device* dev);
 
 /* --- scene (BVH2 build on the host, upload to HBM) --------------------------------- */
 rsd_status rsd_scene_upload(rsd_device* dev, const rsd_scene_desc* desc, rsd_scene** out);
+/* The same with alpha-masked materials (alpha may be NULL = all opaque).  The SD trace applies
+ * the alpha test when rsd_sd_params.alpha_test is set (ray-cone LOD, StochasticDepthMapRT.rt.slang:
+ * 31-37, RAY_CONE_SPREAD of the SD map height); the G-buffer (GBufferRaster useAlphaTest) and the
+ * Raytraced SVAO pass (alphaTest, LOD 0, Common.slang:684-693) test at LOD 0. */
+rsd_status rsd_scene_upload_alpha(rsd_device* dev, const rsd_scene_desc* desc, const rsd_alpha_desc* alpha,
+                                  rsd_scene** out);
 rsd_status rsd_scene_info_get(const rsd_scene* scene, rsd_scene_info* out);
 void rsd_scene_release(rsd_scene* scene);
 
 /* --- host helpers (no GPU work) ---------------------------------------------------- */
+/* RAY_CONE_SPREAD of the SD pass (StochasticDepthMapRT.cpp:266-267): Camera::
+ * computeScreenSpacePixelSpreadAngle(height) (Camera.cpp:296-301) with the fovY of the 24 mm
+ * default frame height, passed through std::to_string ("%f") like the shader define. */
+float rsd_ray_cone_spread(float focal_length, uint32_t height);
 /* Camera::calculateCameraParameters (Camera.cpp:99-185), preserveHeight = true */
 rsd_status rsd_camera_look_at(const float pos[3], const float target[3], const float up[3],
                               float focal_length, float frame_height, float aspect_ratio,
@@ -207,7 +243,7 @@ rsd_status rsd_svao_pass2(const rsd_camera* cam, const rsd_vao_data* vao, const 
 rsd_status rsd_svao_pass2_raytraced(rsd_scene* scene, const rsd_camera* cam, const rsd_vao_data* vao,
                                     const rsd_svao_params* params, const float* d_depth, const uint16_t* d_normals,
                                     uint32_t width, uint32_t height, const uint8_t* d_stencil, uint8_t* d_ao,
-                                    uint32_t cull_mode, uint32_t ray_pipeline, rsd_stream stream);
+                                    uint32_t cull_mode, uint32_t ray_pipeline, uint32_t alpha_test, rsd_stream stream);
 
 /* --- screen-band sharding (multi-GPU) ----------------------------------
  * Band b of B owns: pass-1/pass-2 rows whose 32-row group g (counted from the first
@@ -233,8 +269,8 @@ rsd_status rsd_svao_pass2_raytraced_band(rsd_scene* scene, const rsd_camera* cam
                                          const rsd_svao_params* params, const float* d_depth,
                                          const uint16_t* d_normals, uint32_t width, uint32_t height,
                                          const uint8_t* d_stencil, uint8_t* d_ao, uint32_t cull_mode,
-                                         uint32_t ray_pipeline, uint32_t band_index, uint32_t band_count,
-                                         rsd_stream stream);
+                                         uint32_t ray_pipeline, uint32_t alpha_test, uint32_t band_index,
+                                         uint32_t band_count, rsd_stream stream);
 
 #ifdef __cplusplus
 }

@@ -80,7 +80,16 @@ def lib():
         L.ocpu_svao_pass2_band.argtypes = [vp, vp, vp, vp, vp, u32, u32, vp, vp, u32, u32, vp, u32, u32, i32]
         L.ocpu_svao_pass1.argtypes = [vp, vp, vp, vp, vp, u32, u32, vp, vp, vp, vp, u32, u32]
         L.ocpu_svao_pass2.argtypes = [vp, vp, vp, vp, vp, u32, u32, vp, vp, u32, u32, vp, i32]
-        L.ocpu_svao_pass2_rt_band.argtypes = [vp, vp, vp, vp, vp, vp, u32, u32, vp, vp, u32, u32, u32, u32, i32]
+        L.ocpu_svao_pass2_rt_band.argtypes = [vp, vp, vp, vp, vp, vp, u32, u32, vp, vp, u32, u32, u32, u32, u32, i32]
+        L.ocpu_scene_set_alpha.argtypes = [vp, vp, vp, vp, u32, vp, vp, vp, u32, vp, vp, vp]
+        L.ocpu_alpha_fails.restype = i32
+        L.ocpu_alpha_fails.argtypes = [vp, u32, f32, f32, i32, f32, vp, f32]
+        L.ocpu_alpha_value.restype = f32
+        L.ocpu_alpha_value.argtypes = [vp, u32, f32, f32, i32, f32, vp, f32]
+        L.ocpu_alpha_threshold.restype = f32
+        L.ocpu_alpha_threshold.argtypes = [vp, u32]
+        L.ocpu_ray_cone_spread.restype = f32
+        L.ocpu_ray_cone_spread.argtypes = [f32, u32]
         L.ocpu_hash.restype = f32
         L.ocpu_hash.argtypes = [f32, f32]
         L.ocpu_jitter.argtypes = [u32, u32, vp, vp]
@@ -106,12 +115,38 @@ def _threads(n):
 
 
 class Scene:
-    def __init__(self, positions, indices, flags=None):
+    """alpha: an object with texcoords [nv,2], tri_material [nt], thresholds / alphas /
+    material_textures [m] and textures (list of uint8 [h,w]) -- rsd.scenes.AlphaMaterials."""
+
+    def __init__(self, positions, indices, flags=None, alpha=None):
         self.positions = np.ascontiguousarray(positions, np.float32)
         self.indices = np.ascontiguousarray(indices, np.uint32)
         self.flags = np.ascontiguousarray(flags if flags is not None else np.zeros(len(self.indices)), np.uint32)
         self.h = lib().ocpu_scene_create(_p(self.positions), len(self.positions), _p(self.indices),
                                          len(self.indices), _p(self.flags))
+        if alpha is not None:
+            uv = np.ascontiguousarray(alpha.texcoords, np.float32)
+            tm = np.ascontiguousarray(alpha.tri_material, np.uint32)
+            thr = np.ascontiguousarray(alpha.thresholds, np.float32)
+            al = np.ascontiguousarray(alpha.alphas, np.float32)
+            mt = np.ascontiguousarray(alpha.material_textures, np.uint32)
+            tw = np.array([t.shape[1] for t in alpha.textures], np.uint32)
+            th = np.array([t.shape[0] for t in alpha.textures], np.uint32)
+            mip0 = np.ascontiguousarray(np.concatenate([np.asarray(t, np.uint8).ravel() for t in alpha.textures])
+                                        if len(alpha.textures) else np.zeros(1, np.uint8))
+            lib().ocpu_scene_set_alpha(self.h, _p(self.indices), _p(uv), _p(tm), len(thr), _p(thr), _p(al), _p(mt),
+                                       len(tw), _p(tw), _p(th), _p(mip0))
+
+    def alpha_value(self, prim, bu, bv, lod_ray_cone=False, t=0.0, d=(0.0, 0.0, 1.0), spread=0.0):
+        dd = np.ascontiguousarray(d, np.float32)
+        return lib().ocpu_alpha_value(self.h, prim, bu, bv, int(lod_ray_cone), t, _p(dd), spread)
+
+    def alpha_threshold(self, material):
+        return lib().ocpu_alpha_threshold(self.h, material)
+
+    def alpha_fails(self, prim, bu, bv, lod_ray_cone=False, t=0.0, d=(0.0, 0.0, 1.0), spread=0.0):
+        dd = np.ascontiguousarray(d, np.float32)
+        return bool(lib().ocpu_alpha_fails(self.h, prim, bu, bv, int(lod_ray_cone), t, _p(dd), spread))
 
     @property
     def node_count(self):
@@ -206,14 +241,18 @@ def svao_pass2(cam, vao: VAOData, p: SVAOParams, depth, normals, stencil, sd, ao
     return ao
 
 
+def ray_cone_spread(focal_length, height):
+    return lib().ocpu_ray_cone_spread(focal_length, height)
+
+
 def svao_pass2_raytraced(scene: Scene, cam, vao: VAOData, p: SVAOParams, depth, normals, stencil, ao, cull=1,
-                         ray_pipeline=0, band=(0, 1), threads=None):
+                         ray_pipeline=0, band=(0, 1), threads=None, alpha_test=1):
     """SVAO "AO 2" in the Raytraced secondary mode; returns the updated AO image."""
     H, W = depth.shape
     ao = np.array(ao, np.uint8, copy=True)
     lib().ocpu_svao_pass2_rt_band(scene.h, C.byref(cam), C.byref(vao), C.byref(p), _p(depth), _p(normals), W, H,
-                                  _p(np.ascontiguousarray(stencil, np.uint8)), _p(ao), cull, ray_pipeline, band[0],
-                                  band[1], _threads(threads))
+                                  _p(np.ascontiguousarray(stencil, np.uint8)), _p(ao), cull, ray_pipeline, alpha_test,
+                                  band[0], band[1], _threads(threads))
     return ao
 
 

@@ -16,6 +16,7 @@
 #include "rsd_oracle.h"
 #include <math.h>
 #include <float.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 #include <pthread.h>
@@ -340,6 +341,16 @@ struct oscene {
     uint32_t* order;   /* leaf order -> primitive id */
     onode* nodes;
     uint32_t nnodes;
+    /* alpha-masked materials (ocpu_scene_set_alpha); uv == NULL: none */
+    float* uv;          /* nt * 6: texture coordinates of v0, v1, v2 */
+    uint32_t* mat;      /* nt */
+    float* mthr;        /* alpha threshold, float16-rounded */
+    float* malpha;      /* constant alpha */
+    uint32_t* mtex;     /* texture or 0xffffffff */
+    uint32_t nm, ntex;
+    uint32_t* tw; uint32_t* th; uint32_t* tmips;
+    size_t* toff;       /* first texel of mip 0 */
+    uint8_t* texels;    /* mip chains, R8 */
 };
 
 static float* g_cent; /* centroid array used by the select routine */
@@ -442,8 +453,227 @@ oscene* ocpu_scene_create(const float* pos, uint32_t nv, const uint32_t* ind, ui
 void ocpu_scene_destroy(oscene* s)
 {
     if (!s) return;
-    free(s->tri); free(s->flags); free(s->order); free(s->nodes); free(s);
+    free(s->tri); free(s->flags); free(s->order); free(s->nodes);
+    free(s->uv); free(s->mat); free(s->mthr); free(s->malpha); free(s->mtex);
+    free(s->tw); free(s->th); free(s->tmips); free(s->toff); free(s->texels);
+    free(s);
 }
+
+/* ------------------------------------------------------------------ alpha test
+ * MaterialFactory::alphaTest (Scene/Material/MaterialFactory.slang:124-151) with the
+ * base-colour alpha of StandardMaterial (StandardMaterial.slang:128-132) and the basic test
+ * (AlphaTest.slang:81-84): the hit is discarded when alpha < threshold.  The threshold is
+ * a float16 in MaterialHeader (MaterialData.slang:99).  Texture coordinate interpolation:
+ * Scene::computeVertexData (Scene.slang:444-480).  Sampling follows librsd's definition
+ * (DESIGN.md "Alpha test"): 2x2 box mips (a+b+c+d+2)/4, wrap, bilinear with 8 sub-texel
+ * bits, trilinear with the LOD fraction quantised to 8 bits. */
+
+/* float -> IEEE half (round to nearest even) -> float, through the half's bit pattern */
+static float o_half_round(float f)
+{
+    uint32_t x = o_asuint(f);
+    uint32_t sign = (x >> 16) & 0x8000u;
+    uint32_t e = (x >> 23) & 0xffu, m = x & 0x7fffffu;
+    uint32_t h;
+    if (e == 0xffu) h = sign | 0x7c00u | (m ? 0x200u : 0u);
+    else {
+        int he = (int)e - 127 + 15;
+        if (he >= 31) h = sign | 0x7c00u;
+        else if (he <= 0) {
+            if (he < -10) h = sign;
+            else {
+                uint32_t mm = m | 0x800000u;
+                int shift = 14 - he;            /* 24-bit significand -> subnormal half */
+                uint32_t q = mm >> shift, rem = mm & ((1u << shift) - 1u), half = 1u << (shift - 1);
+                if (rem > half || (rem == half && (q & 1u))) q++;
+                h = sign | q;
+            }
+        } else {
+            uint32_t q = ((uint32_t)he << 10) | (m >> 13), rem = m & 0x1fffu;
+            if (rem > 0x1000u || (rem == 0x1000u && (q & 1u))) q++; /* may carry into inf */
+            h = sign | q;
+        }
+    }
+    /* half -> float */
+    uint32_t hs = (h & 0x8000u) << 16, he2 = (h >> 10) & 0x1fu, hm = h & 0x3ffu;
+    if (he2 == 0x1fu) return o_asfloat(hs | 0x7f800000u | (hm << 13));
+    if (he2 == 0) {
+        float v = (float)hm * (1.0f / 16777216.0f); /* hm 2^-24, exact */
+        return hs ? -v : v;
+    }
+    return o_asfloat(hs | ((he2 - 15 + 127) << 23) | (hm << 13));
+}
+
+void ocpu_scene_set_alpha(oscene* s, const uint32_t* ind, const float* texcoords, const uint32_t* triMat,
+                          uint32_t nm, const float* thr, const float* alpha, const uint32_t* tex,
+                          uint32_t ntex, const uint32_t* tex_w, const uint32_t* tex_h, const uint8_t* mip0)
+{
+    const uint32_t nt = s->nt;
+    s->uv = (float*)malloc(sizeof(float) * 6 * (size_t)(nt ? nt : 1));
+    s->mat = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)(nt ? nt : 1));
+    for (uint32_t i = 0; i < nt; ++i) {
+        for (int k = 0; k < 3; ++k) {
+            const uint32_t v = ind[(size_t)i * 3 + k];
+            s->uv[(size_t)i * 6 + 2 * k] = texcoords[2 * (size_t)v];
+            s->uv[(size_t)i * 6 + 2 * k + 1] = texcoords[2 * (size_t)v + 1];
+        }
+        s->mat[i] = triMat[i];
+    }
+    s->nm = nm;
+    s->mthr = (float*)malloc(sizeof(float) * nm);
+    s->malpha = (float*)malloc(sizeof(float) * nm);
+    s->mtex = (uint32_t*)malloc(sizeof(uint32_t) * nm);
+    for (uint32_t i = 0; i < nm; ++i) {
+        s->mthr[i] = o_half_round(thr[i]);
+        s->malpha[i] = alpha[i];
+        s->mtex[i] = tex[i];
+    }
+    s->ntex = ntex;
+    s->tw = (uint32_t*)malloc(sizeof(uint32_t) * (ntex ? ntex : 1));
+    s->th = (uint32_t*)malloc(sizeof(uint32_t) * (ntex ? ntex : 1));
+    s->tmips = (uint32_t*)malloc(sizeof(uint32_t) * (ntex ? ntex : 1));
+    s->toff = (size_t*)malloc(sizeof(size_t) * (ntex ? ntex : 1));
+    /* total texels of all chains */
+    size_t total = 0;
+    for (uint32_t i = 0; i < ntex; ++i) {
+        uint32_t w = tex_w[i], h = tex_h[i];
+        for (;;) {
+            total += (size_t)w * h;
+            if (w == 1 && h == 1) break;
+            w = w > 1 ? w / 2 : 1;
+            h = h > 1 ? h / 2 : 1;
+        }
+    }
+    s->texels = (uint8_t*)malloc(total ? total : 1);
+    size_t at = 0, src0 = 0;
+    for (uint32_t i = 0; i < ntex; ++i) {
+        uint32_t w = tex_w[i], h = tex_h[i];
+        s->tw[i] = w; s->th[i] = h; s->toff[i] = at;
+        memcpy(s->texels + at, mip0 + src0, (size_t)w * h);
+        src0 += (size_t)w * h;
+        uint32_t mips = 1;
+        while (w > 1 || h > 1) {
+            const uint8_t* src = s->texels + at;
+            uint8_t* dst = s->texels + at + (size_t)w * h;
+            const uint32_t nw = w > 1 ? w / 2 : 1, nh = h > 1 ? h / 2 : 1;
+            for (uint32_t y = 0; y < nh; ++y)
+                for (uint32_t x = 0; x < nw; ++x) {
+                    uint32_t xa = 2 * x < w ? 2 * x : w - 1, xb = 2 * x + 1 < w ? 2 * x + 1 : w - 1;
+                    uint32_t ya = 2 * y < h ? 2 * y : h - 1, yb = 2 * y + 1 < h ? 2 * y + 1 : h - 1;
+                    uint32_t sum = (uint32_t)src[(size_t)ya * w + xa] + src[(size_t)ya * w + xb] +
+                                   src[(size_t)yb * w + xa] + src[(size_t)yb * w + xb];
+                    dst[(size_t)y * nw + x] = (uint8_t)((sum + 2u) >> 2);
+                }
+            at += (size_t)w * h;
+            w = nw; h = nh;
+            mips++;
+        }
+        at += (size_t)w * h;
+        s->tmips[i] = mips;
+    }
+}
+
+static float o_alpha_texel(const uint8_t* lvl, int w, int h, int x, int y)
+{
+    x = ((x % w) + w) % w;
+    y = ((y % h) + h) % h;
+    return (float)lvl[(size_t)y * w + x] / 255.0f;
+}
+
+/* one bilinear tap, wrap addressing, weights quantised to 1/256 */
+static float o_alpha_bilinear(const uint8_t* lvl, int w, int h, float u, float v)
+{
+    float x = u * (float)w - 0.5f, y = v * (float)h - 0.5f;
+    float x0 = floorf(x), y0 = floorf(y);
+    int ix = (int)x0, iy = (int)y0;
+    float qx = floorf((x - x0) * 256.0f + 0.5f), qy = floorf((y - y0) * 256.0f + 0.5f);
+    if (qx >= 256.0f) { qx = 0.0f; ix++; }
+    if (qy >= 256.0f) { qy = 0.0f; iy++; }
+    float wx = qx * (1.0f / 256.0f), wy = qy * (1.0f / 256.0f);
+    float top = o_alpha_texel(lvl, w, h, ix, iy) * (1.0f - wx) + o_alpha_texel(lvl, w, h, ix + 1, iy) * wx;
+    float bot = o_alpha_texel(lvl, w, h, ix, iy + 1) * (1.0f - wx) + o_alpha_texel(lvl, w, h, ix + 1, iy + 1) * wx;
+    return top * (1.0f - wy) + bot * wy;
+}
+
+/* Texture2D.SampleLevel(uv, level), trilinear, LOD clamped to [0, mips - 1], NaN -> 0 */
+static float o_alpha_sample(const oscene* s, uint32_t ti, float u, float v, float level)
+{
+    const int mips = (int)s->tmips[ti];
+    float lod = level;
+    if (lod != lod) lod = 0.0f;
+    if (lod < 0.0f) lod = 0.0f;
+    if (lod > (float)(mips - 1)) lod = (float)(mips - 1);
+    int l = (int)floorf(lod);
+    float qf = floorf((lod - (float)l) * 256.0f + 0.5f);
+    if (qf >= 256.0f) { qf = 0.0f; l++; }
+    size_t off = s->toff[ti];
+    int w = (int)s->tw[ti], h = (int)s->th[ti];
+    for (int m = 0; m < l; ++m) {
+        off += (size_t)w * h;
+        w = w > 1 ? w / 2 : 1;
+        h = h > 1 ? h / 2 : 1;
+    }
+    float a = o_alpha_bilinear(s->texels + off, w, h, u, v);
+    if (qf == 0.0f || l + 1 >= mips) return a;
+    float b = o_alpha_bilinear(s->texels + off + (size_t)w * h, w > 1 ? w / 2 : 1, h > 1 ? h / 2 : 1, u, v);
+    float f = qf * (1.0f / 256.0f);
+    return a * (1.0f - f) + b * f;
+}
+
+/* Camera::computeScreenSpacePixelSpreadAngle (Camera.cpp:296-301) with focalLengthToFovY at
+ * the 24 mm default frame height (FalcorMath.h:123-126), as the "%f" text of the shader
+ * define RAY_CONE_SPREAD (StochasticDepthMapRT.cpp:266-267) read back as a float */
+float ocpu_ray_cone_spread(float focal, uint32_t height)
+{
+    float fov = 2.0f * atanf(0.5f * 24.0f / focal);
+    float ang = atanf(2.0f * tanf(fov * 0.5f) / (float)height);
+    char txt[64];
+    snprintf(txt, sizeof(txt), "%f", (double)ang);
+    return strtof(txt, NULL);
+}
+
+/* 1 = the alpha test discards the hit.  lodRayCone: computeLod of StochasticDepthMapRT.rt.slang:
+ * 31-37 (RayCone(0, spread).propagateDistance(t).computeLOD(0, dir, faceNormalW),
+ * TexLODHelpers.slang:97-129) plus 0.5 log2(w h) (TextureSampler.slang:90-96); else LOD 0.
+ * log2 in double, rounded once (numerics contract). */
+float ocpu_alpha_value(const oscene* s, uint32_t prim, float bu, float bv, int lodRayCone, float t,
+                       const float d[3], float spread)
+{
+    const uint32_t m = s->mat[prim];
+    float alpha = s->malpha[m];
+    const uint32_t ti = s->mtex[m];
+    if (ti != 0xffffffffu) {
+        const float* uv = s->uv + (size_t)prim * 6;
+        const float w0 = 1.0f - bu - bv;
+        float tu = uv[0] * w0 + uv[2] * bu + uv[4] * bv;
+        float tv = uv[1] * w0 + uv[3] * bu + uv[5] * bv;
+        float level = 0.0f;
+        if (lodRayCone) {
+            const float* v = s->tri + (size_t)prim * 9;
+            float e1[3] = {v[3] - v[0], v[4] - v[1], v[5] - v[2]};
+            float e2[3] = {v[6] - v[0], v[7] - v[1], v[8] - v[2]};
+            float cr[3], n[3];
+            o_cross(e1, e2, cr);
+            o_normalize(cr, n);
+            float width = spread * t + 0.0f;
+            float lambda = 0.0f + (float)log2((double)(fabsf(width) / fabsf(o_dot(d, n))));
+            float dims = (float)(s->tw[ti] * s->th[ti]);
+            level = 0.5f * (float)log2((double)dims) + lambda;
+        }
+        alpha = o_alpha_sample(s, ti, tu, tv, level);
+    }
+    return alpha;
+}
+
+int ocpu_alpha_fails(const oscene* s, uint32_t prim, float bu, float bv, int lodRayCone, float t,
+                     const float d[3], float spread)
+{
+    return ocpu_alpha_value(s, prim, bu, bv, lodRayCone, t, d, spread) < s->mthr[s->mat[prim]];
+}
+
+float ocpu_alpha_threshold(const oscene* s, uint32_t material) { return s->mthr[material]; }
+
+static inline int o_alpha_masked(const oscene* s, uint32_t prim) { return s->uv && (s->flags[prim] & 4u); }
 uint32_t ocpu_scene_node_count(const oscene* s) { return s->nnodes; }
 
 /* Conservative slab test in double precision with a relative margin: a node is
@@ -504,7 +734,7 @@ static void o_hits_push(ohits* hs, ohit x)
 }
 
 /* all hits with TMin <= t <= TMax, culling applied, ascending (t, prim) order */
-static void o_collect(const oscene* s, const oray* r, float TMin, float TMax, uint32_t cull, ohits* hs)
+static void o_collect(const oscene* s, const oray* r, float TMin, float TMax, uint32_t cull, int alpha0, ohits* hs)
 {
     if (!s->nt || !(TMin <= TMax)) return;
     uint32_t stack[128];
@@ -523,6 +753,8 @@ static void o_collect(const oscene* s, const oray* r, float TMin, float TMax, ui
                 if (!o_intersect_tri(r, v, v + 3, v + 6, &t, &u, &vv, &det)) continue;
                 if (!(t >= TMin && t <= TMax)) continue;
                 if (o_culled(det, s->flags[prim], cull)) continue;
+                /* any-hit IgnoreHit of an alpha-masked triangle failing at LOD 0 */
+                if (alpha0 && o_alpha_masked(s, prim) && ocpu_alpha_fails(s, prim, u, vv, 0, t, r->d, 0.0f)) continue;
                 ohit x = {t, u, vv, prim, det};
                 o_hits_push(hs, x);
             }
@@ -561,7 +793,7 @@ static void* o_gbuffer_rows(void* arg)
             o_ray_setup(&r, c->posW, d);
             ohits hs = {0};
             hs.limit = 1;
-            o_collect(j->s, &r, tmin, tmax, j->cull, &hs);
+            o_collect(j->s, &r, tmin, tmax, j->cull, 1, &hs); /* GBufferRaster useAlphaTest */
             size_t o = (size_t)y * j->W + x;
             if (hs.n == 0) {
                 if (j->nw) { /* cleared depth buffer / zero normal */
@@ -728,6 +960,7 @@ static void* o_sd_rows(void* arg)
     const uint32_t N = p->sample_count;
     const float DEFAULT = p->normalize ? 1.0f : 3.40282347e+37f; /* Common.slangh:16 */
     const uint32_t ch = N < 4 ? N : 4, layers = (N + 3) / 4;
+    const float spread = ocpu_ray_cone_spread(c->focalLength, j->sdH); /* default dims = SD map */
 
     int32_t lutIdx[33];
     uint32_t* lut = NULL;
@@ -754,13 +987,16 @@ static void* o_sd_rows(void* arg)
                 ohits hs = {0};
                 /* Default / KBuffer always commit by the MAX_COUNT-th hit */
                 hs.limit = (p->implementation == 1) ? 0u : (p->max_count ? p->max_count : 1u);
-                o_collect(j->s, &r, TMin, TMax, p->cull_mode, &hs);
+                o_collect(j->s, &r, TMin, TMax, p->cull_mode, 0, &hs);
                 /* ---- anyHit -> algorithm, Common.slangh:102-254, ascending (t, prim) ---- */
                 for (uint32_t k = 0; k < hs.n; ++k) {
                     j->hits++;
                     float rng = ocpu_hash(hs.h[k].u, hs.h[k].v);
                     float t = hs.h[k].t * cosT; /* RayToViewDepth */
                     if (p->normalize) t = o_saturate((t - c->nearZ) / (c->farZ - c->nearZ));
+                    /* USE_ALPHA_TEST, Common.slangh:155-175: ray-cone LOD at RayTCurrent() */
+                    const int af = p->alpha_test && o_alpha_masked(j->s, hs.h[k].prim) &&
+                                   ocpu_alpha_fails(j->s, hs.h[k].prim, hs.h[k].u, hs.h[k].v, 1, hs.h[k].t, d, spread);
                     int commit;
                     if (p->implementation == 1) { /* CoverageMask */
                         int R = (int)floorf(p->alpha * (float)N + rng);
@@ -771,6 +1007,10 @@ static void* o_sd_rows(void* arg)
                             float a = (float)lutIdx[R], b = (float)lutIdx[R + 1];
                             int index = (int)(a + rng2 * (b - a));
                             mask = lut[index];
+                        }
+                        if (af) { /* alpha test failed: ignore (count stays 0) */
+                            if (count >= p->max_count) break;
+                            continue;
                         }
                         float maxT = 0.0f;
                         for (uint32_t i = 0; i < N; ++i) {
@@ -783,6 +1023,10 @@ static void* o_sd_rows(void* arg)
                         if (t >= depths[N - 1]) { commit = 1; }
                         else {
                             count++;
+                            if (af) {
+                                if (count >= p->max_count) break;
+                                continue;
+                            }
                             float rayT = t;
                             for (uint32_t i = 0; i < N; ++i)
                                 if (t < depths[i]) { float tmp = depths[i]; depths[i] = t; t = tmp; }
@@ -791,7 +1035,7 @@ static void* o_sd_rows(void* arg)
                     } else { /* Default: reservoir */
                         uint32_t slot = count++;
                         if (count > N) slot = (uint32_t)(rng * (float)count);
-                        if (slot < N && !(depths[slot] <= t)) depths[slot] = t; /* opaque: alpha test passes */
+                        if (slot < N && !(depths[slot] <= t) && !af) depths[slot] = t;
                         commit = count >= p->max_count;
                     }
                     if (commit) break; /* committed hit: TMax = t, stream ends */
@@ -1208,7 +1452,7 @@ void ocpu_svao_pass2_band(const ocam* cam, const ovao* d, const osvao_params* p,
  * (t, prim) order, TMax shrinking on a commit. */
 typedef struct {
     const oscene* s; const octx* x; const uint8_t* stencil; uint8_t* ao;
-    uint32_t cull, rayPipeline;
+    uint32_t cull, rayPipeline, alphaTest;
     float invView[9];
     uint32_t y0, y1, bi, bc;
 } ort_job;
@@ -1261,7 +1505,7 @@ static void* o_pass2_rt_rows(void* arg)
                     oray r;
                     o_ray_setup(&r, c->posW, dw);
                     ohits hs = {0};
-                    o_collect(j->s, &r, TMin, TMax, j->cull, &hs);
+                    o_collect(j->s, &r, TMin, TMax, j->cull, (int)j->alphaTest, &hs);
                     for (uint32_t k = 0; k < hs.n; ++k) {
                         const float t = hs.h[k].t;
                         if (t > TMax) break;          /* beyond a committed hit */
@@ -1300,7 +1544,7 @@ static void o_rt_setrows(void* j, uint32_t a, uint32_t b) { ((ort_job*)j)->y0 = 
 void ocpu_svao_pass2_rt_band(const oscene* sc, const ocam* cam, const ovao* d, const osvao_params* p,
                              const float* depth, const uint16_t* normals, uint32_t W, uint32_t H,
                              const uint8_t* stencil, uint8_t* ao, uint32_t cull, uint32_t ray_pipeline,
-                             uint32_t band_index, uint32_t band_count, int nthreads)
+                             uint32_t alpha_test, uint32_t band_index, uint32_t band_count, int nthreads)
 {
     octx x;
     o_ctx_init(&x, cam, d, p, depth, normals, W, H);
@@ -1308,7 +1552,7 @@ void ocpu_svao_pass2_rt_band(const oscene* sc, const ocam* cam, const ovao* d, c
     ort_job* jobs = (ort_job*)calloc((size_t)nthreads, sizeof(ort_job));
     for (int i = 0; i < nthreads; ++i) {
         jobs[i].s = sc; jobs[i].x = &x; jobs[i].stencil = stencil; jobs[i].ao = ao;
-        jobs[i].cull = cull; jobs[i].rayPipeline = ray_pipeline;
+        jobs[i].cull = cull; jobs[i].rayPipeline = ray_pipeline; jobs[i].alphaTest = alpha_test;
         /* float3x3(inverse(viewMat)) = transpose of the view rotation (rigid view matrix) */
         for (int r = 0; r < 3; ++r)
             for (int k = 0; k < 3; ++k) jobs[i].invView[r * 3 + k] = cam->viewMat[k * 4 + r];

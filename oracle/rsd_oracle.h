@@ -91,6 +91,18 @@ typedef struct oscene oscene;
 oscene* ocpu_scene_create(const float* positions, uint32_t nv, const uint32_t* indices,
                           uint32_t nt, const uint32_t* flags);
 void ocpu_scene_destroy(oscene* s);
+/* alpha-masked materials (rsd_alpha_desc restated): texcoords float2[nv], per-triangle
+ * material, per-material threshold / constant alpha / texture (0xffffffff: none), textures
+ * as their mip-0 R8 texels concatenated (the oracle builds its own mip chains) */
+void ocpu_scene_set_alpha(oscene* s, const uint32_t* indices, const float* texcoords, const uint32_t* triMat,
+                          uint32_t nm, const float* threshold, const float* alpha, const uint32_t* texture,
+                          uint32_t ntex, const uint32_t* tex_w, const uint32_t* tex_h, const uint8_t* mip0);
+int ocpu_alpha_fails(const oscene* s, uint32_t prim, float bu, float bv, int lodRayCone, float t,
+                     const float d[3], float spread);
+float ocpu_alpha_value(const oscene* s, uint32_t prim, float bu, float bv, int lodRayCone, float t,
+                       const float d[3], float spread);
+float ocpu_alpha_threshold(const oscene* s, uint32_t material);
+float ocpu_ray_cone_spread(float focal_length, uint32_t height);
 uint32_t ocpu_scene_node_count(const oscene* s);
 
 void ocpu_camera_look_at(const float pos[3], const float target[3], const float up[3],
@@ -162,7 +174,7 @@ int ocpu_intersect(const float o[3], const float d[3], const float v0[3], const 
 void ocpu_svao_pass2_rt_band(const oscene* sc, const ocam* cam, const ovao* d, const osvao_params* p,
                              const float* depth, const uint16_t* normals, uint32_t W, uint32_t H,
                              const uint8_t* stencil, uint8_t* ao, uint32_t cull, uint32_t ray_pipeline,
-                             uint32_t band_index, uint32_t band_count, int nthreads);
+                             uint32_t alpha_test, uint32_t band_index, uint32_t band_count, int nthreads);
 
 #ifdef __cplusplus
 }

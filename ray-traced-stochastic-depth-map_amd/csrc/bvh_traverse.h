@@ -7,6 +7,7 @@
 #pragma once
 #include "rsd_device.h"
 #include "../../include/rsd.h"
+#include "alpha_test.h"
 
 namespace rsd {
 
@@ -165,11 +166,14 @@ constexpr uint32_t kNoItem = 0xffffffffu;
 // useLB, culling applied.  Returns the number of keys found (<= K).  Children are visited
 // nearest-first; the others go to a per-lane LDS stack with their entry distance, and a
 // popped item is dropped without a fetch once the k-th key is nearer than its box.
+// alphaOn: alpha-masked triangles that fail the alpha test at LOD 0 are ignored
+// (closest hit with IgnoreHit in the any-hit shader, GBufferRaster useAlphaTest).
 template <int K>
 __device__ __forceinline__ int trace_knearest(const float4* __restrict__ bvh, uint32_t triOff, const RayCtx& r,
                                               float tmin, float tmax, uint32_t cull, bool useLB, float lbT,
                                               uint32_t lbP, KList<K>& kl, uint32_t* __restrict__ ldsItem,
-                                              float* __restrict__ ldsT, TraceStats& st) {
+                                              float* __restrict__ ldsT, TraceStats& st, bool alphaOn,
+                                              const AlphaData& alpha) {
     kl.clear();
     uint32_t spillItem[kStackTotal - kLdsStack];
     float spillT[kStackTotal - kLdsStack];
@@ -197,6 +201,9 @@ __device__ __forceinline__ int trace_knearest(const float4* __restrict__ bvh, ui
                 if (culled(det, __float_as_uint(q[3 * j + 1].w), cull)) continue;
                 if (useLB && !key_less(lbT, lbP, t, prim)) continue;
                 if (!key_less(t, prim, kl.t[K - 1], kl.p[K - 1])) continue;
+                if (alphaOn && (__float_as_uint(q[3 * j + 1].w) & 4u) &&
+                    alpha_test_fails(alpha, prim, q[3 * j], q[3 * j + 1], q[3 * j + 2], bu, bv, false, t, r.d))
+                    continue;
                 kl.insert(t, prim, first + (uint32_t)j);
                 found = found < K ? found + 1 : K;
             }

@@ -354,7 +354,8 @@ public:
         if (secondary_ == 3) {  // SVAO.cpp:408-455: refine by tracing the scene
             check(rsd_svao_pass2_raytraced(s->scene, &s->camera, &vao_, &svp_, (const float*)depth->ptr,
                                            (const uint16_t*)normals->ptr, width_, height_, (const uint8_t*)stencil->ptr,
-                                           (uint8_t*)ao->ptr, cull_, rayPipeline_ ? 1u : 0u, ctx.stream),
+                                           (uint8_t*)ao->ptr, cull_, rayPipeline_ ? 1u : 0u, alphaTest_ ? 1u : 0u,
+                                           ctx.stream),
                   "SVAO AO 2 (raytraced)");
             return;
         }

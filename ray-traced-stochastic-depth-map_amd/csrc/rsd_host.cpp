@@ -5,9 +5,12 @@
 #include <algorithm>
 #include <cfloat>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <thread>
+#include <vector>
 
 #include "rsd_internal.h"
 
@@ -107,6 +110,144 @@ extern "C" rsd_status rsd_scene_upload(rsd_device* dev, const rsd_scene_desc* de
     return RSD_OK;
 }
 
+namespace {
+// MaterialHeader stores the alpha threshold as float16 (MaterialData.slang:99): round to
+// nearest even at half precision, then widen.
+float round_half(float f) {
+    if (f != f) return f;
+    const float a = std::fabs(f);
+    if (a >= 65520.0f) return std::copysign(INFINITY, f);
+    int e = 0;
+    (void)std::frexp(a, &e);                  // a = m 2^e, m in [0.5, 1)
+    const int q = std::max(e - 11, -24);      // quantum exponent: 10 fraction bits, subnormals
+    return std::ldexp(std::nearbyint(std::ldexp(f, -q)), q);
+}
+
+// The 2x2 box mip chain of one R8 texture (DESIGN.md "Alpha test"): level l+1 texel (x, y)
+// averages level l texels (2x..2x+1, 2y..2y+1), clamped to the level, (a+b+c+d+2)/4.
+void build_mips(const rsd_alpha_texture& t, std::vector<uint8_t>& out, uint32_t& mips) {
+    uint32_t w = t.width, h = t.height;
+    size_t base = out.size();
+    out.insert(out.end(), t.alpha, t.alpha + (size_t)w * h);
+    mips = 1;
+    while (w > 1 || h > 1) {
+        const uint32_t nw = std::max(1u, w >> 1), nh = std::max(1u, h >> 1);
+        const size_t nbase = out.size();
+        out.resize(nbase + (size_t)nw * nh);
+        for (uint32_t y = 0; y < nh; ++y)
+            for (uint32_t x = 0; x < nw; ++x) {
+                const uint32_t x0 = std::min(2 * x, w - 1), x1 = std::min(2 * x + 1, w - 1);
+                const uint32_t y0 = std::min(2 * y, h - 1), y1 = std::min(2 * y + 1, h - 1);
+                const uint8_t* l = out.data() + base;
+                const uint32_t sum = l[(size_t)y0 * w + x0] + l[(size_t)y0 * w + x1] + l[(size_t)y1 * w + x0] +
+                                     l[(size_t)y1 * w + x1] + 2;
+                out[nbase + (size_t)y * nw + x] = (uint8_t)(sum / 4);
+            }
+        base = nbase;
+        w = nw;
+        h = nh;
+        ++mips;
+    }
+}
+}  // namespace
+
+extern "C" rsd_status rsd_scene_upload_alpha(rsd_device* dev, const rsd_scene_desc* desc, const rsd_alpha_desc* alpha,
+                                             rsd_scene** out) {
+    if (!alpha) return rsd_scene_upload(dev, desc, out);
+    if (!dev || !desc || !out || !alpha->triangle_material || !alpha->materials || alpha->material_count == 0 ||
+        (desc->vertex_count && !alpha->texcoords) || (alpha->texture_count && !alpha->textures)) {
+        set_error("rsd_scene_upload_alpha: null argument");
+        return RSD_ERR_INVALID_ARG;
+    }
+    for (uint32_t i = 0; i < alpha->texture_count; ++i) {
+        const rsd_alpha_texture& t = alpha->textures[i];
+        if (t.width == 0 || t.height == 0 || !t.alpha || t.width > 32768 || t.height > 32768) {
+            set_error("rsd_scene_upload_alpha: texture " + std::to_string(i) + " is empty or too large");
+            return RSD_ERR_INVALID_ARG;
+        }
+    }
+    for (uint32_t i = 0; i < alpha->material_count; ++i) {
+        const uint32_t tex = alpha->materials[i].texture;
+        if (tex != RSD_NO_TEXTURE && tex >= alpha->texture_count) {
+            set_error("rsd_scene_upload_alpha: material " + std::to_string(i) + " names a missing texture");
+            return RSD_ERR_INVALID_ARG;
+        }
+    }
+    for (uint32_t i = 0; i < desc->triangle_count; ++i)
+        if (alpha->triangle_material[i] >= alpha->material_count) {
+            set_error("rsd_scene_upload_alpha: triangle_material out of range of material_count");
+            return RSD_ERR_INVALID_ARG;
+        }
+    rsd_status st = rsd_scene_upload(dev, desc, out);
+    if (st != RSD_OK) return st;
+    rsd_scene* s = *out;
+    const uint32_t nt = desc->triangle_count, nm = alpha->material_count, nx = alpha->texture_count;
+    // per-primitive texture coordinates (Scene::computeVertexData reads them per vertex)
+    std::vector<float> uv(6 * (size_t)nt);
+    for (size_t t = 0; t < nt; ++t)
+        for (int j = 0; j < 3; ++j) {
+            const uint32_t v = desc->indices[3 * t + j];
+            uv[6 * t + 2 * j] = alpha->texcoords[2 * (size_t)v];
+            uv[6 * t + 2 * j + 1] = alpha->texcoords[2 * (size_t)v + 1];
+        }
+    std::vector<float> mats(4 * (size_t)nm);
+    for (uint32_t i = 0; i < nm; ++i) {
+        const rsd_material& m = alpha->materials[i];
+        mats[4 * i] = round_half(m.alpha_threshold);
+        mats[4 * i + 1] = m.alpha;
+        std::memcpy(&mats[4 * i + 2], &m.texture, 4);
+        mats[4 * i + 3] = 0.0f;
+    }
+    std::vector<uint32_t> texs(4 * (size_t)nx);
+    std::vector<uint8_t> texels;
+    for (uint32_t i = 0; i < nx; ++i) {
+        texs[4 * i] = alpha->textures[i].width;
+        texs[4 * i + 1] = alpha->textures[i].height;
+        texs[4 * i + 3] = (uint32_t)texels.size();
+        build_mips(alpha->textures[i], texels, texs[4 * i + 2]);
+        if (texels.size() >= (1ull << 32)) {
+            rsd_scene_release(s);
+            *out = nullptr;
+            set_error("rsd_scene_upload_alpha: more than 4 GiB of texels");
+            return RSD_ERR_UNSUPPORTED;
+        }
+    }
+    auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
+    const size_t oUV = 0, oMat = al(uv.size() * 4), oMats = oMat + al(4 * (size_t)nt), oTex = oMats + al(mats.size() * 4),
+                 oTexel = oTex + al(texs.size() * 4), total = oTexel + al(texels.size() + 16);
+    char* d = nullptr;
+    hipError_t e = hipMalloc(&d, total);
+    if (e == hipSuccess) e = hipMemset(d, 0, total);
+    if (e == hipSuccess && nt) e = hipMemcpy(d + oUV, uv.data(), uv.size() * 4, hipMemcpyHostToDevice);
+    if (e == hipSuccess && nt) e = hipMemcpy(d + oMat, alpha->triangle_material, 4 * (size_t)nt, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(d + oMats, mats.data(), mats.size() * 4, hipMemcpyHostToDevice);
+    if (e == hipSuccess && nx) e = hipMemcpy(d + oTex, texs.data(), texs.size() * 4, hipMemcpyHostToDevice);
+    if (e == hipSuccess && !texels.empty()) e = hipMemcpy(d + oTexel, texels.data(), texels.size(), hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        st = rsd::hip_fail(e, "rsd_scene_upload_alpha");
+        (void)hipFree(d);
+        rsd_scene_release(s);
+        *out = nullptr;
+        return st;
+    }
+    s->d_alpha = d;
+    s->alpha.triUV = reinterpret_cast<const float*>(d + oUV);
+    s->alpha.triMat = reinterpret_cast<const uint32_t*>(d + oMat);
+    s->alpha.materials = reinterpret_cast<const float4*>(d + oMats);
+    s->alpha.textures = reinterpret_cast<const uint4*>(d + oTex);
+    s->alpha.texels = reinterpret_cast<const uint8_t*>(d + oTexel);
+    s->device_bytes += total;
+    return RSD_OK;
+}
+
+extern "C" float rsd_ray_cone_spread(float focal_length, uint32_t height) {
+    const float fovY = 2.0f * std::atan(0.5f * 24.0f / focal_length);  // focalLengthToFovY(f, kDefaultFrameHeight)
+    const float angle = std::atan(2.0f * std::tan(fovY * 0.5f) / (float)height);
+    char buf[64];
+    std::snprintf(buf, sizeof(buf), "%f", (double)angle);  // std::to_string(float)
+    return std::strtof(buf, nullptr);
+}
+
 extern "C" rsd_status rsd_scene_info_get(const rsd_scene* s, rsd_scene_info* out) {
     if (!s || !out) {
         set_error("rsd_scene_info_get: null argument");
@@ -129,6 +270,7 @@ extern "C" void rsd_scene_release(rsd_scene* s) {
     (void)hipFree(s->d_counters);
     (void)hipFree(s->d_qctl);
     (void)hipFree(s->d_queue);
+    (void)hipFree(s->d_alpha);
     delete s;
 }
 

@@ -12,6 +12,18 @@ struct rsd_device {
     int cu_count = 0;
 };
 
+namespace rsd {
+// Alpha-masked materials on the device (csrc/alpha_test.h); triUV == null: none uploaded
+struct AlphaData {
+    const float* triUV = nullptr;      // 6 floats per primitive (uv0, uv1, uv2)
+    const uint32_t* triMat = nullptr;  // material per primitive
+    const float4* materials = nullptr; // {threshold (float16-rounded), constant alpha, texture (bits), 0}
+    const uint4* textures = nullptr;   // {width, height, mip count, first texel}
+    const uint8_t* texels = nullptr;   // all mips of all textures, R8
+    float spread = 0.0f;               // RAY_CONE_SPREAD of the SD pass (set per launch)
+};
+}  // namespace rsd
+
 struct rsd_scene {
     rsd_device* dev = nullptr;
     float4* d_nodes = nullptr;   // one allocation: 8 x float4 per wide node, then
@@ -25,6 +37,8 @@ struct rsd_scene {
     uint32_t* d_qctl = nullptr;    // live-ray queue {count[32], head[32]}
     void* d_queue = nullptr;       // SD-trace workspace (live-ray records + K-key slots), grow-only
     size_t queue_cap = 0;          // bytes
+    void* d_alpha = nullptr;       // alpha data (rsd_scene_upload_alpha), one allocation
+    rsd::AlphaData alpha;          // device pointers into d_alpha
 };
 
 namespace rsd {

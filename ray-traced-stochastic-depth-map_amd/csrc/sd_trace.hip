@@ -57,6 +57,8 @@ struct SDArgs {
     int bandIndex, bandCount;  // screen-band sharding: 8-row tile rows t with t % count == index
     int poolSoft;      // row traversal: above this many pooled items a row pops one item per step
     const float* rayTab;  // per-column / per-row ray terms (ray_table_kernel), see sd_ray
+    uint32_t alphaTest;   // USE_ALPHA_TEST and the scene has alpha data
+    AlphaData alphaData;  // spread = RAY_CONE_SPREAD
 };
 
 // Per-column and per-row terms of initRayDesc, evaluated once per frame size with exactly the
@@ -303,6 +305,7 @@ __device__ __forceinline__ void sd_resolve(const SDArgs& a, f3 d, float TMin, fl
         // barycentrics + hash of hit j are computed by lane j % 4 (re-running the identical
         // triangle test on the hit's record), then shared with the quad
         float rngL[J], zL[J];
+        uint32_t afL = 0u;  // bit i: hit 4 i + q fails the alpha test
 #pragma unroll
         for (int i = 0; i < J; ++i) {
             const int j = 4 * i + q;
@@ -314,17 +317,22 @@ __device__ __forceinline__ void sd_resolve(const SDArgs& a, f3 d, float TMin, fl
                 if (jj == j) ti = kl.l[jj];
             if (j < found) {
                 float t, bu, bv, det;
-                intersect_tri(r, a.tris[3 * ti], a.tris[3 * ti + 1], a.tris[3 * ti + 2], t, bu, bv, det);
+                const float4 v0 = a.tris[3 * ti], v1 = a.tris[3 * ti + 1], v2 = a.tris[3 * ti + 2];
+                intersect_tri(r, v0, v1, v2, t, bu, bv, det);
                 rngL[i] = sd_hash(bu, bv);
                 float z = t * cosT;  // RayToViewDepth
                 if (a.normalize) z = saturate((z - c.nearZ) / (c.farZ - c.nearZ));
                 zL[i] = z;
+                if (a.alphaTest && (__float_as_uint(v1.w) & 4u) &&
+                    alpha_test_fails(a.alphaData, __float_as_uint(v0.w), v0, v1, v2, bu, bv, true, t, r.d))
+                    afL |= 1u << i;
             }
         }
 #pragma unroll
         for (int j = 0; j < K; ++j) {
             const float rng = qself(rngL[j / 4], j % 4);
             float z = qself(zL[j / 4], j % 4);
+            const bool af = (qselu(afL, j % 4) >> (j / 4)) & 1u;
             if (commit || j >= found) continue;
             hitsDelivered++;
             if (a.impl == 1u) {  // CoverageMask, Common.slangh:117-131, 189-209
@@ -335,6 +343,10 @@ __device__ __forceinline__ void sd_resolve(const SDArgs& a, f3 d, float TMin, fl
                     const float rng2 = sd_hash(rng, z);  // hash3D(float3(bary, t))
                     const float lo = (float)a.lutIdx[R], hi = (float)a.lutIdx[R + 1];
                     mask = a.lut[(int)(lo + rng2 * (hi - lo))];
+                }
+                if (af) {  // alpha test failed: ignore the hit (count is 0 here)
+                    commit = count >= a.maxCount;
+                    continue;
                 }
                 float maxT = 0.0f;
 #pragma unroll
@@ -348,6 +360,10 @@ __device__ __forceinline__ void sd_resolve(const SDArgs& a, f3 d, float TMin, fl
                     commit = true;
                 } else {
                     count++;
+                    if (af) {
+                        commit = count >= a.maxCount;
+                        continue;
+                    }
                     const float rayT = z;
 #pragma unroll
                     for (int i = 0; i < N; ++i)
@@ -359,7 +375,7 @@ __device__ __forceinline__ void sd_resolve(const SDArgs& a, f3 d, float TMin, fl
                 if (count > (uint32_t)N) slot = (uint32_t)(rng * (float)count);
 #pragma unroll
                 for (int i = 0; i < N; ++i)
-                    if ((uint32_t)i == slot && !(depths[i] <= z)) depths[i] = z;
+                    if ((uint32_t)i == slot && !(depths[i] <= z) && !af) depths[i] = z;
                 commit = count >= a.maxCount;
             }
         }
@@ -549,13 +565,15 @@ __device__ __forceinline__ int row_prefix(int v, int l, int base, int& total) {
 // lane j of the row holds key j's hash `rng` and normalized view depth `z`.  Every lane of
 // the row ends with the same depths / cnt / commit.
 template <int K, int N>
-__device__ __forceinline__ bool sd_algorithm_row(const SDArgs& a, float rng, float z, int found, int base,
-                                                 float (&depths)[N], uint32_t& cnt, uint32_t& delivered) {
+__device__ __forceinline__ bool sd_algorithm_row(const SDArgs& a, float rng, float z, bool afl, int found,
+                                                 int base, float (&depths)[N], uint32_t& cnt, uint32_t& delivered) {
     bool commit = false;
+    const uint64_t afm = __ballot(afl);  // bit base + j: key j fails the alpha test
 #pragma unroll
     for (int j = 0; j < K; ++j) {
         const float rj = __shfl(rng, base + j);
         float zj = __shfl(z, base + j);
+        const bool af = (afm >> (base + j)) & 1u;
         if (commit || j >= found) continue;
         delivered++;
         if (a.impl == 1u) {  // CoverageMask, Common.slangh:117-131, 189-209
@@ -566,6 +584,10 @@ __device__ __forceinline__ bool sd_algorithm_row(const SDArgs& a, float rng, flo
                 const float rng2 = sd_hash(rj, zj);  // hash3D(float3(bary, t))
                 const float lo = (float)a.lutIdx[R], hi = (float)a.lutIdx[R + 1];
                 mask = a.lut[(int)(lo + rng2 * (hi - lo))];
+            }
+            if (af) {  // alpha test failed: ignore the hit (count is 0 here)
+                commit = cnt >= a.maxCount;
+                continue;
             }
             float maxT = 0.0f;
 #pragma unroll
@@ -579,6 +601,10 @@ __device__ __forceinline__ bool sd_algorithm_row(const SDArgs& a, float rng, flo
                 commit = true;
             } else {
                 cnt++;
+                if (af) {
+                    commit = cnt >= a.maxCount;
+                    continue;
+                }
                 const float rayT = zj;
 #pragma unroll
                 for (int i = 0; i < N; ++i)
@@ -590,7 +616,7 @@ __device__ __forceinline__ bool sd_algorithm_row(const SDArgs& a, float rng, flo
             if (cnt > (uint32_t)N) slot = (uint32_t)(rj * (float)cnt);
 #pragma unroll
             for (int i = 0; i < N; ++i)
-                if ((uint32_t)i == slot && !(depths[i] <= zj)) depths[i] = zj;
+                if ((uint32_t)i == slot && !(depths[i] <= zj) && !af) depths[i] = zj;
             commit = cnt >= a.maxCount;
         }
     }
@@ -599,13 +625,18 @@ __device__ __forceinline__ bool sd_algorithm_row(const SDArgs& a, float rng, flo
 
 // hash + normalized view depth of the hit (t, triangle record tri) -- the barycentrics come
 // from re-running the identical triangle test (Common.slangh:110-115)
+// (af: an alpha-masked triangle fails the alpha test at the ray-cone LOD of the hit,
+// StochasticDepthMapRT.rt.slang:31-37 + Common.slangh:155-175)
 __device__ __forceinline__ void sd_hit_terms(const SDArgs& a, const RayCtx& r, float cosT, uint32_t tri, float& rng,
-                                             float& z) {
+                                             float& z, bool& af) {
     float t, bu, bv, det;
-    intersect_tri(r, a.tris[3 * tri], a.tris[3 * tri + 1], a.tris[3 * tri + 2], t, bu, bv, det);
+    const float4 v0 = a.tris[3 * tri], v1 = a.tris[3 * tri + 1], v2 = a.tris[3 * tri + 2];
+    intersect_tri(r, v0, v1, v2, t, bu, bv, det);
     rng = sd_hash(bu, bv);
     z = t * cosT;  // RayToViewDepth
     if (a.normalize) z = saturate((z - a.cam.nearZ) / (a.cam.farZ - a.cam.nearZ));
+    af = a.alphaTest && (__float_as_uint(v1.w) & 4u) &&
+         alpha_test_fails(a.alphaData, __float_as_uint(v0.w), v0, v1, v2, bu, bv, true, t, r.d);
 }
 
 // ROW lanes per ray (8 or 16, >= K: lane j of the row holds key j), 64 / ROW rays per wave.
@@ -841,9 +872,10 @@ __global__ void __launch_bounds__(kBlock) sd_trace_row_kernel(SDArgs a, const fl
         // ascending (t, prim) order; lane j prepares key j
         const int found = min(K, __popc(row_bits<ROW>(kp != kNoItem, base)));
         float rng = 0.0f, z = 0.0f;
-        if (l < found) sd_hit_terms(a, r, cosT, kl, rng, z);
+        bool af = false;
+        if (l < found) sd_hit_terms(a, r, cosT, kl, rng, z, af);
         uint32_t delivered = 0;
-        const bool commit = sd_algorithm_row<K, N>(a, rng, z, found, base, depths, cnt, delivered);
+        const bool commit = sd_algorithm_row<K, N>(a, rng, z, af, found, base, depths, cnt, delivered);
         if (l == 0) hitsDelivered += delivered;
         if (CNT && l == 0) tResolve += __builtin_amdgcn_s_memtime() - tS1;
         if (!commit && found == K) {
@@ -921,18 +953,18 @@ __global__ void __launch_bounds__(kBlock) sd_resolve_row_kernel(SDArgs a, const 
             RayCtx r;
             ray_setup(r, mk(c.posW[0], c.posW[1], c.posW[2]), d);
             float rng = 0.0f, z = 0.0f;
-            bool valid = false;
+            bool valid = false, af = false;
             if (l < K) {
                 const uint2 k = keys[(size_t)slot * K + l];
                 valid = k.y != kNoItem;
-                if (valid) sd_hit_terms(a, r, cosT, k.y, rng, z);
+                if (valid) sd_hit_terms(a, r, cosT, k.y, rng, z, af);
             }
             const int found = __popc(row_bits<ROW>(valid, base));  // keys are sorted: a prefix
             float depths[N];
 #pragma unroll
             for (int i = 0; i < N; ++i) depths[i] = DEFAULT;
             uint32_t cnt = 0;
-            sd_algorithm_row<K, N>(a, rng, z, found, base, depths, cnt, delivered);
+            sd_algorithm_row<K, N>(a, rng, z, af, found, base, depths, cnt, delivered);
             if (l == 0) sd_store<N>(a, (int)(idx % (uint32_t)a.sdW), (int)(idx / (uint32_t)a.sdW), depths);
         }
     }
@@ -954,6 +986,8 @@ struct GBArgs {
     float* z;
     uint16_t* n;
     float4* nw;  // raster mode: world face normal (RGBA32F); z then holds non-linear depth
+    uint32_t alphaTest;  // the scene has alpha data: alpha test at LOD 0 (GBufferRaster useAlphaTest)
+    AlphaData alpha;
 };
 
 __global__ void __launch_bounds__(kBlock) gbuffer_kernel(GBArgs a) {
@@ -974,7 +1008,7 @@ __global__ void __launch_bounds__(kBlock) gbuffer_kernel(GBArgs a) {
     KList<1> kl;
     TraceStats st{0u, 0u, 0u};
     const int found = trace_knearest<1>(a.nodes, a.triOff, r, c.nearZ * invCos, c.farZ * invCos, a.cull, false,
-                                        0.0f, 0u, kl, &sstack[lane], &sstackT[lane], st);
+                                        0.0f, 0u, kl, &sstack[lane], &sstackT[lane], st, a.alphaTest != 0u, a.alpha);
     const size_t o = (size_t)y * a.W + x;
     if (!found) {
         if (a.nw) {
@@ -1181,6 +1215,9 @@ extern "C" rsd_status rsd_sd_trace_band(rsd_scene* scene, const rsd_camera* cam,
     a.counters = nullptr;
     a.bandIndex = (int)band_index;
     a.bandCount = (int)band_count;
+    a.alphaTest = p->alpha_test && scene->d_alpha ? 1u : 0u;
+    a.alphaData = scene->alpha;
+    a.alphaData.spread = rsd_ray_cone_spread(cam->focalLength, sd_h);  // default texture dims = SD map
     if (p->implementation == RSD_SD_COVERAGE_MASK) {
         rsd_status s = ensure_lut(N, &a.lutIdx, &a.lut);
         if (s != RSD_OK) return s;
@@ -1242,7 +1279,7 @@ extern "C" rsd_status rsd_sd_trace_band(rsd_scene* scene, const rsd_camera* cam,
     // depth-first quad walk (A/B measurements)
     const int depth = (int)std::max(1u, scene->stats.wide_depth);
     a.poolSoft = std::min(kPoolCap - 48 - 3 * depth, 160);
-    static const char* walkEnv = std::getenv("RSD_TRACE_WALK");
+    const char* walkEnv = std::getenv("RSD_TRACE_WALK");  // read per call: tests cover every walk
     const std::string walkName = walkEnv ? walkEnv : "";
     // The row walk wins when few rays are live (the launch is the slowest ray's chain); with
     // more SD texels the live rays fill the machine and the quad walk's lane utilisation wins
@@ -1319,7 +1356,7 @@ extern "C" rsd_status rsd_gbuffer(rsd_scene* scene, const rsd_camera* cam, uint3
         return RSD_OK;
     }
     GBArgs a{scene->d_nodes, scene->d_tris, scene->tri_offset, *cam, (int)width, (int)height, cull_mode, d_linear_z,
-             d_normals, nullptr};
+             d_normals, nullptr, scene->d_alpha ? 1u : 0u, scene->alpha};
     dim3 grid((width + kTile - 1) / kTile, (height + kTile - 1) / kTile);
     hipLaunchKernelGGL(gbuffer_kernel, grid, dim3(kBlock), 0, s, a);
     hipError_t e = hipGetLastError();
@@ -1342,7 +1379,7 @@ extern "C" rsd_status rsd_gbuffer_raster(rsd_scene* scene, const rsd_camera* cam
         return RSD_OK;
     }
     GBArgs a{scene->d_nodes, scene->d_tris, scene->tri_offset, *cam, (int)width, (int)height, cull_mode, d_depth,
-             nullptr, reinterpret_cast<float4*>(d_normal_w)};
+             nullptr, reinterpret_cast<float4*>(d_normal_w), scene->d_alpha ? 1u : 0u, scene->alpha};
     dim3 grid((width + kTile - 1) / kTile, (height + kTile - 1) / kTile);
     hipLaunchKernelGGL(gbuffer_kernel, grid, dim3(kBlock), 0, s, a);
     hipError_t e = hipGetLastError();

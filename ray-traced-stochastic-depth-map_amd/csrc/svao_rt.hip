@@ -8,7 +8,8 @@
 //
 // Any-hit order.  As for the SD trace, the hit stream is canonical: ascending t, each
 // triangle once.  aoAnyHit over that stream (accepted = front face, or double-sided, or
-// alpha-masked; culled triangles never arrive):
+// alpha-masked; culled triangles and, with USE_ALPHA_TEST, alpha-masked triangles failing the
+// alpha test at LOD 0 never arrive):
 //     t <= tSphereStart:  halo = max(halo, t); end the query if t >= tConstRadiusStart
 //     t >  tSphereStart:  inside = min(inside, t); commit (TMax = t) -- nothing nearer follows
 // The query therefore ends at the first accepted hit A with term(A) = (A > tSphereStart ||
@@ -35,12 +36,15 @@ struct RtArgs {
     uint32_t cull;
     uint32_t rayPipeline;  // 1: ray-pipeline dispatch extent (SVAO.cpp:429-430), 0: compute (:452-453)
     float invView[9];      // float3x3(inverse(viewMat)), row-major
+    uint32_t alphaTest;    // USE_ALPHA_TEST and the scene has alpha data
+    AlphaData alpha;
 };
 
 // The aoAnyHit stream of one AO ray reduced to (A, B), see the file header.
 __device__ __forceinline__ void trace_ao(const float4* __restrict__ bvh, uint32_t triOff, const RayCtx& r, float tmin,
                                          float tmax, uint32_t cull, float tCRS, float tSS, float& A, float& B,
-                                         uint32_t* __restrict__ ldsItem, float* __restrict__ ldsT) {
+                                         uint32_t* __restrict__ ldsItem, float* __restrict__ ldsT, bool alphaOn,
+                                         const AlphaData& alpha) {
     A = INFINITY;
     B = -INFINITY;
     uint32_t spillItem[kStackTotal - kLdsStack];
@@ -67,6 +71,11 @@ __device__ __forceinline__ void trace_ao(const float4* __restrict__ bvh, uint32_
                 // aoAnyHit: frontFace || isDoubleSided || isAlphaTested (Common.slang:695-697)
                 const bool front = (det > 0.0f) != ((flags & RSD_TRI_FRONT_CW) != 0u);
                 if (!(front || (flags & (RSD_TRI_DOUBLE_SIDED | RSD_TRI_ALPHA_MASK)))) continue;
+                // USE_ALPHA_TEST: alpha test at LOD 0 (Common.slang:683-691) -> AO_HIT_IGNORE
+                if (alphaOn && (flags & RSD_TRI_ALPHA_MASK) &&
+                    alpha_test_fails(alpha, __float_as_uint(q[3 * j].w), q[3 * j], q[3 * j + 1], q[3 * j + 2], bu, bv,
+                                     false, t, r.d))
+                    continue;
                 if (t > tSS || t >= tCRS) A = fminf(A, t);
                 else B = fmaxf(B, t);
             }
@@ -177,7 +186,8 @@ __global__ void __launch_bounds__(64) svao_pass2_rt_kernel(RtArgs ra) {
             RayCtx r;
             ray_setup(r, camPos, dw);
             float A, B;
-            trace_ao(ra.nodes, ra.triOff, r, TMin, TMax, ra.cull, tCRS, tSS, A, B, &sItem[lane], &sT[lane]);
+            trace_ao(ra.nodes, ra.triOff, r, TMin, TMax, ra.cull, tCRS, tSS, A, B, &sItem[lane], &sT[lane],
+                     ra.alphaTest != 0u, ra.alpha);
             if (B != -INFINITY) halo = hmax(halo, B);
             if (A != INFINITY) {
                 if (A <= tSS) halo = hmax(halo, A);
@@ -206,8 +216,8 @@ extern "C" rsd_status rsd_svao_pass2_raytraced_band(rsd_scene* scene, const rsd_
                                                     const rsd_svao_params* p, const float* d_depth,
                                                     const uint16_t* d_normals, uint32_t W, uint32_t H,
                                                     const uint8_t* d_stencil, uint8_t* d_ao, uint32_t cull_mode,
-                                                    uint32_t ray_pipeline, uint32_t band_index, uint32_t band_count,
-                                                    rsd_stream stream) {
+                                                    uint32_t ray_pipeline, uint32_t alpha_test, uint32_t band_index,
+                                                    uint32_t band_count, rsd_stream stream) {
     if (band_count == 0 || band_index >= band_count) {
         set_error("rsd_svao_pass2_raytraced_band: band_index must be < band_count");
         return RSD_ERR_INVALID_ARG;
@@ -242,6 +252,8 @@ extern "C" rsd_status rsd_svao_pass2_raytraced_band(rsd_scene* scene, const rsd_
     ra.triOff = scene->tri_offset;
     ra.cull = cull_mode;
     ra.rayPipeline = ray_pipeline ? 1u : 0u;
+    ra.alphaTest = alpha_test && scene->d_alpha ? 1u : 0u;
+    ra.alpha = scene->alpha;
     // float3x3(inverse(viewMat)): the view matrix is a rotation + translation, so the rotation
     // part of its inverse is the transpose (exact; Falcor's general inverse rounds it)
     for (int r = 0; r < 3; ++r)
@@ -260,7 +272,7 @@ extern "C" rsd_status rsd_svao_pass2_raytraced(rsd_scene* scene, const rsd_camer
                                                const rsd_svao_params* p, const float* d_depth,
                                                const uint16_t* d_normals, uint32_t W, uint32_t H,
                                                const uint8_t* d_stencil, uint8_t* d_ao, uint32_t cull_mode,
-                                               uint32_t ray_pipeline, rsd_stream stream) {
+                                               uint32_t ray_pipeline, uint32_t alpha_test, rsd_stream stream) {
     return rsd_svao_pass2_raytraced_band(scene, cam, vao, p, d_depth, d_normals, W, H, d_stencil, d_ao, cull_mode,
-                                         ray_pipeline, 0, 1, stream);
+                                         ray_pipeline, alpha_test, 0, 1, stream);
 }

@@ -30,6 +30,22 @@ class SceneDesc(C.Structure):
                 ("triangle_count", C.c_uint32), ("triangle_flags", C.c_void_p)]
 
 
+NO_TEXTURE = 0xFFFFFFFF
+
+
+class AlphaTexture(C.Structure):
+    _fields_ = [("width", C.c_uint32), ("height", C.c_uint32), ("alpha", C.c_void_p)]
+
+
+class Material(C.Structure):
+    _fields_ = [("alpha_threshold", C.c_float), ("alpha", C.c_float), ("texture", C.c_uint32)]
+
+
+class AlphaDesc(C.Structure):
+    _fields_ = [("texcoords", C.c_void_p), ("triangle_material", C.c_void_p), ("materials", C.POINTER(Material)),
+                ("material_count", C.c_uint32), ("textures", C.POINTER(AlphaTexture)), ("texture_count", C.c_uint32)]
+
+
 class SceneInfo(C.Structure):
     _fields_ = [("triangle_count", C.c_uint32), ("node_count", C.c_uint32), ("max_depth", C.c_uint32),
                 ("leaf_count", C.c_uint32), ("sah_cost", C.c_double), ("build_ms", C.c_double),
@@ -77,7 +93,8 @@ EXPORTS = ["rsd_abi_version", "rsd_last_error", "rsd_device_open", "rsd_device_c
            "rsd_scene_info_get", "rsd_scene_release", "rsd_camera_look_at", "rsd_svao_make_vao_data",
            "rsd_gbuffer", "rsd_sd_trace", "rsd_svao_clear_intervals", "rsd_svao_pass1", "rsd_svao_pass2",
            "rsd_sd_trace_band", "rsd_svao_pass1_band", "rsd_svao_pass2_band", "rsd_gbuffer_raster",
-           "rsd_linearize_depth", "rsd_compress_normals", "rsd_svao_pass2_raytraced", "rsd_svao_pass2_raytraced_band"]
+           "rsd_linearize_depth", "rsd_compress_normals", "rsd_svao_pass2_raytraced", "rsd_svao_pass2_raytraced_band",
+           "rsd_scene_upload_alpha", "rsd_ray_cone_spread"]
 
 # every symbol include/rsd_graph.h declares
 GRAPH_EXPORTS = ["rsd_graph_create", "rsd_graph_destroy", "rsd_graph_create_pass", "rsd_graph_add_edge",
@@ -112,6 +129,10 @@ def lib():
         L.rsd_device_close.argtypes = [vp]
         L.rsd_scene_upload.restype = st
         L.rsd_scene_upload.argtypes = [vp, C.POINTER(SceneDesc), C.POINTER(vp)]
+        L.rsd_scene_upload_alpha.restype = st
+        L.rsd_scene_upload_alpha.argtypes = [vp, C.POINTER(SceneDesc), C.POINTER(AlphaDesc), C.POINTER(vp)]
+        L.rsd_ray_cone_spread.restype = f32
+        L.rsd_ray_cone_spread.argtypes = [f32, u32]
         L.rsd_scene_info_get.restype = st
         L.rsd_scene_info_get.argtypes = [vp, C.POINTER(SceneInfo)]
         L.rsd_scene_release.argtypes = [vp]
@@ -144,10 +165,10 @@ def lib():
                                           u32, vp, vp, u32, u32, vp, u32, u32, vp]
         L.rsd_svao_pass2_raytraced.restype = st
         L.rsd_svao_pass2_raytraced.argtypes = [vp, C.POINTER(Camera), C.POINTER(VAOData), C.POINTER(SVAOParams), vp, vp,
-                                               u32, u32, vp, vp, u32, u32, vp]
+                                               u32, u32, vp, vp, u32, u32, u32, vp]
         L.rsd_svao_pass2_raytraced_band.restype = st
         L.rsd_svao_pass2_raytraced_band.argtypes = [vp, C.POINTER(Camera), C.POINTER(VAOData), C.POINTER(SVAOParams),
-                                                    vp, vp, u32, u32, vp, vp, u32, u32, u32, u32, vp]
+                                                    vp, vp, u32, u32, vp, vp, u32, u32, u32, u32, u32, vp]
         L.rsd_gbuffer_raster.restype = st
         L.rsd_gbuffer_raster.argtypes = [vp, C.POINTER(Camera), u32, u32, u32, vp, vp, vp]
         L.rsd_linearize_depth.restype = st

@@ -45,6 +45,7 @@ class FrameConfig:
     exponent: float = 2.0
     secondary: int = abi.DEPTH_STOCHASTIC  # SVAO secondaryDepthMode: 0 Single, 2 StochasticDepth, 3 Raytraced
     ray_pipeline: bool = True              # SVAO rayPipeline (SVAO.h:101): pass-2 extent in Raytraced mode
+    alpha_test: bool = True                # SVAO alphaTest (SVAO.h:104) -> SD AlphaTest; no-op on opaque scenes
     thickness: float = 0.0
     sd_guard_px: int = 512
     num_directions: int = 8
@@ -96,7 +97,7 @@ def make_vao(cfg: FrameConfig):
 def sd_params(cfg: FrameConfig, sd_guard: int) -> abi.SDParams:
     # SVAO::compile builds the nested SD pass with these Properties (SVAO.cpp:158-183)
     return abi.SDParams(cfg.sd_samples, cfg.implementation, cfg.max_count, sd_guard, int(cfg.jitter), 1,
-                        int(cfg.ray_interval), cfg.cull_mode, 0, float(np.float32(1.5 / cfg.sd_samples)))
+                        int(cfg.ray_interval), cfg.cull_mode, int(cfg.alpha_test), float(np.float32(1.5 / cfg.sd_samples)))
 
 
 def svao_params(cfg: FrameConfig) -> abi.SVAOParams:
@@ -117,12 +118,31 @@ class Device:
             self.h = None
 
 
+def alpha_desc(a):
+    """rsd_alpha_desc of a scenes.AlphaMaterials (and the objects it points into)."""
+    mats = (abi.Material * len(a.thresholds))(*[abi.Material(float(t), float(al), int(x)) for t, al, x in
+                                                 zip(a.thresholds, a.alphas, a.material_textures)])
+    texs = [np.ascontiguousarray(t, np.uint8) for t in a.textures]
+    tx = (abi.AlphaTexture * max(1, len(texs)))(*[abi.AlphaTexture(t.shape[1], t.shape[0], t.ctypes.data)
+                                                  for t in texs])
+    uv = np.ascontiguousarray(a.texcoords, np.float32)
+    tm = np.ascontiguousarray(a.tri_material, np.uint32)
+    d = abi.AlphaDesc(uv.ctypes.data, tm.ctypes.data, mats, len(mats), tx, len(texs))
+    return d, (mats, texs, tx, uv, tm)
+
+
 class GpuScene:
     def __init__(self, dev: Device, scene: Scene):
         desc = abi.SceneDesc(scene.positions.ctypes.data, scene.positions.shape[0], scene.indices.ctypes.data,
                              scene.indices.shape[0], scene.flags.ctypes.data)
         h = C.c_void_p()
-        abi.check(abi.lib().rsd_scene_upload(dev.h, C.byref(desc), C.byref(h)), "rsd_scene_upload")
+        if scene.alpha is None:
+            abi.check(abi.lib().rsd_scene_upload(dev.h, C.byref(desc), C.byref(h)), "rsd_scene_upload")
+        else:
+            ad, keep = alpha_desc(scene.alpha)
+            abi.check(abi.lib().rsd_scene_upload_alpha(dev.h, C.byref(desc), C.byref(ad), C.byref(h)),
+                      "rsd_scene_upload_alpha")
+            del keep
         self.h = h
         self.info = abi.SceneInfo()
         abi.check(abi.lib().rsd_scene_info_get(h, C.byref(self.info)), "rsd_scene_info_get")
@@ -207,7 +227,7 @@ class Renderer:
                                                           C.byref(self.svp), _ptr(self.depth), _ptr(self.normals),
                                                           self.cfg.fb_w, self.cfg.fb_h, _ptr(self.stencil),
                                                           _ptr(self.ao), self.cfg.cull_mode, int(self.cfg.ray_pipeline),
-                                                          band[0], band[1], self.stream),
+                                                          int(self.cfg.alpha_test), band[0], band[1], self.stream),
                   "rsd_svao_pass2_raytraced_band")
 
     def frame(self):

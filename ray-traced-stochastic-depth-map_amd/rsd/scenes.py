@@ -14,6 +14,11 @@ meshes the same way): positions float32[nv,3], indices uint32[nt,3] and one
 flags word per triangle (bit0 double-sided -> TriangleFacingCullDisable,
 bit1 front-face clockwise -> TriangleFrontCounterClockwise, Scene.cpp:3446-3452).
 Winding is counter-clockwise seen from the front (Falcor's right-handed default).
+
+Alpha-masked materials: with `alpha=True` the thin foliage cards become
+alpha-masked (flag bit2, AlphaMode::Mask) and carry texture coordinates into procedural R8
+leaf / lattice textures (AlphaMaterials); a few extra cards stand in the camera's view.
+The geometry is otherwise identical to the opaque scene of the same name and seed.
 """
 from __future__ import annotations
 
@@ -27,12 +32,55 @@ FLAG_ALPHA_MASK = 4
 
 
 @dataclasses.dataclass
+class AlphaMaterials:
+    """rsd_alpha_desc in numpy: per-vertex texture coordinates, a material per triangle,
+    per-material alpha threshold / constant alpha / texture, R8 textures (mip 0)."""
+    texcoords: np.ndarray          # float32 [nv, 2]
+    tri_material: np.ndarray       # uint32 [nt]
+    thresholds: np.ndarray         # float32 [m]
+    alphas: np.ndarray             # float32 [m]
+    material_textures: np.ndarray  # uint32 [m], NO_TEXTURE = 0xffffffff
+    textures: list                 # uint8 [h, w] each
+
+
+NO_TEXTURE = 0xFFFFFFFF
+
+
+def alpha_textures():
+    """Procedural R8 alpha textures: 0 = leaves (soft-edged ellipses), 1 = lattice (bars),
+    2 = a 3 x 5 odd-sized noise pattern (non-power-of-two mip chain)."""
+    y, x = np.mgrid[0:64, 0:64].astype(np.float64) + 0.5
+    leaf = np.zeros((64, 64))
+    for cx, cy, rx, ry, a in ((20, 18, 14, 8, 0.5), (44, 40, 16, 7, -0.6), (18, 48, 9, 13, 0.2), (50, 12, 8, 6, 1.1)):
+        c, s_ = np.cos(a), np.sin(a)
+        u = ((x - cx) * c + (y - cy) * s_) / rx
+        v = (-(x - cx) * s_ + (y - cy) * c) / ry
+        leaf = np.maximum(leaf, np.clip((1.0 - (u * u + v * v)) * 3.0, 0.0, 1.0))
+    y, x = np.mgrid[0:32, 0:32]
+    lattice = np.where(((x % 8) < 2) | ((y % 8) < 3), 1.0, 0.0)
+    noise = np.random.default_rng(77).integers(0, 256, (5, 3))
+    return [np.round(leaf * 255).astype(np.uint8), np.round(lattice * 255).astype(np.uint8), noise.astype(np.uint8)]
+
+
+# material table of the alpha scenes: (threshold, constant alpha, texture)
+ALPHA_MATERIALS = [
+    (0.5, 1.0, NO_TEXTURE),   # 0: opaque (everything that is not a card)
+    (0.5, 1.0, 0),            # 1: leaves
+    (0.5, 1.0, 1),            # 2: lattice
+    (0.33, 1.0, 0),           # 3: leaves, threshold 0.33 (float16 0.33008)
+    (0.5, 0.3, NO_TEXTURE),   # 4: constant alpha below the threshold: never visible
+    (0.4, 1.0, 2),            # 5: odd-sized noise texture
+]
+
+
+@dataclasses.dataclass
 class Scene:
     name: str
     positions: np.ndarray  # float32 [nv, 3]
     indices: np.ndarray    # uint32 [nt, 3]
     flags: np.ndarray      # uint32 [nt]
     camera: dict           # look-at camera: pos, target, up
+    alpha: AlphaMaterials | None = None
 
     @property
     def triangle_count(self) -> int:
@@ -44,17 +92,21 @@ class _Builder:
         self.pos = []
         self.ind = []
         self.flg = []
+        self.uv = []
+        self.mat = []
         self.nv = 0
 
-    def add(self, p, tri, flags=0):
+    def add(self, p, tri, flags=0, uv=None, mat=0):
         p = np.asarray(p, np.float32).reshape(-1, 3)
         tri = np.asarray(tri, np.int64).reshape(-1, 3) + self.nv
         self.pos.append(p)
         self.ind.append(tri.astype(np.uint32))
         self.flg.append(np.full(tri.shape[0], flags, np.uint32))
+        self.uv.append(np.zeros((p.shape[0], 2), np.float32) if uv is None else np.asarray(uv, np.float32).reshape(-1, 2))
+        self.mat.append(np.full(tri.shape[0], mat, np.uint32))
         self.nv += p.shape[0]
 
-    def grid(self, origin, ex, ey, nx, ny, flags=0):
+    def grid(self, origin, ex, ey, nx, ny, flags=0, uv_scale=None, uv_offset=(0.0, 0.0), mat=0):
         """Quad patch origin + s*ex + t*ey, nx*ny cells, CCW seen from ex x ey."""
         o, ex, ey = (np.asarray(v, np.float64) for v in (origin, ex, ey))
         s = np.linspace(0.0, 1.0, nx + 1)
@@ -65,7 +117,10 @@ class _Builder:
         a, b = i[:-1, :-1], i[:-1, 1:]
         c, d = i[1:, 1:], i[1:, :-1]
         tri = np.concatenate([np.stack([a, b, c], -1).reshape(-1, 3), np.stack([a, c, d], -1).reshape(-1, 3)])
-        self.add(p.reshape(-1, 3), tri, flags)
+        uv = None
+        if uv_scale is not None:
+            uv = np.stack([S * uv_scale[0] + uv_offset[0], T * uv_scale[1] + uv_offset[1]], -1).reshape(-1, 2)
+        self.add(p.reshape(-1, 3), tri, flags, uv, mat)
 
     def box(self, center, half, yaw=0.0, sub=1, flags=0):
         """Closed box with outward CCW faces, rotated by `yaw` about +y."""
@@ -129,16 +184,31 @@ class _Builder:
         keep = (tri[:, 0] != tri[:, 1]) & (tri[:, 1] != tri[:, 2])
         self.add(p, tri[keep], flags)
 
-    def build(self, name, camera):
+    def build(self, name, camera, alpha=False):
         pos = np.concatenate(self.pos).astype(np.float32)
         ind = np.concatenate(self.ind).astype(np.uint32)
         flg = np.concatenate(self.flg).astype(np.uint32)
-        return Scene(name, pos, ind, flg, camera)
+        am = None
+        if alpha:
+            m = np.array(ALPHA_MATERIALS, dtype=np.float64)
+            am = AlphaMaterials(np.concatenate(self.uv).astype(np.float32), np.concatenate(self.mat).astype(np.uint32),
+                                m[:, 0].astype(np.float32), m[:, 1].astype(np.float32),
+                                np.array([t for _, _, t in ALPHA_MATERIALS], np.uint32), alpha_textures())
+        return Scene(name, pos, ind, flg, camera, am)
 
 
-def _architecture(rng, target_tris, room=(40.0, 12.0, 40.0)):
+def _card(B, arng, x, y, z, ex, ey, nx, ny):
+    """An alpha-masked double-sided card (material, uv repeat and offset from `arng`)."""
+    mat = int(arng.choice([1, 1, 2, 3, 4, 5]))
+    rep = arng.uniform(0.5, 3.0, 2)
+    off = arng.uniform(-2.0, 2.0, 2)
+    B.grid((x, y, z), ex, ey, nx, ny, FLAG_DOUBLE_SIDED | FLAG_ALPHA_MASK, rep, off, mat)
+
+
+def _architecture(rng, target_tris, room=(40.0, 12.0, 40.0), arng=None):
     """A hall with a tessellated floor/walls, colonnades, stairs and scattered props.
-    Object counts scale so the triangle count lands near `target_tris`."""
+    Object counts scale so the triangle count lands near `target_tris`.  arng (alpha scenes):
+    the generator of the cards' materials, separate so the geometry does not change."""
     B = _Builder()
     X, Y, Z = room
     scale = max(target_tris / 600_000.0, 0.02)
@@ -188,8 +258,18 @@ def _architecture(rng, target_tris, room=(40.0, 12.0, 40.0)):
             w, hh = rng.uniform(0.3, 1.2), rng.uniform(0.3, 1.5)
             yaw = rng.uniform(0, np.pi)
             ex = (w * np.cos(yaw), 0.0, -w * np.sin(yaw))
-            B.grid((x, 0.05, z), ex, (0.0, hh, 0.0), max(1, sub_box // 2), max(1, sub_box // 2), FLAG_DOUBLE_SIDED)
+            if arng is None:
+                B.grid((x, 0.05, z), ex, (0.0, hh, 0.0), max(1, sub_box // 2), max(1, sub_box // 2), FLAG_DOUBLE_SIDED)
+            else:
+                _card(B, arng, x, 0.05, z, ex, (0.0, hh, 0.0), max(1, sub_box // 2), max(1, sub_box // 2))
         total += sum(i.shape[0] for i in B.ind[n0:])
+    if arng is not None:
+        # foliage in the view corridor: cards of several sizes, some overlapping
+        for k in range(24):
+            x, z = arng.uniform(-3.0, 3.0), arng.uniform(-Z * 0.2, Z * 0.35)
+            w, hh = arng.uniform(0.4, 2.0), arng.uniform(0.4, 2.5)
+            yaw = arng.uniform(0, np.pi)
+            _card(B, arng, x, arng.uniform(0.0, 1.5), z, (w * np.cos(yaw), 0.0, -w * np.sin(yaw)), (0.0, hh, 0.0), 2, 2)
     cam = {"pos": [0.0, 1.7, Z * 0.42], "target": [0.0, 1.2, -Z * 0.3], "up": [0.0, 1.0, 0.0]}
     return B, cam
 
@@ -197,22 +277,28 @@ def _architecture(rng, target_tris, room=(40.0, 12.0, 40.0)):
 _CONFIGS = {
     # name: (target triangles, seed)
     "arcade_tiny": (20_000, 1),
+    "foliage_small": (20_000, 5),  # alpha-masked cards (SURVEY 8(f) row 3 tests)
     "suntemple": (600_000, 2),
     "bistro_exterior": (2_800_000, 3),
     "emerald_square": (10_000_000, 4),
 }
 
 
-def make_scene(name: str = "suntemple", target_tris: int | None = None, seed: int | None = None) -> Scene:
-    """Deterministic synthetic scene.  `name` picks the BASELINE config stand-in."""
+def make_scene(name: str = "suntemple", target_tris: int | None = None, seed: int | None = None,
+               alpha: bool | None = None) -> Scene:
+    """Deterministic synthetic scene.  `name` picks the BASELINE config stand-in; alpha=True
+    makes the foliage cards alpha-masked (default: only the "foliage_*" scenes)."""
     if name not in _CONFIGS:
         raise ValueError(f"unknown scene '{name}' (known: {sorted(_CONFIGS)})")
     t, s = _CONFIGS[name]
     target_tris = t if target_tris is None else int(target_tris)
     seed = s if seed is None else int(seed)
     rng = np.random.default_rng(seed)
-    B, cam = _architecture(rng, target_tris)
+    if alpha is None:
+        alpha = name.startswith("foliage")
+    arng = np.random.default_rng(seed + 1000) if alpha else None
+    B, cam = _architecture(rng, target_tris, arng=arng)
     if name == "arcade_tiny":
         # the Arcade image tests' cube mesh (data/framework/meshes/cube.obj) as an extra prop
         B.box((0.0, 0.5, 6.0), (0.5, 0.5, 0.5))
-    return B.build(name, cam)
+    return B.build(name, cam, alpha)

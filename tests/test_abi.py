@@ -27,7 +27,7 @@ def abi():
 
 def header_functions():
     text = HEADER.read_text()
-    return sorted(set(re.findall(r"^\s*(?:rsd_status|void|uint32_t|const char\*)\s+(rsd_\w+)\s*\(", text, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:rsd_status|void|uint32_t|float|const char\*)\s+(rsd_\w+)\s*\(", text, re.M)))
 
 
 def test_header_and_binding_agree(abi):
@@ -46,7 +46,8 @@ def test_library_exports_every_header_symbol(abi):
 def test_struct_layouts_match_header(abi, tmp_path):
     structs = {"rsd_scene_desc": abi.SceneDesc, "rsd_scene_info": abi.SceneInfo, "rsd_camera": abi.Camera,
                "rsd_sd_params": abi.SDParams, "rsd_vao_data": abi.VAOData, "rsd_svao_params": abi.SVAOParams,
-               "rsd_counters": abi.Counters, "rsd_texture": abi.Texture}
+               "rsd_counters": abi.Counters, "rsd_texture": abi.Texture,
+               "rsd_alpha_texture": abi.AlphaTexture, "rsd_material": abi.Material, "rsd_alpha_desc": abi.AlphaDesc}
     src = "#include <stdio.h>\n#include \"rsd_graph.h\"\nint main(void){\n"
     for name in structs:
         src += f'printf("%zu\\n", sizeof({name}));\n'

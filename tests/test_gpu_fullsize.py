@@ -38,7 +38,7 @@ def test_fullsize_config_parity(oracle, config):
     assert (rmax != 0).sum() > 1000, "no SD rays requested: degenerate frame"
 
     # SD trace: 8-row tile rows spread through the map (every `step`-th tile row)
-    osc = oracle.Scene(scene.positions, scene.indices, scene.flags)
+    osc = oracle.Scene(scene.positions, scene.indices, scene.flags, scene.alpha)
     tiles = (r.sd_h + 7) // 8
     step = max(1, tiles // 12)
     checked = 0

@@ -37,7 +37,7 @@ def scenes(name, device, oracle):
         from rsd.frame import GpuScene
         from rsd.scenes import make_scene
         s = make_scene(name)
-        _scene_cache[name] = (s, GpuScene(device, s), oracle.Scene(s.positions, s.indices, s.flags))
+        _scene_cache[name] = (s, GpuScene(device, s), oracle.Scene(s.positions, s.indices, s.flags, s.alpha))
     return _scene_cache[name]
 
 
@@ -231,3 +231,91 @@ def test_raytraced_band_union_equals_full_frame(device, oracle):
         r.pass2_raytraced(band=(b, 3))
     g = r.numpy()
     assert np.array_equal(g["stencil"], full["stencil"]) and np.array_equal(g["ao"], full["ao"])
+
+
+# ---- alpha-masked materials ------------------------------------------
+
+@pytest.mark.parametrize("cull", [0, 1])
+def test_gbuffer_alpha_parity(device, oracle, cull):
+    """Primary visibility skips alpha-masked hits failing the alpha test at LOD 0."""
+    cfg = small_frame_config(visible=(200, 120), guard=16)
+    cfg.cull_mode = cull
+    r, osc = renderer("foliage_small", cfg, device, oracle)
+    r.gbuffer()
+    g = r.numpy()
+    cam, _, _, _ = oracle_structs(r, oracle)
+    z, n = oracle.gbuffer(osc, cam, cfg.fb_w, cfg.fb_h, cull)
+    assert bits_equal(g["depth"], z)
+    assert np.array_equal(g["normals"], n)
+    # the cards do cut holes: the opaque variant of the scene sees different depths
+    from rsd.scenes import make_scene
+    s = make_scene("foliage_small", alpha=False)
+    zo, _ = oracle.gbuffer(oracle.Scene(s.positions, s.indices, s.flags), cam, cfg.fb_w, cfg.fb_h, cull)
+    assert (zo != z).sum() > 200
+
+
+@pytest.mark.parametrize("walk", ["split", "fused", "quad"])
+@pytest.mark.parametrize("N,impl,max_count", [(4, 0, 8), (8, 3, 8), (4, 1, 8), (2, 0, 1)])
+def test_sd_trace_alpha_parity(device, oracle, walk, N, impl, max_count, monkeypatch):
+    """SD any-hit with USE_ALPHA_TEST at the ray-cone LOD, every traversal walk."""
+    monkeypatch.setenv("RSD_TRACE_WALK", walk)
+    cfg = small_frame_config(visible=(192, 112), guard=32, divisor=2, N=N, max_count=max_count, impl=impl)
+    r, osc = renderer("foliage_small", cfg, device, oracle)
+    r.gbuffer()
+    r.clear_intervals()
+    r.pass1()
+    r.sd_trace()
+    g = r.numpy()
+    cam, vao, sdp, svp = oracle_structs(r, oracle)
+    assert sdp.alpha_test == 1
+    sd, stats = oracle.sd_trace(osc, cam, sdp, g["depth"], g["ray_min"], g["ray_max"], r.sd_w, r.sd_h)
+    assert stats[0] > 0
+    assert bits_equal(g["sd"], sd)
+    # AlphaTest off: the cards are opaque to the SD rays
+    sdp.alpha_test = 0
+    sd0, _ = oracle.sd_trace(osc, cam, sdp, g["depth"], g["ray_min"], g["ray_max"], r.sd_w, r.sd_h)
+    r.sdp.alpha_test = 0
+    r.sd_trace()
+    g0 = r.numpy()
+    assert bits_equal(g0["sd"], sd0)
+    assert not bits_equal(sd0, sd)
+
+
+@pytest.mark.parametrize("alpha_test", [1, 0])
+def test_raytraced_svao_alpha_parity(device, oracle, alpha_test):
+    from rsd import abi
+    cfg = small_frame_config(visible=(160, 96), guard=16, divisor=1)
+    cfg.secondary = abi.DEPTH_RAYTRACED
+    cfg.alpha_test = bool(alpha_test)
+    r, osc = renderer("foliage_small", cfg, device, oracle)
+    r.gbuffer()
+    r.frame()
+    g = r.numpy()
+    cam, vao, sdp, svp = oracle_structs(r, oracle)
+    z, n = oracle.gbuffer(osc, cam, cfg.fb_w, cfg.fb_h, cfg.cull_mode)
+    assert bits_equal(g["depth"], z)
+    ao1, st, _, _ = oracle.svao_pass1(cam, vao, svp, z, n, r.sd_w, r.sd_h)
+    assert np.array_equal(g["stencil"], st)
+    ao = oracle.svao_pass2_raytraced(osc, cam, vao, svp, z, n, st, ao1, cull=cfg.cull_mode,
+                                     ray_pipeline=int(cfg.ray_pipeline), alpha_test=alpha_test)
+    assert np.array_equal(g["ao"], ao)
+
+
+def test_full_frame_alpha_parity(device, oracle):
+    cfg = small_frame_config(visible=(256, 144), guard=32, divisor=4, N=4)
+    r, osc = renderer("foliage_small", cfg, device, oracle)
+    r.gbuffer()
+    r.frame()
+    g = r.numpy()
+    cam, vao, sdp, svp = oracle_structs(r, oracle)
+    o = oracle_frame(oracle, osc, cam, vao, sdp, svp, cfg.fb_w, cfg.fb_h, r.sd_w, r.sd_h)
+    assert bits_equal(g["depth"], o["depth"])
+    assert bits_equal(g["sd"], o["sd"])
+    gv = slice(cfg.guard_band, cfg.fb_h - cfg.guard_band), slice(cfg.guard_band, cfg.fb_w - cfg.guard_band)
+    assert np.array_equal(g["ao"][gv], o["ao"][gv])
+
+
+def test_ray_cone_spread_matches_oracle(oracle):
+    from rsd import abi
+    for f, h in [(21.0, 270), (21.0, 1080), (35.0, 512), (10.0, 77)]:
+        assert abi.lib().rsd_ray_cone_spread(f, h) == oracle.ray_cone_spread(f, h)
