@@ -319,3 +319,30 @@ def test_ray_cone_spread_matches_oracle(oracle):
     from rsd import abi
     for f, h in [(21.0, 270), (21.0, 1080), (35.0, 512), (10.0, 77)]:
         assert abi.lib().rsd_ray_cone_spread(f, h) == oracle.ray_cone_spread(f, h)
+
+
+def test_obj_ingest_frame_parity(device, oracle, tmp_path):
+    """An OBJ scene with an alpha-textured (map_d) double-sided card, loaded by rsd.ingest and
+    uploaded with rsd_scene_upload_alpha: G-buffer and SD map bit-exact vs the oracle."""
+    from test_ingest import _foliage_obj
+    from rsd.frame import GpuScene, Renderer
+    from rsd.ingest import load_obj
+    _foliage_obj(tmp_path)
+    B = load_obj(tmp_path / "scene.obj", double_sided={"leaf"})
+    B.set_camera((0.5, 0.3, 9.0), (0, 0, 0))
+    s = B.build("obj_foliage")
+    cfg = small_frame_config(visible=(160, 96), guard=16, divisor=1, N=4)
+    cfg.ray_interval = False
+    cfg.sd_guard_px = 0
+    gs = GpuScene(device, s)
+    r = Renderer(s, cfg, dev=device, gpu_scene=gs)
+    r.gbuffer()
+    r.sd_trace()
+    g = r.numpy()
+    osc = oracle.Scene(s.positions, s.indices, s.flags, s.alpha)
+    cam, vao, sdp, svp = oracle_structs(r, oracle)
+    z, n = oracle.gbuffer(osc, cam, cfg.fb_w, cfg.fb_h, cfg.cull_mode)
+    assert bits_equal(g["depth"], z) and np.array_equal(g["normals"], n)
+    sd, _ = oracle.sd_trace(osc, cam, sdp, z, None, None, r.sd_w, r.sd_h)
+    assert bits_equal(g["sd"], sd)
+    gs.release()
