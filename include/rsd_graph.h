@@ -71,6 +71,25 @@ rsd_status rsd_graph_pass_times(rsd_graph* g, float* ms, uint32_t cap, uint32_t*
 rsd_status rsd_graph_get_dict_int(const rsd_graph* g, const char* key, int64_t* out);
 rsd_status rsd_graph_pass_count(const rsd_graph* g, uint32_t* passes, uint32_t* edges);
 
+/* --- image passes after SVAO in the graph scripts ------------------ */
+/* CrossBilateralBlur (CrossBilateralBlur.ps.slang:1-88, CrossBilateralBlur.cpp:113-149):
+ * R8Unorm AO -> x blur into d_pingpong -> y blur into d_dst, KERNEL_RADIUS 1..20 (default 4),
+ * betterSlope (default 1); writes only inside the guard band (scissor). */
+rsd_status rsd_cross_bilateral_blur(const uint8_t* d_src, const float* d_linear_z, uint32_t z_w, uint32_t z_h,
+                                    uint8_t* d_pingpong, uint8_t* d_dst, uint32_t width, uint32_t height,
+                                    uint32_t guard_band, uint32_t kernel_radius, uint32_t better_slope,
+                                    rsd_stream stream);
+/* ImageEquation (ImageEquation.cpp:134-160, ImageEquation.ps.slang): `formula` is the HLSL
+ * expression of `float4 result = (FORMULA)` over I0..I3[xy].  Compile on the host (syntax
+ * errors -> RSD_ERR_INVALID_ARG, message in rsd_last_error), run on a stream: inputs[4]
+ * (ptr NULL = unbound), output RGBA32F / RG32F / R32F / R8Unorm. */
+typedef struct rsd_image_program rsd_image_program;
+rsd_status rsd_image_equation_compile(const char* formula, rsd_image_program** out);
+rsd_status rsd_image_equation_info(const rsd_image_program* prog, uint32_t* instructions, uint32_t* texture_mask);
+rsd_status rsd_image_equation_run(const rsd_image_program* prog, const rsd_texture* inputs, const rsd_texture* out,
+                                  rsd_stream stream);
+void rsd_image_equation_release(rsd_image_program* prog);
+
 /* plugin registry */
 rsd_status rsd_plugin_set_dir(const char* dir);
 /* registered pass types, '\n'-separated */

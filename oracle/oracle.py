@@ -88,6 +88,7 @@ def lib():
         L.ocpu_alpha_value.argtypes = [vp, u32, f32, f32, i32, f32, vp, f32]
         L.ocpu_alpha_threshold.restype = f32
         L.ocpu_alpha_threshold.argtypes = [vp, u32]
+        L.ocpu_cross_bilateral_blur.argtypes = [vp, vp, u32, u32, vp, vp, u32, u32, u32, u32, u32]
         L.ocpu_ray_cone_spread.restype = f32
         L.ocpu_ray_cone_spread.argtypes = [f32, u32]
         L.ocpu_hash.restype = f32
@@ -328,3 +329,16 @@ def svao_pass2_into(cam, vao, p, depth, normals, stencil, sd, ao, band=(0, 1), t
     sdH, sdW = sd.shape[1], sd.shape[2]
     lib().ocpu_svao_pass2_band(C.byref(cam), C.byref(vao), C.byref(p), _p(depth), _p(normals), W, H, _p(stencil),
                                _p(sd), sdW, sdH, _p(ao), band[0], band[1], _threads(threads))
+
+
+def cross_bilateral_blur(src, linear_z, guard, radius=4, better_slope=True, dst=None):
+    """CrossBilateralBlur of an R8Unorm image; pixels outside the guard band keep `dst`'s
+    values (zeros by default), as the scissored pass leaves them."""
+    src = np.ascontiguousarray(src, np.uint8)
+    z = np.ascontiguousarray(linear_z, np.float32)
+    H, W = src.shape
+    out = np.zeros_like(src) if dst is None else np.array(dst, np.uint8, copy=True)
+    pp = np.zeros_like(src)
+    lib().ocpu_cross_bilateral_blur(_p(src), _p(z), z.shape[1], z.shape[0], _p(pp), _p(out), W, H, guard, radius,
+                                    int(better_slope))
+    return out, pp

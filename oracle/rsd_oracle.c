@@ -1562,3 +1562,60 @@ void ocpu_svao_pass2_rt_band(const oscene* sc, const ocam* cam, const ovao* d, c
     o_run_rows(o_pass2_rt_rows, jobs, sizeof(ort_job), g, yEnd, nthreads, o_rt_setrows);
     free(jobs);
 }
+
+/* ------------------------------------------------------------------ CrossBilateralBlur
+ * CrossBilateralBlur.ps.slang:1-88 / CrossBilateralBlur.cpp:113-149: x pass into the
+ * ping-pong image, y pass into dst, point sampling (clamp) at texC + d * dir / size clamped
+ * to the guard band's uv bounds (GuardBand.cpp:62-63), writes inside the scissor only. */
+static int o_point(float uv, int n)
+{
+    int t = (int)floorf(uv * (float)n);
+    return t < 0 ? 0 : (t > n - 1 ? n - 1 : t);
+}
+
+static void o_blur_pass(const uint8_t* src, const float* z, int zW, int zH, uint8_t* dst, int W, int H, int g,
+                        int R, int better, float dirX, float dirY)
+{
+    const float uvMinX = ((float)g + 0.5f) / (float)W, uvMinY = ((float)g + 0.5f) / (float)H;
+    const float uvMaxX = ((float)W - ((float)g + 0.5f)) / (float)W;
+    const float uvMaxY = ((float)H - ((float)g + 0.5f)) / (float)H;
+    const float sigma = ((float)R + 1.0f) * 0.5f;
+    const float falloff = 1.0f / (2.0f * sigma * sigma);
+    float zc[41], ac[41];
+    for (int y = g; y < H - g; ++y)
+        for (int x = g; x < W - g; ++x) {
+            const float tx = ((float)x + 0.5f) / (float)W, ty = ((float)y + 0.5f) / (float)H;
+            const float ux = (1.0f / (float)W) * dirX, uy = (1.0f / (float)H) * dirY;
+            for (int d = -R; d <= R; ++d) {
+                float u = o_min(o_max(tx + (float)d * ux, uvMinX), uvMaxX);
+                float v = o_min(o_max(ty + (float)d * uy, uvMinY), uvMaxY);
+                zc[R + d] = z[(size_t)o_point(v, zH) * zW + o_point(u, zW)];
+                ac[R + d] = o_unorm8_to_float(src[(size_t)o_point(v, H) * W + o_point(u, W)]);
+            }
+            float ao = ac[R], ws = 1.0f;
+            float left = zc[R] - zc[R - 1], right = zc[R + 1] - zc[R];
+            float minSlope = fabsf(left) < fabsf(right) ? left : right;
+            for (int side = 0; side < 2; ++side) { /* BlurDirection(+1, minSlope), (-1, -minSlope) */
+                int sgn = side ? -1 : 1;
+                float slope = side ? -minSlope : minSlope;
+                for (int d = 1; d <= R; ++d) {
+                    float a = ac[R + sgn * d], sz = zc[R + sgn * d];
+                    if (d == 1 && !better) slope = sz - zc[R];
+                    sz -= slope * (float)d; /* AddSample */
+                    float dz = fabsf(sz - zc[R]) * 16.0f;
+                    dz = dz * 12.0f / zc[R];
+                    float w = (float)exp2((double)(-(float)(d * d) * falloff - dz * dz));
+                    ao += w * a;
+                    ws += w;
+                }
+            }
+            dst[(size_t)y * W + x] = o_unorm8(ao / ws);
+        }
+}
+
+void ocpu_cross_bilateral_blur(const uint8_t* src, const float* z, uint32_t zW, uint32_t zH, uint8_t* pingpong,
+                               uint8_t* dst, uint32_t W, uint32_t H, uint32_t g, uint32_t R, uint32_t better)
+{
+    o_blur_pass(src, z, (int)zW, (int)zH, pingpong, (int)W, (int)H, (int)g, (int)R, (int)better, 1.0f, 0.0f);
+    o_blur_pass(pingpong, z, (int)zW, (int)zH, dst, (int)W, (int)H, (int)g, (int)R, (int)better, 0.0f, 1.0f);
+}

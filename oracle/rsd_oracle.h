@@ -176,6 +176,11 @@ void ocpu_svao_pass2_rt_band(const oscene* sc, const ocam* cam, const ovao* d, c
                              const uint8_t* stencil, uint8_t* ao, uint32_t cull, uint32_t ray_pipeline,
                              uint32_t alpha_test, uint32_t band_index, uint32_t band_count, int nthreads);
 
+/* CrossBilateralBlur (x then y through pingpong; dst written inside the guard band only) */
+void ocpu_cross_bilateral_blur(const uint8_t* src, const float* z, uint32_t zW, uint32_t zH, uint8_t* pingpong,
+                               uint8_t* dst, uint32_t W, uint32_t H, uint32_t guard, uint32_t radius,
+                               uint32_t better_slope);
+
 #ifdef __cplusplus
 }
 #endif

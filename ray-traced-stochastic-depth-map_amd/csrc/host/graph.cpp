@@ -348,6 +348,28 @@ void RenderGraph::compile(Context& ctx, uint32_t width, uint32_t height, bool al
         auto [p, f] = splitName(o);
         stubOut(p, f, Format::Unknown);
     }
+    // outputs shaped like one of the pass's inputs (Switch.cpp:95-108), in topological order
+    for (auto& p : order_) {
+        for (auto& [key, f] : outs) {
+            if (f.formatFrom.empty() || splitName(key).first != p) continue;
+            for (auto& e : edges_) {
+                if (e.dstPass != p || e.dstField != f.formatFrom || !need.count(e.srcPass)) continue;
+                auto src = outs.find(e.srcPass + "." + e.srcField);
+                if (src == outs.end()) continue;
+                f.format = src->second.format;
+                f.width = src->second.width;
+                f.height = src->second.height;
+                f.layers = src->second.layers;
+            }
+            auto ext = inputs_.find(p + "." + f.formatFrom);
+            if (ext != inputs_.end() && ext->second) {
+                f.format = ext->second->format;
+                f.width = ext->second->width;
+                f.height = ext->second->height;
+                f.layers = ext->second->layers;
+            }
+        }
+    }
     for (auto& [key, f] : outs) {
         Texture t;
         t.width = f.width ? f.width : width_;

@@ -72,6 +72,7 @@ struct Field {
     Format format = Format::Unknown;  // Unknown: take it from the connected producer
     uint32_t width = 0, height = 0;  // 0: the graph's default dims
     uint32_t layers = 1;
+    std::string formatFrom;  // output: copy format and size from this input's producer (Switch)
 };
 
 struct Reflection {

@@ -9,13 +9,19 @@
 //   SVAO                  SVAO.cpp                   rsd_svao_* + a nested "Stochastic Depth"
 //                                                    graph holding StochasticDepthMapRT
 //
-// Every other pass type of the reference scripts (ToneMapper, TAA, CrossBilateralBlur, ...)
+//   CrossBilateralBlur    CrossBilateralBlur.cpp     rsd_cross_bilateral_blur
+//   ImageEquation         ImageEquation.cpp          rsd_image_equation_compile / _run
+//   Switch                Switch.cpp                 copy of the selected input
+//   TemporalAO            TemporalAO.cpp             enabled = False: copy (enabled: unsupported)
+//
+// Every other pass type of the reference scripts (ToneMapper, TAA, ForwardLighting, ...)
 // is outside the hot path; it resolves to a stub that declares whatever fields
 // the script connects and does no work, so the scripts build and run unchanged.
 #include <cmath>
 #include <cstdio>
 
 #include "graph.h"
+#include "../../../include/rsd_graph.h"
 
 namespace rsd::host {
 namespace {
@@ -386,6 +392,170 @@ private:
     std::unique_ptr<RenderGraph> sdGraph_;
 };
 
+// ------------------------------------------------------------------------------ CrossBilateralBlur
+// CrossBilateralBlur.cpp:56-149 + CrossBilateralBlur.h:56-66 defaults (enabled, KERNEL_RADIUS 4,
+// 1 repetition, betterSlope).  The reference takes no properties (UI only); librsd accepts
+// the UI values as optional properties.
+class CrossBilateralBlurPass : public RenderPass {
+public:
+    explicit CrossBilateralBlurPass(const Properties& p) {
+        props_ = p;
+        enabled_ = p.getBool("enabled", true);
+        radius_ = (uint32_t)p.getInt("kernelRadius", 4);
+        repetitions_ = (uint32_t)p.getInt("repetitions", 1);
+        betterSlope_ = p.getBool("betterSlope", true);
+        if (radius_ < 1 || radius_ > 20) throw std::runtime_error("CrossBilateralBlur: kernelRadius must be 1..20");
+    }
+    ~CrossBilateralBlurPass() override { (void)hipFree(pingpong_); }
+    Reflection reflect(const CompileData&) override {
+        Reflection r;
+        r.addInput("color", "color image to be blurred").format = Format::R8Unorm;
+        r.addInput("linear depth", "linear depth").format = Format::R32Float;
+        r.addOutput("colorOut", "blurred color").format = Format::R8Unorm;
+        return r;
+    }
+    void compile(Context&, const CompileData& cd) override {
+        (void)hipFree(pingpong_);
+        pingpong_ = nullptr;
+        if (hipMalloc(&pingpong_, (size_t)cd.defaultWidth * cd.defaultHeight) != hipSuccess)
+            throw std::runtime_error("CrossBilateralBlur: ping-pong allocation failed");
+    }
+    void execute(Context& ctx, const RenderData& rd) override {
+        Texture* in = rd["color"];
+        Texture* z = rd["linear depth"];
+        Texture* out = rd["colorOut"];
+        if (in->format != Format::R8Unorm || in->width != out->width || in->height != out->height)
+            throw Unsupported("CrossBilateralBlur: the color input must be R8Unorm at the output size");
+        if (!enabled_) {  // :120-124 blit
+            if (hipMemcpyAsync(out->ptr, in->ptr, out->bytes(), hipMemcpyDeviceToDevice, ctx.stream) != hipSuccess)
+                throw std::runtime_error("CrossBilateralBlur: copy failed");
+            return;
+        }
+        if (z->format != Format::R32Float) throw Unsupported("CrossBilateralBlur: linear depth must be R32Float");
+        auto& dict = rd.getDictionary();
+        auto it = dict.find("guardBand");
+        const int64_t g = it != dict.end() && std::holds_alternative<int64_t>(it->second)
+                              ? std::get<int64_t>(it->second) : 0;
+        for (uint32_t k = 0; k < repetitions_; ++k)  // :136-148: every repetition blurs the input again
+            check(rsd_cross_bilateral_blur((const uint8_t*)in->ptr, (const float*)z->ptr, z->width, z->height,
+                                           (uint8_t*)pingpong_, (uint8_t*)out->ptr, out->width, out->height,
+                                           (uint32_t)g, radius_, betterSlope_ ? 1u : 0u, ctx.stream),
+                  "CrossBilateralBlur");
+    }
+
+private:
+    bool enabled_, betterSlope_;
+    uint32_t radius_, repetitions_;
+    void* pingpong_ = nullptr;
+};
+
+// ------------------------------------------------------------------------------ ImageEquation
+// ImageEquation.cpp:43-160: `formula` (default "I0[xy]"), `format` (default RGBA32Float).  An
+// invalid formula leaves the pass invalid (execute does nothing), as in the reference.
+class ImageEquationPass : public RenderPass {
+public:
+    explicit ImageEquationPass(const Properties& p) {
+        props_ = p;
+        formula_ = p.getString("formula", "I0[xy]");
+        const std::string f = p.getString("format", "RGBA32Float");
+        if (f == "RGBA32Float") fmt_ = Format::RGBA32Float;
+        else if (f == "RG32Float") fmt_ = Format::RG32Float;
+        else if (f == "R32Float") fmt_ = Format::R32Float;
+        else if (f == "R8Unorm") fmt_ = Format::R8Unorm;
+        else throw Unsupported("ImageEquation: format '" + f + "' (librsd: RGBA32Float, RG32Float, R32Float, R8Unorm)");
+        if (rsd_image_equation_compile(formula_.c_str(), &prog_) != RSD_OK) {
+            std::fprintf(stderr, "[rsd] ImageEquation: %s\n", rsd_last_error());  // :138-150 logWarning
+            prog_ = nullptr;
+        }
+    }
+    ~ImageEquationPass() override { rsd_image_equation_release(prog_); }
+    Reflection reflect(const CompileData&) override {
+        Reflection r;
+        for (const char* n : {"I0", "I1", "I2", "I3"}) r.addInput(n, "input image").optional = true;
+        r.addOutput("out", "output image").format = fmt_;
+        return r;
+    }
+    void execute(Context& ctx, const RenderData& rd) override {
+        if (!prog_) return;
+        rsd_texture in[4] = {};
+        const char* names[4] = {"I0", "I1", "I2", "I3"};
+        for (int k = 0; k < 4; ++k)
+            if (Texture* t = rd[names[k]]) in[k] = rsd_texture{t->ptr, t->width, t->height, t->layers,
+                                                                (uint32_t)t->format, (uint64_t)t->bytes()};
+        Texture* o = rd["out"];
+        rsd_texture out{o->ptr, o->width, o->height, o->layers, (uint32_t)o->format, (uint64_t)o->bytes()};
+        check(rsd_image_equation_run(prog_, in, &out, ctx.stream), "ImageEquation");
+    }
+
+private:
+    std::string formula_;
+    Format fmt_;
+    rsd_image_program* prog_ = nullptr;
+};
+
+// ------------------------------------------------------------------------------ Switch
+// Switch.cpp:41-150: inputs i0..i<count-1> (optional), `selected`, output shaped like the
+// selected input, blit per execute.
+class SwitchPass : public RenderPass {
+public:
+    explicit SwitchPass(const Properties& p) {
+        props_ = p;
+        count_ = (int)p.getInt("count", 2);
+        selected_ = (int)p.getInt("selected", 0);
+        if (count_ < 1 || count_ > 16) throw std::runtime_error("Switch: count must be 1..16");
+    }
+    Reflection reflect(const CompileData&) override {
+        Reflection r;
+        for (int k = 0; k < count_; ++k) r.addInput("i" + std::to_string(k), "input").optional = true;
+        r.addOutput("out", "selected output").formatFrom = "i" + std::to_string(selected_);
+        return r;
+    }
+    void execute(Context& ctx, const RenderData& rd) override {
+        Texture* in = rd["i" + std::to_string(selected_)];
+        if (!in) return;  // :141
+        Texture* out = rd["out"];
+        if (in->bytes() != out->bytes()) throw std::runtime_error("Switch: input and output shapes differ");
+        if (hipMemcpyAsync(out->ptr, in->ptr, out->bytes(), hipMemcpyDeviceToDevice, ctx.stream) != hipSuccess)
+            throw std::runtime_error("Switch: copy failed");
+    }
+
+private:
+    int count_, selected_;
+};
+
+// ------------------------------------------------------------------------------ TemporalAO
+// TemporalAO.cpp:100-170: disabled -> blit aoIn to aoOut (what scripts/SVAO.py configures);
+// the enabled path (motion-vector reprojection with a history buffer) is not implemented.
+class TemporalAOPass : public RenderPass {
+public:
+    explicit TemporalAOPass(const Properties& p) {
+        props_ = p;
+        enabled_ = p.getBool("enabled", true);
+        if (enabled_)
+            throw Unsupported("TemporalAO: enabled = True (temporal reprojection) is outside librsd's scope");
+    }
+    Reflection reflect(const CompileData&) override {
+        Reflection r;
+        r.addInput("aoIn", "AO").format = Format::R8Unorm;
+        r.addInput("linearZ", "linear depth").optional = true;
+        r.addInput("mvec", "motion vectors").optional = true;
+        r.addInput("stableMask", "stable mask").optional = true;
+        r.addOutput("aoOut", "AO").format = Format::R8Unorm;
+        return r;
+    }
+    void execute(Context& ctx, const RenderData& rd) override {
+        Texture* in = rd["aoIn"];
+        Texture* out = rd["aoOut"];
+        if (in->format != Format::R8Unorm || in->bytes() != out->bytes())
+            throw std::runtime_error("TemporalAO: aoIn must be R8Unorm at the output size");
+        if (hipMemcpyAsync(out->ptr, in->ptr, out->bytes(), hipMemcpyDeviceToDevice, ctx.stream) != hipSuccess)
+            throw std::runtime_error("TemporalAO: copy failed");
+    }
+
+private:
+    bool enabled_;
+};
+
 template <class T>
 PluginRegistry::Factory factory() {
     return [](const Properties& p) { return std::unique_ptr<RenderPass>(new T(p)); };
@@ -401,6 +571,10 @@ void registerBuiltinPasses(PluginRegistry& r) {
     r.registerClass("CompressNormals", "view-space 2x8 octahedral normals", factory<CompressNormalsPass>());
     r.registerClass("StochasticDepthMapRT", "ray-traced stochastic depth map", factory<StochasticDepthMapRTPass>());
     r.registerClass("SVAO", "stochastic-depth volumetric ambient occlusion", factory<SVAOPass>());
+    r.registerClass("CrossBilateralBlur", "depth-aware cross bilateral blur", factory<CrossBilateralBlurPass>());
+    r.registerClass("ImageEquation", "per-pixel formula over up to 4 images", factory<ImageEquationPass>());
+    r.registerClass("Switch", "forwards the selected input", factory<SwitchPass>());
+    r.registerClass("TemporalAO", "temporal AO accumulation (disabled: pass-through)", factory<TemporalAOPass>());
 }
 
 }  // namespace rsd::host

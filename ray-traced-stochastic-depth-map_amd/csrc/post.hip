@@ -1,0 +1,330 @@
+// post.hip -- the image passes after SVAO in the reference's graph scripts:
+// CrossBilateralBlur and ImageEquation.  Both are HBM-bound streaming kernels over the
+// frame; one lane per pixel, 64 x 4 workgroups so every wave reads whole cache lines.
+//
+// CrossBilateralBlur (RenderPasses/CrossBilateralBlur/CrossBilateralBlur.ps.slang:1-88,
+// CrossBilateralBlur.cpp:113-149): separable depth-aware blur, x then y through a ping-pong
+// R8Unorm image, KERNEL_RADIUS taps each side with the HBAO+ weights
+//   w(d) = exp2(-d^2 falloff - dz^2),  dz = 12 * 16 |z_d - d * slope - z_0| / z_0,
+// point sampling at texC + d * dir / size clamped to the guard band's [uvMin, uvMax]
+// (GuardBand.cpp:62-63), writes limited to the guard-band scissor (GuardBand.h:4-15).
+// Numerics: rsd_device.h contract; exp2 evaluated in double and rounded once.
+//
+// ImageEquation (ImageEquation.ps.slang:8-13): the formula program of csrc/image_eq.h run
+// per pixel; I<k>[xy] reads Texture2D<float4> semantics (missing channels 0, alpha 1;
+// unbound or out of range: 0).
+#include <cmath>
+
+#include "../../include/rsd_graph.h"
+#include "image_eq.h"
+#include "rsd_device.h"
+#include "rsd_internal.h"
+
+struct rsd_image_program;
+
+namespace rsd {
+const IeProgram& image_program(const rsd_image_program* p);
+
+namespace {
+
+constexpr int kPostW = 64, kPostH = 4;
+
+// ---------------------------------------------------------------------- CrossBilateralBlur
+struct BlurArgs {
+    const uint8_t* src;
+    const float* z;
+    uint8_t* dst;
+    int W, H, g;
+    float dirX, dirY;
+    float uvMinX, uvMinY, uvMaxX, uvMaxY;
+    int zW, zH;
+    uint32_t betterSlope;
+};
+
+__device__ __forceinline__ int point_texel(float uv, int n) {
+    int t = (int)floorf(uv * (float)n);
+    return t < 0 ? 0 : (t > n - 1 ? n - 1 : t);
+}
+
+template <int R>
+__global__ void __launch_bounds__(kPostW * kPostH) blur_kernel(BlurArgs a) {
+    const int x = a.g + (int)(blockIdx.x * kPostW + threadIdx.x);
+    const int y = a.g + (int)(blockIdx.y * kPostH + threadIdx.y);
+    if (x >= a.W - a.g || y >= a.H - a.g) return;  // guard-band scissor
+    const float tcx = ((float)x + 0.5f) / (float)a.W, tcy = ((float)y + 0.5f) / (float)a.H;
+    const float dux = (1.0f / (float)a.W) * a.dirX, duy = (1.0f / (float)a.H) * a.dirY;
+    float dc[2 * R + 1], ac[2 * R + 1];
+#pragma unroll
+    for (int d = -R; d <= R; ++d) {
+        const float u = fminf(fmaxf(tcx + (float)d * dux, a.uvMinX), a.uvMaxX);
+        const float v = fminf(fmaxf(tcy + (float)d * duy, a.uvMinY), a.uvMaxY);
+        dc[R + d] = a.z[(size_t)point_texel(v, a.zH) * a.zW + point_texel(u, a.zW)];
+        ac[R + d] = unorm8_to_float(a.src[(size_t)point_texel(v, a.H) * a.W + point_texel(u, a.W)]);
+    }
+    const float sigma = ((float)R + 1.0f) * 0.5f;
+    const float falloff = 1.0f / (2.0f * sigma * sigma);
+    float ao = ac[R], wsum = 1.0f;
+    const float sl = dc[R] - dc[R - 1], sr = dc[R + 1] - dc[R];
+    const float minSlope = fabsf(sl) < fabsf(sr) ? sl : sr;
+#pragma unroll
+    for (int side = 0; side < 2; ++side) {
+        const int sign = side == 0 ? 1 : -1;
+        float slope = side == 0 ? minSlope : -minSlope;
+#pragma unroll
+        for (int d = 1; d <= R; ++d) {
+            const float sAo = ac[R + sign * d];
+            float sZ = dc[R + sign * d];
+            if (d == 1 && !a.betterSlope) slope = sZ - dc[R];
+            sZ -= slope * (float)d;
+            float dz = fabsf(sZ - dc[R]) * 16.0f;
+            dz = dz * 12.0f / dc[R];
+            const float w = (float)exp2((double)(-(float)(d * d) * falloff - dz * dz));
+            ao += w * sAo;
+            wsum += w;
+        }
+    }
+    a.dst[(size_t)y * a.W + x] = unorm8(ao / wsum);
+}
+
+template <int R>
+hipError_t launch_blur(const BlurArgs& a, hipStream_t s) {
+    const dim3 grid((a.W - 2 * a.g + kPostW - 1) / kPostW, (a.H - 2 * a.g + kPostH - 1) / kPostH);
+    hipLaunchKernelGGL(blur_kernel<R>, grid, dim3(kPostW, kPostH), 0, s, a);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------- ImageEquation
+struct TexDesc {
+    const void* ptr;
+    int w, h;
+    uint32_t fmt;
+};
+struct EqArgs {
+    IeProgram prog;
+    TexDesc in[4];
+    void* out;
+    int W, H;
+    uint32_t outFmt;
+};
+
+__device__ __forceinline__ float4 load_texel(const TexDesc& t, int x, int y) {
+    if (!t.ptr || x >= t.w || y >= t.h) return make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    const size_t o = (size_t)y * t.w + x;
+    switch (t.fmt) {
+        case RSD_FMT_R32F: return make_float4(static_cast<const float*>(t.ptr)[o], 0.0f, 0.0f, 1.0f);
+        case RSD_FMT_RG32F: {
+            const float2 v = static_cast<const float2*>(t.ptr)[o];
+            return make_float4(v.x, v.y, 0.0f, 1.0f);
+        }
+        case RSD_FMT_RGBA32F: return static_cast<const float4*>(t.ptr)[o];
+        case RSD_FMT_R8UNORM: return make_float4(unorm8_to_float(static_cast<const uint8_t*>(t.ptr)[o]), 0.0f, 0.0f, 1.0f);
+        case RSD_FMT_R8U: return make_float4((float)static_cast<const uint8_t*>(t.ptr)[o], 0.0f, 0.0f, 1.0f);
+        case RSD_FMT_R16U: return make_float4((float)static_cast<const uint16_t*>(t.ptr)[o], 0.0f, 0.0f, 1.0f);
+        case RSD_FMT_R32U: return make_float4((float)static_cast<const uint32_t*>(t.ptr)[o], 0.0f, 0.0f, 1.0f);
+        default: return make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    }
+}
+
+__device__ __forceinline__ float lane(float4 v, int i) { return i == 0 ? v.x : i == 1 ? v.y : i == 2 ? v.z : v.w; }
+__device__ __forceinline__ float dbl1(int f, float x) {
+    const double d = (double)x;
+    switch (f) {
+        case F1_EXP2: return (float)exp2(d);
+        case F1_LOG2: return (float)log2(d);
+        case F1_EXP: return (float)exp(d);
+        case F1_LOG: return (float)log(d);
+        case F1_SIN: return (float)sin(d);
+        case F1_COS: return (float)cos(d);
+        default: return (float)(1.0 / sqrt(d));  // F1_RSQRT
+    }
+}
+__device__ __forceinline__ float f1(int f, float x) {
+    switch (f) {
+        case F1_ABS: return fabsf(x);
+        case F1_SAT: return saturate(x);
+        case F1_SQRT: return sqrtf(x);
+        case F1_FLOOR: return floorf(x);
+        case F1_CEIL: return ceilf(x);
+        case F1_FRAC: return x - floorf(x);
+        case F1_SIGN: return x > 0.0f ? 1.0f : (x < 0.0f ? -1.0f : 0.0f);
+        default: return dbl1(f, x);
+    }
+}
+__device__ __forceinline__ float f2(int f, float a, float b) {
+    switch (f) {
+        case F2_MIN: return fminf(a, b);
+        case F2_MAX: return fmaxf(a, b);
+        case F2_POW: return acc_pow(a, b);
+        default: return b >= a ? 1.0f : 0.0f;  // F2_STEP: step(y, x) = x >= y
+    }
+}
+#define RSD_MAP4(e) make_float4(e(x), e(y), e(z), e(w))
+
+__global__ void __launch_bounds__(kPostW * kPostH) image_equation_kernel(EqArgs a) {
+    const int x = (int)(blockIdx.x * kPostW + threadIdx.x), y = (int)(blockIdx.y * kPostH + threadIdx.y);
+    if (x >= a.W || y >= a.H) return;
+    float4 st[kIeMaxStack];
+    int sp = 0;
+    for (int pc = 0; pc < a.prog.n; ++pc) {
+        const IeInstr in = a.prog.code[pc];
+        switch (in.op) {
+            case IE_TEX: st[sp++] = load_texel(a.in[in.a], x, y); break;
+            case IE_CONST: st[sp++] = make_float4(in.k, in.k, in.k, in.k); break;
+            case IE_SWZ: {
+                const float4 v = st[sp - 1];
+                st[sp - 1] = make_float4(lane(v, in.a & 3), lane(v, (in.a >> 2) & 3), lane(v, (in.a >> 4) & 3),
+                                         lane(v, (in.a >> 6) & 3));
+                break;
+            }
+            case IE_NEG: {
+                const float4 v = st[sp - 1];
+                st[sp - 1] = make_float4(-v.x, -v.y, -v.z, -v.w);
+                break;
+            }
+            case IE_ADD: case IE_SUB: case IE_MUL: case IE_DIV: {
+                const float4 p = st[sp - 2], q = st[sp - 1];
+                --sp;
+                float4 r;
+                if (in.op == IE_ADD) r = make_float4(p.x + q.x, p.y + q.y, p.z + q.z, p.w + q.w);
+                else if (in.op == IE_SUB) r = make_float4(p.x - q.x, p.y - q.y, p.z - q.z, p.w - q.w);
+                else if (in.op == IE_MUL) r = make_float4(p.x * q.x, p.y * q.y, p.z * q.z, p.w * q.w);
+                else r = make_float4(p.x / q.x, p.y / q.y, p.z / q.z, p.w / q.w);
+                st[sp - 1] = r;
+                break;
+            }
+            case IE_F1: {
+                const float4 v = st[sp - 1];
+                st[sp - 1] = make_float4(f1(in.a, v.x), f1(in.a, v.y), f1(in.a, v.z), f1(in.a, v.w));
+                break;
+            }
+            case IE_F2: {
+                const float4 p = st[sp - 2], q = st[sp - 1];
+                --sp;
+                st[sp - 1] = make_float4(f2(in.a, p.x, q.x), f2(in.a, p.y, q.y), f2(in.a, p.z, q.z), f2(in.a, p.w, q.w));
+                break;
+            }
+            case IE_F3: {
+                const float4 p = st[sp - 3], q = st[sp - 2], t = st[sp - 1];
+                sp -= 2;
+                float4 r;
+                if (in.a == F3_LERP)  // x + s (y - x)
+                    r = make_float4(p.x + t.x * (q.x - p.x), p.y + t.y * (q.y - p.y), p.z + t.z * (q.z - p.z),
+                                    p.w + t.w * (q.w - p.w));
+                else
+                    r = make_float4(fminf(fmaxf(p.x, q.x), t.x), fminf(fmaxf(p.y, q.y), t.y),
+                                    fminf(fmaxf(p.z, q.z), t.z), fminf(fmaxf(p.w, q.w), t.w));
+                st[sp - 1] = r;
+                break;
+            }
+            case IE_DOT: {
+                const float4 p = st[sp - 2], q = st[sp - 1];
+                --sp;
+                float d = p.x * q.x;
+                if (in.a > 1) d = d + p.y * q.y;
+                if (in.a > 2) d = d + p.z * q.z;
+                if (in.a > 3) d = d + p.w * q.w;
+                st[sp - 1] = make_float4(d, d, d, d);
+                break;
+            }
+            case IE_CTOR: {
+                const int n = in.a;
+                float o[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+                int k = 0;
+                for (int j = 0; j < n; ++j) {
+                    const float4 v = st[sp - n + j];
+                    const int w = ((in.b >> (2 * j)) & 3) + 1;
+                    for (int l = 0; l < w && k < 4; ++l) o[k++] = lane(v, l);
+                }
+                if (n == 1 && (in.b & 3) == 0) o[1] = o[2] = o[3] = o[0];  // floatN(scalar)
+                sp -= n - 1;
+                st[sp - 1] = make_float4(o[0], o[1], o[2], o[3]);
+                break;
+            }
+        }
+    }
+    const float4 r = st[0];
+    const size_t o = (size_t)y * a.W + x;
+    switch (a.outFmt) {
+        case RSD_FMT_RGBA32F: static_cast<float4*>(a.out)[o] = r; break;
+        case RSD_FMT_RG32F: static_cast<float2*>(a.out)[o] = make_float2(r.x, r.y); break;
+        case RSD_FMT_R32F: static_cast<float*>(a.out)[o] = r.x; break;
+        default: static_cast<uint8_t*>(a.out)[o] = unorm8(r.x); break;  // RSD_FMT_R8UNORM
+    }
+}
+
+}  // namespace
+}  // namespace rsd
+
+using namespace rsd;
+
+extern "C" rsd_status rsd_cross_bilateral_blur(const uint8_t* d_src, const float* d_linear_z, uint32_t z_w,
+                                               uint32_t z_h, uint8_t* d_pingpong, uint8_t* d_dst, uint32_t width,
+                                               uint32_t height, uint32_t guard_band, uint32_t kernel_radius,
+                                               uint32_t better_slope, rsd_stream stream) {
+    if (!d_src || !d_linear_z || !d_pingpong || !d_dst || width == 0 || height == 0 || z_w == 0 || z_h == 0 ||
+        kernel_radius < 1 || kernel_radius > 20 || 2 * guard_band >= width || 2 * guard_band >= height) {
+        set_error("rsd_cross_bilateral_blur: invalid argument (radius 1..20, guard band inside the frame)");
+        return RSD_ERR_INVALID_ARG;
+    }
+    BlurArgs a{};
+    a.z = d_linear_z;
+    a.zW = (int)z_w;
+    a.zH = (int)z_h;
+    a.W = (int)width;
+    a.H = (int)height;
+    a.g = (int)guard_band;
+    a.betterSlope = better_slope ? 1u : 0u;
+    // GuardBand.cpp:62-63
+    a.uvMinX = ((float)guard_band + 0.5f) / (float)width;
+    a.uvMinY = ((float)guard_band + 0.5f) / (float)height;
+    a.uvMaxX = ((float)width - ((float)guard_band + 0.5f)) / (float)width;
+    a.uvMaxY = ((float)height - ((float)guard_band + 0.5f)) / (float)height;
+    hipStream_t s = (hipStream_t)stream;
+    for (int pass = 0; pass < 2; ++pass) {  // blur in x into the ping-pong image, then in y
+        a.src = pass == 0 ? d_src : d_pingpong;
+        a.dst = pass == 0 ? d_pingpong : d_dst;
+        a.dirX = pass == 0 ? 1.0f : 0.0f;
+        a.dirY = pass == 0 ? 0.0f : 1.0f;
+        hipError_t e = hipSuccess;
+        switch (kernel_radius) {
+#define RSD_R(r) case r: e = launch_blur<r>(a, s); break;
+            RSD_R(1) RSD_R(2) RSD_R(3) RSD_R(4) RSD_R(5) RSD_R(6) RSD_R(7) RSD_R(8) RSD_R(9) RSD_R(10)
+            RSD_R(11) RSD_R(12) RSD_R(13) RSD_R(14) RSD_R(15) RSD_R(16) RSD_R(17) RSD_R(18) RSD_R(19) RSD_R(20)
+#undef RSD_R
+        }
+        if (e != hipSuccess) return hip_fail(e, "blur_kernel launch");
+    }
+    return RSD_OK;
+}
+
+extern "C" rsd_status rsd_image_equation_run(const rsd_image_program* prog, const rsd_texture* inputs,
+                                             const rsd_texture* out, rsd_stream stream) {
+    if (!prog || !out || !out->ptr || out->width == 0 || out->height == 0) {
+        set_error("rsd_image_equation_run: null program or output");
+        return RSD_ERR_INVALID_ARG;
+    }
+    const uint32_t f = out->format;
+    if (f != RSD_FMT_RGBA32F && f != RSD_FMT_RG32F && f != RSD_FMT_R32F && f != RSD_FMT_R8UNORM) {
+        set_error("rsd_image_equation_run: output format must be RGBA32F, RG32F, R32F or R8Unorm");
+        return RSD_ERR_UNSUPPORTED;
+    }
+    EqArgs a{};
+    a.prog = image_program(prog);
+    for (int k = 0; k < 4; ++k) {
+        if (inputs && inputs[k].ptr) {
+            if (inputs[k].format >= RSD_FMT_UNKNOWN) {
+                set_error("rsd_image_equation_run: input of unknown format");
+                return RSD_ERR_INVALID_ARG;
+            }
+            a.in[k] = TexDesc{inputs[k].ptr, (int)inputs[k].width, (int)inputs[k].height, inputs[k].format};
+        }
+    }
+    a.out = out->ptr;
+    a.W = (int)out->width;
+    a.H = (int)out->height;
+    a.outFmt = f;
+    const dim3 grid((a.W + kPostW - 1) / kPostW, (a.H + kPostH - 1) / kPostH);
+    hipLaunchKernelGGL(image_equation_kernel, grid, dim3(kPostW, kPostH), 0, (hipStream_t)stream, a);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? RSD_OK : hip_fail(e, "image_equation_kernel launch");
+}

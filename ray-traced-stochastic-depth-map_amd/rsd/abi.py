@@ -101,7 +101,9 @@ GRAPH_EXPORTS = ["rsd_graph_create", "rsd_graph_destroy", "rsd_graph_create_pass
                  "rsd_graph_mark_output", "rsd_graph_set_scene", "rsd_graph_set_input", "rsd_graph_compile",
                  "rsd_graph_execute", "rsd_graph_plan", "rsd_graph_resources", "rsd_graph_get_output",
                  "rsd_graph_copy_output", "rsd_graph_execution_order", "rsd_graph_pass_times",
-                 "rsd_graph_get_dict_int", "rsd_graph_pass_count", "rsd_plugin_set_dir", "rsd_plugin_types"]
+                 "rsd_graph_get_dict_int", "rsd_graph_pass_count", "rsd_plugin_set_dir", "rsd_plugin_types",
+                 "rsd_cross_bilateral_blur", "rsd_image_equation_compile", "rsd_image_equation_info",
+                 "rsd_image_equation_run", "rsd_image_equation_release"]
 
 FMT_R32F, FMT_RG32F, FMT_RGBA32F, FMT_R16U, FMT_R8U, FMT_R8UNORM, FMT_R32U, FMT_UNKNOWN = range(8)
 
@@ -199,6 +201,16 @@ def lib():
             fn = getattr(L, name)
             fn.restype = st
             fn.argtypes = args
+        L.rsd_cross_bilateral_blur.restype = st
+        L.rsd_cross_bilateral_blur.argtypes = [vp, vp, u32, u32, vp, vp, u32, u32, u32, u32, u32, vp]
+        L.rsd_image_equation_compile.restype = st
+        L.rsd_image_equation_compile.argtypes = [C.c_char_p, C.POINTER(vp)]
+        L.rsd_image_equation_info.restype = st
+        L.rsd_image_equation_info.argtypes = [vp, C.POINTER(u32), C.POINTER(u32)]
+        L.rsd_image_equation_run.restype = st
+        L.rsd_image_equation_run.argtypes = [vp, C.POINTER(Texture), C.POINTER(Texture), vp]
+        L.rsd_image_equation_release.restype = None
+        L.rsd_image_equation_release.argtypes = [vp]
         L.rsd_graph_destroy.restype = None
         L.rsd_graph_destroy.argtypes = [vp]
         _lib = L

@@ -97,3 +97,45 @@ def test_graph_reexecute_is_stable(setup, expected):
     g.execute()
     torch.cuda.synchronize()
     np.testing.assert_array_equal(_np(g.output_tensor("SVAO.ao")), expected["ao"])
+
+
+def test_graph_blur(setup, expected, oracle):
+    """Blur = CrossBilateralBlur of SVAO.ao over the linear depth, inside the 16 px guard band."""
+    g = setup["g"]
+    want, _ = oracle.cross_bilateral_blur(expected["ao"], expected["linear_z"], 16)
+    got = _np(g.output_tensor("Blur.colorOut"))
+    np.testing.assert_array_equal(got, want)
+    assert not np.array_equal(got[16:-16, 16:-16], expected["ao"][16:-16, 16:-16])
+
+
+def test_graph_ao_post_chain(setup, expected, oracle):
+    """scripts/SVAO.py's chain to the marked output AmbientRef.out (blur -> disabled TemporalAO
+    -> Switch -> ImageEquation 'I0[xy].rrra') and two SAVO_record.py formulas, bit-exact."""
+    from oracle import image_eq as IE
+    from rsd import graph as rg
+    s = setup
+    cfg = s["cfg"]
+    from rsd.frame import Device, GpuScene
+    dev = Device(0)
+    gs = GpuScene(dev, s["scene"])
+    g = rg.load_script(ROOT / "tests" / "graphs" / "svao_post.py")["SVAOPost"]
+    g.set_scene(gs.h, s["cam"])
+    g.compile(cfg.fb_w, cfg.fb_h)
+    g.execute()
+    s["torch"].cuda.synchronize()
+    blurred, _ = oracle.cross_bilateral_blur(expected["ao"], expected["linear_z"], 16)
+    W, H = cfg.fb_w, cfg.fb_h
+    amb = IE.store(IE.evaluate("I0[xy].rrra", [(blurred, IE.FMT_R8UNORM), (None, 0), (None, 0), (None, 0)], W, H),
+                   IE.FMT_RGBA32F)
+    got = _np(g.output_tensor("AmbientRef.out"))
+    np.testing.assert_array_equal(got.view(np.uint32).reshape(-1), amb.view(np.uint32).reshape(-1))
+    e1 = IE.store(IE.evaluate("1.0 - max(I0[xy].x-I0[xy].y, 0.05)", [(amb, IE.FMT_RGBA32F)] + [(None, 0)] * 3, W, H),
+                  IE.FMT_R8UNORM)
+    np.testing.assert_array_equal(_np(g.output_tensor("ImageEquation1.out")).reshape(H, W), e1)
+    lz = IE.store(IE.evaluate("I0[xy]/1000.0", [(expected["linear_z"], IE.FMT_R32F)] + [(None, 0)] * 3, W, H),
+                  IE.FMT_R32F)
+    np.testing.assert_array_equal(_np(g.output_tensor("ImageEquationLinearDepth.out")).view(np.uint32).reshape(-1),
+                                  lz.view(np.uint32).reshape(-1))
+    g.close()
+    gs.release()
+    dev.close()

@@ -1,0 +1,84 @@
+"""GPU parity of the post-SVAO image passes through the C ABI:
+rsd_cross_bilateral_blur vs oracle.cross_bilateral_blur, rsd_image_equation_run vs the
+numpy restatement oracle/image_eq.py.  Bit-exact."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+F = np.float32
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    return torch
+
+
+def _stream(torch):
+    return C.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+@pytest.mark.parametrize("radius,better,guard", [(4, 1, 16), (1, 1, 0), (7, 0, 8), (20, 1, 3)])
+def test_blur_parity(torch, oracle, radius, better, guard):
+    from rsd import abi
+    rng = np.random.default_rng(radius)
+    H, W = 67, 131
+    yy, xx = np.mgrid[0:H, 0:W]
+    z = (5.0 + 3.0 * np.sin(xx / 9.0) + (xx > 70) * 20.0 + 0.01 * yy).astype(F)  # smooth + one depth edge
+    src = rng.integers(0, 256, (H, W)).astype(np.uint8)
+    dz, ds = torch.from_numpy(z).cuda(), torch.from_numpy(src).cuda()
+    pp = torch.zeros((H, W), dtype=torch.uint8, device="cuda")
+    out = torch.zeros((H, W), dtype=torch.uint8, device="cuda")
+    st = abi.lib().rsd_cross_bilateral_blur(C.c_void_p(ds.data_ptr()), C.c_void_p(dz.data_ptr()), W, H,
+                                            C.c_void_p(pp.data_ptr()), C.c_void_p(out.data_ptr()), W, H, guard,
+                                            radius, better, _stream(torch))
+    abi.check(st, "rsd_cross_bilateral_blur")
+    torch.cuda.synchronize()
+    want, _ = oracle.cross_bilateral_blur(src, z, guard, radius, bool(better))
+    assert np.array_equal(out.cpu().numpy(), want)
+
+
+FORMULAS = ["I0[xy].rrra", "I0[xy].r * I1[xy]", "I0[xy].xxxx", "I0[xy].gggg", "1.0 - max(I0[xy].x-I0[xy].y, 0.05)",
+            "I0[xy]", "I0[xy]/1000.0", "saturate(I1[xy] * 2.0f - 0.5)", "float4(I1[xy].bgr, 1.0)",
+            "lerp(I1[xy], I2[xy], 0.25)", "dot(I1[xy].xyz, I2[xy].xyz)", "pow(abs(I1[xy]), 2.2) + -I3[xy]",
+            "clamp(I1[xy], 0.1, 0.9).wzyx", "float4(float2(I0[xy].x, 1), I2[xy].xy)", "step(0.5, I1[xy].r)",
+            "exp2(-I1[xy].r * I2[xy].g) + sqrt(abs(I3[xy])) * frac(I1[xy] * 7.0)", "min(I1[xy], I2[xy]) / I3[xy]",
+            "sin(I1[xy]) * cos(I2[xy].x) + log2(abs(I3[xy]) + 1.0)"]
+
+
+@pytest.mark.parametrize("out_fmt", [2, 0, 5, 1])  # RGBA32F, R32F, R8Unorm, RG32F
+def test_image_equation_parity(torch, out_fmt):
+    from oracle import image_eq as IE
+    from rsd import abi
+    rng = np.random.default_rng(out_fmt)
+    H, W = 37, 70
+    imgs = [rng.integers(0, 256, (H, W)).astype(np.uint8),                     # R8Unorm
+            (rng.random((H, W, 4)) * 3 - 1).astype(F),                         # RGBA32F
+            rng.random((H - 5, W - 9, 2)).astype(F),                           # RG32F, smaller
+            (rng.random((H, W)) * 4 - 2).astype(F)]                            # R32F
+    fmts = [IE.FMT_R8UNORM, IE.FMT_RGBA32F, IE.FMT_RG32F, IE.FMT_R32F]
+    dev = [torch.from_numpy(np.ascontiguousarray(a)).cuda() for a in imgs]
+    tex = (abi.Texture * 4)()
+    for k, (a, t) in enumerate(zip(imgs, dev)):
+        tex[k] = abi.Texture(t.data_ptr(), a.shape[1], a.shape[0], 1, fmts[k], t.numel() * t.element_size())
+    ch = {2: 4, 1: 2, 0: 1, 5: 1}[out_fmt]
+    dt = torch.uint8 if out_fmt == 5 else torch.float32
+    for formula in FORMULAS:
+        h = C.c_void_p()
+        abi.check(abi.lib().rsd_image_equation_compile(formula.encode(), C.byref(h)), formula)
+        out = torch.zeros((H, W, ch), dtype=dt, device="cuda")
+        ot = abi.Texture(out.data_ptr(), W, H, 1, out_fmt, out.numel() * out.element_size())
+        abi.check(abi.lib().rsd_image_equation_run(h, tex, C.byref(ot), _stream(torch)), formula)
+        torch.cuda.synchronize()
+        abi.lib().rsd_image_equation_release(h)
+        want = IE.store(IE.evaluate(formula, list(zip(imgs, fmts)), W, H), out_fmt)
+        got = out.cpu().numpy().reshape(want.shape)
+        if got.dtype == np.uint8:
+            assert np.array_equal(got, want), formula
+        else:  # bit-exact, NaNs (of either sign / payload) compare equal
+            nan = np.isnan(want)
+            assert np.array_equal(np.isnan(got), nan), formula
+            assert np.array_equal(got[~nan].view(np.uint32), want[~nan].view(np.uint32)), formula

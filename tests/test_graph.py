@@ -44,8 +44,8 @@ def test_script_load_and_plan():
     sd = ((FB[0] + 1) // 2 + 64, (FB[1] + 1) // 2 + 64)
     assert res["SVAO.internalRayMin"] == (sd[0], sd[1], 1, "R32Uint")
     assert res["SVAO.internalRayMax"] == (sd[0], sd[1], 1, "R32Uint")
-    # a stub output takes the format the consumer does not constrain: RGBA32F
-    assert res["Blur.colorOut"][3] == "RGBA32Float"
+    # CrossBilateralBlur is a real pass now: R8Unorm like the reference
+    assert res["Blur.colorOut"] == (FB[0], FB[1], 1, "R8Unorm")
     assert "Unused.dst" not in res
 
 
@@ -72,6 +72,13 @@ def test_reference_svao_scripts_plan(name):
     assert order.index("CompressNormals") < order.index("SVAO")
     res = g.resources()
     assert res["SVAO.internalRayMax"][:2] == (768, 558)  # 1080p, divisor 4, 512 px SD guard band
+    if name == "SVAO.py":
+        # the AO chain to the marked output AmbientRef.out runs real passes:
+        # SVAO.ao -> CrossBilateralBlur -> TemporalAO (disabled) -> Switch -> ImageEquation
+        for p in ("CrossBilateralBlur0", "TemporalAO", "AOSwitch", "AmbientRef"):
+            assert p in order
+        assert res["AOSwitch.out"] == (2048, 1208, 1, "R8Unorm")  # shaped like the selected input
+        assert res["AmbientRef.out"] == (2048, 1208, 1, "RGBA32Float")
 
 
 @pytest.mark.skipif(not REF_SCRIPTS.is_dir(), reason="reference scripts not present (GPU box)")
