@@ -91,7 +91,7 @@ extern "C" rsd_status rsd_scene_upload(rsd_device* dev, const rsd_scene_desc* de
     s->tri_offset = (uint32_t)(bvh.nodes.size() / 4);
     hipError_t e = hipMalloc(&s->d_nodes, total);
     if (e == hipSuccess) e = hipMalloc(&s->d_counters, 16 * sizeof(unsigned long long));
-    if (e == hipSuccess) e = hipMalloc(&s->d_qctl, 64 * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMalloc(&s->d_qctl, 128 * sizeof(uint32_t));
     if (e == hipSuccess) e = hipMemset(s->d_nodes, 0, total);
     if (e == hipSuccess) e = hipMemcpy(s->d_nodes, bvh.nodes.data(), nb, hipMemcpyHostToDevice);
     if (e == hipSuccess && tb)

@@ -34,7 +34,9 @@ struct rsd_scene {
     rsd::BvhStats stats;
     uint64_t device_bytes = 0;
     unsigned long long* d_counters = nullptr;  // 8 x u64 scratch for instrumented traces
-    uint32_t* d_qctl = nullptr;    // live-ray queue {count[32], head[32]}
+    uint32_t* d_qctl = nullptr;    // live-ray queue control {count[32], head[32]} x 2 (double-buffered)
+    uint32_t qctl_gen = 0;         // trace calls so far: buffer qctl_gen % 2 is zero and next in line
+    bool qctl_dirty = true;        // reset both buffers before the next trace (first use, failed launch)
     void* d_queue = nullptr;       // SD-trace workspace (live-ray records + K-key slots), grow-only
     size_t queue_cap = 0;          // bytes
     void* d_alpha = nullptr;       // alpha data (rsd_scene_upload_alpha), one allocation

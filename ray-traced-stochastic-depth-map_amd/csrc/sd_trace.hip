@@ -57,6 +57,8 @@ struct SDArgs {
     int bandIndex, bandCount;  // screen-band sharding: 8-row tile rows t with t % count == index
     int poolSoft;      // row traversal: above this many pooled items a row pops one item per step
     const float* rayTab;  // per-column / per-row ray terms (ray_table_kernel), see sd_ray
+    uint32_t deadFast;    // setup may classify rayMin == asuint(FLT_MAX) texels as dead directly
+    uint32_t* qctlNext;   // the other queue-control buffer, zeroed by the setup kernel
     uint32_t alphaTest;   // USE_ALPHA_TEST and the scene has alpha data
     AlphaData alphaData;  // spread = RAY_CONE_SPREAD
 };
@@ -401,9 +403,14 @@ __device__ __forceinline__ void ray_rec_load(const float4* __restrict__ q, uint3
 // is empty keep DEFAULT_DEPTH and are written here; the others are appended to a compact
 // queue of ray records (one atomic per wave) so that phase 2 runs full waves of live rays
 // and starts traversing without recomputing the ray.
+// The queue control words {count[32], head[32]} are double-buffered across calls: call k
+// uses buffer k % 2 (zero on entry) and its setup kernel zeroes buffer (k + 1) % 2, which
+// call k - 1 finished with (stream order) -- no memset launch per trace.
 template <int N>
 __global__ void __launch_bounds__(kBlock) sd_setup_kernel(SDArgs a, float4* __restrict__ queue,
-                                                          uint32_t* __restrict__ qctl) {
+                                                          uint32_t* __restrict__ qctl, uint32_t* __restrict__ qctlNext) {
+    static_assert(kBlock >= 2 * kQueueParts, "one lane per control word");
+    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < 2 * kQueueParts) qctlNext[threadIdx.x] = 0u;
     const int lane = threadIdx.x;
     const int x = blockIdx.x * kTile + (lane & (kTile - 1));
     const int y = ((int)blockIdx.y * a.bandCount + a.bandIndex) * kTile + (lane / kTile);
@@ -412,7 +419,10 @@ __global__ void __launch_bounds__(kBlock) sd_setup_kernel(SDArgs a, float4* __re
     f3 d = mk(0.0f, 0.0f, 0.0f);
     float TMin = 0.0f, TMax = 0.0f, cosT = 0.0f;
     if (inside) {
-        live = sd_ray(a, x, y, d, TMin, TMax, cosT);
+        // rayMin never lowered by pass 1 (still asuint(FLT_MAX)): TMin >= FLT_MAX > TMax, the
+        // texel is dead without evaluating its ray (a.deadFast: the host proved TMax < FLT_MAX)
+        const bool untouched = a.deadFast && a.rayMin[(size_t)y * a.sdW + x] == 0x7f7fffffu;
+        live = !untouched && sd_ray(a, x, y, d, TMin, TMax, cosT);
         if (!live) {
             float depths[N];
             const float DEFAULT = a.normalize ? 1.0f : 3.40282347e+37f;  // Common.slangh:16
@@ -927,7 +937,7 @@ __global__ void __launch_bounds__(kBlock) sd_trace_row_kernel(SDArgs a, const fl
 // (StochasticDepthMapRT.rt.slang:90-104).  Persistent rows stride over the queue partitions.
 template <int K, int N, int ROW>
 __global__ void __launch_bounds__(kBlock) sd_resolve_row_kernel(SDArgs a, const float4* __restrict__ queue,
-                                                                const uint32_t* __restrict__ qctl,
+                                                                uint32_t* __restrict__ qctl,
                                                                 const uint2* __restrict__ keys) {
     constexpr int kRowRays = kBlock / ROW;
     const int lane = threadIdx.x;
@@ -1048,7 +1058,8 @@ template <int K, int N>
 static hipError_t launch_sd_kn(const SDArgs& a, dim3 grid, uint32_t persistentBlocks, float4* queue, uint32_t* qctl,
                                uint2* keys, int walk, hipStream_t s) {
     constexpr int ROW = K <= 8 ? 8 : 16;
-    hipLaunchKernelGGL((sd_setup_kernel<N>), grid, dim3(kBlock), 0, s, a, queue, qctl);
+    uint32_t* qctlNext = a.qctlNext;
+    hipLaunchKernelGGL((sd_setup_kernel<N>), grid, dim3(kBlock), 0, s, a, queue, qctl, qctlNext);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const dim3 pg(persistentBlocks), wb(kBlock);
@@ -1061,7 +1072,11 @@ static hipError_t launch_sd_kn(const SDArgs& a, dim3 grid, uint32_t persistentBl
         if (a.counters) hipLaunchKernelGGL((sd_trace_row_kernel<K, N, ROW, true, true>), pg, wb, 0, s, a, queue, qctl, keys);
         else hipLaunchKernelGGL((sd_trace_row_kernel<K, N, ROW, true, false>), pg, wb, 0, s, a, queue, qctl, keys);
         if ((e = hipGetLastError()) != hipSuccess) return e;
-        hipLaunchKernelGGL((sd_resolve_row_kernel<K, N, ROW>), pg, wb, 0, s, a, queue, qctl, keys);
+        // resolve rows: RSD_RESOLVE_WAVES_PER_CU (experiments) scales the persistent grid
+        static const char* rwEnv = std::getenv("RSD_RESOLVE_WAVES_PER_CU");
+        const uint32_t rb = rwEnv ? std::max(1u, persistentBlocks * (uint32_t)std::max(1, std::atoi(rwEnv)) / 8u)
+                                  : persistentBlocks;
+        hipLaunchKernelGGL((sd_resolve_row_kernel<K, N, ROW>), dim3(rb), wb, 0, s, a, queue, qctl, keys);
     } else if (walk == 1) {
         if (a.counters) hipLaunchKernelGGL((sd_trace_row_kernel<K, N, ROW, false, true>), pg, wb, 0, s, a, queue, qctl, keys);
         else hipLaunchKernelGGL((sd_trace_row_kernel<K, N, ROW, false, false>), pg, wb, 0, s, a, queue, qctl, keys);
@@ -1216,6 +1231,25 @@ extern "C" rsd_status rsd_sd_trace_band(rsd_scene* scene, const rsd_camera* cam,
     a.bandIndex = (int)band_index;
     a.bandCount = (int)band_count;
     a.alphaTest = p->alpha_test && scene->d_alpha ? 1u : 0u;
+    a.deadFast = 0u;
+    if (p->ray_interval && d_ray_min) {
+        // Lower bound of dot(normalize(W), normalize(cam_dir)) over every texel centre of the
+        // map (guard band included): if farZ / bound is far below FLT_MAX, TMax < FLT_MAX for
+        // every texel, so rayMin == asuint(FLT_MAX) means TMin >= FLT_MAX > TMax (dead).
+        const int dimx = (int)sd_w - 2 * p->guard_band, dimy = (int)sd_h - 2 * p->guard_band;
+        auto ndcMax = [](double lo, double hi) { return std::max(std::fabs(2.0 * lo - 1.0), std::fabs(2.0 * hi - 1.0)); };
+        const double nx = ndcMax((-p->guard_band + 0.5) / dimx - cam->jitterX - 1.0 / dimx,
+                                 ((int)sd_w - p->guard_band) / (double)dimx - cam->jitterX + 1.0 / dimx);
+        const double ny = ndcMax((-p->guard_band + 0.5) / dimy + cam->jitterY - 1.0 / dimy,
+                                 ((int)sd_h - p->guard_band) / (double)dimy + cam->jitterY + 1.0 / dimy);
+        auto len = [](const float* v) { return std::sqrt((double)v[0] * v[0] + (double)v[1] * v[1] + (double)v[2] * v[2]); };
+        const double lw = len(cam->W);
+        auto dotw = [&](const float* v) { return ((double)v[0] * cam->W[0] + (double)v[1] * cam->W[1] + (double)v[2] * cam->W[2]) / lw; };
+        const double num = dotw(cam->W) - nx * std::fabs(dotw(cam->U)) - ny * std::fabs(dotw(cam->V));
+        const double den = nx * len(cam->U) + ny * len(cam->V) + lw;
+        const double lb = den > 0.0 ? num / den : 0.0;
+        if (dimx > 0 && dimy > 0 && lb > 1e-3 && (double)cam->farZ / (0.5 * lb) < 1e37) a.deadFast = 1u;
+    }
     a.alphaData = scene->alpha;
     a.alphaData.spread = rsd_ray_cone_spread(cam->focalLength, sd_h);  // default texture dims = SD map
     if (p->implementation == RSD_SD_COVERAGE_MASK) {
@@ -1271,7 +1305,14 @@ extern "C" rsd_status rsd_sd_trace_band(rsd_scene* scene, const rsd_camera* cam,
     }
     float4* queue = reinterpret_cast<float4*>(scene->d_queue);
     uint2* keys = reinterpret_cast<uint2*>(reinterpret_cast<char*>(scene->d_queue) + queueBytes);
-    RSD_HIP(hipMemsetAsync(scene->d_qctl, 0, 2 * kQueueParts * sizeof(uint32_t), s));
+    // double-buffered queue control (sd_setup_kernel); both buffers are reset on first use and
+    // after a failed launch sequence
+    if (scene->qctl_dirty) {
+        RSD_HIP(hipMemsetAsync(scene->d_qctl, 0, 4 * kQueueParts * sizeof(uint32_t), s));
+        scene->qctl_dirty = false;
+    }
+    uint32_t* qctl = scene->d_qctl + (scene->qctl_gen & 1u) * 2 * kQueueParts;
+    a.qctlNext = scene->d_qctl + ((scene->qctl_gen + 1u) & 1u) * 2 * kQueueParts;
     const uint32_t setupBlocks = grid.x * grid.y;
     a.partCap = (setupBlocks + kQueueParts - 1) / kQueueParts * (uint32_t)kBlock;
     // traversal walk: row-parallel (default) unless the tree is too deep for its LDS pool
@@ -1300,10 +1341,14 @@ extern "C" rsd_status rsd_sd_trace_band(rsd_scene* scene, const rsd_camera* cam,
                         kQueueParts;
     hipError_t e = hipSuccess;
     if (bandTiles == 0) {}
-    else if (K == 4) e = launch_sd_k<4>(a, N, grid, pb, queue, scene->d_qctl, keys, walk, s);
-    else if (K == 8) e = launch_sd_k<8>(a, N, grid, pb, queue, scene->d_qctl, keys, walk, s);
-    else e = launch_sd_k<16>(a, N, grid, pb, queue, scene->d_qctl, keys, walk, s);
-    if (e != hipSuccess) return hip_fail(e, "sd_trace_kernel launch");
+    else if (K == 4) e = launch_sd_k<4>(a, N, grid, pb, queue, qctl, keys, walk, s);
+    else if (K == 8) e = launch_sd_k<8>(a, N, grid, pb, queue, qctl, keys, walk, s);
+    else e = launch_sd_k<16>(a, N, grid, pb, queue, qctl, keys, walk, s);
+    if (e != hipSuccess) {
+        scene->qctl_dirty = true;
+        return hip_fail(e, "sd_trace_kernel launch");
+    }
+    if (bandTiles != 0) scene->qctl_gen++;
     if (counters) {
         unsigned long long h[16];
         RSD_HIP(hipMemcpyAsync(h, scene->d_counters, sizeof(h), hipMemcpyDeviceToHost, s));
