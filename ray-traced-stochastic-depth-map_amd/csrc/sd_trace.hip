@@ -539,6 +539,36 @@ __device__ __forceinline__ uint32_t row_bits(bool p, int base) {
     return (uint32_t)(__ballot(p) >> base) & ((1u << ROW) - 1u);
 }
 
+// Row-local moves without the LDS crossbar (8-lane rows: two per 16-lane DPP row; 16-lane
+// rows fall back to __shfl).  DPP row_shr:n -> lane i reads lane i - n, row_shl:n -> i + n.
+constexpr int kDppRowShr1 = 0x111, kDppRowShr4 = 0x114, kDppRowShl4 = 0x104, kDppQuad3 = 0xFF;
+// value of row lane L (3 or 7 for 8-lane rows) in every lane of the row
+template <int ROW, int L>
+__device__ __forceinline__ uint32_t row_bcast(uint32_t v, int l, int base) {
+    if constexpr (ROW == 8 && (L == 3 || L == 7)) {
+        const uint32_t q = dppu<kDppQuad3>(v);  // lanes 0-3 <- lane 3, lanes 4-7 <- lane 7
+        if constexpr (L == 7) {
+            const uint32_t w = dppu<kDppRowShl4>(q);  // lanes 0-3 <- lane 7
+            return l < 4 ? w : q;
+        } else {
+            const uint32_t w = dppu<kDppRowShr4>(q);  // lanes 4-7 <- lane 3
+            return l < 4 ? q : w;
+        }
+    } else {
+        return (uint32_t)__shfl((int)v, base + L);
+    }
+}
+template <int ROW, int L>
+__device__ __forceinline__ float row_bcastf(float v, int l, int base) {
+    return __uint_as_float(row_bcast<ROW, L>(__float_as_uint(v), l, base));
+}
+// value of row lane l - 1 (lane 0's result is unspecified)
+template <int ROW>
+__device__ __forceinline__ uint32_t row_prev(uint32_t v, int l, int base) {
+    if constexpr (ROW == 8) return dppu<kDppRowShr1>(v);
+    else return (uint32_t)__shfl((int)v, base + (l > 0 ? l - 1 : 0));
+}
+
 // insert key (nt, np, nl) into the row-distributed sorted list (lane j holds key j); the
 // largest key falls off the last lane
 template <int ROW>
@@ -546,9 +576,8 @@ __device__ __forceinline__ void row_insert(float& kt, uint32_t& kp, uint32_t& kl
                                            int srcL, int l, int base) {
     const uint32_t nl = __shfl(nlSrc, base + srcL);  // the new key's triangle record, from its lane
     const int pos = __popc(row_bits<ROW>(key_less(kt, kp, nt, np), base));
-    const int src = base + (l > 0 ? l - 1 : 0);
-    const float st = __shfl(kt, src);
-    const uint32_t sp = __shfl(kp, src), sl = __shfl(kl, src);
+    const float st = __uint_as_float(row_prev<ROW>(__float_as_uint(kt), l, base));
+    const uint32_t sp = row_prev<ROW>(kp, l, base), sl = row_prev<ROW>(kl, l, base);
     if (l == pos) {
         kt = nt; kp = np; kl = nl;
     } else if (l > pos) {
@@ -742,8 +771,8 @@ __global__ void __launch_bounds__(kBlock) sd_trace_row_kernel(SDArgs a, const fl
 
         // ---- one traversal step of this row
         const float tlo = useLB ? fmaxf(TMin, lbT) : TMin;
-        float kthT = __shfl(kt, base + K - 1);
-        uint32_t kthP = __shfl(kp, base + K - 1);
+        float kthT = row_bcastf<ROW, K - 1>(kt, l, base);
+        uint32_t kthP = row_bcast<ROW, K - 1>(kp, l, base);
         float thi = fminf(TMax, kthT);
         float ck[4];
         uint32_t ci[4];
@@ -813,8 +842,8 @@ __global__ void __launch_bounds__(kBlock) sd_trace_row_kernel(SDArgs a, const fl
                 const uint32_t bp = __shfl(prim, srcLane);
                 if (key_less(bt, bp, kthT, kthP)) {
                     row_insert<ROW>(kt, kp, kl, bt, bp, firstTri + (uint32_t)j, srcLane - base, l, base);
-                    kthT = __shfl(kt, base + K - 1);
-                    kthP = __shfl(kp, base + K - 1);
+                    kthT = row_bcastf<ROW, K - 1>(kt, l, base);
+                    kthP = row_bcast<ROW, K - 1>(kp, l, base);
                 }
             }
         }
