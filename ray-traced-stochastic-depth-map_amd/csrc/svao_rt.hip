@@ -129,11 +129,69 @@ __device__ __forceinline__ void trace_ao(const float4* __restrict__ bvh, uint32_
     }
 }
 
+// One refined direction of a pixel: primary visibility p (subtracted) and the traced
+// visibility r (added), Common.slang:598-651.
+__device__ __forceinline__ void rt_dir(const RtArgs& ra, const Basic& b, float u, float v, int i, float& p, float& rOut,
+                                       uint32_t* __restrict__ ldsItem, float* __restrict__ ldsT) {
+    const SvaoArgs& a = ra.s;
+    const rsd_vao_data& d = a.d;
+    const f3 camPos = mk(a.cam.posW[0], a.cam.posW[1], a.cam.posW[2]);
+    const float* M = ra.invView;
+    Sample s;
+    bool ssrAbove;
+    sample_init(a, u, v, b, i, s, ssrAbove);
+    eval_primary(a, b, s);
+    p = s.visibility;
+    // getSnappedUV (Common.slang:116-125), not clamped: rays may leave the screen
+    const float su = (floorf(s.su * d.resolution[0]) + 0.5f) / d.resolution[0];
+    const float sv = (floorf(s.sv * d.resolution[1]) + 0.5f) / d.resolution[1];
+    const f3 dv = normalize(uv_to_view(a, su, sv, 1.0f));
+    const f3 dw = mk(M[0] * dv.x + M[1] * dv.y + M[2] * dv.z, M[3] * dv.x + M[4] * dv.y + M[5] * dv.z,
+                     M[6] * dv.x + M[7] * dv.y + M[8] * dv.z);
+    const float initLen = length(s.ip);
+    const float pl = b.posVLength;
+    const float tHalo0 = (pl - s.sphereStart - b.radius - d.thickness * b.radius) * initLen / pl;
+    const float tInside0 = (pl - s.sphereEnd) * initLen / pl;
+    const float tCRS = (pl - b.radius - d.thickness * b.radius) * initLen / pl;
+    const float tSS = (pl - s.sphereStart) * initLen / pl;
+    float TMin = hmax(tHalo0, 0.0f);
+    const float TMax = tInside0;
+    if (!s.isInScreen) { s.visibility = 1.0f; s.objectSpaceZ = 3.402823466e+38f; }  // resetSample
+    const float eps = b.radius * 0.01f;
+    if (s.isInScreen) TMin = hmax(TMin, (pl - s.objectSpaceZ) * initLen / pl + eps);
+    float halo = tHalo0, inside = tInside0;
+    if (TMin <= TMax) {
+        RayCtx r;
+        ray_setup(r, camPos, dw);
+        float A, B;
+        trace_ao(ra.nodes, ra.triOff, r, TMin, TMax, ra.cull, tCRS, tSS, A, B, ldsItem, ldsT, ra.alphaTest != 0u,
+                 ra.alpha);
+        if (B != -INFINITY) halo = hmax(halo, B);
+        if (A != INFINITY) {
+            if (A <= tSS) halo = hmax(halo, A);
+            else inside = hmin(inside, A);
+        }
+    }
+    const float sphereVis = calc_visibility(d, pl - inside * pl / initLen, s.sphereStart, s.sphereEnd, s.pdf,
+                                            b.radius);
+    const float haloVis = calc_halo_visibility(d, pl - halo * pl / initLen, s.sphereStart, s.sphereEnd, s.pdf,
+                                               b.radius);
+    rOut = hmin(s.visibility, hmin(sphereVis, haloVis));
+}
+
 // SVAORaster2.ps.slang:48-65 / Ray.rt.slang:60-75 -> calcAO2 (Common.slang:523-663), Raytraced
-// branch.  8 x 8 pixels per 64-lane workgroup; one lane walks the AO rays of its pixel.
+// branch.  An 8 x 8 pixel tile per 64-lane workgroup: the tile's (pixel, direction) pairs of
+// non-zero stencil are listed in LDS (grouped per pixel, direction order) and every lane
+// traces one AO ray at a time; each pixel's vis = (vis - p_i) + r_i is then applied in
+// direction order (the per-pixel loop's exact float sequence).
 __global__ void __launch_bounds__(64) svao_pass2_rt_kernel(RtArgs ra) {
     __shared__ uint32_t sItem[kLdsStack * 64];
     __shared__ float sT[kLdsStack * 64];
+    __shared__ uint32_t sPix[64];    // slot: local pixel | mask << 8
+    __shared__ uint16_t sPair[512];  // slot << 3 | direction
+    __shared__ uint16_t sFirst[64];
+    __shared__ float sAcc[64], sP[64], sR[64];
+    __shared__ uint32_t sNPix, sNPair;
     const SvaoArgs& a = ra.s;
     const rsd_vao_data& d = a.d;
     const uint32_t lane = threadIdx.x;
@@ -141,71 +199,61 @@ __global__ void __launch_bounds__(64) svao_pass2_rt_kernel(RtArgs ra) {
     // g % bandCount == bandIndex
     const uint32_t by = blockIdx.y;
     const uint32_t tileRow = ((by / 4u) * a.bandCount + a.bandIndex) * 4u + by % 4u;
-    const uint32_t px = a.guard + blockIdx.x * 8u + lane % 8u;
-    const uint32_t py = a.guard + tileRow * 8u + lane / 8u;
+    const uint32_t x0 = a.guard + blockIdx.x * 8u, y0 = a.guard + tileRow * 8u;
     const uint32_t xEnd = ra.rayPipeline ? (uint32_t)a.W : (uint32_t)a.W - a.guard;
     const uint32_t yEnd = ra.rayPipeline ? (uint32_t)a.H : (uint32_t)a.H - a.guard;
-    if (px >= xEnd || py >= yEnd) return;
-    const size_t o = (size_t)py * a.W + px;
-    const uint32_t mask = a.stencil[o];
-    if (mask == 0u) return;
-    const float u = ((float)px + 0.5f) * d.invResolution[0];
-    const float v = ((float)py + 0.5f) * d.invResolution[1];
-    Basic b;
-    basic_init(a, u, v, b);
-    const f3 camPos = mk(a.cam.posW[0], a.cam.posW[1], a.cam.posW[2]);
-    const float* M = ra.invView;
-    float vis = 0.0f;
-#pragma unroll 1
-    for (int i = 0; i < 8; ++i) {
-        if (!(mask & (1u << i))) continue;
-        Sample s;
-        bool ssrAbove;
-        sample_init(a, u, v, b, i, s, ssrAbove);
-        eval_primary(a, b, s);
-        vis -= s.visibility;
-        // getSnappedUV (Common.slang:116-125), not clamped: rays may leave the screen
-        const float su = (floorf(s.su * d.resolution[0]) + 0.5f) / d.resolution[0];
-        const float sv = (floorf(s.sv * d.resolution[1]) + 0.5f) / d.resolution[1];
-        const f3 dv = normalize(uv_to_view(a, su, sv, 1.0f));
-        const f3 dw = mk(M[0] * dv.x + M[1] * dv.y + M[2] * dv.z, M[3] * dv.x + M[4] * dv.y + M[5] * dv.z,
-                         M[6] * dv.x + M[7] * dv.y + M[8] * dv.z);
-        const float initLen = length(s.ip);
-        const float pl = b.posVLength;
-        const float tHalo0 = (pl - s.sphereStart - b.radius - d.thickness * b.radius) * initLen / pl;
-        const float tInside0 = (pl - s.sphereEnd) * initLen / pl;
-        const float tCRS = (pl - b.radius - d.thickness * b.radius) * initLen / pl;
-        const float tSS = (pl - s.sphereStart) * initLen / pl;
-        float TMin = hmax(tHalo0, 0.0f);
-        const float TMax = tInside0;
-        if (!s.isInScreen) { s.visibility = 1.0f; s.objectSpaceZ = 3.402823466e+38f; }  // resetSample
-        const float eps = b.radius * 0.01f;
-        if (s.isInScreen) TMin = hmax(TMin, (pl - s.objectSpaceZ) * initLen / pl + eps);
-        float halo = tHalo0, inside = tInside0;
-        if (TMin <= TMax) {
-            RayCtx r;
-            ray_setup(r, camPos, dw);
-            float A, B;
-            trace_ao(ra.nodes, ra.triOff, r, TMin, TMax, ra.cull, tCRS, tSS, A, B, &sItem[lane], &sT[lane],
-                     ra.alphaTest != 0u, ra.alpha);
-            if (B != -INFINITY) halo = hmax(halo, B);
-            if (A != INFINITY) {
-                if (A <= tSS) halo = hmax(halo, A);
-                else inside = hmin(inside, A);
-            }
+    if (lane == 0) { sNPix = 0u; sNPair = 0u; }
+    __syncthreads();
+    {
+        const uint32_t px = x0 + lane % 8u, py = y0 + lane / 8u;
+        const uint32_t m = (px < xEnd && py < yEnd) ? a.stencil[(size_t)py * a.W + px] : 0u;
+        if (m) {
+            const uint32_t slot = atomicAdd(&sNPix, 1u), base = atomicAdd(&sNPair, (uint32_t)__popc(m));
+            sPix[slot] = lane | (m << 8);
+            sFirst[slot] = (uint16_t)base;
+            sAcc[slot] = 0.0f;
+            uint32_t j = base;
+            for (int i = 0; i < 8; ++i)
+                if (m & (1u << i)) sPair[j++] = (uint16_t)(slot << 3 | i);
         }
-        const float sphereVis = calc_visibility(d, pl - inside * pl / initLen, s.sphereStart, s.sphereEnd, s.pdf,
-                                                b.radius);
-        const float haloVis = calc_halo_visibility(d, pl - halo * pl / initLen, s.sphereStart, s.sphereEnd, s.pdf,
-                                                   b.radius);
-        s.visibility = hmin(s.visibility, hmin(sphereVis, haloVis));
-        vis += s.visibility;
     }
-    vis *= 1.0f / 8.0f;
-    vis *= 2.0f;
-    vis += unorm8_to_float(a.ao[o]);
-    vis = acc_pow(vis, d.exponent);
-    a.ao[o] = unorm8(vis);
+    __syncthreads();
+    const uint32_t nPix = sNPix, nPair = sNPair;
+    for (uint32_t c = 0; c < nPair; c += 64u) {
+        const uint32_t k = c + lane;
+        uint32_t slot = 0;
+        if (k < nPair) {
+            const uint32_t e = sPair[k];
+            slot = e >> 3;
+            const uint32_t lp = sPix[slot] & 63u;
+            const float u = ((float)(x0 + lp % 8u) + 0.5f) * d.invResolution[0];
+            const float v = ((float)(y0 + lp / 8u) + 0.5f) * d.invResolution[1];
+            Basic b;
+            basic_init(a, u, v, b);
+            float p, r;
+            rt_dir(ra, b, u, v, (int)(e & 7u), p, r, &sItem[lane], &sT[lane]);
+            sP[lane] = p;
+            sR[lane] = r;
+        }
+        __syncthreads();
+        if (k < nPair && k == max((uint32_t)sFirst[slot], c)) {
+            float acc = sAcc[slot];
+            for (uint32_t j = k; j < nPair && j < c + 64u && (uint32_t)(sPair[j] >> 3) == slot; ++j)
+                acc = (acc - sP[j - c]) + sR[j - c];
+            sAcc[slot] = acc;
+        }
+        __syncthreads();
+    }
+    if (lane < nPix) {
+        const uint32_t lp = sPix[lane] & 63u;
+        const size_t o = (size_t)(y0 + lp / 8u) * a.W + (x0 + lp % 8u);
+        float vis = sAcc[lane];
+        vis *= 1.0f / 8.0f;
+        vis *= 2.0f;
+        vis += unorm8_to_float(a.ao[o]);
+        vis = acc_pow(vis, d.exponent);
+        a.ao[o] = unorm8(vis);
+    }
 }
 
 }  // namespace rsd
