@@ -179,8 +179,9 @@ class Renderer:
         self.normals = torch.empty((H, W), dtype=torch.int16, device=dv)
         self.ao = torch.zeros((H, W), dtype=torch.uint8, device=dv)  # SVAO.cpp:307 clears on first use
         self.stencil = torch.zeros((H, W), dtype=torch.uint8, device=dv)
-        self.ray_min = torch.empty((self.sd_h, self.sd_w), dtype=torch.int32, device=dv)
-        self.ray_max = torch.empty((self.sd_h, self.sd_w), dtype=torch.int32, device=dv)
+        # rayMin / rayMax in one allocation: a sharded frame all-reduces both in one collective
+        self.ray_minmax = torch.empty((2, self.sd_h, self.sd_w), dtype=torch.int32, device=dv)
+        self.ray_min, self.ray_max = self.ray_minmax[0], self.ray_minmax[1]
         self.sd = torch.empty(((N + 3) // 4, self.sd_h, self.sd_w, min(N, 4)), dtype=torch.float32, device=dv)
 
     @property

@@ -5,9 +5,9 @@ code runs over gloo on CPU tensors for the multi-process tests.  Every rank hold
 replicated BVH and G-buffer.  Per frame, rank r of B:
 
   1. clears the ray-interval maps and runs pass 1 ("AO 1") on its band of rows;
-  2. all-reduces the interval maps (MIN on rayMin, MAX on rayMax, int32 bit patterns of
-     non-negative floats order like the floats) -- now every rank has the exact union the
-     single-GPU pass 1 would have produced;
+  2. all-reduces the interval maps in one collective (MIN on rayMin and on -rayMax: int32
+     bit patterns of non-negative floats order like the floats) -- now every rank has the
+     exact union the single-GPU pass 1 would have produced;
   3. traces its band of SD-map tile rows;
   4. all-gathers the SD map (pass 2 reads SD texels up to ssMaxRadius away);
   5. runs pass 2 ("AO 2") on its band and all-gathers the AO image.
@@ -55,6 +55,16 @@ class BandFrame:
         self.sd_recv = torch.zeros((world,) + tuple(self.sd_send.shape), dtype=b.sd.dtype, device=dev)
         self.ao_send = torch.zeros((self.ao_max, b.ao.shape[1]), dtype=b.ao.dtype, device=dev)
         self.ao_recv = torch.zeros((world, self.ao_max, b.ao.shape[1]), dtype=b.ao.dtype, device=dev)
+        # unpack maps: the valid rows of recv (flattened over ranks) and where they go -- one
+        # index_select + one index_copy per exchange instead of one copy per rank
+        self.sd_unpack = self._unpack_map(self.sd_rows, self.sd_max, dev)
+        self.ao_unpack = self._unpack_map(self.ao_rows, self.ao_max, dev)
+
+    @staticmethod
+    def _unpack_map(rows, cap, dev):
+        src = torch.cat([k * cap + torch.arange(len(r), device=dev) for k, r in enumerate(rows)])
+        dst = torch.cat(list(rows))
+        return src, dst
 
     def _all_gather(self, recv, send):
         if self.nccl:
@@ -62,13 +72,15 @@ class BandFrame:
         else:
             self.dist.all_gather(list(recv.unbind(0)), send, group=self.pg)
 
-    def _gather_rows(self, t, rows, send, recv, dim):
+    def _gather_rows(self, t, rows, send, recv, dim, unpack):
         mine = rows[self.rank]
-        send.narrow(dim, 0, len(mine)).copy_(t.index_select(dim, mine))
+        torch.index_select(t, dim, mine, out=send.narrow(dim, 0, len(mine)))
         self._all_gather(recv, send)
-        for k in range(self.world):
-            if k != self.rank:
-                t.index_copy_(dim, rows[k], recv[k].narrow(dim, 0, len(rows[k])))
+        # recv [world, ..., cap, ...] -> rows (ranks x cap) along dim, then scatter the valid ones
+        # (the own band is written back unchanged)
+        src, dst = unpack
+        flat = recv.movedim(0, dim).flatten(dim, dim + 1) if dim > 0 else recv.flatten(0, 1)
+        t.index_copy_(dim, dst, flat.index_select(dim, src))
 
     def frame(self, sd_events=None):
         """One AO frame.  sd_events: optional (start, end) torch.cuda.Event pair recorded
@@ -77,15 +89,23 @@ class BandFrame:
         b.clear_intervals()
         b.pass1(band=band)
         if self.world > 1:
-            self.dist.all_reduce(b.ray_min, op=self.dist.ReduceOp.MIN, group=self.pg)
-            self.dist.all_reduce(b.ray_max, op=self.dist.ReduceOp.MAX, group=self.pg)
+            both = getattr(b, "ray_minmax", None)
+            if both is not None:
+                # one collective: MIN over [rayMin, -rayMax] (non-negative float bit patterns
+                # as int32: negation reverses their order exactly)
+                b.ray_max.neg_()
+                self.dist.all_reduce(both, op=self.dist.ReduceOp.MIN, group=self.pg)
+                b.ray_max.neg_()
+            else:
+                self.dist.all_reduce(b.ray_min, op=self.dist.ReduceOp.MIN, group=self.pg)
+                self.dist.all_reduce(b.ray_max, op=self.dist.ReduceOp.MAX, group=self.pg)
         if sd_events:
             sd_events[0].record()
         b.sd_trace(band=band)
         if sd_events:
             sd_events[1].record()
         if self.world > 1:
-            self._gather_rows(b.sd, self.sd_rows, self.sd_send, self.sd_recv, 1)
+            self._gather_rows(b.sd, self.sd_rows, self.sd_send, self.sd_recv, 1, self.sd_unpack)
         b.pass2(band=band)
         if self.world > 1:
-            self._gather_rows(b.ao, self.ao_rows, self.ao_send, self.ao_recv, 0)
+            self._gather_rows(b.ao, self.ao_rows, self.ao_send, self.ao_recv, 0, self.ao_unpack)

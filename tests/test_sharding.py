@@ -31,13 +31,14 @@ class OracleBackend:
         self.z, self.n = O.gbuffer(self.osc, self.cam, W, H, cfg.cull_mode, threads=2)
         self.np_ao = np.zeros((H, W), np.uint8)
         self.np_st = np.zeros((H, W), np.uint8)
-        self.np_rmin = np.zeros((self.sd_h, self.sd_w), np.uint32)
-        self.np_rmax = np.zeros((self.sd_h, self.sd_w), np.uint32)
+        # rayMin / rayMax in one buffer, like rsd.frame.Renderer (one all-reduce per frame)
+        self.np_rminmax = np.zeros((2, self.sd_h, self.sd_w), np.uint32)
+        self.np_rmin, self.np_rmax = self.np_rminmax[0], self.np_rminmax[1]
         self.np_sd = np.zeros(((N + 3) // 4, self.sd_h, self.sd_w, min(N, 4)), np.float32)
         self.ao = torch.from_numpy(self.np_ao)
         self.stencil = torch.from_numpy(self.np_st)
-        self.ray_min = torch.from_numpy(self.np_rmin.view(np.int32))
-        self.ray_max = torch.from_numpy(self.np_rmax.view(np.int32))
+        self.ray_minmax = torch.from_numpy(self.np_rminmax.view(np.int32))
+        self.ray_min, self.ray_max = self.ray_minmax[0], self.ray_minmax[1]
         self.sd = torch.from_numpy(self.np_sd)
 
     def clear_intervals(self):
