@@ -245,6 +245,38 @@ struct SnapCache {
 thread_local SnapCache g_snap;
 }  // namespace
 
+namespace {
+__global__ void normal_lut_kernel(float4* lut) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < 65536u) {
+        const f3 n = decode_normal_2x8(i);
+        lut[i] = make_float4(n.x, n.y, n.z, 0.0f);
+    }
+}
+struct NormalLut {
+    int dev = -1;
+    float4* d = nullptr;
+};
+thread_local NormalLut g_nlut;
+}  // namespace
+
+rsd_status normal_lut(const float4** out) {
+    int dev = 0;
+    RSD_HIP(hipGetDevice(&dev));
+    NormalLut& c = g_nlut;
+    if (c.dev != dev || !c.d) {
+        float4* d = nullptr;
+        RSD_HIP(hipMalloc(&d, 65536 * sizeof(float4)));
+        hipLaunchKernelGGL(normal_lut_kernel, dim3(256), dim3(256), 0, (hipStream_t)0, d);
+        RSD_HIP(hipGetLastError());
+        RSD_HIP(hipDeviceSynchronize());  // once per device and host thread
+        c.d = d;
+        c.dev = dev;
+    }
+    *out = c.d;
+    return RSD_OK;
+}
+
 rsd_status snap_tables(const rsd_vao_data& vd, const float** u, const float** v) {
     const int w = (int)vd.resolution[0], h = (int)vd.resolution[1];
     SnapCache& c = g_snap;
@@ -314,6 +346,7 @@ extern "C" rsd_status rsd_svao_pass1_band(const rsd_camera* cam, const rsd_vao_d
     fill_consts(a.k, a.d);
     {
         rsd_status ts = snap_tables(a.d, &a.snapU, &a.snapV);
+        if (ts == RSD_OK) ts = normal_lut(&a.nlut);
         if (ts != RSD_OK) return ts;
     }
     fill_scale(a);
@@ -367,6 +400,7 @@ extern "C" rsd_status rsd_svao_pass2_band(const rsd_camera* cam, const rsd_vao_d
     fill_consts(a.k, a.d);
     {
         rsd_status ts = snap_tables(a.d, &a.snapU, &a.snapV);
+        if (ts == RSD_OK) ts = normal_lut(&a.nlut);
         if (ts != RSD_OK) return ts;
     }
     fill_scale(a);

@@ -41,6 +41,7 @@ struct SvaoArgs {
     float isx, isy;  // imageScale (Common.slang:142), hoisted: 0.5 * (frameW / focal), same bits
     const float* snapU;  // getSnappedUV: snapU[k] = (k + 0.5f) / resolution.x for k in [0, resolution.x]
     const float* snapV;  //               snapV[k] = (k + 0.5f) / resolution.y
+    const float4* nlut;  // decode_normal_2x8 of every 16-bit code (normal_lut), same bits
 };
 
 struct Basic {
@@ -93,7 +94,8 @@ __device__ __forceinline__ bool basic_init(const SvaoArgs& a, float u, float v, 
     b.posVLength = length(b.posV);
     const uint32_t ix = (uint32_t)(u * d.resolution[0]), iy = (uint32_t)(v * d.resolution[1]);
     const uint32_t packed = (ix < (uint32_t)a.W && iy < (uint32_t)a.H) ? a.normals[(size_t)iy * a.W + ix] : 0u;
-    b.normalV = decode_normal_2x8(packed);
+    const float4 nl = a.nlut[packed];  // = decode_normal_2x8(packed), tabulated on the device
+    b.normalV = mk(nl.x, nl.y, nl.z);
     if (dot(b.posV, b.normalV) > 0.0f) b.normalV = -b.normalV;
     const float nu = u * d.noiseScale[0], nv = v * d.noiseScale[1];
     const int ni = ((int)floorf(nu * 4.0f)) & 3, nj = ((int)floorf(nv * 4.0f)) & 3;
@@ -233,6 +235,8 @@ inline void fill_consts(SvaoConsts& k, const rsd_vao_data& d) {
 
 // getSnappedUV tables for a frame size (device copies cached per thread, grow-only)
 rsd_status snap_tables(const rsd_vao_data& d, const float** u, const float** v);
+// decode_normal_2x8 for all 65536 codes, computed by a device kernel (bit-identical), cached
+rsd_status normal_lut(const float4** out);
 
 inline rsd_status check_common(const rsd_camera* cam, const rsd_vao_data* vao, const rsd_svao_params* p,
                                const float* depth, const uint16_t* normals, uint32_t W, uint32_t H, const char* who) {

@@ -283,6 +283,7 @@ extern "C" rsd_status rsd_svao_pass2_raytraced_band(rsd_scene* scene, const rsd_
     fill_consts(a.k, a.d);
     {
         rsd_status ts = snap_tables(a.d, &a.snapU, &a.snapV);
+        if (ts == RSD_OK) ts = normal_lut(&a.nlut);
         if (ts != RSD_OK) return ts;
     }
     fill_scale(a);
