@@ -255,6 +255,17 @@ rsd_status rsd_sd_trace_band(rsd_scene* scene, const rsd_camera* cam, const rsd_
                              const uint32_t* d_ray_min, const uint32_t* d_ray_max,
                              float* d_sd_out, uint32_t sd_w, uint32_t sd_h,
                              uint32_t band_index, uint32_t band_count, rsd_counters* counters, rsd_stream stream);
+/* The same with flags.  RSD_SD_CONSUME_INTERVALS (needs RayInterval): the trace resets every
+ * texel of d_ray_min / d_ray_max (rayMin = asuint(FLT_MAX), rayMax = 0) after reading it --
+ * the whole map, not only the band -- so the next frame's pass 1 may run without
+ * rsd_svao_clear_intervals (SVAO.cpp:334-340 folded into the trace's first kernel). */
+#define RSD_SD_CONSUME_INTERVALS 1u
+rsd_status rsd_sd_trace_band_ex(rsd_scene* scene, const rsd_camera* cam, const rsd_sd_params* params,
+                                const float* d_linear_z, uint32_t z_w, uint32_t z_h,
+                                uint32_t* d_ray_min, uint32_t* d_ray_max,
+                                float* d_sd_out, uint32_t sd_w, uint32_t sd_h,
+                                uint32_t band_index, uint32_t band_count, uint32_t flags,
+                                rsd_counters* counters, rsd_stream stream);
 rsd_status rsd_svao_pass1_band(const rsd_camera* cam, const rsd_vao_data* vao, const rsd_svao_params* params,
                                const float* d_depth, const uint16_t* d_normals, uint32_t width, uint32_t height,
                                uint8_t* d_ao, uint8_t* d_stencil, uint32_t* d_ray_min, uint32_t* d_ray_max,

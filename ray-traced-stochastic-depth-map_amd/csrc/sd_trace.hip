@@ -59,6 +59,9 @@ struct SDArgs {
     const float* rayTab;  // per-column / per-row ray terms (ray_table_kernel), see sd_ray
     uint32_t deadFast;    // setup may classify rayMin == asuint(FLT_MAX) texels as dead directly
     uint32_t* qctlNext;   // the other queue-control buffer, zeroed by the setup kernel
+    uint32_t consume;     // RSD_SD_CONSUME_INTERVALS: setup resets every texel's interval after use
+    uint32_t* rayMinW;    // writable aliases of rayMin / rayMax (consume only)
+    uint32_t* rayMaxW;
     uint32_t alphaTest;   // USE_ALPHA_TEST and the scene has alpha data
     AlphaData alphaData;  // spread = RAY_CONE_SPREAD
 };
@@ -413,8 +416,18 @@ __global__ void __launch_bounds__(kBlock) sd_setup_kernel(SDArgs a, float4* __re
     if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < 2 * kQueueParts) qctlNext[threadIdx.x] = 0u;
     const int lane = threadIdx.x;
     const int x = blockIdx.x * kTile + (lane & (kTile - 1));
-    const int y = ((int)blockIdx.y * a.bandCount + a.bandIndex) * kTile + (lane / kTile);
+    // consume: the grid covers every tile row of the map; other bands' rows only get their
+    // intervals reset (SVAO.cpp:334-340's clear for the next frame)
+    const int tileRow = a.consume ? (int)blockIdx.y : (int)blockIdx.y * a.bandCount + a.bandIndex;
+    const int y = tileRow * kTile + (lane / kTile);
     const bool inside = x < a.sdW && y < a.sdH;
+    if (a.consume && tileRow % a.bandCount != a.bandIndex) {
+        if (inside) {
+            a.rayMinW[(size_t)y * a.sdW + x] = 0x7f7fffffu;  // asuint(FLT_MAX)
+            a.rayMaxW[(size_t)y * a.sdW + x] = 0u;
+        }
+        return;  // uniform over the workgroup
+    }
     bool live = false;
     f3 d = mk(0.0f, 0.0f, 0.0f);
     float TMin = 0.0f, TMax = 0.0f, cosT = 0.0f;
@@ -423,6 +436,10 @@ __global__ void __launch_bounds__(kBlock) sd_setup_kernel(SDArgs a, float4* __re
         // texel is dead without evaluating its ray (a.deadFast: the host proved TMax < FLT_MAX)
         const bool untouched = a.deadFast && a.rayMin[(size_t)y * a.sdW + x] == 0x7f7fffffu;
         live = !untouched && sd_ray(a, x, y, d, TMin, TMax, cosT);
+        if (a.consume) {  // after the last read of this texel's interval
+            a.rayMinW[(size_t)y * a.sdW + x] = 0x7f7fffffu;
+            a.rayMaxW[(size_t)y * a.sdW + x] = 0u;
+        }
         if (!live) {
             float depths[N];
             const float DEFAULT = a.normalize ? 1.0f : 3.40282347e+37f;  // Common.slangh:16
@@ -1193,11 +1210,20 @@ rsd_status ensure_lut(uint32_t N, const int32_t** idx, const uint32_t** lut) {
 }
 }  // namespace
 
-extern "C" rsd_status rsd_sd_trace_band(rsd_scene* scene, const rsd_camera* cam, const rsd_sd_params* p,
-                                        const float* d_linear_z, uint32_t z_w, uint32_t z_h,
-                                        const uint32_t* d_ray_min, const uint32_t* d_ray_max, float* d_sd_out,
-                                        uint32_t sd_w, uint32_t sd_h, uint32_t band_index, uint32_t band_count,
-                                        rsd_counters* counters, rsd_stream stream) {
+extern "C" rsd_status rsd_sd_trace_band_ex(rsd_scene* scene, const rsd_camera* cam, const rsd_sd_params* p,
+                                           const float* d_linear_z, uint32_t z_w, uint32_t z_h, uint32_t* d_ray_min,
+                                           uint32_t* d_ray_max, float* d_sd_out, uint32_t sd_w, uint32_t sd_h,
+                                           uint32_t band_index, uint32_t band_count, uint32_t flags,
+                                           rsd_counters* counters, rsd_stream stream) {
+    const bool consume = (flags & RSD_SD_CONSUME_INTERVALS) != 0u;
+    if (flags & ~RSD_SD_CONSUME_INTERVALS) {
+        set_error("rsd_sd_trace_band_ex: unknown flag");
+        return RSD_ERR_INVALID_ARG;
+    }
+    if (consume && (!p || !p->ray_interval || !d_ray_min || !d_ray_max)) {
+        set_error("rsd_sd_trace_band_ex: RSD_SD_CONSUME_INTERVALS needs RayInterval and both interval maps");
+        return RSD_ERR_INVALID_ARG;
+    }
     if (band_count == 0 || band_index >= band_count) {
         set_error("rsd_sd_trace_band: band_index must be < band_count");
         return RSD_ERR_INVALID_ARG;
@@ -1230,6 +1256,10 @@ extern "C" rsd_status rsd_sd_trace_band(rsd_scene* scene, const rsd_camera* cam,
         std::vector<float> h((size_t)sd_w * sd_h * (N < 4 ? N : 4) * ((N + 3) / 4), def);
         RSD_HIP(hipMemcpyAsync(d_sd_out, h.data(), h.size() * sizeof(float), hipMemcpyHostToDevice, (hipStream_t)stream));
         RSD_HIP(hipStreamSynchronize((hipStream_t)stream));
+        if (consume) {
+            rsd_status cs = rsd_svao_clear_intervals(d_ray_min, d_ray_max, sd_w * sd_h, stream);
+            if (cs != RSD_OK) return cs;
+        }
         if (counters) { *counters = rsd_counters{}; counters->rays_dispatched = (uint64_t)sd_w * sd_h; }
         return RSD_OK;
     }
@@ -1261,6 +1291,9 @@ extern "C" rsd_status rsd_sd_trace_band(rsd_scene* scene, const rsd_camera* cam,
     a.bandCount = (int)band_count;
     a.alphaTest = p->alpha_test && scene->d_alpha ? 1u : 0u;
     a.deadFast = 0u;
+    a.consume = consume ? 1u : 0u;
+    a.rayMinW = d_ray_min;
+    a.rayMaxW = d_ray_max;
     if (p->ray_interval && d_ray_min) {
         // Lower bound of dot(normalize(W), normalize(cam_dir)) over every texel centre of the
         // map (guard band included): if farZ / bound is far below FLT_MAX, TMax < FLT_MAX for
@@ -1316,7 +1349,7 @@ extern "C" rsd_status rsd_sd_trace_band(rsd_scene* scene, const rsd_camera* cam,
     }
     const uint32_t tiles = (sd_h + kTile - 1) / kTile;
     const uint32_t bandTiles = tiles > band_index ? (tiles - band_index + band_count - 1) / band_count : 0u;
-    dim3 grid((sd_w + kTile - 1) / kTile, bandTiles);
+    dim3 grid((sd_w + kTile - 1) / kTile, consume ? tiles : bandTiles);
     // k = the MAX_COUNT nearest keys decide Default and KBuffer; coverage mask streams chunks
     const uint32_t need = p->implementation == RSD_SD_COVERAGE_MASK ? 8u : p->max_count;
     // live-ray queue workspace (grow-only; the first call of a larger map allocates)
@@ -1369,7 +1402,7 @@ extern "C" rsd_status rsd_sd_trace_band(rsd_scene* scene, const rsd_camera* cam,
     const uint32_t pb = ((uint32_t)std::max(1, scene->dev->cu_count) * wavesPerCu + kQueueParts - 1) / kQueueParts *
                         kQueueParts;
     hipError_t e = hipSuccess;
-    if (bandTiles == 0) {}
+    if (grid.y == 0) {}
     else if (K == 4) e = launch_sd_k<4>(a, N, grid, pb, queue, qctl, keys, walk, s);
     else if (K == 8) e = launch_sd_k<8>(a, N, grid, pb, queue, qctl, keys, walk, s);
     else e = launch_sd_k<16>(a, N, grid, pb, queue, qctl, keys, walk, s);
@@ -1377,7 +1410,7 @@ extern "C" rsd_status rsd_sd_trace_band(rsd_scene* scene, const rsd_camera* cam,
         scene->qctl_dirty = true;
         return hip_fail(e, "sd_trace_kernel launch");
     }
-    if (bandTiles != 0) scene->qctl_gen++;
+    if (grid.y != 0) scene->qctl_gen++;
     if (counters) {
         unsigned long long h[16];
         RSD_HIP(hipMemcpyAsync(h, scene->d_counters, sizeof(h), hipMemcpyDeviceToHost, s));
@@ -1401,6 +1434,16 @@ extern "C" rsd_status rsd_sd_trace_band(rsd_scene* scene, const rsd_camera* cam,
         }
     }
     return RSD_OK;
+}
+
+extern "C" rsd_status rsd_sd_trace_band(rsd_scene* scene, const rsd_camera* cam, const rsd_sd_params* p,
+                                        const float* d_linear_z, uint32_t z_w, uint32_t z_h,
+                                        const uint32_t* d_ray_min, const uint32_t* d_ray_max, float* d_sd_out,
+                                        uint32_t sd_w, uint32_t sd_h, uint32_t band_index, uint32_t band_count,
+                                        rsd_counters* counters, rsd_stream stream) {
+    return rsd_sd_trace_band_ex(scene, cam, p, d_linear_z, z_w, z_h, const_cast<uint32_t*>(d_ray_min),
+                                const_cast<uint32_t*>(d_ray_max), d_sd_out, sd_w, sd_h, band_index, band_count, 0u,
+                                counters, stream);
 }
 
 extern "C" rsd_status rsd_sd_trace(rsd_scene* scene, const rsd_camera* cam, const rsd_sd_params* p,

@@ -94,7 +94,9 @@ EXPORTS = ["rsd_abi_version", "rsd_last_error", "rsd_device_open", "rsd_device_c
            "rsd_gbuffer", "rsd_sd_trace", "rsd_svao_clear_intervals", "rsd_svao_pass1", "rsd_svao_pass2",
            "rsd_sd_trace_band", "rsd_svao_pass1_band", "rsd_svao_pass2_band", "rsd_gbuffer_raster",
            "rsd_linearize_depth", "rsd_compress_normals", "rsd_svao_pass2_raytraced", "rsd_svao_pass2_raytraced_band",
-           "rsd_scene_upload_alpha", "rsd_ray_cone_spread"]
+           "rsd_scene_upload_alpha", "rsd_ray_cone_spread", "rsd_sd_trace_band_ex"]
+
+SD_CONSUME_INTERVALS = 1
 
 # every symbol include/rsd_graph.h declares
 GRAPH_EXPORTS = ["rsd_graph_create", "rsd_graph_destroy", "rsd_graph_create_pass", "rsd_graph_add_edge",
@@ -159,6 +161,9 @@ def lib():
         L.rsd_sd_trace_band.restype = st
         L.rsd_sd_trace_band.argtypes = [vp, C.POINTER(Camera), C.POINTER(SDParams), vp, u32, u32, vp, vp, vp, u32,
                                         u32, u32, u32, C.POINTER(Counters), vp]
+        L.rsd_sd_trace_band_ex.restype = st
+        L.rsd_sd_trace_band_ex.argtypes = [vp, C.POINTER(Camera), C.POINTER(SDParams), vp, u32, u32, vp, vp, vp, u32,
+                                           u32, u32, u32, u32, C.POINTER(Counters), vp]
         L.rsd_svao_pass1_band.restype = st
         L.rsd_svao_pass1_band.argtypes = [C.POINTER(Camera), C.POINTER(VAOData), C.POINTER(SVAOParams), vp, vp, u32,
                                           u32, vp, vp, vp, vp, u32, u32, u32, u32, vp]

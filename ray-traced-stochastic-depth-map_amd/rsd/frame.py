@@ -208,13 +208,19 @@ class Renderer:
                                                 _ptr(self.ray_max), self.sd_w, self.sd_h, band[0], band[1],
                                                 self.stream), "rsd_svao_pass1_band")
 
-    def sd_trace(self, counters: bool = False, band=(0, 1)):
+    # the trace can reset the interval maps for the next frame (rsd_sd_trace_band_ex)
+    can_consume_intervals = True
+
+    def sd_trace(self, counters: bool = False, band=(0, 1), consume: bool = False):
+        """consume=True: the trace also resets every interval texel (the next pass 1 needs no
+        clear_intervals); needs RayInterval."""
         cnt = abi.Counters() if counters else None
-        abi.check(abi.lib().rsd_sd_trace_band(self.gscene.h, C.byref(self.cam), C.byref(self.sdp), _ptr(self.depth),
-                                              self.cfg.fb_w, self.cfg.fb_h, _ptr(self.ray_min), _ptr(self.ray_max),
-                                              _ptr(self.sd), self.sd_w, self.sd_h, band[0], band[1],
-                                              C.byref(cnt) if cnt is not None else None, self.stream),
-                  "rsd_sd_trace_band")
+        flags = abi.SD_CONSUME_INTERVALS if consume else 0
+        abi.check(abi.lib().rsd_sd_trace_band_ex(self.gscene.h, C.byref(self.cam), C.byref(self.sdp),
+                                                 _ptr(self.depth), self.cfg.fb_w, self.cfg.fb_h, _ptr(self.ray_min),
+                                                 _ptr(self.ray_max), _ptr(self.sd), self.sd_w, self.sd_h, band[0],
+                                                 band[1], flags, C.byref(cnt) if cnt is not None else None,
+                                                 self.stream), "rsd_sd_trace_band_ex")
         return cnt
 
     def pass2(self, band=(0, 1)):

@@ -37,6 +37,7 @@ class BandFrame:
     def __init__(self, backend, rank: int = 0, world: int = 1, pg=None):
         import torch.distributed as dist
         self.b, self.rank, self.world, self.pg = backend, rank, world, pg
+        self._intervals_clear = False  # set after a trace that consumed (reset) the intervals
         self.dist = dist if world > 1 else None
         self.nccl = world > 1 and dist.get_backend(pg) == "nccl"
         cfg = backend.cfg
@@ -86,7 +87,10 @@ class BandFrame:
         """One AO frame.  sd_events: optional (start, end) torch.cuda.Event pair recorded
         around this rank's SD trace (per-kernel timing in bench.py)."""
         b, band = self.b, (self.rank, self.world)
-        b.clear_intervals()
+        # the previous frame's trace reset the intervals if the backend can fold the clear in
+        consume = getattr(b, "can_consume_intervals", False) and bool(b.cfg.ray_interval)
+        if not (consume and self._intervals_clear):
+            b.clear_intervals()
         b.pass1(band=band)
         if self.world > 1:
             both = getattr(b, "ray_minmax", None)
@@ -101,7 +105,11 @@ class BandFrame:
                 self.dist.all_reduce(b.ray_max, op=self.dist.ReduceOp.MAX, group=self.pg)
         if sd_events:
             sd_events[0].record()
-        b.sd_trace(band=band)
+        if consume:
+            b.sd_trace(band=band, consume=True)
+        else:
+            b.sd_trace(band=band)
+        self._intervals_clear = consume
         if sd_events:
             sd_events[1].record()
         if self.world > 1:

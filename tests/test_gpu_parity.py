@@ -346,3 +346,22 @@ def test_obj_ingest_frame_parity(device, oracle, tmp_path):
     sd, _ = oracle.sd_trace(osc, cam, sdp, z, None, None, r.sd_w, r.sd_h)
     assert bits_equal(g["sd"], sd)
     gs.release()
+
+
+def test_consumed_intervals_frames_match_fresh_frames(device, oracle):
+    """BandFrame folds the interval clear into the trace (RSD_SD_CONSUME_INTERVALS): after
+    a consuming trace the maps are exactly the cleared state, and consecutive frames stay
+    bit-identical to a frame with an explicit clear."""
+    from rsd.shard import BandFrame
+    cfg = small_frame_config(visible=(224, 136), guard=16, divisor=2, N=4)
+    r, osc = renderer("arcade_tiny", cfg, device, oracle)
+    r.gbuffer()
+    r.frame()
+    want = r.numpy()
+    bf = BandFrame(r, 0, 1)
+    for k in range(3):
+        bf.frame()
+        g = r.numpy()
+        assert (g["ray_min"] == 0x7F7FFFFF).all() and (g["ray_max"] == 0).all(), k
+        assert bits_equal(g["sd"], want["sd"]) and np.array_equal(g["ao"], want["ao"]), k
+        assert np.array_equal(g["stencil"], want["stencil"]), k
