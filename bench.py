@@ -200,7 +200,11 @@ def cpu_baseline(r, scene, target_s):
     sys.path.insert(0, str(ROOT / "tests"))
     from helpers import to_oracle
 
+    # one full frame with explicit interval maps (the timed frames consume them, so the maps are
+    # cleared by now): the baseline traces exactly this frame's SD map
+    r.frame()
     g = r.numpy()
+    assert (g["ray_max"] != 0).any(), "the baseline frame has no live SD rays"
     cores = min(os.cpu_count() or 1, 16)
     osc = O.Scene(scene.positions, scene.indices, scene.flags)
     cam, sdp = to_oracle(r.cam, O.Camera), to_oracle(r.sdp, O.SDParams)
