@@ -56,6 +56,7 @@ struct Sample {
     bool isInScreen;
     float su, sv;  // samplePosUV
     float ru, rv;  // rasterSamplePosUV
+    int kx, ky;    // the pixel ru, rv is the centre of
     float visibility, objectSpaceZ;
     f3 ip;  // initialSamplePosV (the Raytraced mode needs its length)
 };
@@ -75,10 +76,21 @@ __device__ __forceinline__ float depth_sample(const SvaoArgs& a, float u, float 
     return tex_bilinear(a.depth, a.W, a.H, u, v, false);  // gTextureSampler: linear, clamp
 }
 
+// The depth at the centre uv of pixel (kx, ky) (Init's uv, getSnappedUV's rasterSamplePosUV).
+// The bilinear filter there resolves to the single texel (kx, ky): uv * size lands within
+// (kx + 0.5) +- size * 2^-22, and an offset below 1/512 rounds the 8-bit weights to 0 (or to
+// 256 of the next texel, tex_bilinear's carry), so for frames up to 4096 px the fetch is
+// direct -- no dependency on the uv arithmetic or the snap-table loads.
+__device__ __forceinline__ float depth_center(const SvaoArgs& a, float u, float v, int kx, int ky) {
+    if (a.W <= 4096 && a.H <= 4096)
+        return a.depth[(size_t)min(max(ky, 0), a.H - 1) * a.W + min(max(kx, 0), a.W - 1)];
+    return depth_sample(a, u, v);
+}
+
 // Common.slang:285-324
 __device__ __forceinline__ bool basic_init(const SvaoArgs& a, float u, float v, Basic& b) {
     const rsd_vao_data& d = a.d;
-    const float z = depth_sample(a, u, v);
+    const float z = depth_center(a, u, v, (int)(u * d.resolution[0]), (int)(v * d.resolution[1]));
     const float rux = (d.radius * a.cam.focalLength) / (a.cam.frameWidth * z);
     const float ruy = (d.radius * a.cam.focalLength) / (a.cam.frameHeight * z);
     const float pa = rux * d.resolution[0], pb = ruy * d.resolution[1];
@@ -153,8 +165,10 @@ __device__ __forceinline__ bool sample_init(const SvaoArgs& a, float u, float v,
     const float cu = saturate(s.su), cv = saturate(s.sv);
     s.isInScreen = (s.su == cu) && (s.sv == cv);
     // getSnappedUV (Common.slang:116-120): (floor(uv * res) + 0.5) / res from the host table
-    s.ru = a.snapU[(int)floorf(cu * d.resolution[0])];
-    s.rv = a.snapV[(int)floorf(cv * d.resolution[1])];
+    s.kx = (int)floorf(cu * d.resolution[0]);
+    s.ky = (int)floorf(cv * d.resolution[1]);
+    s.ru = a.snapU[s.kx];
+    s.rv = a.snapV[s.ky];
     return true;
 }
 
@@ -185,7 +199,7 @@ __device__ __forceinline__ void add_sample(const SvaoArgs& a, const Basic& b, Sa
 
 // Common.slang:492-496
 __device__ __forceinline__ void eval_primary(const SvaoArgs& a, const Basic& b, Sample& s) {
-    const float z = depth_sample(a, s.ru, s.rv);
+    const float z = depth_center(a, s.ru, s.rv, s.kx, s.ky);
     add_sample(a, b, s, uv_to_view(a, s.ru, s.rv, z), true);
 }
 
