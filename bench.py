@@ -12,6 +12,13 @@ N = 4, MAX_COUNT = 8.  Inputs (BVH, G-buffer) are resident in HBM before timing.
   ao_frames_per_s  = frames / timed wall
   sd_kernel_mrays  = SD rays / SD-kernel time (HIP events around the trace launch)
 
+Frames in flight (--frames-in-flight F, default 3 = DXGI's default maximum frame latency):
+frame i runs on HIP stream i % F with its own frame buffers (ao, stencil, interval maps, SD
+map; BVH and G-buffer shared).  Every frame still runs the whole clear -> "AO 1" -> SD trace ->
+"AO 2" chain in order on its stream; frames of different slots overlap, so the latency-bound
+SD trace of one frame (~22 K live rays on 256 CUs) shares the machine with the VALU-bound
+passes of the others.  `sequential` reports the one-frame-in-flight latency of the same frame.
+
 Multi-GPU (torchrun, one rank per GPU): the frame is sharded by screen band (rsd/shard.py).
 Every rank holds the replicated BVH and G-buffer, runs pass 1 on its band of rows, all-
 reduces the ray-interval maps (MIN/MAX), traces its band of SD tile rows, all-gathers the
@@ -45,6 +52,9 @@ def parse():
     ap.add_argument("--config", default="suntemple_1080p_q")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0,
                     help="target wall time of the bounded CPU-oracle sample (0 disables)")
+    ap.add_argument("--frames-in-flight", type=int, default=3,
+                    help="frames in flight: frame i runs on stream i %% F with its own frame buffers "
+                         "(1 = strictly sequential frames)")
     ap.add_argument("--pmc-csv", nargs="*", default=None,
                     help="rocprofv3 --pmc counter_collection.csv file(s) with FETCH_SIZE / WRITE_SIZE for "
                          "roofline.traffic (default: the committed profiles/round1 passes)")
@@ -84,21 +94,29 @@ def main():
         dist.barrier()
 
     from rsd.shard import BandFrame
-    bf = BandFrame(r, rank, world)
+    # frames in flight: F buffer sets (slots) on F streams; frame i runs on slot i % F.  Every
+    # frame does the whole pass 1 -> SD trace -> pass 2 chain; frames of different slots overlap
+    # (the latency-bound SD trace of one frame shares the CUs with another frame's passes)
+    F = max(1, args.frames_in_flight)
+    slots = [BandFrame(r, rank, world)] + [BandFrame(r.frame_slot(), rank, world) for _ in range(F - 1)]
+    streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(F - 1)]
+    for st in streams[1:]:
+        st.wait_stream(streams[0])
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
 
-    def frame(i=None):
-        bf.frame(sd_events=ev[i] if i is not None else None)
+    def frame(i, timed=False):
+        with torch.cuda.stream(streams[i % F]):
+            slots[i % F].frame(sd_events=ev[i] if timed else None)
 
-    for _ in range(args.warmup):
-        frame()
+    for i in range(args.warmup):
+        frame(i)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        frame(i)
+        frame(i, timed=True)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -110,6 +128,19 @@ def main():
         wall = float(t.item())
 
     sd_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+
+    # untimed for `value`: the single-frame latency (one frame in flight, slot 0 only)
+    n_seq = min(args.steps, 20)
+    ev_seq = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n_seq)]
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for i in range(n_seq):
+        slots[0].frame(sd_events=ev_seq[i])
+    torch.cuda.synchronize()
+    seq_ms = (time.perf_counter() - t0) / n_seq * 1e3
+    seq_sd_ms = float(np.mean([a.elapsed_time(b) for a, b in ev_seq]))
     rays = r.sd_rays
     N = cfg.sd_samples
     # B_ray = 16 (linearZ bilinear) + 8 (rayMin+rayMax) + 4N (store) + node bytes + 48 n_tri;
@@ -147,9 +178,13 @@ def main():
         "config": {"workload": args.config, "scene": scene_name, "triangles": scene.triangle_count,
                    "frame_buffer": [cfg.fb_w, cfg.fb_h], "visible": [cfg.visible_w, cfg.visible_h],
                    "sd_map": [r.sd_w, r.sd_h], "sd_samples": N, "max_count": cfg.max_count,
-                   "stoch_map_divisor": cfg.divisor, "parallelism": f"screen-band x{world}"},
+                   "stoch_map_divisor": cfg.divisor, "parallelism": f"screen-band x{world}",
+                   "frames_in_flight": F},
         "ao_frames_per_s": round(frames_per_s, 2),
         "sd_kernel_ms": round(sd_ms, 4),
+        "sequential": {"ms_per_frame": round(seq_ms, 4), "ao_frames_per_s": round(1e3 / seq_ms, 2),
+                       "sd_kernel_ms": round(seq_sd_ms, 4), "frames": n_seq,
+                       "note": "one frame in flight: the frame latency (value counts frames in flight)"},
         "sd_kernel_mrays_per_s": round(rays / (sd_ms * 1e-3) / 1e6, 2),
         "active_rays": int(cnt.rays_active),
         "traversal": {"nodes_per_ray": round(cnt.nodes_visited / rays, 3),

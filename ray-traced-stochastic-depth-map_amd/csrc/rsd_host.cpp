@@ -91,7 +91,6 @@ extern "C" rsd_status rsd_scene_upload(rsd_device* dev, const rsd_scene_desc* de
     s->tri_offset = (uint32_t)(bvh.nodes.size() / 4);
     hipError_t e = hipMalloc(&s->d_nodes, total);
     if (e == hipSuccess) e = hipMalloc(&s->d_counters, 16 * sizeof(unsigned long long));
-    if (e == hipSuccess) e = hipMalloc(&s->d_qctl, 128 * sizeof(uint32_t));
     if (e == hipSuccess) e = hipMemset(s->d_nodes, 0, total);
     if (e == hipSuccess) e = hipMemcpy(s->d_nodes, bvh.nodes.data(), nb, hipMemcpyHostToDevice);
     if (e == hipSuccess && tb)
@@ -100,7 +99,6 @@ extern "C" rsd_status rsd_scene_upload(rsd_device* dev, const rsd_scene_desc* de
         rsd_status st = rsd::hip_fail(e, "rsd_scene_upload");
         (void)hipFree(s->d_nodes);
         (void)hipFree(s->d_counters);
-        (void)hipFree(s->d_qctl);
         delete s;
         return st;
     }
@@ -268,8 +266,7 @@ extern "C" void rsd_scene_release(rsd_scene* s) {
     (void)hipSetDevice(s->dev->hip_device);
     (void)hipFree(s->d_nodes);
     (void)hipFree(s->d_counters);
-    (void)hipFree(s->d_qctl);
-    (void)hipFree(s->d_queue);
+    rsd::release_sd_workspaces(s);
     (void)hipFree(s->d_alpha);
     delete s;
 }

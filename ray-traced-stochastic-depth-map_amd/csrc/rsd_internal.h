@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <string>
+#include <vector>
 
 #include "../../include/rsd.h"
 #include "bvh_build.h"
@@ -24,6 +25,41 @@ struct AlphaData {
 };
 }  // namespace rsd
 
+namespace rsd {
+// Per-frame-size ray terms of the SD setup (ray_table_kernel), keyed by what they depend on
+struct RayTabCache {
+    int w = -1, h = -1, guard = 0;
+    uint32_t jitter = 0;
+    float jx = 0.0f, jy = 0.0f;
+    float camW[3] = {0.0f, 0.0f, 0.0f};
+    int device = -1;
+    float* d = nullptr;
+    size_t cap = 0;
+    bool same(const RayTabCache& k) const {
+        return w == k.w && h == k.h && guard == k.guard && jitter == k.jitter && jx == k.jx && jy == k.jy &&
+               camW[0] == k.camW[0] && camW[1] == k.camW[1] && camW[2] == k.camW[2] && device == k.device;
+    }
+    void setKey(const RayTabCache& k) {
+        w = k.w; h = k.h; guard = k.guard; jitter = k.jitter; jx = k.jx; jy = k.jy;
+        camW[0] = k.camW[0]; camW[1] = k.camW[1]; camW[2] = k.camW[2]; device = k.device;
+    }
+};
+
+// Mutable SD-trace state of one (scene, stream) pair.  Traces of one scene on DIFFERENT
+// streams may run concurrently (frames in flight): each stream owns its queue control,
+// live-ray / key workspace and ray table, so concurrent launches never share scratch.
+struct SdWorkspace {
+    hipStream_t stream = nullptr;
+    uint32_t* qctl = nullptr;      // live-ray queue control {count[32], head[32]} x 2 (double-buffered)
+    uint32_t qctl_gen = 0;         // trace calls so far: buffer qctl_gen % 2 is zero and next in line
+    bool qctl_dirty = true;        // reset both buffers before the next trace (first use, failed launch)
+    void* queue = nullptr;         // live-ray records + K-key slots, grow-only
+    size_t queue_cap = 0;          // bytes
+    RayTabCache raytab;
+};
+void release_sd_workspaces(rsd_scene* s);
+}  // namespace rsd
+
 struct rsd_scene {
     rsd_device* dev = nullptr;
     float4* d_nodes = nullptr;   // one allocation: 8 x float4 per wide node, then
@@ -34,11 +70,7 @@ struct rsd_scene {
     rsd::BvhStats stats;
     uint64_t device_bytes = 0;
     unsigned long long* d_counters = nullptr;  // 8 x u64 scratch for instrumented traces
-    uint32_t* d_qctl = nullptr;    // live-ray queue control {count[32], head[32]} x 2 (double-buffered)
-    uint32_t qctl_gen = 0;         // trace calls so far: buffer qctl_gen % 2 is zero and next in line
-    bool qctl_dirty = true;        // reset both buffers before the next trace (first use, failed launch)
-    void* d_queue = nullptr;       // SD-trace workspace (live-ray records + K-key slots), grow-only
-    size_t queue_cap = 0;          // bytes
+    std::vector<rsd::SdWorkspace*> sd_ws;  // one per stream that traced this scene (few: linear lookup)
     void* d_alpha = nullptr;       // alpha data (rsd_scene_upload_alpha), one allocation
     rsd::AlphaData alpha;          // device pointers into d_alpha
 };

@@ -1157,24 +1157,18 @@ struct LutCache {
 };
 thread_local LutCache g_lut[17];
 
-struct RayTabCache {
-    int w = -1, h = -1, guard = 0;
-    uint32_t jitter = 0;
-    float jx = 0.0f, jy = 0.0f;
-    float camW[3] = {0.0f, 0.0f, 0.0f};
-    int device = -1;
-    float* d = nullptr;
-    size_t cap = 0;
-    bool same(const RayTabCache& k) const {
-        return w == k.w && h == k.h && guard == k.guard && jitter == k.jitter && jx == k.jx && jy == k.jy &&
-               camW[0] == k.camW[0] && camW[1] == k.camW[1] && camW[2] == k.camW[2] && device == k.device;
-    }
-    void setKey(const RayTabCache& k) {
-        w = k.w; h = k.h; guard = k.guard; jitter = k.jitter; jx = k.jx; jy = k.jy;
-        camW[0] = k.camW[0]; camW[1] = k.camW[1]; camW[2] = k.camW[2]; device = k.device;
-    }
-};
-thread_local RayTabCache g_raytab;
+// the SD-trace workspace of (scene, stream); created on the stream's first trace
+rsd_status sd_workspace(rsd_scene* scene, hipStream_t s, SdWorkspace** out) {
+    for (SdWorkspace* w : scene->sd_ws)
+        if (w->stream == s) { *out = w; return RSD_OK; }
+    SdWorkspace* w = new SdWorkspace();
+    w->stream = s;
+    hipError_t e = hipMalloc(&w->qctl, 4 * kQueueParts * sizeof(uint32_t));
+    if (e != hipSuccess) { delete w; return hip_fail(e, "sd workspace"); }
+    scene->sd_ws.push_back(w);
+    *out = w;
+    return RSD_OK;
+}
 
 rsd_status ensure_lut(uint32_t N, const int32_t** idx, const uint32_t** lut) {
     LutCache& c = g_lut[N];
@@ -1319,9 +1313,14 @@ extern "C" rsd_status rsd_sd_trace_band_ex(rsd_scene* scene, const rsd_camera* c
         if (s != RSD_OK) return s;
     }
     hipStream_t s = (hipStream_t)stream;
+    SdWorkspace* ws = nullptr;
+    {
+        rsd_status st = sd_workspace(scene, s, &ws);
+        if (st != RSD_OK) return st;
+    }
     {
         // per-frame-size ray terms (recomputed when the SD map size, guard band or jitter change)
-        RayTabCache& rt = g_raytab;
+        RayTabCache& rt = ws->raytab;
         const RayTabCache key{(int)sd_w, (int)sd_h, p->guard_band, p->jitter, cam->jitterX, cam->jitterY,
                               {cam->W[0], cam->W[1], cam->W[2]}, scene->dev->hip_device};
         const size_t need = (6 * (size_t)sd_w + 6 * (size_t)sd_h + 3) * sizeof(float);
@@ -1358,23 +1357,24 @@ extern "C" rsd_status rsd_sd_trace_band_ex(rsd_scene* scene, const rsd_camera* c
     // split walk (trace -> keys -> resolve) when one chunk of K keys decides every texel
     const bool split = p->implementation != RSD_SD_COVERAGE_MASK && p->max_count <= K;
     const size_t queueBytes = need_q * 32, keyBytes = split ? need_q * K * sizeof(uint2) : 0;
-    if (scene->queue_cap < queueBytes + keyBytes) {
+    if (ws->queue_cap < queueBytes + keyBytes) {
         RSD_HIP(hipStreamSynchronize(s));
-        (void)hipFree(scene->d_queue);
-        scene->d_queue = nullptr;
-        RSD_HIP(hipMalloc(&scene->d_queue, queueBytes + keyBytes));
-        scene->queue_cap = queueBytes + keyBytes;
+        (void)hipFree(ws->queue);
+        ws->queue = nullptr;
+        ws->queue_cap = 0;
+        RSD_HIP(hipMalloc(&ws->queue, queueBytes + keyBytes));
+        ws->queue_cap = queueBytes + keyBytes;
     }
-    float4* queue = reinterpret_cast<float4*>(scene->d_queue);
-    uint2* keys = reinterpret_cast<uint2*>(reinterpret_cast<char*>(scene->d_queue) + queueBytes);
+    float4* queue = reinterpret_cast<float4*>(ws->queue);
+    uint2* keys = reinterpret_cast<uint2*>(reinterpret_cast<char*>(ws->queue) + queueBytes);
     // double-buffered queue control (sd_setup_kernel); both buffers are reset on first use and
     // after a failed launch sequence
-    if (scene->qctl_dirty) {
-        RSD_HIP(hipMemsetAsync(scene->d_qctl, 0, 4 * kQueueParts * sizeof(uint32_t), s));
-        scene->qctl_dirty = false;
+    if (ws->qctl_dirty) {
+        RSD_HIP(hipMemsetAsync(ws->qctl, 0, 4 * kQueueParts * sizeof(uint32_t), s));
+        ws->qctl_dirty = false;
     }
-    uint32_t* qctl = scene->d_qctl + (scene->qctl_gen & 1u) * 2 * kQueueParts;
-    a.qctlNext = scene->d_qctl + ((scene->qctl_gen + 1u) & 1u) * 2 * kQueueParts;
+    uint32_t* qctl = ws->qctl + (ws->qctl_gen & 1u) * 2 * kQueueParts;
+    a.qctlNext = ws->qctl + ((ws->qctl_gen + 1u) & 1u) * 2 * kQueueParts;
     const uint32_t setupBlocks = grid.x * grid.y;
     a.partCap = (setupBlocks + kQueueParts - 1) / kQueueParts * (uint32_t)kBlock;
     // traversal walk: row-parallel (default) unless the tree is too deep for its LDS pool
@@ -1407,10 +1407,10 @@ extern "C" rsd_status rsd_sd_trace_band_ex(rsd_scene* scene, const rsd_camera* c
     else if (K == 8) e = launch_sd_k<8>(a, N, grid, pb, queue, qctl, keys, walk, s);
     else e = launch_sd_k<16>(a, N, grid, pb, queue, qctl, keys, walk, s);
     if (e != hipSuccess) {
-        scene->qctl_dirty = true;
+        ws->qctl_dirty = true;
         return hip_fail(e, "sd_trace_kernel launch");
     }
-    if (grid.y != 0) scene->qctl_gen++;
+    if (grid.y != 0) ws->qctl_gen++;
     if (counters) {
         unsigned long long h[16];
         RSD_HIP(hipMemcpyAsync(h, scene->d_counters, sizeof(h), hipMemcpyDeviceToHost, s));
@@ -1502,3 +1502,15 @@ extern "C" rsd_status rsd_gbuffer_raster(rsd_scene* scene, const rsd_camera* cam
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? RSD_OK : hip_fail(e, "gbuffer_kernel launch");
 }
+
+namespace rsd {
+void release_sd_workspaces(rsd_scene* scene) {
+    for (SdWorkspace* w : scene->sd_ws) {
+        (void)hipFree(w->qctl);
+        (void)hipFree(w->queue);
+        (void)hipFree(w->raytab.d);
+        delete w;
+    }
+    scene->sd_ws.clear();
+}
+}  // namespace rsd

@@ -184,6 +184,22 @@ class Renderer:
         self.ray_min, self.ray_max = self.ray_minmax[0], self.ray_minmax[1]
         self.sd = torch.empty(((N + 3) // 4, self.sd_h, self.sd_w, min(N, 4)), dtype=torch.float32, device=dv)
 
+    def frame_slot(self) -> "Renderer":
+        """Another set of per-frame buffers (ao, stencil, intervals, SD map) over the same scene,
+        camera and G-buffer: the state of one more frame in flight.  Frames of different slots
+        may run concurrently on different streams -- librsd keeps the SD-trace workspace per
+        (scene, stream) -- while frames of one slot stay ordered on its stream."""
+        import copy
+        t = self.torch
+        r = copy.copy(self)
+        r._slot = True
+        r.ao = t.zeros_like(self.ao)
+        r.stencil = t.zeros_like(self.stencil)
+        r.ray_minmax = t.empty_like(self.ray_minmax)
+        r.ray_min, r.ray_max = r.ray_minmax[0], r.ray_minmax[1]
+        r.sd = t.empty_like(self.sd)
+        return r
+
     @property
     def stream(self):
         return C.c_void_p(self.torch.cuda.current_stream().cuda_stream)
@@ -258,4 +274,5 @@ class Renderer:
                     ray_max=self.ray_max.cpu().numpy().view(np.uint32), sd=self.sd.cpu().numpy())
 
     def close(self):
-        self.gscene.release()
+        if not getattr(self, "_slot", False):  # a frame slot shares the scene of its renderer
+            self.gscene.release()

@@ -54,3 +54,42 @@ def test_fullsize_config_parity(oracle, config):
     gv = slice(cfg.guard_band, cfg.fb_h - cfg.guard_band), slice(cfg.guard_band, cfg.fb_w - cfg.guard_band)
     assert np.array_equal(g["ao"][gv], ao[gv])
     r.close()
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("config,flight", [("suntemple_1080p_q", 2), ("suntemple_1080p_q", 3),
+                                           ("emerald_4k_q", 2)])
+def test_frames_in_flight_equal_sequential(config, flight):
+    """bench.py's frames in flight: F frame slots on F streams, frames overlapping across slots
+    (each slot consuming its own interval maps), give the sequential frame bit-for-bit in every
+    slot -- librsd's SD-trace scratch is per (scene, stream), so concurrent traces of one scene
+    never share it.  The sequential frame itself is pinned against the oracle above / by bench.py."""
+    import torch
+    from rsd.frame import CONFIGS, FrameConfig, Renderer
+    from rsd.scenes import make_scene
+    from rsd.shard import BandFrame
+    kw, scene_name = CONFIGS[config]
+    r = Renderer(make_scene(scene_name), FrameConfig(**kw))
+    r.gbuffer()
+    r.frame()
+    ref = r.numpy()
+    slots = [r] + [r.frame_slot() for _ in range(flight - 1)]
+    for s in slots:
+        s.sd.zero_()
+        s.ao.zero_()
+    frames = [BandFrame(s) for s in slots]
+    streams = [torch.cuda.Stream() for _ in slots]
+    for st in streams:
+        st.wait_stream(torch.cuda.current_stream())
+    for i in range(4 * flight):
+        with torch.cuda.stream(streams[i % flight]):
+            frames[i % flight].frame()
+    torch.cuda.synchronize()
+    for k, s in enumerate(slots):
+        g = s.numpy()
+        for key in ("ao", "stencil"):
+            assert np.array_equal(g[key], ref[key]), (k, key)
+        assert np.array_equal(g["sd"].view(np.uint32), ref["sd"].view(np.uint32)), k
+        # the last trace of every slot consumed (reset) its intervals for the next frame
+        assert (g["ray_max"] == 0).all() and (g["ray_min"] == np.uint32(0x7F7FFFFF)).all(), k
+    r.close()
