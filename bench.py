@@ -195,6 +195,9 @@ def main():
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "kernel": "rsd_sd_trace = sd_setup_kernel + sd_trace_row_kernel (+ sd_resolve_row_kernel)",
                      "alg_bytes_per_launch": int(alg_bytes),
+                     "achieved_sequential": round(alg_bytes / (seq_sd_ms * 1e-3) / 1e9, 1),
+                     "note": "achieved uses the trace's duration with frames in flight (it shares the CUs); "
+                             "achieved_sequential the one-frame-in-flight duration",
                      "traffic_source": ", ".join(str(Path(p).relative_to(ROOT)) if Path(p).is_relative_to(ROOT)
                                                  else p for p in pmc if Path(p).exists()) or None},
         "cpu_baseline": cpu,

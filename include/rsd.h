@@ -14,7 +14,9 @@
  *   - the caller owns every d_* buffer (device memory);
  *   - compute entry points are asynchronous and ordered on the given stream
  *     (rsd_stream = hipStream_t; NULL = the legacy default stream);
- *   - one rsd_device per GPU per host thread; scenes are bound to a device.
+ *   - one rsd_device per GPU per host thread; scenes are bound to a device;
+ *   - SD traces of one scene may run concurrently on DIFFERENT streams (frames in flight):
+ *     librsd keeps the trace's scratch per (scene, stream); calls on one stream are ordered.
  */
 #ifndef RSD_H
 #define RSD_H
