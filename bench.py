@@ -19,11 +19,17 @@ map; BVH and G-buffer shared).  Every frame still runs the whole clear -> "AO 1"
 SD trace of one frame (~22 K live rays on 256 CUs) shares the machine with the VALU-bound
 passes of the others.  `sequential` reports the one-frame-in-flight latency of the same frame.
 
-Multi-GPU (torchrun, one rank per GPU): the frame is sharded by screen band (rsd/shard.py).
-Every rank holds the replicated BVH and G-buffer, runs pass 1 on its band of rows, all-
-reduces the ray-interval maps (MIN/MAX), traces its band of SD tile rows, all-gathers the
-SD map, runs pass 2 on its band and all-gathers the AO image (RCCL over xGMI).  Strong
-scaling: the whole job renders the same frame size whatever N is.
+Multi-GPU (torchrun, one rank per GPU), two sharding modes (--shard):
+  frame (default): frames are the independent units -- every rank renders whole frames of the
+    configs[1] size (its own frame stream, BVH + G-buffer replicated), no data-path
+    collective; the barrier and max-over-ranks wall bracket the timed region.  Weak scaling:
+    value = world * K frames * rays / wall.
+  band: one frame sharded by screen band (rsd/shard.py, the north_star's tile split).  Every
+    rank runs pass 1 on its band of rows, all-reduces the ray-interval maps (MIN/MAX),
+    traces its band of SD tile rows, all-gathers the SD map, runs pass 2 on its band and
+    all-gathers the AO image (RCCL over xGMI).  Strong scaling: the whole job renders the
+    same frame whatever N is; at 1080p/4 the three collectives per frame outweigh the
+    per-rank compute, so this is the mode for large frames (4K, full-res SD).
 """
 from __future__ import annotations
 
@@ -55,6 +61,9 @@ def parse():
     ap.add_argument("--frames-in-flight", type=int, default=3,
                     help="frames in flight: frame i runs on stream i %% F with its own frame buffers "
                          "(1 = strictly sequential frames)")
+    ap.add_argument("--shard", choices=("frame", "band"), default="frame",
+                    help="N > 1: frame = every rank renders whole frames (weak scaling, no per-frame "
+                         "collective); band = each frame split by screen band + RCCL exchanges (strong)")
     ap.add_argument("--pmc-csv", nargs="*", default=None,
                     help="rocprofv3 --pmc counter_collection.csv file(s) with FETCH_SIZE / WRITE_SIZE for "
                          "roofline.traffic (default: the committed profiles/round1 passes)")
@@ -75,8 +84,16 @@ def main():
     dist = None
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        # RSD_BENCH_BACKEND=gloo: rehearsal of the N > 1 code paths with several ranks on one GPU
+        # (RCCL needs one GPU per rank); production runs use nccl = RCCL with LOCAL_RANK = GPU
+        backend = os.environ.get("RSD_BENCH_BACKEND", "nccl")
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            local = local % torch.cuda.device_count()
+            torch.cuda.set_device(local)
+            dist.init_process_group(backend)
 
     kw, scene_name = CONFIGS[args.config]
     cfg = FrameConfig(**kw)
@@ -98,7 +115,9 @@ def main():
     # frame does the whole pass 1 -> SD trace -> pass 2 chain; frames of different slots overlap
     # (the latency-bound SD trace of one frame shares the CUs with another frame's passes)
     F = max(1, args.frames_in_flight)
-    slots = [BandFrame(r, rank, world)] + [BandFrame(r.frame_slot(), rank, world) for _ in range(F - 1)]
+    # band: this rank's screen band of every frame; frame: whole frames on every rank
+    bw = (rank, world) if args.shard == "band" else (0, 1)
+    slots = [BandFrame(r, *bw)] + [BandFrame(r.frame_slot(), *bw) for _ in range(F - 1)]
     streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(F - 1)]
     for st in streams[1:]:
         st.wait_stream(streams[0])
@@ -160,7 +179,9 @@ def main():
     if args.cpu_baseline_seconds > 0 and world == 1:
         cpu = cpu_baseline(r, scene, args.cpu_baseline_seconds)
 
-    frames_per_s = args.steps / wall
+    # whole job: frame mode renders `steps` whole frames on every rank, band mode `steps` frames in all
+    frames_total = args.steps * (world if args.shard == "frame" else 1)
+    frames_per_s = frames_total / wall
     value = rays * frames_per_s / 1e6 * 1.0
     line = {
         "metric": "Mrays/s + AO frames/s, 1080p 1/4-res Ray-SD, 1/2/4/8 MI355X",
@@ -171,16 +192,18 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(wall / args.steps * 1e3, 4),
         "higher_is_better": True,
-        "scaling": "strong",
+        "scaling": "strong" if args.shard == "band" and world > 1 else "weak",
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic (seeded procedural stand-in scene; no reference assets in the container)",
         "config": {"workload": args.config, "scene": scene_name, "triangles": scene.triangle_count,
                    "frame_buffer": [cfg.fb_w, cfg.fb_h], "visible": [cfg.visible_w, cfg.visible_h],
                    "sd_map": [r.sd_w, r.sd_h], "sd_samples": N, "max_count": cfg.max_count,
-                   "stoch_map_divisor": cfg.divisor, "parallelism": f"screen-band x{world}",
+                   "stoch_map_divisor": cfg.divisor,
+                   "parallelism": f"screen-band x{world}" if args.shard == "band" else f"frame-parallel x{world}",
                    "frames_in_flight": F},
         "ao_frames_per_s": round(frames_per_s, 2),
+        "frames_total": frames_total,
         "sd_kernel_ms": round(sd_ms, 4),
         "sequential": {"ms_per_frame": round(seq_ms, 4), "ao_frames_per_s": round(1e3 / seq_ms, 2),
                        "sd_kernel_ms": round(seq_sd_ms, 4), "frames": n_seq,
