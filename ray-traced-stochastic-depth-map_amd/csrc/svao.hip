@@ -56,7 +56,7 @@ __global__ void __launch_bounds__(256) svao_pass1_kernel(SvaoArgs a) {
             bool ssrAbove;
             if (!sample_init(a, u, v, b, i, s, ssrAbove)) continue;
             if (fabsf(u - s.ru) < d.invResolution[0] * 0.9f && fabsf(v - s.rv) < d.invResolution[1] * 0.9f) {
-                ao += (s.sphereStart - s.sphereEnd) / s.pdf;  // isSamePixel
+                ao += div_pdf(s.sphereStart - s.sphereEnd, s);  // isSamePixel
                 continue;
             }
             // SVAORaster.ps.slang:62-66: Raytraced mode with TRACE_OUT_OF_SCREEN (SVAO.h:104)
@@ -142,14 +142,14 @@ __device__ __forceinline__ void svao_pass2_dir(const SvaoArgs& a, const Basic& b
         const float y = hmax(s.sphereStart - hmax(s.sphereEnd, oz), 0.0f);
         const float x = oz - (1.0f + d.thickness) * b.radius;
         if (x > 0.0f) {
-            const float halo = saturate(x / s.sphereStart) * (s.sphereStart - s.sphereEnd) / s.pdf;
-            s.visibility = hmin(s.visibility, y / s.pdf + halo);
+            const float halo = div_pdf(halo_ratio(x, s) * (s.sphereStart - s.sphereEnd), s);
+            s.visibility = hmin(s.visibility, div_pdf(y, s) + halo);
         } else {
             ymin = hmin(ymin, y);
             plain = true;
         }
     }
-    if (plain) s.visibility = hmin(s.visibility, ymin / s.pdf);
+    if (plain) s.visibility = hmin(s.visibility, div_pdf(ymin, s));
     r = s.visibility;
 }
 

@@ -21,6 +21,10 @@ struct SvaoConsts {
     // (every pixel whose screen radius is not clamped to ssMaxRadius)
     float dirRadius[8], dirDx[8], dirDy[8], dirHeight[8];
     float ssrMin2;  // smallest float x with sqrtf(x) > ssRadiusCutoff: sqrtf(x) > c <=> x >= ssrMin2
+    // RN(1 / pdf_i) and RN(1 / sphereHeight_i) of those terms (div_rcp); bit i of fastDiv set when
+    // both divisors of direction i lie in [2^-30, 2^30]
+    float rcpPdf[8], rcpHeight[8];
+    uint32_t fastDiv;
 };
 
 struct SvaoArgs {
@@ -59,7 +63,37 @@ struct Sample {
     int kx, ky;    // the pixel ru, rv is the centre of
     float visibility, objectSpaceZ;
     f3 ip;  // initialSamplePosV (the Raytraced mode needs its length)
+    bool fast;             // the host reciprocals below apply (div_rcp)
+    float yPdf, yHeight;   // RN(1 / pdf), RN(1 / sphereStart)
 };
+
+// RN(a / b) for b > 0 given y = RN(1 / b), in five operations instead of the IEEE division's
+// eleven (v_div_scale x2, v_rcp, 6 fma/mul, v_div_fmas, v_div_fixup).  q0 = RN(a y) is within
+// 1.5 ulp of a / b; one residual step (r0 = a - b q0 exact by FMA) brings q1 within 1 ulp; then
+// with r1 = a - b q1 (exact) Markstein's theorem (y within 1/2 ulp of 1/b, q1 within 1 ulp of
+// a / b) makes RN(q1 + r1 y) = RN(a / b).  Preconditions, which every caller's operands meet:
+// no underflow / overflow -- b in [2^-30, 2^30] (host-checked, SvaoConsts::fastDiv) and a = 0
+// or |a| in [2^-60, 2^31] (the SVAO visibility numerators, see the callers).  a = +0 gives +0.
+__device__ __forceinline__ float div_rcp(float a, float b, float y) {
+    const float q0 = a * y;
+    const float r0 = __builtin_fmaf(-q0, b, a);
+    const float q1 = __builtin_fmaf(r0, y, q0);
+    const float r1 = __builtin_fmaf(-q1, b, a);
+    return __builtin_fmaf(r1, y, q1);
+}
+
+// n / pdf for n = 0 or n in (0, 2 * sphereHeight]: max(ss - max(se, oz), 0) (>= ulp(ss) / 2 when
+// non-zero), ss - se (> 0.2 h after the validity test), saturate(x / ss) * (ss - se)
+__device__ __forceinline__ float div_pdf(float n, const Sample& s) {
+    return s.fast ? div_rcp(n, s.pdf, s.yPdf) : n / s.pdf;
+}
+
+// saturate(x / sphereStart) for x > 0 (calcHaloVisibility): x >= ss gives 1 exactly (x / ss >= 1
+// rounds to >= 1); 0 < x < ss is oz - (1 + thickness) r > 0, at least ulp(r) / 2
+__device__ __forceinline__ float halo_ratio(float x, const Sample& s) {
+    if (s.fast) return x >= s.sphereStart ? 1.0f : saturate(div_rcp(x, s.sphereStart, s.yHeight));
+    return saturate(x / s.sphereStart);
+}
 
 __device__ __forceinline__ f3 uv_to_view(const SvaoArgs& a, float u, float v, float z) {
     const float ndcx = u * 2.0f - 1.0f, ndcy = (1.0f - v) * 2.0f - 1.0f;
@@ -139,11 +173,15 @@ __device__ __forceinline__ bool sample_init(const SvaoArgs& a, float u, float v,
                                             bool& ssrAbove) {
     const rsd_vao_data& d = a.d;
     float radius, dx, dy, sphereHeight;
+    s.fast = false;
     if (b.radius == d.radius) {  // the host-evaluated terms (same operations, same bits)
         radius = a.k.dirRadius[i];
         dx = a.k.dirDx[i];
         dy = a.k.dirDy[i];
         sphereHeight = a.k.dirHeight[i];
+        s.fast = (a.k.fastDiv >> i) & 1u;
+        s.yPdf = a.k.rcpPdf[i];
+        s.yHeight = a.k.rcpHeight[i];
     } else {
         radius = a.k.sampleRadius[i] * b.radius;
         dx = radius * a.k.sinDir[i];
@@ -189,11 +227,19 @@ __device__ __forceinline__ float calc_visibility(const rsd_vao_data& d, float oz
     return sphere + halo;
 }
 
+// calc_visibility of a Sample (same bits; divisions by its pdf / sphereStart via div_rcp)
+__device__ __forceinline__ float sample_visibility(const rsd_vao_data& d, float oz, const Sample& s, float radius) {
+    const float sphere = div_pdf(hmax(s.sphereStart - hmax(s.sphereEnd, oz), 0.0f), s);
+    const float x = oz - (1.0f + d.thickness) * radius;
+    const float halo = x > 0.0f ? div_pdf(halo_ratio(x, s) * (s.sphereStart - s.sphereEnd), s) : 0.0f;
+    return sphere + halo;
+}
+
 // Common.slang:463-483
 __device__ __forceinline__ void add_sample(const SvaoArgs& a, const Basic& b, Sample& s, f3 spV, bool init) {
     const float oz = dot(spV - b.posV, b.normal);
     s.objectSpaceZ = init ? oz : hmin(s.objectSpaceZ, oz);
-    const float vis = calc_visibility(a.d, oz, s.sphereStart, s.sphereEnd, s.pdf, b.radius);
+    const float vis = sample_visibility(a.d, oz, s, b.radius);
     s.visibility = init ? vis : hmin(s.visibility, vis);
 }
 
@@ -245,6 +291,16 @@ inline void fill_consts(SvaoConsts& k, const rsd_vao_data& d) {
     while (x > 0.0f && std::sqrt(std::nextafter(x, 0.0f)) > c) x = std::nextafter(x, 0.0f);
     while (!(std::sqrt(x) > c)) x = std::nextafter(x, INFINITY);
     k.ssrMin2 = x;
+    // div_rcp reciprocals: RN(RN64(1 / b)) = RN(1 / b) (double rounding is innocuous for a
+    // quotient when 53 >= 2 * 24 + 2)
+    k.fastDiv = 0u;
+    for (int i = 0; i < 8; ++i) {
+        const float pdf = 2.0f * k.dirHeight[i], h = k.dirHeight[i];
+        k.rcpPdf[i] = (float)(1.0 / (double)pdf);
+        k.rcpHeight[i] = (float)(1.0 / (double)h);
+        const bool ok = h >= 0x1p-30f && pdf <= 0x1p30f;
+        if (ok) k.fastDiv |= 1u << i;
+    }
 }
 
 // getSnappedUV tables for a frame size (device copies cached per thread, grow-only)
