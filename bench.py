@@ -12,12 +12,15 @@ N = 4, MAX_COUNT = 8.  Inputs (BVH, G-buffer) are resident in HBM before timing.
   ao_frames_per_s  = frames / timed wall
   sd_kernel_mrays  = SD rays / SD-kernel time (HIP events around the trace launch)
 
-Frames in flight (--frames-in-flight F, default 3 = DXGI's default maximum frame latency):
+Frames in flight (--frames-in-flight F, default 4, the measured optimum of F = 1..6):
 frame i runs on HIP stream i % F with its own frame buffers (ao, stencil, interval maps, SD
 map; BVH and G-buffer shared).  Every frame still runs the whole clear -> "AO 1" -> SD trace ->
 "AO 2" chain in order on its stream; frames of different slots overlap, so the latency-bound
 SD trace of one frame (~22 K live rays on 256 CUs) shares the machine with the VALU-bound
-passes of the others.  `sequential` reports the one-frame-in-flight latency of the same frame.
+passes of the others.  Overlapping frames trace with librsd's work-efficient walk
+(RSD_SD_THROUGHPUT: 4 lanes per ray) instead of the latency-optimised row walk (8 lanes per ray):
+the row walk's idle lanes would be VALU time taken from the other frames.  `sequential` reports the
+one-frame-in-flight latency of the same frame (row walk).
 
 Multi-GPU (torchrun, one rank per GPU), two sharding modes (--shard):
   frame (default): frames are the independent units -- every rank renders whole frames of the
@@ -53,12 +56,12 @@ SD_KERNELS = ("sd_setup_kernel", "sd_trace_row_kernel", "sd_resolve_row_kernel",
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", default="suntemple_1080p_q")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0,
                     help="target wall time of the bounded CPU-oracle sample (0 disables)")
-    ap.add_argument("--frames-in-flight", type=int, default=3,
+    ap.add_argument("--frames-in-flight", type=int, default=4,
                     help="frames in flight: frame i runs on stream i %% F with its own frame buffers "
                          "(1 = strictly sequential frames)")
     ap.add_argument("--shard", choices=("frame", "band"), default="frame",
@@ -105,7 +108,8 @@ def main():
     # instrumented full-frame trace (not timed): traversal counters for the roofline bytes
     r.clear_intervals()
     r.pass1()
-    cnt = r.sd_trace(counters=True)
+    # counters of the walk the timed frames use (frames in flight: RSD_SD_THROUGHPUT)
+    cnt = r.sd_trace(counters=True, throughput=args.frames_in_flight > 1)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -117,7 +121,9 @@ def main():
     F = max(1, args.frames_in_flight)
     # band: this rank's screen band of every frame; frame: whole frames on every rank
     bw = (rank, world) if args.shard == "band" else (0, 1)
-    slots = [BandFrame(r, *bw)] + [BandFrame(r.frame_slot(), *bw) for _ in range(F - 1)]
+    # with frames overlapping, the trace uses librsd's work-efficient walk (RSD_SD_THROUGHPUT)
+    slots = [BandFrame(r, *bw, throughput=F > 1)] + [BandFrame(r.frame_slot(), *bw, throughput=True)
+                                                     for _ in range(F - 1)]
     streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(F - 1)]
     for st in streams[1:]:
         st.wait_stream(streams[0])
@@ -150,13 +156,14 @@ def main():
 
     # untimed for `value`: the single-frame latency (one frame in flight, slot 0 only)
     n_seq = min(args.steps, 20)
+    seq = BandFrame(r, *bw)  # latency-optimised trace walk (no frames overlap)
     ev_seq = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n_seq)]
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     t0 = time.perf_counter()
     for i in range(n_seq):
-        slots[0].frame(sd_events=ev_seq[i])
+        seq.frame(sd_events=ev_seq[i])
     torch.cuda.synchronize()
     seq_ms = (time.perf_counter() - t0) / n_seq * 1e3
     seq_sd_ms = float(np.mean([a.elapsed_time(b) for a, b in ev_seq]))
@@ -216,7 +223,8 @@ def main():
                       "tris_per_active_ray": round(cnt.tris_tested / max(cnt.rays_active, 1), 2)},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "kernel": "rsd_sd_trace = sd_setup_kernel + sd_trace_row_kernel (+ sd_resolve_row_kernel)",
+                     "kernel": ("rsd_sd_trace = sd_setup_kernel + sd_trace_queue_kernel (frames in flight: RSD_SD_THROUGHPUT)"
+                                if F > 1 else "rsd_sd_trace = sd_setup_kernel + sd_trace_row_kernel + sd_resolve_row_kernel"),
                      "alg_bytes_per_launch": int(alg_bytes),
                      "achieved_sequential": round(alg_bytes / (seq_sd_ms * 1e-3) / 1e9, 1),
                      "note": "achieved uses the trace's duration with frames in flight (it shares the CUs); "

@@ -1210,7 +1210,8 @@ extern "C" rsd_status rsd_sd_trace_band_ex(rsd_scene* scene, const rsd_camera* c
                                            uint32_t band_index, uint32_t band_count, uint32_t flags,
                                            rsd_counters* counters, rsd_stream stream) {
     const bool consume = (flags & RSD_SD_CONSUME_INTERVALS) != 0u;
-    if (flags & ~RSD_SD_CONSUME_INTERVALS) {
+    const bool throughput = (flags & RSD_SD_THROUGHPUT) != 0u;
+    if (flags & ~(RSD_SD_CONSUME_INTERVALS | RSD_SD_THROUGHPUT)) {
         set_error("rsd_sd_trace_band_ex: unknown flag");
         return RSD_ERR_INVALID_ARG;
     }
@@ -1389,8 +1390,11 @@ extern "C" rsd_status rsd_sd_trace_band_ex(rsd_scene* scene, const rsd_camera* c
     // (rsd_sd_trace, row vs quad: 1080p/4 0.43 M texels 92 vs 133 us; 4K/4 1.0 M texels 443 vs
     // 327 us; 1080p full 6.9 M texels 688 vs 294 us -- DESIGN.md section 4)
     const uint64_t bandTexels = (uint64_t)sd_w * sd_h / band_count;
+    // RSD_SD_THROUGHPUT (frames in flight): the row walk's spare lanes are VALU time taken from
+    // the overlapping frames, so the quad walk wins there (1080p/4, 4 frames in flight: 108 vs
+    // 118 us per frame; one frame alone: 245 vs 197 us -- DESIGN.md section 4)
     const bool rowWalk = a.poolSoft >= 16 && walkName != "quad" &&
-                         (walkName == "fused" || walkName == "split" || bandTexels <= 600000u);
+                         (walkName == "fused" || walkName == "split" || (bandTexels <= 600000u && !throughput));
     // default: the split row walk (trace -> keys -> resolve) where one chunk of K keys decides
     // every texel, else the fused row walk; RSD_TRACE_WALK=fused|quad for A/B runs
     const int walk = !rowWalk ? 0 : (split && walkName != "fused") ? 2 : 1;

@@ -97,6 +97,7 @@ EXPORTS = ["rsd_abi_version", "rsd_last_error", "rsd_device_open", "rsd_device_c
            "rsd_scene_upload_alpha", "rsd_ray_cone_spread", "rsd_sd_trace_band_ex"]
 
 SD_CONSUME_INTERVALS = 1
+SD_THROUGHPUT = 2  # frames in flight: the work-efficient traversal (rsd.h RSD_SD_THROUGHPUT)
 
 # every symbol include/rsd_graph.h declares
 GRAPH_EXPORTS = ["rsd_graph_create", "rsd_graph_destroy", "rsd_graph_create_pass", "rsd_graph_add_edge",

@@ -227,11 +227,12 @@ class Renderer:
     # the trace can reset the interval maps for the next frame (rsd_sd_trace_band_ex)
     can_consume_intervals = True
 
-    def sd_trace(self, counters: bool = False, band=(0, 1), consume: bool = False):
+    def sd_trace(self, counters: bool = False, band=(0, 1), consume: bool = False, throughput: bool = False):
         """consume=True: the trace also resets every interval texel (the next pass 1 needs no
-        clear_intervals); needs RayInterval."""
+        clear_intervals); needs RayInterval.  throughput=True: the trace overlaps other frames
+        (RSD_SD_THROUGHPUT: the work-efficient traversal; same bits)."""
         cnt = abi.Counters() if counters else None
-        flags = abi.SD_CONSUME_INTERVALS if consume else 0
+        flags = (abi.SD_CONSUME_INTERVALS if consume else 0) | (abi.SD_THROUGHPUT if throughput else 0)
         abi.check(abi.lib().rsd_sd_trace_band_ex(self.gscene.h, C.byref(self.cam), C.byref(self.sdp),
                                                  _ptr(self.depth), self.cfg.fb_w, self.cfg.fb_h, _ptr(self.ray_min),
                                                  _ptr(self.ray_max), _ptr(self.sd), self.sd_w, self.sd_h, band[0],

@@ -34,9 +34,12 @@ class BandFrame:
     tensors ray_min, ray_max (int32 [sdH, sdW]), sd (float32 [layers, sdH, sdW, ch]),
     ao and stencil (uint8 [H, W]), plus cfg (fb_w, fb_h, guard_band) and sd_h."""
 
-    def __init__(self, backend, rank: int = 0, world: int = 1, pg=None):
+    def __init__(self, backend, rank: int = 0, world: int = 1, pg=None, throughput: bool = False):
+        """throughput=True: this frame overlaps other frames in flight; a backend that supports it
+        (librsd: RSD_SD_THROUGHPUT) then traces with its work-efficient walk."""
         import torch.distributed as dist
         self.b, self.rank, self.world, self.pg = backend, rank, world, pg
+        self.trace_kw = {"throughput": True} if throughput and getattr(backend, "can_consume_intervals", False) else {}
         self._intervals_clear = False  # set after a trace that consumed (reset) the intervals
         self.dist = dist if world > 1 else None
         self.nccl = world > 1 and dist.get_backend(pg) == "nccl"
@@ -106,9 +109,9 @@ class BandFrame:
         if sd_events:
             sd_events[0].record()
         if consume:
-            b.sd_trace(band=band, consume=True)
+            b.sd_trace(band=band, consume=True, **self.trace_kw)
         else:
-            b.sd_trace(band=band)
+            b.sd_trace(band=band, **self.trace_kw)
         self._intervals_clear = consume
         if sd_events:
             sd_events[1].record()

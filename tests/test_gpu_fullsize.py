@@ -77,7 +77,7 @@ def test_frames_in_flight_equal_sequential(config, flight):
     for s in slots:
         s.sd.zero_()
         s.ao.zero_()
-    frames = [BandFrame(s) for s in slots]
+    frames = [BandFrame(s, throughput=flight != 2) for s in slots]  # both trace walks
     streams = [torch.cuda.Stream() for _ in slots]
     for st in streams:
         st.wait_stream(torch.cuda.current_stream())
