@@ -111,3 +111,50 @@ def test_band_rows_partition():
         rows = [band_rows(1144, 32, 64, r, world) for r in range(world)]
         allr = torch.cat(rows).sort().values
         assert torch.equal(allr, torch.arange(64, 64 + 1144))
+
+
+class _RecordingBackend:
+    """Minimal BandFrame backend that records the trace calls (no compute)."""
+
+    def __init__(self, capable):
+        from types import SimpleNamespace
+        self.cfg = SimpleNamespace(fb_w=64, fb_h=48, guard_band=8, ray_interval=1)
+        self.sd_h = 16
+        self.sd = torch.zeros((1, 16, 24, 4))
+        self.ao = torch.zeros((48, 64), dtype=torch.uint8)
+        self.calls = []
+        if capable:
+            self.can_consume_intervals = True
+
+    def clear_intervals(self):
+        self.calls.append(("clear",))
+
+    def pass1(self, band=(0, 1)):
+        self.calls.append(("pass1", band))
+
+    def sd_trace(self, band=(0, 1), **kw):
+        self.calls.append(("trace", band, tuple(sorted(kw.items()))))
+
+    def pass2(self, band=(0, 1)):
+        self.calls.append(("pass2", band))
+
+
+def test_band_frame_throughput_and_consume_plumbing():
+    """bench.py's frames in flight: a librsd-like backend gets consume + throughput on its trace
+    (the first frame clears the intervals, later frames rely on the consuming trace); a backend
+    without those capabilities (the oracle) gets neither."""
+    from rsd.shard import BandFrame
+    cap = _RecordingBackend(capable=True)
+    bf = BandFrame(cap, throughput=True)
+    bf.frame()
+    bf.frame()
+    assert cap.calls == [("clear",), ("pass1", (0, 1)), ("trace", (0, 1), (("consume", True), ("throughput", True))),
+                         ("pass2", (0, 1)),
+                         ("pass1", (0, 1)), ("trace", (0, 1), (("consume", True), ("throughput", True))),
+                         ("pass2", (0, 1))]
+    plain = _RecordingBackend(capable=False)
+    bf = BandFrame(plain, throughput=True)
+    bf.frame()
+    bf.frame()
+    assert [c for c in plain.calls if c[0] == "trace"] == [("trace", (0, 1), ())] * 2
+    assert plain.calls.count(("clear",)) == 2

@@ -26,10 +26,6 @@ def chain_pass2():
     b.pass2()
 
 
-def chain_trace_only_kernel():  # the trace without pass 2
-    b.sd_trace()
-
-
 def run(label, work, reps_b=6, n=10):
     ts = []
     for _ in range(n):
@@ -55,11 +51,8 @@ def b_pass1():
     b.pass1()
 
 
-def b_resolve_chain():
-    b.sd_trace()
-
-
 run("alone", None)
 run("with B sd_trace", chain_trace)
+run("with B sd_trace quad", lambda: b.sd_trace(throughput=True))
 run("with B pass2", chain_pass2)
 run("with B pass1", b_pass1, reps_b=1)
