@@ -1158,9 +1158,16 @@ struct LutCache {
 thread_local LutCache g_lut[17];
 
 // the SD-trace workspace of (scene, stream); created on the stream's first trace
+constexpr size_t kMaxWorkspaces = 16;
 rsd_status sd_workspace(rsd_scene* scene, hipStream_t s, SdWorkspace** out) {
     for (SdWorkspace* w : scene->sd_ws)
         if (w->stream == s) { *out = w; return RSD_OK; }
+    if (scene->sd_ws.size() >= kMaxWorkspaces) {
+        // a caller cycling through many transient streams: drain the device (no trace of this
+        // scene can still be using a workspace) and start over instead of growing without bound
+        RSD_HIP(hipDeviceSynchronize());
+        release_sd_workspaces(scene);
+    }
     SdWorkspace* w = new SdWorkspace();
     w->stream = s;
     hipError_t e = hipMalloc(&w->qctl, 4 * kQueueParts * sizeof(uint32_t));

@@ -365,3 +365,24 @@ def test_consumed_intervals_frames_match_fresh_frames(device, oracle):
         assert (g["ray_min"] == 0x7F7FFFFF).all() and (g["ray_max"] == 0).all(), k
         assert bits_equal(g["sd"], want["sd"]) and np.array_equal(g["ao"], want["ao"]), k
         assert np.array_equal(g["stencil"], want["stencil"]), k
+
+
+def test_sd_trace_on_many_streams(device, oracle):
+    """librsd keeps the SD-trace scratch per (scene, stream) and recycles it past 16 streams:
+    traces on 20 fresh streams (both walks) all give the default-stream SD map."""
+    import torch
+    cfg = small_frame_config(visible=(160, 96), guard=16, divisor=2, N=4)
+    r, _ = renderer("arcade_tiny", cfg, device, oracle)
+    r.gbuffer()
+    r.clear_intervals()
+    r.pass1()
+    r.sd_trace()
+    ref = r.numpy()["sd"].view(np.uint32).copy()
+    for k in range(20):
+        st = torch.cuda.Stream()
+        st.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(st):
+            r.sd.zero_()
+            r.sd_trace(throughput=bool(k % 2))
+        torch.cuda.current_stream().wait_stream(st)
+        assert np.array_equal(r.numpy()["sd"].view(np.uint32), ref), k
