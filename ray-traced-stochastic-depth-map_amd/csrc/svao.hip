@@ -36,6 +36,9 @@ __global__ void clear_intervals_kernel(uint32_t* rmin, uint32_t* rmax, uint32_t 
 }
 
 // SVAORaster.ps.slang:29-122, [numthreads(16,16,1)] with the 2x2 group interleave
+#ifndef RSD_P1_UNROLL
+#define RSD_P1_UNROLL 1
+#endif
 __global__ void __launch_bounds__(256) svao_pass1_kernel(SvaoArgs a) {
     const uint32_t bx = blockIdx.x, by = blockIdx.y;
     const uint32_t ox = (bx / 2u) * 32u + 2u * threadIdx.x + (bx % 2u);
@@ -50,7 +53,7 @@ __global__ void __launch_bounds__(256) svao_pass1_kernel(SvaoArgs a) {
     if (!basic_init(a, u, v, b)) {
         ao = 1.0f;
     } else {
-#pragma unroll 1
+#pragma unroll RSD_P1_UNROLL
         for (int i = 0; i < 8; ++i) {
             Sample s;
             bool ssrAbove;

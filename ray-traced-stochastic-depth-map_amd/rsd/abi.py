@@ -7,10 +7,13 @@ missing or a call fails, a RuntimeError is raised with rsd_last_error().
 from __future__ import annotations
 
 import ctypes as C
+import os
 from pathlib import Path
 
 PKG_DIR = Path(__file__).resolve().parents[1]
-LIB_PATH = PKG_DIR / "librsd.so"
+# RSD_LIB_VARIANT=<name>: load librsd_<name>.so built beside it (A/B builds of one kernel option;
+# experiments only -- the product and the tests load librsd.so)
+LIB_PATH = PKG_DIR / (f"librsd_{os.environ['RSD_LIB_VARIANT']}.so" if os.environ.get("RSD_LIB_VARIANT") else "librsd.so")
 
 RSD_OK = 0
 STATUS_NAMES = {0: "RSD_OK", 1: "RSD_ERR_INVALID_ARG", 2: "RSD_ERR_UNSUPPORTED", 3: "RSD_ERR_HIP",

@@ -89,12 +89,24 @@ class BandFrame:
     def frame(self, sd_events=None):
         """One AO frame.  sd_events: optional (start, end) torch.cuda.Event pair recorded
         around this rank's SD trace (per-kernel timing in bench.py)."""
+        self.front()
+        self.back(sd_events)
+
+    def front(self):
+        """The frame up to pass 1 ("AO 1"): the interval clear when the previous trace did not
+        consume the maps, then pass 1 of this band."""
         b, band = self.b, (self.rank, self.world)
         # the previous frame's trace reset the intervals if the backend can fold the clear in
         consume = getattr(b, "can_consume_intervals", False) and bool(b.cfg.ray_interval)
         if not (consume and self._intervals_clear):
             b.clear_intervals()
         b.pass1(band=band)
+
+    def back(self, sd_events=None):
+        """The rest of the frame after front(): interval exchange, SD trace, SD exchange, pass 2,
+        AO exchange (a host may run it on another stream than front(), ordered by an event)."""
+        b, band = self.b, (self.rank, self.world)
+        consume = getattr(b, "can_consume_intervals", False) and bool(b.cfg.ray_interval)
         if self.world > 1:
             both = getattr(b, "ray_minmax", None)
             if both is not None:
