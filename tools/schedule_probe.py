@@ -2,7 +2,8 @@
   S1 slot streams, slot 0 on torch's current stream (bench.py up to now)
   S2 slot streams, all fresh
   S3 pipeline: front (clear + pass 1) on NP 'pass-1 streams' (frame i -> i % NP), back (trace +
-     pass 2) on NC 'chain streams' (frame i -> i % NC), ordered by events; slot i % F buffers."""
+     pass 2) on NC 'chain streams' (frame i -> i % NC), ordered by events; slot i % F buffers;
+     optionally the chain streams at high and the pass-1 streams at low stream priority."""
 import sys
 import time
 from pathlib import Path
@@ -45,10 +46,11 @@ def slot_sched(F, first_current):
     return step
 
 
-def pipe_sched(F, NP, NC):
+def pipe_sched(F, NP, NC, prio=False):
     frames = [BandFrame(b, throughput=True) for b in bufs[:F]]
-    P = [torch.cuda.Stream() for _ in range(NP)]
-    C = [torch.cuda.Stream() for _ in range(NC)]
+    lo, hi = torch.cuda.Stream.priority_range() if prio else (0, 0)
+    P = [torch.cuda.Stream(priority=lo) for _ in range(NP)]   # pass 1: low priority
+    C = [torch.cuda.Stream(priority=hi) for _ in range(NC)]   # trace + pass 2 chain: high
     for s in P + C:
         s.wait_stream(torch.cuda.current_stream())
     done = [None] * F
@@ -71,8 +73,7 @@ def pipe_sched(F, NP, NC):
     return step
 
 
-timed("S1 F=4 slot streams, slot 0 current", slot_sched(4, True))
+print("priority range (low, high):", torch.cuda.Stream.priority_range(), flush=True)
 timed("S2 F=4 slot streams, fresh", slot_sched(4, False))
-timed("S1 F=3 slot streams, slot 0 current", slot_sched(3, True))
-for F, NP, NC in ((4, 1, 2), (4, 2, 2), (6, 1, 3), (6, 2, 2), (8, 2, 2), (4, 1, 3), (6, 1, 2)):
-    timed(f"S3 F={F} pipeline NP={NP} NC={NC}", pipe_sched(F, NP, NC))
+for F, NP, NC in ((4, 1, 3), (6, 1, 3), (4, 2, 2), (6, 2, 2), (8, 2, 2), (6, 1, 2)):
+    timed(f"S3 F={F} pipeline NP={NP} NC={NC} chain high prio", pipe_sched(F, NP, NC, prio=True))
