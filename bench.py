@@ -231,6 +231,8 @@ def main():
                              "achieved_sequential the one-frame-in-flight duration",
                      "traffic_source": ", ".join(str(Path(p).relative_to(ROOT)) if Path(p).is_relative_to(ROOT)
                                                  else p for p in pmc if Path(p).exists()) or None},
+        # the frame's largest kernel is pass 1, bound by VALU issue rather than HBM
+        "pass1_roofline": pmc_valu(ROOT / "profiles" / "round1" / "pmc_sq_valu.csv", "svao_pass1_kernel"),
         "cpu_baseline": cpu,
     }
     print(json.dumps(line))
@@ -259,6 +261,34 @@ def pmc_traffic(csv_paths, kernel_substrs):
         return None
     mean = lambda k, c: (sum(per[(k, c)]) / len(per[(k, c)])) if (k, c) in per else 0.0  # noqa: E731
     return int(sum(2 * mean(k, "FETCH_SIZE") + mean(k, "WRITE_SIZE") for k in kernel_substrs) * 1024)
+
+
+# VALU issue peak of MI355X (MI355X_MICROARCH.md: a wave64 VALU instruction issues over 2 cycles,
+# 32 lanes/cycle; 157.3 TFLOPS FP32 vector = 2 x this FMA rate): 256 CUs x 4 SIMDs x 32 lanes x
+# 2.4 GHz.  Nominal: f64, transcendental and v_div_* instructions take more than 2 cycles.
+VALU_PEAK_LANE_OPS = 256 * 4 * 32 * 2.4e9
+
+
+def pmc_valu(csv_path, kernel_substr):
+    """VALU issue roofline of one kernel from a rocprofv3 --pmc SQ_INSTS_VALU pass (one frame in
+    flight): lane-instructions per launch / that launch's duration, against VALU_PEAK_LANE_OPS."""
+    import csv
+    if not Path(csv_path).exists():
+        return None
+    insts, durs = [], []
+    with open(csv_path) as f:
+        for row in csv.DictReader(f):
+            if kernel_substr in row.get("Kernel_Name", "") and row.get("Counter_Name") == "SQ_INSTS_VALU":
+                insts.append(float(row["Counter_Value"]))
+                durs.append((int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) * 1e-9)
+    if not insts:
+        return None
+    lane_ops = sum(insts) / len(insts) * 64
+    dur = sum(durs) / len(durs)
+    return {"kernel": kernel_substr, "bound": "valu", "achieved": round(lane_ops / dur / 1e12, 2),
+            "peak": round(VALU_PEAK_LANE_OPS / 1e12, 2), "unit": "T lane-instr/s",
+            "frac": round(lane_ops / dur / VALU_PEAK_LANE_OPS, 3), "duration_us": round(dur * 1e6, 1),
+            "source": str(Path(csv_path).relative_to(ROOT)) if Path(csv_path).is_relative_to(ROOT) else csv_path}
 
 
 def cpu_baseline(r, scene, target_s):
