@@ -39,8 +39,22 @@ __global__ void clear_intervals_kernel(uint32_t* rmin, uint32_t* rmax, uint32_t 
 #ifndef RSD_P1_UNROLL
 #define RSD_P1_UNROLL 1
 #endif
+#ifndef RSD_P1_XCD
+#define RSD_P1_XCD 0
+#endif
 __global__ void __launch_bounds__(256) svao_pass1_kernel(SvaoArgs a) {
+#if RSD_P1_XCD
+    // XCD-aware order: the hardware deals consecutive workgroups round-robin to the 8 XCDs;
+    // remap so that XCD k gets the k-th contiguous eighth of the tile rows (its L2 then holds
+    // the depth / normal rows its tiles share).  Only which workgroup computes which pixels
+    // changes, so the results are the same bits.
+    const uint32_t nb = gridDim.x * gridDim.y;
+    uint32_t lin = blockIdx.y * gridDim.x + blockIdx.x;
+    if (nb % 8u == 0u) lin = (lin % 8u) * (nb / 8u) + lin / 8u;
+    const uint32_t bx = lin % gridDim.x, by = lin / gridDim.x;
+#else
     const uint32_t bx = blockIdx.x, by = blockIdx.y;
+#endif
     const uint32_t ox = (bx / 2u) * 32u + 2u * threadIdx.x + (bx % 2u);
     const uint32_t oy = ((by / 2u) * a.bandCount + a.bandIndex) * 32u + 2u * threadIdx.y + (by % 2u);
     const uint32_t px = ox + a.guard, py = oy + a.guard;
