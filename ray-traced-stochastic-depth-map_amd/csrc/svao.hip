@@ -42,6 +42,9 @@ __global__ void clear_intervals_kernel(uint32_t* rmin, uint32_t* rmax, uint32_t 
 #ifndef RSD_P1_XCD
 #define RSD_P1_XCD 0
 #endif
+#ifndef RSD_P1_PIPE
+#define RSD_P1_PIPE 0
+#endif
 __global__ void __launch_bounds__(256) svao_pass1_kernel(SvaoArgs a) {
 #if RSD_P1_XCD
     // XCD-aware order: the hardware deals consecutive workgroups round-robin to the 8 XCDs;
@@ -67,18 +70,42 @@ __global__ void __launch_bounds__(256) svao_pass1_kernel(SvaoArgs a) {
     if (!basic_init(a, u, v, b)) {
         ao = 1.0f;
     } else {
+#if RSD_P1_PIPE
+        // software pipeline: direction i + 1's sample geometry and its raster depth fetch are
+        // issued before direction i is evaluated (same operations, same bits)
+        Sample sn;
+        bool ssrN = false;
+        bool validN = sample_init(a, u, v, b, 0, sn, ssrN);
+        float zN = validN ? depth_center(a, sn.ru, sn.rv, sn.kx, sn.ky) : 0.0f;
+#endif
 #pragma unroll RSD_P1_UNROLL
         for (int i = 0; i < 8; ++i) {
             Sample s;
             bool ssrAbove;
+#if RSD_P1_PIPE
+            s = sn;
+            ssrAbove = ssrN;
+            const bool valid = validN;
+            const float zc = zN;
+            if (i + 1 < 8) {
+                validN = sample_init(a, u, v, b, i + 1, sn, ssrN);
+                zN = validN ? depth_center(a, sn.ru, sn.rv, sn.kx, sn.ky) : 0.0f;
+            }
+            if (!valid) continue;
+#else
             if (!sample_init(a, u, v, b, i, s, ssrAbove)) continue;
+#endif
             if (fabsf(u - s.ru) < d.invResolution[0] * 0.9f && fabsf(v - s.rv) < d.invResolution[1] * 0.9f) {
                 ao += div_pdf(s.sphereStart - s.sphereEnd, s);  // isSamePixel
                 continue;
             }
             // SVAORaster.ps.slang:62-66: Raytraced mode with TRACE_OUT_OF_SCREEN (SVAO.h:104)
             bool forceRay = a.secondary == 3u && !s.isInScreen;
+#if RSD_P1_PIPE
+            add_sample(a, b, s, uv_to_view(a, s.ru, s.rv, zc), true);  // eval_primary with the prefetched depth
+#else
             eval_primary(a, b, s);
+#endif
             ao += s.visibility;
             if (!s.isInScreen && d.sdGuard > 0) {
                 forceRay = true;
