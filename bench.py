@@ -1,38 +1,39 @@
 #!/usr/bin/env python3
-"""Headline benchmark: Ray-SD + SVAO AO frames on MI355X (BASELINE.json metric
-"Mrays/s + AO frames/s, 1080p 1/4-res Ray-SD").
+"""Headline benchmark: Ray-SD + SVAO on MI355X (BASELINE.json metric "Mrays/s + AO frames/s,
+1080p 1/4-res Ray-SD, 1/2/4/8 MI355X"; definitions BASELINE.md section 4).
 
-A step = one AO frame of the reference's SVAO::execute span (SVAO.cpp:327-455: clear
-ray intervals, "AO 1", StochasticDepthMapRT, "AO 2") over the configs[1] workload:
+A step = one AO frame of the reference's SVAO::execute span (SVAO.cpp:327-455: clear ray
+intervals, "AO 1", StochasticDepthMapRT, "AO 2") over the configs[1] workload by default:
 Sun Temple stand-in (~0.6 M triangles, seed 2), 1920x1080 visible + 64-px guard band
 (2048x1208 frame buffer), 1/4-res SD map (768x558 texels incl. the 128-texel SD guard),
 N = 4, MAX_COUNT = 8.  Inputs (BVH, G-buffer) are resident in HBM before timing.
 
-  value            = SD rays dispatched per frame * frames / timed wall  (Mrays/s, whole job)
-  ao_frames_per_s  = frames / timed wall
-  sd_kernel_mrays  = SD rays / SD-kernel time (HIP events around the trace launch)
+Two timed regions, each K frames between a barrier + torch.cuda.synchronize() pair:
 
-Frames in flight (--frames-in-flight F, default 4, the measured optimum of F = 1..6):
-frame i runs on HIP stream i % F with its own frame buffers (ao, stencil, interval maps, SD
-map; BVH and G-buffer shared).  Every frame still runs the whole clear -> "AO 1" -> SD trace ->
-"AO 2" chain in order on its stream; frames of different slots overlap, so the latency-bound
-SD trace of one frame (~22 K live rays on 256 CUs) shares the machine with the VALU-bound
-passes of the others.  Overlapping frames trace with librsd's work-efficient walk
-(RSD_SD_THROUGHPUT: 4 lanes per ray) instead of the latency-optimised row walk (8 lanes per ray):
-the row walk's idle lanes would be VALU time taken from the other frames.  `sequential` reports the
-one-frame-in-flight latency of the same frame (row walk).
+  latency    one frame in flight (the reference's own schedule: one frame after the other).
+             HIP events around every SD trace and around every AO span (clear -> pass 1 ->
+             trace -> pass 2) give BASELINE.md's two numbers:
+               value (Mrays/s)     = dispatched SD rays / SD-kernel time   (whole job)
+               active_mrays_per_s  = active SD rays (TMin <= TMax) / SD-kernel time
+               ao_frames_per_s     = 1 / AO-span time
+  throughput F frames in flight (--frames-in-flight, default 4): frame i runs on HIP stream
+             i % F with its own frame buffers, frames of different slots overlap (the latency-
+             bound SD trace of one frame shares the machine with the VALU-bound passes of
+             others; overlapping traces use librsd's work-efficient walk, RSD_SD_THROUGHPUT).
+               ms_per_step, throughput.ao_frames_per_s, throughput.frame_mrays_per_s
+
+--camera-path orbit120 (default for configs[4], bistro_4k_full_n16): every frame renders the
+next pose of a 120-pose orbit (rsd.frame.camera_path): camera update + G-buffer + AO frame.
+The G-buffer is inside the frame's wall time but outside the AO span (AO frames/s
+excludes the G-buffer).
 
 Multi-GPU (torchrun, one rank per GPU), two sharding modes (--shard):
-  frame (default): frames are the independent units -- every rank renders whole frames of the
-    configs[1] size (its own frame stream, BVH + G-buffer replicated), no data-path
-    collective; the barrier and max-over-ranks wall bracket the timed region.  Weak scaling:
-    value = world * K frames * rays / wall.
-  band: one frame sharded by screen band (rsd/shard.py, the north_star's tile split).  Every
-    rank runs pass 1 on its band of rows, all-reduces the ray-interval maps (MIN/MAX),
-    traces its band of SD tile rows, all-gathers the SD map, runs pass 2 on its band and
-    all-gathers the AO image (RCCL over xGMI).  Strong scaling: the whole job renders the
-    same frame whatever N is; at 1080p/4 the three collectives per frame outweigh the
-    per-rank compute, so this is the mode for large frames (4K, full-res SD).
+  frame: frames are the independent units -- every rank renders whole frames (its own frame
+    stream, BVH + G-buffer replicated), no data-path collective.  Weak scaling.
+  band (default for the 4K configs): one frame sharded by screen band (rsd/shard.py, the
+    north_star's tile split): pass 1 on the rank's rows, interval all-reduce, trace of the
+    rank's SD tile rows, SD halo exchange with the neighbouring bands (ssMaxRadius), pass 2 on
+    the rank's rows, AO all-gather (RCCL over xGMI).  Strong scaling.
 """
 from __future__ import annotations
 
@@ -50,7 +51,9 @@ for p in (str(ROOT), str(PKG)):
         sys.path.insert(0, p)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8 TB/s (spec)
-SD_KERNELS = ("sd_setup_kernel", "sd_trace_row_kernel", "sd_resolve_row_kernel", "sd_trace_queue_kernel")  # launches of one rsd_sd_trace
+DEFAULT_CONFIG = "suntemple_1080p_q"
+# committed rocprofv3 passes of the default bench (newest round first)
+PROFILE_DIRS = [ROOT / "profiles" / "round2", ROOT / "profiles" / "round1"]
 
 
 def parse():
@@ -58,19 +61,45 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--config", default="suntemple_1080p_q")
+    ap.add_argument("--config", default=DEFAULT_CONFIG)
+    ap.add_argument("--camera-path", default=None,
+                    help="static | orbitN (default: the config's own, orbit120 for bistro_4k_full_n16)")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0,
                     help="target wall time of the bounded CPU-oracle sample (0 disables)")
     ap.add_argument("--frames-in-flight", type=int, default=4,
-                    help="frames in flight: frame i runs on stream i %% F with its own frame buffers "
-                         "(1 = strictly sequential frames)")
-    ap.add_argument("--shard", choices=("frame", "band"), default="frame",
+                    help="throughput region: frame i runs on stream i %% F with its own frame buffers")
+    ap.add_argument("--shard", choices=("frame", "band"), default=None,
                     help="N > 1: frame = every rank renders whole frames (weak scaling, no per-frame "
-                         "collective); band = each frame split by screen band + RCCL exchanges (strong)")
+                         "collective); band = each frame split by screen band + RCCL exchanges (strong). "
+                         "Default: band for the 4K configs, frame otherwise")
     ap.add_argument("--pmc-csv", nargs="*", default=None,
                     help="rocprofv3 --pmc counter_collection.csv file(s) with FETCH_SIZE / WRITE_SIZE for "
-                         "roofline.traffic (default: the committed profiles/round1 passes)")
+                         "roofline.traffic (default: the committed passes of the default config)")
     return ap.parse_args()
+
+
+def host_cpus():
+    """The CPUs the baseline may use and what they are (cores + model)."""
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        usable = os.cpu_count() or 1
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    quota = None
+    try:  # cgroup v2 CPU quota ("max 100000" = none)
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            quota = round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    return {"usable": usable, "nproc": os.cpu_count(), "cgroup_cpu_quota": quota, "model": model}
 
 
 def main():
@@ -78,8 +107,10 @@ def main():
     import numpy as np
     import torch
 
-    from rsd.frame import CONFIGS, FrameConfig, Renderer
+    from rsd import abi
+    from rsd.frame import CONFIGS, DEFAULT_CAMERA_PATH, FrameConfig, Renderer, camera_path
     from rsd.scenes import make_scene
+    from rsd.shard import BandFrame
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -100,82 +131,129 @@ def main():
 
     kw, scene_name = CONFIGS[args.config]
     cfg = FrameConfig(**kw)
+    shard = args.shard or ("band" if cfg.visible_w >= 3840 else "frame")
+    path_name = args.camera_path or DEFAULT_CAMERA_PATH.get(args.config, "static")
+    poses = camera_path(path_name)
     scene = make_scene(scene_name)
     r = Renderer(scene, cfg, device=local)
-    r.gbuffer()
-    torch.cuda.synchronize()
+    bvh_build_s = r.gscene.info.build_ms * 1e-3
+    bw = (rank, world) if shard == "band" else (0, 1)
+    F = max(1, args.frames_in_flight)
+    n_poses = len(poses) if poses else 1
 
-    # instrumented full-frame trace (not timed): traversal counters for the roofline bytes
-    r.clear_intervals()
-    r.pass1()
-    # counters of the walk the timed frames use (frames in flight: RSD_SD_THROUGHPUT)
-    cnt = r.sd_trace(counters=True, throughput=args.frames_in_flight > 1)
+    def pose(rend, i):
+        if poses:
+            rend.set_pose(*poses[i % n_poses])
+            rend.gbuffer()
+
+    # ---- instrumented traces (untimed): traversal counters for the roofline bytes, for both
+    #      walks, averaged over the poses the timed frames render
+    if not poses:
+        r.gbuffer()
+    cnt_seq, cnt_thr = [], []
+    for i in range(min(args.steps, n_poses)):
+        pose(r, i)
+        for acc, thr in ((cnt_seq, False), (cnt_thr, True)):
+            # pass 1 over the whole frame = the exact interval union a band frame all-reduces
+            r.clear_intervals()
+            r.pass1()
+            acc.append(r.sd_trace(counters=True, throughput=thr, band=bw))
     torch.cuda.synchronize()
+    walk_seq, walk_thr = int(cnt_seq[0].walk), int(cnt_thr[0].walk)
+    mean_cnt = lambda cs, f: float(np.mean([getattr(c, f) for c in cs]))  # noqa: E731
     if dist:
         dist.barrier()
 
-    from rsd.shard import BandFrame
-    # frames in flight: F buffer sets (slots) on F streams; frame i runs on slot i % F.  Every
-    # frame does the whole pass 1 -> SD trace -> pass 2 chain; frames of different slots overlap
-    # (the latency-bound SD trace of one frame shares the CUs with another frame's passes)
-    F = max(1, args.frames_in_flight)
-    # band: this rank's screen band of every frame; frame: whole frames on every rank
-    bw = (rank, world) if args.shard == "band" else (0, 1)
-    # with frames overlapping, the trace uses librsd's work-efficient walk (RSD_SD_THROUGHPUT)
-    slots = [BandFrame(r, *bw, throughput=F > 1)] + [BandFrame(r.frame_slot(), *bw, throughput=True)
-                                                     for _ in range(F - 1)]
+    def timed(fn, n):
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        fn(n)
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize()
+        wall = time.perf_counter() - t0
+        if dist:
+            t = torch.tensor([wall], device="cuda")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            wall = float(t.item())
+        return wall
+
+    # ---- latency region: one frame in flight, the latency-optimised trace walk
+    seq = BandFrame(r, *bw)
+    mk_ev = lambda n: [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))  # noqa: E731
+                       for _ in range(n)]
+    ev_sd, ev_ao = mk_ev(args.steps), mk_ev(args.steps)
+
+    def run_seq(n, timed_ev=True):
+        for i in range(n):
+            pose(r, i)
+            if timed_ev:
+                ev_ao[i][0].record()
+            seq.frame(sd_events=ev_sd[i] if timed_ev else None)
+            if timed_ev:
+                ev_ao[i][1].record()
+
+    run_seq(args.warmup, timed_ev=False)
+    wall_seq = timed(run_seq, args.steps)
+    seq_sd_ms = float(np.mean([a.elapsed_time(b) for a, b in ev_sd]))
+    seq_ao_ms = float(np.mean([a.elapsed_time(b) for a, b in ev_ao]))
+
+    # ---- throughput region: F frames in flight on F streams
+    slots = [BandFrame(r, *bw, throughput=F > 1)] + \
+        [BandFrame(r.frame_slot(own_gbuffer=bool(poses)), *bw, throughput=True) for _ in range(F - 1)]
     streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(F - 1)]
     for st in streams[1:]:
         st.wait_stream(streams[0])
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    ev_thr = mk_ev(args.steps)
 
-    def frame(i, timed=False):
-        with torch.cuda.stream(streams[i % F]):
-            slots[i % F].frame(sd_events=ev[i] if timed else None)
+    def run_thr(n, timed_ev=True):
+        for i in range(n):
+            with torch.cuda.stream(streams[i % F]):
+                pose(slots[i % F].b, i)
+                slots[i % F].frame(sd_events=ev_thr[i] if timed_ev else None)
 
-    for i in range(args.warmup):
-        frame(i)
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        frame(i, timed=True)
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    wall = time.perf_counter() - t0
-    if dist:
-        t = torch.tensor([wall], device="cuda")
+    run_thr(args.warmup, timed_ev=False)
+    wall_thr = timed(run_thr, args.steps)
+    thr_sd_ms = float(np.mean([a.elapsed_time(b) for a, b in ev_thr]))
+
+    if dist:  # per-kernel times: the slowest rank
+        t = torch.tensor([seq_sd_ms, seq_ao_ms, thr_sd_ms], device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        wall = float(t.item())
+        seq_sd_ms, seq_ao_ms, thr_sd_ms = (float(x) for x in t.tolist())
 
-    sd_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
-
-    # untimed for `value`: the single-frame latency (one frame in flight, slot 0 only)
-    n_seq = min(args.steps, 20)
-    seq = BandFrame(r, *bw)  # latency-optimised trace walk (no frames overlap)
-    ev_seq = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n_seq)]
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    t0 = time.perf_counter()
-    for i in range(n_seq):
-        seq.frame(sd_events=ev_seq[i])
-    torch.cuda.synchronize()
-    seq_ms = (time.perf_counter() - t0) / n_seq * 1e3
-    seq_sd_ms = float(np.mean([a.elapsed_time(b) for a, b in ev_seq]))
     rays = r.sd_rays
     N = cfg.sd_samples
+    # frame mode: every rank renders whole frames; band mode: the ranks share each frame
+    units = world if shard == "frame" else 1
+    rays_active = mean_cnt(cnt_seq, "rays_active")
+    if dist and shard == "band":  # counters are per band: the frame's totals
+        t = torch.tensor([rays_active, mean_cnt(cnt_seq, "nodes_visited"), mean_cnt(cnt_seq, "tris_tested")],
+                         device="cuda", dtype=torch.float64)
+        dist.all_reduce(t)
+        rays_active, nodes_seq, tris_seq = t.tolist()
+    else:
+        nodes_seq, tris_seq = mean_cnt(cnt_seq, "nodes_visited"), mean_cnt(cnt_seq, "tris_tested")
+    value = units * rays / (seq_sd_ms * 1e-3) / 1e6
     # B_ray = 16 (linearZ bilinear) + 8 (rayMin+rayMax) + 4N (store) + node bytes + 48 n_tri;
-    # librsd's nodes are 4-wide (128 B per visit = two of SURVEY's 64-B BVH2 nodes)
-    alg_bytes = rays * (16 + 8 + 4 * N) + 128 * cnt.nodes_visited + 48 * cnt.tris_tested
-    achieved = alg_bytes / (sd_ms * 1e-3) / 1e9
-    pmc = args.pmc_csv if args.pmc_csv is not None else [str(ROOT / "profiles" / "round1" / f)
-                                                          for f in ("pmc_fetch_size.csv", "pmc_write_size.csv")]
-    traffic = pmc_traffic([p for p in pmc if Path(p).exists()], SD_KERNELS)
+    # librsd's nodes are 4-wide (128 B per visit = two of SURVEY's 64-B BVH2 nodes).  Per launch =
+    # per frame (band mode: the whole frame's bytes over the slowest rank's trace time).
+    alg_bytes = rays * (16 + 8 + 4 * N) + 128 * nodes_seq + 48 * tris_seq
+    achieved = alg_bytes / (seq_sd_ms * 1e-3) / 1e9
+    kernels_seq = abi.WALK_KERNELS[walk_seq]
+    pmc = args.pmc_csv
+    if pmc is None and args.config == DEFAULT_CONFIG and not poses:
+        for d in PROFILE_DIRS:
+            cand = [d / "pmc_fetch_size.csv", d / "pmc_write_size.csv"]
+            if all(p.exists() for p in cand):
+                pmc = [str(p) for p in cand]
+                break
+    pmc = [p for p in (pmc or []) if Path(p).exists()]
+    traffic = pmc_traffic(pmc, kernels_seq)
+    valu_csv = next((d / "pmc_sq_valu.csv" for d in PROFILE_DIRS if (d / "pmc_sq_valu.csv").exists()), None)
 
     if rank != 0:
         if dist:
@@ -184,12 +262,10 @@ def main():
 
     cpu = None
     if args.cpu_baseline_seconds > 0 and world == 1:
-        cpu = cpu_baseline(r, scene, args.cpu_baseline_seconds)
+        cpu = cpu_baseline(r, scene, args.cpu_baseline_seconds, poses)
 
-    # whole job: frame mode renders `steps` whole frames on every rank, band mode `steps` frames in all
-    frames_total = args.steps * (world if args.shard == "frame" else 1)
-    frames_per_s = frames_total / wall
-    value = rays * frames_per_s / 1e6 * 1.0
+    frames_thr = args.steps * units
+    rel = lambda p: str(Path(p).relative_to(ROOT)) if Path(p).is_relative_to(ROOT) else str(p)  # noqa: E731
     line = {
         "metric": "Mrays/s + AO frames/s, 1080p 1/4-res Ray-SD, 1/2/4/8 MI355X",
         "value": round(value, 3),
@@ -197,42 +273,54 @@ def main():
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": round(wall / args.steps * 1e3, 4),
+        "ms_per_step": round(wall_thr / args.steps * 1e3, 4),
         "higher_is_better": True,
-        "scaling": "strong" if args.shard == "band" and world > 1 else "weak",
+        "scaling": "strong" if shard == "band" and world > 1 else "weak",
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic (seeded procedural stand-in scene; no reference assets in the container)",
         "config": {"workload": args.config, "scene": scene_name, "triangles": scene.triangle_count,
                    "frame_buffer": [cfg.fb_w, cfg.fb_h], "visible": [cfg.visible_w, cfg.visible_h],
                    "sd_map": [r.sd_w, r.sd_h], "sd_samples": N, "max_count": cfg.max_count,
-                   "stoch_map_divisor": cfg.divisor,
-                   "parallelism": f"screen-band x{world}" if args.shard == "band" else f"frame-parallel x{world}",
+                   "stoch_map_divisor": cfg.divisor, "camera_path": path_name,
+                   "parallelism": f"screen-band x{world}" if shard == "band" else f"frame-parallel x{world}",
                    "frames_in_flight": F},
-        "ao_frames_per_s": round(frames_per_s, 2),
-        "frames_total": frames_total,
-        "sd_kernel_ms": round(sd_ms, 4),
-        "sequential": {"ms_per_frame": round(seq_ms, 4), "ao_frames_per_s": round(1e3 / seq_ms, 2),
-                       "sd_kernel_ms": round(seq_sd_ms, 4), "frames": n_seq,
-                       "note": "one frame in flight: the frame latency (value counts frames in flight)"},
-        "sd_kernel_mrays_per_s": round(rays / (sd_ms * 1e-3) / 1e6, 2),
-        "active_rays": int(cnt.rays_active),
-        "traversal": {"nodes_per_ray": round(cnt.nodes_visited / rays, 3),
-                      "tris_per_ray": round(cnt.tris_tested / rays, 3),
-                      "nodes_per_active_ray": round(cnt.nodes_visited / max(cnt.rays_active, 1), 2),
-                      "tris_per_active_ray": round(cnt.tris_tested / max(cnt.rays_active, 1), 2)},
+        "value_definition": "dispatched SD rays / SD-kernel time (HIP events around every rsd_sd_trace of the "
+                            "latency region; BASELINE.md section 4), summed over ranks",
+        "sd_kernel_ms": round(seq_sd_ms, 4),
+        "rays_dispatched": rays * units,
+        "active_rays": int(round(rays_active)) * units,
+        "active_mrays_per_s": round(units * rays_active / (seq_sd_ms * 1e-3) / 1e6, 2),
+        "ao_frames_per_s": round(units * 1e3 / seq_ao_ms, 2),
+        "ao_span_ms": round(seq_ao_ms, 4),
+        "latency": {"ms_per_frame": round(wall_seq / args.steps * 1e3, 4), "frames": args.steps,
+                    "walk": ["quad", "fused", "split"][walk_seq],
+                    "note": "one frame in flight; ms_per_frame includes the G-buffer of a camera path, "
+                            "ao_span_ms does not"},
+        "throughput": {"frames_in_flight": F, "frames": frames_thr, "ms_per_frame": round(wall_thr / args.steps * 1e3, 4),
+                       "ao_frames_per_s": round(frames_thr / wall_thr, 2),
+                       "frame_mrays_per_s": round(rays * frames_thr / wall_thr / 1e6, 2),
+                       "sd_kernel_ms_overlapped": round(thr_sd_ms, 4),
+                       "walk": ["quad", "fused", "split"][walk_thr]},
+        "traversal": {"nodes_per_ray": round(nodes_seq / rays / units, 3),
+                      "tris_per_ray": round(tris_seq / rays / units, 3),
+                      "nodes_per_active_ray": round(nodes_seq / max(rays_active, 1), 2),
+                      "tris_per_active_ray": round(tris_seq / max(rays_active, 1), 2),
+                      "max_steps_per_ray": int(max(c.max_steps_per_ray for c in cnt_seq))},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "kernel": ("rsd_sd_trace = sd_setup_kernel + sd_trace_queue_kernel (frames in flight: RSD_SD_THROUGHPUT)"
-                                if F > 1 else "rsd_sd_trace = sd_setup_kernel + sd_trace_row_kernel + sd_resolve_row_kernel"),
+                     "kernel": "rsd_sd_trace = " + " + ".join(kernels_seq),
                      "alg_bytes_per_launch": int(alg_bytes),
-                     "achieved_sequential": round(alg_bytes / (seq_sd_ms * 1e-3) / 1e9, 1),
-                     "note": "achieved uses the trace's duration with frames in flight (it shares the CUs); "
-                             "achieved_sequential the one-frame-in-flight duration",
-                     "traffic_source": ", ".join(str(Path(p).relative_to(ROOT)) if Path(p).is_relative_to(ROOT)
-                                                 else p for p in pmc if Path(p).exists()) or None},
+                     "duration_us": round(seq_sd_ms * 1e3, 2),
+                     "note": "achieved = SURVEY 8(d) algorithmic bytes of one trace / its HIP-event duration in "
+                             "the latency region; traffic = FETCH_SIZE + WRITE_SIZE of the same kernels "
+                             "(per launch, committed rocprofv3 --pmc passes)",
+                     "traffic_source": ", ".join(rel(p) for p in pmc) or None},
         # the frame's largest kernel is pass 1, bound by VALU issue rather than HBM
-        "pass1_roofline": pmc_valu(ROOT / "profiles" / "round1" / "pmc_sq_valu.csv", "svao_pass1_kernel"),
+        "pass1_roofline": pmc_valu(valu_csv, "svao_pass1_kernel") if valu_csv and args.config == DEFAULT_CONFIG
+        else None,
+        "bvh_build_s": round(bvh_build_s, 3),
+        "bvh_build_threads": int(r.gscene.info.build_threads),
         "cpu_baseline": cpu,
     }
     print(json.dumps(line))
@@ -241,9 +329,10 @@ def main():
 
 
 def pmc_traffic(csv_paths, kernel_substrs):
-    """HBM bytes of one SD pass from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (KB units;
-    FETCH_SIZE doubled on gfx950 per MI355X_MICROARCH.md §HBM): per kernel, the mean over its
-    launches; summed over the kernels of the pass."""
+    """HBM bytes of one SD trace from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (KB units;
+    FETCH_SIZE doubled on gfx950 per MI355X_MICROARCH.md section HBM): per kernel, the mean over
+    its launches (the instrumented counter launches excluded); summed over the kernels of ONE
+    trace of the given walk."""
     import csv
     import re
     if not csv_paths:
@@ -291,40 +380,60 @@ def pmc_valu(csv_path, kernel_substr):
             "source": str(Path(csv_path).relative_to(ROOT)) if Path(csv_path).is_relative_to(ROOT) else csv_path}
 
 
-def cpu_baseline(r, scene, target_s):
-    """The CPU oracle (kind "port") timed on the same frame's SD trace, repeated to ~target_s."""
+def cpu_baseline(r, scene, target_s, poses=None):
+    """The CPU oracle (kind "port") timed on the same frame's SD trace, on every CPU this process
+    may use.  The whole SD map when one trace takes < target_s / 4, else a band of rows sized to
+    ~target_s; the traced rows are checked bit-for-bit against the GPU frame."""
     import numpy as np
 
     from oracle import oracle as O
     sys.path.insert(0, str(ROOT / "tests"))
     from helpers import to_oracle
 
-    # one full frame with explicit interval maps (the timed frames consume them, so the maps are
-    # cleared by now): the baseline traces exactly this frame's SD map
+    # one full frame with explicit interval maps (the timed frames consume them): the baseline
+    # traces exactly this frame's SD map (pose 0 of a camera path)
+    if poses:
+        r.set_pose(*poses[0])
+        r.gbuffer()
     r.frame()
     g = r.numpy()
     assert (g["ray_max"] != 0).any(), "the baseline frame has no live SD rays"
-    cores = min(os.cpu_count() or 1, 16)
+    cpus = host_cpus()
+    cores = cpus["usable"]
     osc = O.Scene(scene.positions, scene.indices, scene.flags)
     cam, sdp = to_oracle(r.cam, O.Camera), to_oracle(r.sdp, O.SDParams)
-    # the whole SD map of the frame, repeated until ~target_s of CPU work
+
+    def trace(rows):
+        return O.sd_trace(osc, cam, sdp, g["depth"], g["ray_min"], g["ray_max"], r.sd_w, r.sd_h, rows=rows,
+                          threads=cores)
+
+    # probe: 8 rows through the middle, then the whole map if it is cheap enough
+    mid = r.sd_h // 2 // 8 * 8
     t0 = time.perf_counter()
-    sd, stats = O.sd_trace(osc, cam, sdp, g["depth"], g["ray_min"], g["ray_max"], r.sd_w, r.sd_h, threads=cores)
+    trace((mid, mid + 8))
+    per_row = (time.perf_counter() - t0) / 8
+    if per_row * r.sd_h < target_s / 4:
+        y0, y1 = 0, r.sd_h
+    else:
+        n = max(8, min(r.sd_h, int(target_s / 4 / max(per_row, 1e-9)) // 8 * 8))
+        y0 = max(0, min(r.sd_h - n, mid - n // 2)) // 8 * 8
+        y1 = min(r.sd_h, y0 + n)
+    t0 = time.perf_counter()
+    sd, stats = trace((y0, y1))
     dt = time.perf_counter() - t0
     reps = max(1, int(target_s / max(dt, 1e-4)))
     t0 = time.perf_counter()
     for _ in range(reps):
-        sd, stats = O.sd_trace(osc, cam, sdp, g["depth"], g["ray_min"], g["ray_max"], r.sd_w, r.sd_h,
-                               threads=cores)
+        sd, stats = trace((y0, y1))
     dt = (time.perf_counter() - t0) / reps
-    y0, y1 = 0, r.sd_h
     n = (y1 - y0) * r.sd_w
-    # the sample's share of the GPU result must be bit-identical (the baseline computes the same thing)
     same = bool(np.array_equal(sd[:, y0:y1].view(np.uint32), g["sd"][:, y0:y1].view(np.uint32)))
+    what = "the frame's full SD trace" if (y0, y1) == (0, r.sd_h) else f"SD rows [{y0}, {y1}) of the frame"
     return {"value": round(n / dt / 1e6, 4), "unit": "Mrays/s", "cores": cores, "kind": "port",
-            "sample": f"the frame's full SD trace ({n} rays, {int(stats[0])} live) x {reps} repetitions, "
-                      f"oracle pthreads on {cores} host threads",
-            "seconds": round(dt * reps, 2), "bit_identical_to_gpu": same}
+            "sample": f"{what} ({n} rays, {int(stats[0])} live) x {reps} repetitions, oracle pthreads on "
+                      f"{cores} host threads (every CPU of the process's affinity mask)",
+            "active_mrays_per_s": round(float(stats[0]) / dt / 1e6, 4),
+            "host": cpus, "seconds": round(dt * reps, 2), "bit_identical_to_gpu": same}
 
 
 if __name__ == "__main__":

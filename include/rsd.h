@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define RSD_ABI_VERSION 1
+#define RSD_ABI_VERSION 2
 
 typedef enum {
     RSD_OK = 0,
@@ -65,8 +65,10 @@ typedef struct {
     uint32_t max_depth;
     uint32_t leaf_count;
     double sah_cost;
-    double build_ms;
+    double build_ms;          /* host BVH build wall time */
     uint64_t device_bytes;
+    uint32_t build_threads;   /* host threads of the build (the process's CPU affinity, or RSD_BUILD_THREADS) */
+    uint32_t reserved;
 } rsd_scene_info;
 
 /* Alpha-masked materials (MaterialFactory.slang:124-151, AlphaTest.slang:54-84,
@@ -120,7 +122,24 @@ typedef struct {
     uint32_t cull_mode;      /* CullMode (CULL_MODE_RAY_FLAG) */
     uint32_t alpha_test;     /* AlphaTest (USE_ALPHA_TEST) */
     float alpha;             /* Alpha (ALPHA), coverage-mask implementation */
+    uint32_t hit_order;      /* any-hit delivery order: rsd_hit_order (librsd extension) */
+    uint32_t use_16bit;      /* Use16Bit (StochasticDepthMapRT.cpp:192-198): store R16F / RG16F / RGBA16F,
+                                N <= 4; d_sd_out then holds IEEE binary16 (round to nearest even) */
 } rsd_sd_params;
+
+/* Any-hit order of the SD trace.  DXR calls any-hit in an implementation-defined traversal order
+ * (Common.slangh:136-153 under RAY_FLAG_FORCE_NON_OPAQUE, StochasticDepthMapRT.rt.slang:83-88),
+ * so two orders are defined:
+ *   CANONICAL  ascending (t, primitive id), each triangle once -- independent of the BVH; the
+ *              result depends only on the MAX_COUNT nearest hits (Default == KBuffer on opaque
+ *              geometry: the reservoir never replaces a slot).
+ *   TRAVERSAL  the order of a depth-first walk of the scene's 4-wide BVH: children nearest entry
+ *              distance first (ties: child slot), leaf triangles in record order, each triangle
+ *              once; a committed hit (algorithm returns true = DXR AcceptHit) shrinks the ray's
+ *              TMax to its t and later hits must be nearer (t < TMax), like DXR's RayTCurrent().
+ *              The reservoir samples stochastically; the result depends on the BVH
+ *              (rsd_scene_export_bvh gives the oracle the same tree). */
+typedef enum { RSD_HIT_ORDER_CANONICAL = 0, RSD_HIT_ORDER_TRAVERSAL = 1 } rsd_hit_order;
 
 /* VAOData.slang:33-45 mirror */
 typedef struct {
@@ -158,7 +177,13 @@ typedef struct {
     uint64_t sum_ray_clocks;    /* shader clocks (s_memtime) spent in live rays */
     uint64_t max_ray_clocks;    /* the slowest live ray */
     uint64_t leaves_visited;    /* leaf steps (<= 4 triangle records each) */
+    uint64_t walk;              /* traversal walk of the trace: RSD_WALK_* */
 } rsd_counters;
+/* rsd_counters.walk: which kernels an rsd_sd_trace launched (besides sd_setup_kernel) */
+#define RSD_WALK_QUAD 0u   /* sd_trace_queue_kernel: depth-first, 4 lanes per ray */
+#define RSD_WALK_FUSED 1u  /* sd_trace_row_kernel with the algorithm in-kernel */
+#define RSD_WALK_SPLIT 2u  /* sd_trace_row_kernel (K nearest keys) + sd_resolve_row_kernel */
+#define RSD_WALK_ORDERED 3u /* sd_trace_ordered_kernel: RSD_HIT_ORDER_TRAVERSAL */
 
 /* --- library / device ------------------------------------------------------------ */
 uint32_t rsd_abi_version(void);
@@ -175,6 +200,11 @@ rsd_status rsd_scene_upload(rsd_device* dev, const rsd_scene_desc* desc, rsd_sce
 rsd_status rsd_scene_upload_alpha(rsd_device* dev, const rsd_scene_desc* desc, const rsd_alpha_desc* alpha,
                                   rsd_scene** out);
 rsd_status rsd_scene_info_get(const rsd_scene* scene, rsd_scene_info* out);
+/* Copy of the scene's device BVH (host memory): 4-wide nodes (128 B: SoA lo.x[4] hi.x[4] lo.y[4]
+ * hi.y[4] lo.z[4] hi.z[4] ref[4] count[4]), then 48-B triangle records {v0, prim}{v1, flags}{v2, 0}
+ * from float4 offset *tri_offset.  dst == NULL: only *bytes.  Synchronous. */
+rsd_status rsd_scene_export_bvh(const rsd_scene* scene, void* dst, uint64_t capacity, uint64_t* bytes,
+                                uint32_t* tri_offset);
 void rsd_scene_release(rsd_scene* scene);
 
 /* --- host helpers (no GPU work) ---------------------------------------------------- */

@@ -36,7 +36,7 @@ class SDParams(C.Structure):
     _fields_ = [("sample_count", C.c_uint32), ("implementation", C.c_uint32), ("max_count", C.c_uint32),
                 ("guard_band", C.c_int32), ("jitter", C.c_uint32), ("normalize", C.c_uint32),
                 ("ray_interval", C.c_uint32), ("cull_mode", C.c_uint32), ("alpha_test", C.c_uint32),
-                ("alpha", C.c_float)]
+                ("alpha", C.c_float), ("hit_order", C.c_uint32), ("use_16bit", C.c_uint32)]
 
 
 class VAOData(C.Structure):

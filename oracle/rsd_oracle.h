@@ -58,6 +58,8 @@ typedef struct {
     uint32_t cull_mode;      /* 0 None, 1 Back, 2 Front */
     uint32_t alpha_test;     /* USE_ALPHA_TEST (opaque scenes: no-op) */
     float    alpha;          /* ALPHA (coverage mask) */
+    uint32_t hit_order;      /* rsd_hit_order: 0 canonical (ocpu_sd_trace), 1 traversal (ocpu_sd_trace_ordered) */
+    uint32_t use_16bit;      /* not read by the oracle (tests round the f32 map to binary16 in numpy) */
 } osd_params;
 
 /* Same layout as rsd_vao_data: mirror of VAOData.slang:33-45 */

@@ -1,6 +1,7 @@
 // rsd_host.cpp -- librsd host entry points: errors, devices, scene upload (BVH build +
 // HBM residency), camera and SVAO constant derivation.  No GPU work besides copies.
 #include <hip/hip_runtime.h>
+#include <sched.h>
 
 #include <algorithm>
 #include <cfloat>
@@ -59,6 +60,19 @@ extern "C" rsd_status rsd_device_open(int hip_device, rsd_device** out) {
 
 extern "C" void rsd_device_close(rsd_device* dev) { delete dev; }
 
+namespace {
+// Host threads of the BVH build: every CPU this process may run on (its affinity mask, which is
+// what a container or `taskset` grants), or RSD_BUILD_THREADS.
+unsigned build_threads() {
+    if (const char* env = std::getenv("RSD_BUILD_THREADS"))
+        if (int n = std::atoi(env); n > 0) return (unsigned)n;
+    cpu_set_t set;
+    CPU_ZERO(&set);
+    if (sched_getaffinity(0, sizeof(set), &set) == 0 && CPU_COUNT(&set) > 0) return (unsigned)CPU_COUNT(&set);
+    return std::max(1u, std::thread::hardware_concurrency());
+}
+}  // namespace
+
 extern "C" rsd_status rsd_scene_upload(rsd_device* dev, const rsd_scene_desc* desc, rsd_scene** out) {
     if (!dev || !desc || !out || (desc->triangle_count && (!desc->positions || !desc->indices))) {
         set_error("rsd_scene_upload: null argument");
@@ -75,8 +89,7 @@ extern "C" rsd_status rsd_scene_upload(rsd_device* dev, const rsd_scene_desc* de
         return RSD_ERR_UNSUPPORTED;
     }
     RSD_HIP(hipSetDevice(dev->hip_device));
-    unsigned threads = std::max(1u, std::thread::hardware_concurrency());
-    threads = std::min(threads, 16u);
+    const unsigned threads = build_threads();
     rsd::FlatBvh bvh = rsd::build_bvh(desc->positions, desc->vertex_count, desc->indices, desc->triangle_count,
                                       desc->triangle_flags, threads);
     auto* s = new rsd_scene;
@@ -84,13 +97,13 @@ extern "C" rsd_status rsd_scene_upload(rsd_device* dev, const rsd_scene_desc* de
     s->triangle_count = desc->triangle_count;
     s->node_count = (uint32_t)(bvh.nodes.size() / 32);
     s->stats = bvh.stats;
+    s->build_threads = threads;
     // one allocation: wide nodes, then triangle records, then 12 x 16 B of padding so a
     // traversal step may always fetch 192 B (DESIGN.md "BVH layout in HBM")
     const size_t nb = bvh.nodes.size() * sizeof(float), tb = bvh.tris.size() * sizeof(float);
     const size_t total = nb + tb + 12 * 16;
     s->tri_offset = (uint32_t)(bvh.nodes.size() / 4);
     hipError_t e = hipMalloc(&s->d_nodes, total);
-    if (e == hipSuccess) e = hipMalloc(&s->d_counters, 16 * sizeof(unsigned long long));
     if (e == hipSuccess) e = hipMemset(s->d_nodes, 0, total);
     if (e == hipSuccess) e = hipMemcpy(s->d_nodes, bvh.nodes.data(), nb, hipMemcpyHostToDevice);
     if (e == hipSuccess && tb)
@@ -98,7 +111,6 @@ extern "C" rsd_status rsd_scene_upload(rsd_device* dev, const rsd_scene_desc* de
     if (e != hipSuccess) {
         rsd_status st = rsd::hip_fail(e, "rsd_scene_upload");
         (void)hipFree(s->d_nodes);
-        (void)hipFree(s->d_counters);
         delete s;
         return st;
     }
@@ -258,6 +270,7 @@ extern "C" rsd_status rsd_scene_info_get(const rsd_scene* s, rsd_scene_info* out
     out->sah_cost = s->stats.sah_cost;
     out->build_ms = s->stats.build_ms;
     out->device_bytes = s->device_bytes;
+    out->build_threads = s->build_threads;
     return RSD_OK;
 }
 
@@ -265,7 +278,6 @@ extern "C" void rsd_scene_release(rsd_scene* s) {
     if (!s) return;
     (void)hipSetDevice(s->dev->hip_device);
     (void)hipFree(s->d_nodes);
-    (void)hipFree(s->d_counters);
     rsd::release_sd_workspaces(s);
     (void)hipFree(s->d_alpha);
     delete s;

@@ -56,6 +56,7 @@ struct SdWorkspace {
     void* queue = nullptr;         // live-ray records + K-key slots, grow-only
     size_t queue_cap = 0;          // bytes
     RayTabCache raytab;
+    unsigned long long* counters = nullptr;  // 16 x u64 scratch of instrumented traces on this stream
 };
 void release_sd_workspaces(rsd_scene* s);
 }  // namespace rsd
@@ -68,8 +69,8 @@ struct rsd_scene {
     uint32_t triangle_count = 0;
     uint32_t node_count = 0;
     rsd::BvhStats stats;
+    uint32_t build_threads = 0;  // host threads of the BVH build
     uint64_t device_bytes = 0;
-    unsigned long long* d_counters = nullptr;  // 8 x u64 scratch for instrumented traces
     std::vector<rsd::SdWorkspace*> sd_ws;  // one per stream that traced this scene (few: linear lookup)
     void* d_alpha = nullptr;       // alpha data (rsd_scene_upload_alpha), one allocation
     rsd::AlphaData alpha;          // device pointers into d_alpha

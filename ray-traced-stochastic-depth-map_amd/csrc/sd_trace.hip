@@ -24,6 +24,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -1150,12 +1151,15 @@ static hipError_t launch_sd_k(const SDArgs& a, uint32_t N, dim3 grid, uint32_t p
 using namespace rsd;
 
 namespace {
+// coverage-mask tables per (device, N), process-wide, never freed (kernels in flight on any
+// stream may read them)
 struct LutCache {
-    int n = -1;
     int32_t* d_idx = nullptr;
     uint32_t* d_lut = nullptr;
 };
-thread_local LutCache g_lut[17];
+constexpr int kLutDevices = 64;
+LutCache g_lut[kLutDevices][17];
+std::mutex g_lut_mutex;
 
 // the SD-trace workspace of (scene, stream); created on the stream's first trace
 constexpr size_t kMaxWorkspaces = 16;
@@ -1171,15 +1175,25 @@ rsd_status sd_workspace(rsd_scene* scene, hipStream_t s, SdWorkspace** out) {
     SdWorkspace* w = new SdWorkspace();
     w->stream = s;
     hipError_t e = hipMalloc(&w->qctl, 4 * kQueueParts * sizeof(uint32_t));
-    if (e != hipSuccess) { delete w; return hip_fail(e, "sd workspace"); }
+    if (e == hipSuccess) e = hipMalloc(&w->counters, 16 * sizeof(unsigned long long));
+    if (e != hipSuccess) {
+        (void)hipFree(w->qctl);
+        delete w;
+        return hip_fail(e, "sd workspace");
+    }
     scene->sd_ws.push_back(w);
     *out = w;
     return RSD_OK;
 }
 
-rsd_status ensure_lut(uint32_t N, const int32_t** idx, const uint32_t** lut) {
-    LutCache& c = g_lut[N];
-    if (c.n != (int)N) {
+rsd_status ensure_lut(int dev, uint32_t N, const int32_t** idx, const uint32_t** lut) {
+    if (dev < 0 || dev >= kLutDevices || N > 16) {
+        set_error("rsd_sd_trace: device index >= 64 or N > 16");
+        return RSD_ERR_UNSUPPORTED;
+    }
+    std::lock_guard<std::mutex> lock(g_lut_mutex);
+    LutCache& c = g_lut[dev][N];
+    if (!c.d_lut) {
         // StochasticDepthMapRT.cpp:79-124 generateStratifiedLookupTable
         std::vector<int32_t> ind(N + 1);
         std::vector<uint32_t> tab(1u << N);
@@ -1199,11 +1213,14 @@ rsd_status ensure_lut(uint32_t N, const int32_t** idx, const uint32_t** lut) {
             tab[cur[pc]] = i;
             cur[pc]++;
         }
-        RSD_HIP(hipMalloc(&c.d_idx, sizeof(int32_t) * ind.size()));
-        RSD_HIP(hipMalloc(&c.d_lut, sizeof(uint32_t) * tab.size()));
-        RSD_HIP(hipMemcpy(c.d_idx, ind.data(), sizeof(int32_t) * ind.size(), hipMemcpyHostToDevice));
-        RSD_HIP(hipMemcpy(c.d_lut, tab.data(), sizeof(uint32_t) * tab.size(), hipMemcpyHostToDevice));
-        c.n = (int)N;
+        int32_t* di = nullptr;
+        uint32_t* dl = nullptr;
+        RSD_HIP(hipMalloc(&di, sizeof(int32_t) * ind.size()));
+        RSD_HIP(hipMalloc(&dl, sizeof(uint32_t) * tab.size()));
+        RSD_HIP(hipMemcpy(di, ind.data(), sizeof(int32_t) * ind.size(), hipMemcpyHostToDevice));
+        RSD_HIP(hipMemcpy(dl, tab.data(), sizeof(uint32_t) * tab.size(), hipMemcpyHostToDevice));
+        c.d_idx = di;
+        c.d_lut = dl;
     }
     *idx = c.d_idx;
     *lut = c.d_lut;
@@ -1317,7 +1334,7 @@ extern "C" rsd_status rsd_sd_trace_band_ex(rsd_scene* scene, const rsd_camera* c
     a.alphaData = scene->alpha;
     a.alphaData.spread = rsd_ray_cone_spread(cam->focalLength, sd_h);  // default texture dims = SD map
     if (p->implementation == RSD_SD_COVERAGE_MASK) {
-        rsd_status s = ensure_lut(N, &a.lutIdx, &a.lut);
+        rsd_status s = ensure_lut(scene->dev->hip_device, N, &a.lutIdx, &a.lut);
         if (s != RSD_OK) return s;
     }
     hipStream_t s = (hipStream_t)stream;
@@ -1351,8 +1368,9 @@ extern "C" rsd_status rsd_sd_trace_band_ex(rsd_scene* scene, const rsd_camera* c
         a.rayTab = rt.d;
     }
     if (counters) {
-        RSD_HIP(hipMemsetAsync(scene->d_counters, 0, 16 * sizeof(unsigned long long), s));
-        a.counters = scene->d_counters;
+        // per (scene, stream): concurrent instrumented traces on other streams keep their own
+        RSD_HIP(hipMemsetAsync(ws->counters, 0, 16 * sizeof(unsigned long long), s));
+        a.counters = ws->counters;
     }
     const uint32_t tiles = (sd_h + kTile - 1) / kTile;
     const uint32_t bandTiles = tiles > band_index ? (tiles - band_index + band_count - 1) / band_count : 0u;
@@ -1424,7 +1442,7 @@ extern "C" rsd_status rsd_sd_trace_band_ex(rsd_scene* scene, const rsd_camera* c
     if (grid.y != 0) ws->qctl_gen++;
     if (counters) {
         unsigned long long h[16];
-        RSD_HIP(hipMemcpyAsync(h, scene->d_counters, sizeof(h), hipMemcpyDeviceToHost, s));
+        RSD_HIP(hipMemcpyAsync(h, ws->counters, sizeof(h), hipMemcpyDeviceToHost, s));
         RSD_HIP(hipStreamSynchronize(s));
         counters->rays_dispatched = h[0];
         counters->rays_active = h[1];
@@ -1436,6 +1454,7 @@ extern "C" rsd_status rsd_sd_trace_band_ex(rsd_scene* scene, const rsd_camera* c
         counters->sum_ray_clocks = h[7];
         counters->max_ray_clocks = h[8];
         counters->leaves_visited = h[9];
+        counters->walk = (uint64_t)walk;
         if (const char* dbg = std::getenv("RSD_TRACE_PHASES"))
             if (*dbg) std::fprintf(stderr, "[rsd] row walk phase clocks: fetch %llu step %llu resolve %llu steps %llu loops %llu\n",
                                    h[11], h[12], h[13], h[14], h[15]);
@@ -1520,6 +1539,7 @@ void release_sd_workspaces(rsd_scene* scene) {
         (void)hipFree(w->qctl);
         (void)hipFree(w->queue);
         (void)hipFree(w->raytab.d);
+        (void)hipFree(w->counters);
         delete w;
     }
     scene->sd_ws.clear();

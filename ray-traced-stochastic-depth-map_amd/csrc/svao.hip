@@ -11,6 +11,7 @@
 // the only per-pixel libm call left is pow() in finalize (SVAO Common.slang:326-330).
 #include <cfloat>
 #include <cmath>
+#include <mutex>
 #include <vector>
 
 #include "rsd_device.h"
@@ -282,14 +283,12 @@ __global__ void __launch_bounds__(kP2Lanes) svao_pass2_kernel(SvaoArgs a) {
 
 namespace rsd {
 namespace {
-struct SnapCache {
-    int w = -1, h = -1;
-    float* d = nullptr;
-};
-thread_local SnapCache g_snap;
-}  // namespace
+// Device-resident constant tables, cached per device for the life of the process (a few KB to
+// 1 MB each, never freed: a table may still be read by kernels in flight on any stream).
+// Process-wide with a lock: one rsd_device per GPU per host thread (rsd.h), any thread, any GPU.
+constexpr int kMaxDevices = 64;
+std::mutex g_tab_mutex;
 
-namespace {
 __global__ void normal_lut_kernel(float4* lut) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < 65536u) {
@@ -297,47 +296,63 @@ __global__ void normal_lut_kernel(float4* lut) {
         lut[i] = make_float4(n.x, n.y, n.z, 0.0f);
     }
 }
-struct NormalLut {
-    int dev = -1;
-    float4* d = nullptr;
+float4* g_nlut[kMaxDevices] = {};
+
+struct SnapTable {
+    int w, h;
+    float* d;
 };
-thread_local NormalLut g_nlut;
+std::vector<SnapTable> g_snap[kMaxDevices];  // per device: one table per frame-buffer size
+
+int current_device(int* dev) {
+    if (hipGetDevice(dev) != hipSuccess || *dev < 0 || *dev >= kMaxDevices) return -1;
+    return 0;
+}
 }  // namespace
 
 rsd_status normal_lut(const float4** out) {
     int dev = 0;
-    RSD_HIP(hipGetDevice(&dev));
-    NormalLut& c = g_nlut;
-    if (c.dev != dev || !c.d) {
+    if (current_device(&dev)) {
+        set_error("normal_lut: no current HIP device (or device index >= 64)");
+        return RSD_ERR_NO_DEVICE;
+    }
+    std::lock_guard<std::mutex> lock(g_tab_mutex);
+    if (!g_nlut[dev]) {
         float4* d = nullptr;
         RSD_HIP(hipMalloc(&d, 65536 * sizeof(float4)));
         hipLaunchKernelGGL(normal_lut_kernel, dim3(256), dim3(256), 0, (hipStream_t)0, d);
         RSD_HIP(hipGetLastError());
-        RSD_HIP(hipDeviceSynchronize());  // once per device and host thread
-        c.d = d;
-        c.dev = dev;
+        RSD_HIP(hipDeviceSynchronize());  // once per device
+        g_nlut[dev] = d;
     }
-    *out = c.d;
+    *out = g_nlut[dev];
     return RSD_OK;
 }
 
+// pixel-centre UVs (k + 0.5) / resolution of every column and row of the frame buffer
 rsd_status snap_tables(const rsd_vao_data& vd, const float** u, const float** v) {
     const int w = (int)vd.resolution[0], h = (int)vd.resolution[1];
-    SnapCache& c = g_snap;
-    if (c.w != w || c.h != h) {
-        std::vector<float> t((size_t)w + 1 + (size_t)h + 1);
-        for (int k = 0; k <= w; ++k) t[k] = ((float)k + 0.5f) / vd.resolution[0];
-        for (int k = 0; k <= h; ++k) t[(size_t)w + 1 + k] = ((float)k + 0.5f) / vd.resolution[1];
-        (void)hipFree(c.d);
-        c.d = nullptr;
-        c.w = c.h = -1;
-        RSD_HIP(hipMalloc(&c.d, t.size() * sizeof(float)));
-        RSD_HIP(hipMemcpy(c.d, t.data(), t.size() * sizeof(float), hipMemcpyHostToDevice));
-        c.w = w;
-        c.h = h;
+    int dev = 0;
+    if (current_device(&dev)) {
+        set_error("snap_tables: no current HIP device (or device index >= 64)");
+        return RSD_ERR_NO_DEVICE;
     }
-    *u = c.d;
-    *v = c.d + w + 1;
+    std::lock_guard<std::mutex> lock(g_tab_mutex);
+    for (const SnapTable& t : g_snap[dev])
+        if (t.w == w && t.h == h) {
+            *u = t.d;
+            *v = t.d + w + 1;
+            return RSD_OK;
+        }
+    std::vector<float> t((size_t)w + 1 + (size_t)h + 1);
+    for (int k = 0; k <= w; ++k) t[k] = ((float)k + 0.5f) / vd.resolution[0];
+    for (int k = 0; k <= h; ++k) t[(size_t)w + 1 + k] = ((float)k + 0.5f) / vd.resolution[1];
+    float* d = nullptr;
+    RSD_HIP(hipMalloc(&d, t.size() * sizeof(float)));
+    RSD_HIP(hipMemcpy(d, t.data(), t.size() * sizeof(float), hipMemcpyHostToDevice));
+    g_snap[dev].push_back({w, h, d});
+    *u = d;
+    *v = d + w + 1;
     return RSD_OK;
 }
 }  // namespace rsd

@@ -52,7 +52,7 @@ class AlphaDesc(C.Structure):
 class SceneInfo(C.Structure):
     _fields_ = [("triangle_count", C.c_uint32), ("node_count", C.c_uint32), ("max_depth", C.c_uint32),
                 ("leaf_count", C.c_uint32), ("sah_cost", C.c_double), ("build_ms", C.c_double),
-                ("device_bytes", C.c_uint64)]
+                ("device_bytes", C.c_uint64), ("build_threads", C.c_uint32), ("reserved", C.c_uint32)]
 
 
 class Camera(C.Structure):
@@ -68,7 +68,7 @@ class SDParams(C.Structure):
     _fields_ = [("sample_count", C.c_uint32), ("implementation", C.c_uint32), ("max_count", C.c_uint32),
                 ("guard_band", C.c_int32), ("jitter", C.c_uint32), ("normalize", C.c_uint32),
                 ("ray_interval", C.c_uint32), ("cull_mode", C.c_uint32), ("alpha_test", C.c_uint32),
-                ("alpha", C.c_float)]
+                ("alpha", C.c_float), ("hit_order", C.c_uint32), ("use_16bit", C.c_uint32)]
 
 
 class VAOData(C.Structure):
@@ -88,7 +88,16 @@ class Counters(C.Structure):
     _fields_ = [("rays_dispatched", C.c_uint64), ("rays_active", C.c_uint64), ("nodes_visited", C.c_uint64),
                 ("tris_tested", C.c_uint64), ("hits_delivered", C.c_uint64), ("max_nodes_per_ray", C.c_uint64),
                 ("max_steps_per_ray", C.c_uint64), ("sum_ray_clocks", C.c_uint64), ("max_ray_clocks", C.c_uint64),
-                ("leaves_visited", C.c_uint64)]
+                ("leaves_visited", C.c_uint64), ("walk", C.c_uint64)]
+
+
+WALK_QUAD, WALK_FUSED, WALK_SPLIT, WALK_ORDERED = 0, 1, 2, 3
+HIT_ORDER_CANONICAL, HIT_ORDER_TRAVERSAL = 0, 1
+# kernels of one rsd_sd_trace per walk (rsd_counters.walk)
+WALK_KERNELS = {WALK_QUAD: ("sd_setup_kernel", "sd_trace_queue_kernel"),
+                WALK_FUSED: ("sd_setup_kernel", "sd_trace_row_kernel"),
+                WALK_SPLIT: ("sd_setup_kernel", "sd_trace_row_kernel", "sd_resolve_row_kernel"),
+                WALK_ORDERED: ("sd_setup_kernel", "sd_trace_ordered_kernel")}
 
 
 # every symbol include/rsd.h declares (checked by tests/test_abi.py)

@@ -72,15 +72,54 @@ CONFIGS = {
                            "bistro_exterior"),
 }
 
+# BASELINE.json configs[0]: the Arcade plumbing case -- 256 x 256, SD N = 1, divisor 1, the SD
+# pass driven directly with GuardBand 0 (no SVAO guard band, no SD guard band)
+ARCADE_CONFIG = (dict(visible_w=256, visible_h=256, guard_band=0, divisor=1, sd_samples=1, sd_guard_px=0),
+                 "arcade_tiny")
 
-def make_camera(scene: Scene, cfg: FrameConfig) -> abi.Camera:
+# camera path of each config when the bench animates it (BASELINE configs[4]: 120-frame animated camera)
+DEFAULT_CAMERA_PATH = {"bistro_4k_full_n16": "orbit120"}
+
+
+def look_at(pos, target, up, cfg: FrameConfig) -> abi.Camera:
+    """Camera::calculateCameraParameters through librsd (rsd_camera_look_at, Camera.cpp:99-185)."""
     cam = abi.Camera()
     f3 = lambda v: (C.c_float * 3)(*[float(x) for x in v])
     aspect = np.float32(cfg.fb_w) / np.float32(cfg.fb_h)
-    abi.check(abi.lib().rsd_camera_look_at(f3(scene.camera["pos"]), f3(scene.camera["target"]), f3(scene.camera["up"]),
-                                           cfg.focal_length, cfg.frame_height, float(aspect), cfg.near, cfg.far,
-                                           10000.0, C.byref(cam)), "rsd_camera_look_at")
+    abi.check(abi.lib().rsd_camera_look_at(f3(pos), f3(target), f3(up), cfg.focal_length, cfg.frame_height,
+                                           float(aspect), cfg.near, cfg.far, 10000.0, C.byref(cam)),
+              "rsd_camera_look_at")
     return cam
+
+
+def make_camera(scene: Scene, cfg: FrameConfig) -> abi.Camera:
+    return look_at(scene.camera["pos"], scene.camera["target"], scene.camera["up"], cfg)
+
+
+def camera_path(name: str, seed: int = 5):
+    """Look-at poses (pos, target, up) of a named camera path -- the animated camera of
+    BASELINE configs[4] (the reference benchmarks along camera paths with PathBenchmark,
+    PathBenchmark.cpp:59-90, scripts/SVAO.py:23,54).
+
+    "orbitN": N poses on a closed orbit of the synthetic hall (room 40 x 12 x 40, rsd/scenes.py):
+    radius 17 m at 5.5 m height (above every prop, clear of the colonnades at x = +-12.8, which
+    are the only full-height objects), bobbing +-0.5 m, looking at a target that wanders around
+    the hall centre.  The start angle and the wander phases come from `seed`.  "static": the
+    scene's own camera (one pose)."""
+    if name == "static":
+        return None
+    if not name.startswith("orbit"):
+        raise ValueError(f"unknown camera path '{name}' (static, orbitN)")
+    n = int(name[5:] or 120)
+    rng = np.random.default_rng(seed)
+    a0, p1, p2 = rng.uniform(0.0, 2.0 * np.pi, 3)
+    poses = []
+    for i in range(n):
+        a = a0 + 2.0 * np.pi * i / n
+        pos = [17.0 * np.cos(a), 5.5 + 0.5 * np.sin(2.0 * a + p1), 17.0 * np.sin(a)]
+        tgt = [2.0 * np.cos(3.0 * a + p2), 1.0, 2.0 * np.sin(2.0 * a + p1)]
+        poses.append(([float(np.float32(v)) for v in pos], [float(np.float32(v)) for v in tgt], [0.0, 1.0, 0.0]))
+    return poses
 
 
 def make_vao(cfg: FrameConfig):
@@ -184,11 +223,13 @@ class Renderer:
         self.ray_min, self.ray_max = self.ray_minmax[0], self.ray_minmax[1]
         self.sd = torch.empty(((N + 3) // 4, self.sd_h, self.sd_w, min(N, 4)), dtype=torch.float32, device=dv)
 
-    def frame_slot(self) -> "Renderer":
+    def frame_slot(self, own_gbuffer: bool = False) -> "Renderer":
         """Another set of per-frame buffers (ao, stencil, intervals, SD map) over the same scene,
         camera and G-buffer: the state of one more frame in flight.  Frames of different slots
         may run concurrently on different streams -- librsd keeps the SD-trace workspace per
-        (scene, stream) -- while frames of one slot stay ordered on its stream."""
+        (scene, stream) -- while frames of one slot stay ordered on its stream.
+        own_gbuffer=True: the slot also gets its own camera and G-buffer (an animated camera:
+        every frame in flight renders its own pose)."""
         import copy
         t = self.torch
         r = copy.copy(self)
@@ -198,7 +239,17 @@ class Renderer:
         r.ray_minmax = t.empty_like(self.ray_minmax)
         r.ray_min, r.ray_max = r.ray_minmax[0], r.ray_minmax[1]
         r.sd = t.empty_like(self.sd)
+        if own_gbuffer:
+            r.cam = abi.Camera.from_buffer_copy(self.cam)
+            r.depth = t.empty_like(self.depth)
+            r.normals = t.empty_like(self.normals)
         return r
+
+    def set_pose(self, pos, target, up):
+        """Move the camera (an animated camera path): the next gbuffer() / frame() render this
+        pose.  librsd copies the camera into every launch's arguments, so frames already
+        enqueued keep the pose they were issued with."""
+        self.cam = look_at(pos, target, up, self.cfg)
 
     @property
     def stream(self):
