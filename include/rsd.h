@@ -205,6 +205,10 @@ rsd_status rsd_scene_info_get(const rsd_scene* scene, rsd_scene_info* out);
  * from float4 offset *tri_offset.  dst == NULL: only *bytes.  Synchronous. */
 rsd_status rsd_scene_export_bvh(const rsd_scene* scene, void* dst, uint64_t capacity, uint64_t* bytes,
                                 uint32_t* tri_offset);
+/* The same bytes without a GPU: the host build rsd_scene_upload would upload for `desc`
+ * (deterministic: same desc, same tree).  dst == NULL: only *bytes. */
+rsd_status rsd_bvh_build(const rsd_scene_desc* desc, void* dst, uint64_t capacity, uint64_t* bytes,
+                         uint32_t* tri_offset);
 void rsd_scene_release(rsd_scene* scene);
 
 /* --- host helpers (no GPU work) ---------------------------------------------------- */

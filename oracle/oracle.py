@@ -76,6 +76,8 @@ def lib():
         L.ocpu_sd_ray.argtypes = [vp, vp, vp, u32, u32, vp, vp, u32, u32, u32, u32, vp, vp, vp, vp]
         L.ocpu_svao_clear.argtypes = [vp, vp, u32]
         L.ocpu_sd_trace_band.argtypes = [vp, vp, vp, vp, u32, u32, vp, vp, vp, u32, u32, u32, u32, u32, u32, i32, vp]
+        L.ocpu_sd_trace_ordered.argtypes = [vp, vp, u32, vp, vp, vp, u32, u32, vp, vp, vp, u32, u32, u32, u32, u32, u32,
+                                            i32, vp]
         L.ocpu_svao_pass1_band.argtypes = [vp, vp, vp, vp, vp, u32, u32, vp, vp, vp, vp, u32, u32, u32, u32]
         L.ocpu_svao_pass2_band.argtypes = [vp, vp, vp, vp, vp, u32, u32, vp, vp, u32, u32, vp, u32, u32, i32]
         L.ocpu_svao_pass1.argtypes = [vp, vp, vp, vp, vp, u32, u32, vp, vp, vp, vp, u32, u32]
@@ -200,6 +202,9 @@ def compress_normals(normal_w, cam: Camera):
 
 def sd_trace(scene: Scene, cam: Camera, params: SDParams, linearZ, rayMin, rayMax, sdW, sdH,
              rows=None, threads=None):
+    """The SD trace over the canonical any-hit stream (ascending (t, prim)); independent of any BVH."""
+    if params.hit_order != 0:
+        raise ValueError("hit_order = traversal needs librsd's BVH: use sd_trace_ordered()")
     N = params.sample_count
     ch, layers = min(N, 4), (N + 3) // 4
     sd = np.zeros((layers, sdH, sdW, ch), np.float32)
@@ -208,6 +213,24 @@ def sd_trace(scene: Scene, cam: Camera, params: SDParams, linearZ, rayMin, rayMa
     lz = np.ascontiguousarray(linearZ, np.float32)
     lib().ocpu_sd_trace(scene.h, C.byref(cam), C.byref(params), _p(lz), lz.shape[1], lz.shape[0],
                         _p(rayMin), _p(rayMax), _p(sd), sdW, sdH, r0, r1, _threads(threads), _p(stats))
+    return sd, stats
+
+
+def sd_trace_ordered(scene: Scene, bvh, tri_offset, cam: Camera, params: SDParams, linearZ, rayMin, rayMax, sdW, sdH,
+                     rows=None, band=(0, 1), threads=None):
+    """The SD trace over librsd's traversal-order any-hit stream (rsd.h RSD_HIT_ORDER_TRAVERSAL), walking
+    librsd's own BVH: `bvh` = the float32 array of rsd_scene_export_bvh, tri_offset in float4 units.
+    `scene` supplies the alpha-masked materials."""
+    N = params.sample_count
+    ch, layers = min(N, 4), (N + 3) // 4
+    sd = np.zeros((layers, sdH, sdW, ch), np.float32)
+    r0, r1 = rows if rows else (0, sdH)
+    stats = np.zeros(2, np.uint64)
+    lz = np.ascontiguousarray(linearZ, np.float32)
+    b = np.ascontiguousarray(bvh, np.float32)
+    lib().ocpu_sd_trace_ordered(scene.h, _p(b), int(tri_offset), C.byref(cam), C.byref(params), _p(lz), lz.shape[1],
+                                lz.shape[0], _p(rayMin), _p(rayMax), _p(sd), sdW, sdH, r0, r1, band[0], band[1],
+                                _threads(threads), _p(stats))
     return sd, stats
 
 

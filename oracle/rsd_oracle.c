@@ -942,6 +942,167 @@ void ocpu_sd_ray(const ocam* c, const osd_params* p, const float* z, uint32_t zW
     for (int i = 0; i < 3; ++i) { out[i] = c->posW[i]; out[3 + i] = d[i]; }
 }
 
+/* anyHit -> algorithm (Common.slangh:102-254) for ONE delivered hit: rng = hash(barycentrics),
+ * t = (normalized) view depth, af = the alpha test failed.  Returns the commit decision (the
+ * any-hit shader does not IgnoreHit: DXR accepts the hit, TMax = t). */
+static int o_any_hit(const osd_params* p, uint32_t N, const int32_t* lutIdx, const uint32_t* lut,
+                     float* depths, uint32_t* count, float rng, float t, int af)
+{
+    if (p->implementation == 1) { /* CoverageMask, Common.slangh:117-131, 189-209 */
+        int R = (int)floorf(p->alpha * (float)N + rng);
+        uint32_t mask = 0;
+        if (R >= (int)N) mask = 0xffffu;
+        else if (R != 0) {
+            float rng2 = ocpu_hash(rng, t); /* hash3D(float3(bary, t)) */
+            float a = (float)lutIdx[R], b = (float)lutIdx[R + 1];
+            int index = (int)(a + rng2 * (b - a));
+            mask = lut[index];
+        }
+        if (af) return *count >= p->max_count; /* alpha test failed: ignore (count stays 0) */
+        float maxT = 0.0f;
+        for (uint32_t i = 0; i < N; ++i) {
+            if (mask & (1u << i))
+                if (t < depths[i]) depths[i] = t;
+            maxT = o_max(maxT, depths[i]);
+        }
+        return !(t < maxT);
+    } else if (p->implementation == 3) { /* KBuffer, Common.slangh:132-135, 211-232 */
+        if (t >= depths[N - 1]) return 1;
+        (*count)++;
+        if (af) return *count >= p->max_count;
+        float rayT = t;
+        for (uint32_t i = 0; i < N; ++i)
+            if (t < depths[i]) { float tmp = depths[i]; depths[i] = t; t = tmp; }
+        return (depths[N - 1] == rayT) ? 1 : (*count >= p->max_count);
+    } else { /* Default: reservoir, Common.slangh:136-153, 234-247 */
+        uint32_t slot = (*count)++;
+        if (*count > N) slot = (uint32_t)(rng * (float)*count);
+        if (slot < N && !(depths[slot] <= t) && !af) depths[slot] = t;
+        return *count >= p->max_count;
+    }
+}
+
+/* ---- traversal-order any-hit stream (rsd.h RSD_HIT_ORDER_TRAVERSAL) ----------------------
+ * DXR's any-hit order is the driver's traversal order (third-party, not in the reference), so
+ * librsd DEFINES one: a depth-first walk of its own 4-wide BVH (exported by rsd_scene_export_bvh),
+ * children nearest entry distance first, leaf triangles in record order, each triangle once; a
+ * committed hit sets TMax = t and later candidates must satisfy t < TMax (RayTCurrent()).  This
+ * restates that definition (librsd csrc/sd_trace.hip sd_trace_ordered_ray, box test
+ * csrc/bvh_traverse.h box_hit) over the same tree, so the GPU result is checked bit for bit;
+ * the per-hit algorithm is the reference's (o_any_hit). */
+typedef struct { float invd[3], oinvd[3]; } obox_ray;
+
+static void o_box_setup(obox_ray* b, const float o[3], const float d[3])
+{
+    for (int i = 0; i < 3; ++i) {
+        const float v = fabsf(d[i]) > 1e-20f ? d[i] : copysignf(1e-20f, d[i]); /* axis-parallel rays */
+        b->invd[i] = 1.0f / v;
+        b->oinvd[i] = o[i] * b->invd[i];
+    }
+}
+
+/* conservative slab test, entry/exit widened by a relative 1e-5 (librsd box_hit) */
+static int o_box4(const obox_ray* b, float lox, float hix, float loy, float hiy, float loz, float hiz, float tlo,
+                  float thi, float* tnear)
+{
+    const float x0 = fmaf(lox, b->invd[0], -b->oinvd[0]), x1 = fmaf(hix, b->invd[0], -b->oinvd[0]);
+    const float y0 = fmaf(loy, b->invd[1], -b->oinvd[1]), y1 = fmaf(hiy, b->invd[1], -b->oinvd[1]);
+    const float z0 = fmaf(loz, b->invd[2], -b->oinvd[2]), z1 = fmaf(hiz, b->invd[2], -b->oinvd[2]);
+    float tn = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fminf(z0, z1));
+    float tf = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fmaxf(z0, z1));
+    const float m = 1e-5f * (fabsf(tn) + fabsf(tf));
+    tn -= m;
+    tf += m;
+    *tnear = tn;
+    return fmaxf(tn, tlo) <= fminf(tf, thi);
+}
+
+static void o_cswap4(float* k, uint32_t* it, int a, int b)
+{
+    if (k[b] < k[a]) {
+        const float t = k[a]; k[a] = k[b]; k[b] = t;
+        const uint32_t u = it[a]; it[a] = it[b]; it[b] = u;
+    }
+}
+
+/* Walks one SD ray; returns the number of hits delivered to the any-hit algorithm. */
+static uint64_t o_ordered_walk(const oscene* s, const float* bvh, uint32_t triOff, const ocam* c,
+                               const osd_params* p, const float d[3], float TMin, float TMax, float cosT,
+                               float spread, const int32_t* lutIdx, const uint32_t* lut, float* depths,
+                               uint32_t* count)
+{
+    const uint32_t LEAF = 0x80000000u, OFF = 0x1fffffffu, NONE = 0xffffffffu;
+    const uint32_t N = p->sample_count;
+    oray r;
+    o_ray_setup(&r, c->posW, d);
+    obox_ray b;
+    o_box_setup(&b, c->posW, d);
+    uint32_t stItem[128];
+    float stT[128];
+    int sp = 0, committed = 0;
+    float tCur = TMax;
+    uint64_t delivered = 0;
+    uint32_t item = 0; /* root */
+    for (;;) {
+        const uint32_t off = item & OFF;
+        uint32_t next = NONE;
+        if (item & LEAF) {
+            const uint32_t n = ((item >> 29) & 3u) + 1u;
+            for (uint32_t q = 0; q < n; ++q) {
+                const float* tp = bvh + 4u * (off + 3u * q); /* {v0, prim}{v1, flags}{v2, 0} */
+                float t, bu, bv, det;
+                if (!o_intersect_tri(&r, tp, tp + 4, tp + 8, &t, &bu, &bv, &det)) continue;
+                if (!(t >= TMin) || (committed ? !(t < tCur) : !(t <= tCur))) continue;
+                const uint32_t prim = o_asuint(tp[3]), flags = o_asuint(tp[7]);
+                if (o_culled(det, flags, p->cull_mode)) continue; /* ray flags: before any-hit */
+                delivered++;
+                const float rng = ocpu_hash(bu, bv);
+                float z = t * cosT; /* RayToViewDepth */
+                if (p->normalize) z = o_saturate((z - c->nearZ) / (c->farZ - c->nearZ));
+                const int af = p->alpha_test && o_alpha_masked(s, prim) &&
+                               ocpu_alpha_fails(s, prim, bu, bv, 1, t, d, spread);
+                if (o_any_hit(p, N, lutIdx, lut, depths, count, rng, z, af)) {
+                    tCur = t; /* AcceptHit: TMax = t */
+                    committed = 1;
+                }
+            }
+        } else {
+            const float* nb = bvh + 4u * off; /* lo.x[4] hi.x[4] lo.y[4] hi.y[4] lo.z[4] hi.z[4] ref[4] cnt[4] */
+            float k[4];
+            uint32_t it[4];
+            int m = 0;
+            for (int q = 0; q < 4; ++q) {
+                const uint32_t ref = o_asuint(nb[24 + q]), cnt = o_asuint(nb[28 + q]);
+                float tn = 0.0f;
+                const int hit = ref != NONE && o_box4(&b, nb[q], nb[4 + q], nb[8 + q], nb[12 + q], nb[16 + q],
+                                                      nb[20 + q], TMin, tCur, &tn);
+                k[q] = hit ? tn : INFINITY;
+                it[q] = hit ? (cnt ? (LEAF | ((cnt - 1u) << 29) | (triOff + 3u * ref)) : 8u * ref) : NONE;
+                m += hit;
+            }
+            o_cswap4(k, it, 0, 1); o_cswap4(k, it, 2, 3);
+            o_cswap4(k, it, 0, 2); o_cswap4(k, it, 1, 3);
+            o_cswap4(k, it, 1, 2);
+            next = it[0];
+            for (int q = m - 1; q >= 1; --q) { /* the nearest of the rest on top */
+                if (sp >= 128) abort();
+                stItem[sp] = it[q];
+                stT[sp] = k[q];
+                ++sp;
+            }
+        }
+        if (next == NONE) {
+            while (sp > 0) {
+                --sp;
+                if (stT[sp] <= tCur) { next = stItem[sp]; break; }
+            }
+            if (next == NONE) break;
+        }
+        item = next;
+    }
+    return delivered;
+}
+
 typedef struct {
     const oscene* s; const ocam* c; const osd_params* p;
     const float* z; uint32_t zW, zH;
@@ -950,6 +1111,7 @@ typedef struct {
     uint32_t y0, y1;
     uint32_t bi, bc; /* band: 8-row tile rows t with t % bc == bi */
     uint64_t active, hits;
+    const float* bvh; uint32_t triOff; /* p->hit_order == 1: librsd's exported BVH */
 } osd_job;
 
 static void* o_sd_rows(void* arg)
@@ -980,7 +1142,11 @@ static void* o_sd_rows(void* arg)
             for (uint32_t i = 0; i < N; ++i) depths[i] = DEFAULT;
             uint32_t count = 0;
 
-            if (TMin <= TMax) {
+            if (TMin <= TMax && p->hit_order == 1) {
+                j->active++;
+                j->hits += o_ordered_walk(j->s, j->bvh, j->triOff, c, p, d, TMin, TMax, cosT, spread, lutIdx, lut,
+                                          depths, &count);
+            } else if (TMin <= TMax) {
                 j->active++;
                 oray r;
                 o_ray_setup(&r, c->posW, d);
@@ -997,48 +1163,8 @@ static void* o_sd_rows(void* arg)
                     /* USE_ALPHA_TEST, Common.slangh:155-175: ray-cone LOD at RayTCurrent() */
                     const int af = p->alpha_test && o_alpha_masked(j->s, hs.h[k].prim) &&
                                    ocpu_alpha_fails(j->s, hs.h[k].prim, hs.h[k].u, hs.h[k].v, 1, hs.h[k].t, d, spread);
-                    int commit;
-                    if (p->implementation == 1) { /* CoverageMask */
-                        int R = (int)floorf(p->alpha * (float)N + rng);
-                        uint32_t mask = 0;
-                        if (R >= (int)N) mask = 0xffffu;
-                        else if (R != 0) {
-                            float rng2 = ocpu_hash(rng, t); /* hash3D(float3(bary, t)) */
-                            float a = (float)lutIdx[R], b = (float)lutIdx[R + 1];
-                            int index = (int)(a + rng2 * (b - a));
-                            mask = lut[index];
-                        }
-                        if (af) { /* alpha test failed: ignore (count stays 0) */
-                            if (count >= p->max_count) break;
-                            continue;
-                        }
-                        float maxT = 0.0f;
-                        for (uint32_t i = 0; i < N; ++i) {
-                            if (mask & (1u << i))
-                                if (t < depths[i]) depths[i] = t;
-                            maxT = o_max(maxT, depths[i]);
-                        }
-                        commit = !(t < maxT);
-                    } else if (p->implementation == 3) { /* KBuffer */
-                        if (t >= depths[N - 1]) { commit = 1; }
-                        else {
-                            count++;
-                            if (af) {
-                                if (count >= p->max_count) break;
-                                continue;
-                            }
-                            float rayT = t;
-                            for (uint32_t i = 0; i < N; ++i)
-                                if (t < depths[i]) { float tmp = depths[i]; depths[i] = t; t = tmp; }
-                            commit = (depths[N - 1] == rayT) ? 1 : (count >= p->max_count);
-                        }
-                    } else { /* Default: reservoir */
-                        uint32_t slot = count++;
-                        if (count > N) slot = (uint32_t)(rng * (float)count);
-                        if (slot < N && !(depths[slot] <= t) && !af) depths[slot] = t;
-                        commit = count >= p->max_count;
-                    }
-                    if (commit) break; /* committed hit: TMax = t, stream ends */
+                    if (o_any_hit(p, N, lutIdx, lut, depths, &count, rng, t, af))
+                        break; /* committed hit: TMax = t, stream ends */
                 }
                 free(hs.h);
             }
@@ -1065,12 +1191,42 @@ void ocpu_sd_trace(const oscene* s, const ocam* cam, const osd_params* p,
     ocpu_sd_trace_band(s, cam, p, linearZ, zW, zH, rayMin, rayMax, sd, sdW, sdH, row0, row1, 0, 1, nthreads, stats);
 }
 
+static void o_sd_trace_impl(const oscene* s, const float* bvh, uint32_t triOff, const ocam* cam,
+                            const osd_params* p, const float* linearZ, uint32_t zW, uint32_t zH,
+                            const uint32_t* rayMin, const uint32_t* rayMax, float* sd, uint32_t sdW, uint32_t sdH,
+                            uint32_t row0, uint32_t row1, uint32_t band_index, uint32_t band_count, int nthreads,
+                            uint64_t* stats);
+
 void ocpu_sd_trace_band(const oscene* s, const ocam* cam, const osd_params* p,
                         const float* linearZ, uint32_t zW, uint32_t zH,
                         const uint32_t* rayMin, const uint32_t* rayMax,
                         float* sd, uint32_t sdW, uint32_t sdH,
                         uint32_t row0, uint32_t row1, uint32_t band_index, uint32_t band_count,
                         int nthreads, uint64_t* stats)
+{
+    osd_params q = *p;
+    q.hit_order = 0; /* the canonical stream (ocpu_sd_trace_ordered for the traversal order) */
+    o_sd_trace_impl(s, NULL, 0, cam, &q, linearZ, zW, zH, rayMin, rayMax, sd, sdW, sdH, row0, row1, band_index,
+                    band_count, nthreads, stats);
+}
+
+void ocpu_sd_trace_ordered(const oscene* s, const float* bvh, uint32_t tri_offset, const ocam* cam,
+                           const osd_params* p, const float* linearZ, uint32_t zW, uint32_t zH,
+                           const uint32_t* rayMin, const uint32_t* rayMax, float* sd, uint32_t sdW, uint32_t sdH,
+                           uint32_t row0, uint32_t row1, uint32_t band_index, uint32_t band_count, int nthreads,
+                           uint64_t* stats)
+{
+    osd_params q = *p;
+    q.hit_order = 1;
+    o_sd_trace_impl(s, bvh, tri_offset, cam, &q, linearZ, zW, zH, rayMin, rayMax, sd, sdW, sdH, row0, row1,
+                    band_index, band_count, nthreads, stats);
+}
+
+static void o_sd_trace_impl(const oscene* s, const float* bvh, uint32_t triOff, const ocam* cam,
+                            const osd_params* p, const float* linearZ, uint32_t zW, uint32_t zH,
+                            const uint32_t* rayMin, const uint32_t* rayMax, float* sd, uint32_t sdW, uint32_t sdH,
+                            uint32_t row0, uint32_t row1, uint32_t band_index, uint32_t band_count, int nthreads,
+                            uint64_t* stats)
 {
     if (nthreads < 1) nthreads = 1;
     osd_job* jobs = (osd_job*)calloc((size_t)nthreads, sizeof(osd_job));
@@ -1080,6 +1236,7 @@ void ocpu_sd_trace_band(const oscene* s, const ocam* cam, const osd_params* p,
         jobs[i].rmin = rayMin; jobs[i].rmax = rayMax;
         jobs[i].sd = sd; jobs[i].sdW = sdW; jobs[i].sdH = sdH;
         jobs[i].bi = band_index; jobs[i].bc = band_count ? band_count : 1;
+        jobs[i].bvh = bvh; jobs[i].triOff = triOff;
     }
     if (row1 > sdH) row1 = sdH;
     o_run_rows(o_sd_rows, jobs, sizeof(osd_job), row0, row1, nthreads, o_sd_setrows);

@@ -129,6 +129,15 @@ void ocpu_sd_trace(const oscene* s, const ocam* cam, const osd_params* p,
                    float* sd, uint32_t sdW, uint32_t sdH,
                    uint32_t row0, uint32_t row1, int nthreads, uint64_t* stats);
 
+/* The same SD trace with librsd's traversal-order any-hit stream (rsd.h RSD_HIT_ORDER_TRAVERSAL)
+ * over librsd's own BVH: bvh = the rsd_scene_export_bvh bytes, tri_offset in float4 units.
+ * s supplies the alpha-masked materials (by primitive id).  Rows [row0, row1), band of tile rows. */
+void ocpu_sd_trace_ordered(const oscene* s, const float* bvh, uint32_t tri_offset, const ocam* cam,
+                           const osd_params* p, const float* linearZ, uint32_t zW, uint32_t zH,
+                           const uint32_t* rayMin, const uint32_t* rayMax, float* sd, uint32_t sdW, uint32_t sdH,
+                           uint32_t row0, uint32_t row1, uint32_t band_index, uint32_t band_count, int nthreads,
+                           uint64_t* stats);
+
 /* the SD ray of texel (x, y): origin+direction, TMin, TMax and cosT (for tests) */
 void ocpu_sd_ray(const ocam* c, const osd_params* p, const float* z, uint32_t zW, uint32_t zH,
                  const uint32_t* rmin, const uint32_t* rmax, uint32_t sdW, uint32_t sdH, uint32_t x, uint32_t y,

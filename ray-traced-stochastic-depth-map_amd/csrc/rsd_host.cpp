@@ -116,6 +116,7 @@ extern "C" rsd_status rsd_scene_upload(rsd_device* dev, const rsd_scene_desc* de
     }
     s->d_tris = s->d_nodes + s->tri_offset;
     s->device_bytes = total;
+    s->bvh_bytes = total;
     *out = s;
     return RSD_OK;
 }
@@ -271,6 +272,52 @@ extern "C" rsd_status rsd_scene_info_get(const rsd_scene* s, rsd_scene_info* out
     out->build_ms = s->stats.build_ms;
     out->device_bytes = s->device_bytes;
     out->build_threads = s->build_threads;
+    return RSD_OK;
+}
+
+extern "C" rsd_status rsd_bvh_build(const rsd_scene_desc* desc, void* dst, uint64_t capacity, uint64_t* bytes,
+                                    uint32_t* tri_offset) {
+    if (!desc || !bytes || (desc->triangle_count && (!desc->positions || !desc->indices))) {
+        set_error("rsd_bvh_build: null argument");
+        return RSD_ERR_INVALID_ARG;
+    }
+    for (uint64_t i = 0; i < 3ull * desc->triangle_count; ++i)
+        if (desc->indices[i] >= desc->vertex_count) {
+            set_error("rsd_bvh_build: index out of range of vertex_count");
+            return RSD_ERR_INVALID_ARG;
+        }
+    rsd::FlatBvh bvh = rsd::build_bvh(desc->positions, desc->vertex_count, desc->indices, desc->triangle_count,
+                                      desc->triangle_flags, build_threads());
+    const size_t nb = bvh.nodes.size() * sizeof(float), tb = bvh.tris.size() * sizeof(float);
+    *bytes = nb + tb + 12 * 16;  // the layout of rsd_scene_upload's allocation
+    if (tri_offset) *tri_offset = (uint32_t)(bvh.nodes.size() / 4);
+    if (!dst) return RSD_OK;
+    if (capacity < *bytes) {
+        set_error("rsd_bvh_build: capacity below the BVH size");
+        return RSD_ERR_INVALID_ARG;
+    }
+    std::memcpy(dst, bvh.nodes.data(), nb);
+    if (tb) std::memcpy(static_cast<char*>(dst) + nb, bvh.tris.data(), tb);
+    std::memset(static_cast<char*>(dst) + nb + tb, 0, 12 * 16);
+    return RSD_OK;
+}
+
+extern "C" rsd_status rsd_scene_export_bvh(const rsd_scene* s, void* dst, uint64_t capacity, uint64_t* bytes,
+                                           uint32_t* tri_offset) {
+    if (!s || !bytes) {
+        set_error("rsd_scene_export_bvh: null argument");
+        return RSD_ERR_INVALID_ARG;
+    }
+    *bytes = s->bvh_bytes;
+    if (tri_offset) *tri_offset = s->tri_offset;
+    if (!dst) return RSD_OK;
+    if (capacity < s->bvh_bytes) {
+        set_error("rsd_scene_export_bvh: capacity below the BVH size");
+        return RSD_ERR_INVALID_ARG;
+    }
+    if (s->bvh_bytes == 0) return RSD_OK;
+    RSD_HIP(hipSetDevice(s->dev->hip_device));
+    RSD_HIP(hipMemcpy(dst, s->d_nodes, s->bvh_bytes, hipMemcpyDeviceToHost));
     return RSD_OK;
 }
 

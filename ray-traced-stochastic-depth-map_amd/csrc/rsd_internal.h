@@ -71,6 +71,7 @@ struct rsd_scene {
     rsd::BvhStats stats;
     uint32_t build_threads = 0;  // host threads of the BVH build
     uint64_t device_bytes = 0;
+    uint64_t bvh_bytes = 0;      // the d_nodes allocation (nodes + triangle records + pad)
     std::vector<rsd::SdWorkspace*> sd_ws;  // one per stream that traced this scene (few: linear lookup)
     void* d_alpha = nullptr;       // alpha data (rsd_scene_upload_alpha), one allocation
     rsd::AlphaData alpha;          // device pointers into d_alpha

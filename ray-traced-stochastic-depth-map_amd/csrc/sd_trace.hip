@@ -65,6 +65,7 @@ struct SDArgs {
     uint32_t* rayMaxW;
     uint32_t alphaTest;   // USE_ALPHA_TEST and the scene has alpha data
     AlphaData alphaData;  // spread = RAY_CONE_SPREAD
+    uint32_t f16;         // Use16Bit: the map is R16F / RG16F / RGBA16F (N <= 4)
 };
 
 // Per-column and per-row terms of initRayDesc, evaluated once per frame size with exactly the
@@ -140,11 +141,29 @@ __device__ __forceinline__ bool sd_ray(const SDArgs& a, int x, int y, f3& d, flo
     return TMin <= TMax;
 }
 
-// store, StochasticDepthMapRT.rt.slang:90-104 (Texture2DArray layout [layer][y][x][ch])
+// store, StochasticDepthMapRT.rt.slang:90-104 (Texture2DArray layout [layer][y][x][ch]).
+// Use16Bit (StochasticDepthMapRT.cpp:192-198, N <= 4): the typed store converts to binary16,
+// round to nearest even (v_cvt_f16_f32; overflow -> inf, e.g. DEFAULT_DEPTH without NORMALIZE).
+__device__ __forceinline__ uint32_t f16_bits(float v) {
+    return (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)v);
+}
 template <int N>
 __device__ __forceinline__ void sd_store(const SDArgs& a, int x, int y, const float (&depths)[N]) {
     const size_t plane = (size_t)a.sdW * a.sdH;
     const size_t o = (size_t)y * a.sdW + x;
+    if constexpr (N <= 4) {
+        if (a.f16) {
+            if constexpr (N == 1) {
+                reinterpret_cast<uint16_t*>(a.sd)[o] = (uint16_t)f16_bits(depths[0]);
+            } else if constexpr (N == 2) {
+                reinterpret_cast<uint32_t*>(a.sd)[o] = f16_bits(depths[0]) | (f16_bits(depths[1]) << 16);
+            } else {
+                reinterpret_cast<uint2*>(a.sd)[o] = make_uint2(f16_bits(depths[0]) | (f16_bits(depths[1]) << 16),
+                                                               f16_bits(depths[2]) | (f16_bits(depths[3]) << 16));
+            }
+            return;
+        }
+    }
     if constexpr (N == 1) {
         a.sd[o] = depths[0];
     } else if constexpr (N == 2) {
@@ -154,6 +173,48 @@ __device__ __forceinline__ void sd_store(const SDArgs& a, int x, int y, const fl
         for (int l = 0; l < N / 4; ++l)
             reinterpret_cast<float4*>(a.sd)[l * plane + o] =
                 make_float4(depths[4 * l], depths[4 * l + 1], depths[4 * l + 2], depths[4 * l + 3]);
+    }
+}
+
+// anyHit -> algorithm (Common.slangh:102-254) for ONE delivered hit: hash `rng` of its
+// barycentrics, normalized view depth `z`, `af` = the alpha test failed.  Returns the commit
+// decision (true: the any-hit shader accepts the hit, DXR TMax = t).
+template <int N>
+__device__ __forceinline__ bool sd_any_hit(const SDArgs& a, float rng, float z, bool af, float (&depths)[N],
+                                           uint32_t& cnt) {
+    if (a.impl == 1u) {  // CoverageMask, Common.slangh:117-131, 189-209
+        const int R = (int)floorf(a.alpha * (float)N + rng);
+        uint32_t mask = 0u;
+        if (R >= N) mask = 0xffffu;
+        else if (R != 0) {
+            const float rng2 = sd_hash(rng, z);  // hash3D(float3(bary, t))
+            const float lo = (float)a.lutIdx[R], hi = (float)a.lutIdx[R + 1];
+            mask = a.lut[(int)(lo + rng2 * (hi - lo))];
+        }
+        if (af) return cnt >= a.maxCount;  // alpha test failed: ignore the hit (count is 0 here)
+        float maxT = 0.0f;
+#pragma unroll
+        for (int i = 0; i < N; ++i) {
+            if ((mask & (1u << i)) && z < depths[i]) depths[i] = z;
+            maxT = hmax(maxT, depths[i]);
+        }
+        return !(z < maxT);
+    } else if (a.impl == 3u) {  // KBuffer, Common.slangh:132-135, 211-232
+        if (z >= depths[N - 1]) return true;
+        cnt++;
+        if (af) return cnt >= a.maxCount;
+        const float rayT = z;
+#pragma unroll
+        for (int i = 0; i < N; ++i)
+            if (z < depths[i]) { const float tmp = depths[i]; depths[i] = z; z = tmp; }
+        return (depths[N - 1] == rayT) || cnt >= a.maxCount;
+    } else {  // Default reservoir, Common.slangh:136-153, 234-247
+        uint32_t slot = cnt++;
+        if (cnt > (uint32_t)N) slot = (uint32_t)(rng * (float)cnt);
+#pragma unroll
+        for (int i = 0; i < N; ++i)
+            if ((uint32_t)i == slot && !(depths[i] <= z) && !af) depths[i] = z;
+        return cnt >= a.maxCount;
     }
 }
 
@@ -341,49 +402,7 @@ __device__ __forceinline__ void sd_resolve(const SDArgs& a, f3 d, float TMin, fl
             const bool af = (qselu(afL, j % 4) >> (j / 4)) & 1u;
             if (commit || j >= found) continue;
             hitsDelivered++;
-            if (a.impl == 1u) {  // CoverageMask, Common.slangh:117-131, 189-209
-                const int R = (int)floorf(a.alpha * (float)N + rng);
-                uint32_t mask = 0u;
-                if (R >= N) mask = 0xffffu;
-                else if (R != 0) {
-                    const float rng2 = sd_hash(rng, z);  // hash3D(float3(bary, t))
-                    const float lo = (float)a.lutIdx[R], hi = (float)a.lutIdx[R + 1];
-                    mask = a.lut[(int)(lo + rng2 * (hi - lo))];
-                }
-                if (af) {  // alpha test failed: ignore the hit (count is 0 here)
-                    commit = count >= a.maxCount;
-                    continue;
-                }
-                float maxT = 0.0f;
-#pragma unroll
-                for (int i = 0; i < N; ++i) {
-                    if ((mask & (1u << i)) && z < depths[i]) depths[i] = z;
-                    maxT = hmax(maxT, depths[i]);
-                }
-                commit = !(z < maxT);
-            } else if (a.impl == 3u) {  // KBuffer, Common.slangh:132-135, 211-232
-                if (z >= depths[N - 1]) {
-                    commit = true;
-                } else {
-                    count++;
-                    if (af) {
-                        commit = count >= a.maxCount;
-                        continue;
-                    }
-                    const float rayT = z;
-#pragma unroll
-                    for (int i = 0; i < N; ++i)
-                        if (z < depths[i]) { const float tmp = depths[i]; depths[i] = z; z = tmp; }
-                    commit = (depths[N - 1] == rayT) || count >= a.maxCount;
-                }
-            } else {  // Default reservoir, Common.slangh:136-153, 234-247
-                uint32_t slot = count++;
-                if (count > (uint32_t)N) slot = (uint32_t)(rng * (float)count);
-#pragma unroll
-                for (int i = 0; i < N; ++i)
-                    if ((uint32_t)i == slot && !(depths[i] <= z) && !af) depths[i] = z;
-                commit = count >= a.maxCount;
-            }
+            commit = sd_any_hit<N>(a, rng, z, af, depths, count);
         }
         if (found < K) break;  // stream exhausted
         useLB = true;
@@ -534,6 +553,157 @@ __global__ void __launch_bounds__(kBlock) sd_trace_queue_kernel(SDArgs a, const 
 }
 
 // ------------------------------------------------------------------------------------
+// Traversal-order any-hit stream (rsd_sd_params.hit_order = RSD_HIT_ORDER_TRAVERSAL, rsd.h).
+// The DXR-like order: a depth-first walk of the 4-wide BVH, children nearest entry distance
+// first (the quad sorting network below; ties keep child-slot order), leaf triangles in record
+// order, each triangle delivered once to anyHit -> algorithm as it is found.  A committed hit
+// (Common.slangh: algorithm() == true, the any-hit shader does not IgnoreHit) shrinks the ray's
+// TMax to its t, and later candidates must be nearer (t < TMax), so the reservoir's random slot
+// replacement (Common.slangh:137-151) really samples: the texel depends on the BVH (the oracle
+// walks the same tree, rsd_scene_export_bvh).  A quad (4 lanes) walks one ray: lane q tests
+// child q / triangle q, the leaf's candidates are delivered one by one in record order with the
+// TMax test repeated against the current TMax.  All 4 lanes keep identical algorithm state.
+// ------------------------------------------------------------------------------------
+template <int N>
+__device__ __forceinline__ void sd_trace_ordered_ray(const SDArgs& a, f3 d, float TMin, float TMax, float cosT,
+                                                     float (&depths)[N], uint32_t* __restrict__ sItem,
+                                                     float* __restrict__ sT, int q, int quadBase, TraceStats& st,
+                                                     uint32_t& delivered) {
+    const rsd_camera& c = a.cam;
+    RayCtx r;
+    ray_setup(r, mk(c.posW[0], c.posW[1], c.posW[2]), d);
+    uint32_t cnt = 0;
+    float tCur = TMax;       // RayTCurrent(): TMax, then the t of the last committed hit
+    bool committed = false;  // after a commit only nearer hits (t < tCur) are candidates
+    int sp = 0;
+    uint32_t item = 0;       // the root node
+    const float* bf = reinterpret_cast<const float*>(a.nodes);
+    while (true) {
+        const uint32_t off = item & kOffMask;
+        uint32_t next = kNoItem;
+        if (item & kLeafBit) {
+            st.leaves++;
+            const uint32_t n = ((item >> 29) & 3u) + 1u;
+            bool cand = false, af = false;
+            float t = 0.0f, rng = 0.0f, z = 0.0f;
+            if ((uint32_t)q < n) {
+                const float4* tp = a.nodes + off + 3u * (uint32_t)q;
+                const float4 va = tp[0], vb = tp[1], vc = tp[2];
+                st.tris++;
+                float bu, bv, det;
+                if (intersect_tri(r, va, vb, vc, t, bu, bv, det) && t >= TMin && t <= tCur &&
+                    !culled(det, __float_as_uint(vb.w), a.cull)) {
+                    cand = true;
+                    rng = sd_hash(bu, bv);
+                    z = t * cosT;  // RayToViewDepth
+                    if (a.normalize) z = saturate((z - c.nearZ) / (c.farZ - c.nearZ));
+                    af = a.alphaTest && (__float_as_uint(vb.w) & 4u) &&
+                         alpha_test_fails(a.alphaData, __float_as_uint(va.w), va, vb, vc, bu, bv, true, t, r.d);
+                }
+            }
+            const uint32_t afBits = (uint32_t)(__ballot(af) >> quadBase) & 0xfu;
+            for (uint32_t m = (uint32_t)(__ballot(cand) >> quadBase) & 0xfu; m; m &= m - 1u) {
+                const int j = __ffs(m) - 1;
+                const float tj = qself(t, j), rj = qself(rng, j), zj = qself(z, j);
+                if (committed ? !(tj < tCur) : !(tj <= tCur)) continue;  // behind the committed hit
+                delivered++;
+                if (sd_any_hit<N>(a, rj, zj, ((afBits >> j) & 1u) != 0u, depths, cnt)) {
+                    tCur = tj;  // AcceptHit: TMax = t
+                    committed = true;
+                }
+            }
+        } else {
+            st.nodes++;
+            const float* nb = bf + 4u * off;
+            const float lox = nb[q], hix = nb[4 + q], loy = nb[8 + q], hiy = nb[12 + q], loz = nb[16 + q],
+                        hiz = nb[20 + q];
+            const uint32_t ref = __float_as_uint(nb[24 + q]), ccnt = __float_as_uint(nb[28 + q]);
+            float tn;
+            const bool hit = ref != kNoItem && box_hit(r, lox, hix, loy, hiy, loz, hiz, TMin, tCur, tn);
+            float k = hit ? tn : INFINITY;
+            uint32_t it = hit ? (ccnt ? (kLeafBit | ((ccnt - 1u) << 29) | (a.triOff + 3u * ref)) : 8u * ref) : kNoItem;
+            const int m = __popc((uint32_t)(__ballot(hit) >> quadBase) & 0xfu);
+            // sorting network (0,1)(2,3) (0,2)(1,3) (1,2): a pair swaps only if strictly out of order
+            quad_cx<kDppXor1>(k, it, (q & 1) == 0);
+            quad_cx<kDppXor2>(k, it, (q & 2) == 0);
+            {
+                const float ok = dppf<kDppXor3>(k);
+                const uint32_t oi = dppu<kDppXor3>(it);
+                const bool mid = q == 1 || q == 2;
+                const bool takeOther = mid && ((q == 1) ? (ok < k) : (k < ok));
+                k = takeOther ? ok : k;
+                it = takeOther ? oi : it;
+            }
+            next = qbcu<0>(it);
+            if (q >= 1 && q < m) {
+                const int slot = sp + (m - 1 - q);  // the nearest of the rest on top
+                sItem[slot * kQuadRays] = it;
+                sT[slot * kQuadRays] = k;
+            }
+            sp += m > 0 ? m - 1 : 0;
+        }
+        if (next == kNoItem) {
+            while (sp > 0) {
+                --sp;
+                if (sT[sp * kQuadRays] <= tCur) { next = sItem[sp * kQuadRays]; break; }
+            }
+            if (next == kNoItem) break;
+        }
+        item = next;
+    }
+}
+
+// Persistent waves over the live-ray queue (as sd_trace_queue_kernel), 16 rays per wave.
+template <int N>
+__global__ void __launch_bounds__(kBlock) sd_trace_ordered_kernel(SDArgs a, const float4* __restrict__ queue,
+                                                                  uint32_t* __restrict__ qctl) {
+    __shared__ uint32_t sItem[kQuadStack * kQuadRays];
+    __shared__ float sT[kQuadStack * kQuadRays];
+    const int lane = threadIdx.x;
+    const int q = lane & 3, quad = lane >> 2, quadBase = lane & ~3;
+    const uint32_t part = blockIdx.x % kQueueParts, wavesPerPart = gridDim.x / kQueueParts;
+    const uint32_t count = __hip_atomic_load(&qctl[part], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t slot0 = part * a.partCap;
+    const float DEFAULT = a.normalize ? 1.0f : 3.40282347e+37f;  // Common.slangh:16
+    TraceStats st{0u, 0u, 0u};
+    uint32_t active = 0, delivered = 0, maxNodes = 0, maxSteps = 0;
+    uint32_t base = (blockIdx.x / kQueueParts) * (uint32_t)kQuadRays;
+    while (base < count) {
+        const uint32_t qi = base + (uint32_t)quad;
+        if (qi < count) {
+            f3 d;
+            float TMin, TMax, cosT;
+            uint32_t idx;
+            ray_rec_load(queue, slot0 + qi, d, TMin, TMax, cosT, idx);
+            float depths[N];
+#pragma unroll
+            for (int i = 0; i < N; ++i) depths[i] = DEFAULT;
+            const uint32_t n0 = st.nodes, l0 = st.leaves;
+            sd_trace_ordered_ray<N>(a, d, TMin, TMax, cosT, depths, &sItem[quad], &sT[quad], q, quadBase, st,
+                                    delivered);
+            if (q == 0) {
+                maxNodes = max(maxNodes, st.nodes - n0);
+                maxSteps = max(maxSteps, st.nodes - n0 + st.leaves - l0);
+                active++;
+                sd_store<N>(a, (int)(idx % (uint32_t)a.sdW), (int)(idx / (uint32_t)a.sdW), depths);
+            }
+        }
+        if (lane == 0)
+            base = wavesPerPart * (uint32_t)kQuadRays + atomicAdd(&qctl[kQueueParts + part], (uint32_t)kQuadRays);
+        base = __shfl(base, 0);
+    }
+    if (a.counters) {
+        atomicAdd(&a.counters[1], (unsigned long long)active);
+        atomicAdd(&a.counters[2], (unsigned long long)(q == 0 ? st.nodes : 0u));
+        atomicAdd(&a.counters[3], (unsigned long long)st.tris);
+        atomicAdd(&a.counters[4], (unsigned long long)(q == 0 ? delivered : 0u));
+        atomicMax(&a.counters[5], (unsigned long long)maxNodes);
+        atomicMax(&a.counters[6], (unsigned long long)maxSteps);
+        atomicAdd(&a.counters[9], (unsigned long long)(q == 0 ? st.leaves : 0u));
+    }
+}
+
+// ------------------------------------------------------------------------------------
 // Row-parallel traversal (the default SD trace).  The quad walk above is depth-first: its
 // critical path is every node and leaf the ray visits, one dependent fetch after the other
 // (the slowest live ray of a 1080p/4 frame visits ~130 items, and the launch lasts as long
@@ -633,49 +803,7 @@ __device__ __forceinline__ bool sd_algorithm_row(const SDArgs& a, float rng, flo
         const bool af = (afm >> (base + j)) & 1u;
         if (commit || j >= found) continue;
         delivered++;
-        if (a.impl == 1u) {  // CoverageMask, Common.slangh:117-131, 189-209
-            const int R = (int)floorf(a.alpha * (float)N + rj);
-            uint32_t mask = 0u;
-            if (R >= N) mask = 0xffffu;
-            else if (R != 0) {
-                const float rng2 = sd_hash(rj, zj);  // hash3D(float3(bary, t))
-                const float lo = (float)a.lutIdx[R], hi = (float)a.lutIdx[R + 1];
-                mask = a.lut[(int)(lo + rng2 * (hi - lo))];
-            }
-            if (af) {  // alpha test failed: ignore the hit (count is 0 here)
-                commit = cnt >= a.maxCount;
-                continue;
-            }
-            float maxT = 0.0f;
-#pragma unroll
-            for (int i = 0; i < N; ++i) {
-                if ((mask & (1u << i)) && zj < depths[i]) depths[i] = zj;
-                maxT = hmax(maxT, depths[i]);
-            }
-            commit = !(zj < maxT);
-        } else if (a.impl == 3u) {  // KBuffer, Common.slangh:132-135, 211-232
-            if (zj >= depths[N - 1]) {
-                commit = true;
-            } else {
-                cnt++;
-                if (af) {
-                    commit = cnt >= a.maxCount;
-                    continue;
-                }
-                const float rayT = zj;
-#pragma unroll
-                for (int i = 0; i < N; ++i)
-                    if (zj < depths[i]) { const float tmp = depths[i]; depths[i] = zj; zj = tmp; }
-                commit = (depths[N - 1] == rayT) || cnt >= a.maxCount;
-            }
-        } else {  // Default reservoir, Common.slangh:136-153, 234-247
-            uint32_t slot = cnt++;
-            if (cnt > (uint32_t)N) slot = (uint32_t)(rj * (float)cnt);
-#pragma unroll
-            for (int i = 0; i < N; ++i)
-                if ((uint32_t)i == slot && !(depths[i] <= zj) && !af) depths[i] = zj;
-            commit = cnt >= a.maxCount;
-        }
+        commit = sd_any_hit<N>(a, rj, zj, af, depths, cnt);
     }
     return commit;
 }
@@ -1100,7 +1228,7 @@ __global__ void __launch_bounds__(kBlock) gbuffer_kernel(GBArgs a) {
 // launchers
 // ------------------------------------------------------------------------------------
 // walk: 0 = quad (depth-first), 1 = row walk + in-kernel algorithm, 2 = split (row walk ->
-// keys -> resolve kernel)
+// keys -> resolve kernel), 3 = traversal-order any-hit stream (rsd_hit_order)
 template <int K, int N>
 static hipError_t launch_sd_kn(const SDArgs& a, dim3 grid, uint32_t persistentBlocks, float4* queue, uint32_t* qctl,
                                uint2* keys, int walk, hipStream_t s) {
@@ -1124,6 +1252,8 @@ static hipError_t launch_sd_kn(const SDArgs& a, dim3 grid, uint32_t persistentBl
         const uint32_t rb = rwEnv ? std::max(1u, persistentBlocks * (uint32_t)std::max(1, std::atoi(rwEnv)) / 8u)
                                   : persistentBlocks;
         hipLaunchKernelGGL((sd_resolve_row_kernel<K, N, ROW>), dim3(rb), wb, 0, s, a, queue, qctl, keys);
+    } else if (walk == 3) {
+        hipLaunchKernelGGL((sd_trace_ordered_kernel<N>), pg, wb, 0, s, a, queue, qctl);
     } else if (walk == 1) {
         if (a.counters) hipLaunchKernelGGL((sd_trace_row_kernel<K, N, ROW, false, true>), pg, wb, 0, s, a, queue, qctl, keys);
         else hipLaunchKernelGGL((sd_trace_row_kernel<K, N, ROW, false, false>), pg, wb, 0, s, a, queue, qctl, keys);
@@ -1261,6 +1391,15 @@ extern "C" rsd_status rsd_sd_trace_band_ex(rsd_scene* scene, const rsd_camera* c
         set_error("rsd_sd_trace: ReservoirSampling is a raster-only implementation");
         return RSD_ERR_UNSUPPORTED;
     }
+    if (p->hit_order > RSD_HIT_ORDER_TRAVERSAL) {
+        set_error("rsd_sd_trace: hit_order must be RSD_HIT_ORDER_CANONICAL or RSD_HIT_ORDER_TRAVERSAL");
+        return RSD_ERR_INVALID_ARG;
+    }
+    if (p->use_16bit && N > 4) {
+        // StochasticDepthMapRT.cpp:199 throws for 16-bit maps with more than 4 samples
+        set_error("rsd_sd_trace: Use16Bit supports SampleCount 1, 2 and 4 only");
+        return RSD_ERR_UNSUPPORTED;
+    }
     if (p->max_count == 0 && p->implementation != RSD_SD_COVERAGE_MASK) {
         set_error("rsd_sd_trace: MaxCount must be >= 1");
         return RSD_ERR_INVALID_ARG;
@@ -1272,8 +1411,13 @@ extern "C" rsd_status rsd_sd_trace_band_ex(rsd_scene* scene, const rsd_camera* c
     if (scene->triangle_count == 0) {
         // no geometry: every texel keeps DEFAULT_DEPTH
         const float def = p->normalize ? 1.0f : 3.40282347e+37f;
-        std::vector<float> h((size_t)sd_w * sd_h * (N < 4 ? N : 4) * ((N + 3) / 4), def);
-        RSD_HIP(hipMemcpyAsync(d_sd_out, h.data(), h.size() * sizeof(float), hipMemcpyHostToDevice, (hipStream_t)stream));
+        const size_t n = (size_t)sd_w * sd_h * (N < 4 ? N : 4) * ((N + 3) / 4);
+        std::vector<float> h(n, def);
+        std::vector<uint16_t> h16(n, p->normalize ? (uint16_t)0x3c00u : (uint16_t)0x7c00u);  // 1.0 / +inf
+        if (p->use_16bit)
+            RSD_HIP(hipMemcpyAsync(d_sd_out, h16.data(), n * 2, hipMemcpyHostToDevice, (hipStream_t)stream));
+        else
+            RSD_HIP(hipMemcpyAsync(d_sd_out, h.data(), n * 4, hipMemcpyHostToDevice, (hipStream_t)stream));
         RSD_HIP(hipStreamSynchronize((hipStream_t)stream));
         if (consume) {
             rsd_status cs = rsd_svao_clear_intervals(d_ray_min, d_ray_max, sd_w * sd_h, stream);
@@ -1309,6 +1453,7 @@ extern "C" rsd_status rsd_sd_trace_band_ex(rsd_scene* scene, const rsd_camera* c
     a.bandIndex = (int)band_index;
     a.bandCount = (int)band_count;
     a.alphaTest = p->alpha_test && scene->d_alpha ? 1u : 0u;
+    a.f16 = p->use_16bit ? 1u : 0u;
     a.deadFast = 0u;
     a.consume = consume ? 1u : 0u;
     a.rayMinW = d_ray_min;
@@ -1422,7 +1567,7 @@ extern "C" rsd_status rsd_sd_trace_band_ex(rsd_scene* scene, const rsd_camera* c
                          (walkName == "fused" || walkName == "split" || (bandTexels <= 600000u && !throughput));
     // default: the split row walk (trace -> keys -> resolve) where one chunk of K keys decides
     // every texel, else the fused row walk; RSD_TRACE_WALK=fused|quad for A/B runs
-    const int walk = !rowWalk ? 0 : (split && walkName != "fused") ? 2 : 1;
+    const int walk = p->hit_order == RSD_HIT_ORDER_TRAVERSAL ? 3 : !rowWalk ? 0 : (split && walkName != "fused") ? 2 : 1;
     // persistent waves: 8 per CU.  At 1080p/4 every row gets one of the ~22 K live rays in its
     // static first slot and the launch lasts as long as the slowest ray; 16 waves per CU (the
     // split walk holds < 128 VGPRs) measured no faster (tools/sd_time.py sweep)

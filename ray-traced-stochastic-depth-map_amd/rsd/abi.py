@@ -16,6 +16,7 @@ PKG_DIR = Path(__file__).resolve().parents[1]
 LIB_PATH = PKG_DIR / (f"librsd_{os.environ['RSD_LIB_VARIANT']}.so" if os.environ.get("RSD_LIB_VARIANT") else "librsd.so")
 
 RSD_OK = 0
+ERR_INVALID_ARG, ERR_UNSUPPORTED, ERR_HIP = 1, 2, 3
 STATUS_NAMES = {0: "RSD_OK", 1: "RSD_ERR_INVALID_ARG", 2: "RSD_ERR_UNSUPPORTED", 3: "RSD_ERR_HIP",
                 4: "RSD_ERR_OUT_OF_MEMORY", 5: "RSD_ERR_NO_DEVICE"}
 
@@ -106,7 +107,8 @@ EXPORTS = ["rsd_abi_version", "rsd_last_error", "rsd_device_open", "rsd_device_c
            "rsd_gbuffer", "rsd_sd_trace", "rsd_svao_clear_intervals", "rsd_svao_pass1", "rsd_svao_pass2",
            "rsd_sd_trace_band", "rsd_svao_pass1_band", "rsd_svao_pass2_band", "rsd_gbuffer_raster",
            "rsd_linearize_depth", "rsd_compress_normals", "rsd_svao_pass2_raytraced", "rsd_svao_pass2_raytraced_band",
-           "rsd_scene_upload_alpha", "rsd_ray_cone_spread", "rsd_sd_trace_band_ex"]
+           "rsd_scene_upload_alpha", "rsd_ray_cone_spread", "rsd_sd_trace_band_ex", "rsd_scene_export_bvh",
+           "rsd_bvh_build"]
 
 SD_CONSUME_INTERVALS = 1
 SD_THROUGHPUT = 2  # frames in flight: the work-efficient traversal (rsd.h RSD_SD_THROUGHPUT)
@@ -153,6 +155,10 @@ def lib():
         L.rsd_scene_info_get.restype = st
         L.rsd_scene_info_get.argtypes = [vp, C.POINTER(SceneInfo)]
         L.rsd_scene_release.argtypes = [vp]
+        L.rsd_scene_export_bvh.restype = st
+        L.rsd_scene_export_bvh.argtypes = [vp, vp, C.c_uint64, C.POINTER(C.c_uint64), C.POINTER(u32)]
+        L.rsd_bvh_build.restype = st
+        L.rsd_bvh_build.argtypes = [C.POINTER(SceneDesc), vp, C.c_uint64, C.POINTER(C.c_uint64), C.POINTER(u32)]
         L.rsd_camera_look_at.restype = st
         L.rsd_camera_look_at.argtypes = [vp, vp, vp, f32, f32, f32, f32, f32, f32, C.POINTER(Camera)]
         L.rsd_svao_make_vao_data.restype = st

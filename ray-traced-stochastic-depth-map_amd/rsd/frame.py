@@ -38,6 +38,8 @@ class FrameConfig:
     sd_samples: int = 4
     max_count: int = 8
     implementation: int = abi.SD_DEFAULT
+    hit_order: int = abi.HIT_ORDER_CANONICAL  # any-hit order (rsd.h rsd_hit_order; librsd extension)
+    use_16bit: bool = False                   # SD pass Use16Bit (standalone SD pass only; N <= 4)
     jitter: bool = True
     ray_interval: bool = True
     cull_mode: int = abi.CULL_BACK
@@ -136,7 +138,8 @@ def make_vao(cfg: FrameConfig):
 def sd_params(cfg: FrameConfig, sd_guard: int) -> abi.SDParams:
     # SVAO::compile builds the nested SD pass with these Properties (SVAO.cpp:158-183)
     return abi.SDParams(cfg.sd_samples, cfg.implementation, cfg.max_count, sd_guard, int(cfg.jitter), 1,
-                        int(cfg.ray_interval), cfg.cull_mode, int(cfg.alpha_test), float(np.float32(1.5 / cfg.sd_samples)))
+                        int(cfg.ray_interval), cfg.cull_mode, int(cfg.alpha_test), float(np.float32(1.5 / cfg.sd_samples)),
+                        int(cfg.hit_order), int(cfg.use_16bit))
 
 
 def svao_params(cfg: FrameConfig) -> abi.SVAOParams:
@@ -170,6 +173,19 @@ def alpha_desc(a):
     return d, (mats, texs, tx, uv, tm)
 
 
+def host_bvh(scene: Scene):
+    """librsd's BVH of `scene` built on the host without a GPU (rsd_bvh_build): the bytes
+    rsd_scene_upload puts in HBM, as (float32 array, triangle-record offset in float4 units)."""
+    desc = abi.SceneDesc(scene.positions.ctypes.data, scene.positions.shape[0], scene.indices.ctypes.data,
+                         scene.indices.shape[0], scene.flags.ctypes.data)
+    n, off = C.c_uint64(), C.c_uint32()
+    abi.check(abi.lib().rsd_bvh_build(C.byref(desc), None, 0, C.byref(n), C.byref(off)), "rsd_bvh_build")
+    buf = np.zeros(n.value // 4, np.float32)
+    abi.check(abi.lib().rsd_bvh_build(C.byref(desc), buf.ctypes.data, n.value, C.byref(n), C.byref(off)),
+              "rsd_bvh_build")
+    return buf, off.value
+
+
 class GpuScene:
     def __init__(self, dev: Device, scene: Scene):
         desc = abi.SceneDesc(scene.positions.ctypes.data, scene.positions.shape[0], scene.indices.ctypes.data,
@@ -185,6 +201,16 @@ class GpuScene:
         self.h = h
         self.info = abi.SceneInfo()
         abi.check(abi.lib().rsd_scene_info_get(h, C.byref(self.info)), "rsd_scene_info_get")
+
+    def export_bvh(self):
+        """The device BVH (rsd_scene_export_bvh): (float32 array of the whole allocation,
+        triangle-record offset in float4 units) -- what the oracle's traversal-order walk reads."""
+        n, off = C.c_uint64(), C.c_uint32()
+        abi.check(abi.lib().rsd_scene_export_bvh(self.h, None, 0, C.byref(n), C.byref(off)), "rsd_scene_export_bvh")
+        buf = np.zeros(n.value // 4, np.float32)
+        abi.check(abi.lib().rsd_scene_export_bvh(self.h, buf.ctypes.data, n.value, C.byref(n), C.byref(off)),
+                  "rsd_scene_export_bvh")
+        return buf, off.value
 
     def release(self):
         if self.h:
@@ -221,7 +247,9 @@ class Renderer:
         # rayMin / rayMax in one allocation: a sharded frame all-reduces both in one collective
         self.ray_minmax = torch.empty((2, self.sd_h, self.sd_w), dtype=torch.int32, device=dv)
         self.ray_min, self.ray_max = self.ray_minmax[0], self.ray_minmax[1]
-        self.sd = torch.empty(((N + 3) // 4, self.sd_h, self.sd_w, min(N, 4)), dtype=torch.float32, device=dv)
+        # Use16Bit (standalone SD pass): R16F / RG16F / RGBA16F
+        self.sd = torch.empty(((N + 3) // 4, self.sd_h, self.sd_w, min(N, 4)),
+                              dtype=torch.float16 if cfg.use_16bit else torch.float32, device=dv)
 
     def frame_slot(self, own_gbuffer: bool = False) -> "Renderer":
         """Another set of per-frame buffers (ao, stencil, intervals, SD map) over the same scene,
@@ -292,6 +320,8 @@ class Renderer:
         return cnt
 
     def pass2(self, band=(0, 1)):
+        if self.cfg.use_16bit:  # SVAO never sets Use16Bit on its SD pass (SVAO.cpp:158-183)
+            raise ValueError("SVAO pass 2 reads 32-bit SD maps; Use16Bit is a standalone SD-pass property")
         abi.check(abi.lib().rsd_svao_pass2_band(C.byref(self.cam), C.byref(self.vao), C.byref(self.svp),
                                                 _ptr(self.depth), _ptr(self.normals), self.cfg.fb_w, self.cfg.fb_h,
                                                 _ptr(self.stencil), _ptr(self.sd), self.sd_w, self.sd_h,
