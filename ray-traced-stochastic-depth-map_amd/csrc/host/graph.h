@@ -54,7 +54,8 @@ private:
 };
 
 // ---- resources
-enum class Format { R32Float, RG32Float, RGBA32Float, R16Uint, R8Uint, R8Unorm, R32Uint, Unknown };
+enum class Format { R32Float, RG32Float, RGBA32Float, R16Uint, R8Uint, R8Unorm, R32Uint, Unknown,
+                    R16Float, RG16Float, RGBA16Float };
 size_t formatBytes(Format f);
 const char* formatName(Format f);
 

@@ -54,6 +54,7 @@ const std::initializer_list<const char*> kDepthModeNames = {"SingleDepth", "Dual
                                                             "Raytraced"};  // VAO/DepthMode.h
 const std::initializer_list<const char*> kImplNames = {"Default", "CoverageMask", "ReservoirSampling",
                                                        "KBuffer"};  // StochasticDepthImplementation.h
+const std::initializer_list<const char*> kHitOrderNames = {"Canonical", "Traversal"};  // rsd.h rsd_hit_order
 
 const SceneRef* requireScene(const SceneRef* s, const std::string& who) {
     if (!s || !s->scene) throw std::runtime_error(who + ": no scene set");
@@ -194,6 +195,9 @@ public:
         prm_.ray_interval = p.getBool("RayInterval", true);
         prm_.guard_band = (int32_t)p.getInt("GuardBand", 0);
         prm_.max_count = (uint32_t)p.getInt("MaxCount", 8);
+        prm_.use_16bit = p.getBool("Use16Bit", false);
+        // librsd extension: "HitOrder" = "Canonical" (default) | "Traversal" (rsd.h rsd_hit_order)
+        prm_.hit_order = enumProp(p, "HitOrder", kHitOrderNames, 0);
         if (p.getBool("StoreNormals", false))  // StochasticDepthMapRT.cpp:198-203
             throw Unsupported("StochasticDepthMapRT: Storing normals is not supported yet");
         if (p.getBool("useRayPipeline", true) == false)
@@ -208,9 +212,15 @@ public:
         st.optional = true;
         r.addInput("rayMin", "min ray T distance for depth values").optional = true;
         r.addInput("rayMax", "max ray T distance for depth values").optional = true;
+        if (N != 1 && N != 2 && N != 4 && N != 8 && N != 16)  // StochasticDepthMapRT.cpp:190 (+ N = 16)
+            throw Unsupported("StochasticDepthMapRT: Only 1, 2, 4 and 8 samples are supported (16: librsd extension)");
+        if (prm_.use_16bit && N > 4)  // StochasticDepthMapRT.cpp:199
+            throw Unsupported("StochasticDepthMapRT: Only 1, 2 and 4 samples are supported");
         auto& o = r.addOutput("stochasticDepth", "stochastic depths in [0,1]");
-        // [layer][y][x][min(N,4)] f32 (the reference stores 16-bit floats for N <= 4 with Use16Bit)
-        o.format = N == 1 ? Format::R32Float : N == 2 ? Format::RG32Float : Format::RGBA32Float;
+        // [layer][y][x][min(N,4)]: R32F / RG32F / RGBA32F, or with Use16Bit R16F / RG16F / RGBA16F
+        // (StochasticDepthMapRT.cpp:181-198)
+        if (prm_.use_16bit) o.format = N == 1 ? Format::R16Float : N == 2 ? Format::RG16Float : Format::RGBA16Float;
+        else o.format = N == 1 ? Format::R32Float : N == 2 ? Format::RG32Float : Format::RGBA32Float;
         o.layers = (N + 3) / 4;
         return r;
     }
@@ -242,7 +252,8 @@ private:
 // SVAO.cpp:73-100 Properties, :117-140 reflect, :143-190 compile (nested SD graph),
 // :192-455 execute.  Members the reference sets only from its GUI (SVAO.h:90-126) are
 // accepted as extra Properties with the same defaults: stochSamples, stochMaxCount,
-// stochGuardBand, stochJitter, rayInterval, cullMode, sampleCount, stochImplementation.
+// stochGuardBand, stochJitter, rayInterval, cullMode, sampleCount, stochImplementation; and the
+// librsd extension stochHitOrder (rsd_hit_order, passed on as the SD pass's HitOrder).
 class SVAOPass : public RenderPass {
 public:
     explicit SVAOPass(const Properties& p) {
@@ -263,6 +274,7 @@ public:
         cull_ = toRsdCull(enumProp(p, "cullMode", kCullNames, 2));
         directions_ = (uint32_t)p.getInt("sampleCount", 8);
         impl_ = enumProp(p, "stochImplementation", kImplNames, 0);
+        hitOrder_ = enumProp(p, "stochHitOrder", kHitOrderNames, 0);  // librsd extension (rsd_hit_order)
         rayPipeline_ = p.getBool("rayPipeline", true);  // SVAO.h:101
     }
     void checkSupported() const {
@@ -316,6 +328,7 @@ public:
         sd.set("SampleCount", (int64_t)samples_);
         sd.set("AlphaTest", alphaTest_);
         sd.set("Implementation", (int64_t)impl_);
+        sd.set("HitOrder", (int64_t)hitOrder_);
         sd.set("Alpha", (double)(float)(1.5 / samples_));
         sd.set("RayInterval", rayInterval_);
         sd.set("CullMode", std::string(cull_ == RSD_CULL_NONE ? "None" : cull_ == RSD_CULL_FRONT ? "Front" : "Back"));
@@ -383,7 +396,7 @@ public:
 private:
     const SceneRef* scene_ = nullptr;
     float radius_, exponent_, thickness_;
-    uint32_t primary_, secondary_, divisor_, samples_, maxCount_, cull_, directions_, impl_;
+    uint32_t primary_, secondary_, divisor_, samples_, maxCount_, cull_, directions_, impl_, hitOrder_;
     int32_t guardPx_;
     bool dualAo_, alphaTest_, jitter_, rayInterval_, rayPipeline_;
     uint32_t width_ = 0, height_ = 0, sdW_ = 0, sdH_ = 0;

@@ -123,6 +123,7 @@ GRAPH_EXPORTS = ["rsd_graph_create", "rsd_graph_destroy", "rsd_graph_create_pass
                  "rsd_image_equation_run", "rsd_image_equation_release"]
 
 FMT_R32F, FMT_RG32F, FMT_RGBA32F, FMT_R16U, FMT_R8U, FMT_R8UNORM, FMT_R32U, FMT_UNKNOWN = range(8)
+FMT_R16F, FMT_RG16F, FMT_RGBA16F = 8, 9, 10
 
 
 class Texture(C.Structure):

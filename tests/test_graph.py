@@ -5,6 +5,7 @@ import os
 import subprocess
 from pathlib import Path
 
+import numpy as np
 import pytest
 
 from conftest import PKG as PKG_DIR, ROOT
@@ -192,3 +193,33 @@ def test_graph_header_exports():
     exported = set(re.findall(r" T (rsd_\w+)$", out, re.M))
     assert set(abi.GRAPH_EXPORTS) <= exported
     assert os.path.getsize(abi.LIB_PATH) > 0
+
+
+@pytest.mark.parametrize("N,use16,fmt,layers", [(1, False, "R32Float", 1), (4, False, "RGBA32Float", 1),
+                                                (8, False, "RGBA32Float", 2), (16, False, "RGBA32Float", 4),
+                                                (1, True, "R16Float", 1), (2, True, "RG16Float", 1),
+                                                (4, True, "RGBA16Float", 1)])
+def test_sd_pass_output_format(N, use16, fmt, layers):
+    """StochasticDepthMapRT::reflect (StochasticDepthMapRT.cpp:177-216): 32-bit or, with Use16Bit,
+    16-bit float maps; N = 8 is two RGBA layers (16: four, librsd's extension)."""
+    g = rsdgraph.RenderGraph("sd")
+    g.create_pass("SD", "StochasticDepthMapRT", {"SampleCount": N, "Use16Bit": use16, "HitOrder": "Traversal"})
+    g.mark_output("SD.stochasticDepth")
+    z = np.zeros((32, 64), np.float32)  # planned only: never read (no device work)
+    g.set_input("SD.linearZ", z.ctypes.data, 64, 32, abi.FMT_R32F)
+    g.plan(64, 32)
+    assert g.resources()["SD.stochasticDepth"] == (64, 32, layers, fmt)
+    g.close()
+
+
+@pytest.mark.parametrize("N,use16", [(8, True), (3, False)])
+def test_sd_pass_refuses_like_the_reference(N, use16):
+    """StochasticDepthMapRT.cpp:190,199: unsupported sample counts throw."""
+    g = rsdgraph.RenderGraph("sd")
+    g.create_pass("SD", "StochasticDepthMapRT", {"SampleCount": N, "Use16Bit": use16})
+    g.mark_output("SD.stochasticDepth")
+    z = np.zeros((32, 64), np.float32)
+    g.set_input("SD.linearZ", z.ctypes.data, 64, 32, abi.FMT_R32F)
+    with pytest.raises(abi.RsdError):
+        g.plan(64, 32)
+    g.close()
