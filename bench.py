@@ -27,13 +27,15 @@ next pose of a 120-pose orbit (rsd.frame.camera_path): camera update + G-buffer 
 The G-buffer is inside the frame's wall time but outside the AO span (AO frames/s
 excludes the G-buffer).
 
-Multi-GPU (torchrun, one rank per GPU), two sharding modes (--shard):
-  frame: frames are the independent units -- every rank renders whole frames (its own frame
-    stream, BVH + G-buffer replicated), no data-path collective.  Weak scaling.
-  band (default for the 4K configs): one frame sharded by screen band (rsd/shard.py, the
-    north_star's tile split): pass 1 on the rank's rows, interval all-reduce, trace of the
-    rank's SD tile rows, SD halo exchange with the neighbouring bands (ssMaxRadius), pass 2 on
-    the rank's rows, AO all-gather (RCCL over xGMI).  Strong scaling.
+Multi-GPU (torchrun, one rank per GPU), sharding modes (--shard):
+  frame (default for the 1080p configs): frames are the independent units -- every rank renders
+    whole frames (its own frame stream, BVH + G-buffer replicated), no data-path collective.
+    Weak scaling.
+  band (default for the 4K configs): the north_star's screen split (rsd/shard.py HaloFrame):
+    contiguous bands; pass 1 of the rank's rows, interval halo exchange with the bands its
+    samples reach (point-to-point send / recv: ncclSend / ncclRecv under RCCL), trace of the
+    rank's SD rows, SD halo exchange, pass 2 of the rank's rows, AO all-gather.  Strong scaling.
+  gather: round-1 v1 of band -- interleaved bands, whole-map interval all-reduce and SD all-gather.
 """
 from __future__ import annotations
 
@@ -68,10 +70,12 @@ def parse():
                     help="target wall time of the bounded CPU-oracle sample (0 disables)")
     ap.add_argument("--frames-in-flight", type=int, default=4,
                     help="throughput region: frame i runs on stream i %% F with its own frame buffers")
-    ap.add_argument("--shard", choices=("frame", "band"), default=None,
+    ap.add_argument("--shard", choices=("frame", "band", "gather"), default=None,
                     help="N > 1: frame = every rank renders whole frames (weak scaling, no per-frame "
-                         "collective); band = each frame split by screen band + RCCL exchanges (strong). "
-                         "Default: band for the 4K configs, frame otherwise")
+                         "collective); band = each frame split into contiguous screen bands with interval / SD "
+                         "halo exchanges (point-to-point RCCL) + AO all-gather (strong); gather = interleaved "
+                         "bands with whole-map all-reduce / all-gather (round-1 v1). Default: band for the 4K "
+                         "configs, frame otherwise")
     ap.add_argument("--pmc-csv", nargs="*", default=None,
                     help="rocprofv3 --pmc counter_collection.csv file(s) with FETCH_SIZE / WRITE_SIZE for "
                          "roofline.traffic (default: the committed passes of the default config)")
@@ -110,7 +114,7 @@ def main():
     from rsd import abi
     from rsd.frame import CONFIGS, DEFAULT_CAMERA_PATH, FrameConfig, Renderer, camera_path
     from rsd.scenes import make_scene
-    from rsd.shard import BandFrame
+    from rsd.shard import BandFrame, HaloFrame
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -137,8 +141,15 @@ def main():
     scene = make_scene(scene_name)
     r = Renderer(scene, cfg, device=local)
     bvh_build_s = r.gscene.info.build_ms * 1e-3
-    bw = (rank, world) if shard == "band" else (0, 1)
+    bw = (rank, world) if shard == "gather" else (0, 1)
     F = max(1, args.frames_in_flight)
+
+    def make_frame(rend, throughput=False):
+        if shard == "band":
+            return HaloFrame(rend, rank, world, throughput=throughput)
+        return BandFrame(rend, *bw, throughput=throughput)
+
+    seq = make_frame(r)  # latency region: one frame in flight, the latency-optimised trace walk
     n_poses = len(poses) if poses else 1
 
     def pose(rend, i):
@@ -157,7 +168,10 @@ def main():
             # pass 1 over the whole frame = the exact interval union a band frame all-reduces
             r.clear_intervals()
             r.pass1()
-            acc.append(r.sd_trace(counters=True, throughput=thr, band=bw))
+            if shard == "band":
+                acc.append(r.sd_trace_rows(seq.sd_rows[rank], counters=True, throughput=thr))
+            else:
+                acc.append(r.sd_trace(counters=True, throughput=thr, band=bw))
     torch.cuda.synchronize()
     walk_seq, walk_thr = int(cnt_seq[0].walk), int(cnt_thr[0].walk)
     mean_cnt = lambda cs, f: float(np.mean([getattr(c, f) for c in cs]))  # noqa: E731
@@ -183,7 +197,6 @@ def main():
         return wall
 
     # ---- latency region: one frame in flight, the latency-optimised trace walk
-    seq = BandFrame(r, *bw)
     mk_ev = lambda n: [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))  # noqa: E731
                        for _ in range(n)]
     ev_sd, ev_ao = mk_ev(args.steps), mk_ev(args.steps)
@@ -203,8 +216,8 @@ def main():
     seq_ao_ms = float(np.mean([a.elapsed_time(b) for a, b in ev_ao]))
 
     # ---- throughput region: F frames in flight on F streams
-    slots = [BandFrame(r, *bw, throughput=F > 1)] + \
-        [BandFrame(r.frame_slot(own_gbuffer=bool(poses)), *bw, throughput=True) for _ in range(F - 1)]
+    slots = [make_frame(r, throughput=F > 1)] + \
+        [make_frame(r.frame_slot(own_gbuffer=bool(poses)), throughput=True) for _ in range(F - 1)]
     streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(F - 1)]
     for st in streams[1:]:
         st.wait_stream(streams[0])
@@ -230,7 +243,7 @@ def main():
     # frame mode: every rank renders whole frames; band mode: the ranks share each frame
     units = world if shard == "frame" else 1
     rays_active = mean_cnt(cnt_seq, "rays_active")
-    if dist and shard == "band":  # counters are per band: the frame's totals
+    if dist and shard != "frame":  # counters are per band: the frame's totals
         t = torch.tensor([rays_active, mean_cnt(cnt_seq, "nodes_visited"), mean_cnt(cnt_seq, "tris_tested")],
                          device="cuda", dtype=torch.float64)
         dist.all_reduce(t)
@@ -275,7 +288,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(wall_thr / args.steps * 1e3, 4),
         "higher_is_better": True,
-        "scaling": "strong" if shard == "band" and world > 1 else "weak",
+        "scaling": "strong" if shard != "frame" and world > 1 else "weak",
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic (seeded procedural stand-in scene; no reference assets in the container)",
@@ -283,7 +296,8 @@ def main():
                    "frame_buffer": [cfg.fb_w, cfg.fb_h], "visible": [cfg.visible_w, cfg.visible_h],
                    "sd_map": [r.sd_w, r.sd_h], "sd_samples": N, "max_count": cfg.max_count,
                    "stoch_map_divisor": cfg.divisor, "camera_path": path_name,
-                   "parallelism": f"screen-band x{world}" if shard == "band" else f"frame-parallel x{world}",
+                   "parallelism": {"band": f"screen-band+halo x{world}", "gather": f"screen-band+allgather x{world}",
+                                   "frame": f"frame-parallel x{world}"}[shard],
                    "frames_in_flight": F},
         "value_definition": "dispatched SD rays / SD-kernel time (HIP events around every rsd_sd_trace of the "
                             "latency region; BASELINE.md section 4), summed over ranks",
@@ -319,6 +333,7 @@ def main():
         # the frame's largest kernel is pass 1, bound by VALU issue rather than HBM
         "pass1_roofline": pmc_valu(valu_csv, "svao_pass1_kernel") if valu_csv and args.config == DEFAULT_CONFIG
         else None,
+        "exchange_bytes_per_frame": seq.bytes_per_frame() if shard == "band" and world > 1 else None,
         "bvh_build_s": round(bvh_build_s, 3),
         "bvh_build_threads": int(r.gscene.info.build_threads),
         "cpu_baseline": cpu,

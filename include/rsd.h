@@ -316,6 +316,25 @@ rsd_status rsd_svao_pass2_band(const rsd_camera* cam, const rsd_vao_data* vao, c
                                const uint8_t* d_stencil, const float* d_sd, uint32_t sd_w, uint32_t sd_h,
                                uint8_t* d_ao, uint32_t band_index, uint32_t band_count, rsd_stream stream);
 
+/* Contiguous screen bands (the halo-exchange split, rsd/shard.py HaloFrame): pass 1 / pass 2 of the
+ * visible rows [row0, row1) counted from the first visible row (multiples of 32: the 2x2 group
+ * interleave of SVAORaster.ps.slang:36 stays inside 32-row groups; row1 may end the frame), and
+ * the SD trace of the SD-map rows [row0, row1) (multiples of 8; row1 may be sd_h).  Same kernels
+ * and bits as the band calls; flags as rsd_sd_trace_band_ex (CONSUME resets the whole map). */
+rsd_status rsd_svao_pass1_rows(const rsd_camera* cam, const rsd_vao_data* vao, const rsd_svao_params* params,
+                               const float* d_depth, const uint16_t* d_normals, uint32_t width, uint32_t height,
+                               uint8_t* d_ao, uint8_t* d_stencil, uint32_t* d_ray_min, uint32_t* d_ray_max,
+                               uint32_t sd_w, uint32_t sd_h, uint32_t row0, uint32_t row1, rsd_stream stream);
+rsd_status rsd_svao_pass2_rows(const rsd_camera* cam, const rsd_vao_data* vao, const rsd_svao_params* params,
+                               const float* d_depth, const uint16_t* d_normals, uint32_t width, uint32_t height,
+                               const uint8_t* d_stencil, const float* d_sd, uint32_t sd_w, uint32_t sd_h,
+                               uint8_t* d_ao, uint32_t row0, uint32_t row1, rsd_stream stream);
+rsd_status rsd_sd_trace_rows(rsd_scene* scene, const rsd_camera* cam, const rsd_sd_params* params,
+                             const float* d_linear_z, uint32_t z_w, uint32_t z_h,
+                             uint32_t* d_ray_min, uint32_t* d_ray_max,
+                             float* d_sd_out, uint32_t sd_w, uint32_t sd_h,
+                             uint32_t row0, uint32_t row1, uint32_t flags, rsd_counters* counters, rsd_stream stream);
+
 rsd_status rsd_svao_pass2_raytraced_band(rsd_scene* scene, const rsd_camera* cam, const rsd_vao_data* vao,
                                          const rsd_svao_params* params, const float* d_depth,
                                          const uint16_t* d_normals, uint32_t width, uint32_t height,

@@ -79,6 +79,8 @@ def lib():
         L.ocpu_sd_trace_ordered.argtypes = [vp, vp, u32, vp, vp, vp, u32, u32, vp, vp, vp, u32, u32, u32, u32, u32, u32,
                                             i32, vp]
         L.ocpu_svao_pass1_band.argtypes = [vp, vp, vp, vp, vp, u32, u32, vp, vp, vp, vp, u32, u32, u32, u32]
+        L.ocpu_svao_pass1_rows.argtypes = [vp, vp, vp, vp, vp, u32, u32, vp, vp, vp, vp, u32, u32, u32, u32]
+        L.ocpu_svao_pass2_rows.argtypes = [vp, vp, vp, vp, vp, u32, u32, vp, vp, u32, u32, vp, u32, u32, i32]
         L.ocpu_svao_pass2_band.argtypes = [vp, vp, vp, vp, vp, u32, u32, vp, vp, u32, u32, vp, u32, u32, i32]
         L.ocpu_svao_pass1.argtypes = [vp, vp, vp, vp, vp, u32, u32, vp, vp, vp, vp, u32, u32]
         L.ocpu_svao_pass2.argtypes = [vp, vp, vp, vp, vp, u32, u32, vp, vp, u32, u32, vp, i32]
@@ -336,6 +338,32 @@ def svao_pass1_into(cam, vao, p, depth, normals, ao, st, rmin, rmax, band=(0, 1)
     sdH, sdW = rmin.shape
     lib().ocpu_svao_pass1_band(C.byref(cam), C.byref(vao), C.byref(p), _p(depth), _p(normals), W, H, _p(ao), _p(st),
                                _p(rmin), _p(rmax), sdW, sdH, band[0], band[1])
+
+
+def svao_pass1_rows_into(cam, vao, p, depth, normals, ao, st, rmin, rmax, rows):
+    """Pass 1 of the visible rows [rows[0], rows[1]) (a contiguous screen band)."""
+    H, W = depth.shape
+    sdH, sdW = rmin.shape
+    lib().ocpu_svao_pass1_rows(C.byref(cam), C.byref(vao), C.byref(p), _p(depth), _p(normals), W, H, _p(ao), _p(st),
+                               _p(rmin), _p(rmax), sdW, sdH, rows[0], rows[1])
+
+
+def svao_pass2_rows_into(cam, vao, p, depth, normals, stencil, sd, ao, rows, threads=None):
+    H, W = depth.shape
+    sdc = np.ascontiguousarray(sd, np.float32)
+    sdH, sdW = sdc.shape[1], sdc.shape[2]
+    lib().ocpu_svao_pass2_rows(C.byref(cam), C.byref(vao), C.byref(p), _p(depth), _p(normals), W, H, _p(stencil),
+                               _p(sdc), sdW, sdH, _p(ao), rows[0], rows[1], _threads(threads))
+
+
+def sd_trace_rows_into(scene, cam, params, linearZ, rmin, rmax, sd, rows, threads=None):
+    """The SD trace of SD rows [rows[0], rows[1]) into `sd` (the other rows untouched)."""
+    sdH, sdW = sd.shape[1], sd.shape[2]
+    stats = np.zeros(2, np.uint64)
+    lib().ocpu_sd_trace_band(scene.h, C.byref(cam), C.byref(params), _p(linearZ), linearZ.shape[1], linearZ.shape[0],
+                             _p(rmin), _p(rmax), _p(sd), sdW, sdH, rows[0], rows[1], 0, 1, _threads(threads),
+                             _p(stats))
+    return stats
 
 
 def sd_trace_into(scene, cam, params, linearZ, rmin, rmax, sd, band=(0, 1), threads=None):

@@ -1443,10 +1443,36 @@ void ocpu_svao_pass1(const ocam* cam, const ovao* d, const osvao_params* p,
     ocpu_svao_pass1_band(cam, d, p, depth, normals, W, H, ao, stencil, rayMin, rayMax, sdW, sdH, 0, 1);
 }
 
+static void o_pass1_impl(const ocam* cam, const ovao* d, const osvao_params* p,
+                         const float* depth, const uint16_t* normals, uint32_t W, uint32_t H,
+                         uint8_t* ao, uint8_t* stencil, uint32_t* rayMin, uint32_t* rayMax,
+                         uint32_t sdW, uint32_t sdH, uint32_t band_index, uint32_t band_count,
+                         uint32_t row0, uint32_t row1);
+
 void ocpu_svao_pass1_band(const ocam* cam, const ovao* d, const osvao_params* p,
                           const float* depth, const uint16_t* normals, uint32_t W, uint32_t H,
                           uint8_t* ao, uint8_t* stencil, uint32_t* rayMin, uint32_t* rayMax,
                           uint32_t sdW, uint32_t sdH, uint32_t band_index, uint32_t band_count)
+{
+    o_pass1_impl(cam, d, p, depth, normals, W, H, ao, stencil, rayMin, rayMax, sdW, sdH, band_index, band_count, 0,
+                 0xffffffffu);
+}
+
+/* visible rows [row0, row1) counted from the first visible row (multiples of 32, a
+ * contiguous screen band: librsd rsd_svao_pass1_rows) */
+void ocpu_svao_pass1_rows(const ocam* cam, const ovao* d, const osvao_params* p,
+                          const float* depth, const uint16_t* normals, uint32_t W, uint32_t H,
+                          uint8_t* ao, uint8_t* stencil, uint32_t* rayMin, uint32_t* rayMax,
+                          uint32_t sdW, uint32_t sdH, uint32_t row0, uint32_t row1)
+{
+    o_pass1_impl(cam, d, p, depth, normals, W, H, ao, stencil, rayMin, rayMax, sdW, sdH, 0, 1, row0, row1);
+}
+
+static void o_pass1_impl(const ocam* cam, const ovao* d, const osvao_params* p,
+                         const float* depth, const uint16_t* normals, uint32_t W, uint32_t H,
+                         uint8_t* ao, uint8_t* stencil, uint32_t* rayMin, uint32_t* rayMax,
+                         uint32_t sdW, uint32_t sdH, uint32_t band_index, uint32_t band_count,
+                         uint32_t row0, uint32_t row1)
 {
     if (!band_count) band_count = 1;
     octx x;
@@ -1455,7 +1481,7 @@ void ocpu_svao_pass1_band(const ocam* cam, const ovao* d, const osvao_params* p,
     /* SVAO.cpp:347-350: dispatch roundup32(dims - 2 guardBand); the 2x2 group interleave
      * (SVAORaster.ps.slang:36) is a bijection of that range, so iterate it directly. */
     uint32_t nx = ((W - 2 * g) + 31u) / 32u * 32u, ny = ((H - 2 * g) + 31u) / 32u * 32u;
-    for (uint32_t oy = 0; oy < ny; ++oy)
+    for (uint32_t oy = row0; oy < ny && oy < row1; ++oy)
         for (uint32_t ox = 0; ox < nx; ++ox) {
             if ((oy / 32u) % band_count != band_index) break;
             uint32_t px = ox + g, py = oy + g;
@@ -1582,6 +1608,27 @@ void ocpu_svao_pass2(const ocam* cam, const ovao* d, const osvao_params* p,
                      uint8_t* ao, int nthreads)
 {
     ocpu_svao_pass2_band(cam, d, p, depth, normals, W, H, stencil, sd, sdW, sdH, ao, 0, 1, nthreads);
+}
+
+/* visible rows [row0, row1) from the first visible row (librsd rsd_svao_pass2_rows) */
+void ocpu_svao_pass2_rows(const ocam* cam, const ovao* d, const osvao_params* p,
+                          const float* depth, const uint16_t* normals, uint32_t W, uint32_t H,
+                          const uint8_t* stencil, const float* sd, uint32_t sdW, uint32_t sdH,
+                          uint8_t* ao, uint32_t row0, uint32_t row1, int nthreads)
+{
+    octx x;
+    o_ctx_init(&x, cam, d, p, depth, normals, W, H);
+    if (nthreads < 1) nthreads = 1;
+    op2_job* jobs = (op2_job*)calloc((size_t)nthreads, sizeof(op2_job));
+    for (int i = 0; i < nthreads; ++i) {
+        jobs[i].x = &x; jobs[i].stencil = stencil; jobs[i].sd = sd;
+        jobs[i].sdW = sdW; jobs[i].sdH = sdH; jobs[i].ao = ao;
+        jobs[i].bi = 0; jobs[i].bc = 1;
+    }
+    const uint32_t y0 = p->guard_band + row0, yEnd = H - p->guard_band;
+    const uint32_t y1 = row1 < yEnd - p->guard_band ? p->guard_band + row1 : yEnd;
+    if (y0 < y1) o_run_rows(o_pass2_rows, jobs, sizeof(op2_job), y0, y1, nthreads, o_p2_setrows);
+    free(jobs);
 }
 
 void ocpu_svao_pass2_band(const ocam* cam, const ovao* d, const osvao_params* p,

@@ -144,6 +144,15 @@ void ocpu_sd_ray(const ocam* c, const osd_params* p, const float* z, uint32_t zW
                  float out[6], float* tmin, float* tmax, float* cosT);
 
 void ocpu_svao_clear(uint32_t* rayMin, uint32_t* rayMax, uint32_t n);
+/* contiguous screen bands: visible rows [row0, row1) counted from the first visible row */
+void ocpu_svao_pass1_rows(const ocam* cam, const ovao* d, const osvao_params* p,
+                          const float* depth, const uint16_t* normals, uint32_t W, uint32_t H,
+                          uint8_t* ao, uint8_t* stencil, uint32_t* rayMin, uint32_t* rayMax,
+                          uint32_t sdW, uint32_t sdH, uint32_t row0, uint32_t row1);
+void ocpu_svao_pass2_rows(const ocam* cam, const ovao* d, const osvao_params* p,
+                          const float* depth, const uint16_t* normals, uint32_t W, uint32_t H,
+                          const uint8_t* stencil, const float* sd, uint32_t sdW, uint32_t sdH,
+                          uint8_t* ao, uint32_t row0, uint32_t row1, int nthreads);
 void ocpu_svao_pass1(const ocam* cam, const ovao* d, const osvao_params* p,
                      const float* depth, const uint16_t* normals, uint32_t W, uint32_t H,
                      uint8_t* ao, uint8_t* stencil, uint32_t* rayMin, uint32_t* rayMax,

@@ -55,7 +55,9 @@ struct SDArgs {
     const uint32_t* lut;    // coverage mask: look-up table [2^N]
     unsigned long long* counters;
     uint32_t partCap;  // live-ray queue: capacity of one partition
-    int bandIndex, bandCount;  // screen-band sharding: 8-row tile rows t with t % count == index
+    // screen-band sharding: the 8-row tile rows t = bandStart + k * bandStep, k < bandN (an
+    // interleaved band: start = index, step = count; a contiguous row range: step = 1)
+    int bandStart, bandStep, bandN;
     int poolSoft;      // row traversal: above this many pooled items a row pops one item per step
     const float* rayTab;  // per-column / per-row ray terms (ray_table_kernel), see sd_ray
     uint32_t deadFast;    // setup may classify rayMin == asuint(FLT_MAX) texels as dead directly
@@ -438,10 +440,11 @@ __global__ void __launch_bounds__(kBlock) sd_setup_kernel(SDArgs a, float4* __re
     const int x = blockIdx.x * kTile + (lane & (kTile - 1));
     // consume: the grid covers every tile row of the map; other bands' rows only get their
     // intervals reset (SVAO.cpp:334-340's clear for the next frame)
-    const int tileRow = a.consume ? (int)blockIdx.y : (int)blockIdx.y * a.bandCount + a.bandIndex;
+    const int tileRow = a.consume ? (int)blockIdx.y : (int)blockIdx.y * a.bandStep + a.bandStart;
     const int y = tileRow * kTile + (lane / kTile);
     const bool inside = x < a.sdW && y < a.sdH;
-    if (a.consume && tileRow % a.bandCount != a.bandIndex) {
+    if (a.consume && (tileRow < a.bandStart || (tileRow - a.bandStart) % a.bandStep != 0 ||
+                      (tileRow - a.bandStart) / a.bandStep >= a.bandN)) {
         if (inside) {
             a.rayMinW[(size_t)y * a.sdW + x] = 0x7f7fffffu;  // asuint(FLT_MAX)
             a.rayMaxW[(size_t)y * a.sdW + x] = 0u;
@@ -1358,11 +1361,13 @@ rsd_status ensure_lut(int dev, uint32_t N, const int32_t** idx, const uint32_t**
 }
 }  // namespace
 
-extern "C" rsd_status rsd_sd_trace_band_ex(rsd_scene* scene, const rsd_camera* cam, const rsd_sd_params* p,
-                                           const float* d_linear_z, uint32_t z_w, uint32_t z_h, uint32_t* d_ray_min,
-                                           uint32_t* d_ray_max, float* d_sd_out, uint32_t sd_w, uint32_t sd_h,
-                                           uint32_t band_index, uint32_t band_count, uint32_t flags,
-                                           rsd_counters* counters, rsd_stream stream) {
+namespace {
+// The SD trace of the 8-row tile rows t = start + k * step, k < n (rsd_sd_trace_band_ex: an
+// interleaved band; rsd_sd_trace_rows: a contiguous range).
+rsd_status sd_trace_impl(rsd_scene* scene, const rsd_camera* cam, const rsd_sd_params* p, const float* d_linear_z,
+                         uint32_t z_w, uint32_t z_h, uint32_t* d_ray_min, uint32_t* d_ray_max, float* d_sd_out,
+                         uint32_t sd_w, uint32_t sd_h, uint32_t start, uint32_t step, uint32_t n, uint32_t flags,
+                         rsd_counters* counters, rsd_stream stream) {
     const bool consume = (flags & RSD_SD_CONSUME_INTERVALS) != 0u;
     const bool throughput = (flags & RSD_SD_THROUGHPUT) != 0u;
     if (flags & ~(RSD_SD_CONSUME_INTERVALS | RSD_SD_THROUGHPUT)) {
@@ -1371,10 +1376,6 @@ extern "C" rsd_status rsd_sd_trace_band_ex(rsd_scene* scene, const rsd_camera* c
     }
     if (consume && (!p || !p->ray_interval || !d_ray_min || !d_ray_max)) {
         set_error("rsd_sd_trace_band_ex: RSD_SD_CONSUME_INTERVALS needs RayInterval and both interval maps");
-        return RSD_ERR_INVALID_ARG;
-    }
-    if (band_count == 0 || band_index >= band_count) {
-        set_error("rsd_sd_trace_band: band_index must be < band_count");
         return RSD_ERR_INVALID_ARG;
     }
     if (!scene || !cam || !p || !d_linear_z || !d_sd_out || sd_w == 0 || sd_h == 0 || z_w == 0 || z_h == 0) {
@@ -1450,8 +1451,9 @@ extern "C" rsd_status rsd_sd_trace_band_ex(rsd_scene* scene, const rsd_camera* c
     a.lutIdx = nullptr;
     a.lut = nullptr;
     a.counters = nullptr;
-    a.bandIndex = (int)band_index;
-    a.bandCount = (int)band_count;
+    a.bandStart = (int)start;
+    a.bandStep = (int)step;
+    a.bandN = (int)n;
     a.alphaTest = p->alpha_test && scene->d_alpha ? 1u : 0u;
     a.f16 = p->use_16bit ? 1u : 0u;
     a.deadFast = 0u;
@@ -1518,8 +1520,7 @@ extern "C" rsd_status rsd_sd_trace_band_ex(rsd_scene* scene, const rsd_camera* c
         a.counters = ws->counters;
     }
     const uint32_t tiles = (sd_h + kTile - 1) / kTile;
-    const uint32_t bandTiles = tiles > band_index ? (tiles - band_index + band_count - 1) / band_count : 0u;
-    dim3 grid((sd_w + kTile - 1) / kTile, consume ? tiles : bandTiles);
+    dim3 grid((sd_w + kTile - 1) / kTile, consume ? tiles : n);
     // k = the MAX_COUNT nearest keys decide Default and KBuffer; coverage mask streams chunks
     const uint32_t need = p->implementation == RSD_SD_COVERAGE_MASK ? 8u : p->max_count;
     // live-ray queue workspace (grow-only; the first call of a larger map allocates)
@@ -1559,7 +1560,7 @@ extern "C" rsd_status rsd_sd_trace_band_ex(rsd_scene* scene, const rsd_camera* c
     // more SD texels the live rays fill the machine and the quad walk's lane utilisation wins
     // (rsd_sd_trace, row vs quad: 1080p/4 0.43 M texels 92 vs 133 us; 4K/4 1.0 M texels 443 vs
     // 327 us; 1080p full 6.9 M texels 688 vs 294 us -- DESIGN.md section 4)
-    const uint64_t bandTexels = (uint64_t)sd_w * sd_h / band_count;
+    const uint64_t bandTexels = (uint64_t)sd_w * std::min<uint64_t>((uint64_t)n * kTile, sd_h);
     // RSD_SD_THROUGHPUT (frames in flight): the row walk's spare lanes are VALU time taken from
     // the overlapping frames, so the quad walk wins there (1080p/4, 4 frames in flight: 108 vs
     // 118 us per frame; one frame alone: 245 vs 197 us -- DESIGN.md section 4)
@@ -1609,6 +1610,37 @@ extern "C" rsd_status rsd_sd_trace_band_ex(rsd_scene* scene, const rsd_camera* c
         }
     }
     return RSD_OK;
+}
+
+}  // namespace
+
+extern "C" rsd_status rsd_sd_trace_band_ex(rsd_scene* scene, const rsd_camera* cam, const rsd_sd_params* p,
+                                           const float* d_linear_z, uint32_t z_w, uint32_t z_h, uint32_t* d_ray_min,
+                                           uint32_t* d_ray_max, float* d_sd_out, uint32_t sd_w, uint32_t sd_h,
+                                           uint32_t band_index, uint32_t band_count, uint32_t flags,
+                                           rsd_counters* counters, rsd_stream stream) {
+    if (band_count == 0 || band_index >= band_count) {
+        set_error("rsd_sd_trace_band: band_index must be < band_count");
+        return RSD_ERR_INVALID_ARG;
+    }
+    const uint32_t tiles = (sd_h + kTile - 1) / kTile;
+    const uint32_t n = tiles > band_index ? (tiles - band_index + band_count - 1) / band_count : 0u;
+    return sd_trace_impl(scene, cam, p, d_linear_z, z_w, z_h, d_ray_min, d_ray_max, d_sd_out, sd_w, sd_h, band_index,
+                         band_count, n, flags, counters, stream);
+}
+
+extern "C" rsd_status rsd_sd_trace_rows(rsd_scene* scene, const rsd_camera* cam, const rsd_sd_params* p,
+                                        const float* d_linear_z, uint32_t z_w, uint32_t z_h, uint32_t* d_ray_min,
+                                        uint32_t* d_ray_max, float* d_sd_out, uint32_t sd_w, uint32_t sd_h,
+                                        uint32_t row0, uint32_t row1, uint32_t flags, rsd_counters* counters,
+                                        rsd_stream stream) {
+    if (row0 > row1 || row1 > sd_h || row0 % kTile != 0u || (row1 % kTile != 0u && row1 != sd_h)) {
+        set_error("rsd_sd_trace_rows: rows must satisfy row0 <= row1 <= sd_h, multiples of 8 (row1 may be sd_h)");
+        return RSD_ERR_INVALID_ARG;
+    }
+    const uint32_t t0 = row0 / kTile, t1 = (row1 + kTile - 1) / kTile;
+    return sd_trace_impl(scene, cam, p, d_linear_z, z_w, z_h, d_ray_min, d_ray_max, d_sd_out, sd_w, sd_h, t0, 1u,
+                         t1 - t0, flags, counters, stream);
 }
 
 extern "C" rsd_status rsd_sd_trace_band(rsd_scene* scene, const rsd_camera* cam, const rsd_sd_params* p,

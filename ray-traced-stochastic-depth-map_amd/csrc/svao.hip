@@ -9,6 +9,7 @@
 // SD depths at texels up to ssMaxRadius away.  Per-pixel transcendentals are tables
 // (16 noise angles, 8 direction angles) computed on the host in double and rounded once;
 // the only per-pixel libm call left is pow() in finalize (SVAO Common.slang:326-330).
+#include <algorithm>
 #include <cfloat>
 #include <cmath>
 #include <mutex>
@@ -380,14 +381,14 @@ static rsd_status check_band(uint32_t index, uint32_t count, const char* who) {
     return RSD_OK;
 }
 
-extern "C" rsd_status rsd_svao_pass1_band(const rsd_camera* cam, const rsd_vao_data* vao, const rsd_svao_params* p,
-                                          const float* d_depth, const uint16_t* d_normals, uint32_t W, uint32_t H,
-                                          uint8_t* d_ao, uint8_t* d_stencil, uint32_t* d_ray_min, uint32_t* d_ray_max,
-                                          uint32_t sd_w, uint32_t sd_h, uint32_t band_index, uint32_t band_count,
-                                          rsd_stream stream) {
-    rsd_status st = check_band(band_index, band_count, "rsd_svao_pass1_band");
-    if (st != RSD_OK) return st;
-    st = check_common(cam, vao, p, d_depth, d_normals, W, H, "rsd_svao_pass1");
+// 32-row groups g = start + k * step, k < n -- or, with n = ~0u, every group of an interleaved band
+// (start = index, step = count) -- counted from the first visible row
+namespace {
+rsd_status pass1_impl(const rsd_camera* cam, const rsd_vao_data* vao, const rsd_svao_params* p, const float* d_depth,
+                      const uint16_t* d_normals, uint32_t W, uint32_t H, uint8_t* d_ao, uint8_t* d_stencil,
+                      uint32_t* d_ray_min, uint32_t* d_ray_max, uint32_t sd_w, uint32_t sd_h, uint32_t start,
+                      uint32_t step, uint32_t n, rsd_stream stream) {
+    rsd_status st = check_common(cam, vao, p, d_depth, d_normals, W, H, "rsd_svao_pass1");
     if (st != RSD_OK) return st;
     if (!d_ao || !d_stencil || (p->secondary_depth_mode == 2 && (!d_ray_min || !d_ray_max || !sd_w || !sd_h))) {
         set_error("rsd_svao_pass1: null output buffer");
@@ -427,22 +428,46 @@ extern "C" rsd_status rsd_svao_pass1_band(const rsd_camera* cam, const rsd_vao_d
     // SVAO.cpp:347-350: nThreads = roundup32(dims - 2 guardBand), 16x16 groups
     const uint32_t nx = (W - 2 * p->guard_band + 31u) / 32u * 32u, ny = (H - 2 * p->guard_band + 31u) / 32u * 32u;
     const uint32_t groups = ny / 32u;
-    const uint32_t bandGroups = groups > band_index ? (groups - band_index + band_count - 1) / band_count : 0u;
-    a.bandIndex = band_index;
-    a.bandCount = band_count;
+    const uint32_t bandGroups = std::min(n, groups > start ? (groups - start + step - 1) / step : 0u);
+    a.bandIndex = start;
+    a.bandCount = step;
     if (bandGroups == 0) return RSD_OK;
     hipLaunchKernelGGL(svao_pass1_kernel, dim3(nx / 16, 2 * bandGroups), dim3(16, 16), 0, (hipStream_t)stream, a);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? RSD_OK : hip_fail(e, "svao_pass1_kernel launch");
 }
+}  // namespace
 
-extern "C" rsd_status rsd_svao_pass2_band(const rsd_camera* cam, const rsd_vao_data* vao, const rsd_svao_params* p,
+extern "C" rsd_status rsd_svao_pass1_band(const rsd_camera* cam, const rsd_vao_data* vao, const rsd_svao_params* p,
                                           const float* d_depth, const uint16_t* d_normals, uint32_t W, uint32_t H,
-                                          const uint8_t* d_stencil, const float* d_sd, uint32_t sd_w, uint32_t sd_h,
-                                          uint8_t* d_ao, uint32_t band_index, uint32_t band_count, rsd_stream stream) {
-    rsd_status st = check_band(band_index, band_count, "rsd_svao_pass2_band");
+                                          uint8_t* d_ao, uint8_t* d_stencil, uint32_t* d_ray_min, uint32_t* d_ray_max,
+                                          uint32_t sd_w, uint32_t sd_h, uint32_t band_index, uint32_t band_count,
+                                          rsd_stream stream) {
+    rsd_status st = check_band(band_index, band_count, "rsd_svao_pass1_band");
     if (st != RSD_OK) return st;
-    st = check_common(cam, vao, p, d_depth, d_normals, W, H, "rsd_svao_pass2");
+    return pass1_impl(cam, vao, p, d_depth, d_normals, W, H, d_ao, d_stencil, d_ray_min, d_ray_max, sd_w, sd_h,
+                      band_index, band_count, ~0u, stream);
+}
+
+extern "C" rsd_status rsd_svao_pass1_rows(const rsd_camera* cam, const rsd_vao_data* vao, const rsd_svao_params* p,
+                                          const float* d_depth, const uint16_t* d_normals, uint32_t W, uint32_t H,
+                                          uint8_t* d_ao, uint8_t* d_stencil, uint32_t* d_ray_min, uint32_t* d_ray_max,
+                                          uint32_t sd_w, uint32_t sd_h, uint32_t row0, uint32_t row1,
+                                          rsd_stream stream) {
+    if (row0 > row1 || row0 % 32u != 0u || (row1 % 32u != 0u && row1 + 2u * (uint32_t)p->guard_band < H)) {
+        set_error("rsd_svao_pass1_rows: rows must be multiples of 32 from the first visible row (row1 may end the frame)");
+        return RSD_ERR_INVALID_ARG;
+    }
+    return pass1_impl(cam, vao, p, d_depth, d_normals, W, H, d_ao, d_stencil, d_ray_min, d_ray_max, sd_w, sd_h,
+                      row0 / 32u, 1u, (row1 - row0 + 31u) / 32u, stream);
+}
+
+namespace {
+rsd_status pass2_impl(const rsd_camera* cam, const rsd_vao_data* vao, const rsd_svao_params* p, const float* d_depth,
+                      const uint16_t* d_normals, uint32_t W, uint32_t H, const uint8_t* d_stencil, const float* d_sd,
+                      uint32_t sd_w, uint32_t sd_h, uint8_t* d_ao, uint32_t start, uint32_t step, uint32_t n,
+                      rsd_stream stream) {
+    rsd_status st = check_common(cam, vao, p, d_depth, d_normals, W, H, "rsd_svao_pass2");
     if (st != RSD_OK) return st;
     if (!d_stencil || !d_sd || !d_ao || !sd_w || !sd_h) {
         set_error("rsd_svao_pass2: null buffer");
@@ -479,9 +504,9 @@ extern "C" rsd_status rsd_svao_pass2_band(const rsd_camera* cam, const rsd_vao_d
     a.N = N;
     const uint32_t vw = W - 2 * p->guard_band, vh = H - 2 * p->guard_band;
     const uint32_t groups = (vh + 31u) / 32u;
-    const uint32_t bandGroups = groups > band_index ? (groups - band_index + band_count - 1) / band_count : 0u;
-    a.bandIndex = band_index;
-    a.bandCount = band_count;
+    const uint32_t bandGroups = std::min(n, groups > start ? (groups - start + step - 1) / step : 0u);
+    a.bandIndex = start;
+    a.bandCount = step;
     if (bandGroups == 0) return RSD_OK;
     dim3 grid((vw + kP2Tile - 1) / kP2Tile, (32 / kP2Tile) * bandGroups), block(kP2Lanes);
     hipStream_t s = (hipStream_t)stream;
@@ -494,6 +519,29 @@ extern "C" rsd_status rsd_svao_pass2_band(const rsd_camera* cam, const rsd_vao_d
     }
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? RSD_OK : hip_fail(e, "svao_pass2_kernel launch");
+}
+}  // namespace
+
+extern "C" rsd_status rsd_svao_pass2_band(const rsd_camera* cam, const rsd_vao_data* vao, const rsd_svao_params* p,
+                                          const float* d_depth, const uint16_t* d_normals, uint32_t W, uint32_t H,
+                                          const uint8_t* d_stencil, const float* d_sd, uint32_t sd_w, uint32_t sd_h,
+                                          uint8_t* d_ao, uint32_t band_index, uint32_t band_count, rsd_stream stream) {
+    rsd_status st = check_band(band_index, band_count, "rsd_svao_pass2_band");
+    if (st != RSD_OK) return st;
+    return pass2_impl(cam, vao, p, d_depth, d_normals, W, H, d_stencil, d_sd, sd_w, sd_h, d_ao, band_index, band_count,
+                      ~0u, stream);
+}
+
+extern "C" rsd_status rsd_svao_pass2_rows(const rsd_camera* cam, const rsd_vao_data* vao, const rsd_svao_params* p,
+                                          const float* d_depth, const uint16_t* d_normals, uint32_t W, uint32_t H,
+                                          const uint8_t* d_stencil, const float* d_sd, uint32_t sd_w, uint32_t sd_h,
+                                          uint8_t* d_ao, uint32_t row0, uint32_t row1, rsd_stream stream) {
+    if (row0 > row1 || row0 % 32u != 0u || (row1 % 32u != 0u && row1 + 2u * (uint32_t)p->guard_band < H)) {
+        set_error("rsd_svao_pass2_rows: rows must be multiples of 32 from the first visible row (row1 may end the frame)");
+        return RSD_ERR_INVALID_ARG;
+    }
+    return pass2_impl(cam, vao, p, d_depth, d_normals, W, H, d_stencil, d_sd, sd_w, sd_h, d_ao, row0 / 32u, 1u,
+                      (row1 - row0 + 31u) / 32u, stream);
 }
 
 extern "C" rsd_status rsd_svao_pass1(const rsd_camera* cam, const rsd_vao_data* vao, const rsd_svao_params* p,

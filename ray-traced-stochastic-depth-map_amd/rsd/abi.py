@@ -108,7 +108,7 @@ EXPORTS = ["rsd_abi_version", "rsd_last_error", "rsd_device_open", "rsd_device_c
            "rsd_sd_trace_band", "rsd_svao_pass1_band", "rsd_svao_pass2_band", "rsd_gbuffer_raster",
            "rsd_linearize_depth", "rsd_compress_normals", "rsd_svao_pass2_raytraced", "rsd_svao_pass2_raytraced_band",
            "rsd_scene_upload_alpha", "rsd_ray_cone_spread", "rsd_sd_trace_band_ex", "rsd_scene_export_bvh",
-           "rsd_bvh_build"]
+           "rsd_bvh_build", "rsd_svao_pass1_rows", "rsd_svao_pass2_rows", "rsd_sd_trace_rows"]
 
 SD_CONSUME_INTERVALS = 1
 SD_THROUGHPUT = 2  # frames in flight: the work-efficient traversal (rsd.h RSD_SD_THROUGHPUT)
@@ -190,6 +190,13 @@ def lib():
         L.rsd_svao_pass2_band.restype = st
         L.rsd_svao_pass2_band.argtypes = [C.POINTER(Camera), C.POINTER(VAOData), C.POINTER(SVAOParams), vp, vp, u32,
                                           u32, vp, vp, u32, u32, vp, u32, u32, vp]
+        L.rsd_svao_pass1_rows.restype = st
+        L.rsd_svao_pass1_rows.argtypes = L.rsd_svao_pass1_band.argtypes
+        L.rsd_svao_pass2_rows.restype = st
+        L.rsd_svao_pass2_rows.argtypes = L.rsd_svao_pass2_band.argtypes
+        L.rsd_sd_trace_rows.restype = st
+        L.rsd_sd_trace_rows.argtypes = [vp, C.POINTER(Camera), C.POINTER(SDParams), vp, u32, u32, vp, vp, vp, u32,
+                                        u32, u32, u32, u32, C.POINTER(Counters), vp]
         L.rsd_svao_pass2_raytraced.restype = st
         L.rsd_svao_pass2_raytraced.argtypes = [vp, C.POINTER(Camera), C.POINTER(VAOData), C.POINTER(SVAOParams), vp, vp,
                                                u32, u32, vp, vp, u32, u32, u32, vp]

@@ -327,6 +327,32 @@ class Renderer:
                                                 _ptr(self.stencil), _ptr(self.sd), self.sd_w, self.sd_h,
                                                 _ptr(self.ao), band[0], band[1], self.stream), "rsd_svao_pass2_band")
 
+    # ---- contiguous screen bands (rsd/shard.py HaloFrame): visible rows / SD rows [row0, row1)
+    def pass1_rows(self, rows):
+        abi.check(abi.lib().rsd_svao_pass1_rows(C.byref(self.cam), C.byref(self.vao), C.byref(self.svp),
+                                                _ptr(self.depth), _ptr(self.normals), self.cfg.fb_w, self.cfg.fb_h,
+                                                _ptr(self.ao), _ptr(self.stencil), _ptr(self.ray_min),
+                                                _ptr(self.ray_max), self.sd_w, self.sd_h, rows[0], rows[1],
+                                                self.stream), "rsd_svao_pass1_rows")
+
+    def sd_trace_rows(self, rows, consume: bool = False, throughput: bool = False, counters: bool = False):
+        cnt = abi.Counters() if counters else None
+        flags = (abi.SD_CONSUME_INTERVALS if consume else 0) | (abi.SD_THROUGHPUT if throughput else 0)
+        abi.check(abi.lib().rsd_sd_trace_rows(self.gscene.h, C.byref(self.cam), C.byref(self.sdp), _ptr(self.depth),
+                                              self.cfg.fb_w, self.cfg.fb_h, _ptr(self.ray_min), _ptr(self.ray_max),
+                                              _ptr(self.sd), self.sd_w, self.sd_h, rows[0], rows[1], flags,
+                                              C.byref(cnt) if cnt is not None else None, self.stream),
+                  "rsd_sd_trace_rows")
+        return cnt
+
+    def pass2_rows(self, rows):
+        if self.cfg.use_16bit:
+            raise ValueError("SVAO pass 2 reads 32-bit SD maps; Use16Bit is a standalone SD-pass property")
+        abi.check(abi.lib().rsd_svao_pass2_rows(C.byref(self.cam), C.byref(self.vao), C.byref(self.svp),
+                                                _ptr(self.depth), _ptr(self.normals), self.cfg.fb_w, self.cfg.fb_h,
+                                                _ptr(self.stencil), _ptr(self.sd), self.sd_w, self.sd_h,
+                                                _ptr(self.ao), rows[0], rows[1], self.stream), "rsd_svao_pass2_rows")
+
     def pass2_raytraced(self, band=(0, 1)):
         abi.check(abi.lib().rsd_svao_pass2_raytraced_band(self.gscene.h, C.byref(self.cam), C.byref(self.vao),
                                                           C.byref(self.svp), _ptr(self.depth), _ptr(self.normals),

@@ -132,3 +132,174 @@ class BandFrame:
         b.pass2(band=band)
         if self.world > 1:
             self._gather_rows(b.ao, self.ao_rows, self.ao_send, self.ao_recv, 0, self.ao_unpack)
+
+
+def halo_px(cfg, max_radius_px: float = 512.0) -> int:
+    """Bound (frame-buffer pixels, vertical) on how far from its pixel an SVAO sample lands: the
+    AO disk (world radius R with R * f / z <= ssMaxRadius, VAOData.slang:44; Common.slang:285-300)
+    lies in the plane perpendicular to the view ray, so off-axis it projects larger than
+    ssMaxRadius (perspective stretch, ~1/cos of the ray angle and more at the frame corners).
+    Evaluated numerically over the frame border (where the stretch is largest) for the config's
+    pinhole camera (focal length / frame height, Camera.cpp:99-185), plus 4 px of slack."""
+    import numpy as np
+    W, H = cfg.fb_w, cfg.fb_h
+    f = cfg.focal_length / cfg.frame_height * H  # focal length in pixels (preserveHeight)
+    # border pixels (x, y) relative to the principal point, and 64 disk directions
+    t = np.linspace(0.0, 1.0, 257)
+    xs = np.concatenate([(t - 0.5) * W, np.full_like(t, -0.5 * W), np.full_like(t, 0.5 * W), (t - 0.5) * W])
+    ys = np.concatenate([np.full_like(t, -0.5 * H), (t - 0.5) * H, (t - 0.5) * H, np.full_like(t, 0.5 * H)])
+    worst = 0.0
+    for x, y in zip(xs, ys):
+        d = np.array([x, y, f]) / np.linalg.norm([x, y, f])  # view ray (z = 1 at the image plane)
+        P = d / d[2]  # the point at linear depth z = 1
+        R = max_radius_px / f  # world radius at z = 1 whose screen radius is max_radius_px
+        a = np.cross(d, [0.0, 1.0, 0.0]) if abs(d[1]) < 0.99 else np.cross(d, [1.0, 0.0, 0.0])
+        a /= np.linalg.norm(a)
+        b = np.cross(d, a)
+        ang = np.linspace(0.0, 2.0 * np.pi, 64, endpoint=False)
+        S = P[None, :] + R * (np.cos(ang)[:, None] * a[None, :] + np.sin(ang)[:, None] * b[None, :])
+        worst = max(worst, float(np.abs(f * S[:, 1] / S[:, 2] - y).max()))
+    return int(np.ceil(worst)) + 4
+
+
+class HaloFrame:
+    """One AO frame split into CONTIGUOUS screen bands with halo exchanges:
+    the ranks exchange only the rows within reach of each other's samples instead of
+    all-reducing / all-gathering whole maps.
+
+    Rank r of B owns visible rows [32 g_r, 32 g_{r+1}) (32-row groups split evenly) and the SD
+    rows [S_r, S_{r+1}) under them (8-row aligned).  Per frame:
+
+      1. pass 1 of its own rows (rsd_svao_pass1_rows) -- its partial ray intervals land within
+         `halo` SD rows of its band (the window W_r);
+      2. interval halo exchange: the part of W_r inside band k goes to rank k, which merges it
+         with MIN / MAX (exact on the non-negative float bit patterns) -> every rank holds the
+         exact union for its own SD rows, like the 1-GPU pass 1;
+      3. SD trace of its own SD rows (rsd_sd_trace_rows; consume resets the whole map);
+      4. SD halo exchange: rank k sends the rows of its band inside W_r to rank r (pass 2 of
+         band r reads SD texels only inside W_r);
+      5. pass 2 of its own rows (rsd_svao_pass2_rows) and an all-gather of the AO bands.
+
+    Every SD texel and AO pixel is produced by exactly one rank with the same kernels, so the
+    frame is bit-identical to the 1-GPU frame.  Data per rank and frame: 2 x 4 B per texel of
+    the interval halo rows and 4N B per texel of the SD halo rows, instead of the whole maps.
+
+    `backend` provides pass1_rows(rows), sd_trace_rows(rows, consume=...), pass2_rows(rows),
+    clear_intervals(), tensors ray_minmax (int32 [2, sdH, sdW]), sd, ao, and cfg / vao / sd_h."""
+
+    def __init__(self, backend, rank: int = 0, world: int = 1, pg=None, throughput: bool = False):
+        import torch.distributed as dist
+        b = self.b = backend
+        self.rank, self.world, self.pg = rank, world, pg
+        self.dist = dist if world > 1 else None
+        self.trace_kw = {"throughput": True} if throughput and getattr(b, "can_consume_intervals", False) else {}
+        self._intervals_clear = False
+        cfg = b.cfg
+        g, div, sdg, sdh = cfg.guard_band, cfg.divisor, int(b.vao.sdGuard), b.sd_h
+        V = cfg.fb_h - 2 * g
+        G = (V + 31) // 32
+        gb = [G * r // world for r in range(world + 1)]
+        self.px_rows = [(32 * gb[r], 32 * gb[r + 1]) for r in range(world)]  # visible rows, API ranges
+        # SD rows under each band: SD row of frame-buffer row y = y / div + sdGuard (SVAO.cpp:700-716)
+        S = [0] + [min(sdh, ((g + 32 * gb[r]) // div + sdg) // 8 * 8) for r in range(1, world)] + [sdh]
+        for r in range(1, world + 1):
+            S[r] = max(S[r], S[r - 1])
+        self.sd_rows = [(S[r], S[r + 1]) for r in range(world)]
+        self.halo_px = halo_px(cfg, float(b.vao.ssMaxRadius))
+        self.window = []
+        for r in range(world):
+            a_px = g + self.px_rows[r][0] - self.halo_px
+            b_px = g + min(self.px_rows[r][1], V) + self.halo_px
+            self.window.append((max(0, a_px // div + sdg - 1), min(sdh, b_px // div + sdg + 2)))
+
+        def overlap(a, c):
+            lo, hi = max(a[0], c[0]), min(a[1], c[1])
+            return (lo, hi) if lo < hi else None
+        # interval halo: my window inside band k -> rank k;  SD halo: band k inside my window <- rank k
+        me = rank
+        self.iv_send = {k: overlap(self.window[me], self.sd_rows[k]) for k in range(world) if k != me}
+        self.iv_recv = {k: overlap(self.window[k], self.sd_rows[me]) for k in range(world) if k != me}
+        self.sd_send = {k: overlap(self.window[k], self.sd_rows[me]) for k in range(world) if k != me}
+        self.sd_recv = {k: overlap(self.window[me], self.sd_rows[k]) for k in range(world) if k != me}
+        dev = b.sd.device
+        mk = lambda t, rows: torch.empty((t.shape[0], rows[1] - rows[0]) + tuple(t.shape[2:]), dtype=t.dtype,  # noqa: E731
+                                         device=dev)
+        self.iv_sbuf = {k: mk(b.ray_minmax, r) for k, r in self.iv_send.items() if r}
+        self.iv_rbuf = {k: mk(b.ray_minmax, r) for k, r in self.iv_recv.items() if r}
+        self.sd_sbuf = {k: mk(b.sd, r) for k, r in self.sd_send.items() if r}
+        self.sd_rbuf = {k: mk(b.sd, r) for k, r in self.sd_recv.items() if r}
+        # AO bands (frame-buffer rows), padded to the largest for one all-gather.  Pass 1 dispatches
+        # roundup32 of the visible rows (SVAO.cpp:347-349), so the last band also writes the AO of up
+        # to 31 guard-band rows below the visible region.
+        self.ao_rows = [(g + self.px_rows[r][0], min(cfg.fb_h, g + self.px_rows[r][1])) for r in range(world)]
+        self.ao_max = max(hi - lo for lo, hi in self.ao_rows)
+        W = b.ao.shape[1]
+        self.ao_send = torch.zeros((self.ao_max, W), dtype=b.ao.dtype, device=dev)
+        self.ao_recv = torch.zeros((world, self.ao_max, W), dtype=b.ao.dtype, device=dev)
+        self.nccl = world > 1 and dist.get_backend(pg) == "nccl"
+
+    def bytes_per_frame(self):
+        """Bytes this rank sends per frame: interval halo, SD halo, AO band."""
+        iv = sum(t.numel() * t.element_size() for t in self.iv_sbuf.values())
+        sd = sum(t.numel() * t.element_size() for t in self.sd_sbuf.values())
+        return {"intervals": iv, "sd": sd, "ao": self.ao_send.numel() * self.ao_send.element_size()}
+
+    def _exchange(self, sends, recvs):
+        """Point-to-point exchange (ncclSend / ncclRecv under RCCL): sends {peer: tensor}, recvs
+        {peer: tensor}; returns after every transfer completed (stream-ordered for NCCL)."""
+        staged = not self.nccl and any(t.is_cuda for t in list(sends.values()) + list(recvs.values()))
+        if staged:  # gloo rehearsal with device tensors (several ranks on one GPU): via host copies
+            sends = {k: t.cpu() for k, t in sends.items()}
+            recvs_dev, recvs = recvs, {k: torch.empty(t.shape, dtype=t.dtype) for k, t in recvs.items()}
+        ops = [self.dist.P2POp(self.dist.isend, t, k, group=self.pg) for k, t in sends.items()]
+        ops += [self.dist.P2POp(self.dist.irecv, t, k, group=self.pg) for k, t in recvs.items()]
+        if ops:
+            for w in self.dist.batch_isend_irecv(ops):
+                w.wait()
+        if staged:
+            for k, t in recvs.items():
+                recvs_dev[k].copy_(t)
+
+    def frame(self, sd_events=None):
+        b, me = self.b, self.rank
+        consume = getattr(b, "can_consume_intervals", False) and bool(b.cfg.ray_interval)
+        if not (consume and self._intervals_clear):
+            b.clear_intervals()
+        b.pass1_rows(self.px_rows[me])
+        if self.world > 1 and b.cfg.ray_interval:
+            for k, t in self.iv_sbuf.items():
+                lo, hi = self.iv_send[k]
+                t.copy_(b.ray_minmax[:, lo:hi])
+            self._exchange(self.iv_sbuf, self.iv_rbuf)
+            for k, t in self.iv_rbuf.items():
+                lo, hi = self.iv_recv[k]
+                torch.minimum(b.ray_minmax[0, lo:hi], t[0], out=b.ray_minmax[0, lo:hi])
+                torch.maximum(b.ray_minmax[1, lo:hi], t[1], out=b.ray_minmax[1, lo:hi])
+        if sd_events:
+            sd_events[0].record()
+        if consume:
+            b.sd_trace_rows(self.sd_rows[me], consume=True, **self.trace_kw)
+        else:
+            b.sd_trace_rows(self.sd_rows[me], **self.trace_kw)
+        self._intervals_clear = consume
+        if sd_events:
+            sd_events[1].record()
+        if self.world > 1:
+            for k, t in self.sd_sbuf.items():
+                lo, hi = self.sd_send[k]
+                t.copy_(b.sd[:, lo:hi])
+            self._exchange(self.sd_sbuf, self.sd_rbuf)
+            for k, t in self.sd_rbuf.items():
+                lo, hi = self.sd_recv[k]
+                b.sd[:, lo:hi].copy_(t)
+        b.pass2_rows(self.px_rows[me])
+        if self.world > 1:
+            lo, hi = self.ao_rows[me]
+            self.ao_send[:hi - lo].copy_(b.ao[lo:hi])
+            if self.nccl:
+                self.dist.all_gather_into_tensor(self.ao_recv.view(-1), self.ao_send.view(-1), group=self.pg)
+            else:
+                self.dist.all_gather(list(self.ao_recv.unbind(0)), self.ao_send, group=self.pg)
+            for k, (lo, hi) in enumerate(self.ao_rows):
+                if k != me:
+                    b.ao[lo:hi].copy_(self.ao_recv[k, :hi - lo])

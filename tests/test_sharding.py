@@ -17,13 +17,15 @@ from helpers import oracle_vao, small_frame_config
 class OracleBackend:
     """BandFrame backend on the CPU oracle; numpy buffers shared with torch tensors."""
 
-    def __init__(self, O, scene, cfg):
+    def __init__(self, O, scene, cfg, ss_max_radius=None):
         self.O, self.cfg = O, cfg
         self.osc = O.Scene(scene.positions, scene.indices, scene.flags)
         W, H = cfg.fb_w, cfg.fb_h
         aspect = float(np.float32(W) / np.float32(H))
         self.cam = O.camera_look_at(scene.camera["pos"], scene.camera["target"], scene.camera["up"], aspect=aspect)
         self.vao, self.sd_w, self.sd_h = oracle_vao(O, W, H, cfg.divisor, cfg.sd_guard_px, cfg.radius)
+        if ss_max_radius is not None:  # a small sample reach: halo windows narrower than the map
+            self.vao.ssMaxRadius = ss_max_radius
         N = cfg.sd_samples
         self.sdp = O.SDParams(N, cfg.implementation, cfg.max_count, self.vao.sdGuard, 1, 1, 1, cfg.cull_mode, 0,
                               float(np.float32(1.5 / N)))
@@ -56,12 +58,25 @@ class OracleBackend:
         self.O.svao_pass2_into(self.cam, self.vao, self.svp, self.z, self.n, self.np_st, self.np_sd, self.np_ao, band,
                                threads=2)
 
+    # contiguous bands (HaloFrame)
+    def pass1_rows(self, rows):
+        self.O.svao_pass1_rows_into(self.cam, self.vao, self.svp, self.z, self.n, self.np_ao, self.np_st, self.np_rmin,
+                                    self.np_rmax, rows)
+
+    def sd_trace_rows(self, rows):
+        self.O.sd_trace_rows_into(self.osc, self.cam, self.sdp, self.z, self.np_rmin, self.np_rmax, self.np_sd, rows,
+                                  threads=2)
+
+    def pass2_rows(self, rows):
+        self.O.svao_pass2_rows_into(self.cam, self.vao, self.svp, self.z, self.n, self.np_st, self.np_sd, self.np_ao,
+                                    rows, threads=2)
+
 
 def _cfg():
     return small_frame_config(visible=(192, 104), guard=16, divisor=2, N=4)
 
 
-def _worker(rank, world, port, out_dir):
+def _worker(rank, world, port, out_dir, mode="band"):
     import sys
     from pathlib import Path
     root = Path(__file__).resolve().parents[1]
@@ -72,10 +87,14 @@ def _worker(rank, world, port, out_dir):
 
     from oracle import oracle as O
     from rsd.scenes import make_scene
-    from rsd.shard import BandFrame
+    from rsd.shard import BandFrame, HaloFrame
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
-    be = OracleBackend(O, make_scene("arcade_tiny"), _cfg())
-    BandFrame(be, rank, world).frame()
+    cfg = _cfg() if mode == "band" else _halo_cfg()
+    be = OracleBackend(O, make_scene("arcade_tiny"), cfg, None if mode == "band" else HALO_REACH)
+    f = (BandFrame if mode == "band" else HaloFrame)(be, rank, world)
+    f.frame()
+    if mode == "halo":
+        f.frame()  # a second frame: intervals cleared again, the exchange buffers reused
     np.save(os.path.join(out_dir, f"ao_{rank}.npy"), be.np_ao)
     np.save(os.path.join(out_dir, f"sd_{rank}.npy"), be.np_sd)
     dist.barrier()
@@ -103,6 +122,72 @@ def test_band_sharded_frame_equals_single_process(oracle, tmp_path, world):
         assert np.array_equal(np.load(tmp_path / f"ao_{r}.npy"), ref.np_ao), f"rank {r} AO"
         assert np.array_equal(np.load(tmp_path / f"sd_{r}.npy").view(np.uint32), ref.np_sd.view(np.uint32)), \
             f"rank {r} SD map"
+
+
+HALO_REACH = 24.0  # ssMaxRadius of the halo tests: ~40-px windows in a 448-row frame
+
+
+def _halo_cfg():
+    return small_frame_config(visible=(96, 448), guard=16, divisor=2, N=2)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_halo_sharded_frame_equals_single_process(oracle, tmp_path, world):
+    """HaloFrame (contiguous bands, interval + SD halo exchange over point-to-point sends):
+    every rank ends with the single-process AO image; its own SD rows equal the reference."""
+    from rsd.scenes import make_scene
+    from rsd.shard import BandFrame
+    ref = OracleBackend(oracle, make_scene("arcade_tiny"), _halo_cfg(), HALO_REACH)
+    BandFrame(ref, 0, 1).frame()
+    assert (ref.np_st != 0).any()
+    mp.start_processes(_worker, args=(world, _free_port(), str(tmp_path), "halo"), nprocs=world, join=True,
+                       start_method="spawn")
+    for r in range(world):
+        assert np.array_equal(np.load(tmp_path / f"ao_{r}.npy"), ref.np_ao), f"rank {r} AO"
+        sd = np.load(tmp_path / f"sd_{r}.npy")
+        lo, hi = _halo_plan(oracle, world, r).sd_rows[r]
+        assert np.array_equal(sd[:, lo:hi].view(np.uint32), ref.np_sd[:, lo:hi].view(np.uint32)), f"rank {r} SD"
+    p = _halo_plan(oracle, world, 0)
+    assert p.window[0][1] < p.b.sd_h  # rank 0 did not receive the whole map
+
+
+def _halo_plan(oracle, world, rank):
+    """The HaloFrame partition of _halo_cfg() as seen by `rank` (no process group needed)."""
+    from types import SimpleNamespace
+
+    from rsd.shard import HaloFrame
+    cfg = _halo_cfg()
+    vao, sd_w, sd_h = oracle_vao(oracle, cfg.fb_w, cfg.fb_h, cfg.divisor, cfg.sd_guard_px, cfg.radius)
+    vao.ssMaxRadius = HALO_REACH
+    N = cfg.sd_samples
+    be = SimpleNamespace(cfg=cfg, vao=vao, sd_h=sd_h, sd=torch.zeros((1, sd_h, sd_w, N)),
+                         ray_minmax=torch.zeros((2, sd_h, sd_w), dtype=torch.int32),
+                         ao=torch.zeros((cfg.fb_h, cfg.fb_w), dtype=torch.uint8))
+    import torch.distributed as dist
+    orig = dist.get_backend
+    dist.get_backend = lambda pg=None: "gloo"
+    try:
+        return HaloFrame(be, rank, world)
+    finally:
+        dist.get_backend = orig
+
+
+def test_halo_plan_partitions_and_bounds(oracle):
+    for world in (1, 2, 3, 4):
+        plans = [_halo_plan(oracle, world, r) for r in range(world)]
+        p0 = plans[0]
+        # pixel groups and SD rows partition the frame / map
+        assert p0.px_rows[0][0] == 0 and all(p0.px_rows[r][1] == p0.px_rows[r + 1][0] for r in range(world - 1))
+        assert p0.sd_rows[0][0] == 0 and p0.sd_rows[-1][1] == plans[0].b.sd_h
+        assert all(p0.sd_rows[r][1] == p0.sd_rows[r + 1][0] for r in range(world - 1))
+        for r, p in enumerate(plans):
+            assert p.window[r][0] < p.window[r][1]
+            if world >= 3:  # the halo is a real restriction: a window leaves rows of the map out
+                assert any(q.window[k] != (0, q.b.sd_h) for k, q in enumerate(plans))
+            # what r sends to k is what k expects from r (same row ranges on both sides)
+            for k, q in enumerate(plans):
+                if k != r:
+                    assert p.iv_send[k] == q.iv_recv[r] and p.sd_recv[k] == q.sd_send[r]
 
 
 def test_band_rows_partition():
