@@ -308,14 +308,14 @@ def main():
         "ao_frames_per_s": round(units * 1e3 / seq_ao_ms, 2),
         "ao_span_ms": round(seq_ao_ms, 4),
         "latency": {"ms_per_frame": round(wall_seq / args.steps * 1e3, 4), "frames": args.steps,
-                    "walk": ["quad", "fused", "split"][walk_seq],
+                    "walk": abi.WALK_NAMES[walk_seq],
                     "note": "one frame in flight; ms_per_frame includes the G-buffer of a camera path, "
                             "ao_span_ms does not"},
         "throughput": {"frames_in_flight": F, "frames": frames_thr, "ms_per_frame": round(wall_thr / args.steps * 1e3, 4),
                        "ao_frames_per_s": round(frames_thr / wall_thr, 2),
                        "frame_mrays_per_s": round(rays * frames_thr / wall_thr / 1e6, 2),
                        "sd_kernel_ms_overlapped": round(thr_sd_ms, 4),
-                       "walk": ["quad", "fused", "split"][walk_thr]},
+                       "walk": abi.WALK_NAMES[walk_thr]},
         "traversal": {"nodes_per_ray": round(nodes_seq / rays / units, 3),
                       "tris_per_ray": round(tris_seq / rays / units, 3),
                       "nodes_per_active_ray": round(nodes_seq / max(rays_active, 1), 2),

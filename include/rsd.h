@@ -184,6 +184,7 @@ typedef struct {
 #define RSD_WALK_FUSED 1u  /* sd_trace_row_kernel with the algorithm in-kernel */
 #define RSD_WALK_SPLIT 2u  /* sd_trace_row_kernel (K nearest keys) + sd_resolve_row_kernel */
 #define RSD_WALK_ORDERED 3u /* sd_trace_ordered_kernel: RSD_HIT_ORDER_TRAVERSAL */
+#define RSD_WALK_RASTER 4u  /* sd_raster_kernel (triangles -> K nearest keys per texel) + sd_resolve_row_kernel */
 
 /* --- library / device ------------------------------------------------------------ */
 uint32_t rsd_abi_version(void);

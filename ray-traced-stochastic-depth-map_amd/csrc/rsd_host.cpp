@@ -117,6 +117,26 @@ extern "C" rsd_status rsd_scene_upload(rsd_device* dev, const rsd_scene_desc* de
     s->d_tris = s->d_nodes + s->tri_offset;
     s->device_bytes = total;
     s->bvh_bytes = total;
+    if (desc->triangle_count) {
+        // primitive id -> triangle record (record r holds prim in v0.w): the raster SD walk keys its
+        // hits by (t, prim) and its resolve pass needs the record of each key
+        std::vector<uint32_t> pr(desc->triangle_count, 0u);
+        for (uint32_t r = 0; r < desc->triangle_count; ++r) {
+            uint32_t prim;
+            std::memcpy(&prim, &bvh.tris[(size_t)r * 12 + 3], 4);
+            pr[prim] = r;
+        }
+        e = hipMalloc(&s->d_prim_rec, pr.size() * 4);
+        if (e == hipSuccess) e = hipMemcpy(s->d_prim_rec, pr.data(), pr.size() * 4, hipMemcpyHostToDevice);
+        if (e != hipSuccess) {
+            rsd_status st = rsd::hip_fail(e, "rsd_scene_upload (prim map)");
+            (void)hipFree(s->d_prim_rec);
+            (void)hipFree(s->d_nodes);
+            delete s;
+            return st;
+        }
+        s->device_bytes += pr.size() * 4;
+    }
     *out = s;
     return RSD_OK;
 }
@@ -325,6 +345,7 @@ extern "C" void rsd_scene_release(rsd_scene* s) {
     if (!s) return;
     (void)hipSetDevice(s->dev->hip_device);
     (void)hipFree(s->d_nodes);
+    (void)hipFree(s->d_prim_rec);
     rsd::release_sd_workspaces(s);
     (void)hipFree(s->d_alpha);
     delete s;

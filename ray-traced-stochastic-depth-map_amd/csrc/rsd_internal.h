@@ -57,6 +57,8 @@ struct SdWorkspace {
     size_t queue_cap = 0;          // bytes
     RayTabCache raytab;
     unsigned long long* counters = nullptr;  // 16 x u64 scratch of instrumented traces on this stream
+    void* raster = nullptr;        // raster walk: slot map, tile records, 64-bit key lists (grow-only)
+    size_t raster_cap = 0;         // bytes
 };
 void release_sd_workspaces(rsd_scene* s);
 }  // namespace rsd
@@ -72,6 +74,7 @@ struct rsd_scene {
     uint32_t build_threads = 0;  // host threads of the BVH build
     uint64_t device_bytes = 0;
     uint64_t bvh_bytes = 0;      // the d_nodes allocation (nodes + triangle records + pad)
+    uint32_t* d_prim_rec = nullptr;  // primitive id -> triangle record index (raster walk's keys)
     std::vector<rsd::SdWorkspace*> sd_ws;  // one per stream that traced this scene (few: linear lookup)
     void* d_alpha = nullptr;       // alpha data (rsd_scene_upload_alpha), one allocation
     rsd::AlphaData alpha;          // device pointers into d_alpha

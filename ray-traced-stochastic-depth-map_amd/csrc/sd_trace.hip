@@ -68,6 +68,18 @@ struct SDArgs {
     uint32_t alphaTest;   // USE_ALPHA_TEST and the scene has alpha data
     AlphaData alphaData;  // spread = RAY_CONE_SPREAD
     uint32_t f16;         // Use16Bit: the map is R16F / RG16F / RGBA16F (N <= 4)
+    // raster walk (RSD_WALK_RASTER): per-texel queue slot (-1: no live ray), per-8x8-tile view-depth
+    // range of its live rays, the K-key lists of the live rays (64-bit (t bits, prim) keys), the
+    // prim -> triangle record map, and the camera projection onto the SD texel grid
+    uint32_t raster, keysK, nTris;
+    int32_t* slotMap;
+    float2* tileRec;
+    unsigned long long* keys64;
+    const uint32_t* primRec;
+    int tilesW;
+    float projU[3], projV[3], projW[3];  // U / |U|^2, V / |V|^2, W / |W|^2
+    float camWn[3];                      // normalize(W): view depth of a point = dot(P - o, Wn)
+    float wClip;                         // near clip in projW units below every valid hit
 };
 
 // Per-column and per-row terms of initRayDesc, evaluated once per frame size with exactly the
@@ -480,10 +492,24 @@ __global__ void __launch_bounds__(kBlock) sd_setup_kernel(SDArgs a, float4* __re
     uint32_t base = 0;
     if (lane == 0 && n) base = atomicAdd(&qctl[part], n);
     base = __shfl(base, 0);
+    const uint32_t slot = part * a.partCap + base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
     if (live) {
-        const uint32_t slot = part * a.partCap + base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
         queue[2u * slot] = make_float4(d.x, d.y, d.z, TMin);
         queue[2u * slot + 1u] = make_float4(TMax, cosT, __uint_as_float((uint32_t)y * (uint32_t)a.sdW + x), 0.0f);
+    }
+    if (a.raster) {
+        // the raster walk's inputs: slot map, the tile's view-depth range, empty key lists
+        if (inside) a.slotMap[(size_t)y * a.sdW + x] = live ? (int32_t)slot : -1;
+        float zlo = live ? TMin * cosT : INFINITY, zhi = live ? TMax * cosT : -INFINITY;
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) {
+            zlo = fminf(zlo, __shfl_xor(zlo, o));
+            zhi = fmaxf(zhi, __shfl_xor(zhi, o));
+        }
+        if (lane == 0) a.tileRec[(size_t)tileRow * a.tilesW + blockIdx.x] = make_float2(zlo, zhi);
+        if (live)
+            for (uint32_t k = 0; k < a.keysK; ++k) a.keys64[(size_t)slot * a.keysK + k] = ~0ull;
+        if (a.counters && lane == 0) atomicAdd(&a.counters[1], (unsigned long long)n);
     }
     const unsigned long long in = __ballot(inside);
     if (a.counters && lane == 0) atomicAdd(&a.counters[0], (unsigned long long)__popcll(in));
@@ -707,6 +733,143 @@ __global__ void __launch_bounds__(kBlock) sd_trace_ordered_kernel(SDArgs a, cons
 }
 
 // ------------------------------------------------------------------------------------
+// Raster walk (RSD_WALK_RASTER).  Every SD ray starts at the camera position, so the canonical
+// any-hit set of a texel -- the triangles its ray hits with TMin <= t <= TMax, culling applied --
+// can be found from the triangles' side: project each triangle onto the SD texel grid (texel x's
+// ray passes through image-plane x coordinate (sx + jitter) / dimx, jitter in (0, 1)), and run the
+// exact watertight test (intersect_tri, the traversal's own) for the live texels under its
+// footprint.  Hits go into the texel's K-list of 64-bit keys (t bits << 32 | prim: t > 0, so the
+// integer order is the (t, prim) order) by the atomicMin insertion chain: the list ends with the K
+// smallest keys whatever the insertion order, i.e. exactly the K nearest keys the BVH walks find,
+// so sd_resolve_row_kernel<..., RASTER> gives the same bits.  The work is throughput-bound (one
+// thread per triangle record, no dependent traversal chain): tiles whose live rays' view-depth
+// range misses the triangle's are skipped, footprints over kRasterSmall texels are walked by the
+// whole wave.
+// ------------------------------------------------------------------------------------
+constexpr int kRasterBlock = 256;
+constexpr int kRasterSmall = 16;
+
+__device__ __forceinline__ float dot3(const float* a, f3 v) { return a[0] * v.x + a[1] * v.y + a[2] * v.z; }
+
+// footprint of the triangle on the SD texel grid (clipped at the near plane wClip) and its view-
+// depth range; false if it covers no texel of the map
+__device__ __forceinline__ bool raster_footprint(const SDArgs& a, float4 v0, float4 v1, float4 v2, int& bx0, int& bx1,
+                                                 int& by0, int& by1, float& zlo, float& zhi) {
+    const rsd_camera& c = a.cam;
+    const f3 o = mk(c.posW[0], c.posW[1], c.posW[2]);
+    const f3 p[3] = {mk(v0.x - o.x, v0.y - o.y, v0.z - o.z), mk(v1.x - o.x, v1.y - o.y, v1.z - o.z),
+                     mk(v2.x - o.x, v2.y - o.y, v2.z - o.z)};
+    float pa[3], pb[3], pw[3];
+    zlo = INFINITY;
+    zhi = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        pa[i] = dot3(a.projU, p[i]);
+        pb[i] = dot3(a.projV, p[i]);
+        pw[i] = dot3(a.projW, p[i]);
+        const float z = dot3(a.camWn, p[i]);
+        zlo = fminf(zlo, z);
+        zhi = fmaxf(zhi, z);
+    }
+    // conservative depth range (float error of the dot products)
+    const float zm = 1e-4f * fmaxf(fabsf(zlo), fabsf(zhi)) + 1e-4f;
+    zlo -= zm;
+    zhi += zm;
+    const float wc = a.wClip;
+    if (!(pw[0] >= wc || pw[1] >= wc || pw[2] >= wc)) return false;  // wholly behind the near clip
+    float xlo = INFINITY, xhi = -INFINITY, ylo = INFINITY, yhi = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const int j = i == 2 ? 0 : i + 1;
+        if (pw[i] >= wc) {
+            const float u = pa[i] / pw[i], v = pb[i] / pw[i];
+            xlo = fminf(xlo, u); xhi = fmaxf(xhi, u); ylo = fminf(ylo, v); yhi = fmaxf(yhi, v);
+        }
+        if ((pw[i] >= wc) != (pw[j] >= wc)) {  // the edge crosses the clip plane
+            const float s = (wc - pw[i]) / (pw[j] - pw[i]);
+            const float u = (pa[i] + s * (pa[j] - pa[i])) / wc, v = (pb[i] + s * (pb[j] - pb[i])) / wc;
+            xlo = fminf(xlo, u); xhi = fmaxf(xhi, u); ylo = fminf(ylo, v); yhi = fmaxf(yhi, v);
+        }
+    }
+    // NDC -> texel: sx + jitter = (ndcx + 1) / 2 * dimx, sy + jitter = (1 - ndcy) / 2 * dimy; 0.05 texel margin
+    const int dimx = a.sdW - 2 * a.guard, dimy = a.sdH - 2 * a.guard;
+    const float fx0 = (xlo + 1.0f) * 0.5f * (float)dimx - 0.05f, fx1 = (xhi + 1.0f) * 0.5f * (float)dimx + 0.05f;
+    const float fy0 = (1.0f - yhi) * 0.5f * (float)dimy - 0.05f, fy1 = (1.0f - ylo) * 0.5f * (float)dimy + 0.05f;
+    const float lim = 1e8f;  // near-clipped vertices project far away: clamp before converting
+    bx0 = max((int)floorf(fmaxf(fx0, -lim)) + a.guard, 0);
+    bx1 = min((int)floorf(fminf(fx1, lim)) + a.guard, a.sdW - 1);
+    by0 = max((int)floorf(fmaxf(fy0, -lim)) + a.guard, 0);
+    by1 = min((int)floorf(fminf(fy1, lim)) + a.guard, a.sdH - 1);
+    return bx0 <= bx1 && by0 <= by1;
+}
+
+// one (triangle, texel) pair: tile depth range, slot, exact test, K-list insertion
+template <int K>
+__device__ __forceinline__ uint32_t raster_texel(const SDArgs& a, int x, int y, float4 v0, float4 v1, float4 v2,
+                                                 float zlo, float zhi, const float4* __restrict__ queue) {
+    const int ty = y >> 3;
+    if (ty < a.bandStart || (ty - a.bandStart) % a.bandStep != 0 || (ty - a.bandStart) / a.bandStep >= a.bandN)
+        return 0u;  // not this band's texel (its tile record may be stale)
+    const float2 tr = a.tileRec[(size_t)ty * a.tilesW + (x >> 3)];
+    if (!(zhi >= tr.x && zlo <= tr.y)) return 0u;  // no live ray of the tile can reach the triangle
+    const int32_t slot = a.slotMap[(size_t)y * a.sdW + x];
+    if (slot < 0) return 0u;
+    const float4 r0 = queue[2u * (uint32_t)slot], r1 = queue[2u * (uint32_t)slot + 1u];
+    RayCtx r;
+    ray_setup(r, mk(a.cam.posW[0], a.cam.posW[1], a.cam.posW[2]), mk(r0.x, r0.y, r0.z));
+    float t, bu, bv, det;
+    if (!intersect_tri(r, v0, v1, v2, t, bu, bv, det) || !(t >= r0.w && t <= r1.x) ||
+        culled(det, __float_as_uint(v1.w), a.cull))
+        return 1u;
+    unsigned long long key = ((unsigned long long)__float_as_uint(t) << 32) | (unsigned long long)__float_as_uint(v0.w);
+    unsigned long long* L = a.keys64 + (size_t)slot * K;
+    if (key >= __hip_atomic_load(&L[K - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return 1u;
+#pragma unroll
+    for (int j = 0; j < K; ++j) {  // sorted insertion: each slot keeps the smaller key, the larger moves on
+        const unsigned long long old = atomicMin(&L[j], key);
+        if (old == ~0ull) break;
+        key = old > key ? old : key;
+    }
+    return 1u;
+}
+
+template <int K>
+__global__ void __launch_bounds__(kRasterBlock) sd_raster_kernel(SDArgs a, const float4* __restrict__ queue) {
+    const uint32_t i = blockIdx.x * kRasterBlock + threadIdx.x;
+    const int lane = (int)(threadIdx.x & 63u);
+    float4 v0 = make_float4(0.f, 0.f, 0.f, 0.f), v1 = v0, v2 = v0;
+    int bx0 = 0, bx1 = -1, by0 = 0, by1 = -1;
+    float zlo = 0.0f, zhi = 0.0f;
+    bool any = false;
+    if (i < a.nTris) {
+        v0 = a.tris[3u * i];
+        v1 = a.tris[3u * i + 1u];
+        v2 = a.tris[3u * i + 2u];
+        any = raster_footprint(a, v0, v1, v2, bx0, bx1, by0, by1, zlo, zhi);
+    }
+    const int area = any ? (bx1 - bx0 + 1) * (by1 - by0 + 1) : 0;
+    uint32_t tests = 0u;
+    if (any && area <= kRasterSmall)
+        for (int y = by0; y <= by1; ++y)
+            for (int x = bx0; x <= bx1; ++x) tests += raster_texel<K>(a, x, y, v0, v1, v2, zlo, zhi, queue);
+    // large footprints: the whole wave walks one triangle's texels at a time
+    for (unsigned long long bm = __ballot(area > kRasterSmall); bm; bm &= bm - 1ull) {
+        const int b = __ffsll((long long)bm) - 1;
+        const float4 w0 = make_float4(__shfl(v0.x, b), __shfl(v0.y, b), __shfl(v0.z, b), __shfl(v0.w, b));
+        const float4 w1 = make_float4(__shfl(v1.x, b), __shfl(v1.y, b), __shfl(v1.z, b), __shfl(v1.w, b));
+        const float4 w2 = make_float4(__shfl(v2.x, b), __shfl(v2.y, b), __shfl(v2.z, b), __shfl(v2.w, b));
+        const int cx0 = __shfl(bx0, b), cx1 = __shfl(bx1, b), cy0 = __shfl(by0, b), cy1 = __shfl(by1, b);
+        const float czlo = __shfl(zlo, b), czhi = __shfl(zhi, b);
+        const int w = cx1 - cx0 + 1, n = w * (cy1 - cy0 + 1);
+        for (int k = lane; k < n; k += 64) tests += raster_texel<K>(a, cx0 + k % w, cy0 + k / w, w0, w1, w2, czlo, czhi, queue);
+    }
+    if (a.counters) {
+        atomicAdd(&a.counters[3], (unsigned long long)tests);                        // exact tests
+        if (i < a.nTris) atomicAdd(&a.counters[9], 1ull);                              // records read
+    }
+}
+
+// ------------------------------------------------------------------------------------
 // Row-parallel traversal (the default SD trace).  The quad walk above is depth-first: its
 // critical path is every node and leaf the ray visits, one dependent fetch after the other
 // (the slowest live ray of a 1080p/4 frame visits ~130 items, and the launch lasts as long
@@ -832,17 +995,17 @@ __device__ __forceinline__ void sd_hit_terms(const SDArgs& a, const RayCtx& r, f
 // per queue slot); sd_resolve_row_kernel runs the algorithm.  Valid when one chunk of K keys
 // always decides the texel: Default / KBuffer with MaxCount <= K.  Otherwise the algorithm
 // runs here and the walk continues after the K-th key while it has not committed.
-template <int K, int N, int ROW, bool SPLIT, bool CNT>
+template <int K, int N, int ROW, bool SPLIT, bool CNT, int POOL = kPoolCap>
 __global__ void __launch_bounds__(kBlock) sd_trace_row_kernel(SDArgs a, const float4* __restrict__ queue,
                                                               uint32_t* __restrict__ qctl, uint2* __restrict__ keys) {
     static_assert(K <= ROW, "one key per lane");
     constexpr int kRow = ROW, kRowRays = kBlock / ROW;
-    __shared__ uint32_t sItem[kRowRays * kPoolCap];
-    __shared__ float sT[kRowRays * kPoolCap];
+    __shared__ uint32_t sItem[kRowRays * POOL];
+    __shared__ float sT[kRowRays * POOL];
     const int lane = threadIdx.x;
     const int l = lane & (kRow - 1), base = lane & ~(kRow - 1), row = lane / kRow;
-    uint32_t* pItem = sItem + row * kPoolCap;
-    float* pT = sT + row * kPoolCap;
+    uint32_t* pItem = sItem + row * POOL;
+    float* pT = sT + row * POOL;
     const uint32_t part = blockIdx.x % kQueueParts, wavesPerPart = gridDim.x / kQueueParts;
     const uint32_t count = __hip_atomic_load(&qctl[part], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const uint32_t slot0 = part * a.partCap;
@@ -1003,10 +1166,10 @@ __global__ void __launch_bounds__(kBlock) sd_trace_row_kernel(SDArgs a, const fl
         for (int j = 0; j < 4; ++j) keep += (j < nc && ck[j] <= thi) ? 1 : 0;  // ck ascending: a prefix
         int total;
         const int pre = row_prefix<ROW>(keep, l, base, total);
-        if (pool + total > kPoolCap) {  // unreachable by the pool bound; never write out of range
+        if (pool + total > POOL) {  // unreachable by the pool bound; never write out of range
             if (a.counters && l == 0) atomicAdd(&a.counters[10], 1ull);  // always checked
-            keep = max(0, min(keep, kPoolCap - pool - pre));
-            total = kPoolCap - pool;
+            keep = max(0, min(keep, POOL - pool - pre));
+            total = POOL - pool;
         }
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -1113,7 +1276,7 @@ __global__ void __launch_bounds__(kBlock) sd_trace_row_kernel(SDArgs a, const fl
 // Phase 3 of the split trace: anyHit -> algorithm over the K nearest keys of every live ray
 // (one row of ROW lanes per ray, lane j prepares key j), then the SD texel store
 // (StochasticDepthMapRT.rt.slang:90-104).  Persistent rows stride over the queue partitions.
-template <int K, int N, int ROW>
+template <int K, int N, int ROW, bool RASTER = false>
 __global__ void __launch_bounds__(kBlock) sd_resolve_row_kernel(SDArgs a, const float4* __restrict__ queue,
                                                                 uint32_t* __restrict__ qctl,
                                                                 const uint2* __restrict__ keys) {
@@ -1143,9 +1306,15 @@ __global__ void __launch_bounds__(kBlock) sd_resolve_row_kernel(SDArgs a, const 
             float rng = 0.0f, z = 0.0f;
             bool valid = false, af = false;
             if (l < K) {
-                const uint2 k = keys[(size_t)slot * K + l];
-                valid = k.y != kNoItem;
-                if (valid) sd_hit_terms(a, r, cosT, k.y, rng, z, af);
+                if constexpr (RASTER) {  // 64-bit (t, prim) keys of the raster walk
+                    const unsigned long long k = a.keys64[(size_t)slot * K + l];
+                    valid = k != ~0ull;
+                    if (valid) sd_hit_terms(a, r, cosT, a.primRec[(uint32_t)k], rng, z, af);
+                } else {
+                    const uint2 k = keys[(size_t)slot * K + l];
+                    valid = k.y != kNoItem;
+                    if (valid) sd_hit_terms(a, r, cosT, k.y, rng, z, af);
+                }
             }
             const int found = __popc(row_bits<ROW>(valid, base));  // keys are sorted: a prefix
             float depths[N];
@@ -1231,10 +1400,11 @@ __global__ void __launch_bounds__(kBlock) gbuffer_kernel(GBArgs a) {
 // launchers
 // ------------------------------------------------------------------------------------
 // walk: 0 = quad (depth-first), 1 = row walk + in-kernel algorithm, 2 = split (row walk ->
-// keys -> resolve kernel), 3 = traversal-order any-hit stream (rsd_hit_order)
+// keys -> resolve kernel), 3 = traversal-order any-hit stream (rsd_hit_order), 4 = raster (triangles
+// -> 64-bit key lists -> resolve kernel)
 template <int K, int N>
 static hipError_t launch_sd_kn(const SDArgs& a, dim3 grid, uint32_t persistentBlocks, float4* queue, uint32_t* qctl,
-                               uint2* keys, int walk, hipStream_t s) {
+                               uint2* keys, int walk, int pool, hipStream_t s) {
     constexpr int ROW = K <= 8 ? 8 : 16;
     uint32_t* qctlNext = a.qctlNext;
     hipLaunchKernelGGL((sd_setup_kernel<N>), grid, dim3(kBlock), 0, s, a, queue, qctl, qctlNext);
@@ -1248,6 +1418,7 @@ static hipError_t launch_sd_kn(const SDArgs& a, dim3 grid, uint32_t persistentBl
         hipLaunchKernelGGL((sd_resolve_row_kernel<K, N, 16>), pg, wb, 0, s, a, queue, qctl, keys);
     } else if (walk == 2) {
         if (a.counters) hipLaunchKernelGGL((sd_trace_row_kernel<K, N, ROW, true, true>), pg, wb, 0, s, a, queue, qctl, keys);
+        else if (pool == 128) hipLaunchKernelGGL((sd_trace_row_kernel<K, N, ROW, true, false, 128>), pg, wb, 0, s, a, queue, qctl, keys);
         else hipLaunchKernelGGL((sd_trace_row_kernel<K, N, ROW, true, false>), pg, wb, 0, s, a, queue, qctl, keys);
         if ((e = hipGetLastError()) != hipSuccess) return e;
         // resolve rows: RSD_RESOLVE_WAVES_PER_CU (experiments) scales the persistent grid
@@ -1257,6 +1428,11 @@ static hipError_t launch_sd_kn(const SDArgs& a, dim3 grid, uint32_t persistentBl
         hipLaunchKernelGGL((sd_resolve_row_kernel<K, N, ROW>), dim3(rb), wb, 0, s, a, queue, qctl, keys);
     } else if (walk == 3) {
         hipLaunchKernelGGL((sd_trace_ordered_kernel<N>), pg, wb, 0, s, a, queue, qctl);
+    } else if (walk == 4) {
+        hipLaunchKernelGGL((sd_raster_kernel<K>), dim3((a.nTris + kRasterBlock - 1) / kRasterBlock), dim3(kRasterBlock),
+                           0, s, a, queue);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        hipLaunchKernelGGL((sd_resolve_row_kernel<K, N, ROW, true>), pg, wb, 0, s, a, queue, qctl, keys);
     } else if (walk == 1) {
         if (a.counters) hipLaunchKernelGGL((sd_trace_row_kernel<K, N, ROW, false, true>), pg, wb, 0, s, a, queue, qctl, keys);
         else hipLaunchKernelGGL((sd_trace_row_kernel<K, N, ROW, false, false>), pg, wb, 0, s, a, queue, qctl, keys);
@@ -1268,13 +1444,13 @@ static hipError_t launch_sd_kn(const SDArgs& a, dim3 grid, uint32_t persistentBl
 
 template <int K>
 static hipError_t launch_sd_k(const SDArgs& a, uint32_t N, dim3 grid, uint32_t pb, float4* q, uint32_t* qc, uint2* keys,
-                              int walk, hipStream_t s) {
+                              int walk, int pool, hipStream_t s) {
     switch (N) {
-        case 1: return launch_sd_kn<K, 1>(a, grid, pb, q, qc, keys, walk, s);
-        case 2: return launch_sd_kn<K, 2>(a, grid, pb, q, qc, keys, walk, s);
-        case 4: return launch_sd_kn<K, 4>(a, grid, pb, q, qc, keys, walk, s);
-        case 8: return launch_sd_kn<K, 8>(a, grid, pb, q, qc, keys, walk, s);
-        case 16: return launch_sd_kn<K, 16>(a, grid, pb, q, qc, keys, walk, s);
+        case 1: return launch_sd_kn<K, 1>(a, grid, pb, q, qc, keys, walk, pool, s);
+        case 2: return launch_sd_kn<K, 2>(a, grid, pb, q, qc, keys, walk, pool, s);
+        case 4: return launch_sd_kn<K, 4>(a, grid, pb, q, qc, keys, walk, pool, s);
+        case 8: return launch_sd_kn<K, 8>(a, grid, pb, q, qc, keys, walk, pool, s);
+        case 16: return launch_sd_kn<K, 16>(a, grid, pb, q, qc, keys, walk, pool, s);
         default: return hipErrorInvalidValue;
     }
 }
@@ -1460,10 +1636,10 @@ rsd_status sd_trace_impl(rsd_scene* scene, const rsd_camera* cam, const rsd_sd_p
     a.consume = consume ? 1u : 0u;
     a.rayMinW = d_ray_min;
     a.rayMaxW = d_ray_max;
-    if (p->ray_interval && d_ray_min) {
-        // Lower bound of dot(normalize(W), normalize(cam_dir)) over every texel centre of the
-        // map (guard band included): if farZ / bound is far below FLT_MAX, TMax < FLT_MAX for
-        // every texel, so rayMin == asuint(FLT_MAX) means TMin >= FLT_MAX > TMax (dead).
+    // Lower bound of dot(normalize(W), normalize(cam_dir)) over every texel centre of the map
+    // (guard band included, +-1 texel): the cosine of every SD ray's direction to the view axis
+    double cosLower = 0.0;
+    {
         const int dimx = (int)sd_w - 2 * p->guard_band, dimy = (int)sd_h - 2 * p->guard_band;
         auto ndcMax = [](double lo, double hi) { return std::max(std::fabs(2.0 * lo - 1.0), std::fabs(2.0 * hi - 1.0)); };
         const double nx = ndcMax((-p->guard_band + 0.5) / dimx - cam->jitterX - 1.0 / dimx,
@@ -1475,9 +1651,13 @@ rsd_status sd_trace_impl(rsd_scene* scene, const rsd_camera* cam, const rsd_sd_p
         auto dotw = [&](const float* v) { return ((double)v[0] * cam->W[0] + (double)v[1] * cam->W[1] + (double)v[2] * cam->W[2]) / lw; };
         const double num = dotw(cam->W) - nx * std::fabs(dotw(cam->U)) - ny * std::fabs(dotw(cam->V));
         const double den = nx * len(cam->U) + ny * len(cam->V) + lw;
-        const double lb = den > 0.0 ? num / den : 0.0;
-        if (dimx > 0 && dimy > 0 && lb > 1e-3 && (double)cam->farZ / (0.5 * lb) < 1e37) a.deadFast = 1u;
+        if (dimx > 0 && dimy > 0 && den > 0.0) cosLower = num / den;
     }
+    // if farZ / bound is far below FLT_MAX, TMax < FLT_MAX for every texel, so rayMin ==
+    // asuint(FLT_MAX) means TMin >= FLT_MAX > TMax (dead)
+    if (p->ray_interval && d_ray_min && cosLower > 1e-3 && (double)cam->farZ / (0.5 * cosLower) < 1e37)
+        a.deadFast = 1u;
+    a.raster = 0u;
     a.alphaData = scene->alpha;
     a.alphaData.spread = rsd_ray_cone_spread(cam->focalLength, sd_h);  // default texture dims = SD map
     if (p->implementation == RSD_SD_COVERAGE_MASK) {
@@ -1553,7 +1733,11 @@ rsd_status sd_trace_impl(rsd_scene* scene, const rsd_camera* cam, const rsd_sd_p
     // bound (kPoolCap >= poolSoft + 48 + 3 * depth), or RSD_TRACE_WALK=quad asks for the
     // depth-first quad walk (A/B measurements)
     const int depth = (int)std::max(1u, scene->stats.wide_depth);
-    a.poolSoft = std::min(kPoolCap - 48 - 3 * depth, 160);
+    // experiments: RSD_TRACE_POOL=128 halves the row walk's LDS pool (8 KB per wave: 20 waves / CU)
+    static const char* poolEnv = std::getenv("RSD_TRACE_POOL");
+    int pool = poolEnv && std::atoi(poolEnv) == 128 && !counters ? 128 : kPoolCap;
+    if (pool - 48 - 3 * depth < 16) pool = kPoolCap;
+    a.poolSoft = std::min(pool - 48 - 3 * depth, 160);
     const char* walkEnv = std::getenv("RSD_TRACE_WALK");  // read per call: tests cover every walk
     const std::string walkName = walkEnv ? walkEnv : "";
     // The row walk wins when few rays are live (the launch is the slowest ray's chain); with
@@ -1568,7 +1752,46 @@ rsd_status sd_trace_impl(rsd_scene* scene, const rsd_camera* cam, const rsd_sd_p
                          (walkName == "fused" || walkName == "split" || (bandTexels <= 600000u && !throughput));
     // default: the split row walk (trace -> keys -> resolve) where one chunk of K keys decides
     // every texel, else the fused row walk; RSD_TRACE_WALK=fused|quad for A/B runs
-    const int walk = p->hit_order == RSD_HIT_ORDER_TRAVERSAL ? 3 : !rowWalk ? 0 : (split && walkName != "fused") ? 2 : 1;
+    // raster walk: triangles -> per-texel K nearest keys (split-eligible canonical traces; the near
+    // clip needs the cosine bound)
+    const bool rasterOk = split && p->hit_order == RSD_HIT_ORDER_CANONICAL && cosLower > 1e-3 && scene->d_prim_rec;
+    const bool raster = rasterOk && walkName == "raster";
+    const int walk = p->hit_order == RSD_HIT_ORDER_TRAVERSAL ? 3 : raster ? 4 : !rowWalk ? 0
+                     : (split && walkName != "fused") ? 2 : 1;
+    if (walk == 4) {
+        const uint32_t tilesW = (sd_w + kTile - 1) / kTile, tilesH = (sd_h + kTile - 1) / kTile;
+        const size_t slotBytes = (size_t)sd_w * sd_h * 4, tileBytes = (size_t)tilesW * tilesH * 8;
+        const size_t keys64Bytes = (size_t)a.partCap * kQueueParts * K * 8;
+        const size_t rb = slotBytes + tileBytes + keys64Bytes + 256;
+        if (ws->raster_cap < rb) {
+            RSD_HIP(hipStreamSynchronize(s));
+            (void)hipFree(ws->raster);
+            ws->raster = nullptr;
+            ws->raster_cap = 0;
+            RSD_HIP(hipMalloc(&ws->raster, rb));
+            ws->raster_cap = rb;
+        }
+        char* base = static_cast<char*>(ws->raster);
+        a.raster = 1u;
+        a.keysK = K;
+        a.nTris = scene->triangle_count;
+        a.keys64 = reinterpret_cast<unsigned long long*>(base);
+        a.slotMap = reinterpret_cast<int32_t*>(base + keys64Bytes);
+        a.tileRec = reinterpret_cast<float2*>(base + keys64Bytes + slotBytes);
+        a.primRec = scene->d_prim_rec;
+        a.tilesW = (int)tilesW;
+        auto dot3h = [](const float* u, const float* v) { return (double)u[0] * v[0] + (double)u[1] * v[1] + (double)u[2] * v[2]; };
+        const double uu = dot3h(cam->U, cam->U), vv = dot3h(cam->V, cam->V), ww = dot3h(cam->W, cam->W);
+        for (int k = 0; k < 3; ++k) {
+            a.projU[k] = (float)(cam->U[k] / uu);
+            a.projV[k] = (float)(cam->V[k] / vv);
+            a.projW[k] = (float)(cam->W[k] / ww);
+            a.camWn[k] = (float)(cam->W[k] / std::sqrt(ww));
+        }
+        // every valid hit has t >= TMin >= 0.1 nearZ (initRayDesc eps) and cos >= cosLower, i.e. a
+        // view depth >= 0.1 nearZ cosLower = w |W|: clip at half of that
+        a.wClip = (float)(0.5 * 0.1 * cam->nearZ * cosLower / std::sqrt(ww));
+    }
     // persistent waves: 8 per CU.  At 1080p/4 every row gets one of the ~22 K live rays in its
     // static first slot and the launch lasts as long as the slowest ray; 16 waves per CU (the
     // split walk holds < 128 VGPRs) measured no faster (tools/sd_time.py sweep)
@@ -1578,9 +1801,9 @@ rsd_status sd_trace_impl(rsd_scene* scene, const rsd_camera* cam, const rsd_sd_p
                         kQueueParts;
     hipError_t e = hipSuccess;
     if (grid.y == 0) {}
-    else if (K == 4) e = launch_sd_k<4>(a, N, grid, pb, queue, qctl, keys, walk, s);
-    else if (K == 8) e = launch_sd_k<8>(a, N, grid, pb, queue, qctl, keys, walk, s);
-    else e = launch_sd_k<16>(a, N, grid, pb, queue, qctl, keys, walk, s);
+    else if (K == 4) e = launch_sd_k<4>(a, N, grid, pb, queue, qctl, keys, walk, pool, s);
+    else if (K == 8) e = launch_sd_k<8>(a, N, grid, pb, queue, qctl, keys, walk, pool, s);
+    else e = launch_sd_k<16>(a, N, grid, pb, queue, qctl, keys, walk, pool, s);
     if (e != hipSuccess) {
         ws->qctl_dirty = true;
         return hip_fail(e, "sd_trace_kernel launch");
