@@ -37,6 +37,12 @@ namespace rsd {
 // ------------------------------------------------------------------------------------
 // SD map kernel
 // ------------------------------------------------------------------------------------
+// queue-control words of one trace: {count[32], head[32]} of the live-ray queue partitions, the
+// raster walk's live-tile count, spare
+constexpr int kQctlWords = 2 * (int)kQueueParts + 32;
+constexpr int kQctlLiveTiles = 2 * (int)kQueueParts;
+constexpr int kSetupWaves = 4;  // sd_setup_kernel: tiles (waves) per workgroup
+
 struct SDArgs {
     const float4* nodes;  // BVH base (wide nodes, then triangle records)
     const float4* tris;   // = nodes + triOff
@@ -74,6 +80,7 @@ struct SDArgs {
     uint32_t raster, keysK, nTris;
     int32_t* slotMap;
     float2* tileRec;
+    uint32_t* liveTiles;  // the tiles with live rays (count: qctl[kQctlLiveTiles])
     unsigned long long* keys64;
     const uint32_t* primRec;
     int tilesW;
@@ -444,12 +451,16 @@ __device__ __forceinline__ void ray_rec_load(const float4* __restrict__ q, uint3
 // uses buffer k % 2 (zero on entry) and its setup kernel zeroes buffer (k + 1) % 2, which
 // call k - 1 finished with (stream order) -- no memset launch per trace.
 template <int N>
-__global__ void __launch_bounds__(kBlock) sd_setup_kernel(SDArgs a, float4* __restrict__ queue,
-                                                          uint32_t* __restrict__ qctl, uint32_t* __restrict__ qctlNext) {
-    static_assert(kBlock >= 2 * kQueueParts, "one lane per control word");
-    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < 2 * kQueueParts) qctlNext[threadIdx.x] = 0u;
-    const int lane = threadIdx.x;
-    const int x = blockIdx.x * kTile + (lane & (kTile - 1));
+__global__ void __launch_bounds__(kSetupWaves * kBlock) sd_setup_kernel(SDArgs a, float4* __restrict__ queue,
+                                                                        uint32_t* __restrict__ qctl,
+                                                                        uint32_t* __restrict__ qctlNext) {
+    if (blockIdx.x == 0 && blockIdx.y == 0)
+        for (int w = threadIdx.x; w < kQctlWords; w += kSetupWaves * kBlock) qctlNext[w] = 0u;
+    // one wave per 8x8 tile, kSetupWaves tiles of a tile row per workgroup
+    const int lane = threadIdx.x & (kBlock - 1);
+    const int tileX = (int)blockIdx.x * kSetupWaves + (int)(threadIdx.x / kBlock);
+    const int tilesX = (a.sdW + kTile - 1) / kTile;
+    const int x = tileX * kTile + (lane & (kTile - 1));
     // consume: the grid covers every tile row of the map; other bands' rows only get their
     // intervals reset (SVAO.cpp:334-340's clear for the next frame)
     const int tileRow = a.consume ? (int)blockIdx.y : (int)blockIdx.y * a.bandStep + a.bandStart;
@@ -487,7 +498,7 @@ __global__ void __launch_bounds__(kBlock) sd_setup_kernel(SDArgs a, float4* __re
     const uint32_t n = (uint32_t)__popcll(m);
     // the queue is split in kQueueParts partitions (block b -> partition b % kQueueParts), each
     // with its own counter: one counter word serialises ~90 atomics/us.
-    const uint32_t lin = blockIdx.y * gridDim.x + blockIdx.x;
+    const uint32_t lin = blockIdx.y * (uint32_t)tilesX + (uint32_t)tileX;
     const uint32_t part = lin % kQueueParts;
     uint32_t base = 0;
     if (lane == 0 && n) base = atomicAdd(&qctl[part], n);
@@ -506,7 +517,10 @@ __global__ void __launch_bounds__(kBlock) sd_setup_kernel(SDArgs a, float4* __re
             zlo = fminf(zlo, __shfl_xor(zlo, o));
             zhi = fmaxf(zhi, __shfl_xor(zhi, o));
         }
-        if (lane == 0) a.tileRec[(size_t)tileRow * a.tilesW + blockIdx.x] = make_float2(zlo, zhi);
+        if (lane == 0 && tileX < tilesX) {
+            a.tileRec[(size_t)tileRow * a.tilesW + tileX] = make_float2(zlo, zhi);
+            if (n) a.liveTiles[atomicAdd(&qctl[kQctlLiveTiles], 1u)] = (uint32_t)tileRow * (uint32_t)a.tilesW + tileX;
+        }
         if (live)
             for (uint32_t k = 0; k < a.keysK; ++k) a.keys64[(size_t)slot * a.keysK + k] = ~0ull;
         if (a.counters && lane == 0) atomicAdd(&a.counters[1], (unsigned long long)n);
@@ -803,15 +817,19 @@ __device__ __forceinline__ bool raster_footprint(const SDArgs& a, float4 v0, flo
     return bx0 <= bx1 && by0 <= by1;
 }
 
-// one (triangle, texel) pair: tile depth range, slot, exact test, K-list insertion
+// may the live rays of 8x8 tile (tx, ty) hit a triangle of view depth [zlo, zhi]?  (false for tiles
+// of other bands: their records may be stale)
+__device__ __forceinline__ bool raster_tile(const SDArgs& a, int tx, int ty, float zlo, float zhi) {
+    if (ty < a.bandStart || (ty - a.bandStart) % a.bandStep != 0 || (ty - a.bandStart) / a.bandStep >= a.bandN)
+        return false;
+    const float2 tr = a.tileRec[(size_t)ty * a.tilesW + tx];
+    return zhi >= tr.x && zlo <= tr.y;  // a tile without live rays has the empty range [inf, -inf]
+}
+
+// one (triangle, texel) pair of a tile that passed raster_tile: slot, exact test, K-list insertion
 template <int K>
 __device__ __forceinline__ uint32_t raster_texel(const SDArgs& a, int x, int y, float4 v0, float4 v1, float4 v2,
-                                                 float zlo, float zhi, const float4* __restrict__ queue) {
-    const int ty = y >> 3;
-    if (ty < a.bandStart || (ty - a.bandStart) % a.bandStep != 0 || (ty - a.bandStart) / a.bandStep >= a.bandN)
-        return 0u;  // not this band's texel (its tile record may be stale)
-    const float2 tr = a.tileRec[(size_t)ty * a.tilesW + (x >> 3)];
-    if (!(zhi >= tr.x && zlo <= tr.y)) return 0u;  // no live ray of the tile can reach the triangle
+                                                 const float4* __restrict__ queue) {
     const int32_t slot = a.slotMap[(size_t)y * a.sdW + x];
     if (slot < 0) return 0u;
     const float4 r0 = queue[2u * (uint32_t)slot], r1 = queue[2u * (uint32_t)slot + 1u];
@@ -834,8 +852,10 @@ __device__ __forceinline__ uint32_t raster_texel(const SDArgs& a, int x, int y, 
 }
 
 template <int K>
-__global__ void __launch_bounds__(kRasterBlock) sd_raster_kernel(SDArgs a, const float4* __restrict__ queue) {
+__global__ void __launch_bounds__(kRasterBlock) sd_raster_kernel(SDArgs a, const float4* __restrict__ queue,
+                                                                 const uint32_t* __restrict__ qctl) {
     const uint32_t i = blockIdx.x * kRasterBlock + threadIdx.x;
+    const uint32_t liveCount = qctl[kQctlLiveTiles];
     const int lane = (int)(threadIdx.x & 63u);
     float4 v0 = make_float4(0.f, 0.f, 0.f, 0.f), v1 = v0, v2 = v0;
     int bx0 = 0, bx1 = -1, by0 = 0, by1 = -1;
@@ -851,8 +871,10 @@ __global__ void __launch_bounds__(kRasterBlock) sd_raster_kernel(SDArgs a, const
     uint32_t tests = 0u;
     if (any && area <= kRasterSmall)
         for (int y = by0; y <= by1; ++y)
-            for (int x = bx0; x <= bx1; ++x) tests += raster_texel<K>(a, x, y, v0, v1, v2, zlo, zhi, queue);
-    // large footprints: the whole wave walks one triangle's texels at a time
+            for (int x = bx0; x <= bx1; ++x)
+                if (raster_tile(a, x >> 3, y >> 3, zlo, zhi)) tests += raster_texel<K>(a, x, y, v0, v1, v2, queue);
+    // large footprints, one triangle at a time for the whole wave: the lanes test its 8x8 tiles,
+    // then walk the texels of each passing tile (one lane per texel)
     for (unsigned long long bm = __ballot(area > kRasterSmall); bm; bm &= bm - 1ull) {
         const int b = __ffsll((long long)bm) - 1;
         const float4 w0 = make_float4(__shfl(v0.x, b), __shfl(v0.y, b), __shfl(v0.z, b), __shfl(v0.w, b));
@@ -860,8 +882,33 @@ __global__ void __launch_bounds__(kRasterBlock) sd_raster_kernel(SDArgs a, const
         const float4 w2 = make_float4(__shfl(v2.x, b), __shfl(v2.y, b), __shfl(v2.z, b), __shfl(v2.w, b));
         const int cx0 = __shfl(bx0, b), cx1 = __shfl(bx1, b), cy0 = __shfl(by0, b), cy1 = __shfl(by1, b);
         const float czlo = __shfl(zlo, b), czhi = __shfl(zhi, b);
-        const int w = cx1 - cx0 + 1, n = w * (cy1 - cy0 + 1);
-        for (int k = lane; k < n; k += 64) tests += raster_texel<K>(a, cx0 + k % w, cy0 + k / w, w0, w1, w2, czlo, czhi, queue);
+        const int tx0 = cx0 >> 3, ty0 = cy0 >> 3, tw = (cx1 >> 3) - tx0 + 1, nt = tw * ((cy1 >> 3) - ty0 + 1);
+        // the footprint's tiles, or the list of tiles with live rays when that is shorter
+        const bool byList = nt > (int)liveCount;
+        const int nIter = byList ? (int)liveCount : nt;
+        for (int k0 = 0; k0 < nIter; k0 += 64) {
+            const int k = k0 + lane;
+            int tx = 0, ty = 0;
+            bool pass = false;
+            if (k < nIter) {
+                if (byList) {
+                    const uint32_t t = a.liveTiles[k];
+                    tx = (int)(t % (uint32_t)a.tilesW);
+                    ty = (int)(t / (uint32_t)a.tilesW);
+                    pass = tx >= tx0 && tx < tx0 + tw && ty >= ty0 && ty <= (cy1 >> 3);
+                } else {
+                    tx = tx0 + k % tw;
+                    ty = ty0 + k / tw;
+                    pass = true;
+                }
+                pass = pass && raster_tile(a, tx, ty, czlo, czhi);
+            }
+            for (unsigned long long tm = __ballot(pass); tm; tm &= tm - 1ull) {
+                const int src = __ffsll((long long)tm) - 1;
+                const int x = __shfl(tx, src) * 8 + (lane & 7), y = __shfl(ty, src) * 8 + (lane >> 3);
+                if (x >= cx0 && x <= cx1 && y >= cy0 && y <= cy1) tests += raster_texel<K>(a, x, y, w0, w1, w2, queue);
+            }
+        }
     }
     if (a.counters) {
         atomicAdd(&a.counters[3], (unsigned long long)tests);                        // exact tests
@@ -923,19 +970,18 @@ __device__ __forceinline__ uint32_t row_prev(uint32_t v, int l, int base) {
     else return (uint32_t)__shfl((int)v, base + (l > 0 ? l - 1 : 0));
 }
 
-// insert key (nt, np, nl) into the row-distributed sorted list (lane j holds key j); the
-// largest key falls off the last lane
+// insert key (nt, np) into the row-distributed sorted list (lane j holds key j); the largest key
+// falls off the last lane.  Keys are (t, prim): the resolve pass finds a key's triangle record by
+// its primitive id (rsd_scene.d_prim_rec), so the list carries no record index.
 template <int ROW>
-__device__ __forceinline__ void row_insert(float& kt, uint32_t& kp, uint32_t& kl, float nt, uint32_t np, uint32_t nlSrc,
-                                           int srcL, int l, int base) {
-    const uint32_t nl = __shfl(nlSrc, base + srcL);  // the new key's triangle record, from its lane
+__device__ __forceinline__ void row_insert(float& kt, uint32_t& kp, float nt, uint32_t np, int l, int base) {
     const int pos = __popc(row_bits<ROW>(key_less(kt, kp, nt, np), base));
     const float st = __uint_as_float(row_prev<ROW>(__float_as_uint(kt), l, base));
-    const uint32_t sp = row_prev<ROW>(kp, l, base), sl = row_prev<ROW>(kl, l, base);
+    const uint32_t sp = row_prev<ROW>(kp, l, base);
     if (l == pos) {
-        kt = nt; kp = np; kl = nl;
+        kt = nt; kp = np;
     } else if (l > pos) {
-        kt = st; kp = sp; kl = sl;
+        kt = st; kp = sp;
     }
 }
 
@@ -1029,13 +1075,14 @@ __global__ void __launch_bounds__(kBlock) sd_trace_row_kernel(SDArgs a, const fl
     int pool = 0;         // items in this ray's LDS pool
     uint32_t item = kNoItem;  // per lane: the work item of this step
     float kt = INFINITY;  // per lane: key l of the row's sorted k-list
-    uint32_t kp = kNoItem, kl = 0u;
+    uint32_t kp = kNoItem;
     // ---- statistics (counters build)
     TraceStats st{0u, 0u, 0u};
     uint32_t active = 0, hitsDelivered = 0, maxSteps = 0, raySteps = 0, maxNodes = 0, rayNodes = 0;
     unsigned long long sumCycles = 0, maxCycles = 0, c0 = 0;
 
     unsigned long long tFetch = 0, tStep = 0, tResolve = 0, nStep = 0, nLoop = 0, tS0 = 0, tS1 = 0;
+    unsigned long long tMem = 0, tComp = 0, tPool = 0, tMark = 0;  // step split (instrumented build)
     while (__ballot(phase != kExit) != 0ull) {
         if constexpr (CNT) { tS0 = __builtin_amdgcn_s_memtime(); nLoop += lane == 0; }
         const bool fetching = phase == kFetch;
@@ -1065,7 +1112,7 @@ __global__ void __launch_bounds__(kBlock) sd_trace_row_kernel(SDArgs a, const fl
                 useLB = false;
                 pool = 0;
                 item = l == 0 ? 0u : kNoItem;  // the root node
-                kt = INFINITY; kp = kNoItem; kl = 0u;
+                kt = INFINITY; kp = kNoItem;
                 phase = kTrace;
                 if constexpr (CNT) {
                     active += l == 0;
@@ -1089,15 +1136,27 @@ __global__ void __launch_bounds__(kBlock) sd_trace_row_kernel(SDArgs a, const fl
         float ck[4];
         uint32_t ci[4];
         int nc = 0;
-        // one 128-B fetch: a 4-wide node, or triangle records 0-1 (+ 2/3 of record 2) of a
-        // leaf; records 2-3 of a larger leaf are re-read below (same or next cache line)
+        // one fetch per step, all loads issued before the first use: a 4-wide node (128 B), or the
+        // leaf's triangle records (48 B each; a leaf of 3-4 triangles reads 192 B -- the BVH
+        // allocation is padded by 192 B, so the tail loads never leave it)
         const float4* p = a.nodes + (item & kOffMask);
-        float4 q[8];
+        float4 q[12];
+        const bool isLeaf = item != kNoItem && (item & kLeafBit);
+        if constexpr (CNT) tMark = __builtin_amdgcn_s_memtime();
         if (item != kNoItem) {
 #pragma unroll
             for (int j = 0; j < 8; ++j) q[j] = p[j];
+            if (isLeaf && (item >> 29 & 3u) >= 2u) {
+#pragma unroll
+                for (int j = 8; j < 12; ++j) q[j] = p[j];
+            }
         }
-        const bool isLeaf = item != kNoItem && (item & kLeafBit);
+        if constexpr (CNT) {  // the step's fetch latency (the instrumented build waits here)
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            const unsigned long long t = __builtin_amdgcn_s_memtime();
+            if (l == 0) tMem += t - tMark;
+            tMark = t;
+        }
         if (item != kNoItem && !isLeaf) {
             st.nodes++;
             rayNodes++;
@@ -1128,7 +1187,6 @@ __global__ void __launch_bounds__(kBlock) sd_trace_row_kernel(SDArgs a, const fl
         // ---- leaves: triangle j of every leaf lane, then the row merges the accepted hits
         //      into its k-list (one insert each) before triangle j + 1
         const uint32_t lc = isLeaf ? ((item >> 29) & 3u) + 1u : 0u;
-        const uint32_t firstTri = ((item & kOffMask) - a.triOff) / 3u;
         if (isLeaf) st.leaves++;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -1138,9 +1196,7 @@ __global__ void __launch_bounds__(kBlock) sd_trace_row_kernel(SDArgs a, const fl
             uint32_t prim = 0u;
             if ((uint32_t)j < lc) {
                 st.tris++;
-                const float4 v0 = j < 2 ? q[3 * j] : (j == 2 ? q[6] : p[9]);
-                const float4 v1 = j < 2 ? q[3 * j + 1] : (j == 2 ? q[7] : p[10]);
-                const float4 v2 = j < 2 ? q[3 * j + 2] : p[3 * j + 2];
+                const float4 v0 = q[3 * j], v1 = q[3 * j + 1], v2 = q[3 * j + 2];
                 float bu, bv, det;
                 if (intersect_tri(r, v0, v1, v2, t, bu, bv, det) && t >= TMin && t <= TMax) {
                     prim = __float_as_uint(v0.w);
@@ -1153,7 +1209,7 @@ __global__ void __launch_bounds__(kBlock) sd_trace_row_kernel(SDArgs a, const fl
                 const float bt = __shfl(t, srcLane);
                 const uint32_t bp = __shfl(prim, srcLane);
                 if (key_less(bt, bp, kthT, kthP)) {
-                    row_insert<ROW>(kt, kp, kl, bt, bp, firstTri + (uint32_t)j, srcLane - base, l, base);
+                    row_insert<ROW>(kt, kp, bt, bp, l, base);
                     kthT = row_bcastf<ROW, K - 1>(kt, l, base);
                     kthP = row_bcast<ROW, K - 1>(kp, l, base);
                 }
@@ -1170,6 +1226,11 @@ __global__ void __launch_bounds__(kBlock) sd_trace_row_kernel(SDArgs a, const fl
             if (a.counters && l == 0) atomicAdd(&a.counters[10], 1ull);  // always checked
             keep = max(0, min(keep, POOL - pool - pre));
             total = POOL - pool;
+        }
+        if constexpr (CNT) {
+            const unsigned long long t = __builtin_amdgcn_s_memtime();
+            if (l == 0) tComp += t - tMark;
+            tMark = t;
         }
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -1192,6 +1253,8 @@ __global__ void __launch_bounds__(kBlock) sd_trace_row_kernel(SDArgs a, const fl
         pool -= take;
         __builtin_amdgcn_wave_barrier();
         if constexpr (CNT) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            if (l == 0) tPool += __builtin_amdgcn_s_memtime() - tMark;
             raySteps++;
             const unsigned long long t2 = __builtin_amdgcn_s_memtime();
             if (l == 0) { tStep += t2 - tS1; nStep++; }
@@ -1202,7 +1265,7 @@ __global__ void __launch_bounds__(kBlock) sd_trace_row_kernel(SDArgs a, const fl
         // ---- traversal done
         if constexpr (SPLIT) {
             // the K nearest keys of the ray -> sd_resolve_row_kernel
-            if (l < K) keys[(size_t)slot * K + l] = make_uint2(__float_as_uint(kt), kp == kNoItem ? kNoItem : kl);
+            if (l < K) keys[(size_t)slot * K + l] = make_uint2(__float_as_uint(kt), kp);
             phase = kFetch;
             if constexpr (CNT) {
                 uint32_t n = rayNodes;
@@ -1224,7 +1287,7 @@ __global__ void __launch_bounds__(kBlock) sd_trace_row_kernel(SDArgs a, const fl
         const int found = min(K, __popc(row_bits<ROW>(kp != kNoItem, base)));
         float rng = 0.0f, z = 0.0f;
         bool af = false;
-        if (l < found) sd_hit_terms(a, r, cosT, kl, rng, z, af);
+        if (l < found) sd_hit_terms(a, r, cosT, a.primRec[kp], rng, z, af);
         uint32_t delivered = 0;
         const bool commit = sd_algorithm_row<K, N>(a, rng, z, af, found, base, depths, cnt, delivered);
         if (l == 0) hitsDelivered += delivered;
@@ -1236,7 +1299,7 @@ __global__ void __launch_bounds__(kBlock) sd_trace_row_kernel(SDArgs a, const fl
             lbP = __shfl(kp, base + K - 1);
             pool = 0;
             item = l == 0 ? 0u : kNoItem;
-            kt = INFINITY; kp = kNoItem; kl = 0u;
+            kt = INFINITY; kp = kNoItem;
             continue;
         }
         if (l == 0) sd_store<N>(a, x, y, depths);
@@ -1270,6 +1333,9 @@ __global__ void __launch_bounds__(kBlock) sd_trace_row_kernel(SDArgs a, const fl
         atomicAdd(&a.counters[13], tResolve);
         atomicAdd(&a.counters[14], nStep);
         atomicAdd(&a.counters[15], nLoop);
+        atomicAdd(&a.counters[16], tMem);
+        atomicAdd(&a.counters[17], tComp);
+        atomicAdd(&a.counters[18], tPool);
     }
 }
 
@@ -1310,10 +1376,10 @@ __global__ void __launch_bounds__(kBlock) sd_resolve_row_kernel(SDArgs a, const 
                     const unsigned long long k = a.keys64[(size_t)slot * K + l];
                     valid = k != ~0ull;
                     if (valid) sd_hit_terms(a, r, cosT, a.primRec[(uint32_t)k], rng, z, af);
-                } else {
+                } else {  // (t bits, prim) keys of the row walk
                     const uint2 k = keys[(size_t)slot * K + l];
                     valid = k.y != kNoItem;
-                    if (valid) sd_hit_terms(a, r, cosT, k.y, rng, z, af);
+                    if (valid) sd_hit_terms(a, r, cosT, a.primRec[k.y], rng, z, af);
                 }
             }
             const int found = __popc(row_bits<ROW>(valid, base));  // keys are sorted: a prefix
@@ -1407,7 +1473,8 @@ static hipError_t launch_sd_kn(const SDArgs& a, dim3 grid, uint32_t persistentBl
                                uint2* keys, int walk, int pool, hipStream_t s) {
     constexpr int ROW = K <= 8 ? 8 : 16;
     uint32_t* qctlNext = a.qctlNext;
-    hipLaunchKernelGGL((sd_setup_kernel<N>), grid, dim3(kBlock), 0, s, a, queue, qctl, qctlNext);
+    const dim3 sgrid((grid.x + kSetupWaves - 1) / kSetupWaves, grid.y);
+    hipLaunchKernelGGL((sd_setup_kernel<N>), sgrid, dim3(kSetupWaves * kBlock), 0, s, a, queue, qctl, qctlNext);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const dim3 pg(persistentBlocks), wb(kBlock);
@@ -1430,7 +1497,7 @@ static hipError_t launch_sd_kn(const SDArgs& a, dim3 grid, uint32_t persistentBl
         hipLaunchKernelGGL((sd_trace_ordered_kernel<N>), pg, wb, 0, s, a, queue, qctl);
     } else if (walk == 4) {
         hipLaunchKernelGGL((sd_raster_kernel<K>), dim3((a.nTris + kRasterBlock - 1) / kRasterBlock), dim3(kRasterBlock),
-                           0, s, a, queue);
+                           0, s, a, queue, qctl);
         if ((e = hipGetLastError()) != hipSuccess) return e;
         hipLaunchKernelGGL((sd_resolve_row_kernel<K, N, ROW, true>), pg, wb, 0, s, a, queue, qctl, keys);
     } else if (walk == 1) {
@@ -1483,8 +1550,8 @@ rsd_status sd_workspace(rsd_scene* scene, hipStream_t s, SdWorkspace** out) {
     }
     SdWorkspace* w = new SdWorkspace();
     w->stream = s;
-    hipError_t e = hipMalloc(&w->qctl, 4 * kQueueParts * sizeof(uint32_t));
-    if (e == hipSuccess) e = hipMalloc(&w->counters, 16 * sizeof(unsigned long long));
+    hipError_t e = hipMalloc(&w->qctl, 2 * kQctlWords * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMalloc(&w->counters, 24 * sizeof(unsigned long long));
     if (e != hipSuccess) {
         (void)hipFree(w->qctl);
         delete w;
@@ -1658,6 +1725,7 @@ rsd_status sd_trace_impl(rsd_scene* scene, const rsd_camera* cam, const rsd_sd_p
     if (p->ray_interval && d_ray_min && cosLower > 1e-3 && (double)cam->farZ / (0.5 * cosLower) < 1e37)
         a.deadFast = 1u;
     a.raster = 0u;
+    a.primRec = scene->d_prim_rec;
     a.alphaData = scene->alpha;
     a.alphaData.spread = rsd_ray_cone_spread(cam->focalLength, sd_h);  // default texture dims = SD map
     if (p->implementation == RSD_SD_COVERAGE_MASK) {
@@ -1696,15 +1764,18 @@ rsd_status sd_trace_impl(rsd_scene* scene, const rsd_camera* cam, const rsd_sd_p
     }
     if (counters) {
         // per (scene, stream): concurrent instrumented traces on other streams keep their own
-        RSD_HIP(hipMemsetAsync(ws->counters, 0, 16 * sizeof(unsigned long long), s));
+        RSD_HIP(hipMemsetAsync(ws->counters, 0, 24 * sizeof(unsigned long long), s));
         a.counters = ws->counters;
     }
     const uint32_t tiles = (sd_h + kTile - 1) / kTile;
     dim3 grid((sd_w + kTile - 1) / kTile, consume ? tiles : n);
     // k = the MAX_COUNT nearest keys decide Default and KBuffer; coverage mask streams chunks
     const uint32_t need = p->implementation == RSD_SD_COVERAGE_MASK ? 8u : p->max_count;
+    const uint32_t setupBlocks = grid.x * grid.y;
+    a.partCap = (setupBlocks + kQueueParts - 1) / kQueueParts * (uint32_t)kBlock;
     // live-ray queue workspace (grow-only; the first call of a larger map allocates)
-    const size_t need_q = ((size_t)(sd_w + kTile - 1) / kTile * ((sd_h + kTile - 1) / kTile) + kQueueParts) * kBlock;
+    const size_t need_q = std::max(((size_t)(sd_w + kTile - 1) / kTile * ((sd_h + kTile - 1) / kTile) + kQueueParts) * kBlock,
+                                   (size_t)a.partCap * kQueueParts);
     const uint32_t K = need <= 4 ? 4u : (need <= 8 ? 8u : 16u);
     // split walk (trace -> keys -> resolve) when one chunk of K keys decides every texel
     const bool split = p->implementation != RSD_SD_COVERAGE_MASK && p->max_count <= K;
@@ -1722,13 +1793,11 @@ rsd_status sd_trace_impl(rsd_scene* scene, const rsd_camera* cam, const rsd_sd_p
     // double-buffered queue control (sd_setup_kernel); both buffers are reset on first use and
     // after a failed launch sequence
     if (ws->qctl_dirty) {
-        RSD_HIP(hipMemsetAsync(ws->qctl, 0, 4 * kQueueParts * sizeof(uint32_t), s));
+        RSD_HIP(hipMemsetAsync(ws->qctl, 0, 2 * kQctlWords * sizeof(uint32_t), s));
         ws->qctl_dirty = false;
     }
-    uint32_t* qctl = ws->qctl + (ws->qctl_gen & 1u) * 2 * kQueueParts;
-    a.qctlNext = ws->qctl + ((ws->qctl_gen + 1u) & 1u) * 2 * kQueueParts;
-    const uint32_t setupBlocks = grid.x * grid.y;
-    a.partCap = (setupBlocks + kQueueParts - 1) / kQueueParts * (uint32_t)kBlock;
+    uint32_t* qctl = ws->qctl + (ws->qctl_gen & 1u) * kQctlWords;
+    a.qctlNext = ws->qctl + ((ws->qctl_gen + 1u) & 1u) * kQctlWords;
     // traversal walk: row-parallel (default) unless the tree is too deep for its LDS pool
     // bound (kPoolCap >= poolSoft + 48 + 3 * depth), or RSD_TRACE_WALK=quad asks for the
     // depth-first quad walk (A/B measurements)
@@ -1762,7 +1831,8 @@ rsd_status sd_trace_impl(rsd_scene* scene, const rsd_camera* cam, const rsd_sd_p
         const uint32_t tilesW = (sd_w + kTile - 1) / kTile, tilesH = (sd_h + kTile - 1) / kTile;
         const size_t slotBytes = (size_t)sd_w * sd_h * 4, tileBytes = (size_t)tilesW * tilesH * 8;
         const size_t keys64Bytes = (size_t)a.partCap * kQueueParts * K * 8;
-        const size_t rb = slotBytes + tileBytes + keys64Bytes + 256;
+        const size_t liveBytes = (size_t)tilesW * tilesH * 4;
+        const size_t rb = slotBytes + tileBytes + liveBytes + keys64Bytes + 256;
         if (ws->raster_cap < rb) {
             RSD_HIP(hipStreamSynchronize(s));
             (void)hipFree(ws->raster);
@@ -1778,6 +1848,7 @@ rsd_status sd_trace_impl(rsd_scene* scene, const rsd_camera* cam, const rsd_sd_p
         a.keys64 = reinterpret_cast<unsigned long long*>(base);
         a.slotMap = reinterpret_cast<int32_t*>(base + keys64Bytes);
         a.tileRec = reinterpret_cast<float2*>(base + keys64Bytes + slotBytes);
+        a.liveTiles = reinterpret_cast<uint32_t*>(base + keys64Bytes + slotBytes + tileBytes);
         a.primRec = scene->d_prim_rec;
         a.tilesW = (int)tilesW;
         auto dot3h = [](const float* u, const float* v) { return (double)u[0] * v[0] + (double)u[1] * v[1] + (double)u[2] * v[2]; };
@@ -1810,7 +1881,7 @@ rsd_status sd_trace_impl(rsd_scene* scene, const rsd_camera* cam, const rsd_sd_p
     }
     if (grid.y != 0) ws->qctl_gen++;
     if (counters) {
-        unsigned long long h[16];
+        unsigned long long h[24];
         RSD_HIP(hipMemcpyAsync(h, ws->counters, sizeof(h), hipMemcpyDeviceToHost, s));
         RSD_HIP(hipStreamSynchronize(s));
         counters->rays_dispatched = h[0];
@@ -1825,8 +1896,9 @@ rsd_status sd_trace_impl(rsd_scene* scene, const rsd_camera* cam, const rsd_sd_p
         counters->leaves_visited = h[9];
         counters->walk = (uint64_t)walk;
         if (const char* dbg = std::getenv("RSD_TRACE_PHASES"))
-            if (*dbg) std::fprintf(stderr, "[rsd] row walk phase clocks: fetch %llu step %llu resolve %llu steps %llu loops %llu\n",
-                                   h[11], h[12], h[13], h[14], h[15]);
+            if (*dbg) std::fprintf(stderr, "[rsd] row walk phase clocks: fetch %llu step %llu resolve %llu steps %llu loops %llu"
+                                   " | step split: mem %llu compute %llu pool %llu\n",
+                                   h[11], h[12], h[13], h[14], h[15], h[16], h[17], h[18]);
         if (h[10]) {  // the pool bound was violated: results of this trace are not reliable
             set_error("rsd_sd_trace: traversal pool overflow (BVH deeper than the row walk supports)");
             return RSD_ERR_HIP;
