@@ -80,6 +80,21 @@ rsd_status rsd_cross_bilateral_blur(const uint8_t* d_src, const float* d_linear_
                                     uint8_t* d_pingpong, uint8_t* d_dst, uint32_t width, uint32_t height,
                                     uint32_t guard_band, uint32_t kernel_radius, uint32_t better_slope,
                                     rsd_stream stream);
+/* TemporalAO enabled (TemporalAO.cpp:113-163, TemporalAO.ps.slang:55-101): reproject the previous
+ * frame's AO along the motion vectors (RG32F, uv units), reject on > 10 % relative depth change or
+ * a non-zero stable-mask pixel (d_stable_mask may be NULL: none), accumulate up to 30 frames.
+ * prev_view_to_cur_view = viewMat * inverse(prevViewMat), row-major (TemporalAO.cpp:156).
+ * Writes AO (R8Unorm) and the history count (R8Uint) inside the guard-band scissor; the caller
+ * keeps the previous frame's linear depth, AO output and history (the pass's blits, :165-168). */
+rsd_status rsd_temporal_ao(const uint8_t* d_ao_in, const float* d_linear_z, const float* d_mvec,
+                           const float* d_prev_linear_z, const uint8_t* d_prev_ao, const uint8_t* d_prev_history,
+                           const uint8_t* d_stable_mask, uint32_t width, uint32_t height, uint32_t guard_band,
+                           const rsd_camera* cam, const float prev_view_to_cur_view[16], uint8_t* d_ao_out,
+                           uint8_t* d_history_out, rsd_stream stream);
+/* GBufferRaster.mvec for a static scene and a moving camera (librsd definition): the pixel-centre
+ * primary hit (from the linear depth) projected with the previous camera, prevUV - uv (RG32F). */
+rsd_status rsd_motion_vectors(const rsd_camera* cam, const rsd_camera* prev_cam, const float* d_linear_z,
+                              uint32_t width, uint32_t height, float* d_mvec, rsd_stream stream);
 /* ImageEquation (ImageEquation.cpp:134-160, ImageEquation.ps.slang): `formula` is the HLSL
  * expression of `float4 result = (FORMULA)` over I0..I3[xy].  Compile on the host (syntax
  * errors -> RSD_ERR_INVALID_ARG, message in rsd_last_error), run on a stream: inputs[4]

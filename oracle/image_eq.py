@@ -71,7 +71,16 @@ _F2 = {"min": np.fmin, "max": np.fmax, "pow": _pow,
 
 
 def evaluate(formula, inputs, W, H):
-    """inputs: list of 4 (image or None, fmt).  Returns the float4 result [H, W, 4]."""
+    """inputs: list of 4 (image or None, fmt).  Returns the float4 result [H, W, 4].
+
+    Arithmetic is IEEE binary32 with the special values HLSL / D3D11 define for it: x / +-0 =
+    +-inf (sign of x times sign of 0), 0 / 0 = inf / inf = inf - inf = 0 * inf = NaN -- numpy's
+    float32 results, with its floating-point warnings silenced (they are not errors here)."""
+    with np.errstate(divide="ignore", invalid="ignore", over="ignore", under="ignore"):
+        return _evaluate(formula, inputs, W, H)
+
+
+def _evaluate(formula, inputs, W, H):
     toks = re.findall(r"\d+\.\d*(?:[eE][-+]?\d+)?[fFhH]?|\.\d+(?:[eE][-+]?\d+)?[fFhH]?|\d+(?:[eE][-+]?\d+)?[fFhH]?"
                       r"|[A-Za-z_]\w*|[-+*/().,\[\]]", formula)
     pos = [0]

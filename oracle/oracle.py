@@ -93,6 +93,8 @@ def lib():
         L.ocpu_alpha_threshold.restype = f32
         L.ocpu_alpha_threshold.argtypes = [vp, u32]
         L.ocpu_cross_bilateral_blur.argtypes = [vp, vp, u32, u32, vp, vp, u32, u32, u32, u32, u32]
+        L.ocpu_temporal_ao.argtypes = [vp, vp, vp, vp, vp, vp, vp, u32, u32, u32, vp, vp, vp, vp]
+        L.ocpu_motion_vectors.argtypes = [vp, vp, vp, u32, u32, vp]
         L.ocpu_ray_cone_spread.restype = f32
         L.ocpu_ray_cone_spread.argtypes = [f32, u32]
         L.ocpu_hash.restype = f32
@@ -380,6 +382,35 @@ def svao_pass2_into(cam, vao, p, depth, normals, stencil, sd, ao, band=(0, 1), t
     sdH, sdW = sd.shape[1], sd.shape[2]
     lib().ocpu_svao_pass2_band(C.byref(cam), C.byref(vao), C.byref(p), _p(depth), _p(normals), W, H, _p(stencil),
                                _p(sd), sdW, sdH, _p(ao), band[0], band[1], _threads(threads))
+
+
+def temporal_ao(ao_in, linear_z, mvec, prev_z, prev_ao, prev_history, cam, prev_view_to_cur_view, guard,
+                stable_mask=None, ao_dst=None, history_dst=None):
+    """TemporalAO (enabled) of one frame (rsd_oracle.c ocpu_temporal_ao, TemporalAO.ps.slang:55-101).
+    Pixels outside the guard band keep the destinations' values (zeros by default)."""
+    ao_in = np.ascontiguousarray(ao_in, np.uint8)
+    H, W = ao_in.shape
+    z = np.ascontiguousarray(linear_z, np.float32)
+    mv = np.ascontiguousarray(mvec, np.float32)
+    pz = np.ascontiguousarray(prev_z, np.float32)
+    pa = np.ascontiguousarray(prev_ao, np.uint8)
+    pn = np.ascontiguousarray(prev_history, np.uint8)
+    assert z.shape == (H, W) and mv.shape == (H, W, 2) and pz.shape == (H, W) and pa.shape == (H, W)
+    st = None if stable_mask is None else np.ascontiguousarray(stable_mask, np.uint8)
+    m = np.ascontiguousarray(prev_view_to_cur_view, np.float32).reshape(16)
+    ao = np.zeros_like(ao_in) if ao_dst is None else np.array(ao_dst, np.uint8, copy=True)
+    n = np.zeros_like(ao_in) if history_dst is None else np.array(history_dst, np.uint8, copy=True)
+    lib().ocpu_temporal_ao(_p(ao_in), _p(z), _p(mv), _p(pz), _p(pa), _p(pn), None if st is None else _p(st), W, H,
+                           guard, C.byref(cam), _p(m), _p(ao), _p(n))
+    return ao, n
+
+
+def motion_vectors(cam, prev_cam, linear_z):
+    """GBufferRaster.mvec (RG32F, H x W x 2) for a static scene seen from cam after prev_cam."""
+    z = np.ascontiguousarray(linear_z, np.float32)
+    out = np.zeros(z.shape + (2,), np.float32)
+    lib().ocpu_motion_vectors(C.byref(cam), C.byref(prev_cam), _p(z), z.shape[1], z.shape[0], _p(out))
+    return out
 
 
 def cross_bilateral_blur(src, linear_z, guard, radius=4, better_slope=True, dst=None):

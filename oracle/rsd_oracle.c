@@ -1823,3 +1823,96 @@ void ocpu_cross_bilateral_blur(const uint8_t* src, const float* z, uint32_t zW, 
     o_blur_pass(src, z, (int)zW, (int)zH, pingpong, (int)W, (int)H, (int)g, (int)R, (int)better, 1.0f, 0.0f);
     o_blur_pass(pingpong, z, (int)zW, (int)zH, dst, (int)W, (int)H, (int)g, (int)R, (int)better, 0.0f, 1.0f);
 }
+
+/* ------------------------------------------------------------------ TemporalAO
+ * TemporalAO.ps.slang:55-101 (TemporalAO.cpp:113-163, enabled).  gDepth / gMotionVec / gAO are
+ * sampled at the pixel centre (= the texel); the previous AO is a clamped bilinear R8Unorm
+ * fetch at texC + mvec (TemporalAO.cpp:73-77); prevDepth / prevHistory are loaded at the pixel
+ * UVToPixel(texC + mvec); writes only inside the guard-band scissor (TemporalAO.cpp:144). */
+static float o_bilinear_u8(const uint8_t* t, int W, int H, float u, float v)
+{
+    float x = u * (float)W - 0.5f, y = v * (float)H - 0.5f;
+    float fx0 = floorf(x), fy0 = floorf(y);
+    float qx = floorf((x - fx0) * 256.0f + 0.5f), qy = floorf((y - fy0) * 256.0f + 0.5f);
+    int ix = (int)fx0, iy = (int)fy0;
+    if (qx >= 256.0f) { ix += 1; qx = 0.0f; }
+    if (qy >= 256.0f) { iy += 1; qy = 0.0f; }
+    float wx = qx * (1.0f / 256.0f), wy = qy * (1.0f / 256.0f);
+    int x0 = o_addr(ix, W, 0), x1 = o_addr(ix + 1, W, 0), y0 = o_addr(iy, H, 0), y1 = o_addr(iy + 1, H, 0);
+    float t00 = o_unorm8_to_float(t[(size_t)y0 * W + x0]), t10 = o_unorm8_to_float(t[(size_t)y0 * W + x1]);
+    float t01 = o_unorm8_to_float(t[(size_t)y1 * W + x0]), t11 = o_unorm8_to_float(t[(size_t)y1 * W + x1]);
+    float r0 = t00 * (1.0f - wx) + t10 * wx, r1 = t01 * (1.0f - wx) + t11 * wx;
+    return r0 * (1.0f - wy) + r1 * wy;
+}
+
+void ocpu_temporal_ao(const uint8_t* aoIn, const float* z, const float* mvec, const float* prevZ,
+                      const uint8_t* prevAo, const uint8_t* prevN, const uint8_t* stable, uint32_t W_,
+                      uint32_t H_, uint32_t g_, const ocam* cam, const float m[16], uint8_t* aoOut,
+                      uint8_t* nOut)
+{
+    const int W = (int)W_, H = (int)H_, g = (int)g_;
+    const float uvMinX = ((float)g + 0.5f) / (float)W, uvMinY = ((float)g + 0.5f) / (float)H;
+    const float uvMaxX = ((float)W - ((float)g + 0.5f)) / (float)W;
+    const float uvMaxY = ((float)H - ((float)g + 0.5f)) / (float)H;
+    const float isx = 0.5f * (cam->frameWidth / cam->focalLength), isy = 0.5f * (cam->frameHeight / cam->focalLength);
+    for (int y = g; y < H - g; ++y)
+        for (int x = g; x < W - g; ++x) {
+            const size_t o = (size_t)y * W + x;
+            const float tu = ((float)x + 0.5f) / (float)W, tv = ((float)y + 0.5f) / (float)H;
+            const float depth = z[o];
+            float ao = o_unorm8_to_float(aoIn[o]);
+            uint32_t n = 1;
+            const float pu = tu + mvec[2 * o], pv = tv + mvec[2 * o + 1];
+            if (pu >= uvMinX && pu <= uvMaxX && pv >= uvMinY && pv <= uvMaxY) { /* isInValidArea */
+                int qx = (int)floorf(pu * (float)W), qy = (int)floorf(pv * (float)H); /* UVToPixel */
+                qx = qx < 0 ? 0 : (qx > W - 1 ? W - 1 : qx);
+                qy = qy < 0 ? 0 : (qy > H - 1 ? H - 1 : qy);
+                const size_t po = (size_t)qy * W + qx;
+                const float prevRaw = prevZ[po];
+                const float ndcx = pu * 2.0f - 1.0f, ndcy = (1.0f - pv) * 2.0f - 1.0f; /* UVToViewSpace */
+                const float vx = ndcx * prevRaw * isx, vy = ndcy * prevRaw * isy, vz = -prevRaw;
+                const float pz = m[8] * vx + m[9] * vy + m[10] * vz + m[11];
+                const float prevDepth = -pz;
+                const int isStable = stable && stable[o] != 0;
+                if (fabsf(1.0f - prevDepth / depth) < 0.1f && !isStable) { /* RelativeDepth */
+                    const float pa = o_bilinear_u8(prevAo, W, H, pu, pv);
+                    const uint32_t pn = prevN[po];
+                    ao = ((float)pn * pa + ao) / (float)(pn + 1u);
+                    n = pn + 1u < 30u ? pn + 1u : 30u;
+                }
+            }
+            aoOut[o] = o_unorm8(ao);
+            nOut[o] = (uint8_t)n;
+        }
+}
+
+/* GBufferRaster.mvec for a static scene and a moving camera (librsd's definition, rsd_graph.h):
+ * the pixel-centre primary hit from the linear depth, projected with the previous camera. */
+void ocpu_motion_vectors(const ocam* c, const ocam* prev, const float* z, uint32_t W_, uint32_t H_, float* mvec)
+{
+    const int W = (int)W_, H = (int)H_;
+    float pU[3], pV[3], pW[3], wn[3];
+    const double uu = (double)prev->U[0] * prev->U[0] + (double)prev->U[1] * prev->U[1] + (double)prev->U[2] * prev->U[2];
+    const double vv = (double)prev->V[0] * prev->V[0] + (double)prev->V[1] * prev->V[1] + (double)prev->V[2] * prev->V[2];
+    const double ww = (double)prev->W[0] * prev->W[0] + (double)prev->W[1] * prev->W[1] + (double)prev->W[2] * prev->W[2];
+    for (int k = 0; k < 3; ++k) {
+        pU[k] = (float)(prev->U[k] / uu);
+        pV[k] = (float)(prev->V[k] / vv);
+        pW[k] = (float)(prev->W[k] / ww);
+    }
+    o_normalize(c->W, wn);
+    for (int y = 0; y < H; ++y)
+        for (int x = 0; x < W; ++x) {
+            const float u = ((float)x + 0.5f) / (float)W, v = ((float)y + 0.5f) / (float)H;
+            float dn[3], d[3], rel[3];
+            for (int k = 0; k < 3; ++k) dn[k] = (2.0f * u + -1.0f) * c->U[k] + (-2.0f * v + 1.0f) * c->V[k] + c->W[k];
+            o_normalize(dn, d);
+            const float t = z[(size_t)y * W + x] / o_dot(wn, d);
+            for (int k = 0; k < 3; ++k) rel[k] = c->posW[k] + t * d[k] - prev->posW[k];
+            const float pa = o_dot(rel, pU), pb = o_dot(rel, pV), pw = o_dot(rel, pW);
+            float mx = 2.0f, my = 2.0f;
+            if (pw > 0.0f) { mx = (pa / pw + 1.0f) * 0.5f - u; my = (1.0f - pb / pw) * 0.5f - v; }
+            mvec[2 * ((size_t)y * W + x)] = mx;
+            mvec[2 * ((size_t)y * W + x) + 1] = my;
+        }
+}

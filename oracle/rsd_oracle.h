@@ -200,6 +200,11 @@ void ocpu_svao_pass2_rt_band(const oscene* sc, const ocam* cam, const ovao* d, c
 void ocpu_cross_bilateral_blur(const uint8_t* src, const float* z, uint32_t zW, uint32_t zH, uint8_t* pingpong,
                                uint8_t* dst, uint32_t W, uint32_t H, uint32_t guard, uint32_t radius,
                                uint32_t better_slope);
+void ocpu_temporal_ao(const uint8_t* aoIn, const float* z, const float* mvec, const float* prevZ,
+                      const uint8_t* prevAo, const uint8_t* prevN, const uint8_t* stable, uint32_t W,
+                      uint32_t H, uint32_t g, const ocam* cam, const float m[16], uint8_t* aoOut,
+                      uint8_t* nOut);
+void ocpu_motion_vectors(const ocam* c, const ocam* prev, const float* z, uint32_t W, uint32_t H, float* mvec);
 
 #ifdef __cplusplus
 }

@@ -2,7 +2,8 @@
 // the RenderPass interface of graph.h:
 //
 //   GuardBand             GuardBand.cpp:38-64        dict["guardBand"]
-//   GBufferRaster         GBufferRaster.cpp:86-230   depth + faceNormalW (rsd_gbuffer_raster)
+//   GBufferRaster         GBufferRaster.cpp:86-230   depth + faceNormalW (rsd_gbuffer_raster),
+//                                                    mvec when connected (rsd_motion_vectors)
 //   LinearizeDepth        LinearizeDepth.cpp:73-96   rsd_linearize_depth
 //   CompressNormals       CompressNormals.cpp:70-96  rsd_compress_normals (viewSpace, 16 bit)
 //   StochasticDepthMapRT  StochasticDepthMapRT.cpp   rsd_sd_trace            (the hot path)
@@ -12,7 +13,7 @@
 //   CrossBilateralBlur    CrossBilateralBlur.cpp     rsd_cross_bilateral_blur
 //   ImageEquation         ImageEquation.cpp          rsd_image_equation_compile / _run
 //   Switch                Switch.cpp                 copy of the selected input
-//   TemporalAO            TemporalAO.cpp             enabled = False: copy (enabled: unsupported)
+//   TemporalAO            TemporalAO.cpp             rsd_temporal_ao (enabled = False: copy)
 //
 // Every other pass type of the reference scripts (ToneMapper, TAA, ForwardLighting, ...)
 // is outside the hot path; it resolves to a stub that declares whatever fields
@@ -100,9 +101,14 @@ public:
         Reflection r;
         r.addOutput("depth", "Depth buffer (D32 non-linear, R32F here)").format = Format::R32Float;
         r.addOutput("faceNormalW", "Face normal in world space").format = Format::RGBA32Float;
+        r.addOutput("mvec", "Motion vector (uv units, RG32F)").format = Format::RG32Float;
         return r;
     }
-    void setScene(Context&, const SceneRef* s) override { scene_ = s; }
+    ~GBufferRasterPass() override { (void)hipFree(linZ_); }
+    void setScene(Context&, const SceneRef* s) override {
+        scene_ = s;
+        hasPrev_ = false;
+    }
     void execute(Context& ctx, const RenderData& rd) override {
         if (!scene_) return;  // GBufferRaster.cpp:157 no scene -> outputs stay cleared
         Texture* d = rd["depth"];
@@ -110,13 +116,39 @@ public:
         check(rsd_gbuffer_raster(scene_->scene, &scene_->camera, d->width, d->height, cull_, (float*)d->ptr,
                                  (float*)n->ptr, ctx.stream),
               "GBufferRaster");
+        // mvec (GBufferRaster.cpp:62 "Motion vector").  Static scene: the camera's motion between this frame and the previous execute (the
+        // first frame's previous camera is its own, Camera::beginFrame).
+        const rsd_camera prev = hasPrev_ ? prevCam_ : scene_->camera;
+        prevCam_ = scene_->camera;
+        hasPrev_ = true;
+        Texture* mv = rd["mvec"];
+        if (mv->format != Format::RG32Float || mv->width != d->width || mv->height != d->height)
+            throw Unsupported("GBufferRaster: mvec must be RG32Float at the depth size");
+        const size_t px = (size_t)d->width * d->height;
+        if (px > linZCap_) {
+            (void)hipFree(linZ_);
+            linZ_ = nullptr;
+            linZCap_ = 0;
+            if (hipMalloc(&linZ_, px * sizeof(float)) != hipSuccess)
+                throw std::runtime_error("GBufferRaster: mvec scratch allocation failed");
+            linZCap_ = px;
+        }
+        check(rsd_linearize_depth((const float*)d->ptr, linZ_, (uint32_t)px, scene_->camera.nearZ,
+                                  scene_->camera.farZ, ctx.stream),
+              "GBufferRaster mvec");
+        check(rsd_motion_vectors(&scene_->camera, &prev, linZ_, d->width, d->height, (float*)mv->ptr, ctx.stream),
+              "GBufferRaster mvec");
     }
-    // further channels (posW, normW, mvec, ...) feed passes outside the hot path
+    // further channels (posW, normW, ...) feed passes outside the hot path
     bool acceptsAnyField() const override { return true; }
 
 private:
     const SceneRef* scene_ = nullptr;
     uint32_t cull_;
+    rsd_camera prevCam_{};
+    bool hasPrev_ = false;
+    float* linZ_ = nullptr;
+    size_t linZCap_ = 0;
 };
 
 // ------------------------------------------------------------------------------ LinearizeDepth
@@ -537,36 +569,125 @@ private:
 };
 
 // ------------------------------------------------------------------------------ TemporalAO
-// TemporalAO.cpp:100-170: disabled -> blit aoIn to aoOut (what scripts/SVAO.py configures);
-// the enabled path (motion-vector reprojection with a history buffer) is not implemented.
+// TemporalAO.cpp:52-169: `enabled` (default True), `useStableMask`.  Disabled: blit aoIn to aoOut
+// and drop the history (:128-135, what scripts/SVAO.py configures).  Enabled: rsd_temporal_ao
+// against the previous frame's depth / AO / history (allocated on the first enabled frame,
+// reset by compile, :105-111, 137-140), then the end-of-frame copies (:165-168).
 class TemporalAOPass : public RenderPass {
 public:
     explicit TemporalAOPass(const Properties& p) {
         props_ = p;
         enabled_ = p.getBool("enabled", true);
-        if (enabled_)
-            throw Unsupported("TemporalAO: enabled = True (temporal reprojection) is outside librsd's scope");
+        useStableMask_ = p.getBool("useStableMask", false);
     }
+    ~TemporalAOPass() override { release(); }
     Reflection reflect(const CompileData&) override {
         Reflection r;
         r.addInput("aoIn", "AO").format = Format::R8Unorm;
-        r.addInput("linearZ", "linear depth").optional = true;
-        r.addInput("mvec", "motion vectors").optional = true;
+        Field& z = r.addInput("linearZ", "linear depth");
+        z.optional = !enabled_;
+        z.format = Format::R32Float;
+        Field& mv = r.addInput("mvec", "motion vectors");
+        mv.optional = !enabled_;
+        mv.format = Format::RG32Float;
         r.addInput("stableMask", "stable mask").optional = true;
         r.addOutput("aoOut", "AO").format = Format::R8Unorm;
         return r;
+    }
+    void compile(Context&, const CompileData&) override { release(); }
+    void setScene(Context&, const SceneRef* s) override {
+        scene_ = s;
+        hasPrev_ = false;
     }
     void execute(Context& ctx, const RenderData& rd) override {
         Texture* in = rd["aoIn"];
         Texture* out = rd["aoOut"];
         if (in->format != Format::R8Unorm || in->bytes() != out->bytes())
             throw std::runtime_error("TemporalAO: aoIn must be R8Unorm at the output size");
-        if (hipMemcpyAsync(out->ptr, in->ptr, out->bytes(), hipMemcpyDeviceToDevice, ctx.stream) != hipSuccess)
-            throw std::runtime_error("TemporalAO: copy failed");
+        if (!scene_) return;  // :115
+        if (!enabled_) {      // :128-135 blit, drop the history
+            release();
+            if (hipMemcpyAsync(out->ptr, in->ptr, out->bytes(), hipMemcpyDeviceToDevice, ctx.stream) != hipSuccess)
+                throw std::runtime_error("TemporalAO: copy failed");
+            return;
+        }
+        Texture* z = rd["linearZ"];
+        Texture* mv = rd["mvec"];
+        Texture* mask = useStableMask_ ? rd["stableMask"] : nullptr;
+        const uint32_t W = out->width, H = out->height;
+        if (z->format != Format::R32Float || z->width != W || z->height != H)
+            throw Unsupported("TemporalAO: linearZ must be R32Float at the output size");
+        if (mv->format != Format::RG32Float || mv->width != W || mv->height != H)
+            throw Unsupported("TemporalAO: mvec must be RG32Float at the output size");
+        if (mask && (formatBytes(mask->format) != 1 || mask->width != W || mask->height != H))
+            throw Unsupported("TemporalAO: stableMask must be an 8-bit mask at the output size");
+        if (!prevDepth_ || W != w_ || H != h_) {  // allocatePrevFrameTexture
+            release();
+            const size_t px = (size_t)W * H;
+            if (hipMalloc(&prevDepth_, px * 4) != hipSuccess || hipMalloc(&prevAo_, px) != hipSuccess ||
+                hipMalloc(&prevHist_, px) != hipSuccess || hipMalloc(&hist_, px) != hipSuccess) {
+                release();
+                throw std::runtime_error("TemporalAO: history allocation failed");
+            }
+            w_ = W;
+            h_ = H;
+            (void)hipMemsetAsync(prevDepth_, 0, px * 4, ctx.stream);
+            (void)hipMemsetAsync(prevAo_, 0, px, ctx.stream);
+            (void)hipMemsetAsync(prevHist_, 0, px, ctx.stream);
+            (void)hipMemsetAsync(hist_, 0, px, ctx.stream);
+        }
+        auto& dict = rd.getDictionary();
+        auto it = dict.find("guardBand");
+        const int64_t g = it != dict.end() && std::holds_alternative<int64_t>(it->second)
+                              ? std::get<int64_t>(it->second) : 0;
+        // :156 prevViewToCurView = viewMat * inverse(prevViewMat); the view matrix is rigid
+        const rsd_camera& cur = scene_->camera;
+        const rsd_camera prev = hasPrev_ ? prevCam_ : cur;
+        prevCam_ = cur;
+        hasPrev_ = true;
+        double inv[16] = {};
+        for (int r = 0; r < 3; ++r) {
+            for (int c = 0; c < 3; ++c) inv[r * 4 + c] = prev.viewMat[c * 4 + r];
+            inv[r * 4 + 3] = -((double)prev.viewMat[0 * 4 + r] * prev.viewMat[3] +
+                               (double)prev.viewMat[1 * 4 + r] * prev.viewMat[7] +
+                               (double)prev.viewMat[2 * 4 + r] * prev.viewMat[11]);
+        }
+        inv[15] = 1.0;
+        float m[16];
+        for (int r = 0; r < 4; ++r)
+            for (int c = 0; c < 4; ++c) {
+                double acc = 0.0;
+                for (int k = 0; k < 4; ++k) acc += (double)cur.viewMat[r * 4 + k] * inv[k * 4 + c];
+                m[r * 4 + c] = (float)acc;
+            }
+        check(rsd_temporal_ao((const uint8_t*)in->ptr, (const float*)z->ptr, (const float*)mv->ptr, prevDepth_,
+                              prevAo_, prevHist_, mask ? (const uint8_t*)mask->ptr : nullptr, W, H, (uint32_t)g,
+                              &cur, m, (uint8_t*)out->ptr, hist_, ctx.stream),
+              "TemporalAO");
+        const size_t px = (size_t)W * H;
+        if (hipMemcpyAsync(prevDepth_, z->ptr, px * 4, hipMemcpyDeviceToDevice, ctx.stream) != hipSuccess ||
+            hipMemcpyAsync(prevAo_, out->ptr, px, hipMemcpyDeviceToDevice, ctx.stream) != hipSuccess ||
+            hipMemcpyAsync(prevHist_, hist_, px, hipMemcpyDeviceToDevice, ctx.stream) != hipSuccess)
+            throw std::runtime_error("TemporalAO: history copy failed");
     }
 
 private:
-    bool enabled_;
+    void release() {
+        (void)hipFree(prevDepth_);
+        (void)hipFree(prevAo_);
+        (void)hipFree(prevHist_);
+        (void)hipFree(hist_);
+        prevDepth_ = nullptr;
+        prevAo_ = prevHist_ = hist_ = nullptr;
+        w_ = h_ = 0;
+    }
+    bool enabled_, useStableMask_;
+    const SceneRef* scene_ = nullptr;
+    rsd_camera prevCam_{};
+    bool hasPrev_ = false;
+    float* prevDepth_ = nullptr;
+    uint8_t *prevAo_ = nullptr, *prevHist_ = nullptr, *hist_ = nullptr;
+    uint32_t w_ = 0, h_ = 0;
 };
 
 template <class T>
@@ -587,7 +708,7 @@ void registerBuiltinPasses(PluginRegistry& r) {
     r.registerClass("CrossBilateralBlur", "depth-aware cross bilateral blur", factory<CrossBilateralBlurPass>());
     r.registerClass("ImageEquation", "per-pixel formula over up to 4 images", factory<ImageEquationPass>());
     r.registerClass("Switch", "forwards the selected input", factory<SwitchPass>());
-    r.registerClass("TemporalAO", "temporal AO accumulation (disabled: pass-through)", factory<TemporalAOPass>());
+    r.registerClass("TemporalAO", "temporal AO accumulation over motion vectors", factory<TemporalAOPass>());
 }
 
 }  // namespace rsd::host

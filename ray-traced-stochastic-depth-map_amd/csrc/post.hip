@@ -93,6 +93,109 @@ hipError_t launch_blur(const BlurArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------- TemporalAO
+// TemporalAO.ps.slang:55-101 (TemporalAO.cpp:113-163, enabled): reproject the previous frame's
+// AO along the motion vector, reject on a > 10 % relative depth change (or a stable-mask pixel),
+// accumulate up to 30 frames.  Samplers: gAOSampler linear / clamp (R8Unorm, librsd's 8-bit
+// sub-texel bilinear), gDepthSampler at pixel centres (exactly the texel); writes only inside
+// the guard-band scissor.
+struct TaoArgs {
+    const uint8_t* aoIn;
+    const float* z;
+    const float2* mvec;
+    const float* prevZ;
+    const uint8_t* prevAo;
+    const uint8_t* prevN;
+    const uint8_t* stable;  // may be null (unbound: every pixel unstable)
+    uint8_t* aoOut;
+    uint8_t* nOut;
+    int W, H, g;
+    float m[16];  // prevViewToCurView, row-major
+    float uvMinX, uvMinY, uvMaxX, uvMaxY;
+    float isx, isy;  // 0.5 * frameWidth / focalLength, 0.5 * frameHeight / focalLength
+};
+
+// bilinear of an R8Unorm texture (clamp), librsd's sampler definition (tex_bilinear on unorm8/255)
+__device__ __forceinline__ float unorm8_bilinear(const uint8_t* __restrict__ t, int W, int H, float u, float v) {
+    float x = u * (float)W - 0.5f, y = v * (float)H - 0.5f;
+    const float fx0 = floorf(x), fy0 = floorf(y);
+    float qx = floorf((x - fx0) * 256.0f + 0.5f), qy = floorf((y - fy0) * 256.0f + 0.5f);
+    int ix = (int)fx0, iy = (int)fy0;
+    if (qx >= 256.0f) { ix += 1; qx = 0.0f; }
+    if (qy >= 256.0f) { iy += 1; qy = 0.0f; }
+    const float wx = qx * (1.0f / 256.0f), wy = qy * (1.0f / 256.0f);
+    const int x0 = min(max(ix, 0), W - 1), x1 = min(max(ix + 1, 0), W - 1);
+    const int y0 = min(max(iy, 0), H - 1), y1 = min(max(iy + 1, 0), H - 1);
+    const float t00 = unorm8_to_float(t[(size_t)y0 * W + x0]), t10 = unorm8_to_float(t[(size_t)y0 * W + x1]);
+    const float t01 = unorm8_to_float(t[(size_t)y1 * W + x0]), t11 = unorm8_to_float(t[(size_t)y1 * W + x1]);
+    const float r0 = t00 * (1.0f - wx) + t10 * wx, r1 = t01 * (1.0f - wx) + t11 * wx;
+    return r0 * (1.0f - wy) + r1 * wy;
+}
+
+__global__ void __launch_bounds__(kPostW * kPostH) temporal_ao_kernel(TaoArgs a) {
+    const int x = a.g + (int)(blockIdx.x * kPostW + threadIdx.x);
+    const int y = a.g + (int)(blockIdx.y * kPostH + threadIdx.y);
+    if (x >= a.W - a.g || y >= a.H - a.g) return;  // guard-band scissor
+    const size_t o = (size_t)y * a.W + x;
+    const float tu = ((float)x + 0.5f) / (float)a.W, tv = ((float)y + 0.5f) / (float)a.H;  // texC
+    const float depth = a.z[o];
+    float ao = unorm8_to_float(a.aoIn[o]);
+    uint32_t n = 1u;
+    const float2 mv = a.mvec[o];
+    const float pu = tu + mv.x, pv = tv + mv.y;
+    if (pu >= a.uvMinX && pu <= a.uvMaxX && pv >= a.uvMinY && pv <= a.uvMaxY) {  // isInValidArea
+        const int qx = (int)floorf(pu * (float)a.W), qy = (int)floorf(pv * (float)a.H);  // UVToPixel
+        const size_t po = (size_t)min(max(qy, 0), a.H - 1) * a.W + min(max(qx, 0), a.W - 1);
+        const float prevRaw = a.prevZ[po];
+        // UVToViewSpace(texC + mvec, prevRawDepth), then prevViewToCurView
+        const float ndcx = pu * 2.0f - 1.0f, ndcy = (1.0f - pv) * 2.0f - 1.0f;
+        const float vx = ndcx * prevRaw * a.isx, vy = ndcy * prevRaw * a.isy, vz = -prevRaw;
+        const float pz = a.m[8] * vx + a.m[9] * vy + a.m[10] * vz + a.m[11];
+        const float prevDepth = -pz;
+        const bool stable = a.stable && a.stable[o] != 0u;
+        if (fabsf(1.0f - prevDepth / depth) < 0.1f && !stable) {  // RelativeDepth(depth, prevDepth)
+            const float prevAo = unorm8_bilinear(a.prevAo, a.W, a.H, pu, pv);
+            const uint32_t prevN = a.prevN[po];
+            ao = ((float)prevN * prevAo + ao) / (float)(prevN + 1u);
+            n = min(prevN + 1u, 30u);
+        }
+    }
+    a.aoOut[o] = unorm8(ao);
+    a.nOut[o] = (uint8_t)n;
+}
+
+// GBufferRaster's motion vectors for a static scene and a moving camera (librsd definition):
+// the pixel-centre primary hit P = posW + (z / cos) d (z: linear depth, d: the normalized pixel
+// ray, cos = dot(normalize(W), d)) projected with the previous camera: mvec = prevUV(P) - uv.
+// P behind the previous camera -> mvec = (2, 2) (off screen: TemporalAO resets the pixel).
+struct MvecArgs {
+    rsd_camera cam, prev;
+    const float* z;
+    float2* mvec;
+    int W, H;
+    float pU[3], pV[3], pW[3];  // prev U / |U|^2, V / |V|^2, W / |W|^2
+};
+
+__global__ void __launch_bounds__(kPostW * kPostH) motion_vector_kernel(MvecArgs a) {
+    const int x = (int)(blockIdx.x * kPostW + threadIdx.x), y = (int)(blockIdx.y * kPostH + threadIdx.y);
+    if (x >= a.W || y >= a.H) return;
+    const rsd_camera& c = a.cam;
+    const float u = ((float)x + 0.5f) / (float)a.W, v = ((float)y + 0.5f) / (float)a.H;
+    const f3 wn = normalize(mk(c.W[0], c.W[1], c.W[2]));
+    const f3 d = normalize(mk((2.0f * u + -1.0f) * c.U[0] + (-2.0f * v + 1.0f) * c.V[0] + c.W[0],
+                              (2.0f * u + -1.0f) * c.U[1] + (-2.0f * v + 1.0f) * c.V[1] + c.W[1],
+                              (2.0f * u + -1.0f) * c.U[2] + (-2.0f * v + 1.0f) * c.V[2] + c.W[2]));
+    const float t = a.z[(size_t)y * a.W + x] / dot(wn, d);
+    const f3 rel = mk(c.posW[0] + t * d.x - a.prev.posW[0], c.posW[1] + t * d.y - a.prev.posW[1],
+                      c.posW[2] + t * d.z - a.prev.posW[2]);
+    const float pa = rel.x * a.pU[0] + rel.y * a.pU[1] + rel.z * a.pU[2];
+    const float pb = rel.x * a.pV[0] + rel.y * a.pV[1] + rel.z * a.pV[2];
+    const float pw = rel.x * a.pW[0] + rel.y * a.pW[1] + rel.z * a.pW[2];
+    float2 mv = make_float2(2.0f, 2.0f);
+    if (pw > 0.0f) mv = make_float2((pa / pw + 1.0f) * 0.5f - u, (1.0f - pb / pw) * 0.5f - v);
+    a.mvec[(size_t)y * a.W + x] = mv;
+}
+
 // ---------------------------------------------------------------------- ImageEquation
 struct TexDesc {
     const void* ptr;
@@ -295,6 +398,72 @@ extern "C" rsd_status rsd_cross_bilateral_blur(const uint8_t* d_src, const float
         if (e != hipSuccess) return hip_fail(e, "blur_kernel launch");
     }
     return RSD_OK;
+}
+
+extern "C" rsd_status rsd_temporal_ao(const uint8_t* d_ao_in, const float* d_linear_z, const float* d_mvec,
+                                      const float* d_prev_linear_z, const uint8_t* d_prev_ao,
+                                      const uint8_t* d_prev_history, const uint8_t* d_stable_mask, uint32_t width,
+                                      uint32_t height, uint32_t guard_band, const rsd_camera* cam,
+                                      const float prev_view_to_cur_view[16], uint8_t* d_ao_out,
+                                      uint8_t* d_history_out, rsd_stream stream) {
+    if (!d_ao_in || !d_linear_z || !d_mvec || !d_prev_linear_z || !d_prev_ao || !d_prev_history || !cam ||
+        !prev_view_to_cur_view || !d_ao_out || !d_history_out || width == 0 || height == 0 ||
+        2 * guard_band >= width || 2 * guard_band >= height) {
+        set_error("rsd_temporal_ao: invalid argument");
+        return RSD_ERR_INVALID_ARG;
+    }
+    TaoArgs a{};
+    a.aoIn = d_ao_in;
+    a.z = d_linear_z;
+    a.mvec = reinterpret_cast<const float2*>(d_mvec);
+    a.prevZ = d_prev_linear_z;
+    a.prevAo = d_prev_ao;
+    a.prevN = d_prev_history;
+    a.stable = d_stable_mask;
+    a.aoOut = d_ao_out;
+    a.nOut = d_history_out;
+    a.W = (int)width;
+    a.H = (int)height;
+    a.g = (int)guard_band;
+    for (int i = 0; i < 16; ++i) a.m[i] = prev_view_to_cur_view[i];
+    // GuardBand.cpp:62-63
+    a.uvMinX = ((float)guard_band + 0.5f) / (float)width;
+    a.uvMinY = ((float)guard_band + 0.5f) / (float)height;
+    a.uvMaxX = ((float)width - ((float)guard_band + 0.5f)) / (float)width;
+    a.uvMaxY = ((float)height - ((float)guard_band + 0.5f)) / (float)height;
+    a.isx = 0.5f * (cam->frameWidth / cam->focalLength);  // TemporalAO.ps.slang:42 imageScale
+    a.isy = 0.5f * (cam->frameHeight / cam->focalLength);
+    const dim3 grid((width - 2 * guard_band + kPostW - 1) / kPostW, (height - 2 * guard_band + kPostH - 1) / kPostH);
+    hipLaunchKernelGGL(temporal_ao_kernel, grid, dim3(kPostW, kPostH), 0, (hipStream_t)stream, a);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? RSD_OK : hip_fail(e, "temporal_ao_kernel launch");
+}
+
+extern "C" rsd_status rsd_motion_vectors(const rsd_camera* cam, const rsd_camera* prev_cam, const float* d_linear_z,
+                                         uint32_t width, uint32_t height, float* d_mvec, rsd_stream stream) {
+    if (!cam || !prev_cam || !d_linear_z || !d_mvec || width == 0 || height == 0) {
+        set_error("rsd_motion_vectors: invalid argument");
+        return RSD_ERR_INVALID_ARG;
+    }
+    MvecArgs a{};
+    a.cam = *cam;
+    a.prev = *prev_cam;
+    a.z = d_linear_z;
+    a.mvec = reinterpret_cast<float2*>(d_mvec);
+    a.W = (int)width;
+    a.H = (int)height;
+    auto dot3 = [](const float* p, const float* q) { return (double)p[0] * q[0] + (double)p[1] * q[1] + (double)p[2] * q[2]; };
+    const double uu = dot3(prev_cam->U, prev_cam->U), vv = dot3(prev_cam->V, prev_cam->V),
+                 ww = dot3(prev_cam->W, prev_cam->W);
+    for (int k = 0; k < 3; ++k) {
+        a.pU[k] = (float)(prev_cam->U[k] / uu);
+        a.pV[k] = (float)(prev_cam->V[k] / vv);
+        a.pW[k] = (float)(prev_cam->W[k] / ww);
+    }
+    const dim3 grid((width + kPostW - 1) / kPostW, (height + kPostH - 1) / kPostH);
+    hipLaunchKernelGGL(motion_vector_kernel, grid, dim3(kPostW, kPostH), 0, (hipStream_t)stream, a);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? RSD_OK : hip_fail(e, "motion_vector_kernel launch");
 }
 
 extern "C" rsd_status rsd_image_equation_run(const rsd_image_program* prog, const rsd_texture* inputs,

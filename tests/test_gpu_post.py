@@ -82,3 +82,43 @@ def test_image_equation_parity(torch, out_fmt):
             nan = np.isnan(want)
             assert np.array_equal(np.isnan(got), nan), formula
             assert np.array_equal(got[~nan].view(np.uint32), want[~nan].view(np.uint32)), formula
+
+
+def test_image_equation_ieee_special_values(torch):
+    """Division by +-0, 0/0, inf/inf, inf - inf and 0 * inf: the kernel's IEEE binary32 results,
+    pinned as bit patterns (not via numpy), and their R8Unorm stores (NaN -> 0, D3D11 3.2.3.6)."""
+    from rsd import abi
+    num = np.array([1.0, -1.0, 1.0, 0.0, np.inf, np.inf, 0.0, 2.0], F)
+    den = np.array([0.0, 0.0, -0.0, 0.0, np.inf, -np.inf, np.inf, 4.0], F)
+    want_div = np.array([0x7F800000, 0xFF800000, 0xFF800000, None, None, None, 0x00000000, 0x3F000000], object)
+    want_sub = np.array([0x3F800000, 0xBF800000, 0x3F800000, 0x00000000, None, 0x7F800000, 0xFF800000,
+                         0xC0000000], object)   # num - den
+    want_mul = np.array([0x00000000, 0x80000000, 0x80000000, 0x00000000, 0x7F800000, 0xFF800000, None,
+                         0x41000000], object)   # num * den
+    W, H = 8, 1
+    a = torch.from_numpy(num.reshape(H, W)).cuda()
+    b = torch.from_numpy(den.reshape(H, W)).cuda()
+    tex = (abi.Texture * 4)()
+    tex[0] = abi.Texture(a.data_ptr(), W, H, 1, abi.FMT_R32F, a.numel() * 4)
+    tex[1] = abi.Texture(b.data_ptr(), W, H, 1, abi.FMT_R32F, b.numel() * 4)
+    for formula, want in (("I0[xy].r / I1[xy].r", want_div), ("I0[xy].r - I1[xy].r", want_sub), ("I0[xy].r * I1[xy].r", want_mul)):
+        h = C.c_void_p()
+        abi.check(abi.lib().rsd_image_equation_compile(formula.encode(), C.byref(h)), formula)
+        out = torch.zeros((H, W), dtype=torch.float32, device="cuda")
+        out8 = torch.zeros((H, W), dtype=torch.uint8, device="cuda")
+        ot = abi.Texture(out.data_ptr(), W, H, 1, abi.FMT_R32F, out.numel() * 4)
+        ot8 = abi.Texture(out8.data_ptr(), W, H, 1, abi.FMT_R8UNORM, out8.numel())
+        abi.check(abi.lib().rsd_image_equation_run(h, tex, C.byref(ot), _stream(torch)), formula)
+        abi.check(abi.lib().rsd_image_equation_run(h, tex, C.byref(ot8), _stream(torch)), formula)
+        torch.cuda.synchronize()
+        abi.lib().rsd_image_equation_release(h)
+        bits = out.cpu().numpy().reshape(-1).view(np.uint32)
+        got8 = out8.cpu().numpy().reshape(-1)
+        for k, w in enumerate(want):
+            if w is None:  # NaN (any payload)
+                assert np.isnan(bits[k:k + 1].view(F))[0], (formula, k, hex(bits[k]))
+                assert got8[k] == 0, (formula, k)  # NaN -> 0 in a UNORM store
+            else:
+                assert bits[k] == w, (formula, k, hex(bits[k]), hex(w))
+                v = np.array([w], np.uint32).view(F)[0]
+                assert got8[k] == (255 if v >= 1 else 0 if not v > 0 else int(np.floor(v * 255 + 0.5))), (formula, k)

@@ -1,0 +1,168 @@
+"""GPU parity of TemporalAO (enabled) and the motion vectors through the C ABI
+(rsd_temporal_ao, rsd_motion_vectors) against the oracle (ocpu_temporal_ao,
+ocpu_motion_vectors): synthetic inputs with every branch of TemporalAO.ps.slang:55-101, and a
+rendered camera sequence (G-buffer -> SVAO -> motion vectors -> TemporalAO) whose history must
+grow where the reprojection holds.  Bit-exact."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from helpers import small_frame_config, to_oracle
+
+pytestmark = pytest.mark.gpu
+F = np.float32
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    return torch
+
+
+def _p(t):
+    return C.c_void_p(t.data_ptr()) if t is not None else None
+
+
+@pytest.mark.parametrize("guard,use_mask", [(0, False), (16, True), (5, False)])
+def test_temporal_ao_synthetic_parity(torch, oracle, guard, use_mask):
+    from rsd import abi
+    from rsd.frame import FrameConfig, look_at
+    from rsd.temporal import prev_view_to_cur_view
+    rng = np.random.default_rng(guard)
+    H, W = 90, 150
+    cfg = FrameConfig(visible_w=W, visible_h=H, guard_band=0)
+    c0 = look_at([0.0, 2.0, 8.0], [0.0, 1.0, 0.0], [0.0, 1.0, 0.0], cfg)
+    c1 = look_at([0.2, 2.1, 7.7], [0.1, 1.0, 0.0], [0.0, 1.0, 0.0], cfg)
+    m = np.ascontiguousarray(prev_view_to_cur_view(c1, c0), F)
+    ao = rng.integers(0, 256, (H, W)).astype(np.uint8)
+    z = (2.0 + 10.0 * rng.random((H, W))).astype(F)
+    mv = (rng.normal(0.0, 0.01, (H, W, 2))).astype(F)
+    mv[rng.random((H, W)) < 0.1] = 0.7  # off screen
+    mv[rng.random((H, W)) < 0.1] = 0.0
+    # previous depth: the current depth give or take up to 20 % (both sides of the 10 % test)
+    prev_z = (z * (1.0 + rng.uniform(-0.2, 0.2, (H, W)))).astype(F)
+    prev_z[rng.random((H, W)) < 0.02] = 0.0
+    prev_ao = rng.integers(0, 256, (H, W)).astype(np.uint8)
+    prev_n = rng.integers(0, 31, (H, W)).astype(np.uint8)
+    mask = (rng.random((H, W)) < 0.2).astype(np.uint8) if use_mask else None
+    d = {k: torch.from_numpy(np.ascontiguousarray(v)).cuda() for k, v in
+         dict(ao=ao, z=z, mv=mv, pz=prev_z, pa=prev_ao, pn=prev_n).items()}
+    dm = torch.from_numpy(mask).cuda() if use_mask else None
+    out = torch.full((H, W), 7, dtype=torch.uint8, device="cuda")
+    hist = torch.full((H, W), 9, dtype=torch.uint8, device="cuda")
+    s = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    abi.check(abi.lib().rsd_temporal_ao(_p(d["ao"]), _p(d["z"]), _p(d["mv"]), _p(d["pz"]), _p(d["pa"]), _p(d["pn"]),
+                                        _p(dm), W, H, guard, C.byref(c1), m.ctypes.data_as(C.c_void_p), _p(out),
+                                        _p(hist), s), "rsd_temporal_ao")
+    torch.cuda.synchronize()
+    want, want_n = oracle.temporal_ao(ao, z, mv, prev_z, prev_ao, prev_n, to_oracle(c1, oracle.Camera), m, guard,
+                                      stable_mask=mask, ao_dst=np.full((H, W), 7, np.uint8),
+                                      history_dst=np.full((H, W), 9, np.uint8))
+    got_n = hist.cpu().numpy()
+    assert np.array_equal(out.cpu().numpy(), want)
+    assert np.array_equal(got_n, want_n)
+    inner = got_n[guard:H - guard, guard:W - guard]
+    assert (inner == 1).mean() > 0.1 and (inner > 1).mean() > 0.1  # both branches exercised
+
+
+def test_temporal_ao_rejects_bad_arguments(torch):
+    from rsd import abi
+    from rsd.frame import FrameConfig, look_at
+    cfg = FrameConfig(visible_w=64, visible_h=64, guard_band=0)
+    c = look_at([0.0, 2.0, 8.0], [0.0, 1.0, 0.0], [0.0, 1.0, 0.0], cfg)
+    m = np.eye(4, dtype=F)
+    t = torch.zeros((64, 64), dtype=torch.float32, device="cuda")
+    st = abi.lib().rsd_temporal_ao(_p(t), _p(t), _p(t), _p(t), _p(t), _p(t), None, 64, 64, 32, C.byref(c),
+                                   m.ctypes.data_as(C.c_void_p), _p(t), _p(t), None)
+    assert st == abi.ERR_INVALID_ARG  # 2 * guard >= size
+    st = abi.lib().rsd_temporal_ao(None, _p(t), _p(t), _p(t), _p(t), _p(t), None, 64, 64, 0, C.byref(c),
+                                   m.ctypes.data_as(C.c_void_p), _p(t), _p(t), None)
+    assert st == abi.ERR_INVALID_ARG
+
+
+def test_temporal_sequence_parity_and_accumulation(torch, oracle):
+    """Four poses of a slowly moving camera: each frame's motion vectors and TemporalAO output
+    equal the oracle's, and the history grows where the reprojection holds."""
+    from rsd.frame import Renderer
+    from rsd.scenes import make_scene
+    from rsd.temporal import TemporalAO, motion_vectors, prev_view_to_cur_view
+    cfg = small_frame_config(visible=(256, 144), guard=32, divisor=2, N=4)
+    scene = make_scene("arcade_tiny")
+    r = Renderer(scene, cfg)
+    pos0, tgt0, up = (np.array(scene.camera[k], np.float64) for k in ("pos", "target", "up"))
+    tao = TemporalAO(enabled=True)
+    prev_cam, o_prev = None, None
+    g = cfg.guard_band
+    for i in range(4):
+        step = np.array([0.02, 0.0, 0.01]) * i
+        r.set_pose((pos0 + step).tolist(), (tgt0 + step).tolist(), up.tolist())
+        r.gbuffer()
+        r.ao.zero_()
+        r.frame()
+        prev_cam = prev_cam or r.cam
+        mv = motion_vectors(r.cam, prev_cam, r.depth)
+        out = tao.execute(r.ao, r.depth, mv, r.cam, prev_cam, g)
+        torch.cuda.synchronize()
+        z, ao_in = r.depth.cpu().numpy(), r.ao.cpu().numpy()
+        oc, op = to_oracle(r.cam, oracle.Camera), to_oracle(prev_cam, oracle.Camera)
+        want_mv = oracle.motion_vectors(oc, op, z)
+        assert np.array_equal(mv.cpu().numpy().view(np.uint32), want_mv.view(np.uint32)), i
+        if o_prev is None:
+            H, W = z.shape
+            o_prev = (np.zeros_like(z), np.zeros_like(ao_in), np.zeros_like(ao_in))
+        m = prev_view_to_cur_view(r.cam, prev_cam)
+        want, want_n = oracle.temporal_ao(ao_in, z, want_mv, *o_prev, oc, m, g)
+        assert np.array_equal(out.cpu().numpy(), want), i
+        assert np.array_equal(tao.history.cpu().numpy(), want_n), i
+        o_prev = (z, want, want_n)
+        prev_cam = r.cam
+    inner = want_n[g:-g, g:-g]
+    assert (inner == 4).mean() > 0.8, np.bincount(inner.ravel())
+    r.close()
+
+
+def test_graph_temporal_ao_enabled(torch, oracle):
+    """scripts/SVAO.py's chain with TemporalAO enabled, run by the C++ graph host over three
+    camera poses: GBufferRaster.mvec and TemporalAO.aoOut equal the oracle's every frame."""
+    from conftest import ROOT
+    from rsd import graph as rg
+    from rsd.frame import Device, GpuScene, look_at
+    from rsd.scenes import make_scene
+    from rsd.temporal import prev_view_to_cur_view
+    cfg = small_frame_config()
+    scene = make_scene("arcade_tiny")
+    dev = Device(0)
+    gs = GpuScene(dev, scene)
+    g = rg.load_script(ROOT / "tests" / "graphs" / "svao_temporal.py")["SVAOTemporal"]
+    pos0, tgt0 = np.array(scene.camera["pos"]), np.array(scene.camera["target"])
+    prev_cam, o_prev = None, None
+    G = 16  # svao_temporal.py GuardBand
+    for i in range(3):
+        step = np.array([0.03, 0.0, 0.0]) * i
+        cam = look_at((pos0 + step).tolist(), (tgt0 + step).tolist(), scene.camera["up"], cfg)
+        g.set_scene(gs.h, cam)
+        if i == 0:
+            g.compile(cfg.fb_w, cfg.fb_h)
+        g.execute()
+        torch.cuda.synchronize()
+        z = g.output_tensor("LinearizeDepth.linearDepth").cpu().numpy().reshape(cfg.fb_h, cfg.fb_w)
+        blurred = g.output_tensor("CrossBilateralBlur0.colorOut").cpu().numpy().reshape(cfg.fb_h, cfg.fb_w)
+        mv = g.output_tensor("GBufferRaster.mvec").cpu().numpy().reshape(cfg.fb_h, cfg.fb_w, 2)
+        ao = g.output_tensor("TemporalAO.aoOut").cpu().numpy().reshape(cfg.fb_h, cfg.fb_w)
+        oc = to_oracle(cam, oracle.Camera)
+        op = to_oracle(prev_cam or cam, oracle.Camera)
+        want_mv = oracle.motion_vectors(oc, op, z)
+        assert np.array_equal(mv.view(np.uint32), want_mv.view(np.uint32)), i
+        if o_prev is None:
+            o_prev = (np.zeros_like(z), np.zeros_like(blurred), np.zeros_like(blurred))
+        want, want_n = oracle.temporal_ao(blurred, z, want_mv, *o_prev, oc, prev_view_to_cur_view(cam, prev_cam or cam),
+                                          G)
+        assert np.array_equal(ao[G:-G, G:-G], want[G:-G, G:-G]), i
+        o_prev = (z, want, want_n)
+        prev_cam = cam
+    assert (want_n[G:-G, G:-G] == 3).mean() > 0.8
+    g.close()
+    gs.release()
+    dev.close()

@@ -223,3 +223,28 @@ def test_sd_pass_refuses_like_the_reference(N, use16):
     with pytest.raises(abi.RsdError):
         g.plan(64, 32)
     g.close()
+
+
+def test_temporal_ao_enabled_plans():
+    """TemporalAO enabled (TemporalAO.cpp:92-103): linearZ and mvec become required inputs;
+    GBufferRaster declares mvec (RG32Float)."""
+    g = rsdgraph.load_script(ROOT / "tests" / "graphs" / "svao_temporal.py")["SVAOTemporal"]
+    g.plan(*FB)
+    order = g.execution_order()
+    assert order.index("GBufferRaster") < order.index("TemporalAO") and order.index("SVAO") < order.index("TemporalAO")
+    res = g.resources()
+    assert res["GBufferRaster.mvec"] == (FB[0], FB[1], 1, "RG32Float")
+    assert res["TemporalAO.aoOut"] == (FB[0], FB[1], 1, "R8Unorm")
+    h = rsdgraph.RenderGraph("tao")
+    h.create_pass("GBufferRaster", "GBufferRaster", {})
+    h.create_pass("TemporalAO", "TemporalAO", {"enabled": True})
+    h.add_edge("GBufferRaster.mvec", "TemporalAO.aoIn")
+    h.mark_output("TemporalAO.aoOut")
+    with pytest.raises(abi.RsdError, match="required input 'TemporalAO.linearZ'"):
+        h.plan(*FB)
+    d = rsdgraph.RenderGraph("tao_off")  # disabled: a pass-through needing only aoIn
+    d.create_pass("GBufferRaster", "GBufferRaster", {})
+    d.create_pass("TemporalAO", "TemporalAO", {"enabled": False})
+    d.add_edge("GBufferRaster.mvec", "TemporalAO.aoIn")
+    d.mark_output("TemporalAO.aoOut")
+    d.plan(*FB)

@@ -1,0 +1,95 @@
+"""TemporalAO (enabled) and motion vectors: properties of the oracle restatement
+(oracle/rsd_oracle.c ocpu_temporal_ao / ocpu_motion_vectors, TemporalAO.ps.slang:55-101) on CPU,
+and the host-side prevViewToCurView.  The reference holds no TemporalAO fixtures, so the pass is
+pinned by its defining behaviour: a static camera accumulates up to 30 frames, a stable-mask
+pixel, an off-screen motion vector or a > 10 % depth change resets the history to 1."""
+import numpy as np
+import pytest
+
+F = np.float32
+
+
+def _cam(oracle, pos=(0.0, 2.0, 8.0), target=(0.0, 1.0, 0.0)):
+    return oracle.camera_look_at(pos, target, (0.0, 1.0, 0.0), aspect=96 / 64)
+
+
+def _m(cam, prev):
+    from rsd.temporal import prev_view_to_cur_view
+    return prev_view_to_cur_view(cam, prev)
+
+
+def test_prev_view_to_cur_view_identity_and_translation(oracle):
+    c0 = _cam(oracle)
+    assert np.allclose(_m(c0, c0), np.eye(4), atol=1e-6)
+    c1 = _cam(oracle, pos=(0.0, 2.0, 7.0), target=(0.0, 1.0, -1.0))  # moved 1 m along -z, same orientation
+    m = _m(c1, c0)
+    assert np.allclose(m[:3, :3], np.eye(3), atol=1e-6)
+    # a point 5 m in front of c0 is 4 m in front of c1 (view space looks down -z)
+    p = m @ np.array([0.0, 0.0, -5.0, 1.0])
+    assert abs(-p[2] - 5.0 * np.cos(np.arctan(1 / 8)) + 1.0 * np.cos(np.arctan(1 / 8))) < 0.2
+
+
+def test_motion_vectors_static_camera_are_zero(oracle):
+    c = _cam(oracle)
+    z = np.linspace(1.0, 30.0, 64 * 96, dtype=F).reshape(64, 96)
+    mv = oracle.motion_vectors(c, c, z)
+    assert np.abs(mv).max() < 2e-5
+
+
+def test_motion_vectors_follow_the_camera(oracle):
+    """Camera moved to the right: scene points move left on screen -> prevUV - uv > 0 in x."""
+    c0 = _cam(oracle, pos=(0.0, 2.0, 8.0), target=(0.0, 1.0, 0.0))
+    c1 = _cam(oracle, pos=(0.3, 2.0, 8.0), target=(0.3, 1.0, 0.0))
+    z = np.full((64, 96), 8.0, F)
+    mv = oracle.motion_vectors(c1, c0, z)
+    assert (mv[..., 0] > 0).all() and np.abs(mv[..., 1]).max() < 0.01
+    behind = oracle.motion_vectors(c1, _cam(oracle, pos=(0.0, 2.0, -30.0), target=(0.0, 1.0, -40.0)), z)
+    assert (behind == 2.0).all()  # every hit is behind that previous camera: off screen
+
+
+def test_temporal_accumulates_to_thirty_and_resets(oracle):
+    H, W, g = 64, 96, 4
+    c = _cam(oracle)
+    rng = np.random.default_rng(3)
+    ao = rng.integers(0, 256, (H, W)).astype(np.uint8)
+    z = (5.0 + rng.random((H, W))).astype(F)
+    mv = np.zeros((H, W, 2), F)
+    m = _m(c, c)
+    prev_z, prev_ao, prev_n = np.zeros_like(z), np.zeros_like(ao), np.zeros_like(ao)
+    for frame in range(35):
+        out, n = oracle.temporal_ao(ao, z, mv, prev_z, prev_ao, prev_n, c, m, g)
+        prev_z, prev_ao, prev_n = z, out, n
+        inner = (slice(g, H - g), slice(g, W - g))
+        want = 1 if frame == 0 else min(frame + 1, 30)
+        assert (n[inner] == want).all(), frame
+        assert np.array_equal(out[inner], ao[inner])  # a constant signal stays itself
+        assert (n[:g] == 0).all() and (out[:, :g] == 0).all()  # scissor
+    # stable mask, off-screen motion, depth change: history back to 1, AO = the new AO
+    mask = np.zeros_like(ao)
+    mask[10:20, 10:20] = 1
+    mv2 = mv.copy()
+    mv2[30:40, 30:40] = 0.9
+    z2 = z.copy()
+    z2[50:55, 50:60] *= 1.2
+    ao2 = (255 - ao).astype(np.uint8)
+    out, n = oracle.temporal_ao(ao2, z2, mv2, prev_z, prev_ao, prev_n, c, m, g, stable_mask=mask)
+    for sl in ((slice(10, 20), slice(10, 20)), (slice(30, 40), slice(30, 40)), (slice(50, 55), slice(50, 60))):
+        assert (n[sl] == 1).all() and np.array_equal(out[sl], ao2[sl])
+    assert (n[25:28, 70:80] == 30).all()
+    # elsewhere the 30-frame history dominates: (30 * old + new) / 31
+    exp = np.floor((30 * int(ao[25, 70]) / 255 + int(ao2[25, 70]) / 255) / 31 * 255 + 0.5)
+    assert abs(int(out[25, 70]) - exp) <= 1
+
+
+def test_temporal_ao_host_mirror_refuses_bad_shapes():
+    pytest.importorskip("torch")
+    import torch
+
+    from rsd.temporal import TemporalAO
+    t = TemporalAO(enabled=True)
+    ao = torch.zeros((8, 8), dtype=torch.uint8)
+    with pytest.raises(ValueError):
+        t.execute(ao, torch.zeros((8, 8), dtype=torch.float64), torch.zeros((8, 8, 2)), None, None)
+    d = TemporalAO(enabled=False)  # disabled: a copy, no librsd call
+    src = torch.arange(64, dtype=torch.uint8).reshape(8, 8)
+    assert torch.equal(d.execute(src, None, None, None, None), src)
