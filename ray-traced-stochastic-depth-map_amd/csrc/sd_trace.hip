@@ -942,17 +942,17 @@ __device__ __forceinline__ uint32_t row_bits(bool p, int base) {
 
 // Row-local moves without the LDS crossbar (8-lane rows: two per 16-lane DPP row; 16-lane
 // rows fall back to __shfl).  DPP row_shr:n -> lane i reads lane i - n, row_shl:n -> i + n.
-constexpr int kDppRowShr1 = 0x111, kDppRowShr4 = 0x114, kDppRowShl4 = 0x104, kDppQuad3 = 0xFF;
+constexpr int kDppRowShr1 = 0x111, kDppRowShr4 = 0x114, kDppRowShl4 = 0x104;
 // value of row lane L (3 or 7 for 8-lane rows) in every lane of the row
 template <int ROW, int L>
 __device__ __forceinline__ uint32_t row_bcast(uint32_t v, int l, int base) {
-    if constexpr (ROW == 8 && (L == 3 || L == 7)) {
-        const uint32_t q = dppu<kDppQuad3>(v);  // lanes 0-3 <- lane 3, lanes 4-7 <- lane 7
-        if constexpr (L == 7) {
-            const uint32_t w = dppu<kDppRowShl4>(q);  // lanes 0-3 <- lane 7
+    if constexpr (ROW == 8) {
+        const uint32_t q = dppu<(L & 3) * 0x55>(v);  // lanes 0-3 <- lane L % 4, lanes 4-7 <- lane 4 + L % 4
+        if constexpr (L >= 4) {
+            const uint32_t w = dppu<kDppRowShl4>(q);  // lanes 0-3 <- lane L
             return l < 4 ? w : q;
         } else {
-            const uint32_t w = dppu<kDppRowShr4>(q);  // lanes 4-7 <- lane 3
+            const uint32_t w = dppu<kDppRowShr4>(q);  // lanes 4-7 <- lane L
             return l < 4 ? q : w;
         }
     } else {
@@ -982,6 +982,21 @@ __device__ __forceinline__ void row_insert(float& kt, uint32_t& kp, float nt, ui
         kt = nt; kp = np;
     } else if (l > pos) {
         kt = st; kp = sp;
+    }
+}
+// the same with the key's barycentrics (the fused walk's hit terms)
+template <int ROW>
+__device__ __forceinline__ void row_insert(float& kt, uint32_t& kp, float& ku, float& kv, float nt, uint32_t np,
+                                           float nu, float nv, int l, int base) {
+    const int pos = __popc(row_bits<ROW>(key_less(kt, kp, nt, np), base));
+    const float st = __uint_as_float(row_prev<ROW>(__float_as_uint(kt), l, base));
+    const uint32_t sp = row_prev<ROW>(kp, l, base);
+    const float su = __uint_as_float(row_prev<ROW>(__float_as_uint(ku), l, base));
+    const float sv = __uint_as_float(row_prev<ROW>(__float_as_uint(kv), l, base));
+    if (l == pos) {
+        kt = nt; kp = np; ku = nu; kv = nv;
+    } else if (l > pos) {
+        kt = st; kp = sp; ku = su; kv = sv;
     }
 }
 
@@ -1076,6 +1091,7 @@ __global__ void __launch_bounds__(kBlock) sd_trace_row_kernel(SDArgs a, const fl
     uint32_t item = kNoItem;  // per lane: the work item of this step
     float kt = INFINITY;  // per lane: key l of the row's sorted k-list
     uint32_t kp = kNoItem;
+    float ku = 0.0f, kv = 0.0f;  // per lane: key l's barycentrics (fused walk: the hit terms' inputs)
     // ---- statistics (counters build)
     TraceStats st{0u, 0u, 0u};
     uint32_t active = 0, hitsDelivered = 0, maxSteps = 0, raySteps = 0, maxNodes = 0, rayNodes = 0;
@@ -1112,7 +1128,7 @@ __global__ void __launch_bounds__(kBlock) sd_trace_row_kernel(SDArgs a, const fl
                 useLB = false;
                 pool = 0;
                 item = l == 0 ? 0u : kNoItem;  // the root node
-                kt = INFINITY; kp = kNoItem;
+                kt = INFINITY; kp = kNoItem; ku = kv = 0.0f;
                 phase = kTrace;
                 if constexpr (CNT) {
                     active += l == 0;
@@ -1184,34 +1200,49 @@ __global__ void __launch_bounds__(kBlock) sd_trace_row_kernel(SDArgs a, const fl
             cswap(ck[1], ci[1], ck[3], ci[3]);
             cswap(ck[1], ci[1], ck[2], ci[2]);
         }
-        // ---- leaves: triangle j of every leaf lane, then the row merges the accepted hits
-        //      into its k-list (one insert each) before triangle j + 1
+        // ---- leaves: every triangle test of the step first (independent dependency chains), then
+        //      the row merges the accepted hits into its k-list, one insert each (the merge
+        //      re-checks each hit against the current K-th key)
         const uint32_t lc = isLeaf ? ((item >> 29) & 3u) + 1u : 0u;
         if (isLeaf) st.leaves++;
+        if (__ballot(lc != 0u) != 0ull) {
+            float tj[4], uj[4], vj[4];
+            uint32_t pj[4];
+            bool aj[4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            if (row_bits<ROW>((uint32_t)j < lc, base) == 0u) break;
-            bool acc = false;
-            float t = 0.0f;
-            uint32_t prim = 0u;
-            if ((uint32_t)j < lc) {
-                st.tris++;
-                const float4 v0 = q[3 * j], v1 = q[3 * j + 1], v2 = q[3 * j + 2];
-                float bu, bv, det;
-                if (intersect_tri(r, v0, v1, v2, t, bu, bv, det) && t >= TMin && t <= TMax) {
-                    prim = __float_as_uint(v0.w);
-                    acc = !culled(det, __float_as_uint(v1.w), a.cull) && (!useLB || key_less(lbT, lbP, t, prim)) &&
-                          key_less(t, prim, kthT, kthP);
+            for (int j = 0; j < 4; ++j) {
+                aj[j] = false;
+                tj[j] = 0.0f; uj[j] = 0.0f; vj[j] = 0.0f;
+                pj[j] = 0u;
+                if ((uint32_t)j < lc) {
+                    st.tris++;
+                    const float4 v0 = q[3 * j], v1 = q[3 * j + 1], v2 = q[3 * j + 2];
+                    float det, t, bu, bv;
+                    if (intersect_tri(r, v0, v1, v2, t, bu, bv, det) && t >= TMin && t <= TMax) {
+                        const uint32_t prim = __float_as_uint(v0.w);
+                        aj[j] = !culled(det, __float_as_uint(v1.w), a.cull) &&
+                                (!useLB || key_less(lbT, lbP, t, prim)) && key_less(t, prim, kthT, kthP);
+                        tj[j] = t; pj[j] = prim; uj[j] = bu; vj[j] = bv;
+                    }
                 }
             }
-            for (uint32_t m = row_bits<ROW>(acc, base); m; m &= m - 1u) {
-                const int srcLane = base + __ffs(m) - 1;
-                const float bt = __shfl(t, srcLane);
-                const uint32_t bp = __shfl(prim, srcLane);
-                if (key_less(bt, bp, kthT, kthP)) {
-                    row_insert<ROW>(kt, kp, bt, bp, l, base);
-                    kthT = row_bcastf<ROW, K - 1>(kt, l, base);
-                    kthP = row_bcast<ROW, K - 1>(kp, l, base);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                for (uint32_t m = row_bits<ROW>(aj[j], base); m; m &= m - 1u) {
+                    const int srcLane = base + __ffs(m) - 1;
+                    const float bt = __shfl(tj[j], srcLane);
+                    const uint32_t bp = __shfl(pj[j], srcLane);
+                    float nu = 0.0f, nv = 0.0f;
+                    if constexpr (!SPLIT) {
+                        nu = __shfl(uj[j], srcLane);
+                        nv = __shfl(vj[j], srcLane);
+                    }
+                    if (key_less(bt, bp, kthT, kthP)) {
+                        if constexpr (SPLIT) row_insert<ROW>(kt, kp, bt, bp, l, base);
+                        else row_insert<ROW>(kt, kp, ku, kv, bt, bp, nu, nv, l, base);
+                        kthT = row_bcastf<ROW, K - 1>(kt, l, base);
+                        kthP = row_bcast<ROW, K - 1>(kp, l, base);
+                    }
                 }
             }
         }
@@ -1285,9 +1316,19 @@ __global__ void __launch_bounds__(kBlock) sd_trace_row_kernel(SDArgs a, const fl
         // TraceRay + anyHit -> algorithm (Common.slangh:102-254) over the found keys, in
         // ascending (t, prim) order; lane j prepares key j
         const int found = min(K, __popc(row_bits<ROW>(kp != kNoItem, base)));
+        // lane j: key j's terms from the (t, barycentrics) its leaf test found -- sd_hit_terms'
+        // values bit for bit; the alpha test (alpha scenes only) re-reads the triangle
         float rng = 0.0f, z = 0.0f;
         bool af = false;
-        if (l < found) sd_hit_terms(a, r, cosT, a.primRec[kp], rng, z, af);
+        if (l < found) {
+            if (a.alphaTest) {
+                sd_hit_terms(a, r, cosT, a.primRec[kp], rng, z, af);
+            } else {
+                rng = sd_hash(ku, kv);
+                z = kt * cosT;  // RayToViewDepth
+                if (a.normalize) z = saturate((z - a.cam.nearZ) / (a.cam.farZ - a.cam.nearZ));
+            }
+        }
         uint32_t delivered = 0;
         const bool commit = sd_algorithm_row<K, N>(a, rng, z, af, found, base, depths, cnt, delivered);
         if (l == 0) hitsDelivered += delivered;
@@ -1299,7 +1340,7 @@ __global__ void __launch_bounds__(kBlock) sd_trace_row_kernel(SDArgs a, const fl
             lbP = __shfl(kp, base + K - 1);
             pool = 0;
             item = l == 0 ? 0u : kNoItem;
-            kt = INFINITY; kp = kNoItem;
+            kt = INFINITY; kp = kNoItem; ku = kv = 0.0f;
             continue;
         }
         if (l == 0) sd_store<N>(a, x, y, depths);
@@ -1819,14 +1860,15 @@ rsd_status sd_trace_impl(rsd_scene* scene, const rsd_camera* cam, const rsd_sd_p
     // 118 us per frame; one frame alone: 245 vs 197 us -- DESIGN.md section 4)
     const bool rowWalk = a.poolSoft >= 16 && walkName != "quad" &&
                          (walkName == "fused" || walkName == "split" || (bandTexels <= 600000u && !throughput));
-    // default: the split row walk (trace -> keys -> resolve) where one chunk of K keys decides
-    // every texel, else the fused row walk; RSD_TRACE_WALK=fused|quad for A/B runs
+    // default: the fused row walk; RSD_TRACE_WALK=split|quad for A/B runs
     // raster walk: triangles -> per-texel K nearest keys (split-eligible canonical traces; the near
     // clip needs the cosine bound)
     const bool rasterOk = split && p->hit_order == RSD_HIT_ORDER_CANONICAL && cosLower > 1e-3 && scene->d_prim_rec;
     const bool raster = rasterOk && walkName == "raster";
+    // the fused row walk carries every key's hit terms from its leaf test, so it needs no resolve
+    // pass; RSD_TRACE_WALK=split keeps the key-list + resolve-kernel variant for A/B runs
     const int walk = p->hit_order == RSD_HIT_ORDER_TRAVERSAL ? 3 : raster ? 4 : !rowWalk ? 0
-                     : (split && walkName != "fused") ? 2 : 1;
+                     : (split && walkName == "split") ? 2 : 1;
     if (walk == 4) {
         const uint32_t tilesW = (sd_w + kTile - 1) / kTile, tilesH = (sd_h + kTile - 1) / kTile;
         const size_t slotBytes = (size_t)sd_w * sd_h * 4, tileBytes = (size_t)tilesW * tilesH * 8;

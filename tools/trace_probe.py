@@ -17,16 +17,20 @@ from rsd.frame import CONFIGS, FrameConfig, Renderer  # noqa: E402
 from rsd.scenes import make_scene  # noqa: E402
 
 
-def timeit(fn, n=20):
+def timeit(fn, n=40, batches=7):
+    """median over `batches` of the mean launch time of n back-to-back calls (us)"""
     fn()
     torch.cuda.synchronize()
-    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    s.record()
-    for _ in range(n):
-        fn()
-    e.record()
-    torch.cuda.synchronize()
-    return s.elapsed_time(e) / n * 1e3  # us
+    res = []
+    for _ in range(batches):
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(n):
+            fn()
+        e.record()
+        torch.cuda.synchronize()
+        res.append(s.elapsed_time(e) / n * 1e3)
+    return float(np.median(res))
 
 
 def main():
@@ -53,6 +57,15 @@ def main():
 
     out["all_us"] = keep(live)
     out["none_us"] = keep(live[:0])
+    if "--counters" in sys.argv:  # instrumented trace: per-ray chain statistics (s_memtime cycles)
+        def cnt(idx):
+            keep(idx)
+            c = r.sd_trace(counters=True)
+            return {k: int(getattr(c, k)) for k, _ in c._fields_}
+        out["counters_all"] = cnt(live)
+        for k in (16, 2048):
+            sel = live[torch.from_numpy(rng.choice(live.numel(), k, replace=False)).to(live.device)]
+            out[f"counters_{k}"] = cnt(sel)
     if "--quick" in sys.argv:
         print(json.dumps(out))
         return
