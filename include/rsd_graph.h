@@ -80,6 +80,14 @@ rsd_status rsd_cross_bilateral_blur(const uint8_t* d_src, const float* d_linear_
                                     uint8_t* d_pingpong, uint8_t* d_dst, uint32_t width, uint32_t height,
                                     uint32_t guard_band, uint32_t kernel_radius, uint32_t better_slope,
                                     rsd_stream stream);
+/* TAA (TAA.cpp:99-124, TAA.ps.slang:78-150): colour-box clamped, motion-compensated history
+ * blend.  Colours RGBA32F (the output's alpha is 1), motion vectors RG32F in uv units; the
+ * caller keeps d_prev_color = the previous output (TAA.cpp:123 blit; zeros on the first frame).
+ * TAA.h defaults: alpha 0.1, color_box_sigma 1.0, anti_flicker 1.  d_color_out must not alias
+ * d_prev_color. */
+rsd_status rsd_taa(const float* d_color_in, const float* d_mvec, const float* d_prev_color, uint32_t width,
+                   uint32_t height, float alpha, float color_box_sigma, uint32_t anti_flicker, float* d_color_out,
+                   rsd_stream stream);
 /* TemporalAO enabled (TemporalAO.cpp:113-163, TemporalAO.ps.slang:55-101): reproject the previous
  * frame's AO along the motion vectors (RG32F, uv units), reject on > 10 % relative depth change or
  * a non-zero stable-mask pixel (d_stable_mask may be NULL: none), accumulate up to 30 frames.

@@ -95,6 +95,7 @@ def lib():
         L.ocpu_cross_bilateral_blur.argtypes = [vp, vp, u32, u32, vp, vp, u32, u32, u32, u32, u32]
         L.ocpu_temporal_ao.argtypes = [vp, vp, vp, vp, vp, vp, vp, u32, u32, u32, vp, vp, vp, vp]
         L.ocpu_motion_vectors.argtypes = [vp, vp, vp, u32, u32, vp]
+        L.ocpu_taa.argtypes = [vp, vp, vp, u32, u32, f32, f32, u32, vp]
         L.ocpu_ray_cone_spread.restype = f32
         L.ocpu_ray_cone_spread.argtypes = [f32, u32]
         L.ocpu_hash.restype = f32
@@ -410,6 +411,19 @@ def motion_vectors(cam, prev_cam, linear_z):
     z = np.ascontiguousarray(linear_z, np.float32)
     out = np.zeros(z.shape + (2,), np.float32)
     lib().ocpu_motion_vectors(C.byref(cam), C.byref(prev_cam), _p(z), z.shape[1], z.shape[0], _p(out))
+    return out
+
+
+def taa(color, mvec, prev_color, alpha=0.1, color_box_sigma=1.0, anti_flicker=True):
+    """TAA of one frame (rsd_oracle.c ocpu_taa, TAA.ps.slang:78-150): RGBA32F (H, W, 4) colours,
+    RG32F (H, W, 2) motion vectors; returns the RGBA32F output (the next frame's prev_color)."""
+    c = np.ascontiguousarray(color, np.float32)
+    H, W = c.shape[:2]
+    mv = np.ascontiguousarray(mvec, np.float32)
+    pv = np.ascontiguousarray(prev_color, np.float32)
+    assert c.shape == (H, W, 4) and mv.shape == (H, W, 2) and pv.shape == (H, W, 4)
+    out = np.zeros_like(c)
+    lib().ocpu_taa(_p(c), _p(mv), _p(pv), W, H, alpha, color_box_sigma, int(bool(anti_flicker)), _p(out))
     return out
 
 

@@ -1916,3 +1916,118 @@ void ocpu_motion_vectors(const ocam* c, const ocam* prev, const float* z, uint32
             mvec[2 * ((size_t)y * W + x) + 1] = my;
         }
 }
+
+/* ------------------------------------------------------------------ TAA
+ * TAA.ps.slang:78-150 (TAA.cpp:99-124); librsd's definitions where HLSL leaves them open:
+ * lerp(x, y, s) = x + s * (y - x), Load outside the texture = 0, gSampler = linear + wrap with
+ * 8-bit sub-texel weights (all four taps), min / max / clamp return the non-NaN operand. */
+static void o_ycgco(const float* c, float out[3])
+{
+    out[0] = c[0] * 0.25f + c[1] * 0.50f + c[2] * 0.25f;
+    out[1] = c[0] * -0.25f + c[1] * 0.50f + c[2] * -0.25f;
+    out[2] = c[0] * 0.50f + c[1] * 0.00f + c[2] * -0.50f;
+}
+
+static void o_bilinear_rgb_wrap(const float* t, int W, int H, float u, float v, float out[3])
+{
+    float x = u * (float)W - 0.5f, y = v * (float)H - 0.5f;
+    float fx0 = floorf(x), fy0 = floorf(y);
+    float qx = floorf((x - fx0) * 256.0f + 0.5f), qy = floorf((y - fy0) * 256.0f + 0.5f);
+    int ix = (int)fx0, iy = (int)fy0;
+    if (qx >= 256.0f) { ix += 1; qx = 0.0f; }
+    if (qy >= 256.0f) { iy += 1; qy = 0.0f; }
+    float wx = qx * (1.0f / 256.0f), wy = qy * (1.0f / 256.0f);
+    int x0 = o_addr(ix, W, 1), x1 = o_addr(ix + 1, W, 1), y0 = o_addr(iy, H, 1), y1 = o_addr(iy + 1, H, 1);
+    const float *a = t + 4 * ((size_t)y0 * W + x0), *b = t + 4 * ((size_t)y0 * W + x1);
+    const float *c = t + 4 * ((size_t)y1 * W + x0), *d = t + 4 * ((size_t)y1 * W + x1);
+    for (int k = 0; k < 3; ++k) {
+        float r0 = a[k] * (1.0f - wx) + b[k] * wx, r1 = c[k] * (1.0f - wx) + d[k] * wx;
+        out[k] = r0 * (1.0f - wy) + r1 * wy;
+    }
+}
+
+void ocpu_taa(const float* color, const float* mvec, const float* prev, uint32_t W_, uint32_t H_, float alpha,
+              float sigma, uint32_t antiFlicker, float* out)
+{
+    static const int ox[8] = {-1, -1, 1, 1, 1, 0, 0, -1}, oy[8] = {-1, 1, -1, 1, 0, -1, 1, 0};
+    const int W = (int)W_, H = (int)H_;
+    const float inv[2] = {1.0f / (float)W, 1.0f / (float)H};
+    static const float zero4[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    for (int y = 0; y < H; ++y)
+        for (int x = 0; x < W; ++x) {
+            const float tu = ((float)x + 0.5f) / (float)W, tv = ((float)y + 0.5f) / (float)H;
+            float col[3], avg[3], var[3];
+            o_ycgco(color + 4 * ((size_t)y * W + x), col);
+            for (int k = 0; k < 3; ++k) { avg[k] = col[k]; var[k] = col[k] * col[k]; }
+            for (int n = 0; n < 8; ++n) {
+                const int xx = x + ox[n], yy = y + oy[n];
+                const float* src = (xx < 0 || yy < 0 || xx >= W || yy >= H) ? zero4 : color + 4 * ((size_t)yy * W + xx);
+                float c[3];
+                o_ycgco(src, c);
+                for (int k = 0; k < 3; ++k) { avg[k] = avg[k] + c[k]; var[k] = var[k] + c[k] * c[k]; }
+            }
+            const float nine = 1.0f / 9.0f;
+            float cmin[3], cmax[3];
+            for (int k = 0; k < 3; ++k) {
+                avg[k] = avg[k] * nine;
+                var[k] = var[k] * nine;
+                const float sg = sqrtf(o_max(0.0f, var[k] - avg[k] * avg[k]));
+                cmin[k] = avg[k] - sigma * sg;
+                cmax[k] = avg[k] + sigma * sg;
+            }
+            float mx = mvec[2 * ((size_t)y * W + x)], my = mvec[2 * ((size_t)y * W + x) + 1];
+            for (int n = 0; n < 8; ++n) {
+                const int xx = x + ox[n], yy = y + oy[n];
+                float m0 = 0.0f, m1 = 0.0f;
+                if (!(xx < 0 || yy < 0 || xx >= W || yy >= H)) {
+                    m0 = mvec[2 * ((size_t)yy * W + xx)];
+                    m1 = mvec[2 * ((size_t)yy * W + xx) + 1];
+                }
+                if (m0 * m0 + m1 * m1 > mx * mx + my * my) { mx = m0; my = m1; }
+            }
+            const float sp[2] = {(tu + mx) * (float)W, (tv + my) * (float)H};
+            float w0[2], w12[2], w3[2], c0[2], c12[2], c3[2];
+            for (int k = 0; k < 2; ++k) {
+                const float tc = floorf(sp[k] - 0.5f) + 0.5f;
+                const float f = sp[k] - tc, f2 = f * f, f3 = f2 * f;
+                const float q0 = f2 - 0.5f * (f3 + f);
+                const float q1 = 1.5f * f3 - 2.5f * f2 + 1.0f;
+                const float q3 = 0.5f * (f3 - f2);
+                const float q2 = 1.0f - q0 - q1 - q3;
+                w0[k] = q0;
+                w12[k] = q1 + q2;
+                w3[k] = q3;
+                c0[k] = (tc - 1.0f) * inv[k];
+                c12[k] = (tc + q2 / w12[k]) * inv[k];
+                c3[k] = (tc + 2.0f) * inv[k];
+            }
+            const float xs[3] = {c0[0], c12[0], c3[0]}, ys[3] = {c0[1], c12[1], c3[1]};
+            const float wxs[3] = {w0[0], w12[0], w3[0]}, wys[3] = {w0[1], w12[1], w3[1]};
+            float h[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+            for (int i = 0; i < 3; ++i)
+                for (int j = 0; j < 3; ++j) {
+                    float t[3];
+                    o_bilinear_rgb_wrap(prev, W, H, xs[i], ys[j], t);
+                    const float w = wxs[i] * wys[j];
+                    for (int k = 0; k < 3; ++k) h[k] = (i == 0 && j == 0) ? t[k] * w : h[k] + t[k] * w;
+                }
+            float hist[3];
+            o_ycgco(h, hist);
+            float al = alpha;
+            if (antiFlicker) {
+                const float dist = o_min(fabsf(cmin[0] - hist[0]), fabsf(cmax[0] - hist[0]));
+                al = o_min(o_max((alpha * dist) / (dist + cmax[0] - cmin[0]), 0.0f), 1.0f);
+            }
+            float l[3];
+            for (int k = 0; k < 3; ++k) {
+                const float hc = o_min(o_max(hist[k], cmin[k]), cmax[k]);
+                l[k] = hc + al * (col[k] - hc);
+            }
+            const float tmp = l[0] - l[1];
+            float* o = out + 4 * ((size_t)y * W + x);
+            o[0] = tmp + l[2];
+            o[1] = l[0] + l[1];
+            o[2] = tmp - l[2];
+            o[3] = 1.0f;
+        }
+}

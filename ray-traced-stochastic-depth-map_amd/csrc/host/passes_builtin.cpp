@@ -14,8 +14,9 @@
 //   ImageEquation         ImageEquation.cpp          rsd_image_equation_compile / _run
 //   Switch                Switch.cpp                 copy of the selected input
 //   TemporalAO            TemporalAO.cpp             rsd_temporal_ao (enabled = False: copy)
+//   TAA                   TAA.cpp                    rsd_taa
 //
-// Every other pass type of the reference scripts (ToneMapper, TAA, ForwardLighting, ...)
+// Every other pass type of the reference scripts (ToneMapper, ForwardLighting, ...)
 // is outside the hot path; it resolves to a stub that declares whatever fields
 // the script connects and does no work, so the scripts build and run unchanged.
 #include <cmath>
@@ -690,6 +691,56 @@ private:
     uint32_t w_ = 0, h_ = 0;
 };
 
+// ------------------------------------------------------------------------------ TAA
+// TAA.cpp:59-124: `alpha`, `colorBoxSigma`, `antiFlicker` (TAA.h defaults 0.1, 1.0, true); the
+// previous output is kept (allocatePrevColor: re-allocated, zeroed, when the size changes) and
+// refreshed by a copy after every execute (:123).
+class TAAPass : public RenderPass {
+public:
+    explicit TAAPass(const Properties& p) {
+        props_ = p;
+        alpha_ = (float)p.getFloat("alpha", 0.1);
+        sigma_ = (float)p.getFloat("colorBoxSigma", 1.0);
+        antiFlicker_ = p.getBool("antiFlicker", true);
+    }
+    ~TAAPass() override { (void)hipFree(prev_); }
+    Reflection reflect(const CompileData&) override {
+        Reflection r;
+        r.addInput("motionVecs", "Screen-space motion vectors").format = Format::RG32Float;
+        r.addInput("colorIn", "Color-buffer of the current frame").format = Format::RGBA32Float;
+        r.addOutput("colorOut", "Anti-aliased color buffer").format = Format::RGBA32Float;
+        return r;
+    }
+    void execute(Context& ctx, const RenderData& rd) override {
+        Texture* in = rd["colorIn"];
+        Texture* mv = rd["motionVecs"];
+        Texture* out = rd["colorOut"];
+        if (in->format != Format::RGBA32Float || in->width != out->width || in->height != out->height)
+            throw Unsupported("TAA: colorIn must be RGBA32Float at the output size");
+        if (mv->format != Format::RG32Float || mv->width != out->width || mv->height != out->height)
+            throw Unsupported("TAA: motionVecs must be RG32Float at the output size");
+        if (!prev_ || w_ != out->width || h_ != out->height) {
+            (void)hipFree(prev_);
+            prev_ = nullptr;
+            if (hipMalloc(&prev_, out->bytes()) != hipSuccess) throw std::runtime_error("TAA: history allocation failed");
+            (void)hipMemsetAsync(prev_, 0, out->bytes(), ctx.stream);
+            w_ = out->width;
+            h_ = out->height;
+        }
+        check(rsd_taa((const float*)in->ptr, (const float*)mv->ptr, (const float*)prev_, out->width, out->height,
+                      alpha_, sigma_, antiFlicker_ ? 1u : 0u, (float*)out->ptr, ctx.stream),
+              "TAA");
+        if (hipMemcpyAsync(prev_, out->ptr, out->bytes(), hipMemcpyDeviceToDevice, ctx.stream) != hipSuccess)
+            throw std::runtime_error("TAA: history copy failed");
+    }
+
+private:
+    float alpha_, sigma_;
+    bool antiFlicker_;
+    void* prev_ = nullptr;
+    uint32_t w_ = 0, h_ = 0;
+};
+
 template <class T>
 PluginRegistry::Factory factory() {
     return [](const Properties& p) { return std::unique_ptr<RenderPass>(new T(p)); };
@@ -709,6 +760,7 @@ void registerBuiltinPasses(PluginRegistry& r) {
     r.registerClass("ImageEquation", "per-pixel formula over up to 4 images", factory<ImageEquationPass>());
     r.registerClass("Switch", "forwards the selected input", factory<SwitchPass>());
     r.registerClass("TemporalAO", "temporal AO accumulation over motion vectors", factory<TemporalAOPass>());
+    r.registerClass("TAA", "temporal anti-aliasing (colour-box clamped history)", factory<TAAPass>());
 }
 
 }  // namespace rsd::host

@@ -93,6 +93,131 @@ hipError_t launch_blur(const BlurArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------- TAA
+// TAA.ps.slang:78-150 (TAA.cpp:99-124): YCgCo colour box of the 3x3 neighbourhood (Load: texels
+// outside the image read 0), the longest motion vector of the 3x3, the history through the
+// 9-tap Catmull-Rom filter (bilinear taps of gSampler: linear, wrap -- Falcor's default address
+// mode; librsd's 8-bit sub-texel weights), anti-flicker blend factor, clamp, lerp.  HLSL
+// lerp(x, y, s) = x + s * (y - x); clamp / min / max return the non-NaN operand.
+struct TaaArgs {
+    const float4* color;
+    const float2* mvec;
+    const float4* prev;
+    float4* out;
+    int W, H;
+    float alpha, sigma;
+    uint32_t antiFlicker;
+    float invW, invH;  // 1.0 / texDim
+};
+
+__device__ __forceinline__ f3 rgb_to_ycgco(float4 c) {
+    const float Y = c.x * 0.25f + c.y * 0.50f + c.z * 0.25f;
+    const float Cg = c.x * -0.25f + c.y * 0.50f + c.z * -0.25f;
+    const float Co = c.x * 0.50f + c.y * 0.00f + c.z * -0.50f;
+    return mk(Y, Cg, Co);
+}
+
+__device__ __forceinline__ float4 taa_load(const float4* __restrict__ t, int W, int H, int x, int y) {
+    if (x < 0 || y < 0 || x >= W || y >= H) return make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    return t[(size_t)y * W + x];
+}
+
+__device__ __forceinline__ int wrap_addr(int i, int n) {
+    i %= n;
+    return i < 0 ? i + n : i;
+}
+
+// bilinear RGB of an RGBA32F texture, wrap addressing, 8-bit sub-texel weights (all 4 taps)
+__device__ __forceinline__ f3 taa_bilinear(const float4* __restrict__ t, int W, int H, float u, float v) {
+    const float x = u * (float)W - 0.5f, y = v * (float)H - 0.5f;
+    const float fx0 = floorf(x), fy0 = floorf(y);
+    float qx = floorf((x - fx0) * 256.0f + 0.5f), qy = floorf((y - fy0) * 256.0f + 0.5f);
+    int ix = (int)fx0, iy = (int)fy0;
+    if (qx >= 256.0f) { ix += 1; qx = 0.0f; }
+    if (qy >= 256.0f) { iy += 1; qy = 0.0f; }
+    const float wx = qx * (1.0f / 256.0f), wy = qy * (1.0f / 256.0f);
+    const int x0 = wrap_addr(ix, W), x1 = wrap_addr(ix + 1, W), y0 = wrap_addr(iy, H), y1 = wrap_addr(iy + 1, H);
+    const float4 a = t[(size_t)y0 * W + x0], b = t[(size_t)y0 * W + x1];
+    const float4 c = t[(size_t)y1 * W + x0], d = t[(size_t)y1 * W + x1];
+    auto lerp2 = [&](float p, float q, float r, float s) {
+        const float r0 = p * (1.0f - wx) + q * wx, r1 = r * (1.0f - wx) + s * wx;
+        return r0 * (1.0f - wy) + r1 * wy;
+    };
+    return mk(lerp2(a.x, b.x, c.x, d.x), lerp2(a.y, b.y, c.y, d.y), lerp2(a.z, b.z, c.z, d.z));
+}
+
+__global__ void __launch_bounds__(kPostW * kPostH) taa_kernel(TaaArgs a) {
+    const int x = (int)(blockIdx.x * kPostW + threadIdx.x), y = (int)(blockIdx.y * kPostH + threadIdx.y);
+    if (x >= a.W || y >= a.H) return;
+    constexpr int ox[8] = {-1, -1, 1, 1, 1, 0, 0, -1}, oy[8] = {-1, 1, -1, 1, 0, -1, 1, 0};
+    const float tu = ((float)x + 0.5f) / (float)a.W, tv = ((float)y + 0.5f) / (float)a.H;  // texC
+    const f3 color = rgb_to_ycgco(a.color[(size_t)y * a.W + x]);
+    f3 avg = color, var = mk(color.x * color.x, color.y * color.y, color.z * color.z);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const f3 c = rgb_to_ycgco(taa_load(a.color, a.W, a.H, x + ox[k], y + oy[k]));
+        avg = mk(avg.x + c.x, avg.y + c.y, avg.z + c.z);
+        var = mk(var.x + c.x * c.x, var.y + c.y * c.y, var.z + c.z * c.z);
+    }
+    const float nine = 1.0f / 9.0f;
+    avg = mk(avg.x * nine, avg.y * nine, avg.z * nine);
+    var = mk(var.x * nine, var.y * nine, var.z * nine);
+    const f3 sg = mk(sqrtf(hmax(0.0f, var.x - avg.x * avg.x)), sqrtf(hmax(0.0f, var.y - avg.y * avg.y)),
+                     sqrtf(hmax(0.0f, var.z - avg.z * avg.z)));
+    const f3 cmin = mk(avg.x - a.sigma * sg.x, avg.y - a.sigma * sg.y, avg.z - a.sigma * sg.z);
+    const f3 cmax = mk(avg.x + a.sigma * sg.x, avg.y + a.sigma * sg.y, avg.z + a.sigma * sg.z);
+    float2 motion = a.mvec[(size_t)y * a.W + x];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const int xx = x + ox[k], yy = y + oy[k];
+        const float2 m = (xx < 0 || yy < 0 || xx >= a.W || yy >= a.H) ? make_float2(0.0f, 0.0f)
+                                                                        : a.mvec[(size_t)yy * a.W + xx];
+        if (m.x * m.x + m.y * m.y > motion.x * motion.x + motion.y * motion.y) motion = m;
+    }
+    // bicubicSampleCatmullRom((texC + motion) * texDim, texDim)
+    const float spx = (tu + motion.x) * (float)a.W, spy = (tv + motion.y) * (float)a.H;
+    const float tcx = floorf(spx - 0.5f) + 0.5f, tcy = floorf(spy - 0.5f) + 0.5f;
+    float w0[2], w12[2], w3[2], c0[2], c12[2], c3[2];
+    const float fv[2] = {spx - tcx, spy - tcy}, tcv[2] = {tcx, tcy}, inv[2] = {a.invW, a.invH};
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const float f = fv[k], f2 = f * f, f3v = f2 * f;
+        const float q0 = f2 - 0.5f * (f3v + f);
+        const float q1 = 1.5f * f3v - 2.5f * f2 + 1.0f;
+        const float q3 = 0.5f * (f3v - f2);
+        const float q2 = 1.0f - q0 - q1 - q3;
+        w0[k] = q0;
+        w12[k] = q1 + q2;
+        w3[k] = q3;
+        c0[k] = (tcv[k] - 1.0f) * inv[k];
+        c12[k] = (tcv[k] + q2 / w12[k]) * inv[k];
+        c3[k] = (tcv[k] + 2.0f) * inv[k];
+    }
+    const float xs[3] = {c0[0], c12[0], c3[0]}, ys[3] = {c0[1], c12[1], c3[1]};
+    const float wxs[3] = {w0[0], w12[0], w3[0]}, wys[3] = {w0[1], w12[1], w3[1]};
+    f3 h = mk(0.0f, 0.0f, 0.0f);
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            const f3 t = taa_bilinear(a.prev, a.W, a.H, xs[i], ys[j]);
+            const float w = wxs[i] * wys[j];
+            if (i == 0 && j == 0) h = mk(t.x * w, t.y * w, t.z * w);
+            else h = mk(h.x + t.x * w, h.y + t.y * w, h.z + t.z * w);
+        }
+    f3 hist = rgb_to_ycgco(make_float4(h.x, h.y, h.z, 0.0f));
+    float alpha = a.alpha;
+    if (a.antiFlicker) {
+        const float dist = hmin(fabsf(cmin.x - hist.x), fabsf(cmax.x - hist.x));
+        alpha = hmin(hmax((a.alpha * dist) / (dist + cmax.x - cmin.x), 0.0f), 1.0f);
+    }
+    hist = mk(hmin(hmax(hist.x, cmin.x), cmax.x), hmin(hmax(hist.y, cmin.y), cmax.y), hmin(hmax(hist.z, cmin.z), cmax.z));
+    const f3 l = mk(hist.x + alpha * (color.x - hist.x), hist.y + alpha * (color.y - hist.y),
+                    hist.z + alpha * (color.z - hist.z));
+    const float tmp = l.x - l.y;
+    a.out[(size_t)y * a.W + x] = make_float4(tmp + l.z, l.x + l.y, tmp - l.z, 1.0f);
+}
+
 // ---------------------------------------------------------------------- TemporalAO
 // TemporalAO.ps.slang:55-101 (TemporalAO.cpp:113-163, enabled): reproject the previous frame's
 // AO along the motion vector, reject on a > 10 % relative depth change (or a stable-mask pixel),
@@ -398,6 +523,31 @@ extern "C" rsd_status rsd_cross_bilateral_blur(const uint8_t* d_src, const float
         if (e != hipSuccess) return hip_fail(e, "blur_kernel launch");
     }
     return RSD_OK;
+}
+
+extern "C" rsd_status rsd_taa(const float* d_color_in, const float* d_mvec, const float* d_prev_color, uint32_t width,
+                              uint32_t height, float alpha, float color_box_sigma, uint32_t anti_flicker,
+                              float* d_color_out, rsd_stream stream) {
+    if (!d_color_in || !d_mvec || !d_prev_color || !d_color_out || width == 0 || height == 0) {
+        set_error("rsd_taa: invalid argument");
+        return RSD_ERR_INVALID_ARG;
+    }
+    TaaArgs a{};
+    a.color = reinterpret_cast<const float4*>(d_color_in);
+    a.mvec = reinterpret_cast<const float2*>(d_mvec);
+    a.prev = reinterpret_cast<const float4*>(d_prev_color);
+    a.out = reinterpret_cast<float4*>(d_color_out);
+    a.W = (int)width;
+    a.H = (int)height;
+    a.alpha = alpha;
+    a.sigma = color_box_sigma;
+    a.antiFlicker = anti_flicker;
+    a.invW = 1.0f / (float)width;  // TAA.ps.slang:47 invTextureSize
+    a.invH = 1.0f / (float)height;
+    const dim3 grid((width + kPostW - 1) / kPostW, (height + kPostH - 1) / kPostH);
+    hipLaunchKernelGGL(taa_kernel, grid, dim3(kPostW, kPostH), 0, (hipStream_t)stream, a);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? RSD_OK : hip_fail(e, "taa_kernel launch");
 }
 
 extern "C" rsd_status rsd_temporal_ao(const uint8_t* d_ao_in, const float* d_linear_z, const float* d_mvec,

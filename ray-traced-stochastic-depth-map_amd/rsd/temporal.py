@@ -1,6 +1,6 @@
-"""TemporalAO (enabled) and the G-buffer's motion vectors on the GPU (librsd rsd_temporal_ao /
-rsd_motion_vectors, include/rsd_graph.h) -- the pass after SVAO in the reference's graphs
-(scripts/SVAO.py: SVAO -> TemporalAO -> CrossBilateralBlur).
+"""TemporalAO (enabled), TAA and the G-buffer's motion vectors on the GPU (librsd rsd_temporal_ao /
+rsd_taa / rsd_motion_vectors, include/rsd_graph.h) -- the temporal passes of the reference's AO
+chain (scripts/SVAO.py: SVAO -> CrossBilateralBlur -> TemporalAO -> Switch -> ImageEquation -> TAA).
 
 TemporalAO mirrors Source/RenderPasses/TemporalAO/TemporalAO.cpp: properties `enabled` and
 `useStableMask` (:42-43), previous-frame depth / AO / history textures (re)allocated on the first
@@ -99,3 +99,29 @@ class TemporalAO:
         self.prev_ao.copy_(ao_out)
         self.prev_history.copy_(self.history)
         return ao_out
+
+
+class TAA:
+    """One TAA pass instance (TAA.cpp): keeps the previous output; properties `alpha`,
+    `colorBoxSigma`, `antiFlicker` with TAA.h's defaults."""
+
+    def __init__(self, alpha: float = 0.1, color_box_sigma: float = 1.0, anti_flicker: bool = True):
+        self.alpha, self.color_box_sigma, self.anti_flicker = alpha, color_box_sigma, anti_flicker
+        self.prev = None
+
+    def execute(self, color_in, motion_vecs, color_out=None):
+        """color_in: (H, W, 4) float32; motion_vecs: (H, W, 2) float32.  Returns color_out."""
+        import torch
+        H, W = color_in.shape[:2]
+        for t, shp in ((color_in, (H, W, 4)), (motion_vecs, (H, W, 2))):
+            if t.dtype != torch.float32 or tuple(t.shape) != shp or not t.is_contiguous():
+                raise ValueError(f"TAA: expected a contiguous float32 {shp} tensor, got {t.dtype} {tuple(t.shape)}")
+        if color_out is None:
+            color_out = torch.empty_like(color_in)
+        if self.prev is None or tuple(self.prev.shape) != (H, W, 4):  # allocatePrevColor
+            self.prev = torch.zeros_like(color_in)
+        s = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+        abi.check(abi.lib().rsd_taa(_ptr(color_in), _ptr(motion_vecs), _ptr(self.prev), W, H, self.alpha,
+                                    self.color_box_sigma, int(bool(self.anti_flicker)), _ptr(color_out), s), "rsd_taa")
+        self.prev.copy_(color_out)  # TAA.cpp:123
+        return color_out

@@ -166,3 +166,57 @@ def test_graph_temporal_ao_enabled(torch, oracle):
     g.close()
     gs.release()
     dev.close()
+
+
+@pytest.mark.parametrize("sigma,anti", [(1.0, True), (0.5, False), (4.0, True)])
+def test_taa_parity(torch, oracle, sigma, anti):
+    """rsd_taa vs ocpu_taa on random colours / motion (some pointing off the image: wrap taps)."""
+    from rsd.temporal import TAA
+    rng = np.random.default_rng(int(sigma * 10))
+    H, W = 45, 77
+    frames = [(rng.random((H, W, 4)) * 2).astype(F) for _ in range(3)]
+    mvs = [rng.normal(0.0, 0.02, (H, W, 2)).astype(F) for _ in range(3)]
+    mvs[1][:5] = 0.6  # far off the image: wrap addressing
+    t = TAA(alpha=0.1, color_box_sigma=sigma, anti_flicker=anti)
+    prev = np.zeros((H, W, 4), F)
+    for c, mv in zip(frames, mvs):
+        out = t.execute(torch.from_numpy(c).cuda(), torch.from_numpy(mv).cuda())
+        torch.cuda.synchronize()
+        want = oracle.taa(c, mv, prev, alpha=0.1, color_box_sigma=sigma, anti_flicker=anti)
+        got = out.cpu().numpy()
+        assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
+        prev = want
+
+
+def test_graph_taa_after_temporal_chain(torch, oracle):
+    """scripts/SVAO.py's AmbientTAA: ImageEquation 'I0[xy].rrra' -> TAA with GBufferRaster.mvec,
+    two camera poses, bit-exact against ocpu_taa on the graph's own inputs."""
+    from conftest import ROOT
+    from rsd import graph as rg
+    from rsd.frame import Device, GpuScene, look_at
+    from rsd.scenes import make_scene
+    cfg = small_frame_config()
+    scene = make_scene("arcade_tiny")
+    dev = Device(0)
+    gs = GpuScene(dev, scene)
+    g = rg.load_script(ROOT / "tests" / "graphs" / "svao_temporal.py")["SVAOTemporal"]
+    pos0, tgt0 = np.array(scene.camera["pos"]), np.array(scene.camera["target"])
+    prev = None
+    for i in range(2):
+        step = np.array([0.0, 0.02, 0.03]) * i
+        cam = look_at((pos0 + step).tolist(), (tgt0 + step).tolist(), scene.camera["up"], cfg)
+        g.set_scene(gs.h, cam)
+        if i == 0:
+            g.compile(cfg.fb_w, cfg.fb_h)
+        g.execute()
+        torch.cuda.synchronize()
+        amb = g.output_tensor("AmbientRef.out").cpu().numpy().reshape(cfg.fb_h, cfg.fb_w, 4)
+        mv = g.output_tensor("GBufferRaster.mvec").cpu().numpy().reshape(cfg.fb_h, cfg.fb_w, 2)
+        got = g.output_tensor("AmbientTAA.colorOut").cpu().numpy().reshape(cfg.fb_h, cfg.fb_w, 4)
+        prev = np.zeros_like(amb) if prev is None else prev
+        want = oracle.taa(amb, mv, prev, alpha=0.1, color_box_sigma=1.0, anti_flicker=True)
+        assert np.array_equal(got.view(np.uint32), want.view(np.uint32)), i
+        prev = want
+    g.close()
+    gs.release()
+    dev.close()

@@ -93,3 +93,33 @@ def test_temporal_ao_host_mirror_refuses_bad_shapes():
     d = TemporalAO(enabled=False)  # disabled: a copy, no librsd call
     src = torch.arange(64, dtype=torch.uint8).reshape(8, 8)
     assert torch.equal(d.execute(src, None, None, None, None), src)
+
+
+def test_taa_static_history_is_identity_without_clamp(oracle):
+    """Catmull-Rom at texel centres reproduces the history; with a wide colour box and no
+    anti-flicker a static frame blended with itself stays itself (TAA.ps.slang:44-150)."""
+    rng = np.random.default_rng(4)
+    H, W = 24, 40
+    c = rng.random((H, W, 4)).astype(F)
+    out = oracle.taa(c, np.zeros((H, W, 2), F), c, color_box_sigma=100.0, anti_flicker=False)
+    assert np.abs(out[..., :3] - c[..., :3]).max() < 1e-6 and (out[..., 3] == 1.0).all()
+
+
+def test_taa_first_frame_and_clamp(oracle):
+    """First frame (zero history): the history is clamped into the colour box, then blended by
+    alpha; a constant image stays constant whatever the history (box of zero width)."""
+    H, W = 16, 16
+    const = np.full((H, W, 4), 0.5, F)
+    out = oracle.taa(const, np.zeros((H, W, 2), F), np.zeros_like(const))
+    inner = out[1:-1, 1:-1, :3]  # border pixels see zero neighbours (Load outside = 0)
+    assert np.allclose(inner, 0.5, atol=1e-6)
+    # the longest 3x3 motion vector steers the history fetch: a history shifted by one texel
+    # and a matching motion vector give the same result as no shift
+    rng = np.random.default_rng(5)
+    c = rng.random((H, W, 4)).astype(F)
+    prev = np.roll(c, 1, axis=1)  # prev[x] = c[x - 1]
+    mv = np.zeros((H, W, 2), F)
+    mv[..., 0] = 1.0 / W  # history at x + 1 px
+    a = oracle.taa(c, mv, prev, color_box_sigma=100.0, anti_flicker=False)
+    b = oracle.taa(c, np.zeros_like(mv), c, color_box_sigma=100.0, anti_flicker=False)
+    assert np.abs(a - b).max() < 1e-5
