@@ -80,6 +80,15 @@ rsd_status rsd_cross_bilateral_blur(const uint8_t* d_src, const float* d_linear_
                                     uint8_t* d_pingpong, uint8_t* d_dst, uint32_t width, uint32_t height,
                                     uint32_t guard_band, uint32_t kernel_radius, uint32_t better_slope,
                                     rsd_stream stream);
+/* AOFlickerMask (AOFlickerMask.cpp:73-86, AOFlickerMask.ps.slang:43-63): 1 where the pixel's
+ * x and y neighbours lie in its view-space normal plane (|dot| <= 0.1), else 0 (R8Uint).
+ * d_normal_w: world-space normals, RGBA32F (GBufferRaster.faceNormalW). */
+rsd_status rsd_ao_flicker_mask(const float* d_linear_z, const float* d_normal_w, uint32_t width, uint32_t height,
+                               const rsd_camera* cam, uint8_t* d_mask, rsd_stream stream);
+/* BinaryDilation (BinaryDilation.ps.slang:13-43): min (op_max 0) or max (op_max 1) over the
+ * five 2x2 Gather footprints of the pixel (R8Uint in and out, not in place). */
+rsd_status rsd_binary_dilation(const uint8_t* d_in, uint32_t width, uint32_t height, uint32_t op_max, uint8_t* d_out,
+                               rsd_stream stream);
 /* TAA (TAA.cpp:99-124, TAA.ps.slang:78-150): colour-box clamped, motion-compensated history
  * blend.  Colours RGBA32F (the output's alpha is 1), motion vectors RG32F in uv units; the
  * caller keeps d_prev_color = the previous output (TAA.cpp:123 blit; zeros on the first frame).

@@ -96,6 +96,8 @@ def lib():
         L.ocpu_temporal_ao.argtypes = [vp, vp, vp, vp, vp, vp, vp, u32, u32, u32, vp, vp, vp, vp]
         L.ocpu_motion_vectors.argtypes = [vp, vp, vp, u32, u32, vp]
         L.ocpu_taa.argtypes = [vp, vp, vp, u32, u32, f32, f32, u32, vp]
+        L.ocpu_ao_flicker_mask.argtypes = [vp, vp, u32, u32, vp, vp]
+        L.ocpu_binary_dilation.argtypes = [vp, u32, u32, u32, vp]
         L.ocpu_ray_cone_spread.restype = f32
         L.ocpu_ray_cone_spread.argtypes = [f32, u32]
         L.ocpu_hash.restype = f32
@@ -411,6 +413,25 @@ def motion_vectors(cam, prev_cam, linear_z):
     z = np.ascontiguousarray(linear_z, np.float32)
     out = np.zeros(z.shape + (2,), np.float32)
     lib().ocpu_motion_vectors(C.byref(cam), C.byref(prev_cam), _p(z), z.shape[1], z.shape[0], _p(out))
+    return out
+
+
+def ao_flicker_mask(linear_z, normal_w, cam):
+    """AOFlickerMask (rsd_oracle.c ocpu_ao_flicker_mask): R8Uint stable mask (H, W)."""
+    z = np.ascontiguousarray(linear_z, np.float32)
+    n = np.ascontiguousarray(normal_w, np.float32)
+    H, W = z.shape
+    assert n.shape == (H, W, 4)
+    out = np.zeros((H, W), np.uint8)
+    lib().ocpu_ao_flicker_mask(_p(z), _p(n), W, H, C.byref(cam), _p(out))
+    return out
+
+
+def binary_dilation(mask, op="min"):
+    """BinaryDilation (rsd_oracle.c ocpu_binary_dilation), op 'min' or 'max'."""
+    m = np.ascontiguousarray(mask, np.uint8)
+    out = np.zeros_like(m)
+    lib().ocpu_binary_dilation(_p(m), m.shape[1], m.shape[0], {"min": 0, "max": 1}[op], _p(out))
     return out
 
 

@@ -2031,3 +2031,77 @@ void ocpu_taa(const float* color, const float* mvec, const float* prev, uint32_t
             o[3] = 1.0f;
         }
 }
+
+/* ------------------------------------------------------------------ AOFlickerMask
+ * AOFlickerMask.ps.slang:43-63: Loads outside the image read 0; min returns the non-NaN operand. */
+static void o_px_view(int i, int j, int W, int H, float d, float isx, float isy, float out[3])
+{
+    float u = o_saturate(((float)i + 0.5f) / (float)W), v = o_saturate(((float)j + 0.5f) / (float)H);
+    float ndcx = u * 2.0f - 1.0f, ndcy = (1.0f - v) * 2.0f - 1.0f;
+    out[0] = ndcx * d * isx;
+    out[1] = ndcy * d * isy;
+    out[2] = -d;
+}
+
+void ocpu_ao_flicker_mask(const float* z, const float* nw, uint32_t W_, uint32_t H_, const ocam* cam, uint8_t* mask)
+{
+    const int W = (int)W_, H = (int)H_;
+    const float isx = 0.5f * (cam->frameWidth / cam->focalLength), isy = 0.5f * (cam->frameHeight / cam->focalLength);
+    const float* m = cam->viewMat;
+    for (int y = 0; y < H; ++y)
+        for (int x = 0; x < W; ++x) {
+#define LD(i, j) (((i) < 0 || (j) < 0 || (i) >= W || (j) >= H) ? 0.0f : z[(size_t)(j) * W + (i)])
+            const float* n = nw + 4 * ((size_t)y * W + x);
+            float nv[3] = {m[0] * n[0] + m[1] * n[1] + m[2] * n[2], m[4] * n[0] + m[5] * n[1] + m[6] * n[2],
+                           m[8] * n[0] + m[9] * n[1] + m[10] * n[2]};
+            float P[3];
+            o_px_view(x, y, W, H, LD(x, y), isx, isy, P);
+            const int nx[4] = {x + 1, x - 1, x, x}, ny[4] = {y, y, y + 1, y - 1};
+            float pd[4];
+            for (int k = 0; k < 4; ++k) {
+                float q[3], dlt[3], dn[3];
+                o_px_view(nx[k], ny[k], W, H, LD(nx[k], ny[k]), isx, isy, q);
+                for (int c = 0; c < 3; ++c) dlt[c] = P[c] - q[c];
+                o_normalize(dlt, dn);
+                pd[k] = fabsf(o_dot(dn, nv));
+            }
+#undef LD
+            const float dx = o_min(pd[0], pd[1]), dy = o_min(pd[2], pd[3]);
+            mask[(size_t)y * W + x] = (dx <= 0.1f && dy <= 0.1f) ? 1u : 0u;
+        }
+}
+
+/* ------------------------------------------------------------------ BinaryDilation
+ * BinaryDilation.ps.slang:13-43: OP over five Gather footprints (librsd's bilinear footprint,
+ * wrap addressing). */
+static uint32_t o_gather_op(const uint8_t* t, int W, int H, float u, float v, int mx)
+{
+    float x = u * (float)W - 0.5f, y = v * (float)H - 0.5f;
+    float fx0 = floorf(x), fy0 = floorf(y);
+    float qx = floorf((x - fx0) * 256.0f + 0.5f), qy = floorf((y - fy0) * 256.0f + 0.5f);
+    int ix = (int)fx0, iy = (int)fy0;
+    if (qx >= 256.0f) ix += 1;
+    if (qy >= 256.0f) iy += 1;
+    int x0 = o_addr(ix, W, 1), x1 = o_addr(ix + 1, W, 1), y0 = o_addr(iy, H, 1), y1 = o_addr(iy + 1, H, 1);
+    uint32_t v4[4] = {t[(size_t)y1 * W + x0], t[(size_t)y1 * W + x1], t[(size_t)y0 * W + x1], t[(size_t)y0 * W + x0]};
+    uint32_t r = v4[0];
+    for (int k = 1; k < 4; ++k) r = mx ? (v4[k] > r ? v4[k] : r) : (v4[k] < r ? v4[k] : r);
+    return r;
+}
+
+void ocpu_binary_dilation(const uint8_t* in, uint32_t W_, uint32_t H_, uint32_t opMax, uint8_t* out)
+{
+    const int W = (int)W_, H = (int)H_, mx = opMax != 0u;
+    for (int y = 0; y < H; ++y)
+        for (int x = 0; x < W; ++x) {
+            const float u = ((float)x + 0.5f) / (float)W, v = ((float)y + 0.5f) / (float)H;
+            const float dx = 0.5f / (float)W, dy = 0.5f / (float)H;
+            uint32_t r[5] = {o_gather_op(in, W, H, u + dx, v + 3.0f * dy, mx),
+                             o_gather_op(in, W, H, u + 3.0f * dx, v + -dy, mx),
+                             o_gather_op(in, W, H, u + -dx, v + -3.0f * dy, mx),
+                             o_gather_op(in, W, H, u + -3.0f * dx, v + dy, mx), o_gather_op(in, W, H, u, v, mx)};
+            uint32_t o = r[0];
+            for (int k = 1; k < 5; ++k) o = mx ? (r[k] > o ? r[k] : o) : (r[k] < o ? r[k] : o);
+            out[(size_t)y * W + x] = (uint8_t)o;
+        }
+}

@@ -15,6 +15,8 @@
 //   Switch                Switch.cpp                 copy of the selected input
 //   TemporalAO            TemporalAO.cpp             rsd_temporal_ao (enabled = False: copy)
 //   TAA                   TAA.cpp                    rsd_taa
+//   AOFlickerMask         AOFlickerMask.cpp          rsd_ao_flicker_mask
+//   BinaryDilation        BinaryDilation.cpp         rsd_binary_dilation
 //
 // Every other pass type of the reference scripts (ToneMapper, ForwardLighting, ...)
 // is outside the hot path; it resolves to a stub that declares whatever fields
@@ -741,6 +743,66 @@ private:
     uint32_t w_ = 0, h_ = 0;
 };
 
+// ------------------------------------------------------------------------------ AOFlickerMask
+// AOFlickerMask.cpp:59-86: linearZ + normalW -> R8Uint stable mask (no properties; no scene: no-op)
+class AOFlickerMaskPass : public RenderPass {
+public:
+    explicit AOFlickerMaskPass(const Properties& p) { props_ = p; }
+    Reflection reflect(const CompileData&) override {
+        Reflection r;
+        r.addInput("linearZ", "linear depths").format = Format::R32Float;
+        r.addInput("normalW", "world space normals").format = Format::RGBA32Float;
+        r.addOutput("mask", "mask with stable pixels (1) and unstable/flickering (0)").format = Format::R8Uint;
+        return r;
+    }
+    void setScene(Context&, const SceneRef* s) override { scene_ = s; }
+    void execute(Context& ctx, const RenderData& rd) override {
+        if (!scene_) return;
+        Texture* z = rd["linearZ"];
+        Texture* n = rd["normalW"];
+        Texture* m = rd["mask"];
+        if (z->format != Format::R32Float || n->format != Format::RGBA32Float || z->width != m->width ||
+            z->height != m->height || n->width != m->width || n->height != m->height)
+            throw Unsupported("AOFlickerMask: linearZ R32Float and normalW RGBA32Float at the output size");
+        check(rsd_ao_flicker_mask((const float*)z->ptr, (const float*)n->ptr, m->width, m->height, &scene_->camera,
+                                  (uint8_t*)m->ptr, ctx.stream),
+              "AOFlickerMask");
+    }
+
+private:
+    const SceneRef* scene_ = nullptr;
+};
+
+// ------------------------------------------------------------------------------ BinaryDilation
+// BinaryDilation.cpp:44-110: `op` = "min" (default) or "max" (the shader's OP define)
+class BinaryDilationPass : public RenderPass {
+public:
+    explicit BinaryDilationPass(const Properties& p) {
+        props_ = p;
+        const std::string op = p.getString("op", "min");
+        if (op != "min" && op != "max") throw Unsupported("BinaryDilation: op must be 'min' or 'max'");
+        opMax_ = op == "max";
+    }
+    Reflection reflect(const CompileData&) override {
+        Reflection r;
+        r.addInput("input", "binary input").format = Format::R8Uint;
+        r.addOutput("output", "dilated binary output").format = Format::R8Uint;
+        return r;
+    }
+    void execute(Context& ctx, const RenderData& rd) override {
+        Texture* in = rd["input"];
+        Texture* out = rd["output"];
+        if (formatBytes(in->format) != 1 || in->width != out->width || in->height != out->height)
+            throw Unsupported("BinaryDilation: input must be an 8-bit mask at the output size");
+        check(rsd_binary_dilation((const uint8_t*)in->ptr, out->width, out->height, opMax_ ? 1u : 0u,
+                                  (uint8_t*)out->ptr, ctx.stream),
+              "BinaryDilation");
+    }
+
+private:
+    bool opMax_;
+};
+
 template <class T>
 PluginRegistry::Factory factory() {
     return [](const Properties& p) { return std::unique_ptr<RenderPass>(new T(p)); };
@@ -761,6 +823,8 @@ void registerBuiltinPasses(PluginRegistry& r) {
     r.registerClass("Switch", "forwards the selected input", factory<SwitchPass>());
     r.registerClass("TemporalAO", "temporal AO accumulation over motion vectors", factory<TemporalAOPass>());
     r.registerClass("TAA", "temporal anti-aliasing (colour-box clamped history)", factory<TAAPass>());
+    r.registerClass("AOFlickerMask", "stable-pixel mask from depth and normals", factory<AOFlickerMaskPass>());
+    r.registerClass("BinaryDilation", "min / max over a radius-2 gather ring", factory<BinaryDilationPass>());
 }
 
 }  // namespace rsd::host

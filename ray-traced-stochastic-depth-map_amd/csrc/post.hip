@@ -218,6 +218,71 @@ __global__ void __launch_bounds__(kPostW * kPostH) taa_kernel(TaaArgs a) {
     a.out[(size_t)y * a.W + x] = make_float4(tmp + l.z, l.x + l.y, tmp - l.z, 1.0f);
 }
 
+// ---------------------------------------------------------------------- AOFlickerMask
+// AOFlickerMask.ps.slang:43-63 (AOFlickerMask.cpp:73-86): a pixel is stable (1) when, in x and
+// in y, one of its two neighbours lies in the plane of its view-space normal to within 0.1 (|dot|
+// of the unit offset with the normal).  Loads outside the image read 0; HLSL min returns the
+// non-NaN operand (a zero offset normalizes to NaN).
+__global__ void __launch_bounds__(kPostW * kPostH) flicker_mask_kernel(const float* __restrict__ z,
+                                                                        const float4* __restrict__ nw, int W, int H,
+                                                                        rsd_camera cam, float isx, float isy,
+                                                                        uint8_t* __restrict__ mask) {
+    const int x = (int)(blockIdx.x * kPostW + threadIdx.x), y = (int)(blockIdx.y * kPostH + threadIdx.y);
+    if (x >= W || y >= H) return;
+    auto ld = [&](int i, int j) { return (i < 0 || j < 0 || i >= W || j >= H) ? 0.0f : z[(size_t)j * W + i]; };
+    auto view = [&](int i, int j, float d) {  // UVToViewSpace(PixelToUV(px), d)
+        const float u = saturate(((float)i + 0.5f) / (float)W), v = saturate(((float)j + 0.5f) / (float)H);
+        const float ndcx = u * 2.0f - 1.0f, ndcy = (1.0f - v) * 2.0f - 1.0f;
+        return mk(ndcx * d * isx, ndcy * d * isy, -d);
+    };
+    const float4 n = nw[(size_t)y * W + x];
+    const float* m = cam.viewMat;  // mul(float3x3(viewMat), n)
+    const f3 nv = mk(m[0] * n.x + m[1] * n.y + m[2] * n.z, m[4] * n.x + m[5] * n.y + m[6] * n.z,
+                     m[8] * n.x + m[9] * n.y + m[10] * n.z);
+    const f3 P = view(x, y, ld(x, y));
+    auto plane = [&](int i, int j) {
+        const f3 q = view(i, j, ld(i, j));
+        return fabsf(dot(normalize(P - q), nv));
+    };
+    const float dx = hmin(plane(x + 1, y), plane(x - 1, y));
+    const float dy = hmin(plane(x, y + 1), plane(x, y - 1));
+    mask[(size_t)y * W + x] = (dx <= 0.1f && dy <= 0.1f) ? 1u : 0u;
+}
+
+// ---------------------------------------------------------------------- BinaryDilation
+// BinaryDilation.ps.slang:13-43: OP (min / max) over five Gather footprints (2x2 texels each):
+// the centre and four at (+-0.5, +-1.5) px offsets (a radius-2 ring).  Gather's footprint is the
+// bilinear footprint of the sample position (librsd's 8-bit sub-texel quantization), wrap
+// addressing (the unbound sampler S: Falcor's default).
+__device__ __forceinline__ uint32_t gather_op(const uint8_t* __restrict__ t, int W, int H, float u, float v, bool mx) {
+    const float x = u * (float)W - 0.5f, y = v * (float)H - 0.5f;
+    const float fx0 = floorf(x), fy0 = floorf(y);
+    const float qx = floorf((x - fx0) * 256.0f + 0.5f), qy = floorf((y - fy0) * 256.0f + 0.5f);
+    int ix = (int)fx0, iy = (int)fy0;
+    if (qx >= 256.0f) ix += 1;
+    if (qy >= 256.0f) iy += 1;
+    const int x0 = wrap_addr(ix, W), x1 = wrap_addr(ix + 1, W), y0 = wrap_addr(iy, H), y1 = wrap_addr(iy + 1, H);
+    const uint32_t a = t[(size_t)y1 * W + x0], b = t[(size_t)y1 * W + x1], c = t[(size_t)y0 * W + x1],
+                   d = t[(size_t)y0 * W + x0];  // Gather order w, z, ... (irrelevant to min / max)
+    return mx ? max(max(a, b), max(c, d)) : min(min(a, b), min(c, d));
+}
+
+__global__ void __launch_bounds__(kPostW * kPostH) binary_dilation_kernel(const uint8_t* __restrict__ in, int W, int H,
+                                                                           uint32_t opMax, uint8_t* __restrict__ out) {
+    const int x = (int)(blockIdx.x * kPostW + threadIdx.x), y = (int)(blockIdx.y * kPostH + threadIdx.y);
+    if (x >= W || y >= H) return;
+    const bool mx = opMax != 0u;
+    const float u = ((float)x + 0.5f) / (float)W, v = ((float)y + 0.5f) / (float)H;
+    const float dx = 0.5f / (float)W, dy = 0.5f / (float)H;
+    auto op = [&](uint32_t p, uint32_t q) { return mx ? max(p, q) : min(p, q); };
+    uint32_t r0 = gather_op(in, W, H, u + dx, v + 3.0f * dy, mx);
+    const uint32_t r1 = gather_op(in, W, H, u + 3.0f * dx, v + -dy, mx);
+    const uint32_t r2 = gather_op(in, W, H, u + -dx, v + -3.0f * dy, mx);
+    const uint32_t r3 = gather_op(in, W, H, u + -3.0f * dx, v + dy, mx);
+    r0 = op(r0, gather_op(in, W, H, u, v, mx));
+    out[(size_t)y * W + x] = (uint8_t)op(op(r0, r1), op(r2, r3));
+}
+
 // ---------------------------------------------------------------------- TemporalAO
 // TemporalAO.ps.slang:55-101 (TemporalAO.cpp:113-163, enabled): reproject the previous frame's
 // AO along the motion vector, reject on a > 10 % relative depth change (or a stable-mask pixel),
@@ -523,6 +588,33 @@ extern "C" rsd_status rsd_cross_bilateral_blur(const uint8_t* d_src, const float
         if (e != hipSuccess) return hip_fail(e, "blur_kernel launch");
     }
     return RSD_OK;
+}
+
+extern "C" rsd_status rsd_ao_flicker_mask(const float* d_linear_z, const float* d_normal_w, uint32_t width,
+                                          uint32_t height, const rsd_camera* cam, uint8_t* d_mask, rsd_stream stream) {
+    if (!d_linear_z || !d_normal_w || !cam || !d_mask || width == 0 || height == 0) {
+        set_error("rsd_ao_flicker_mask: invalid argument");
+        return RSD_ERR_INVALID_ARG;
+    }
+    const float isx = 0.5f * (cam->frameWidth / cam->focalLength), isy = 0.5f * (cam->frameHeight / cam->focalLength);
+    const dim3 grid((width + kPostW - 1) / kPostW, (height + kPostH - 1) / kPostH);
+    hipLaunchKernelGGL(flicker_mask_kernel, grid, dim3(kPostW, kPostH), 0, (hipStream_t)stream, d_linear_z,
+                       reinterpret_cast<const float4*>(d_normal_w), (int)width, (int)height, *cam, isx, isy, d_mask);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? RSD_OK : hip_fail(e, "flicker_mask_kernel launch");
+}
+
+extern "C" rsd_status rsd_binary_dilation(const uint8_t* d_in, uint32_t width, uint32_t height, uint32_t op_max,
+                                          uint8_t* d_out, rsd_stream stream) {
+    if (!d_in || !d_out || width == 0 || height == 0 || op_max > 1u || d_in == d_out) {
+        set_error("rsd_binary_dilation: invalid argument (op_max 0 = min, 1 = max; no in-place)");
+        return RSD_ERR_INVALID_ARG;
+    }
+    const dim3 grid((width + kPostW - 1) / kPostW, (height + kPostH - 1) / kPostH);
+    hipLaunchKernelGGL(binary_dilation_kernel, grid, dim3(kPostW, kPostH), 0, (hipStream_t)stream, d_in, (int)width,
+                       (int)height, op_max, d_out);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? RSD_OK : hip_fail(e, "binary_dilation_kernel launch");
 }
 
 extern "C" rsd_status rsd_taa(const float* d_color_in, const float* d_mvec, const float* d_prev_color, uint32_t width,

@@ -123,7 +123,7 @@ GRAPH_EXPORTS = ["rsd_graph_create", "rsd_graph_destroy", "rsd_graph_create_pass
                  "rsd_graph_get_dict_int", "rsd_graph_pass_count", "rsd_plugin_set_dir", "rsd_plugin_types",
                  "rsd_cross_bilateral_blur", "rsd_image_equation_compile", "rsd_image_equation_info",
                  "rsd_image_equation_run", "rsd_image_equation_release", "rsd_temporal_ao",
-                 "rsd_motion_vectors", "rsd_taa"]
+                 "rsd_motion_vectors", "rsd_taa", "rsd_ao_flicker_mask", "rsd_binary_dilation"]
 
 FMT_R32F, FMT_RG32F, FMT_RGBA32F, FMT_R16U, FMT_R8U, FMT_R8UNORM, FMT_R32U, FMT_UNKNOWN = range(8)
 FMT_R16F, FMT_RG16F, FMT_RGBA16F = 8, 9, 10
@@ -240,6 +240,10 @@ def lib():
         L.rsd_cross_bilateral_blur.argtypes = [vp, vp, u32, u32, vp, vp, u32, u32, u32, u32, u32, vp]
         L.rsd_temporal_ao.restype = st
         L.rsd_temporal_ao.argtypes = [vp, vp, vp, vp, vp, vp, vp, u32, u32, u32, C.POINTER(Camera), vp, vp, vp, vp]
+        L.rsd_ao_flicker_mask.restype = st
+        L.rsd_ao_flicker_mask.argtypes = [vp, vp, u32, u32, C.POINTER(Camera), vp, vp]
+        L.rsd_binary_dilation.restype = st
+        L.rsd_binary_dilation.argtypes = [vp, u32, u32, u32, vp, vp]
         L.rsd_taa.restype = st
         L.rsd_taa.argtypes = [vp, vp, vp, u32, u32, f32, f32, u32, vp, vp]
         L.rsd_motion_vectors.restype = st

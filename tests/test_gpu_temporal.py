@@ -220,3 +220,81 @@ def test_graph_taa_after_temporal_chain(torch, oracle):
     g.close()
     gs.release()
     dev.close()
+
+
+def test_flicker_mask_and_dilation_parity(torch, oracle):
+    from rsd import abi
+    from rsd.frame import FrameConfig, look_at
+    rng = np.random.default_rng(11)
+    H, W = 70, 110
+    cfg = FrameConfig(visible_w=W, visible_h=H, guard_band=0)
+    cam = look_at([0.3, 2.0, 8.0], [0.0, 1.0, 0.0], [0.0, 1.0, 0.0], cfg)
+    z = (4.0 + np.cumsum(rng.normal(0, 0.05, (H, W)), axis=1)).astype(F)
+    z[:, 40:] += 3.0  # a depth step
+    z[5:9, 5:9] = z[5:9, 5:9][::-1]  # a flipped patch
+    n = rng.normal(0, 1, (H, W, 4)).astype(F)
+    n[..., :3] /= np.linalg.norm(n[..., :3], axis=-1, keepdims=True)
+    n[::3, ::3, :3] = [0.0, 0.0, 1.0]
+    dz, dn = torch.from_numpy(z).cuda(), torch.from_numpy(n).cuda()
+    mask = torch.full((H, W), 7, dtype=torch.uint8, device="cuda")
+    s = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    abi.check(abi.lib().rsd_ao_flicker_mask(_p(dz), _p(dn), W, H, C.byref(cam), _p(mask), s), "rsd_ao_flicker_mask")
+    torch.cuda.synchronize()
+    want = oracle.ao_flicker_mask(z, n, to_oracle(cam, oracle.Camera))
+    got = mask.cpu().numpy()
+    assert np.array_equal(got, want)
+    assert 0 < got.sum() < got.size
+    for op in (0, 1):
+        out = torch.zeros_like(mask)
+        abi.check(abi.lib().rsd_binary_dilation(_p(mask), W, H, op, _p(out), s), "rsd_binary_dilation")
+        torch.cuda.synchronize()
+        assert np.array_equal(out.cpu().numpy(), oracle.binary_dilation(want, "max" if op else "min")), op
+    assert abi.lib().rsd_binary_dilation(_p(mask), W, H, 0, _p(mask), s) == abi.ERR_INVALID_ARG  # no in-place
+
+
+def test_graph_temporal_ao_with_stable_mask(torch, oracle):
+    """scripts/SVAO.py's stable mask: AOFlickerMask -> BinaryDilation(min) -> TemporalAO.stableMask
+    (useStableMask), three poses, bit-exact against the oracle chain on the graph's own inputs."""
+    from conftest import ROOT
+    from rsd import graph as rg
+    from rsd.frame import Device, GpuScene, look_at
+    from rsd.scenes import make_scene
+    from rsd.temporal import prev_view_to_cur_view
+    cfg = small_frame_config()
+    scene = make_scene("arcade_tiny")
+    dev = Device(0)
+    gs = GpuScene(dev, scene)
+    g = rg.load_script(ROOT / "tests" / "graphs" / "svao_temporal_mask.py")["SVAOTemporalMask"]
+    pos0, tgt0 = np.array(scene.camera["pos"]), np.array(scene.camera["target"])
+    prev_cam, o_prev = None, None
+    G = 16
+    hw = (cfg.fb_h, cfg.fb_w)
+    for i in range(3):
+        step = np.array([0.03, 0.0, 0.0]) * i
+        cam = look_at((pos0 + step).tolist(), (tgt0 + step).tolist(), scene.camera["up"], cfg)
+        g.set_scene(gs.h, cam)
+        if i == 0:
+            g.compile(cfg.fb_w, cfg.fb_h)
+        g.execute()
+        torch.cuda.synchronize()
+        z = g.output_tensor("LinearizeDepth.linearDepth").cpu().numpy().reshape(hw)
+        blurred = g.output_tensor("CrossBilateralBlur0.colorOut").cpu().numpy().reshape(hw)
+        mv = g.output_tensor("GBufferRaster.mvec").cpu().numpy().reshape(hw + (2,))
+        mask = g.output_tensor("AOFlickerMask.mask").cpu().numpy().reshape(hw)
+        dil = g.output_tensor("BinaryDilation.output").cpu().numpy().reshape(hw)
+        ao = g.output_tensor("TemporalAO.aoOut").cpu().numpy().reshape(hw)
+        oc = to_oracle(cam, oracle.Camera)
+        nrm = g.output_tensor("GBufferRaster.faceNormalW").cpu().numpy().reshape(hw + (4,))
+        assert np.array_equal(mask, oracle.ao_flicker_mask(z, nrm, oc)), i
+        assert np.array_equal(dil, oracle.binary_dilation(mask, "min")), i
+        assert 0 < dil.sum() < dil.size
+        if o_prev is None:
+            o_prev = (np.zeros_like(z), np.zeros_like(blurred), np.zeros_like(blurred))
+        want, want_n = oracle.temporal_ao(blurred, z, mv, *o_prev, oc, prev_view_to_cur_view(cam, prev_cam or cam), G,
+                                          stable_mask=dil)
+        assert np.array_equal(ao[G:-G, G:-G], want[G:-G, G:-G]), i
+        o_prev = (z, want, want_n)
+        prev_cam = cam
+    g.close()
+    gs.release()
+    dev.close()

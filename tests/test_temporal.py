@@ -123,3 +123,38 @@ def test_taa_first_frame_and_clamp(oracle):
     a = oracle.taa(c, mv, prev, color_box_sigma=100.0, anti_flicker=False)
     b = oracle.taa(c, np.zeros_like(mv), c, color_box_sigma=100.0, anti_flicker=False)
     assert np.abs(a - b).max() < 1e-5
+
+
+def test_flicker_mask_plane_and_edge(oracle):
+    """A fronto-parallel plane is stable everywhere inside; a depth step makes the pixels next to
+    it unstable only where neither neighbour of an axis lies in the plane."""
+    H, W = 32, 48
+    c = oracle.camera_look_at((0.0, 0.0, 0.0), (0.0, 0.0, -1.0), (0.0, 1.0, 0.0), aspect=W / H)
+    z = np.full((H, W), 5.0, F)
+    n = np.zeros((H, W, 4), F)
+    n[..., 2] = 1.0  # world +z = towards the camera (view space +z)
+    m = oracle.ao_flicker_mask(z, n, c)
+    assert (m[1:-1, 1:-1] == 1).all()
+    z2 = z.copy()
+    z2[:, 24:] = 9.0
+    m2 = oracle.ao_flicker_mask(z2, n, c)
+    assert (m2[1:-1, 1:23] == 1).all() and (m2[1:-1, 25:-1] == 1).all()  # one in-plane neighbour suffices
+    z3 = z.copy()
+    z3[:, ::2] = 9.0  # alternating columns: no in-plane neighbour in x
+    assert (oracle.ao_flicker_mask(z3, n, c)[1:-1, 1:-1] == 0).all()
+
+
+def test_binary_dilation_ring(oracle):
+    """min spreads a single 0 over the gather footprints around it; max spreads a single 1; a
+    uniform mask is unchanged; wrap addressing at the border."""
+    H, W = 20, 20
+    ones = np.ones((H, W), np.uint8)
+    assert (oracle.binary_dilation(ones, "min") == 1).all()
+    hole = ones.copy()
+    hole[10, 10] = 0
+    d = oracle.binary_dilation(hole, "min")
+    assert d[10, 10] == 0 and 4 <= (d == 0).sum() <= 25 and d[0, 0] == 1
+    dot = np.zeros((H, W), np.uint8)
+    dot[0, 0] = 1
+    dm = oracle.binary_dilation(dot, "max")
+    assert dm[0, 0] == 1 and dm[H - 1, W - 1] == 1  # wraps around the corner
