@@ -1519,21 +1519,12 @@ static hipError_t launch_sd_kn(const SDArgs& a, dim3 grid, uint32_t persistentBl
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const dim3 pg(persistentBlocks), wb(kBlock);
-    static const char* row16Env = std::getenv("RSD_TRACE_ROW16");  // experiments: 16 lanes per ray
-    if (walk == 2 && row16Env && *row16Env == '1' && !a.counters) {
-        hipLaunchKernelGGL((sd_trace_row_kernel<K, N, 16, true, false>), pg, wb, 0, s, a, queue, qctl, keys);
-        if ((e = hipGetLastError()) != hipSuccess) return e;
-        hipLaunchKernelGGL((sd_resolve_row_kernel<K, N, 16>), pg, wb, 0, s, a, queue, qctl, keys);
-    } else if (walk == 2) {
+    if (walk == 2) {
         if (a.counters) hipLaunchKernelGGL((sd_trace_row_kernel<K, N, ROW, true, true>), pg, wb, 0, s, a, queue, qctl, keys);
         else if (pool == 128) hipLaunchKernelGGL((sd_trace_row_kernel<K, N, ROW, true, false, 128>), pg, wb, 0, s, a, queue, qctl, keys);
         else hipLaunchKernelGGL((sd_trace_row_kernel<K, N, ROW, true, false>), pg, wb, 0, s, a, queue, qctl, keys);
         if ((e = hipGetLastError()) != hipSuccess) return e;
-        // resolve rows: RSD_RESOLVE_WAVES_PER_CU (experiments) scales the persistent grid
-        static const char* rwEnv = std::getenv("RSD_RESOLVE_WAVES_PER_CU");
-        const uint32_t rb = rwEnv ? std::max(1u, persistentBlocks * (uint32_t)std::max(1, std::atoi(rwEnv)) / 8u)
-                                  : persistentBlocks;
-        hipLaunchKernelGGL((sd_resolve_row_kernel<K, N, ROW>), dim3(rb), wb, 0, s, a, queue, qctl, keys);
+        hipLaunchKernelGGL((sd_resolve_row_kernel<K, N, ROW>), pg, wb, 0, s, a, queue, qctl, keys);
     } else if (walk == 3) {
         hipLaunchKernelGGL((sd_trace_ordered_kernel<N>), pg, wb, 0, s, a, queue, qctl);
     } else if (walk == 4) {

@@ -38,28 +38,8 @@ __global__ void clear_intervals_kernel(uint32_t* rmin, uint32_t* rmax, uint32_t 
 }
 
 // SVAORaster.ps.slang:29-122, [numthreads(16,16,1)] with the 2x2 group interleave
-#ifndef RSD_P1_UNROLL
-#define RSD_P1_UNROLL 1
-#endif
-#ifndef RSD_P1_XCD
-#define RSD_P1_XCD 0
-#endif
-#ifndef RSD_P1_PIPE
-#define RSD_P1_PIPE 0
-#endif
 __global__ void __launch_bounds__(256) svao_pass1_kernel(SvaoArgs a) {
-#if RSD_P1_XCD
-    // XCD-aware order: the hardware deals consecutive workgroups round-robin to the 8 XCDs;
-    // remap so that XCD k gets the k-th contiguous eighth of the tile rows (its L2 then holds
-    // the depth / normal rows its tiles share).  Only which workgroup computes which pixels
-    // changes, so the results are the same bits.
-    const uint32_t nb = gridDim.x * gridDim.y;
-    uint32_t lin = blockIdx.y * gridDim.x + blockIdx.x;
-    if (nb % 8u == 0u) lin = (lin % 8u) * (nb / 8u) + lin / 8u;
-    const uint32_t bx = lin % gridDim.x, by = lin / gridDim.x;
-#else
     const uint32_t bx = blockIdx.x, by = blockIdx.y;
-#endif
     const uint32_t ox = (bx / 2u) * 32u + 2u * threadIdx.x + (bx % 2u);
     const uint32_t oy = ((by / 2u) * a.bandCount + a.bandIndex) * 32u + 2u * threadIdx.y + (by % 2u);
     const uint32_t px = ox + a.guard, py = oy + a.guard;
@@ -72,42 +52,18 @@ __global__ void __launch_bounds__(256) svao_pass1_kernel(SvaoArgs a) {
     if (!basic_init(a, u, v, b)) {
         ao = 1.0f;
     } else {
-#if RSD_P1_PIPE
-        // software pipeline: direction i + 1's sample geometry and its raster depth fetch are
-        // issued before direction i is evaluated (same operations, same bits)
-        Sample sn;
-        bool ssrN = false;
-        bool validN = sample_init(a, u, v, b, 0, sn, ssrN);
-        float zN = validN ? depth_center(a, sn.ru, sn.rv, sn.kx, sn.ky) : 0.0f;
-#endif
-#pragma unroll RSD_P1_UNROLL
+#pragma unroll 1
         for (int i = 0; i < 8; ++i) {
             Sample s;
             bool ssrAbove;
-#if RSD_P1_PIPE
-            s = sn;
-            ssrAbove = ssrN;
-            const bool valid = validN;
-            const float zc = zN;
-            if (i + 1 < 8) {
-                validN = sample_init(a, u, v, b, i + 1, sn, ssrN);
-                zN = validN ? depth_center(a, sn.ru, sn.rv, sn.kx, sn.ky) : 0.0f;
-            }
-            if (!valid) continue;
-#else
             if (!sample_init(a, u, v, b, i, s, ssrAbove)) continue;
-#endif
             if (fabsf(u - s.ru) < d.invResolution[0] * 0.9f && fabsf(v - s.rv) < d.invResolution[1] * 0.9f) {
                 ao += div_pdf(s.sphereStart - s.sphereEnd, s);  // isSamePixel
                 continue;
             }
             // SVAORaster.ps.slang:62-66: Raytraced mode with TRACE_OUT_OF_SCREEN (SVAO.h:104)
             bool forceRay = a.secondary == 3u && !s.isInScreen;
-#if RSD_P1_PIPE
-            add_sample(a, b, s, uv_to_view(a, s.ru, s.rv, zc), true);  // eval_primary with the prefetched depth
-#else
             eval_primary(a, b, s);
-#endif
             ao += s.visibility;
             if (!s.isInScreen && d.sdGuard > 0) {
                 forceRay = true;
