@@ -57,6 +57,15 @@ def main():
 
     out["all_us"] = keep(live)
     out["none_us"] = keep(live[:0])
+    if "--tail" in sys.argv:  # drop the rays with the longest intervals: is the launch tail-bound?
+        lo = full[0].flatten()[live].view(torch.float32)
+        hi = full[1].flatten()[live].view(torch.float32)
+        order = torch.argsort(hi - lo, descending=True)
+        for frac in (0.001, 0.01, 0.05, 0.2):
+            k = int(live.numel() * frac)
+            out[f"drop_longest_{frac}"] = keep(live[order[k:]])
+            out[f"drop_random_{frac}"] = keep(live[torch.randperm(live.numel(), device=live.device)[k:]])
+        # rows of the queue in dequeue order: the longest rays first vs last (queue order = tile order)
     if "--counters" in sys.argv:  # instrumented trace: per-ray chain statistics (s_memtime cycles)
         def cnt(idx):
             keep(idx)
