@@ -39,8 +39,9 @@ namespace rsd {
 // ------------------------------------------------------------------------------------
 // queue-control words of one trace: {count[32], head[32]} of the live-ray queue partitions, the
 // raster walk's live-tile count, spare
-constexpr int kQctlWords = 2 * (int)kQueueParts + 32;
+constexpr int kQctlWords = 3 * (int)kQueueParts + 32;
 constexpr int kQctlLiveTiles = 2 * (int)kQueueParts;
+constexpr int kQctlShort = 2 * (int)kQueueParts + 32;  // lpt: short-ray counts (filled from the partition's end)
 constexpr int kSetupWaves = 4;  // sd_setup_kernel: tiles (waves) per workgroup
 
 struct SDArgs {
@@ -87,7 +88,18 @@ struct SDArgs {
     float projU[3], projV[3], projW[3];  // U / |U|^2, V / |V|^2, W / |W|^2
     float camWn[3];                      // normalize(W): view depth of a point = dot(P - o, Wn)
     float wClip;                         // near clip in projW units below every valid hit
+    // longest-first queue (fused row walk): rays with TMax - TMin > lptLen go to the front of their
+    // partition, the others to its back, so the expensive rays are dequeued first
+    uint32_t lpt;
+    float lptLen;
 };
+
+// queue slot of the qi-th ray of partition part (lpt: the long rays [0, nLong) from the front, the
+// short ones from the back)
+__device__ __forceinline__ uint32_t queue_slot(const SDArgs& a, uint32_t part, uint32_t qi, uint32_t nLong) {
+    const uint32_t base = part * a.partCap;
+    return (!a.lpt || qi < nLong) ? base + qi : base + a.partCap - 1u - (qi - nLong);
+}
 
 // Per-column and per-row terms of initRayDesc, evaluated once per frame size with exactly the
 // operations sd_ray used to evaluate per texel (so the bits are unchanged):
@@ -500,10 +512,26 @@ __global__ void __launch_bounds__(kSetupWaves * kBlock) sd_setup_kernel(SDArgs a
     // with its own counter: one counter word serialises ~90 atomics/us.
     const uint32_t lin = blockIdx.y * (uint32_t)tilesX + (uint32_t)tileX;
     const uint32_t part = lin % kQueueParts;
-    uint32_t base = 0;
-    if (lane == 0 && n) base = atomicAdd(&qctl[part], n);
-    base = __shfl(base, 0);
-    const uint32_t slot = part * a.partCap + base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+    uint32_t slot;
+    if (a.lpt) {
+        // lptLen > 0: absolute interval length; < 0: relative to TMin
+        const bool isLong = live && TMax - TMin > (a.lptLen >= 0.0f ? a.lptLen : -a.lptLen * TMin);
+        const unsigned long long ml = __ballot(isLong), ms = m & ~ml;
+        const uint32_t nl = (uint32_t)__popcll(ml), ns = (uint32_t)__popcll(ms);
+        uint32_t bl = 0, bs = 0;
+        if (lane == 0 && nl) bl = atomicAdd(&qctl[part], nl);
+        if (lane == 0 && ns) bs = atomicAdd(&qctl[kQctlShort + part], ns);
+        bl = __shfl(bl, 0);
+        bs = __shfl(bs, 0);
+        const unsigned long long below = (1ull << lane) - 1ull;
+        slot = isLong ? part * a.partCap + bl + (uint32_t)__popcll(ml & below)
+                      : part * a.partCap + a.partCap - 1u - (bs + (uint32_t)__popcll(ms & below));
+    } else {
+        uint32_t base = 0;
+        if (lane == 0 && n) base = atomicAdd(&qctl[part], n);
+        base = __shfl(base, 0);
+        slot = part * a.partCap + base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+    }
     if (live) {
         queue[2u * slot] = make_float4(d.x, d.y, d.z, TMin);
         queue[2u * slot + 1u] = make_float4(TMax, cosT, __uint_as_float((uint32_t)y * (uint32_t)a.sdW + x), 0.0f);
@@ -543,8 +571,9 @@ __global__ void __launch_bounds__(kBlock) sd_trace_queue_kernel(SDArgs a, const 
     const int q = lane & 3, quad = lane >> 2, quadBase = lane & ~3;
     // wave w serves partition w % kQueueParts (gridDim.x is a multiple of kQueueParts)
     const uint32_t part = blockIdx.x % kQueueParts, wavesPerPart = gridDim.x / kQueueParts;
-    const uint32_t count = __hip_atomic_load(&qctl[part], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const uint32_t slot0 = part * a.partCap;
+    const uint32_t nLong = __hip_atomic_load(&qctl[part], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t count = nLong + (a.lpt ? __hip_atomic_load(&qctl[kQctlShort + part], __ATOMIC_RELAXED,
+                                                               __HIP_MEMORY_SCOPE_AGENT) : 0u);
     TraceStats st{0u, 0u, 0u};
     uint32_t active = 0, hitsDelivered = 0, maxNodes = 0, maxSteps = 0;
     unsigned long long sumCycles = 0, maxCycles = 0;
@@ -555,7 +584,7 @@ __global__ void __launch_bounds__(kBlock) sd_trace_queue_kernel(SDArgs a, const 
             f3 d;
             float TMin, TMax, cosT;
             uint32_t idx;
-            ray_rec_load(queue, slot0 + qi, d, TMin, TMax, cosT, idx);
+            ray_rec_load(queue, queue_slot(a, part, qi, nLong), d, TMin, TMax, cosT, idx);
             const int x = (int)(idx % (uint32_t)a.sdW), y = (int)(idx / (uint32_t)a.sdW);
             float depths[N];
             const float DEFAULT = a.normalize ? 1.0f : 3.40282347e+37f;
@@ -1068,8 +1097,9 @@ __global__ void __launch_bounds__(kBlock) sd_trace_row_kernel(SDArgs a, const fl
     uint32_t* pItem = sItem + row * POOL;
     float* pT = sT + row * POOL;
     const uint32_t part = blockIdx.x % kQueueParts, wavesPerPart = gridDim.x / kQueueParts;
-    const uint32_t count = __hip_atomic_load(&qctl[part], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const uint32_t slot0 = part * a.partCap;
+    const uint32_t nLong = __hip_atomic_load(&qctl[part], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t count = nLong + (a.lpt ? __hip_atomic_load(&qctl[kQctlShort + part], __ATOMIC_RELAXED,
+                                                               __HIP_MEMORY_SCOPE_AGENT) : 0u);
     const rsd_camera& c = a.cam;
     const float DEFAULT = a.normalize ? 1.0f : 3.40282347e+37f;  // Common.slangh:16
     const int soft = a.poolSoft;
@@ -1115,7 +1145,7 @@ __global__ void __launch_bounds__(kBlock) sd_trace_row_kernel(SDArgs a, const fl
             if (qi >= count) {
                 phase = kExit;
             } else {
-                slot = slot0 + qi;
+                slot = queue_slot(a, part, qi, nLong);
                 f3 d;
                 uint32_t idx;
                 ray_rec_load(queue, slot, d, TMin, TMax, cosT, idx);
@@ -1757,6 +1787,8 @@ rsd_status sd_trace_impl(rsd_scene* scene, const rsd_camera* cam, const rsd_sd_p
     if (p->ray_interval && d_ray_min && cosLower > 1e-3 && (double)cam->farZ / (0.5 * cosLower) < 1e37)
         a.deadFast = 1u;
     a.raster = 0u;
+    a.lpt = 0u;
+    a.lptLen = 0.0f;
     a.primRec = scene->d_prim_rec;
     a.alphaData = scene->alpha;
     a.alphaData.spread = rsd_ray_cone_spread(cam->focalLength, sd_h);  // default texture dims = SD map
@@ -1860,6 +1892,14 @@ rsd_status sd_trace_impl(rsd_scene* scene, const rsd_camera* cam, const rsd_sd_p
     // pass; RSD_TRACE_WALK=split keeps the key-list + resolve-kernel variant for A/B runs
     const int walk = p->hit_order == RSD_HIT_ORDER_TRAVERSAL ? 3 : raster ? 4 : !rowWalk ? 0
                      : (split && walkName == "split") ? 2 : 1;
+    if (walk == 1 || walk == 0) {
+        // longest-first queue: rays whose interval exceeds 0.1 x TMin are dequeued first (configs[1]:
+        // 90 -> 84 us); RSD_TRACE_LPT = off | a threshold (> 0 absolute, < 0 relative to TMin)
+        const char* lptEnv = std::getenv("RSD_TRACE_LPT");
+        const bool off = lptEnv && std::string(lptEnv) == "off";
+        a.lpt = off ? 0u : 1u;
+        a.lptLen = lptEnv && *lptEnv && !off ? (float)std::atof(lptEnv) : -0.1f;
+    }
     if (walk == 4) {
         const uint32_t tilesW = (sd_w + kTile - 1) / kTile, tilesH = (sd_h + kTile - 1) / kTile;
         const size_t slotBytes = (size_t)sd_w * sd_h * 4, tileBytes = (size_t)tilesW * tilesH * 8;
