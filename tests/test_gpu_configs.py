@@ -168,3 +168,35 @@ def test_camera_path_frames_in_flight():
         assert bits_equal(out[i]["sd"], ref[i]["sd"]), i
     assert not np.array_equal(ref[0]["ao"], ref[3]["ao"])  # the poses differ
     r.close()
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("walk", ["fused", "quad"])
+def test_longest_first_queue_same_bits(monkeypatch, walk):
+    """The longest-first live-ray queue (default) only reorders the work: the SD map equals the
+    single-ended queue's (RSD_TRACE_LPT=off) and an absolute-threshold split's, bit for bit."""
+    import torch
+    from rsd.frame import CONFIGS, FrameConfig, Renderer
+    from rsd.scenes import make_scene
+    kw, name = CONFIGS["suntemple_1080p_q"]
+    r = Renderer(make_scene(name), FrameConfig(**kw))
+    r.gbuffer()
+    r.clear_intervals()
+    r.pass1()
+    torch.cuda.synchronize()
+    iv = r.ray_minmax.clone()
+    maps = []
+    for lpt in ("off", None, "2.0", "-0.5"):
+        monkeypatch.setenv("RSD_TRACE_WALK", walk)
+        if lpt is None:
+            monkeypatch.delenv("RSD_TRACE_LPT", raising=False)
+        else:
+            monkeypatch.setenv("RSD_TRACE_LPT", lpt)
+        r.ray_minmax.copy_(iv)
+        r.sd.zero_()
+        r.sd_trace()
+        torch.cuda.synchronize()
+        maps.append(r.sd.cpu().numpy().view(np.uint32).copy())
+    for m in maps[1:]:
+        assert np.array_equal(m, maps[0])
+    r.close()
