@@ -173,6 +173,7 @@ __global__ void __launch_bounds__(kP2Lanes) svao_pass2_kernel(SvaoArgs a) {
     __shared__ uint16_t sFirst[L];     // first pair of each slot
     __shared__ float sAcc[L];          // running vis of each slot
     __shared__ float sP[L], sR[L];
+    __shared__ Basic sBasic[L];        // the pixel's BasicAOData, evaluated once per pixel, not per pair
     __shared__ uint32_t sNPix, sNPair;
     const uint32_t tid = threadIdx.x;
     const rsd_vao_data& d = a.d;
@@ -194,6 +195,12 @@ __global__ void __launch_bounds__(kP2Lanes) svao_pass2_kernel(SvaoArgs a) {
             uint32_t j = base;
             for (int i = 0; i < 8; ++i)
                 if (m & (1u << i)) sPair[j++] = (uint16_t)(slot << 3 | i);
+            // a non-zero stencil means pass 1's basic_init of this pixel succeeded (same bits)
+            const float u = ((float)px + 0.5f) * d.invResolution[0];
+            const float v = ((float)py + 0.5f) * d.invResolution[1];
+            Basic b;
+            basic_init(a, u, v, b);
+            sBasic[slot] = b;
         }
     }
     __syncthreads();
@@ -207,8 +214,7 @@ __global__ void __launch_bounds__(kP2Lanes) svao_pass2_kernel(SvaoArgs a) {
             const uint32_t lp = sPix[slot] & 255u;
             const float u = ((float)(x0 + lp % T) + 0.5f) * d.invResolution[0];
             const float v = ((float)(y0 + lp / T) + 0.5f) * d.invResolution[1];
-            Basic b;
-            basic_init(a, u, v, b);
+            const Basic b = sBasic[slot];
             float p, r;
             svao_pass2_dir<N>(a, b, u, v, (int)(e & 7u), p, r);
             sP[tid] = p;
