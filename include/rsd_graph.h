@@ -80,6 +80,14 @@ rsd_status rsd_cross_bilateral_blur(const uint8_t* d_src, const float* d_linear_
                                     uint8_t* d_pingpong, uint8_t* d_dst, uint32_t width, uint32_t height,
                                     uint32_t guard_band, uint32_t kernel_radius, uint32_t better_slope,
                                     rsd_stream stream);
+/* DeinterleaveTexture (Deinterleave.slang, DeinterleaveTexture.cpp:143-158): a width x height
+ * texture of texel_bytes-byte texels -> 16 layers of ceil(width/4) x ceil(height/4), layer
+ * (dy * 4 + dx) holding src[4y + dy][4x + dx] (0 outside the source).  InterleaveTexture
+ * (Interleave.slang): the inverse, width x height (the full-size image) from the 16 layers. */
+rsd_status rsd_deinterleave(const void* d_src, uint32_t width, uint32_t height, uint32_t texel_bytes, void* d_dst,
+                            rsd_stream stream);
+rsd_status rsd_interleave(const void* d_src, uint32_t width, uint32_t height, uint32_t texel_bytes, void* d_dst,
+                          rsd_stream stream);
 /* AOFlickerMask (AOFlickerMask.cpp:73-86, AOFlickerMask.ps.slang:43-63): 1 where the pixel's
  * x and y neighbours lie in its view-space normal plane (|dot| <= 0.1), else 0 (R8Uint).
  * d_normal_w: world-space normals, RGBA32F (GBufferRaster.faceNormalW). */

@@ -373,6 +373,15 @@ void RenderGraph::compile(Context& ctx, uint32_t width, uint32_t height, bool al
                 f.height = ext->second->height;
                 f.layers = ext->second->layers;
             }
+            if (f.fromFormatOnly) {
+                f.width = f.height = 0;
+                f.layers = 1;
+            } else if (f.shrink > 1 || f.layersOut) {
+                const uint32_t w = f.width ? f.width : width, h = f.height ? f.height : height;
+                f.width = (w + f.shrink - 1) / f.shrink;
+                f.height = (h + f.shrink - 1) / f.shrink;
+                if (f.layersOut) f.layers = f.layersOut;
+            }
         }
     }
     for (auto& [key, f] : outs) {

@@ -74,6 +74,10 @@ struct Field {
     uint32_t width = 0, height = 0;  // 0: the graph's default dims
     uint32_t layers = 1;
     std::string formatFrom;  // output: copy format and size from this input's producer (Switch)
+    // with formatFrom: divide the copied size by this (rounding up) and set the layer count
+    // (DeinterleaveTexture: 4, 16 layers); fromFormatOnly: copy the format only (InterleaveTexture)
+    uint32_t shrink = 1, layersOut = 0;
+    bool fromFormatOnly = false;
 };
 
 struct Reflection {

@@ -17,6 +17,8 @@
 //   TAA                   TAA.cpp                    rsd_taa
 //   AOFlickerMask         AOFlickerMask.cpp          rsd_ao_flicker_mask
 //   BinaryDilation        BinaryDilation.cpp         rsd_binary_dilation
+//   DeinterleaveTexture   DeinterleaveTexture.cpp    rsd_deinterleave (16 layers of 1/4 x 1/4)
+//   InterleaveTexture     InterleaveTexture.cpp      rsd_interleave
 //
 // Every other pass type of the reference scripts (ToneMapper, ForwardLighting, ...)
 // is outside the hot path; it resolves to a stub that declares whatever fields
@@ -803,6 +805,56 @@ private:
     bool opMax_;
 };
 
+// ------------------------------------------------------------------------------ (De)interleave
+// DeinterleaveTexture.cpp:80-158: texIn -> texOut, a 16-layer array of ceil(w/4) x ceil(h/4) in the
+// input's format (depth formats arrive as R32Float here).  InterleaveTexture.cpp:62-110: the
+// inverse, output in the input's format at the graph's default size.
+class DeinterleaveTexturePass : public RenderPass {
+public:
+    explicit DeinterleaveTexturePass(const Properties& p) { props_ = p; }
+    Reflection reflect(const CompileData&) override {
+        Reflection r;
+        r.addInput("texIn", "texture 2D");
+        Field& o = r.addOutput("texOut", "texture 2D array");
+        o.formatFrom = "texIn";
+        o.shrink = 4;
+        o.layersOut = 16;
+        return r;
+    }
+    void execute(Context& ctx, const RenderData& rd) override {
+        Texture* in = rd["texIn"];
+        Texture* out = rd["texOut"];
+        if (in->layers != 1 || out->layers != 16 || out->format != in->format ||
+            out->width != (in->width + 3) / 4 || out->height != (in->height + 3) / 4)
+            throw Unsupported("DeinterleaveTexture: output must be 16 layers of ceil(w/4) x ceil(h/4) in the input format");
+        check(rsd_deinterleave(in->ptr, in->width, in->height, (uint32_t)formatBytes(in->format), out->ptr, ctx.stream),
+              "DeinterleaveTexture");
+    }
+};
+
+class InterleaveTexturePass : public RenderPass {
+public:
+    explicit InterleaveTexturePass(const Properties& p) { props_ = p; }
+    Reflection reflect(const CompileData&) override {
+        Reflection r;
+        r.addInput("texIn", "Texture2DArray");
+        Field& o = r.addOutput("texOut", "Texture2D");
+        o.formatFrom = "texIn";
+        o.fromFormatOnly = true;
+        return r;
+    }
+    void execute(Context& ctx, const RenderData& rd) override {
+        Texture* in = rd["texIn"];
+        Texture* out = rd["texOut"];
+        if (in->layers == 1) return;  // fed by a stub pass (e.g. ConvolutionalNet): no data to interleave
+        if (in->layers != 16 || in->format != out->format || in->width != (out->width + 3) / 4 ||
+            in->height != (out->height + 3) / 4)
+            throw Unsupported("InterleaveTexture: input must be 16 layers of ceil(w/4) x ceil(h/4) of the output");
+        check(rsd_interleave(in->ptr, out->width, out->height, (uint32_t)formatBytes(in->format), out->ptr, ctx.stream),
+              "InterleaveTexture");
+    }
+};
+
 template <class T>
 PluginRegistry::Factory factory() {
     return [](const Properties& p) { return std::unique_ptr<RenderPass>(new T(p)); };
@@ -825,6 +877,8 @@ void registerBuiltinPasses(PluginRegistry& r) {
     r.registerClass("TAA", "temporal anti-aliasing (colour-box clamped history)", factory<TAAPass>());
     r.registerClass("AOFlickerMask", "stable-pixel mask from depth and normals", factory<AOFlickerMaskPass>());
     r.registerClass("BinaryDilation", "min / max over a radius-2 gather ring", factory<BinaryDilationPass>());
+    r.registerClass("DeinterleaveTexture", "4x4 deinterleave into 16 quarter-size layers", factory<DeinterleaveTexturePass>());
+    r.registerClass("InterleaveTexture", "16 quarter-size layers back into one image", factory<InterleaveTexturePass>());
 }
 
 }  // namespace rsd::host

@@ -218,6 +218,47 @@ __global__ void __launch_bounds__(kPostW * kPostH) taa_kernel(TaaArgs a) {
     a.out[(size_t)y * a.W + x] = make_float4(tmp + l.z, l.x + l.y, tmp - l.z, 1.0f);
 }
 
+// ---------------------------------------------------------------------- Deinterleave / Interleave
+// DeinterleaveTexture (Deinterleave.slang, DeinterleaveTexture.cpp:143-158): a W x H texture ->
+// 16 layers of ceil(W/4) x ceil(H/4), layer s = off.y * 4 + off.x holding src[4 y + off.y][4 x +
+// off.x] (Loads outside the source read 0).  InterleaveTexture (Interleave.slang): the inverse,
+// out[y][x] = src[layer (y % 4) * 4 + x % 4][y / 4][x / 4].  Byte shuffles of ELEM-byte texels.
+template <int ELEM>
+struct TexelT { uint8_t b[ELEM]; };
+template <>
+struct TexelT<4> { uint32_t v; };
+template <>
+struct TexelT<8> { uint2 v; };
+template <>
+struct TexelT<16> { uint4 v; };
+
+template <int ELEM>
+__global__ void __launch_bounds__(kPostW * kPostH) deinterleave_kernel(const TexelT<ELEM>* __restrict__ src, int W,
+                                                                        int H, TexelT<ELEM>* __restrict__ dst, int w4,
+                                                                        int h4) {
+    const int x = (int)(blockIdx.x * kPostW + threadIdx.x), y = (int)(blockIdx.y * kPostH + threadIdx.y);
+    if (x >= w4 || y >= h4) return;
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+        const int sx = 4 * x + (s & 3), sy = 4 * y + (s >> 2);
+        TexelT<ELEM> t{};
+        if (sx < W && sy < H) t = src[(size_t)sy * W + sx];
+        dst[((size_t)s * h4 + y) * w4 + x] = t;
+    }
+}
+
+template <int ELEM>
+__global__ void __launch_bounds__(kPostW * kPostH) interleave_kernel(const TexelT<ELEM>* __restrict__ src, int w4,
+                                                                      int h4, TexelT<ELEM>* __restrict__ dst, int W,
+                                                                      int H) {
+    const int x = (int)(blockIdx.x * kPostW + threadIdx.x), y = (int)(blockIdx.y * kPostH + threadIdx.y);
+    if (x >= W || y >= H) return;
+    const int xq = x >> 2, yq = y >> 2, s = (y & 3) * 4 + (x & 3);
+    TexelT<ELEM> t{};
+    if (xq < w4 && yq < h4) t = src[((size_t)s * h4 + yq) * w4 + xq];
+    dst[(size_t)y * W + x] = t;
+}
+
 // ---------------------------------------------------------------------- AOFlickerMask
 // AOFlickerMask.ps.slang:43-63 (AOFlickerMask.cpp:73-86): a pixel is stable (1) when, in x and
 // in y, one of its two neighbours lies in the plane of its view-space normal to within 0.1 (|dot|
@@ -588,6 +629,53 @@ extern "C" rsd_status rsd_cross_bilateral_blur(const uint8_t* d_src, const float
         if (e != hipSuccess) return hip_fail(e, "blur_kernel launch");
     }
     return RSD_OK;
+}
+
+namespace {
+template <template <int> class KERNEL>
+rsd_status launch_by_elem(uint32_t elem, dim3 grid, hipStream_t s, const void* src, int a0, int a1, void* dst, int b0,
+                          int b1, const char* what) {
+    switch (elem) {
+        case 1: hipLaunchKernelGGL(KERNEL<1>::fn, grid, dim3(kPostW, kPostH), 0, s, (const TexelT<1>*)src, a0, a1, (TexelT<1>*)dst, b0, b1); break;
+        case 2: hipLaunchKernelGGL(KERNEL<2>::fn, grid, dim3(kPostW, kPostH), 0, s, (const TexelT<2>*)src, a0, a1, (TexelT<2>*)dst, b0, b1); break;
+        case 4: hipLaunchKernelGGL(KERNEL<4>::fn, grid, dim3(kPostW, kPostH), 0, s, (const TexelT<4>*)src, a0, a1, (TexelT<4>*)dst, b0, b1); break;
+        case 8: hipLaunchKernelGGL(KERNEL<8>::fn, grid, dim3(kPostW, kPostH), 0, s, (const TexelT<8>*)src, a0, a1, (TexelT<8>*)dst, b0, b1); break;
+        case 16: hipLaunchKernelGGL(KERNEL<16>::fn, grid, dim3(kPostW, kPostH), 0, s, (const TexelT<16>*)src, a0, a1, (TexelT<16>*)dst, b0, b1); break;
+        default:
+            set_error(std::string(what) + ": texel size must be 1, 2, 4, 8 or 16 bytes");
+            return RSD_ERR_UNSUPPORTED;
+    }
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? RSD_OK : hip_fail(e, what);
+}
+template <int E>
+struct DeinterleaveK { static constexpr auto fn = deinterleave_kernel<E>; };
+template <int E>
+struct InterleaveK { static constexpr auto fn = interleave_kernel<E>; };
+}  // namespace
+
+extern "C" rsd_status rsd_deinterleave(const void* d_src, uint32_t width, uint32_t height, uint32_t texel_bytes,
+                                       void* d_dst, rsd_stream stream) {
+    if (!d_src || !d_dst || width == 0 || height == 0 || d_src == d_dst) {
+        set_error("rsd_deinterleave: invalid argument");
+        return RSD_ERR_INVALID_ARG;
+    }
+    const uint32_t w4 = (width + 3) / 4, h4 = (height + 3) / 4;
+    const dim3 grid((w4 + kPostW - 1) / kPostW, (h4 + kPostH - 1) / kPostH);
+    return launch_by_elem<DeinterleaveK>(texel_bytes, grid, (hipStream_t)stream, d_src, (int)width, (int)height, d_dst,
+                                         (int)w4, (int)h4, "rsd_deinterleave");
+}
+
+extern "C" rsd_status rsd_interleave(const void* d_src, uint32_t width, uint32_t height, uint32_t texel_bytes,
+                                     void* d_dst, rsd_stream stream) {
+    if (!d_src || !d_dst || width == 0 || height == 0 || d_src == d_dst) {
+        set_error("rsd_interleave: invalid argument");
+        return RSD_ERR_INVALID_ARG;
+    }
+    const uint32_t w4 = (width + 3) / 4, h4 = (height + 3) / 4;
+    const dim3 grid((width + kPostW - 1) / kPostW, (height + kPostH - 1) / kPostH);
+    return launch_by_elem<InterleaveK>(texel_bytes, grid, (hipStream_t)stream, d_src, (int)w4, (int)h4, d_dst,
+                                       (int)width, (int)height, "rsd_interleave");
 }
 
 extern "C" rsd_status rsd_ao_flicker_mask(const float* d_linear_z, const float* d_normal_w, uint32_t width,

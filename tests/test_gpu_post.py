@@ -122,3 +122,26 @@ def test_image_equation_ieee_special_values(torch):
                 assert bits[k] == w, (formula, k, hex(bits[k]), hex(w))
                 v = np.array([w], np.uint32).view(F)[0]
                 assert got8[k] == (255 if v >= 1 else 0 if not v > 0 else int(np.floor(v * 255 + 0.5))), (formula, k)
+
+
+@pytest.mark.parametrize("shape,dtype", [((37, 70), np.float32), ((64, 40, 4), np.float32), ((21, 33), np.uint8),
+                                         ((18, 18, 2), np.float32)])
+def test_deinterleave_interleave_parity(torch, shape, dtype):
+    from oracle.texops import deinterleave, interleave
+    from rsd import abi
+    rng = np.random.default_rng(sum(shape))
+    a = (rng.random(shape) * 255).astype(dtype)
+    H, W = shape[:2]
+    texel = a.itemsize * (shape[2] if len(shape) == 3 else 1)
+    src = torch.from_numpy(a).cuda()
+    want = deinterleave(a)
+    dst = torch.full(want.shape, 7, dtype=src.dtype, device="cuda")
+    abi.check(abi.lib().rsd_deinterleave(C.c_void_p(src.data_ptr()), W, H, texel, C.c_void_p(dst.data_ptr()),
+                                         _stream(torch)), "rsd_deinterleave")
+    back = torch.full_like(src, 9)
+    abi.check(abi.lib().rsd_interleave(C.c_void_p(dst.data_ptr()), W, H, texel, C.c_void_p(back.data_ptr()),
+                                       _stream(torch)), "rsd_interleave")
+    torch.cuda.synchronize()
+    assert np.array_equal(dst.cpu().numpy(), want)
+    assert np.array_equal(back.cpu().numpy(), interleave(want, H, W))
+    assert np.array_equal(back.cpu().numpy(), a)

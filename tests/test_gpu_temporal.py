@@ -298,3 +298,39 @@ def test_graph_temporal_ao_with_stable_mask(torch, oracle):
     g.close()
     gs.release()
     dev.close()
+
+
+def test_graph_deinterleave_roundtrip(torch, oracle):
+    """DeinterleaveTexture -> InterleaveTexture in the C++ graph host: the 16 layers equal the
+    numpy restatement (oracle/texops.py) and the round trip gives the linear depth back."""
+    from oracle.texops import deinterleave
+    from rsd import graph as rg
+    from rsd.frame import Device, GpuScene, make_camera
+    from rsd.scenes import make_scene
+    cfg = small_frame_config()
+    scene = make_scene("arcade_tiny")
+    dev = Device(0)
+    gs = GpuScene(dev, scene)
+    g = rg.RenderGraph("dei")
+    g.create_pass("GBufferRaster", "GBufferRaster", {})
+    g.create_pass("LinearizeDepth", "LinearizeDepth", {})
+    g.create_pass("Dei", "DeinterleaveTexture", {})
+    g.create_pass("Int", "InterleaveTexture", {})
+    g.add_edge("GBufferRaster.depth", "LinearizeDepth.depth")
+    g.add_edge("LinearizeDepth.linearDepth", "Dei.texIn")
+    g.add_edge("Dei.texOut", "Int.texIn")
+    for o in ("Int.texOut", "Dei.texOut", "LinearizeDepth.linearDepth"):
+        g.mark_output(o)
+    g.set_scene(gs.h, make_camera(scene, cfg))
+    g.compile(cfg.fb_w, cfg.fb_h)
+    g.execute()
+    torch.cuda.synchronize()
+    H, W = cfg.fb_h, cfg.fb_w
+    z = g.output_tensor("LinearizeDepth.linearDepth").cpu().numpy().reshape(H, W)
+    layers = g.output_tensor("Dei.texOut").cpu().numpy().reshape(16, (H + 3) // 4, (W + 3) // 4)
+    assert np.array_equal(layers.view(np.uint32), deinterleave(z).view(np.uint32))
+    back = g.output_tensor("Int.texOut").cpu().numpy().reshape(H, W)
+    assert np.array_equal(back.view(np.uint32), z.view(np.uint32))
+    g.close()
+    gs.release()
+    dev.close()

@@ -248,3 +248,21 @@ def test_temporal_ao_enabled_plans():
     d.add_edge("GBufferRaster.mvec", "TemporalAO.aoIn")
     d.mark_output("TemporalAO.aoOut")
     d.plan(*FB)
+
+
+def test_deinterleave_shapes_plan():
+    """DeinterleaveTexture (DeinterleaveTexture.cpp:80-125): 16 layers of ceil(w/4) x ceil(h/4) in
+    the input's format; InterleaveTexture: the input's format at the default size."""
+    g = rsdgraph.RenderGraph("dei")
+    g.create_pass("GBufferRaster", "GBufferRaster", {})
+    g.create_pass("LinearizeDepth", "LinearizeDepth", {})
+    g.create_pass("Dei", "DeinterleaveTexture", {})
+    g.create_pass("Int", "InterleaveTexture", {})
+    g.add_edge("GBufferRaster.depth", "LinearizeDepth.depth")
+    g.add_edge("LinearizeDepth.linearDepth", "Dei.texIn")
+    g.add_edge("Dei.texOut", "Int.texIn")
+    g.mark_output("Int.texOut")
+    g.plan(130, 70)
+    res = g.resources()
+    assert res["Dei.texOut"] == (33, 18, 16, "R32Float")
+    assert res["Int.texOut"] == (130, 70, 1, "R32Float")

@@ -158,3 +158,18 @@ def test_binary_dilation_ring(oracle):
     dot[0, 0] = 1
     dm = oracle.binary_dilation(dot, "max")
     assert dm[0, 0] == 1 and dm[H - 1, W - 1] == 1  # wraps around the corner
+
+
+def test_deinterleave_interleave_oracle():
+    """DeinterleaveTexture / InterleaveTexture restated in numpy: layer contents, zero padding of
+    ragged sizes, and the round trip."""
+    from oracle.texops import deinterleave, interleave
+    rng = np.random.default_rng(7)
+    for H, W in ((8, 12), (13, 9), (1, 1)):
+        a = rng.random((H, W)).astype(F)
+        d = deinterleave(a)
+        assert d.shape == (16, (H + 3) // 4, (W + 3) // 4)
+        assert d[5, 0, 0] == (a[1, 1] if H > 1 and W > 1 else 0.0)
+        assert np.array_equal(interleave(d, H, W), a)
+        if H % 4:
+            assert (d[12:, -1, :] == 0).all()  # rows beyond the source read 0
