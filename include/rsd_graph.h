@@ -80,6 +80,10 @@ rsd_status rsd_cross_bilateral_blur(const uint8_t* d_src, const float* d_linear_
                                     uint8_t* d_pingpong, uint8_t* d_dst, uint32_t width, uint32_t height,
                                     uint32_t guard_band, uint32_t kernel_radius, uint32_t better_slope,
                                     rsd_stream stream);
+/* RayMinMaxLength (RayMinMaxLength.ps.slang:4-16): the SD ray interval length per texel,
+ * max(0, asfloat(rayMax) - asfloat(rayMin)) / 32, and 0 where rayMax is 0 (R32Float). */
+rsd_status rsd_ray_min_max_length(const uint32_t* d_ray_min, const uint32_t* d_ray_max, uint32_t width,
+                                  uint32_t height, float* d_out, rsd_stream stream);
 /* DeinterleaveTexture (Deinterleave.slang, DeinterleaveTexture.cpp:143-158): a width x height
  * texture of texel_bytes-byte texels -> 16 layers of ceil(width/4) x ceil(height/4), layer
  * (dy * 4 + dx) holding src[4y + dy][4x + dx] (0 outside the source).  InterleaveTexture

@@ -357,6 +357,7 @@ void RenderGraph::compile(Context& ctx, uint32_t width, uint32_t height, bool al
     for (auto& p : order_) {
         for (auto& [key, f] : outs) {
             if (f.formatFrom.empty() || splitName(key).first != p) continue;
+            const Format declared = f.format;
             for (auto& e : edges_) {
                 if (e.dstPass != p || e.dstField != f.formatFrom || !need.count(e.srcPass)) continue;
                 auto src = outs.find(e.srcPass + "." + e.srcField);
@@ -373,7 +374,10 @@ void RenderGraph::compile(Context& ctx, uint32_t width, uint32_t height, bool al
                 f.height = ext->second->height;
                 f.layers = ext->second->layers;
             }
-            if (f.fromFormatOnly) {
+            if (f.fromSizeOnly) {
+                f.format = declared;
+                f.layers = 1;
+            } else if (f.fromFormatOnly) {
                 f.width = f.height = 0;
                 f.layers = 1;
             } else if (f.shrink > 1 || f.layersOut) {

@@ -78,6 +78,7 @@ struct Field {
     // (DeinterleaveTexture: 4, 16 layers); fromFormatOnly: copy the format only (InterleaveTexture)
     uint32_t shrink = 1, layersOut = 0;
     bool fromFormatOnly = false;
+    bool fromSizeOnly = false;  // with formatFrom: copy the size, keep the declared format (RayMinMaxLength)
 };
 
 struct Reflection {

@@ -19,6 +19,7 @@
 //   BinaryDilation        BinaryDilation.cpp         rsd_binary_dilation
 //   DeinterleaveTexture   DeinterleaveTexture.cpp    rsd_deinterleave (16 layers of 1/4 x 1/4)
 //   InterleaveTexture     InterleaveTexture.cpp      rsd_interleave
+//   RayMinMaxLength       RayMinMaxLength.cpp        rsd_ray_min_max_length
 //
 // Every other pass type of the reference scripts (ToneMapper, ForwardLighting, ...)
 // is outside the hot path; it resolves to a stub that declares whatever fields
@@ -855,6 +856,35 @@ public:
     }
 };
 
+// ------------------------------------------------------------------------------ RayMinMaxLength
+// RayMinMaxLength.cpp:55-95: kRayMin + kRayMax (SVAO's internal interval maps) -> len (R32Float,
+// the inputs' size)
+class RayMinMaxLengthPass : public RenderPass {
+public:
+    explicit RayMinMaxLengthPass(const Properties& p) { props_ = p; }
+    Reflection reflect(const CompileData&) override {
+        Reflection r;
+        r.addInput("kRayMin", "Minimum ray length");
+        r.addInput("kRayMax", "Maximum ray length");
+        Field& o = r.addOutput("len", "Ray Length");
+        o.format = Format::R32Float;
+        o.formatFrom = "kRayMin";
+        o.fromSizeOnly = true;
+        return r;
+    }
+    void execute(Context& ctx, const RenderData& rd) override {
+        Texture* mn = rd["kRayMin"];
+        Texture* mx = rd["kRayMax"];
+        Texture* out = rd["len"];
+        if (formatBytes(mn->format) != 4 || formatBytes(mx->format) != 4 || mn->width != out->width ||
+            mn->height != out->height || mx->width != out->width || mx->height != out->height)
+            throw Unsupported("RayMinMaxLength: 32-bit interval maps at the output size");
+        check(rsd_ray_min_max_length((const uint32_t*)mn->ptr, (const uint32_t*)mx->ptr, out->width, out->height,
+                                     (float*)out->ptr, ctx.stream),
+              "RayMinMaxLength");
+    }
+};
+
 template <class T>
 PluginRegistry::Factory factory() {
     return [](const Properties& p) { return std::unique_ptr<RenderPass>(new T(p)); };
@@ -879,6 +909,7 @@ void registerBuiltinPasses(PluginRegistry& r) {
     r.registerClass("BinaryDilation", "min / max over a radius-2 gather ring", factory<BinaryDilationPass>());
     r.registerClass("DeinterleaveTexture", "4x4 deinterleave into 16 quarter-size layers", factory<DeinterleaveTexturePass>());
     r.registerClass("InterleaveTexture", "16 quarter-size layers back into one image", factory<InterleaveTexturePass>());
+    r.registerClass("RayMinMaxLength", "SD ray interval lengths (debug view)", factory<RayMinMaxLengthPass>());
 }
 
 }  // namespace rsd::host

@@ -259,6 +259,18 @@ __global__ void __launch_bounds__(kPostW * kPostH) interleave_kernel(const Texel
     dst[(size_t)y * W + x] = t;
 }
 
+// ---------------------------------------------------------------------- RayMinMaxLength
+// RayMinMaxLength.ps.slang:4-16: the SD ray interval length of every texel, 0 where rayMax was never
+// raised, max(0, rayMax - rayMin) / 32 otherwise (the interval maps hold float bit patterns)
+__global__ void __launch_bounds__(256) ray_length_kernel(const uint32_t* __restrict__ rmin,
+                                                         const uint32_t* __restrict__ rmax, uint32_t n,
+                                                         float* __restrict__ out) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t mx = rmax[i];
+    out[i] = mx == 0u ? 0.0f : hmax(0.0f, __uint_as_float(mx) - __uint_as_float(rmin[i])) / 32.0f;
+}
+
 // ---------------------------------------------------------------------- AOFlickerMask
 // AOFlickerMask.ps.slang:43-63 (AOFlickerMask.cpp:73-86): a pixel is stable (1) when, in x and
 // in y, one of its two neighbours lies in the plane of its view-space normal to within 0.1 (|dot|
@@ -676,6 +688,19 @@ extern "C" rsd_status rsd_interleave(const void* d_src, uint32_t width, uint32_t
     const dim3 grid((width + kPostW - 1) / kPostW, (height + kPostH - 1) / kPostH);
     return launch_by_elem<InterleaveK>(texel_bytes, grid, (hipStream_t)stream, d_src, (int)w4, (int)h4, d_dst,
                                        (int)width, (int)height, "rsd_interleave");
+}
+
+extern "C" rsd_status rsd_ray_min_max_length(const uint32_t* d_ray_min, const uint32_t* d_ray_max, uint32_t width,
+                                             uint32_t height, float* d_out, rsd_stream stream) {
+    if (!d_ray_min || !d_ray_max || !d_out || width == 0 || height == 0) {
+        set_error("rsd_ray_min_max_length: invalid argument");
+        return RSD_ERR_INVALID_ARG;
+    }
+    const uint32_t n = width * height;
+    hipLaunchKernelGGL(ray_length_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, d_ray_min,
+                       d_ray_max, n, d_out);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? RSD_OK : hip_fail(e, "ray_length_kernel launch");
 }
 
 extern "C" rsd_status rsd_ao_flicker_mask(const float* d_linear_z, const float* d_normal_w, uint32_t width,

@@ -124,7 +124,7 @@ GRAPH_EXPORTS = ["rsd_graph_create", "rsd_graph_destroy", "rsd_graph_create_pass
                  "rsd_cross_bilateral_blur", "rsd_image_equation_compile", "rsd_image_equation_info",
                  "rsd_image_equation_run", "rsd_image_equation_release", "rsd_temporal_ao",
                  "rsd_motion_vectors", "rsd_taa", "rsd_ao_flicker_mask", "rsd_binary_dilation",
-                 "rsd_deinterleave", "rsd_interleave"]
+                 "rsd_deinterleave", "rsd_interleave", "rsd_ray_min_max_length"]
 
 FMT_R32F, FMT_RG32F, FMT_RGBA32F, FMT_R16U, FMT_R8U, FMT_R8UNORM, FMT_R32U, FMT_UNKNOWN = range(8)
 FMT_R16F, FMT_RG16F, FMT_RGBA16F = 8, 9, 10
@@ -246,6 +246,8 @@ def lib():
         L.rsd_binary_dilation.restype = st
         L.rsd_binary_dilation.argtypes = [vp, u32, u32, u32, vp, vp]
         L.rsd_taa.restype = st
+        L.rsd_ray_min_max_length.restype = st
+        L.rsd_ray_min_max_length.argtypes = [vp, vp, u32, u32, vp, vp]
         for fn in (L.rsd_deinterleave, L.rsd_interleave):
             fn.restype = st
             fn.argtypes = [vp, u32, u32, u32, vp, vp]

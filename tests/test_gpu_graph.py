@@ -139,3 +139,30 @@ def test_graph_ao_post_chain(setup, expected, oracle):
     g.close()
     gs.release()
     dev.close()
+
+
+def test_graph_ray_min_max_length(setup, expected):
+    """RayMinMaxLength fed by SVAO's internal interval maps (scripts/SVAO.py:70-71) in the C++
+    graph host: the lengths of the frame's SD ray intervals."""
+    from oracle.texops import ray_min_max_length
+    from rsd import graph as rg
+    torch, cfg = setup["torch"], setup["cfg"]
+    g = rg.load_script(SCRIPT)["SVAOHotPath"]
+    g.create_pass("RayMinMaxLength", "RayMinMaxLength", {})
+    g.add_edge("SVAO.internalRayMin", "RayMinMaxLength.kRayMin")
+    g.add_edge("SVAO.internalRayMax", "RayMinMaxLength.kRayMax")
+    g.mark_output("RayMinMaxLength.len")
+    from rsd.frame import Device, GpuScene
+    dev = Device(0)
+    gs = GpuScene(dev, setup["scene"])
+    g.set_scene(gs.h, setup["cam"])
+    g.compile(cfg.fb_w, cfg.fb_h)
+    g.execute()
+    torch.cuda.synchronize()
+    got = _np(g.output_tensor("RayMinMaxLength.len")).reshape(setup["sd_h"], setup["sd_w"])
+    want = ray_min_max_length(expected["ray_min"], expected["ray_max"])
+    np.testing.assert_array_equal(got.view(np.uint32), want.view(np.uint32))
+    assert (got > 0).sum() > 0
+    g.close()
+    gs.release()
+    dev.close()

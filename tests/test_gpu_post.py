@@ -145,3 +145,28 @@ def test_deinterleave_interleave_parity(torch, shape, dtype):
     assert np.array_equal(dst.cpu().numpy(), want)
     assert np.array_equal(back.cpu().numpy(), interleave(want, H, W))
     assert np.array_equal(back.cpu().numpy(), a)
+
+
+def test_ray_min_max_length_parity(torch):
+    """rsd_ray_min_max_length over random interval words plus the special cases: rayMax == 0,
+    inverted intervals, +-inf and NaN bit patterns."""
+    from oracle.texops import ray_min_max_length
+    from rsd import abi
+    rng = np.random.default_rng(5)
+    H, W = 45, 77
+    mn = (rng.random((H, W)) * 50).astype(F)
+    mx = (mn + (rng.random((H, W)) * 10 - 2)).astype(F)
+    mnu, mxu = mn.view(np.uint32).copy(), mx.view(np.uint32).copy()
+    mxu[rng.random((H, W)) < 0.2] = 0
+    special = np.array([0x7F800000, 0xFF800000, 0x7FC00000, 0x00000001, 0x80000000], np.uint32)
+    mnu[0, :25] = np.repeat(special, 5)
+    mxu[0, :25] = np.tile(special, 5)
+    dmn, dmx = torch.from_numpy(mnu.view(np.int32)).cuda(), torch.from_numpy(mxu.view(np.int32)).cuda()
+    out = torch.full((H, W), 7.0, dtype=torch.float32, device="cuda")
+    abi.check(abi.lib().rsd_ray_min_max_length(C.c_void_p(dmn.data_ptr()), C.c_void_p(dmx.data_ptr()), W, H,
+                                               C.c_void_p(out.data_ptr()), _stream(torch)), "rsd_ray_min_max_length")
+    torch.cuda.synchronize()
+    got = out.cpu().numpy()
+    want = ray_min_max_length(mnu, mxu)
+    assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
+    assert (got > 0).mean() > 0.4 and (got[mxu == 0] == 0).all()

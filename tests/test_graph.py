@@ -250,6 +250,20 @@ def test_temporal_ao_enabled_plans():
     d.plan(*FB)
 
 
+def test_ray_min_max_length_plan():
+    """RayMinMaxLength (RayMinMaxLength.cpp:55-70): R32Float `len` at the interval maps' size."""
+    g = hotpath()
+    g.create_pass("RayMinMaxLength", "RayMinMaxLength", {})
+    g.add_edge("SVAO.internalRayMin", "RayMinMaxLength.kRayMin")
+    g.add_edge("SVAO.internalRayMax", "RayMinMaxLength.kRayMax")
+    g.mark_output("RayMinMaxLength.len")
+    g.plan(*FB)
+    res = g.resources()
+    sd = ((FB[0] + 1) // 2 + 64, (FB[1] + 1) // 2 + 64)
+    assert res["RayMinMaxLength.len"] == (sd[0], sd[1], 1, "R32Float")
+    assert g.execution_order()[-1] == "RayMinMaxLength"
+
+
 def test_deinterleave_shapes_plan():
     """DeinterleaveTexture (DeinterleaveTexture.cpp:80-125): 16 layers of ceil(w/4) x ceil(h/4) in
     the input's format; InterleaveTexture: the input's format at the default size."""

@@ -173,3 +173,14 @@ def test_deinterleave_interleave_oracle():
         assert np.array_equal(interleave(d, H, W), a)
         if H % 4:
             assert (d[12:, -1, :] == 0).all()  # rows beyond the source read 0
+
+
+def test_ray_min_max_length_oracle():
+    """RayMinMaxLength.ps.slang:4-16 known answers: rayMax word 0 -> 0, inverted -> 0, NaN -> 0."""
+    from oracle.texops import ray_min_max_length
+    f = lambda *v: np.array(v, np.float32).view(np.uint32)  # noqa: E731
+    mn = f(1.0, 2.0, 5.0, 0.0, np.inf, 1.0)
+    mx = f(33.0, 0.0, 3.0, 0.0, np.inf, np.nan)
+    mx[1] = 0
+    got = ray_min_max_length(mn, mx)
+    assert got.tolist() == [1.0, 0.0, 0.0, 0.0, 0.0, 0.0]
