@@ -76,6 +76,9 @@ def parse():
                          "halo exchanges (point-to-point RCCL) + AO all-gather (strong); gather = interleaved "
                          "bands with whole-map all-reduce / all-gather (round-1 v1). Default: band for the 4K "
                          "configs, frame otherwise")
+    ap.add_argument("--scene-file", default=None,
+                    help="a .pyscene or .obj scene (rsd.pyscene / rsd.ingest) instead of the config's stand-in "
+                         "scene; the config still sets the frame, SD map and N")
     ap.add_argument("--pmc-csv", nargs="*", default=None,
                     help="rocprofv3 --pmc counter_collection.csv file(s) with FETCH_SIZE / WRITE_SIZE for "
                          "roofline.traffic (default: the committed passes of the default config)")
@@ -138,7 +141,12 @@ def main():
     shard = args.shard or ("band" if cfg.visible_w >= 3840 else "frame")
     path_name = args.camera_path or DEFAULT_CAMERA_PATH.get(args.config, "static")
     poses = camera_path(path_name)
-    scene = make_scene(scene_name)
+    if args.scene_file:
+        from rsd.pyscene import load_scene_file
+        scene_name = os.path.basename(args.scene_file)
+        scene = load_scene_file(args.scene_file).build(scene_name)
+    else:
+        scene = make_scene(scene_name)
     r = Renderer(scene, cfg, device=local)
     bvh_build_s = r.gscene.info.build_ms * 1e-3
     bw = (rank, world) if shard == "gather" else (0, 1)
@@ -258,7 +266,7 @@ def main():
     achieved = alg_bytes / (seq_sd_ms * 1e-3) / 1e9
     kernels_seq = abi.WALK_KERNELS[walk_seq]
     pmc = args.pmc_csv
-    if pmc is None and args.config == DEFAULT_CONFIG and not poses:
+    if pmc is None and args.config == DEFAULT_CONFIG and not poses and not args.scene_file:
         for d in PROFILE_DIRS:
             cand = [d / "pmc_fetch_size.csv", d / "pmc_write_size.csv"]
             if all(p.exists() for p in cand):
@@ -331,7 +339,7 @@ def main():
                              "(per launch, committed rocprofv3 --pmc passes)",
                      "traffic_source": ", ".join(rel(p) for p in pmc) or None},
         # the frame's largest kernel is pass 1, bound by VALU issue rather than HBM
-        "pass1_roofline": pmc_valu(valu_csv, "svao_pass1_kernel") if valu_csv and args.config == DEFAULT_CONFIG
+        "pass1_roofline": pmc_valu(valu_csv, "svao_pass1_kernel") if valu_csv and args.config == DEFAULT_CONFIG and not args.scene_file
         else None,
         "exchange_bytes_per_frame": seq.bytes_per_frame() if shard == "band" and world > 1 else None,
         "bvh_build_s": round(bvh_build_s, 3),

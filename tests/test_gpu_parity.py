@@ -348,6 +348,32 @@ def test_obj_ingest_frame_parity(device, oracle, tmp_path):
     gs.release()
 
 
+def test_pyscene_ingest_frame_parity(device, oracle):
+    """A .pyscene scene (built-in meshes under a node hierarchy, a mirrored instance, an imported
+    OBJ, an alpha-masked pane) loaded by rsd.pyscene: G-buffer, SD map and AO bit-exact vs the
+    oracle."""
+    from conftest import ROOT
+    from rsd.frame import GpuScene, Renderer
+    from rsd.pyscene import load_pyscene
+    s = load_pyscene(ROOT / "tests" / "fixtures" / "courtyard.pyscene").build("courtyard")
+    cfg = small_frame_config(visible=(160, 96), guard=16, divisor=2, N=4)
+    gs = GpuScene(device, s)
+    r = Renderer(s, cfg, dev=device, gpu_scene=gs)
+    r.gbuffer()
+    r.frame()
+    g = r.numpy()
+    osc = oracle.Scene(s.positions, s.indices, s.flags, s.alpha)
+    cam, vao, sdp, svp = oracle_structs(r, oracle)
+    z, n = oracle.gbuffer(osc, cam, cfg.fb_w, cfg.fb_h, cfg.cull_mode)
+    assert bits_equal(g["depth"], z) and np.array_equal(g["normals"], n)
+    ao1, st, rmin, rmax = oracle.svao_pass1(cam, vao, svp, z, n, r.sd_w, r.sd_h)
+    sd, _ = oracle.sd_trace(osc, cam, sdp, z, rmin, rmax, r.sd_w, r.sd_h)
+    assert bits_equal(g["sd"], sd)
+    assert np.array_equal(g["ao"], oracle.svao_pass2(cam, vao, svp, z, n, st, sd, ao1))
+    assert (rmax != 0).sum() > 0
+    gs.release()
+
+
 def test_consumed_intervals_frames_match_fresh_frames(device, oracle):
     """BandFrame folds the interval clear into the trace (RSD_SD_CONSUME_INTERVALS): after
     a consuming trace the maps are exactly the cleared state, and consecutive frames stay
