@@ -57,7 +57,10 @@ __global__ void __launch_bounds__(256) svao_pass1_kernel(SvaoArgs a) {
             Sample s;
             bool ssrAbove;
             if (!sample_init(a, u, v, b, i, s, ssrAbove)) continue;
-            if (fabsf(u - s.ru) < d.invResolution[0] * 0.9f && fabsf(v - s.rv) < d.invResolution[1] * 0.9f) {
+            const bool same = a.k.samePixelInt ? (s.kx == (int)px && s.ky == (int)py)
+                                               : (fabsf(u - s.ru) < d.invResolution[0] * 0.9f &&
+                                                  fabsf(v - s.rv) < d.invResolution[1] * 0.9f);
+            if (same) {
                 ao += div_pdf(s.sphereStart - s.sphereEnd, s);  // isSamePixel
                 continue;
             }

@@ -25,6 +25,7 @@ struct SvaoConsts {
     // both divisors of direction i lie in [2^-30, 2^30]
     float rcpPdf[8], rcpHeight[8];
     uint32_t fastDiv;
+    uint32_t samePixelInt;  // isSamePixel decided on pixel indices (fill_consts)
 };
 
 struct SvaoArgs {
@@ -293,6 +294,11 @@ inline void fill_consts(SvaoConsts& k, const rsd_vao_data& d) {
     k.ssrMin2 = x;
     // div_rcp reciprocals: RN(RN64(1 / b)) = RN(1 / b) (double rounding is innocuous for a
     // quotient when 53 >= 2 * 24 + 2)
+    // isSamePixel (Common.slang:129-133): |texC - rasterSamplePosUV| < 0.9 / res per axis.  Both
+    // uvs are pixel centres within a few ulp (<= 2^-22 for uv < 2) of (k + 0.5) / res, so the test
+    // holds exactly when the pixel indices agree (difference < 2^-21 << 0.9 / res) and fails when
+    // they differ (difference >= 1 / res - 2^-21 > 0.9 / res) for res <= 2^18
+    k.samePixelInt = d.resolution[0] <= 262144.0f && d.resolution[1] <= 262144.0f;
     k.fastDiv = 0u;
     for (int i = 0; i < 8; ++i) {
         const float pdf = 2.0f * k.dirHeight[i], h = k.dirHeight[i];
