@@ -65,10 +65,10 @@ typedef struct {
     uint32_t max_depth;
     uint32_t leaf_count;
     double sah_cost;
-    double build_ms;          /* host BVH build wall time */
+    double build_ms;          /* host build wall time: BVH + segment entry grid */
     uint64_t device_bytes;
     uint32_t build_threads;   /* host threads of the build (the process's CPU affinity, or RSD_BUILD_THREADS) */
-    uint32_t reserved;
+    uint32_t entry_cells;     /* cells of the segment entry grid (RSD_ENTRY_CELLS bounds it, 0 = none) */
 } rsd_scene_info;
 
 /* Alpha-masked materials (MaterialFactory.slang:124-151, AlphaTest.slang:54-84,

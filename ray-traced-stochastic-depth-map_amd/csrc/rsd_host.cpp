@@ -13,6 +13,7 @@
 #include <thread>
 #include <vector>
 
+#include "entry_grid.h"
 #include "rsd_internal.h"
 
 namespace rsd {
@@ -136,6 +137,39 @@ extern "C" rsd_status rsd_scene_upload(rsd_device* dev, const rsd_scene_desc* de
             return st;
         }
         s->device_bytes += pr.size() * 4;
+    }
+    // segment entry grid (RSD_ENTRY_CELLS bounds its cells, 0 = none)
+    uint64_t maxCells = 1ull << 21;
+    if (const char* env = std::getenv("RSD_ENTRY_CELLS")) maxCells = (uint64_t)std::atoll(env);
+    if (desc->triangle_count && maxCells) {
+        const rsd::EntryGrid g = rsd::build_entry_grid(bvh.nodes, s->tri_offset, maxCells, threads);
+        if (g.cells) {
+            const size_t sb = g.slots.size() * 4, ib = g.items.size() * 4;
+            void* d = nullptr;
+            e = hipMalloc(&d, sb + ib);
+            if (e == hipSuccess) e = hipMemcpy(d, g.slots.data(), sb, hipMemcpyHostToDevice);
+            if (e == hipSuccess) e = hipMemcpy(static_cast<char*>(d) + sb, g.items.data(), ib, hipMemcpyHostToDevice);
+            if (e != hipSuccess) {
+                rsd_status st = rsd::hip_fail(e, "rsd_scene_upload (entry grid)");
+                (void)hipFree(d);
+                (void)hipFree(s->d_prim_rec);
+                (void)hipFree(s->d_nodes);
+                delete s;
+                return st;
+            }
+            s->d_entry = d;
+            s->entry_items_off = sb;
+            uint32_t bits = 0;
+            while ((4ull << bits) < g.slots.size()) ++bits;
+            s->entry_bits = bits;
+            s->entry_probe = g.max_probe;
+            s->entry_rmax = g.rmax;
+            s->entry_cells = g.cells;
+            for (int k = 0; k < 3; ++k) s->entry_origin[k] = g.origin[k];
+            s->entry_extent = g.extent;
+            s->entry_build_ms = g.build_ms;
+            s->device_bytes += sb + ib;
+        }
     }
     *out = s;
     return RSD_OK;
@@ -289,9 +323,10 @@ extern "C" rsd_status rsd_scene_info_get(const rsd_scene* s, rsd_scene_info* out
     out->max_depth = s->stats.max_depth;
     out->leaf_count = s->stats.leaves;
     out->sah_cost = s->stats.sah_cost;
-    out->build_ms = s->stats.build_ms;
+    out->build_ms = s->stats.build_ms + s->entry_build_ms;
     out->device_bytes = s->device_bytes;
     out->build_threads = s->build_threads;
+    out->entry_cells = s->entry_cells;
     return RSD_OK;
 }
 
@@ -348,6 +383,7 @@ extern "C" void rsd_scene_release(rsd_scene* s) {
     (void)hipFree(s->d_prim_rec);
     rsd::release_sd_workspaces(s);
     (void)hipFree(s->d_alpha);
+    (void)hipFree(s->d_entry);
     delete s;
 }
 

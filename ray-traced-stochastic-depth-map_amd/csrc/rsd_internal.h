@@ -78,6 +78,12 @@ struct rsd_scene {
     std::vector<rsd::SdWorkspace*> sd_ws;  // one per stream that traced this scene (few: linear lookup)
     void* d_alpha = nullptr;       // alpha data (rsd_scene_upload_alpha), one allocation
     rsd::AlphaData alpha;          // device pointers into d_alpha
+    // segment entry grid (entry_grid.h): one allocation, hash slots (uint4) then entry items
+    void* d_entry = nullptr;
+    uint32_t entry_bits = 0, entry_probe = 0, entry_rmax = 0, entry_cells = 0;
+    float entry_origin[3] = {0.0f, 0.0f, 0.0f}, entry_extent = 0.0f;
+    uint64_t entry_items_off = 0;  // bytes from d_entry to the item array
+    double entry_build_ms = 0.0;
 };
 
 namespace rsd {

@@ -29,6 +29,7 @@
 #include <vector>
 
 #include "bvh_traverse.h"
+#include "entry_grid.h"
 #include "rsd_device.h"
 #include "rsd_internal.h"
 
@@ -92,7 +93,54 @@ struct SDArgs {
     // partition, the others to its back, so the expensive rays are dequeued first
     uint32_t lpt;
     float lptLen;
+    // segment entry grid (entry_grid.h, canonical walks): the setup kernel looks up the frontier of
+    // each live ray's segment and copies its items to entQ[slot * kEntryCap ..]
+    uint32_t entOn;
+    const uint4* entSlots;
+    const float4* entItems;  // 2 x float4 per entry: {code, lo.xyz} {hi.xyz, 0}
+    uint32_t entBits, entProbe;
+    int entRmax;
+    float entOrigin[3], entExtent;
+    uint32_t* entQ;
 };
+
+// entry_lookup results besides first << 4 | count
+constexpr uint32_t kEntryRoot = 0u;           // walk from the root
+constexpr uint32_t kEntryDead = 0xffffffffu;  // no BVH box near the segment: no hit
+
+// The frontier of the segment [TMin, TMax] of the ray (o, d) (entry_grid.h).  The segment's AABB
+// is padded by 2^-14 of the coordinate magnitude (float rounding of o + d t, of the watertight
+// test's hit point, and of the cell index below are all ~2^-23 relative); the loose cell of its
+// centre at the finest level with m <= cell edge contains it.
+__device__ __forceinline__ uint32_t entry_lookup(const SDArgs& a, f3 o, f3 d, float TMin, float TMax) {
+    const float pad = 0x1p-14f * (fabsf(o.x) + fabsf(o.y) + fabsf(o.z) + TMax) + 1e-30f;
+    const f3 p0 = o + d * TMin, p1 = o + d * TMax;
+    const float lx = fminf(p0.x, p1.x) - pad, hx = fmaxf(p0.x, p1.x) + pad;
+    const float ly = fminf(p0.y, p1.y) - pad, hy = fmaxf(p0.y, p1.y) + pad;
+    const float lz = fminf(p0.z, p1.z) - pad, hz = fmaxf(p0.z, p1.z) + pad;
+    const float m = fmaxf(fmaxf(hx - lx, hy - ly), hz - lz);
+    const float E = a.entExtent;
+    if (!(m <= E)) return kEntryRoot;  // longer than the scene (or NaN): the root
+    int R = min(a.entRmax, ilogbf(E / m));
+    while (R > 0 && m > ldexpf(E, -R)) --R;
+    const float sc = ldexpf(1.0f, R) / E;
+    const int i = (int)floorf((0.5f * (lx + hx) - a.entOrigin[0]) * sc);
+    const int j = (int)floorf((0.5f * (ly + hy) - a.entOrigin[1]) * sc);
+    const int k = (int)floorf((0.5f * (lz + hz) - a.entOrigin[2]) * sc);
+    const int hi = 1 << R;
+    if (i < -1 || j < -1 || k < -1 || i > hi || j > hi || k > hi) return kEntryDead;  // outside every box
+    const unsigned long long key = ((unsigned long long)(R + 1) << 60) | ((unsigned long long)(i + 1) << 40) |
+                                   ((unsigned long long)(j + 1) << 20) | (unsigned long long)(k + 1);
+    uint32_t h = (uint32_t)((key * 0x9E3779B97F4A7C15ull) >> (64 - a.entBits));
+    const uint32_t mask = (1u << a.entBits) - 1u;
+    const uint32_t klo = (uint32_t)key, khi = (uint32_t)(key >> 32);
+    for (uint32_t n = 0; n <= a.entProbe; ++n, h = (h + 1u) & mask) {
+        const uint4 s = a.entSlots[h];
+        if (s.x == klo && s.y == khi) return s.z;
+        if (s.x == 0u && s.y == 0u) break;
+    }
+    return kEntryDead;  // the level is complete: an absent cell overlaps no BVH box
+}
 
 // queue slot of the qi-th ray of partition part (lpt: the long rays [0, nLong) from the front, the
 // short ones from the back)
@@ -301,10 +349,22 @@ template <int K>
 __device__ __forceinline__ int trace_knearest_quad(const float4* __restrict__ bvh, uint32_t triOff, const RayCtx& r,
                                                    float tmin, float tmax, uint32_t cull, bool useLB, float lbT,
                                                    uint32_t lbP, KList<K>& kl, uint32_t* __restrict__ sItem,
-                                                   float* __restrict__ sT, int q, int quadBase, TraceStats& st) {
+                                                   float* __restrict__ sT, int q, int quadBase, TraceStats& st,
+                                                   const uint32_t* __restrict__ ent, uint32_t nEnt) {
     kl.clear();
     int sp = 0, found = 0;
     uint32_t item = 0;
+    if (nEnt) {
+        // the segment's entry-grid frontier (entry_grid.h): item 0 first, the rest on the stack
+        // (entry distance -inf: always popped; the result does not depend on the order)
+        item = ent[0];
+        if (q == 0)
+            for (uint32_t e = 1; e < nEnt; ++e) {
+                sItem[(e - 1) * kQuadRays] = ent[e];
+                sT[(e - 1) * kQuadRays] = -INFINITY;
+            }
+        sp = (int)nEnt - 1;
+    }
     const float tlo = useLB ? fmaxf(tmin, lbT) : tmin;
     const float* bf = reinterpret_cast<const float*>(bvh);
     while (true) {
@@ -389,7 +449,8 @@ __device__ __forceinline__ int trace_knearest_quad(const float4* __restrict__ bv
 template <int K, int N>
 __device__ __forceinline__ void sd_resolve(const SDArgs& a, f3 d, float TMin, float TMax, float cosT, float (&depths)[N],
                                            uint32_t* sItem, float* sT, int q, int quadBase, TraceStats& st,
-                                           uint32_t& hitsDelivered) {
+                                           uint32_t& hitsDelivered, const uint32_t* ent = nullptr,
+                                           uint32_t nEnt = 0u) {
     const rsd_camera& c = a.cam;
     RayCtx r;
     ray_setup(r, mk(c.posW[0], c.posW[1], c.posW[2]), d);
@@ -401,7 +462,7 @@ __device__ __forceinline__ void sd_resolve(const SDArgs& a, f3 d, float TMin, fl
     constexpr int J = (K + 3) / 4;  // hits per lane in the epilogue
     while (!commit) {
         const int found = trace_knearest_quad<K>(a.nodes, a.triOff, r, TMin, TMax, a.cull, useLB, lbT, lbP, kl, sItem,
-                                                 sT, q, quadBase, st);
+                                                 sT, q, quadBase, st, ent, nEnt);
         // barycentrics + hash of hit j are computed by lane j % 4 (re-running the identical
         // triangle test on the hit's record), then shared with the quad
         float rngL[J], zL[J];
@@ -444,15 +505,22 @@ __device__ __forceinline__ void sd_resolve(const SDArgs& a, f3 d, float TMin, fl
     }
 }
 
-// A live ray in the queue: 2 x 16 B {dir.xyz, TMin} {TMax, cosT, texel, 0}
+// A live ray in the queue: 2 x 16 B {dir.xyz, TMin} {TMax, cosT, texel, nEnt}; nEnt > 0: the walk starts
+// from the nEnt entry-grid items at entQ[slot * kEntryCap] instead of the root
 __device__ __forceinline__ void ray_rec_load(const float4* __restrict__ q, uint32_t slot, f3& d, float& TMin,
-                                             float& TMax, float& cosT, uint32_t& texel) {
+                                             float& TMax, float& cosT, uint32_t& texel, uint32_t& nEnt) {
     const float4 r0 = q[2u * slot], r1 = q[2u * slot + 1u];
     d = mk(r0.x, r0.y, r0.z);
     TMin = r0.w;
     TMax = r1.x;
     cosT = r1.y;
     texel = __float_as_uint(r1.z);
+    nEnt = __float_as_uint(r1.w);
+}
+__device__ __forceinline__ void ray_rec_load(const float4* __restrict__ q, uint32_t slot, f3& d, float& TMin,
+                                             float& TMax, float& cosT, uint32_t& texel) {
+    uint32_t nEnt;
+    ray_rec_load(q, slot, d, TMin, TMax, cosT, texel, nEnt);
 }
 
 // Phase 1 (rayGen up to TraceRay): one lane per SD texel of the band.  Rays whose interval
@@ -486,7 +554,8 @@ __global__ void __launch_bounds__(kSetupWaves * kBlock) sd_setup_kernel(SDArgs a
         }
         return;  // uniform over the workgroup
     }
-    bool live = false;
+    bool live = false, culled = false;
+    uint32_t ent = kEntryRoot, keep = 0u;  // keep: the frontier items the ray passes
     f3 d = mk(0.0f, 0.0f, 0.0f);
     float TMin = 0.0f, TMax = 0.0f, cosT = 0.0f;
     if (inside) {
@@ -497,6 +566,26 @@ __global__ void __launch_bounds__(kSetupWaves * kBlock) sd_setup_kernel(SDArgs a
         if (a.consume) {  // after the last read of this texel's interval
             a.rayMinW[(size_t)y * a.sdW + x] = 0x7f7fffffu;
             a.rayMaxW[(size_t)y * a.sdW + x] = 0u;
+        }
+        if (live && a.entOn) {
+            const f3 o = mk(a.cam.posW[0], a.cam.posW[1], a.cam.posW[2]);
+            ent = entry_lookup(a, o, d, TMin, TMax);
+            if (ent != kEntryRoot && ent != kEntryDead) {
+                // the frontier items whose boxes the ray passes (the walk's own child test)
+                RayCtx r;
+                ray_setup(r, o, d);
+                const uint32_t first = ent >> 4, n = ent & 15u;
+                for (uint32_t e = 0; e < n; ++e) {
+                    const float4 b0 = a.entItems[2u * (first + e)], b1 = a.entItems[2u * (first + e) + 1u];
+                    float tn;
+                    if (box_hit(r, b0.y, b1.x, b0.z, b1.y, b0.w, b1.z, TMin, TMax, tn)) keep |= 1u << e;
+                }
+                if (keep == 0u) ent = kEntryDead;
+            }
+            if (ent == kEntryDead) {  // a live interval that can hit nothing: DEFAULT_DEPTH, no walk
+                live = false;
+                culled = true;
+            }
         }
         if (!live) {
             float depths[N];
@@ -533,9 +622,15 @@ __global__ void __launch_bounds__(kSetupWaves * kBlock) sd_setup_kernel(SDArgs a
         slot = part * a.partCap + base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
     }
     if (live) {
+        // record word 7: the number of entry items stored to entQ (0: walk from the root)
         queue[2u * slot] = make_float4(d.x, d.y, d.z, TMin);
-        queue[2u * slot + 1u] = make_float4(TMax, cosT, __uint_as_float((uint32_t)y * (uint32_t)a.sdW + x), 0.0f);
+        queue[2u * slot + 1u] =
+            make_float4(TMax, cosT, __uint_as_float((uint32_t)y * (uint32_t)a.sdW + x), __uint_as_float(__popc(keep)));
+        uint32_t e = 0;
+        for (uint32_t m = keep; m; m &= m - 1u)
+            a.entQ[(size_t)slot * kEntryCap + e++] = __float_as_uint(a.entItems[2u * ((ent >> 4) + __ffs(m) - 1u)].x);
     }
+    if (a.counters && culled) atomicAdd(&a.counters[1], 1ull);  // still an active ray (rsd_counters)
     if (a.raster) {
         // the raster walk's inputs: slot map, the tile's view-depth range, empty key lists
         if (inside) a.slotMap[(size_t)y * a.sdW + x] = live ? (int32_t)slot : -1;
@@ -583,8 +678,9 @@ __global__ void __launch_bounds__(kBlock) sd_trace_queue_kernel(SDArgs a, const 
         if (qi < count) {
             f3 d;
             float TMin, TMax, cosT;
-            uint32_t idx;
-            ray_rec_load(queue, queue_slot(a, part, qi, nLong), d, TMin, TMax, cosT, idx);
+            uint32_t idx, nEnt;
+            const uint32_t slot = queue_slot(a, part, qi, nLong);
+            ray_rec_load(queue, slot, d, TMin, TMax, cosT, idx, nEnt);
             const int x = (int)(idx % (uint32_t)a.sdW), y = (int)(idx / (uint32_t)a.sdW);
             float depths[N];
             const float DEFAULT = a.normalize ? 1.0f : 3.40282347e+37f;
@@ -593,7 +689,7 @@ __global__ void __launch_bounds__(kBlock) sd_trace_queue_kernel(SDArgs a, const 
             const uint32_t n0 = st.nodes, l0 = st.leaves;
             const unsigned long long c0 = a.counters ? __builtin_amdgcn_s_memtime() : 0ull;
             sd_resolve<K, N>(a, d, TMin, TMax, cosT, depths, &sItem[quad], &sT[quad], q, quadBase, st,
-                             hitsDelivered);
+                             hitsDelivered, a.entOn ? a.entQ + (size_t)slot * kEntryCap : nullptr, nEnt);
             if (q == 0) {
                 if (a.counters) {
                     const unsigned long long dc = __builtin_amdgcn_s_memtime() - c0;
@@ -1089,6 +1185,7 @@ template <int K, int N, int ROW, bool SPLIT, bool CNT, int POOL = kPoolCap>
 __global__ void __launch_bounds__(kBlock) sd_trace_row_kernel(SDArgs a, const float4* __restrict__ queue,
                                                               uint32_t* __restrict__ qctl, uint2* __restrict__ keys) {
     static_assert(K <= ROW, "one key per lane");
+    static_assert(kEntryCap <= (uint32_t)ROW, "entry items start one per lane");
     constexpr int kRow = ROW, kRowRays = kBlock / ROW;
     __shared__ uint32_t sItem[kRowRays * POOL];
     __shared__ float sT[kRowRays * POOL];
@@ -1104,6 +1201,7 @@ __global__ void __launch_bounds__(kBlock) sd_trace_row_kernel(SDArgs a, const fl
     const float DEFAULT = a.normalize ? 1.0f : 3.40282347e+37f;  // Common.slangh:16
     const int soft = a.poolSoft;
     uint32_t slot = 0;  // queue slot of the row's ray
+    uint32_t nEnt = 0;  // entry-grid items of the row's ray (0: the root)
 
     // ---- per-row state (the same value in the 16 lanes of a row unless noted)
     constexpr int kFetch = 0, kTrace = 1, kExit = 2;
@@ -1148,7 +1246,9 @@ __global__ void __launch_bounds__(kBlock) sd_trace_row_kernel(SDArgs a, const fl
                 slot = queue_slot(a, part, qi, nLong);
                 f3 d;
                 uint32_t idx;
-                ray_rec_load(queue, slot, d, TMin, TMax, cosT, idx);
+                // the entry items load with the record (the setup kernel wrote both)
+                const uint32_t e = a.entOn && l < (int)kEntryCap ? a.entQ[(size_t)slot * kEntryCap + l] : kNoItem;
+                ray_rec_load(queue, slot, d, TMin, TMax, cosT, idx, nEnt);
                 x = (int)(idx % (uint32_t)a.sdW);
                 y = (int)(idx / (uint32_t)a.sdW);
                 ray_setup(r, mk(c.posW[0], c.posW[1], c.posW[2]), d);
@@ -1157,7 +1257,8 @@ __global__ void __launch_bounds__(kBlock) sd_trace_row_kernel(SDArgs a, const fl
                 cnt = 0u;
                 useLB = false;
                 pool = 0;
-                item = l == 0 ? 0u : kNoItem;  // the root node
+                // the root node, or the segment's entry-grid frontier (one item per lane)
+                item = nEnt ? ((uint32_t)l < nEnt ? e : kNoItem) : (l == 0 ? 0u : kNoItem);
                 kt = INFINITY; kp = kNoItem; ku = kv = 0.0f;
                 phase = kTrace;
                 if constexpr (CNT) {
@@ -1369,7 +1470,7 @@ __global__ void __launch_bounds__(kBlock) sd_trace_row_kernel(SDArgs a, const fl
             lbT = __shfl(kt, base + K - 1);
             lbP = __shfl(kp, base + K - 1);
             pool = 0;
-            item = l == 0 ? 0u : kNoItem;
+            item = nEnt ? ((uint32_t)l < nEnt ? a.entQ[(size_t)slot * kEntryCap + l] : kNoItem) : (l == 0 ? 0u : kNoItem);
             kt = INFINITY; kp = kNoItem; ku = kv = 0.0f;
             continue;
         }
@@ -1790,6 +1891,17 @@ rsd_status sd_trace_impl(rsd_scene* scene, const rsd_camera* cam, const rsd_sd_p
     a.lpt = 0u;
     a.lptLen = 0.0f;
     a.primRec = scene->d_prim_rec;
+    a.entOn = 0u;
+    a.entSlots = static_cast<const uint4*>(scene->d_entry);
+    a.entItems = scene->d_entry ? reinterpret_cast<const float4*>(static_cast<const char*>(scene->d_entry) +
+                                                                   scene->entry_items_off)
+                                : nullptr;
+    a.entBits = scene->entry_bits;
+    a.entProbe = scene->entry_probe;
+    a.entRmax = (int)scene->entry_rmax;
+    for (int k = 0; k < 3; ++k) a.entOrigin[k] = scene->entry_origin[k];
+    a.entExtent = scene->entry_extent;
+    a.entQ = nullptr;
     a.alphaData = scene->alpha;
     a.alphaData.spread = rsd_ray_cone_spread(cam->focalLength, sd_h);  // default texture dims = SD map
     if (p->implementation == RSD_SD_COVERAGE_MASK) {
@@ -1844,16 +1956,18 @@ rsd_status sd_trace_impl(rsd_scene* scene, const rsd_camera* cam, const rsd_sd_p
     // split walk (trace -> keys -> resolve) when one chunk of K keys decides every texel
     const bool split = p->implementation != RSD_SD_COVERAGE_MASK && p->max_count <= K;
     const size_t queueBytes = need_q * 32, keyBytes = split ? need_q * K * sizeof(uint2) : 0;
-    if (ws->queue_cap < queueBytes + keyBytes) {
+    const size_t entBytes = scene->d_entry ? need_q * kEntryCap * sizeof(uint32_t) : 0;
+    if (ws->queue_cap < queueBytes + keyBytes + entBytes) {
         RSD_HIP(hipStreamSynchronize(s));
         (void)hipFree(ws->queue);
         ws->queue = nullptr;
         ws->queue_cap = 0;
-        RSD_HIP(hipMalloc(&ws->queue, queueBytes + keyBytes));
-        ws->queue_cap = queueBytes + keyBytes;
+        RSD_HIP(hipMalloc(&ws->queue, queueBytes + keyBytes + entBytes));
+        ws->queue_cap = queueBytes + keyBytes + entBytes;
     }
     float4* queue = reinterpret_cast<float4*>(ws->queue);
     uint2* keys = reinterpret_cast<uint2*>(reinterpret_cast<char*>(ws->queue) + queueBytes);
+    if (entBytes) a.entQ = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(ws->queue) + queueBytes + keyBytes);
     // double-buffered queue control (sd_setup_kernel); both buffers are reset on first use and
     // after a failed launch sequence
     if (ws->qctl_dirty) {
@@ -1892,6 +2006,12 @@ rsd_status sd_trace_impl(rsd_scene* scene, const rsd_camera* cam, const rsd_sd_p
     // pass; RSD_TRACE_WALK=split keeps the key-list + resolve-kernel variant for A/B runs
     const int walk = p->hit_order == RSD_HIT_ORDER_TRAVERSAL ? 3 : raster ? 4 : !rowWalk ? 0
                      : (split && walkName == "split") ? 2 : 1;
+    // segment entry grid: canonical walks (row, quad, split) start from the frontier of each ray's
+    // segment; RSD_TRACE_ENTRY=off walks every ray from the root (A/B runs)
+    if ((walk == 0 || walk == 1 || walk == 2) && a.entQ) {
+        const char* entEnv = std::getenv("RSD_TRACE_ENTRY");
+        a.entOn = entEnv && std::string(entEnv) == "off" ? 0u : 1u;
+    }
     if (walk == 1 || walk == 0) {
         // longest-first queue: rays whose interval exceeds 0.1 x TMin are dequeued first (configs[1]:
         // 90 -> 84 us); RSD_TRACE_LPT = off | a threshold (> 0 absolute, < 0 relative to TMin)
