@@ -556,6 +556,7 @@ __global__ void __launch_bounds__(kSetupWaves * kBlock) sd_setup_kernel(SDArgs a
     }
     bool live = false, culled = false;
     uint32_t ent = kEntryRoot, keep = 0u;  // keep: the frontier items the ray passes
+    uint32_t code[kEntryCap];              // their item codes
     f3 d = mk(0.0f, 0.0f, 0.0f);
     float TMin = 0.0f, TMax = 0.0f, cosT = 0.0f;
     if (inside) {
@@ -575,10 +576,16 @@ __global__ void __launch_bounds__(kSetupWaves * kBlock) sd_setup_kernel(SDArgs a
                 RayCtx r;
                 ray_setup(r, o, d);
                 const uint32_t first = ent >> 4, n = ent & 15u;
-                for (uint32_t e = 0; e < n; ++e) {
-                    const float4 b0 = a.entItems[2u * (first + e)], b1 = a.entItems[2u * (first + e) + 1u];
+                float4 b0[kEntryCap], b1[kEntryCap];
+#pragma unroll
+                for (uint32_t e = 0; e < kEntryCap; ++e)  // every load before the first test
+                    if (e < n) { b0[e] = a.entItems[2u * (first + e)]; b1[e] = a.entItems[2u * (first + e) + 1u]; }
+#pragma unroll
+                for (uint32_t e = 0; e < kEntryCap; ++e) {
                     float tn;
-                    if (box_hit(r, b0.y, b1.x, b0.z, b1.y, b0.w, b1.z, TMin, TMax, tn)) keep |= 1u << e;
+                    code[e] = __float_as_uint(b0[e].x);
+                    if (e < n && box_hit(r, b0[e].y, b1[e].x, b0[e].z, b1[e].y, b0[e].w, b1[e].z, TMin, TMax, tn))
+                        keep |= 1u << e;
                 }
                 if (keep == 0u) ent = kEntryDead;
             }
@@ -626,9 +633,9 @@ __global__ void __launch_bounds__(kSetupWaves * kBlock) sd_setup_kernel(SDArgs a
         queue[2u * slot] = make_float4(d.x, d.y, d.z, TMin);
         queue[2u * slot + 1u] =
             make_float4(TMax, cosT, __uint_as_float((uint32_t)y * (uint32_t)a.sdW + x), __uint_as_float(__popc(keep)));
-        uint32_t e = 0;
-        for (uint32_t m = keep; m; m &= m - 1u)
-            a.entQ[(size_t)slot * kEntryCap + e++] = __float_as_uint(a.entItems[2u * ((ent >> 4) + __ffs(m) - 1u)].x);
+#pragma unroll
+        for (uint32_t e = 0; e < kEntryCap; ++e)
+            if ((keep >> e) & 1u) a.entQ[(size_t)slot * kEntryCap + __popc(keep & ((1u << e) - 1u))] = code[e];
     }
     if (a.counters && culled) atomicAdd(&a.counters[1], 1ull);  // still an active ray (rsd_counters)
     if (a.raster) {

@@ -57,6 +57,9 @@ def main():
                     "nodes_per_active_ray": round(c.nodes_visited / act, 2),
                     "tris_per_active_ray": round(c.tris_tested / act, 2),
                     "max_steps_per_ray": int(c.max_steps_per_ray),
+                    "leaves_per_active_ray": round(c.leaves_visited / act, 2),
+                    "mean_ray_clocks": round(c.sum_ray_clocks / act, 1),
+                    "max_ray_clocks": int(c.max_ray_clocks),
                     "walk": int(c.walk),
                 }
         os.environ.pop("RSD_TRACE_ENTRY")
