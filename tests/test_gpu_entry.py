@@ -64,7 +64,6 @@ def test_entry_grid_same_bits(device, oracle, monkeypatch, scene, walk, N, impl,
     off, c_off = trace(r, monkeypatch, "off", walk)
     assert np.array_equal(on, off)
     assert c_on.rays_active == c_off.rays_active > 0
-    assert c_on.nodes_visited <= c_off.nodes_visited
     if scene == "arcade_tiny":
         g = r.numpy()
         cam = to_oracle(r.cam, oracle.Camera)
