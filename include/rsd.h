@@ -157,7 +157,7 @@ typedef struct {
 
 /* SVAO compile-time defines (SVAO.cpp:221-237) + the per-frame guardBand */
 typedef struct {
-    uint32_t num_directions;       /* NUM_DIRECTIONS (8) */
+    uint32_t num_directions;       /* NUM_DIRECTIONS: 8 (default), 16 or 32 */
     uint32_t sd_samples;           /* MSAA_SAMPLES = SD N */
     uint32_t secondary_depth_mode; /* DepthMode: 0 SingleDepth, 2 StochasticDepth, 3 Raytraced */
     uint32_t ray_interval;         /* USE_RAY_INTERVAL */
@@ -258,7 +258,10 @@ rsd_status rsd_sd_trace(rsd_scene* scene, const rsd_camera* cam, const rsd_sd_pa
 /* SVAO.cpp:330-341: rayMax <- 0, rayMin <- asuint(FLT_MAX) */
 rsd_status rsd_svao_clear_intervals(uint32_t* d_ray_min, uint32_t* d_ray_max, uint32_t count, rsd_stream stream);
 
-/* "AO 1": SVAORaster.ps.slang:29-122, dispatched as SVAO.cpp:344-350 */
+/* "AO 1": SVAORaster.ps.slang:29-122, dispatched as SVAO.cpp:344-350.
+ * params->num_directions (NUM_DIRECTIONS) is 8, 16 or 32 (Common.slang:51-58); the stencil texel is
+ * R8Uint / R16Uint / R32Uint accordingly (SVAO.cpp:132-134): d_stencil holds width * height texels of
+ * num_directions / 8 bytes (the same for every pass that takes a stencil). */
 rsd_status rsd_svao_pass1(const rsd_camera* cam, const rsd_vao_data* vao, const rsd_svao_params* params,
                           const float* d_depth, const uint16_t* d_normals, uint32_t width, uint32_t height,
                           uint8_t* d_ao, uint8_t* d_stencil, uint32_t* d_ray_min, uint32_t* d_ray_max,

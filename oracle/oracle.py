@@ -250,10 +250,15 @@ def sd_ray(cam: Camera, params: SDParams, linearZ, rayMin, rayMax, sdW, sdH, x, 
     return out[:3], out[3:], tmin.value, tmax.value, cosT.value
 
 
+def stencil_dtype(num_directions):
+    """The SVAO stencil texel (SVAO.cpp:132-134): R8Uint / R16Uint / R32Uint for 8 / 16 / 32 directions."""
+    return {8: np.uint8, 16: np.uint16, 32: np.uint32}[int(num_directions)]
+
+
 def svao_pass1(cam, vao: VAOData, p: SVAOParams, depth, normals, sdW, sdH):
     H, W = depth.shape
     ao = np.zeros((H, W), np.uint8)
-    st = np.zeros((H, W), np.uint8)
+    st = np.zeros((H, W), stencil_dtype(p.num_directions))
     rmin = np.zeros((sdH, sdW), np.uint32)
     rmax = np.zeros((sdH, sdW), np.uint32)
     lib().ocpu_svao_clear(_p(rmin), _p(rmax), sdW * sdH)
@@ -267,6 +272,7 @@ def svao_pass2(cam, vao: VAOData, p: SVAOParams, depth, normals, stencil, sd, ao
     ao = np.array(ao, np.uint8, copy=True)
     sdH, sdW = sd.shape[1], sd.shape[2]
     sdc = np.ascontiguousarray(sd, np.float32)
+    stencil = np.ascontiguousarray(stencil, stencil_dtype(p.num_directions))
     lib().ocpu_svao_pass2(C.byref(cam), C.byref(vao), C.byref(p), _p(depth), _p(normals), W, H,
                           _p(stencil), _p(sdc), sdW, sdH, _p(ao), _threads(threads))
     return ao
@@ -282,7 +288,8 @@ def svao_pass2_raytraced(scene: Scene, cam, vao: VAOData, p: SVAOParams, depth, 
     H, W = depth.shape
     ao = np.array(ao, np.uint8, copy=True)
     lib().ocpu_svao_pass2_rt_band(scene.h, C.byref(cam), C.byref(vao), C.byref(p), _p(depth), _p(normals), W, H,
-                                  _p(np.ascontiguousarray(stencil, np.uint8)), _p(ao), cull, ray_pipeline, alpha_test,
+                                  _p(np.ascontiguousarray(stencil, stencil_dtype(p.num_directions))), _p(ao), cull,
+                                  ray_pipeline, alpha_test,
                                   band[0], band[1], _threads(threads))
     return ao
 

@@ -69,9 +69,30 @@ static const float k_jitter[16][2] = {
     {0.7173641100525856f, 0.6695209294557571f},  {0.6563677340745926f, 0.35924511030316353f},
 };
 
-/* SVAO/Common.slang:53 -- VAO sample radii for NUM_DIRECTIONS = 8 */
+/* SVAO/Common.slang:52-58 -- VAO sample radii for NUM_DIRECTIONS = 8, 16, 32 (the shader's float
+ * constants; the 16 / 32 tables are double literals there, rounded to float like these) */
 static const float k_radius8[8] = {0.917883f, 0.564429f, 0.734504f, 0.359545f,
                                    0.820004f, 0.470149f, 0.650919f, 0.205215f};
+static const float k_radius16[16] = {
+    0.949098221604059, 0.5865639019441775, 0.7554681720909893, 0.3895439574863043,
+    0.8425560503012255, 0.4948003867747738, 0.6719196866381647, 0.25203100417434543,
+    0.8908588816103737, 0.5418210823278604, 0.7136427497994143, 0.32724136087586453,
+    0.7980920320691521, 0.4445340224611676, 0.6297373536812639, 0.1447182620692375,
+};
+static const float k_radius32[32] = {
+    0.9682458365518543, 0.5974803093982587, 0.7660169295429302, 0.4038472576817624,
+    0.8541535023444914, 0.5068159098187986, 0.6823727109604635, 0.2726076670970059,
+    0.904018191941786, 0.5531894754180758, 0.7240656647095169, 0.34372202910162664,
+    0.8089818132350507, 0.45747336127867605, 0.640354849019649, 0.17748061996818404,
+    0.9327350969376332, 0.5755500192397054, 0.7449678114312224, 0.37479566486456295,
+    0.8311856199411515, 0.4825843210309559, 0.6614378277661477, 0.22975243551455923,
+    0.878233108646881, 0.5303115209931901, 0.7032256306171377, 0.3099952198410562,
+    0.7873133907642258, 0.43130429537268, 0.6190581352335289, 0.10219580968897692,
+};
+static const float* o_radius_table(uint32_t nd)
+{
+    return nd == 32 ? k_radius32 : nd == 16 ? k_radius16 : k_radius8;
+}
 
 /* Jitter.slangh:27-50 randomJitter */
 void ocpu_jitter(uint32_t x, uint32_t y, float* jx, float* jy)
@@ -83,7 +104,8 @@ void ocpu_jitter(uint32_t x, uint32_t y, float* jx, float* jy)
 
 float ocpu_sample_radius(uint32_t num_directions, uint32_t i)
 {
-    if (num_directions == 8 && i < 8) return k_radius8[i];
+    if ((num_directions == 8 || num_directions == 16 || num_directions == 32) && i < num_directions)
+        return o_radius_table(num_directions)[i];
     return 0.0f;
 }
 
@@ -1252,8 +1274,24 @@ typedef struct {
     const ocam* c; const ovao* d; const osvao_params* p;
     const float* depth; const uint16_t* normals; uint32_t W, H;
     float sinNoise[16], cosNoise[16];
-    float sinDir[8], cosDir[8];
+    uint32_t nd;  /* NUM_DIRECTIONS: 8, 16, 32 */
+    float sinDir[32], cosDir[32];
 } octx;
+
+/* the SVAO stencil texel (SVAO.cpp:132-134): R8Uint / R16Uint / R32Uint for 8 / 16 / 32 directions,
+ * NUM_DIRECTIONS / 8 bytes per pixel, little-endian */
+static uint32_t o_stencil_get(const uint8_t* st, size_t i, uint32_t nd)
+{
+    if (nd == 32) { uint32_t v; memcpy(&v, st + 4 * i, 4); return v; }
+    if (nd == 16) { uint16_t v; memcpy(&v, st + 2 * i, 2); return v; }
+    return st[i];
+}
+static void o_stencil_set(uint8_t* st, size_t i, uint32_t nd, uint32_t v)
+{
+    if (nd == 32) memcpy(st + 4 * i, &v, 4);
+    else if (nd == 16) { uint16_t h = (uint16_t)v; memcpy(st + 2 * i, &h, 2); }
+    else st[i] = (uint8_t)v;
+}
 
 typedef struct {
     float posV[3]; float posVLength;
@@ -1282,8 +1320,9 @@ static void o_ctx_init(octx* x, const ocam* c, const ovao* d, const osvao_params
         x->sinNoise[i] = o_sin(rr);
         x->cosNoise[i] = o_cos(rr);
     }
-    for (int i = 0; i < 8; ++i) {
-        float a = ((float)i / 8.0f) * 2.0f * 3.141f; /* Common.slang:357 */
+    x->nd = p->num_directions == 16 || p->num_directions == 32 ? p->num_directions : 8u;
+    for (uint32_t i = 0; i < x->nd; ++i) {
+        float a = ((float)i / (float)x->nd) * 2.0f * 3.141f; /* Common.slang:357 */
         x->sinDir[i] = o_sin(a);
         x->cosDir[i] = o_cos(a);
     }
@@ -1366,7 +1405,7 @@ static float o_make_nonzero(float v, float eps)
 static int o_sample_init(const octx* x, float u, float v, const obasic* b, uint32_t i, osample* s)
 {
     const ovao* d = x->d;
-    s->radius = k_radius8[i] * b->radius;
+    s->radius = o_radius_table(x->nd)[i] * b->radius;
     float dir[2] = {s->radius * x->sinDir[i], s->radius * x->cosDir[i]};
     float sphereHeight = sqrtf(b->radius * b->radius - s->radius * s->radius);
     s->pdf = 2.0f * sphereHeight;
@@ -1493,7 +1532,7 @@ static void o_pass1_impl(const ocam* cam, const ovao* d, const osvao_params* p,
             if (!o_basic_init(&x, u, v, &b)) {
                 aoOut = 1.0f;
             } else {
-                for (uint32_t i = 0; i < 8; ++i) {
+                for (uint32_t i = 0; i < x.nd; ++i) {
                     osample s;
                     if (!o_sample_init(&x, u, v, &b, i, &s)) continue;
                     /* isSamePixel, Common.slang:129-134 */
@@ -1531,13 +1570,13 @@ static void o_pass1_impl(const ocam* cam, const ovao* d, const osvao_params* p,
                         }
                     }
                 }
-                aoOut *= 1.0f / 8.0f;
+                aoOut *= 1.0f / (float)x.nd;  /* SVAORaster.ps.slang:108-109 */
                 aoOut *= 2.0f;
                 if (p->secondary_depth_mode == 0 || st == 0) aoOut = o_pow(aoOut, d->exponent);
             }
             if (px < W && py < H) {
                 ao[(size_t)py * W + px] = o_unorm8(aoOut);
-                stencil[(size_t)py * W + px] = (uint8_t)st;
+                o_stencil_set(stencil, (size_t)py * W + px, x.nd, st);
             }
         }
     (void)sdH;
@@ -1562,14 +1601,14 @@ static void* o_pass2_rows(void* arg)
         for (uint32_t px = g; px < W - g; ++px) {
             if (((py - g) / 32u) % j->bc != j->bi) break;
             size_t o = (size_t)py * W + px;
-            uint32_t mask = j->stencil[o];
+            uint32_t mask = o_stencil_get(j->stencil, o, x->nd);
             if (mask == 0) continue;
             float u = ((float)px + 0.5f) * d->invResolution[0];
             float v = ((float)py + 0.5f) * d->invResolution[1];
             obasic b;
             o_basic_init(x, u, v, &b);
             float vis = 0.0f;
-            for (uint32_t i = 0; i < 8; ++i) {
+            for (uint32_t i = 0; i < x->nd; ++i) {
                 if (!(mask & (1u << i))) continue;
                 osample s;
                 o_sample_init(x, u, v, &b, i, &s);
@@ -1591,7 +1630,7 @@ static void* o_pass2_rows(void* arg)
                 }
                 vis += s.visibility;
             }
-            vis *= 1.0f / 8.0f;
+            vis *= 1.0f / (float)x->nd;  /* Common.slang:660-661 */
             vis *= 2.0f;
             vis += o_unorm8_to_float(j->ao[o]);
             vis = o_pow(vis, d->exponent);
@@ -1674,14 +1713,14 @@ static void* o_pass2_rt_rows(void* arg)
         for (uint32_t px = g; px < xEnd; ++px) {
             if (((py - g) / 32u) % j->bc != j->bi) break;
             size_t o = (size_t)py * W + px;
-            uint32_t mask = j->stencil[o];
+            uint32_t mask = o_stencil_get(j->stencil, o, x->nd);
             if (mask == 0) continue;
             float u = ((float)px + 0.5f) * d->invResolution[0];
             float v = ((float)py + 0.5f) * d->invResolution[1];
             obasic b;
             o_basic_init(x, u, v, &b);
             float vis = 0.0f;
-            for (uint32_t i = 0; i < 8; ++i) {
+            for (uint32_t i = 0; i < x->nd; ++i) {
                 if (!(mask & (1u << i))) continue;
                 osample s;
                 o_sample_init(x, u, v, &b, i, &s);
@@ -1734,7 +1773,7 @@ static void* o_pass2_rt_rows(void* arg)
                 s.visibility = o_min(s.visibility, o_min(sphereVis, haloVis));
                 vis += s.visibility;
             }
-            vis *= 1.0f / 8.0f;
+            vis *= 1.0f / (float)x->nd;  /* Common.slang:660-661 */
             vis *= 2.0f;
             vis += o_unorm8_to_float(j->ao[o]);
             vis = o_pow(vis, d->exponent);

@@ -319,6 +319,9 @@ public:
         if (primary_ != 0) throw Unsupported("SVAO: primaryDepthMode other than SingleDepth is not implemented");
         if (secondary_ == 1) throw Unsupported("SVAO: secondaryDepthMode DualDepth is not implemented (SURVEY 8(f))");
         if (dualAo_) throw Unsupported("SVAO: dualAO is not implemented");
+        // Common.slang:51-58 holds sample radii for 8, 16 and 32 directions only
+        if (directions_ != 8 && directions_ != 16 && directions_ != 32)
+            throw Unsupported("SVAO: sampleCount must be 8, 16 or 32");
     }
     void sdSize(uint32_t w, uint32_t h, rsd_vao_data* vao, uint32_t* sw, uint32_t* sh) const {
         // getExtraGuardBand (SVAO.cpp:718-723): only the StochasticDepth mode has an SD guard band
@@ -339,8 +342,9 @@ public:
         r.addInput("normals", "View space normals, 2x8 octahedral").format = Format::R16Uint;
         opt("color", "Color for pixel importance");
         r.addOutput("ao", "Ambient Occlusion").format = Format::R8Unorm;
-        // NUM_DIRECTIONS = 8 -> R8Uint (SVAO.cpp:132-135)
-        r.addOutput("stencil", "Stencil Bitmask for primary / secondary ao").format = Format::R8Uint;
+        // NUM_DIRECTIONS 8 / 16 / 32 -> R8Uint / R16Uint / R32Uint (SVAO.cpp:132-135)
+        r.addOutput("stencil", "Stencil Bitmask for primary / secondary ao").format =
+            directions_ > 16 ? Format::R32Uint : directions_ > 8 ? Format::R16Uint : Format::R8Uint;
         for (const char* n : {"internalRayMin", "internalRayMax"}) {
             auto& f = r.addOutput(n, n[8] == 'M' && n[10] == 'n' ? "internal ray min" : "internal ray max");
             f.format = Format::R32Uint;  // R32Int in the reference; the bit patterns are non-negative floats

@@ -53,7 +53,7 @@ __global__ void __launch_bounds__(256) svao_pass1_kernel(SvaoArgs a) {
         ao = 1.0f;
     } else {
 #pragma unroll 1
-        for (int i = 0; i < 8; ++i) {
+        for (int i = 0; i < (int)a.k.nd; ++i) {
             Sample s;
             bool ssrAbove;
             if (!sample_init(a, u, v, b, i, s, ssrAbove)) continue;
@@ -90,13 +90,13 @@ __global__ void __launch_bounds__(256) svao_pass1_kernel(SvaoArgs a) {
                 }
             }
         }
-        ao *= 1.0f / 8.0f;
+        ao *= a.k.invNd;  // SVAORaster.ps.slang:108-109
         ao *= 2.0f;
         if (a.secondary == 0u || st == 0u) ao = acc_pow(ao, d.exponent);
     }
     if (px < (uint32_t)a.W && py < (uint32_t)a.H) {
         a.ao[(size_t)py * a.W + px] = unorm8(ao);
-        a.stencil[(size_t)py * a.W + px] = (uint8_t)st;
+        stencil_store(a, (size_t)py * a.W + px, st);
     }
 }
 
@@ -168,11 +168,11 @@ __device__ __forceinline__ void svao_pass2_dir(const SvaoArgs& a, const Basic& b
 // many passes as its mean direction count (<= the old per-lane maximum).
 constexpr int kP2Tile = 16;                   // pass-2 tile edge (pixels): 16 measured 33 us, 8 35 us, 32 65 us
 constexpr int kP2Lanes = kP2Tile * kP2Tile;   // lanes per workgroup = pixels per tile
-template <int N>
+template <int N, int ND>
 __global__ void __launch_bounds__(kP2Lanes) svao_pass2_kernel(SvaoArgs a) {
     constexpr uint32_t T = kP2Tile, L = kP2Lanes;
-    __shared__ uint32_t sPix[L];       // active pixel slot: local index | mask << 8
-    __shared__ uint16_t sPair[8 * L];  // pair: slot << 3 | direction
+    __shared__ uint32_t sPix[L];        // active pixel slot: local index
+    __shared__ uint16_t sPair[ND * L];  // pair: slot << 5 | direction
     __shared__ uint16_t sFirst[L];     // first pair of each slot
     __shared__ float sAcc[L];          // running vis of each slot
     __shared__ float sP[L], sR[L];
@@ -189,15 +189,15 @@ __global__ void __launch_bounds__(kP2Lanes) svao_pass2_kernel(SvaoArgs a) {
     {
         const uint32_t px = x0 + (tid % T), py = y0 + (tid / T);
         const uint32_t m =
-            (px < (uint32_t)a.W - a.guard && py < (uint32_t)a.H - a.guard) ? a.stencil[(size_t)py * a.W + px] : 0u;
+            (px < (uint32_t)a.W - a.guard && py < (uint32_t)a.H - a.guard) ? stencil_load(a, (size_t)py * a.W + px) : 0u;
         if (m) {
             const uint32_t slot = atomicAdd(&sNPix, 1u), base = atomicAdd(&sNPair, (uint32_t)__popc(m));
-            sPix[slot] = tid | (m << 8);
+            sPix[slot] = tid;
             sFirst[slot] = (uint16_t)base;
             sAcc[slot] = 0.0f;
             uint32_t j = base;
-            for (int i = 0; i < 8; ++i)
-                if (m & (1u << i)) sPair[j++] = (uint16_t)(slot << 3 | i);
+            for (int i = 0; i < ND; ++i)
+                if (m & (1u << i)) sPair[j++] = (uint16_t)(slot << 5 | i);
             // a non-zero stencil means pass 1's basic_init of this pixel succeeded (same bits)
             const float u = ((float)px + 0.5f) * d.invResolution[0];
             const float v = ((float)py + 0.5f) * d.invResolution[1];
@@ -213,13 +213,13 @@ __global__ void __launch_bounds__(kP2Lanes) svao_pass2_kernel(SvaoArgs a) {
         uint32_t slot = 0;
         if (k < nPair) {
             const uint32_t e = sPair[k];
-            slot = e >> 3;
+            slot = e >> 5;
             const uint32_t lp = sPix[slot] & 255u;
             const float u = ((float)(x0 + lp % T) + 0.5f) * d.invResolution[0];
             const float v = ((float)(y0 + lp / T) + 0.5f) * d.invResolution[1];
             const Basic b = sBasic[slot];
             float p, r;
-            svao_pass2_dir<N>(a, b, u, v, (int)(e & 7u), p, r);
+            svao_pass2_dir<N>(a, b, u, v, (int)(e & 31u), p, r);
             sP[tid] = p;
             sR[tid] = r;
         }
@@ -227,7 +227,7 @@ __global__ void __launch_bounds__(kP2Lanes) svao_pass2_kernel(SvaoArgs a) {
         // the lane of a pixel's first pair in this chunk applies its pairs in direction order
         if (k < nPair && k == max((uint32_t)sFirst[slot], c)) {
             float acc = sAcc[slot];
-            for (uint32_t j = k; j < nPair && j < c + L && (uint32_t)(sPair[j] >> 3) == slot; ++j)
+            for (uint32_t j = k; j < nPair && j < c + L && (uint32_t)(sPair[j] >> 5) == slot; ++j)
                 acc = (acc - sP[j - c]) + sR[j - c];
             sAcc[slot] = acc;
         }
@@ -237,7 +237,7 @@ __global__ void __launch_bounds__(kP2Lanes) svao_pass2_kernel(SvaoArgs a) {
         const uint32_t lp = sPix[sl] & 255u;
         const size_t o = (size_t)(y0 + lp / T) * a.W + (x0 + lp % T);
         float vis = sAcc[sl];
-        vis *= 1.0f / 8.0f;
+        vis *= a.k.invNd;  // Common.slang:660-661
         vis *= 2.0f;
         vis += unorm8_to_float(a.ao[o]);
         vis = acc_pow(vis, d.exponent);
@@ -368,7 +368,7 @@ rsd_status pass1_impl(const rsd_camera* cam, const rsd_vao_data* vao, const rsd_
     SvaoArgs a{};
     a.cam = *cam;
     a.d = *vao;
-    fill_consts(a.k, a.d);
+    fill_consts(a.k, a.d, p->num_directions);
     {
         rsd_status ts = snap_tables(a.d, &a.snapU, &a.snapV);
         if (ts == RSD_OK) ts = normal_lut(&a.nlut);
@@ -446,7 +446,7 @@ rsd_status pass2_impl(const rsd_camera* cam, const rsd_vao_data* vao, const rsd_
     SvaoArgs a{};
     a.cam = *cam;
     a.d = *vao;
-    fill_consts(a.k, a.d);
+    fill_consts(a.k, a.d, p->num_directions);
     {
         rsd_status ts = snap_tables(a.d, &a.snapU, &a.snapV);
         if (ts == RSD_OK) ts = normal_lut(&a.nlut);
@@ -475,13 +475,19 @@ rsd_status pass2_impl(const rsd_camera* cam, const rsd_vao_data* vao, const rsd_
     if (bandGroups == 0) return RSD_OK;
     dim3 grid((vw + kP2Tile - 1) / kP2Tile, (32 / kP2Tile) * bandGroups), block(kP2Lanes);
     hipStream_t s = (hipStream_t)stream;
+    const uint32_t nd = a.k.nd;
+#define RSD_P2(NN)                                                                                           \
+    if (nd == 32u) hipLaunchKernelGGL((svao_pass2_kernel<NN, 32>), grid, block, 0, s, a);                  \
+    else if (nd == 16u) hipLaunchKernelGGL((svao_pass2_kernel<NN, 16>), grid, block, 0, s, a);             \
+    else hipLaunchKernelGGL((svao_pass2_kernel<NN, 8>), grid, block, 0, s, a);
     switch (N) {
-        case 1: hipLaunchKernelGGL(svao_pass2_kernel<1>, grid, block, 0, s, a); break;
-        case 2: hipLaunchKernelGGL(svao_pass2_kernel<2>, grid, block, 0, s, a); break;
-        case 4: hipLaunchKernelGGL(svao_pass2_kernel<4>, grid, block, 0, s, a); break;
-        case 8: hipLaunchKernelGGL(svao_pass2_kernel<8>, grid, block, 0, s, a); break;
-        default: hipLaunchKernelGGL(svao_pass2_kernel<16>, grid, block, 0, s, a); break;
+        case 1: RSD_P2(1) break;
+        case 2: RSD_P2(2) break;
+        case 4: RSD_P2(4) break;
+        case 8: RSD_P2(8) break;
+        default: RSD_P2(16) break;
     }
+#undef RSD_P2
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? RSD_OK : hip_fail(e, "svao_pass2_kernel launch");
 }

@@ -12,20 +12,24 @@
 
 namespace rsd {
 
+constexpr int kMaxDirections = 32;  // NUM_DIRECTIONS: 8, 16 or 32 (Common.slang:51-58)
+
 struct SvaoConsts {
     float sinNoise[16], cosNoise[16];
-    float sinDir[8], cosDir[8];
-    float sampleRadius[8];
+    float sinDir[kMaxDirections], cosDir[kMaxDirections];
+    float sampleRadius[kMaxDirections];
     // SampleAOData::Init terms that only depend on the AO radius (Common.slang:358-363),
     // evaluated on the host with the device's float operations for radius == VAOData.radius
     // (every pixel whose screen radius is not clamped to ssMaxRadius)
-    float dirRadius[8], dirDx[8], dirDy[8], dirHeight[8];
+    float dirRadius[kMaxDirections], dirDx[kMaxDirections], dirDy[kMaxDirections], dirHeight[kMaxDirections];
     float ssrMin2;  // smallest float x with sqrtf(x) > ssRadiusCutoff: sqrtf(x) > c <=> x >= ssrMin2
     // RN(1 / pdf_i) and RN(1 / sphereHeight_i) of those terms (div_rcp); bit i of fastDiv set when
     // both divisors of direction i lie in [2^-30, 2^30]
-    float rcpPdf[8], rcpHeight[8];
+    float rcpPdf[kMaxDirections], rcpHeight[kMaxDirections];
     uint32_t fastDiv;
     uint32_t samePixelInt;  // isSamePixel decided on pixel indices (fill_consts)
+    uint32_t nd;            // NUM_DIRECTIONS
+    float invNd;            // 1.0 / float(NUM_DIRECTIONS) (SVAORaster.ps.slang:108, Common.slang:660)
 };
 
 struct SvaoArgs {
@@ -36,7 +40,7 @@ struct SvaoArgs {
     const uint16_t* normals;
     int W, H;
     uint8_t* ao;
-    uint8_t* stencil;
+    uint8_t* stencil;  // NUM_DIRECTIONS / 8 bytes per pixel: R8Uint / R16Uint / R32Uint (SVAO.cpp:132-134)
     uint32_t* rayMin;
     uint32_t* rayMax;
     const float* sd;
@@ -120,6 +124,18 @@ __device__ __forceinline__ float depth_center(const SvaoArgs& a, float u, float 
     if (a.W <= 4096 && a.H <= 4096)
         return a.depth[(size_t)min(max(ky, 0), a.H - 1) * a.W + min(max(kx, 0), a.W - 1)];
     return depth_sample(a, u, v);
+}
+
+// the stencil bitmask of pixel o (one bit per direction)
+__device__ __forceinline__ uint32_t stencil_load(const SvaoArgs& a, size_t o) {
+    if (a.k.nd == 32u) return reinterpret_cast<const uint32_t*>(a.stencil)[o];
+    if (a.k.nd == 16u) return reinterpret_cast<const uint16_t*>(a.stencil)[o];
+    return a.stencil[o];
+}
+__device__ __forceinline__ void stencil_store(const SvaoArgs& a, size_t o, uint32_t m) {
+    if (a.k.nd == 32u) reinterpret_cast<uint32_t*>(a.stencil)[o] = m;
+    else if (a.k.nd == 16u) reinterpret_cast<uint16_t*>(a.stencil)[o] = (uint16_t)m;
+    else a.stencil[o] = (uint8_t)m;
 }
 
 // Common.slang:285-324
@@ -263,7 +279,7 @@ inline void fill_scale(SvaoArgs& a) {
     a.isy = 0.5f * (a.cam.frameHeight / a.cam.focalLength);
 }
 
-inline void fill_consts(SvaoConsts& k, const rsd_vao_data& d) {
+inline void fill_consts(SvaoConsts& k, const rsd_vao_data& d, uint32_t nd) {
     // SVAO.cpp:670-684 -> R8Unorm noise; Common.slang:311-312 randRotation, :357 alpha
     static const float dither[16] = {0.0f, 8.0f, 2.0f, 10.0f, 12.0f, 4.0f, 14.0f, 6.0f,
                                      3.0f, 11.0f, 1.0f, 9.0f, 15.0f, 7.0f, 13.0f, 5.0f};
@@ -273,13 +289,33 @@ inline void fill_consts(SvaoConsts& k, const rsd_vao_data& d) {
         k.sinNoise[i] = (float)std::sin((double)rr);
         k.cosNoise[i] = (float)std::cos((double)rr);
     }
+    // Common.slang:52-58 (VAO kernel): the 16 / 32 tables are double literals there, rounded to float
     static const float radius8[8] = {0.917883f, 0.564429f, 0.734504f, 0.359545f,
-                                     0.820004f, 0.470149f, 0.650919f, 0.205215f};  // Common.slang:53
-    for (int i = 0; i < 8; ++i) {
-        const float al = ((float)i / 8.0f) * 2.0f * 3.141f;
+                                     0.820004f, 0.470149f, 0.650919f, 0.205215f};
+    static const float radius16[16] = {
+        0.949098221604059, 0.5865639019441775, 0.7554681720909893, 0.3895439574863043,
+        0.8425560503012255, 0.4948003867747738, 0.6719196866381647, 0.25203100417434543,
+        0.8908588816103737, 0.5418210823278604, 0.7136427497994143, 0.32724136087586453,
+        0.7980920320691521, 0.4445340224611676, 0.6297373536812639, 0.1447182620692375,
+    };
+    static const float radius32[32] = {
+        0.9682458365518543, 0.5974803093982587, 0.7660169295429302, 0.4038472576817624,
+        0.8541535023444914, 0.5068159098187986, 0.6823727109604635, 0.2726076670970059,
+        0.904018191941786, 0.5531894754180758, 0.7240656647095169, 0.34372202910162664,
+        0.8089818132350507, 0.45747336127867605, 0.640354849019649, 0.17748061996818404,
+        0.9327350969376332, 0.5755500192397054, 0.7449678114312224, 0.37479566486456295,
+        0.8311856199411515, 0.4825843210309559, 0.6614378277661477, 0.22975243551455923,
+        0.878233108646881, 0.5303115209931901, 0.7032256306171377, 0.3099952198410562,
+        0.7873133907642258, 0.43130429537268, 0.6190581352335289, 0.10219580968897692,
+    };
+    k.nd = nd == 16u || nd == 32u ? nd : 8u;
+    k.invNd = 1.0f / (float)k.nd;
+    const float* radius = k.nd == 32u ? radius32 : k.nd == 16u ? radius16 : radius8;
+    for (int i = 0; i < (int)k.nd; ++i) {
+        const float al = ((float)i / (float)k.nd) * 2.0f * 3.141f;  // Common.slang:357
         k.sinDir[i] = (float)std::sin((double)al);
         k.cosDir[i] = (float)std::cos((double)al);
-        k.sampleRadius[i] = radius8[i];
+        k.sampleRadius[i] = radius[i];
         // Common.slang:358-361 at radius = VAOData.radius (float ops as on the device)
         k.dirRadius[i] = k.sampleRadius[i] * d.radius;
         k.dirDx[i] = k.dirRadius[i] * k.sinDir[i];
@@ -300,7 +336,7 @@ inline void fill_consts(SvaoConsts& k, const rsd_vao_data& d) {
     // they differ (difference >= 1 / res - 2^-21 > 0.9 / res) for res <= 2^18
     k.samePixelInt = d.resolution[0] <= 262144.0f && d.resolution[1] <= 262144.0f;
     k.fastDiv = 0u;
-    for (int i = 0; i < 8; ++i) {
+    for (int i = 0; i < (int)k.nd; ++i) {
         const float pdf = 2.0f * k.dirHeight[i], h = k.dirHeight[i];
         k.rcpPdf[i] = (float)(1.0 / (double)pdf);
         k.rcpHeight[i] = (float)(1.0 / (double)h);
@@ -320,8 +356,9 @@ inline rsd_status check_common(const rsd_camera* cam, const rsd_vao_data* vao, c
         set_error(std::string(who) + ": null argument or empty extent");
         return RSD_ERR_INVALID_ARG;
     }
-    if (p->num_directions != 8) {
-        set_error(std::string(who) + ": only NUM_DIRECTIONS = 8 (the SVAO default) is implemented");
+    if (p->num_directions != 8 && p->num_directions != 16 && p->num_directions != 32) {
+        // Common.slang:51-58 holds sample radii for 8, 16 and 32 directions only
+        set_error(std::string(who) + ": NUM_DIRECTIONS must be 8, 16 or 32");
         return RSD_ERR_UNSUPPORTED;
     }
     if (2 * p->guard_band >= W || 2 * p->guard_band >= H) {

@@ -187,8 +187,8 @@ __device__ __forceinline__ void rt_dir(const RtArgs& ra, const Basic& b, float u
 __global__ void __launch_bounds__(64) svao_pass2_rt_kernel(RtArgs ra) {
     __shared__ uint32_t sItem[kLdsStack * 64];
     __shared__ float sT[kLdsStack * 64];
-    __shared__ uint32_t sPix[64];    // slot: local pixel | mask << 8
-    __shared__ uint16_t sPair[512];  // slot << 3 | direction
+    __shared__ uint32_t sPix[64];                    // slot: local pixel
+    __shared__ uint16_t sPair[kMaxDirections * 64];  // slot << 5 | direction
     __shared__ uint16_t sFirst[64];
     __shared__ float sAcc[64], sP[64], sR[64];
     __shared__ uint32_t sNPix, sNPair;
@@ -206,15 +206,15 @@ __global__ void __launch_bounds__(64) svao_pass2_rt_kernel(RtArgs ra) {
     __syncthreads();
     {
         const uint32_t px = x0 + lane % 8u, py = y0 + lane / 8u;
-        const uint32_t m = (px < xEnd && py < yEnd) ? a.stencil[(size_t)py * a.W + px] : 0u;
+        const uint32_t m = (px < xEnd && py < yEnd) ? stencil_load(a, (size_t)py * a.W + px) : 0u;
         if (m) {
             const uint32_t slot = atomicAdd(&sNPix, 1u), base = atomicAdd(&sNPair, (uint32_t)__popc(m));
-            sPix[slot] = lane | (m << 8);
+            sPix[slot] = lane;
             sFirst[slot] = (uint16_t)base;
             sAcc[slot] = 0.0f;
             uint32_t j = base;
-            for (int i = 0; i < 8; ++i)
-                if (m & (1u << i)) sPair[j++] = (uint16_t)(slot << 3 | i);
+            for (int i = 0; i < (int)a.k.nd; ++i)
+                if (m & (1u << i)) sPair[j++] = (uint16_t)(slot << 5 | i);
         }
     }
     __syncthreads();
@@ -224,21 +224,21 @@ __global__ void __launch_bounds__(64) svao_pass2_rt_kernel(RtArgs ra) {
         uint32_t slot = 0;
         if (k < nPair) {
             const uint32_t e = sPair[k];
-            slot = e >> 3;
+            slot = e >> 5;
             const uint32_t lp = sPix[slot] & 63u;
             const float u = ((float)(x0 + lp % 8u) + 0.5f) * d.invResolution[0];
             const float v = ((float)(y0 + lp / 8u) + 0.5f) * d.invResolution[1];
             Basic b;
             basic_init(a, u, v, b);
             float p, r;
-            rt_dir(ra, b, u, v, (int)(e & 7u), p, r, &sItem[lane], &sT[lane]);
+            rt_dir(ra, b, u, v, (int)(e & 31u), p, r, &sItem[lane], &sT[lane]);
             sP[lane] = p;
             sR[lane] = r;
         }
         __syncthreads();
         if (k < nPair && k == max((uint32_t)sFirst[slot], c)) {
             float acc = sAcc[slot];
-            for (uint32_t j = k; j < nPair && j < c + 64u && (uint32_t)(sPair[j] >> 3) == slot; ++j)
+            for (uint32_t j = k; j < nPair && j < c + 64u && (uint32_t)(sPair[j] >> 5) == slot; ++j)
                 acc = (acc - sP[j - c]) + sR[j - c];
             sAcc[slot] = acc;
         }
@@ -248,7 +248,7 @@ __global__ void __launch_bounds__(64) svao_pass2_rt_kernel(RtArgs ra) {
         const uint32_t lp = sPix[lane] & 63u;
         const size_t o = (size_t)(y0 + lp / 8u) * a.W + (x0 + lp % 8u);
         float vis = sAcc[lane];
-        vis *= 1.0f / 8.0f;
+        vis *= a.k.invNd;  // Common.slang:660-661
         vis *= 2.0f;
         vis += unorm8_to_float(a.ao[o]);
         vis = acc_pow(vis, d.exponent);
@@ -280,7 +280,7 @@ extern "C" rsd_status rsd_svao_pass2_raytraced_band(rsd_scene* scene, const rsd_
     SvaoArgs& a = ra.s;
     a.cam = *cam;
     a.d = *vao;
-    fill_consts(a.k, a.d);
+    fill_consts(a.k, a.d, p->num_directions);
     {
         rsd_status ts = snap_tables(a.d, &a.snapU, &a.snapV);
         if (ts == RSD_OK) ts = normal_lut(&a.nlut);

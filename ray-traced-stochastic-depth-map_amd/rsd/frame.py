@@ -243,7 +243,9 @@ class Renderer:
         self.depth = torch.empty((H, W), dtype=torch.float32, device=dv)
         self.normals = torch.empty((H, W), dtype=torch.int16, device=dv)
         self.ao = torch.zeros((H, W), dtype=torch.uint8, device=dv)  # SVAO.cpp:307 clears on first use
-        self.stencil = torch.zeros((H, W), dtype=torch.uint8, device=dv)
+        # SVAO.cpp:132-134: R8Uint / R16Uint / R32Uint for 8 / 16 / 32 directions
+        st_dtype = {8: torch.uint8, 16: torch.int16, 32: torch.int32}[cfg.num_directions]
+        self.stencil = torch.zeros((H, W), dtype=st_dtype, device=dv)
         # rayMin / rayMax in one allocation: a sharded frame all-reduces both in one collective
         self.ray_minmax = torch.empty((2, self.sd_h, self.sd_w), dtype=torch.int32, device=dv)
         self.ray_min, self.ray_max = self.ray_minmax[0], self.ray_minmax[1]
@@ -377,7 +379,7 @@ class Renderer:
         t = self.torch
         t.cuda.synchronize()
         return dict(depth=self.depth.cpu().numpy(), normals=self.normals.cpu().numpy().view(np.uint16),
-                    ao=self.ao.cpu().numpy(), stencil=self.stencil.cpu().numpy(),
+                    ao=self.ao.cpu().numpy(), stencil=self.stencil.cpu().numpy().view({1: np.uint8, 2: np.uint16, 4: np.uint32}[self.stencil.element_size()]),
                     ray_min=self.ray_min.cpu().numpy().view(np.uint32),
                     ray_max=self.ray_max.cpu().numpy().view(np.uint32), sd=self.sd.cpu().numpy())
 

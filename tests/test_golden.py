@@ -23,11 +23,14 @@ def test_jitter_table_matches_reference(oracle):
             assert got == (f32(want[0]), f32(want[1]))
 
 
-def test_sample_radius_matches_reference(oracle):
-    # SVAO/Common.slang:53 (NUM_DIRECTIONS = 8, VAO kernel)
-    table = GOLDEN["sampleRadius"]["VAO"]["8"]
+@pytest.mark.parametrize("n", [8, 16, 32])
+def test_sample_radius_matches_reference(oracle, n):
+    # SVAO/Common.slang:52-58 (NUM_DIRECTIONS = 8 / 16 / 32, VAO kernel; the shader's float constants)
+    table = GOLDEN["sampleRadius"]["VAO"][str(n)]
+    assert len(table) == n
     for i, r in enumerate(table):
-        assert oracle.sample_radius(8, i) == f32(r)
+        assert oracle.sample_radius(n, i) == f32(r)
+    assert oracle.sample_radius(n, n) == 0.0  # out of range
 
 
 def vdc(n, base=2):

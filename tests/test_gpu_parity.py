@@ -412,3 +412,54 @@ def test_sd_trace_on_many_streams(device, oracle):
             r.sd_trace(throughput=bool(k % 2))
         torch.cuda.current_stream().wait_stream(st)
         assert np.array_equal(r.numpy()["sd"].view(np.uint32), ref), k
+
+
+# ---- NUM_DIRECTIONS 16 / 32 (Common.slang:51-58; R16Uint / R32Uint stencils, SVAO.cpp:132-134) ----
+
+@pytest.mark.parametrize("nd", [16, 32])
+@pytest.mark.parametrize("N,divisor", [(4, 2), (8, 1)])
+def test_directions_full_frame_parity(device, oracle, nd, N, divisor):
+    cfg = small_frame_config(visible=(224, 128), guard=32, divisor=divisor, N=N)
+    cfg.num_directions = nd
+    r, osc = renderer("arcade_tiny", cfg, device, oracle)
+    r.gbuffer()
+    r.frame()
+    g = r.numpy()
+    cam, vao, sdp, svp = oracle_structs(r, oracle)
+    assert svp.num_directions == nd
+    o = oracle_frame(oracle, osc, cam, vao, sdp, svp, cfg.fb_w, cfg.fb_h, r.sd_w, r.sd_h)
+    assert g["stencil"].dtype == o["stencil"].dtype == {16: np.uint16, 32: np.uint32}[nd]
+    assert np.array_equal(g["stencil"], o["stencil"])
+    assert (o["stencil"] >> 8 != 0).sum() > 50, "no direction above 8 refined: the frame is degenerate"
+    assert np.array_equal(g["ray_min"], o["ray_min"]) and np.array_equal(g["ray_max"], o["ray_max"])
+    assert bits_equal(g["sd"], o["sd"])
+    gv = slice(cfg.guard_band, cfg.fb_h - cfg.guard_band), slice(cfg.guard_band, cfg.fb_w - cfg.guard_band)
+    assert np.array_equal(g["ao"][gv], o["ao"][gv])
+
+
+@pytest.mark.parametrize("nd", [16, 32])
+def test_directions_raytraced_parity(device, oracle, nd):
+    from rsd import abi
+    cfg = small_frame_config(visible=(160, 96), guard=16, divisor=1)
+    cfg.secondary = abi.DEPTH_RAYTRACED
+    cfg.num_directions = nd
+    r, osc = renderer("arcade_tiny", cfg, device, oracle)
+    r.gbuffer()
+    r.frame()
+    g = r.numpy()
+    cam, vao, sdp, svp = oracle_structs(r, oracle)
+    z, n = oracle.gbuffer(osc, cam, cfg.fb_w, cfg.fb_h, cfg.cull_mode)
+    ao1, st, _, _ = oracle.svao_pass1(cam, vao, svp, z, n, r.sd_w, r.sd_h)
+    assert np.array_equal(g["stencil"], st)
+    ao = oracle.svao_pass2_raytraced(osc, cam, vao, svp, z, n, st, ao1, cull=cfg.cull_mode, ray_pipeline=1)
+    assert np.array_equal(g["ao"], ao)
+
+
+def test_directions_unsupported(device, oracle):
+    """Common.slang:51-58 has sample radii for 8, 16 and 32 directions only: librsd refuses others."""
+    cfg = small_frame_config(visible=(96, 64), guard=16, divisor=2)
+    r, _ = renderer("arcade_tiny", cfg, device, oracle)
+    r.gbuffer()
+    r.svp.num_directions = 12
+    with pytest.raises(Exception, match="NUM_DIRECTIONS"):
+        r.pass1()

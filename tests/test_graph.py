@@ -280,3 +280,29 @@ def test_deinterleave_shapes_plan():
     res = g.resources()
     assert res["Dei.texOut"] == (33, 18, 16, "R32Float")
     assert res["Int.texOut"] == (130, 70, 1, "R32Float")
+
+
+@pytest.mark.parametrize("n,fmt", [(8, "R8Uint"), (16, "R16Uint"), (32, "R32Uint")])
+def test_svao_stencil_format_by_directions(n, fmt):
+    """SVAO.cpp:132-134: the stencil holds one bit per direction (sampleCount 8 / 16 / 32)."""
+    g = rsdgraph.RenderGraph("svao")
+    g.create_pass("Z", "Source", {})
+    g.create_pass("N", "Source", {})
+    g.create_pass("AO", "SVAO", {"sampleCount": n})
+    g.add_edge("Z.z", "AO.depth")
+    g.add_edge("N.n", "AO.normals")
+    g.mark_output("AO.stencil")
+    g.plan(128, 96)
+    assert g.resources()["AO.stencil"][3] == fmt
+
+
+def test_svao_refuses_other_direction_counts():
+    g = rsdgraph.RenderGraph("svao")
+    g.create_pass("Z", "Source", {})
+    g.create_pass("N", "Source", {})
+    g.create_pass("AO", "SVAO", {"sampleCount": 12})
+    g.add_edge("Z.z", "AO.depth")
+    g.add_edge("N.n", "AO.normals")
+    g.mark_output("AO.ao")
+    with pytest.raises(abi.RsdError, match="sampleCount must be 8, 16 or 32"):
+        g.plan(128, 96)

@@ -243,3 +243,30 @@ def test_raytraced_ao_independent_of_bvh(oracle):
     assert np.array_equal(ao, ao2)
     assert not np.array_equal(ao, ao1)
     assert np.array_equal(ao[st == 0], ao1[st == 0])
+
+
+@pytest.mark.parametrize("nd", [16, 32])
+def test_oracle_pass1_direction_counts(oracle, nd):
+    """NUM_DIRECTIONS 16 / 32: the stencil widens to R16Uint / R32Uint and directions above 8 refine;
+    with secondaryDepthMode SingleDepth the AO is the per-direction mean (the same scene at 8, 16
+    and 32 directions gives close AO: the three radius tables sample the same disc)."""
+    from rsd.frame import FrameConfig, make_camera, make_vao, svao_params
+    from rsd.scenes import make_scene
+    from helpers import to_oracle
+    scene = make_scene("arcade_tiny")
+    osc = oracle.Scene(scene.positions, scene.indices, scene.flags)
+    out = {}
+    for n in (8, nd):
+        cfg = FrameConfig(visible_w=160, visible_h=96, guard_band=16, divisor=2, sd_samples=4, sd_guard_px=64,
+                          radius=1.0, num_directions=n)
+        cam = to_oracle(make_camera(scene, cfg), oracle.Camera)
+        vao, sdw, sdh = make_vao(cfg)
+        z, nrm = oracle.gbuffer(osc, cam, cfg.fb_w, cfg.fb_h, 1, threads=4)
+        ao, st, rmin, rmax = oracle.svao_pass1(cam, to_oracle(vao, oracle.VAOData),
+                                               to_oracle(svao_params(cfg), oracle.SVAOParams), z, nrm, sdw, sdh)
+        out[n] = (ao, st)
+    ao, st = out[nd]
+    assert st.dtype == {16: np.uint16, 32: np.uint32}[nd]
+    assert (st >> 8).any()  # directions above the eighth requested SD rays
+    a8 = out[8][0].astype(np.int32)
+    assert np.abs(ao.astype(np.int32) - a8)[out[8][1] == 0].mean() < 12  # same disc, finer sampling
