@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define RSD_ABI_VERSION 2
+#define RSD_ABI_VERSION 3
 
 typedef enum {
     RSD_OK = 0,
@@ -163,6 +163,8 @@ typedef struct {
     uint32_t ray_interval;         /* USE_RAY_INTERVAL */
     uint32_t sd_jitter;            /* SD_JITTER */
     uint32_t guard_band;           /* dict["guardBand"] from the GuardBand pass */
+    uint32_t dual_ao;              /* DUAL_AO (SVAO dualAO, SVAO.cpp:130): d_ao is RG8Unorm -- R bright, G dark
+                                      (SVAORaster.ps.slang:103, SVAORaster2.ps.slang:62), 2 bytes per pixel */
 } rsd_svao_params;
 
 /* Traversal counters of the last instrumented trace (roofline bytes) */

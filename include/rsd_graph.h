@@ -34,7 +34,8 @@ typedef struct rsd_graph rsd_graph;
 typedef enum {
     RSD_FMT_R32F = 0, RSD_FMT_RG32F = 1, RSD_FMT_RGBA32F = 2, RSD_FMT_R16U = 3,
     RSD_FMT_R8U = 4, RSD_FMT_R8UNORM = 5, RSD_FMT_R32U = 6, RSD_FMT_UNKNOWN = 7,
-    RSD_FMT_R16F = 8, RSD_FMT_RG16F = 9, RSD_FMT_RGBA16F = 10  /* StochasticDepthMapRT Use16Bit */
+    RSD_FMT_R16F = 8, RSD_FMT_RG16F = 9, RSD_FMT_RGBA16F = 10, /* StochasticDepthMapRT Use16Bit */
+    RSD_FMT_RG8UNORM = 11                                      /* SVAO ao with dualAO */
 } rsd_format;
 
 typedef struct {

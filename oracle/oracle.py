@@ -49,7 +49,7 @@ class VAOData(C.Structure):
 class SVAOParams(C.Structure):
     _fields_ = [("num_directions", C.c_uint32), ("sd_samples", C.c_uint32),
                 ("secondary_depth_mode", C.c_uint32), ("ray_interval", C.c_uint32),
-                ("sd_jitter", C.c_uint32), ("guard_band", C.c_uint32)]
+                ("sd_jitter", C.c_uint32), ("guard_band", C.c_uint32), ("dual_ao", C.c_uint32)]
 
 
 _lib = None
@@ -257,7 +257,7 @@ def stencil_dtype(num_directions):
 
 def svao_pass1(cam, vao: VAOData, p: SVAOParams, depth, normals, sdW, sdH):
     H, W = depth.shape
-    ao = np.zeros((H, W), np.uint8)
+    ao = np.zeros((H, W, 2) if p.dual_ao else (H, W), np.uint8)  # dualAO: RG8Unorm (bright, dark)
     st = np.zeros((H, W), stencil_dtype(p.num_directions))
     rmin = np.zeros((sdH, sdW), np.uint32)
     rmax = np.zeros((sdH, sdW), np.uint32)

@@ -1526,11 +1526,11 @@ static void o_pass1_impl(const ocam* cam, const ovao* d, const osvao_params* p,
             uint32_t px = ox + g, py = oy + g;
             float u = ((float)px + 0.5f) * d->invResolution[0];
             float v = ((float)py + 0.5f) * d->invResolution[1];
-            float aoOut = 0.0f;
+            float aoOut = 0.0f, aoD = 0.0f; /* ao_t: bright, dark (DUAL_AO, SVAORaster.ps.slang:13) */
             uint32_t st = 0;
             obasic b;
             if (!o_basic_init(&x, u, v, &b)) {
-                aoOut = 1.0f;
+                aoOut = aoD = 1.0f;
             } else {
                 for (uint32_t i = 0; i < x.nd; ++i) {
                     osample s;
@@ -1538,7 +1538,9 @@ static void o_pass1_impl(const ocam* cam, const ovao* d, const osvao_params* p,
                     /* isSamePixel, Common.slang:129-134 */
                     if (fabsf(u - s.rasterSamplePosUV[0]) < d->invResolution[0] * 0.9f &&
                         fabsf(v - s.rasterSamplePosUV[1]) < d->invResolution[1] * 0.9f) {
-                        aoOut += (s.sphereStart - s.sphereEnd) / s.pdf;
+                        float w = (s.sphereStart - s.sphereEnd) / s.pdf;
+                        aoOut += w;
+                        aoD += w;
                         continue;
                     }
                     /* SVAORaster.ps.slang:62-66: Raytraced mode with TRACE_OUT_OF_SCREEN (SVAO.h:104) */
@@ -1568,18 +1570,51 @@ static void o_pass1_impl(const ocam* cam, const ovao* d, const osvao_params* p,
                                 rayMax[o] = 1u;
                             }
                         }
+                    } else {
+                        aoD += s.visibility; /* darkmap, SVAORaster.ps.slang:101-104 */
                     }
                 }
                 aoOut *= 1.0f / (float)x.nd;  /* SVAORaster.ps.slang:108-109 */
                 aoOut *= 2.0f;
-                if (p->secondary_depth_mode == 0 || st == 0) aoOut = o_pow(aoOut, d->exponent);
+                aoD *= 1.0f / (float)x.nd;
+                aoD *= 2.0f;
+                if (p->secondary_depth_mode == 0 || st == 0) {
+                    aoOut = o_pow(aoOut, d->exponent);
+                    aoD = o_pow(aoD, d->exponent);
+                }
             }
             if (px < W && py < H) {
-                ao[(size_t)py * W + px] = o_unorm8(aoOut);
+                if (p->dual_ao) {
+                    ao[2 * ((size_t)py * W + px)] = o_unorm8(aoOut);
+                    ao[2 * ((size_t)py * W + px) + 1] = o_unorm8(aoD);
+                } else {
+                    ao[(size_t)py * W + px] = o_unorm8(aoOut);
+                }
                 o_stencil_set(stencil, (size_t)py * W + px, x.nd, st);
             }
         }
     (void)sdH;
+}
+
+/* SVAORaster2.ps.slang:60-64: the direction sums * 2 / NUM_DIRECTIONS (Common.slang:660-661) plus
+ * the pass-1 AO, dark = min(bright, dark) (DUAL_AO), finalize, store */
+static void o_ao_finish(const octx* x, uint8_t* ao, size_t o, float vis, float visD)
+{
+    const float e = x->d->exponent;
+    vis *= 1.0f / (float)x->nd;
+    vis *= 2.0f;
+    if (!x->p->dual_ao) {
+        vis += o_unorm8_to_float(ao[o]);
+        ao[o] = o_unorm8(o_pow(vis, e));
+        return;
+    }
+    visD *= 1.0f / (float)x->nd;
+    visD *= 2.0f;
+    vis += o_unorm8_to_float(ao[2 * o]);
+    visD += o_unorm8_to_float(ao[2 * o + 1]);
+    visD = o_min(vis, visD);
+    ao[2 * o] = o_unorm8(o_pow(vis, e));
+    ao[2 * o + 1] = o_unorm8(o_pow(visD, e));
 }
 
 /* SVAORaster2.ps.slang:48-65 -> calcAO2 (Common.slang:523-663), stochastic branch */
@@ -1607,7 +1642,7 @@ static void* o_pass2_rows(void* arg)
             float v = ((float)py + 0.5f) * d->invResolution[1];
             obasic b;
             o_basic_init(x, u, v, &b);
-            float vis = 0.0f;
+            float vis = 0.0f, visD = 0.0f; /* bright, dark (DUAL_AO) */
             for (uint32_t i = 0; i < x->nd; ++i) {
                 if (!(mask & (1u << i))) continue;
                 osample s;
@@ -1629,12 +1664,9 @@ static void* o_pass2_rows(void* arg)
                     o_add_sample(x, &b, &s, spV, 0);
                 }
                 vis += s.visibility;
+                visD += s.visibility;
             }
-            vis *= 1.0f / (float)x->nd;  /* Common.slang:660-661 */
-            vis *= 2.0f;
-            vis += o_unorm8_to_float(j->ao[o]);
-            vis = o_pow(vis, d->exponent);
-            j->ao[o] = o_unorm8(vis);
+            o_ao_finish(x, j->ao, o, vis, visD);
         }
     return NULL;
 }
@@ -1719,7 +1751,7 @@ static void* o_pass2_rt_rows(void* arg)
             float v = ((float)py + 0.5f) * d->invResolution[1];
             obasic b;
             o_basic_init(x, u, v, &b);
-            float vis = 0.0f;
+            float vis = 0.0f, visD = 0.0f; /* bright, dark (DUAL_AO) */
             for (uint32_t i = 0; i < x->nd; ++i) {
                 if (!(mask & (1u << i))) continue;
                 osample s;
@@ -1772,12 +1804,9 @@ static void* o_pass2_rt_rows(void* arg)
                                 (s.sphereStart - s.sphereEnd) / s.pdf;
                 s.visibility = o_min(s.visibility, o_min(sphereVis, haloVis));
                 vis += s.visibility;
+                visD += s.visibility;
             }
-            vis *= 1.0f / (float)x->nd;  /* Common.slang:660-661 */
-            vis *= 2.0f;
-            vis += o_unorm8_to_float(j->ao[o]);
-            vis = o_pow(vis, d->exponent);
-            j->ao[o] = o_unorm8(vis);
+            o_ao_finish(x, j->ao, o, vis, visD);
         }
     return NULL;
 }

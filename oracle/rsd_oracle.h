@@ -84,6 +84,7 @@ typedef struct {
     uint32_t ray_interval;     /* USE_RAY_INTERVAL */
     uint32_t sd_jitter;        /* SD_JITTER */
     uint32_t guard_band;       /* frame-buffer guard band (GuardBand pass) */
+    uint32_t dual_ao;          /* DUAL_AO: ao is RG8Unorm (bright, dark), 2 bytes per pixel */
 } osvao_params;
 
 typedef struct oscene oscene;

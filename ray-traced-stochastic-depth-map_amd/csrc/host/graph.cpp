@@ -136,7 +136,7 @@ size_t formatBytes(Format f) {
         case Format::R32Float: case Format::R32Uint: return 4;
         case Format::RG32Float: return 8;
         case Format::RGBA32Float: return 16;
-        case Format::R16Uint: case Format::R16Float: return 2;
+        case Format::R16Uint: case Format::R16Float: case Format::RG8Unorm: return 2;
         case Format::RG16Float: return 4;
         case Format::RGBA16Float: return 8;
         case Format::R8Uint: case Format::R8Unorm: return 1;
@@ -155,6 +155,7 @@ const char* formatName(Format f) {
         case Format::R16Float: return "R16Float";
         case Format::RG16Float: return "RG16Float";
         case Format::RGBA16Float: return "RGBA16Float";
+        case Format::RG8Unorm: return "RG8Unorm";
         default: return "Unknown";
     }
 }

@@ -55,7 +55,7 @@ private:
 
 // ---- resources
 enum class Format { R32Float, RG32Float, RGBA32Float, R16Uint, R8Uint, R8Unorm, R32Uint, Unknown,
-                    R16Float, RG16Float, RGBA16Float };
+                    R16Float, RG16Float, RGBA16Float, RG8Unorm };
 size_t formatBytes(Format f);
 const char* formatName(Format f);
 

@@ -318,7 +318,6 @@ public:
     void checkSupported() const {
         if (primary_ != 0) throw Unsupported("SVAO: primaryDepthMode other than SingleDepth is not implemented");
         if (secondary_ == 1) throw Unsupported("SVAO: secondaryDepthMode DualDepth is not implemented (SURVEY 8(f))");
-        if (dualAo_) throw Unsupported("SVAO: dualAO is not implemented");
         // Common.slang:51-58 holds sample radii for 8, 16 and 32 directions only
         if (directions_ != 8 && directions_ != 16 && directions_ != 32)
             throw Unsupported("SVAO: sampleCount must be 8, 16 or 32");
@@ -341,7 +340,9 @@ public:
         opt("depth2", "Linear Depth-buffer of second layer");
         r.addInput("normals", "View space normals, 2x8 octahedral").format = Format::R16Uint;
         opt("color", "Color for pixel importance");
-        r.addOutput("ao", "Ambient Occlusion").format = Format::R8Unorm;
+        // SVAO.cpp:129-131: RG8Unorm (bright, dark) with dualAO
+        r.addOutput("ao", "Ambient Occlusion (bright/dark if dualAO is enabled)").format =
+            dualAo_ ? Format::RG8Unorm : Format::R8Unorm;
         // NUM_DIRECTIONS 8 / 16 / 32 -> R8Uint / R16Uint / R32Uint (SVAO.cpp:132-135)
         r.addOutput("stencil", "Stencil Bitmask for primary / secondary ao").format =
             directions_ > 16 ? Format::R32Uint : directions_ > 8 ? Format::R16Uint : Format::R8Uint;
@@ -362,7 +363,8 @@ public:
         width_ = cd.defaultWidth;
         height_ = cd.defaultHeight;
         sdSize(width_, height_, &vao_, &sdW_, &sdH_);
-        svp_ = rsd_svao_params{directions_, samples_, secondary_, (uint32_t)rayInterval_, (uint32_t)jitter_, 0};
+        svp_ = rsd_svao_params{directions_, samples_, secondary_, (uint32_t)rayInterval_, (uint32_t)jitter_, 0,
+                               (uint32_t)dualAo_};
         sdGraph_.reset();
         if (secondary_ != 2) return;
         // SVAO.cpp:157-189: the nested "Stochastic Depth" graph

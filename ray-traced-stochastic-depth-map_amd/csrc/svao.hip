@@ -46,11 +46,11 @@ __global__ void __launch_bounds__(256) svao_pass1_kernel(SvaoArgs a) {
     const rsd_vao_data& d = a.d;
     const float u = ((float)px + 0.5f) * d.invResolution[0];
     const float v = ((float)py + 0.5f) * d.invResolution[1];
-    float ao = 0.0f;
+    float ao = 0.0f, aoD = 0.0f;  // bright, dark (DUAL_AO: SVAORaster.ps.slang:13 ao_t = float2)
     uint32_t st = 0;
     Basic b;
     if (!basic_init(a, u, v, b)) {
-        ao = 1.0f;
+        ao = aoD = 1.0f;
     } else {
 #pragma unroll 1
         for (int i = 0; i < (int)a.k.nd; ++i) {
@@ -61,7 +61,9 @@ __global__ void __launch_bounds__(256) svao_pass1_kernel(SvaoArgs a) {
                                                : (fabsf(u - s.ru) < d.invResolution[0] * 0.9f &&
                                                   fabsf(v - s.rv) < d.invResolution[1] * 0.9f);
             if (same) {
-                ao += div_pdf(s.sphereStart - s.sphereEnd, s);  // isSamePixel
+                const float w = div_pdf(s.sphereStart - s.sphereEnd, s);  // isSamePixel
+                ao += w;
+                aoD += w;
                 continue;
             }
             // SVAORaster.ps.slang:62-66: Raytraced mode with TRACE_OUT_OF_SCREEN (SVAO.h:104)
@@ -88,14 +90,21 @@ __global__ void __launch_bounds__(256) svao_pass1_kernel(SvaoArgs a) {
                         a.rayMax[o] = 1u;
                     }
                 }
+            } else {
+                aoD += s.visibility;  // darkmap: the dark channel keeps directions that need no ray
             }
         }
         ao *= a.k.invNd;  // SVAORaster.ps.slang:108-109
         ao *= 2.0f;
-        if (a.secondary == 0u || st == 0u) ao = acc_pow(ao, d.exponent);
+        aoD *= a.k.invNd;
+        aoD *= 2.0f;
+        if (a.secondary == 0u || st == 0u) {
+            ao = acc_pow(ao, d.exponent);
+            aoD = acc_pow(aoD, d.exponent);
+        }
     }
     if (px < (uint32_t)a.W && py < (uint32_t)a.H) {
-        a.ao[(size_t)py * a.W + px] = unorm8(ao);
+        ao_store(a, (size_t)py * a.W + px, ao, aoD);
         stencil_store(a, (size_t)py * a.W + px, st);
     }
 }
@@ -174,7 +183,8 @@ __global__ void __launch_bounds__(kP2Lanes) svao_pass2_kernel(SvaoArgs a) {
     __shared__ uint32_t sPix[L];        // active pixel slot: local index
     __shared__ uint16_t sPair[ND * L];  // pair: slot << 5 | direction
     __shared__ uint16_t sFirst[L];     // first pair of each slot
-    __shared__ float sAcc[L];          // running vis of each slot
+    __shared__ float sAcc[L];          // running vis of each slot (bright)
+    __shared__ float sAccD[L];         // ... dark channel (DUAL_AO)
     __shared__ float sP[L], sR[L];
     __shared__ Basic sBasic[L];        // the pixel's BasicAOData, evaluated once per pixel, not per pair
     __shared__ uint32_t sNPix, sNPair;
@@ -195,6 +205,7 @@ __global__ void __launch_bounds__(kP2Lanes) svao_pass2_kernel(SvaoArgs a) {
             sPix[slot] = tid;
             sFirst[slot] = (uint16_t)base;
             sAcc[slot] = 0.0f;
+            sAccD[slot] = 0.0f;
             uint32_t j = base;
             for (int i = 0; i < ND; ++i)
                 if (m & (1u << i)) sPair[j++] = (uint16_t)(slot << 5 | i);
@@ -226,22 +237,20 @@ __global__ void __launch_bounds__(kP2Lanes) svao_pass2_kernel(SvaoArgs a) {
         __syncthreads();
         // the lane of a pixel's first pair in this chunk applies its pairs in direction order
         if (k < nPair && k == max((uint32_t)sFirst[slot], c)) {
-            float acc = sAcc[slot];
-            for (uint32_t j = k; j < nPair && j < c + L && (uint32_t)(sPair[j] >> 5) == slot; ++j)
-                acc = (acc - sP[j - c]) + sR[j - c];
+            float acc = sAcc[slot], accD = sAccD[slot];
+            for (uint32_t j = k; j < nPair && j < c + L && (uint32_t)(sPair[j] >> 5) == slot; ++j) {
+                acc = (acc - sP[j - c]) + sR[j - c];  // calcAO2: visibility.x -= raster; visibility += refined
+                accD = accD + sR[j - c];
+            }
             sAcc[slot] = acc;
+            sAccD[slot] = accD;
         }
         __syncthreads();
     }
     for (uint32_t sl = tid; sl < nPix; sl += L) {
         const uint32_t lp = sPix[sl] & 255u;
         const size_t o = (size_t)(y0 + lp / T) * a.W + (x0 + lp % T);
-        float vis = sAcc[sl];
-        vis *= a.k.invNd;  // Common.slang:660-661
-        vis *= 2.0f;
-        vis += unorm8_to_float(a.ao[o]);
-        vis = acc_pow(vis, d.exponent);
-        a.ao[o] = unorm8(vis);
+        ao_finish(a, o, sAcc[sl], sAccD[sl]);
     }
 }
 
@@ -387,6 +396,7 @@ rsd_status pass1_impl(const rsd_camera* cam, const rsd_vao_data* vao, const rsd_
     a.sdH = (int)sd_h;
     a.guard = p->guard_band;
     a.secondary = p->secondary_depth_mode;
+    a.dual = p->dual_ao ? 1u : 0u;
     a.rayInterval = p->ray_interval;
     a.sdJitter = p->sd_jitter;
     a.N = p->sd_samples;
@@ -464,6 +474,7 @@ rsd_status pass2_impl(const rsd_camera* cam, const rsd_vao_data* vao, const rsd_
     a.sdH = (int)sd_h;
     a.guard = p->guard_band;
     a.secondary = p->secondary_depth_mode;
+    a.dual = p->dual_ao ? 1u : 0u;
     a.rayInterval = p->ray_interval;
     a.sdJitter = p->sd_jitter;
     a.N = N;

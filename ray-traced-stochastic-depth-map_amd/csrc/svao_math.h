@@ -46,6 +46,7 @@ struct SvaoArgs {
     const float* sd;
     int sdW, sdH;
     uint32_t guard, secondary, rayInterval, sdJitter, N;
+    uint32_t dual;  // DUAL_AO: ao holds (bright, dark) byte pairs (RG8Unorm)
     uint32_t bandIndex, bandCount;  // 32-row groups g (offset space) with g % count == index
     float isx, isy;  // imageScale (Common.slang:142), hoisted: 0.5 * (frameW / focal), same bits
     const float* snapU;  // getSnappedUV: snapU[k] = (k + 0.5f) / resolution.x for k in [0, resolution.x]
@@ -124,6 +125,33 @@ __device__ __forceinline__ float depth_center(const SvaoArgs& a, float u, float 
     if (a.W <= 4096 && a.H <= 4096)
         return a.depth[(size_t)min(max(ky, 0), a.H - 1) * a.W + min(max(kx, 0), a.W - 1)];
     return depth_sample(a, u, v);
+}
+
+// the AO of pixel o: one R8Unorm byte, or the (bright, dark) RG8Unorm pair with DUAL_AO
+__device__ __forceinline__ void ao_store(const SvaoArgs& a, size_t o, float bright, float dark) {
+    if (a.dual) reinterpret_cast<uchar2*>(a.ao)[o] = make_uchar2(unorm8(bright), unorm8(dark));
+    else a.ao[o] = unorm8(bright);
+}
+// pass 2's (and the Raytraced pass 2's) end of a refined pixel, SVAORaster2.ps.slang:60-64: the
+// direction sums (bright: sum of refined - raster visibility; dark: sum of refined) scaled by
+// 2 / NUM_DIRECTIONS (Common.slang:660-661), plus the pass-1 AO, dark = min(bright, dark), finalize
+__device__ __forceinline__ void ao_finish(const SvaoArgs& a, size_t o, float accB, float accD) {
+    float vb = accB;
+    vb *= a.k.invNd;
+    vb *= 2.0f;
+    if (!a.dual) {
+        vb += unorm8_to_float(a.ao[o]);
+        a.ao[o] = unorm8(acc_pow(vb, a.d.exponent));
+        return;
+    }
+    const uchar2 prev = reinterpret_cast<const uchar2*>(a.ao)[o];
+    float vd = accD;
+    vd *= a.k.invNd;
+    vd *= 2.0f;
+    vb += unorm8_to_float(prev.x);
+    vd += unorm8_to_float(prev.y);
+    vd = hmin(vb, vd);
+    reinterpret_cast<uchar2*>(a.ao)[o] = make_uchar2(unorm8(acc_pow(vb, a.d.exponent)), unorm8(acc_pow(vd, a.d.exponent)));
 }
 
 // the stencil bitmask of pixel o (one bit per direction)

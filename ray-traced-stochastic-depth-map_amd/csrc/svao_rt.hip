@@ -190,7 +190,7 @@ __global__ void __launch_bounds__(64) svao_pass2_rt_kernel(RtArgs ra) {
     __shared__ uint32_t sPix[64];                    // slot: local pixel
     __shared__ uint16_t sPair[kMaxDirections * 64];  // slot << 5 | direction
     __shared__ uint16_t sFirst[64];
-    __shared__ float sAcc[64], sP[64], sR[64];
+    __shared__ float sAcc[64], sAccD[64], sP[64], sR[64];  // bright / dark (DUAL_AO) sums
     __shared__ uint32_t sNPix, sNPair;
     const SvaoArgs& a = ra.s;
     const rsd_vao_data& d = a.d;
@@ -212,6 +212,7 @@ __global__ void __launch_bounds__(64) svao_pass2_rt_kernel(RtArgs ra) {
             sPix[slot] = lane;
             sFirst[slot] = (uint16_t)base;
             sAcc[slot] = 0.0f;
+            sAccD[slot] = 0.0f;
             uint32_t j = base;
             for (int i = 0; i < (int)a.k.nd; ++i)
                 if (m & (1u << i)) sPair[j++] = (uint16_t)(slot << 5 | i);
@@ -237,22 +238,20 @@ __global__ void __launch_bounds__(64) svao_pass2_rt_kernel(RtArgs ra) {
         }
         __syncthreads();
         if (k < nPair && k == max((uint32_t)sFirst[slot], c)) {
-            float acc = sAcc[slot];
-            for (uint32_t j = k; j < nPair && j < c + 64u && (uint32_t)(sPair[j] >> 5) == slot; ++j)
+            float acc = sAcc[slot], accD = sAccD[slot];
+            for (uint32_t j = k; j < nPair && j < c + 64u && (uint32_t)(sPair[j] >> 5) == slot; ++j) {
                 acc = (acc - sP[j - c]) + sR[j - c];
+                accD = accD + sR[j - c];
+            }
             sAcc[slot] = acc;
+            sAccD[slot] = accD;
         }
         __syncthreads();
     }
     if (lane < nPix) {
         const uint32_t lp = sPix[lane] & 63u;
         const size_t o = (size_t)(y0 + lp / 8u) * a.W + (x0 + lp % 8u);
-        float vis = sAcc[lane];
-        vis *= a.k.invNd;  // Common.slang:660-661
-        vis *= 2.0f;
-        vis += unorm8_to_float(a.ao[o]);
-        vis = acc_pow(vis, d.exponent);
-        a.ao[o] = unorm8(vis);
+        ao_finish(a, o, sAcc[lane], sAccD[lane]);
     }
 }
 
@@ -295,6 +294,7 @@ extern "C" rsd_status rsd_svao_pass2_raytraced_band(rsd_scene* scene, const rsd_
     a.stencil = const_cast<uint8_t*>(d_stencil);
     a.guard = p->guard_band;
     a.secondary = 3u;
+    a.dual = p->dual_ao ? 1u : 0u;
     a.bandIndex = band_index;
     a.bandCount = band_count;
     ra.nodes = scene->d_nodes;

@@ -82,7 +82,7 @@ class VAOData(C.Structure):
 class SVAOParams(C.Structure):
     _fields_ = [("num_directions", C.c_uint32), ("sd_samples", C.c_uint32),
                 ("secondary_depth_mode", C.c_uint32), ("ray_interval", C.c_uint32),
-                ("sd_jitter", C.c_uint32), ("guard_band", C.c_uint32)]
+                ("sd_jitter", C.c_uint32), ("guard_band", C.c_uint32), ("dual_ao", C.c_uint32)]
 
 
 class Counters(C.Structure):
@@ -127,7 +127,7 @@ GRAPH_EXPORTS = ["rsd_graph_create", "rsd_graph_destroy", "rsd_graph_create_pass
                  "rsd_deinterleave", "rsd_interleave", "rsd_ray_min_max_length"]
 
 FMT_R32F, FMT_RG32F, FMT_RGBA32F, FMT_R16U, FMT_R8U, FMT_R8UNORM, FMT_R32U, FMT_UNKNOWN = range(8)
-FMT_R16F, FMT_RG16F, FMT_RGBA16F = 8, 9, 10
+FMT_R16F, FMT_RG16F, FMT_RGBA16F, FMT_RG8UNORM = 8, 9, 10, 11
 
 
 class Texture(C.Structure):

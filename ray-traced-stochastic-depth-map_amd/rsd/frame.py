@@ -51,6 +51,7 @@ class FrameConfig:
     thickness: float = 0.0
     sd_guard_px: int = 512
     num_directions: int = 8
+    dual_ao: bool = False                  # SVAO dualAO (SVAO.cpp:130): ao is RG8Unorm (bright, dark)
     focal_length: float = 21.0
     frame_height: float = 24.0
     near: float = 0.1
@@ -144,7 +145,7 @@ def sd_params(cfg: FrameConfig, sd_guard: int) -> abi.SDParams:
 
 def svao_params(cfg: FrameConfig) -> abi.SVAOParams:
     return abi.SVAOParams(cfg.num_directions, cfg.sd_samples, cfg.secondary, int(cfg.ray_interval), int(cfg.jitter),
-                          cfg.guard_band)
+                          cfg.guard_band, int(cfg.dual_ao))
 
 
 class Device:
@@ -242,7 +243,8 @@ class Renderer:
         dv = torch.device("cuda", self.dev.index)
         self.depth = torch.empty((H, W), dtype=torch.float32, device=dv)
         self.normals = torch.empty((H, W), dtype=torch.int16, device=dv)
-        self.ao = torch.zeros((H, W), dtype=torch.uint8, device=dv)  # SVAO.cpp:307 clears on first use
+        # SVAO.cpp:307 clears on first use; dualAO: RG8Unorm (bright, dark)
+        self.ao = torch.zeros((H, W, 2) if cfg.dual_ao else (H, W), dtype=torch.uint8, device=dv)
         # SVAO.cpp:132-134: R8Uint / R16Uint / R32Uint for 8 / 16 / 32 directions
         st_dtype = {8: torch.uint8, 16: torch.int16, 32: torch.int32}[cfg.num_directions]
         self.stencil = torch.zeros((H, W), dtype=st_dtype, device=dv)

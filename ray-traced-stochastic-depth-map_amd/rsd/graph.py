@@ -29,7 +29,7 @@ from . import abi
 _FORMAT_DTYPE = {abi.FMT_R32F: ("float32", 1), abi.FMT_RG32F: ("float32", 2), abi.FMT_RGBA32F: ("float32", 4),
                  abi.FMT_R16U: ("int16", 1), abi.FMT_R8U: ("uint8", 1), abi.FMT_R8UNORM: ("uint8", 1),
                  abi.FMT_R32U: ("int32", 1), abi.FMT_R16F: ("float16", 1), abi.FMT_RG16F: ("float16", 2),
-                 abi.FMT_RGBA16F: ("float16", 4)}
+                 abi.FMT_RGBA16F: ("float16", 4), abi.FMT_RG8UNORM: ("uint8", 2)}
 
 
 def _props_json(props: dict | None) -> bytes:

@@ -463,3 +463,41 @@ def test_directions_unsupported(device, oracle):
     r.svp.num_directions = 12
     with pytest.raises(Exception, match="NUM_DIRECTIONS"):
         r.pass1()
+
+
+# ---- dualAO (SVAO.cpp:129-131: RG8Unorm bright / dark; SVAORaster.ps.slang:101-104, SVAORaster2.ps.slang:60-64) ----
+
+@pytest.mark.parametrize("nd", [8, 16])
+def test_dual_ao_full_frame_parity(device, oracle, nd):
+    cfg = small_frame_config(visible=(224, 128), guard=32, divisor=2, N=4)
+    cfg.dual_ao = True
+    cfg.num_directions = nd
+    r, osc = renderer("arcade_tiny", cfg, device, oracle)
+    r.gbuffer()
+    r.frame()
+    g = r.numpy()
+    cam, vao, sdp, svp = oracle_structs(r, oracle)
+    assert svp.dual_ao == 1
+    o = oracle_frame(oracle, osc, cam, vao, sdp, svp, cfg.fb_w, cfg.fb_h, r.sd_w, r.sd_h)
+    assert g["ao"].shape == o["ao"].shape == (cfg.fb_h, cfg.fb_w, 2)
+    assert np.array_equal(g["stencil"], o["stencil"])
+    gv = slice(cfg.guard_band, cfg.fb_h - cfg.guard_band), slice(cfg.guard_band, cfg.fb_w - cfg.guard_band)
+    assert np.array_equal(g["ao"][gv], o["ao"][gv])
+    assert (o["ao"][gv][..., 1] < o["ao"][gv][..., 0]).any()  # the dark channel differs somewhere
+
+
+def test_dual_ao_raytraced_parity(device, oracle):
+    from rsd import abi
+    cfg = small_frame_config(visible=(160, 96), guard=16, divisor=1)
+    cfg.secondary = abi.DEPTH_RAYTRACED
+    cfg.dual_ao = True
+    r, osc = renderer("arcade_tiny", cfg, device, oracle)
+    r.gbuffer()
+    r.frame()
+    g = r.numpy()
+    cam, vao, sdp, svp = oracle_structs(r, oracle)
+    z, n = oracle.gbuffer(osc, cam, cfg.fb_w, cfg.fb_h, cfg.cull_mode)
+    ao1, st, _, _ = oracle.svao_pass1(cam, vao, svp, z, n, r.sd_w, r.sd_h)
+    assert np.array_equal(g["stencil"], st)
+    ao = oracle.svao_pass2_raytraced(osc, cam, vao, svp, z, n, st, ao1, cull=cfg.cull_mode, ray_pipeline=1)
+    assert np.array_equal(g["ao"], ao)

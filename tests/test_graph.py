@@ -306,3 +306,17 @@ def test_svao_refuses_other_direction_counts():
     g.mark_output("AO.ao")
     with pytest.raises(abi.RsdError, match="sampleCount must be 8, 16 or 32"):
         g.plan(128, 96)
+
+
+def test_svao_dual_ao_output_format():
+    """SVAO.cpp:129-131: dualAO makes the ao output RG8Unorm (bright, dark)."""
+    for dual, fmt in ((False, "R8Unorm"), (True, "RG8Unorm")):
+        g = rsdgraph.RenderGraph("svao")
+        g.create_pass("Z", "Source", {})
+        g.create_pass("N", "Source", {})
+        g.create_pass("AO", "SVAO", {"dualAO": dual})
+        g.add_edge("Z.z", "AO.depth")
+        g.add_edge("N.n", "AO.normals")
+        g.mark_output("AO.ao")
+        g.plan(128, 96)
+        assert g.resources()["AO.ao"][3] == fmt

@@ -270,3 +270,31 @@ def test_oracle_pass1_direction_counts(oracle, nd):
     assert (st >> 8).any()  # directions above the eighth requested SD rays
     a8 = out[8][0].astype(np.int32)
     assert np.abs(ao.astype(np.int32) - a8)[out[8][1] == 0].mean() < 12  # same disc, finer sampling
+
+
+def test_oracle_dual_ao(oracle):
+    """dualAO (SVAORaster.ps.slang:13,101-104; SVAORaster2.ps.slang:60-64): the bright channel is the
+    single-channel AO bit for bit; the dark channel equals it where no direction needed a ray, and
+    after pass 2 dark <= bright everywhere."""
+    from rsd.frame import FrameConfig, make_camera, make_vao, sd_params, svao_params
+    from rsd.scenes import make_scene
+    from helpers import to_oracle
+    scene = make_scene("arcade_tiny")
+    osc = oracle.Scene(scene.positions, scene.indices, scene.flags)
+    res = {}
+    for dual in (False, True):
+        cfg = FrameConfig(visible_w=160, visible_h=96, guard_band=16, divisor=2, sd_samples=4, sd_guard_px=64,
+                          radius=1.0, dual_ao=dual)
+        cam = to_oracle(make_camera(scene, cfg), oracle.Camera)
+        vao, sdw, sdh = make_vao(cfg)
+        ov, svp = to_oracle(vao, oracle.VAOData), to_oracle(svao_params(cfg), oracle.SVAOParams)
+        z, nrm = oracle.gbuffer(osc, cam, cfg.fb_w, cfg.fb_h, 1, threads=4)
+        ao1, st, rmin, rmax = oracle.svao_pass1(cam, ov, svp, z, nrm, sdw, sdh)
+        sd, _ = oracle.sd_trace(osc, cam, to_oracle(sd_params(cfg, vao.sdGuard), oracle.SDParams), z, rmin, rmax,
+                                sdw, sdh, threads=4)
+        res[dual] = (ao1, st, oracle.svao_pass2(cam, ov, svp, z, nrm, st, sd, ao1, threads=4))
+    ao1, st, ao2 = res[True]
+    assert ao1.shape[-1] == 2 and ao2.shape[-1] == 2
+    assert np.array_equal(ao1[..., 0], res[False][0]) and np.array_equal(ao2[..., 0], res[False][2])
+    assert np.array_equal(ao1[..., 0][st == 0], ao1[..., 1][st == 0])
+    assert (st != 0).any() and (ao2[..., 1] <= ao2[..., 0]).all()
