@@ -186,7 +186,9 @@ __global__ void __launch_bounds__(kP2Lanes) svao_pass2_kernel(SvaoArgs a) {
     __shared__ float sAcc[L];          // running vis of each slot (bright)
     __shared__ float sAccD[L];         // ... dark channel (DUAL_AO)
     __shared__ float sP[L], sR[L];
-    __shared__ Basic sBasic[L];        // the pixel's BasicAOData, evaluated once per pixel, not per pair
+    // the pixel's BasicAOData, evaluated once per pixel, not per pair: the 16 floats pass 2 reads
+    // (posVLength, normalV, radiusInPixels stay out: 26 KB of LDS -> 6 workgroups per CU, not 5)
+    __shared__ float sBasic[L][16];
     __shared__ uint32_t sNPix, sNPair;
     const uint32_t tid = threadIdx.x;
     const rsd_vao_data& d = a.d;
@@ -214,7 +216,13 @@ __global__ void __launch_bounds__(kP2Lanes) svao_pass2_kernel(SvaoArgs a) {
             const float v = ((float)py + 0.5f) * d.invResolution[1];
             Basic b;
             basic_init(a, u, v, b);
-            sBasic[slot] = b;
+            float* q = sBasic[slot];
+            q[0] = b.posV.x; q[1] = b.posV.y; q[2] = b.posV.z;
+            q[3] = b.normal.x; q[4] = b.normal.y; q[5] = b.normal.z;
+            q[6] = b.tangent.x; q[7] = b.tangent.y; q[8] = b.tangent.z;
+            q[9] = b.bitangent.x; q[10] = b.bitangent.y; q[11] = b.bitangent.z;
+            q[12] = b.normalO.x; q[13] = b.normalO.y; q[14] = b.normalO.z;
+            q[15] = b.radius;
         }
     }
     __syncthreads();
@@ -228,7 +236,17 @@ __global__ void __launch_bounds__(kP2Lanes) svao_pass2_kernel(SvaoArgs a) {
             const uint32_t lp = sPix[slot] & 255u;
             const float u = ((float)(x0 + lp % T) + 0.5f) * d.invResolution[0];
             const float v = ((float)(y0 + lp / T) + 0.5f) * d.invResolution[1];
-            const Basic b = sBasic[slot];
+            const float* q = sBasic[slot];
+            Basic b;
+            b.posV = mk(q[0], q[1], q[2]);
+            b.normal = mk(q[3], q[4], q[5]);
+            b.tangent = mk(q[6], q[7], q[8]);
+            b.bitangent = mk(q[9], q[10], q[11]);
+            b.normalO = mk(q[12], q[13], q[14]);
+            b.radius = q[15];
+            b.posVLength = 0.0f;  // not read by pass 2
+            b.normalV = b.normal;
+            b.radiusInPixels = 0.0f;
             float p, r;
             svao_pass2_dir<N>(a, b, u, v, (int)(e & 31u), p, r);
             sP[tid] = p;
