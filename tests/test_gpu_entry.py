@@ -119,3 +119,4 @@ def test_scene_without_entry_grid(device, monkeypatch):
         r.pass1()
         maps.append(trace(r, monkeypatch, "on", None)[0])
     assert np.array_equal(maps[0], maps[1])
+
