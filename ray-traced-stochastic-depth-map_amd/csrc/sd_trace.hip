@@ -102,6 +102,9 @@ struct SDArgs {
     int entRmax;
     float entOrigin[3], entExtent;
     uint32_t* entQ;
+    // diagnostics (instrumented fused walk, RSD_TRACE_RAYLOG): 8 words per queue slot {texel, steps,
+    // nodes, leaves, keys found, clocks, TMax - TMin, TMin}
+    uint32_t* rayLog;
 };
 
 // entry_lookup results besides first << 4 | count
@@ -1229,7 +1232,7 @@ __global__ void __launch_bounds__(kBlock) sd_trace_row_kernel(SDArgs a, const fl
     float ku = 0.0f, kv = 0.0f;  // per lane: key l's barycentrics (fused walk: the hit terms' inputs)
     // ---- statistics (counters build)
     TraceStats st{0u, 0u, 0u};
-    uint32_t active = 0, hitsDelivered = 0, maxSteps = 0, raySteps = 0, maxNodes = 0, rayNodes = 0;
+    uint32_t active = 0, hitsDelivered = 0, maxSteps = 0, raySteps = 0, maxNodes = 0, rayNodes = 0, rayLeaves = 0;
     unsigned long long sumCycles = 0, maxCycles = 0, c0 = 0;
 
     unsigned long long tFetch = 0, tStep = 0, tResolve = 0, nStep = 0, nLoop = 0, tS0 = 0, tS1 = 0;
@@ -1272,6 +1275,7 @@ __global__ void __launch_bounds__(kBlock) sd_trace_row_kernel(SDArgs a, const fl
                     active += l == 0;
                     raySteps = 0;
                     rayNodes = 0;
+                    rayLeaves = 0;
                     c0 = __builtin_amdgcn_s_memtime();
                 }
             }
@@ -1343,6 +1347,7 @@ __global__ void __launch_bounds__(kBlock) sd_trace_row_kernel(SDArgs a, const fl
         //      re-checks each hit against the current K-th key)
         const uint32_t lc = isLeaf ? ((item >> 29) & 3u) + 1u : 0u;
         if (isLeaf) st.leaves++;
+        if (CNT && isLeaf) rayLeaves++;
         if (__ballot(lc != 0u) != 0ull) {
             float tj[4], uj[4], vj[4];
             uint32_t pj[4];
@@ -1491,9 +1496,23 @@ __global__ void __launch_bounds__(kBlock) sd_trace_row_kernel(SDArgs a, const fl
             maxNodes = max(maxNodes, n);
             maxSteps = max(maxSteps, raySteps);
             const unsigned long long dc = __builtin_amdgcn_s_memtime() - c0;
+            uint32_t nl = rayLeaves;
+#pragma unroll
+            for (int o = ROW / 2; o >= 1; o >>= 1) nl += __shfl_xor(nl, o);
             if (l == 0) {
                 sumCycles += dc;
                 maxCycles = dc > maxCycles ? dc : maxCycles;
+                if (a.rayLog) {
+                    uint32_t* g = a.rayLog + (size_t)slot * 8u;
+                    g[0] = (uint32_t)y * (uint32_t)a.sdW + (uint32_t)x;
+                    g[1] = raySteps;
+                    g[2] = n;
+                    g[3] = nl;
+                    g[4] = (uint32_t)found;
+                    g[5] = (uint32_t)min(dc, 0xffffffffull);
+                    g[6] = __float_as_uint(TMax - TMin);
+                    g[7] = __float_as_uint(TMin);
+                }
             }
         }
     }
@@ -1909,6 +1928,7 @@ rsd_status sd_trace_impl(rsd_scene* scene, const rsd_camera* cam, const rsd_sd_p
     for (int k = 0; k < 3; ++k) a.entOrigin[k] = scene->entry_origin[k];
     a.entExtent = scene->entry_extent;
     a.entQ = nullptr;
+    a.rayLog = nullptr;
     a.alphaData = scene->alpha;
     a.alphaData.spread = rsd_ray_cone_spread(cam->focalLength, sd_h);  // default texture dims = SD map
     if (p->implementation == RSD_SD_COVERAGE_MASK) {
@@ -1950,6 +1970,7 @@ rsd_status sd_trace_impl(rsd_scene* scene, const rsd_camera* cam, const rsd_sd_p
         RSD_HIP(hipMemsetAsync(ws->counters, 0, 24 * sizeof(unsigned long long), s));
         a.counters = ws->counters;
     }
+    const char* rayLogPath = counters ? std::getenv("RSD_TRACE_RAYLOG") : nullptr;  // diagnostics only
     const uint32_t tiles = (sd_h + kTile - 1) / kTile;
     dim3 grid((sd_w + kTile - 1) / kTile, consume ? tiles : n);
     // k = the MAX_COUNT nearest keys decide Default and KBuffer; coverage mask streams chunks
@@ -1975,6 +1996,11 @@ rsd_status sd_trace_impl(rsd_scene* scene, const rsd_camera* cam, const rsd_sd_p
     float4* queue = reinterpret_cast<float4*>(ws->queue);
     uint2* keys = reinterpret_cast<uint2*>(reinterpret_cast<char*>(ws->queue) + queueBytes);
     if (entBytes) a.entQ = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(ws->queue) + queueBytes + keyBytes);
+    const size_t rayLogBytes = rayLogPath && *rayLogPath ? need_q * 8 * sizeof(uint32_t) : 0;
+    if (rayLogBytes) {
+        RSD_HIP(hipMalloc(&a.rayLog, rayLogBytes));
+        RSD_HIP(hipMemsetAsync(a.rayLog, 0, rayLogBytes, s));
+    }
     // double-buffered queue control (sd_setup_kernel); both buffers are reset on first use and
     // after a failed launch sequence
     if (ws->qctl_dirty) {
@@ -2099,6 +2125,15 @@ rsd_status sd_trace_impl(rsd_scene* scene, const rsd_camera* cam, const rsd_sd_p
             if (*dbg) std::fprintf(stderr, "[rsd] row walk phase clocks: fetch %llu step %llu resolve %llu steps %llu loops %llu"
                                    " | step split: mem %llu compute %llu pool %llu\n",
                                    h[11], h[12], h[13], h[14], h[15], h[16], h[17], h[18]);
+        if (a.rayLog) {
+            std::vector<uint32_t> lg(rayLogBytes / 4);
+            RSD_HIP(hipMemcpy(lg.data(), a.rayLog, rayLogBytes, hipMemcpyDeviceToHost));
+            (void)hipFree(a.rayLog);
+            if (FILE* f = std::fopen(rayLogPath, "wb")) {
+                std::fwrite(lg.data(), 4, lg.size(), f);
+                std::fclose(f);
+            }
+        }
         if (h[10]) {  // the pool bound was violated: results of this trace are not reliable
             set_error("rsd_sd_trace: traversal pool overflow (BVH deeper than the row walk supports)");
             return RSD_ERR_HIP;
