@@ -2,6 +2,7 @@
 #include "bvh_build.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <atomic>
 #include <chrono>
 #include <cmath>
@@ -45,7 +46,13 @@ struct TNode {             // temporary binary-tree node
 };
 
 constexpr int kBins = 32;
-constexpr double kTraversalCost = 1.0;  // relative to one triangle test
+constexpr double kTraversalCostDefault = 1.0;  // relative to one triangle test
+// RSD_BVH_TCOST overrides the SAH traversal cost (build-quality experiments; results do not depend
+// on the tree for canonical traces)
+const double kTraversalCost = [] {
+    const char* e = std::getenv("RSD_BVH_TCOST");
+    return e && std::atof(e) > 0.0 ? std::atof(e) : kTraversalCostDefault;
+}();
 
 struct Builder {
     const std::vector<Aabb>& tb;       // triangle boxes
