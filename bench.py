@@ -251,18 +251,21 @@ def main():
     # frame mode: every rank renders whole frames; band mode: the ranks share each frame
     units = world if shard == "frame" else 1
     rays_active = mean_cnt(cnt_seq, "rays_active")
+    # the segment entry grid's lookups: one 16-B hash slot + 32 B per frontier item tested
+    entry_bytes = 16 * mean_cnt(cnt_seq, "entry_lookups") + 32 * mean_cnt(cnt_seq, "entry_items")
     if dist and shard != "frame":  # counters are per band: the frame's totals
-        t = torch.tensor([rays_active, mean_cnt(cnt_seq, "nodes_visited"), mean_cnt(cnt_seq, "tris_tested")],
-                         device="cuda", dtype=torch.float64)
+        t = torch.tensor([rays_active, mean_cnt(cnt_seq, "nodes_visited"), mean_cnt(cnt_seq, "tris_tested"),
+                          entry_bytes], device="cuda", dtype=torch.float64)
         dist.all_reduce(t)
-        rays_active, nodes_seq, tris_seq = t.tolist()
+        rays_active, nodes_seq, tris_seq, entry_bytes = t.tolist()
     else:
         nodes_seq, tris_seq = mean_cnt(cnt_seq, "nodes_visited"), mean_cnt(cnt_seq, "tris_tested")
     value = units * rays / (seq_sd_ms * 1e-3) / 1e6
-    # B_ray = 16 (linearZ bilinear) + 8 (rayMin+rayMax) + 4N (store) + node bytes + 48 n_tri;
+    # B_ray = 16 (linearZ bilinear) + 8 (rayMin+rayMax) + 4N (store) + node bytes + 48 n_tri
+    # (+ the entry grid's lookups, which replace the top of the walk);
     # librsd's nodes are 4-wide (128 B per visit = two of SURVEY's 64-B BVH2 nodes).  Per launch =
     # per frame (band mode: the whole frame's bytes over the slowest rank's trace time).
-    alg_bytes = rays * (16 + 8 + 4 * N) + 128 * nodes_seq + 48 * tris_seq
+    alg_bytes = rays * (16 + 8 + 4 * N) + 128 * nodes_seq + 48 * tris_seq + entry_bytes
     achieved = alg_bytes / (seq_sd_ms * 1e-3) / 1e9
     kernels_seq = abi.WALK_KERNELS[walk_seq]
     pmc = args.pmc_csv

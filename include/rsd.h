@@ -180,6 +180,8 @@ typedef struct {
     uint64_t max_ray_clocks;    /* the slowest live ray */
     uint64_t leaves_visited;    /* leaf steps (<= 4 triangle records each) */
     uint64_t walk;              /* traversal walk of the trace: RSD_WALK_* */
+    uint64_t entry_lookups;     /* segment entry-grid lookups (one 16-B hash slot each, first probe) */
+    uint64_t entry_items;       /* frontier items tested by the setup kernel (32 B each) */
 } rsd_counters;
 /* rsd_counters.walk: which kernels an rsd_sd_trace launched (besides sd_setup_kernel) */
 #define RSD_WALK_QUAD 0u   /* sd_trace_queue_kernel: depth-first, 4 lanes per ray */

@@ -574,6 +574,10 @@ __global__ void __launch_bounds__(kSetupWaves * kBlock) sd_setup_kernel(SDArgs a
         if (live && a.entOn) {
             const f3 o = mk(a.cam.posW[0], a.cam.posW[1], a.cam.posW[2]);
             ent = entry_lookup(a, o, d, TMin, TMax);
+            if (a.counters) {  // roofline bytes of the lookup (rsd_counters.entry_*)
+                atomicAdd(&a.counters[19], 1ull);
+                if (ent != kEntryRoot && ent != kEntryDead) atomicAdd(&a.counters[20], (unsigned long long)(ent & 15u));
+            }
             if (ent != kEntryRoot && ent != kEntryDead) {
                 // the frontier items whose boxes the ray passes (the walk's own child test)
                 RayCtx r;
@@ -2121,6 +2125,8 @@ rsd_status sd_trace_impl(rsd_scene* scene, const rsd_camera* cam, const rsd_sd_p
         counters->max_ray_clocks = h[8];
         counters->leaves_visited = h[9];
         counters->walk = (uint64_t)walk;
+        counters->entry_lookups = h[19];
+        counters->entry_items = h[20];
         if (const char* dbg = std::getenv("RSD_TRACE_PHASES"))
             if (*dbg) std::fprintf(stderr, "[rsd] row walk phase clocks: fetch %llu step %llu resolve %llu steps %llu loops %llu"
                                    " | step split: mem %llu compute %llu pool %llu\n",

@@ -89,7 +89,8 @@ class Counters(C.Structure):
     _fields_ = [("rays_dispatched", C.c_uint64), ("rays_active", C.c_uint64), ("nodes_visited", C.c_uint64),
                 ("tris_tested", C.c_uint64), ("hits_delivered", C.c_uint64), ("max_nodes_per_ray", C.c_uint64),
                 ("max_steps_per_ray", C.c_uint64), ("sum_ray_clocks", C.c_uint64), ("max_ray_clocks", C.c_uint64),
-                ("leaves_visited", C.c_uint64), ("walk", C.c_uint64)]
+                ("leaves_visited", C.c_uint64), ("walk", C.c_uint64), ("entry_lookups", C.c_uint64),
+                ("entry_items", C.c_uint64)]
 
 
 WALK_QUAD, WALK_FUSED, WALK_SPLIT, WALK_ORDERED, WALK_RASTER = 0, 1, 2, 3, 4
