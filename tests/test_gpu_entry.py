@@ -120,3 +120,36 @@ def test_scene_without_entry_grid(device, monkeypatch):
         maps.append(trace(r, monkeypatch, "on", None)[0])
     assert np.array_equal(maps[0], maps[1])
 
+
+
+@pytest.mark.parametrize("offset", [(3000.0, -500.0, 7000.0), (-40000.0, 0.0, 25000.0)])
+def test_entry_grid_far_from_origin(device, oracle, monkeypatch, offset):
+    """The scene and camera translated far from the origin: coarser float spacing in the setup's
+    lookup (segment box pad, cell index) must still only change where the walk starts."""
+    import dataclasses
+    from rsd.frame import GpuScene, Renderer
+    from rsd.scenes import make_scene
+    s0 = make_scene("arcade_tiny")
+    off = np.asarray(offset, np.float32)
+    cam = dict(s0.camera)
+    cam["pos"] = [float(a + b) for a, b in zip(cam["pos"], off)]
+    cam["target"] = [float(a + b) for a, b in zip(cam["target"], off)]
+    s = dataclasses.replace(s0, name="arcade_far", positions=(s0.positions + off).astype(np.float32), camera=cam)
+    gs = GpuScene(device, s)
+    assert gs.info.entry_cells > 0
+    cfg = small_frame_config(visible=(192, 112), guard=32, divisor=2, N=4, max_count=8)
+    r = Renderer(s, cfg, dev=device, gpu_scene=gs)
+    r.gbuffer()
+    r.clear_intervals()
+    r.pass1()
+    on, c_on = trace(r, monkeypatch, "on", None)
+    off_, _ = trace(r, monkeypatch, "off", None)
+    q, _ = trace(r, monkeypatch, "on", "quad")
+    assert np.array_equal(on, off_) and np.array_equal(on, q)
+    assert c_on.rays_active > 0
+    g = r.numpy()
+    osc = oracle.Scene(s.positions, s.indices, s.flags)
+    sd, _ = oracle.sd_trace(osc, to_oracle(r.cam, oracle.Camera), to_oracle(r.sdp, oracle.SDParams), g["depth"],
+                            g["ray_min"], g["ray_max"], r.sd_w, r.sd_h)
+    assert np.array_equal(on, np.ascontiguousarray(sd).view(np.uint32))
+    gs.release()
