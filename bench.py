@@ -41,6 +41,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -106,7 +107,11 @@ def host_cpus():
             quota = round(int(q) / int(per), 2)
     except (OSError, ValueError):
         pass
-    return {"usable": usable, "nproc": os.cpu_count(), "cgroup_cpu_quota": quota, "model": model}
+    # the CPU time the process may actually use: the affinity mask capped by the cgroup quota
+    # (a 256-CPU mask under a 16-CPU quota runs at most 16 CPUs' worth of threads at once)
+    effective = usable if quota is None else max(1, min(usable, math.ceil(quota)))
+    return {"usable": usable, "nproc": os.cpu_count(), "cgroup_cpu_quota": quota, "effective": effective,
+            "model": model}
 
 
 def main():
@@ -425,7 +430,7 @@ def cpu_baseline(r, scene, target_s, poses=None):
     g = r.numpy()
     assert (g["ray_max"] != 0).any(), "the baseline frame has no live SD rays"
     cpus = host_cpus()
-    cores = cpus["usable"]
+    cores = cpus["effective"]
     osc = O.Scene(scene.positions, scene.indices, scene.flags)
     cam, sdp = to_oracle(r.cam, O.Camera), to_oracle(r.sdp, O.SDParams)
 
@@ -457,7 +462,8 @@ def cpu_baseline(r, scene, target_s, poses=None):
     what = "the frame's full SD trace" if (y0, y1) == (0, r.sd_h) else f"SD rows [{y0}, {y1}) of the frame"
     return {"value": round(n / dt / 1e6, 4), "unit": "Mrays/s", "cores": cores, "kind": "port",
             "sample": f"{what} ({n} rays, {int(stats[0])} live) x {reps} repetitions, oracle pthreads on "
-                      f"{cores} host threads (every CPU of the process's affinity mask)",
+                      f"{cores} host threads (= min(affinity mask {cpus['usable']} CPUs, ceil(cgroup quota "
+                      f"{cpus['cgroup_cpu_quota']})): the effective core count)",
             "active_mrays_per_s": round(float(stats[0]) / dt / 1e6, 4),
             "host": cpus, "seconds": round(dt * reps, 2), "bit_identical_to_gpu": same}
 

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define RSD_ABI_VERSION 3
+#define RSD_ABI_VERSION 4
 
 typedef enum {
     RSD_OK = 0,
@@ -165,7 +165,16 @@ typedef struct {
     uint32_t guard_band;           /* dict["guardBand"] from the GuardBand pass */
     uint32_t dual_ao;              /* DUAL_AO (SVAO dualAO, SVAO.cpp:130): d_ao is RG8Unorm -- R bright, G dark
                                       (SVAORaster.ps.slang:103, SVAORaster2.ps.slang:62), 2 bytes per pixel */
+    uint8_t* tile_flags;           /* ABI v4, optional (NULL = none): busy-tile flags, one byte per 16x16 tile
+                                      of the visible region (rsd_svao_tile_count), caller-owned, zeroed once.
+                                      Pass 1 sets the flag of every tile holding a stencilled pixel; pass 2
+                                      visits only flagged tiles and clears the flags it consumed (the
+                                      reference's pass 2 returns on aoMask == 0, SVAORaster2.ps.slang:50-52).
+                                      Pass 2 must get the flags of the pass 1 that wrote d_stencil. */
 } rsd_svao_params;
+/* Bytes of rsd_svao_params.tile_flags for a width x height frame buffer with guard_band: one per 16x16
+ * tile of the visible region rounded up to 32 rows (the padded pass-1 dispatch, SVAO.cpp:347-350). */
+uint32_t rsd_svao_tile_count(uint32_t width, uint32_t height, uint32_t guard_band);
 
 /* Traversal counters of the last instrumented trace (roofline bytes) */
 typedef struct {

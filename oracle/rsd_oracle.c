@@ -1955,7 +1955,9 @@ void ocpu_temporal_ao(const uint8_t* aoIn, const float* z, const float* mvec, co
 }
 
 /* GBufferRaster.mvec for a static scene and a moving camera (librsd's definition, rsd_graph.h):
- * the pixel-centre primary hit from the linear depth, projected with the previous camera. */
+ * the pixel-centre primary hit from the linear depth, projected with the previous camera.
+ * Background (linear depth >= farZ) -> (0, 0): GBufferRaster clears mvec (GBufferRaster.cpp:176)
+ * and writes it for rasterized geometry only (GBufferRaster.3d.slang:117). */
 void ocpu_motion_vectors(const ocam* c, const ocam* prev, const float* z, uint32_t W_, uint32_t H_, float* mvec)
 {
     const int W = (int)W_, H = (int)H_;
@@ -1973,6 +1975,11 @@ void ocpu_motion_vectors(const ocam* c, const ocam* prev, const float* z, uint32
         for (int x = 0; x < W; ++x) {
             const float u = ((float)x + 0.5f) / (float)W, v = ((float)y + 0.5f) / (float)H;
             float dn[3], d[3], rel[3];
+            if (!(z[(size_t)y * W + x] < c->farZ)) {
+                mvec[2 * ((size_t)y * W + x)] = 0.0f;
+                mvec[2 * ((size_t)y * W + x) + 1] = 0.0f;
+                continue;
+            }
             for (int k = 0; k < 3; ++k) dn[k] = (2.0f * u + -1.0f) * c->U[k] + (-2.0f * v + 1.0f) * c->V[k] + c->W[k];
             o_normalize(dn, d);
             const float t = z[(size_t)y * W + x] / o_dot(wn, d);

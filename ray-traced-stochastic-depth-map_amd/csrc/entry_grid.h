@@ -27,7 +27,9 @@
 namespace rsd {
 
 constexpr uint32_t kEntryCap = 8;         // frontier items per cell (one row-walk step)
-constexpr uint32_t kEntryMaxLevel = 18;   // cell indices + 1 fit 20 bits
+constexpr uint32_t kEntryMaxLevel = 14;   // level + 1 fits the key's 4 bits, cell indices + 1 its 20
+static_assert(kEntryMaxLevel + 1 < 16, "entry_key stores level + 1 in 4 bits (bits 60-63)");
+static_assert((1u << kEntryMaxLevel) + 1 < (1u << 20), "entry_key stores cell index + 1 in 20 bits");
 
 struct EntryGrid {
     float origin[3] = {0.0f, 0.0f, 0.0f};  // the cube's low corner (the root box's)

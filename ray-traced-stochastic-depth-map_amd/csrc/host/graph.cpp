@@ -327,9 +327,15 @@ void RenderGraph::compile(Context& ctx, uint32_t width, uint32_t height, bool al
         return passes_.at(p).refl.find(f);
     };
     std::map<std::string, Field> outs;  // "pass.field" -> field description
+    // optional outputs (Falcor RenderPassReflection Field::Flags::Optional) get a resource only when
+    // something reads them: an edge into a needed pass or a marked graph output
+    std::set<std::string> consumed(outputs_.begin(), outputs_.end());
+    for (auto& e : edges_)
+        if (!e.srcField.empty() && need.count(e.srcPass) && need.count(e.dstPass))
+            consumed.insert(e.srcPass + "." + e.srcField);
     for (auto& p : order_) {
         for (auto& f : passes_.at(p).refl.fields)
-            if (!f.isInput) outs[p + "." + f.name] = f;
+            if (!f.isInput && (!f.optional || consumed.count(p + "." + f.name))) outs[p + "." + f.name] = f;
     }
     auto stubOut = [&](const std::string& p, const std::string& f, Format hint) {
         const std::string key = p + "." + f;

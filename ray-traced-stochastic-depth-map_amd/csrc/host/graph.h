@@ -69,7 +69,7 @@ struct Texture {
 struct Field {
     std::string name, desc;
     bool isInput = true;
-    bool optional = false;
+    bool optional = false;  // input: may stay unconnected; output: allocated only when consumed
     Format format = Format::Unknown;  // Unknown: take it from the connected producer
     uint32_t width = 0, height = 0;  // 0: the graph's default dims
     uint32_t layers = 1;

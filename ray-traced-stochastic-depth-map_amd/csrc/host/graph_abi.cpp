@@ -112,7 +112,9 @@ rsd_status rsd_graph_set_scene(rsd_graph* g, rsd_scene* scene, const rsd_camera*
 rsd_status rsd_graph_set_input(rsd_graph* g, const char* name, const rsd_texture* tex) {
     if (!g || !name || !tex || !tex->ptr) return nullArg("rsd_graph_set_input");
     return guarded("rsd_graph_set_input", [&] {
-        if (tex->format > RSD_FMT_RGBA16F) throw std::runtime_error("bad format");
+        // every real format of rsd_format (RSD_FMT_UNKNOWN is a graph-internal placeholder)
+        if (tex->format > RSD_FMT_RG8UNORM || tex->format == RSD_FMT_UNKNOWN)
+            throw std::runtime_error("bad format");
         Texture& t = g->inputs[name];
         t.ptr = tex->ptr;
         t.width = tex->width;

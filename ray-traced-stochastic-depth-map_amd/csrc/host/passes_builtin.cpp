@@ -107,7 +107,9 @@ public:
         Reflection r;
         r.addOutput("depth", "Depth buffer (D32 non-linear, R32F here)").format = Format::R32Float;
         r.addOutput("faceNormalW", "Face normal in world space").format = Format::RGBA32Float;
-        r.addOutput("mvec", "Motion vector (uv units, RG32F)").format = Format::RG32Float;
+        Field& mv = r.addOutput("mvec", "Motion vector (uv units, RG32F)");
+        mv.format = Format::RG32Float;
+        mv.optional = true;  // GBuffer.cpp:48: mvec is an optional channel, computed only when read
         return r;
     }
     ~GBufferRasterPass() override { (void)hipFree(linZ_); }
@@ -128,6 +130,7 @@ public:
         prevCam_ = scene_->camera;
         hasPrev_ = true;
         Texture* mv = rd["mvec"];
+        if (!mv) return;  // nothing reads mvec: no linearize / motion-vector launches, no scratch
         if (mv->format != Format::RG32Float || mv->width != d->width || mv->height != d->height)
             throw Unsupported("GBufferRaster: mvec must be RG32Float at the depth size");
         const size_t px = (size_t)d->width * d->height;
@@ -406,6 +409,21 @@ public:
         if (auto it = dict.find("guardBand"); it != dict.end() && std::holds_alternative<int64_t>(it->second))
             guard = std::get<int64_t>(it->second);
         svp_.guard_band = (uint32_t)guard;
+        svp_.tile_flags = nullptr;
+        if (secondary_ == 2) {
+            // busy 16x16 tiles of this pass's stencil (rsd_svao_params.tile_flags): pass 1 sets, pass 2
+            // consumes; sized by the guard band of this frame, zeroed once per allocation
+            const uint32_t n = rsd_svao_tile_count(width_, height_, (uint32_t)guard);
+            if (n != flagsN_) {
+                (void)hipFree(flags_);
+                flags_ = nullptr;
+                flagsN_ = 0;
+                if (n && (hipMalloc(&flags_, n) != hipSuccess || hipMemsetAsync(flags_, 0, n, ctx.stream) != hipSuccess))
+                    throw std::runtime_error("SVAO: tile flag allocation failed");
+                flagsN_ = n;
+            }
+            svp_.tile_flags = flags_;
+        }
         if (secondary_ == 2)  // SVAO.cpp:330-341
             check(rsd_svao_clear_intervals((uint32_t*)rmin->ptr, (uint32_t*)rmax->ptr, sdW_ * sdH_, ctx.stream),
                   "SVAO clear");
@@ -435,6 +453,7 @@ public:
                              (uint8_t*)ao->ptr, ctx.stream),
               "SVAO AO 2");
     }
+    ~SVAOPass() override { (void)hipFree(flags_); }
     RenderGraph* stochasticDepthGraph() { return sdGraph_.get(); }
 
 private:
@@ -446,6 +465,8 @@ private:
     uint32_t width_ = 0, height_ = 0, sdW_ = 0, sdH_ = 0;
     rsd_vao_data vao_{};
     rsd_svao_params svp_{};
+    uint8_t* flags_ = nullptr;  // busy-tile flags (rsd_svao_params.tile_flags)
+    uint32_t flagsN_ = 0;
     std::unique_ptr<RenderGraph> sdGraph_;
 };
 

@@ -411,6 +411,9 @@ __global__ void __launch_bounds__(kPostW * kPostH) temporal_ao_kernel(TaoArgs a)
 // the pixel-centre primary hit P = posW + (z / cos) d (z: linear depth, d: the normalized pixel
 // ray, cos = dot(normalize(W), d)) projected with the previous camera: mvec = prevUV(P) - uv.
 // P behind the previous camera -> mvec = (2, 2) (off screen: TemporalAO resets the pixel).
+// Background (no geometry: linear depth >= farZ, i.e. rsd_gbuffer's miss value farZ or the
+// linearized cleared raster depth 1.0) -> mvec = (0, 0): GBufferRaster clears mvec
+// (GBufferRaster.cpp:176) and writes it only for rasterized geometry (GBufferRaster.3d.slang:117).
 struct MvecArgs {
     rsd_camera cam, prev;
     const float* z;
@@ -424,11 +427,16 @@ __global__ void __launch_bounds__(kPostW * kPostH) motion_vector_kernel(MvecArgs
     if (x >= a.W || y >= a.H) return;
     const rsd_camera& c = a.cam;
     const float u = ((float)x + 0.5f) / (float)a.W, v = ((float)y + 0.5f) / (float)a.H;
+    const float z = a.z[(size_t)y * a.W + x];
+    if (!(z < c.farZ)) {
+        a.mvec[(size_t)y * a.W + x] = make_float2(0.0f, 0.0f);
+        return;
+    }
     const f3 wn = normalize(mk(c.W[0], c.W[1], c.W[2]));
     const f3 d = normalize(mk((2.0f * u + -1.0f) * c.U[0] + (-2.0f * v + 1.0f) * c.V[0] + c.W[0],
                               (2.0f * u + -1.0f) * c.U[1] + (-2.0f * v + 1.0f) * c.V[1] + c.W[1],
                               (2.0f * u + -1.0f) * c.U[2] + (-2.0f * v + 1.0f) * c.V[2] + c.W[2]));
-    const float t = a.z[(size_t)y * a.W + x] / dot(wn, d);
+    const float t = z / dot(wn, d);
     const f3 rel = mk(c.posW[0] + t * d.x - a.prev.posW[0], c.posW[1] + t * d.y - a.prev.posW[1],
                       c.posW[2] + t * d.z - a.prev.posW[2]);
     const float pa = rel.x * a.pU[0] + rel.y * a.pU[1] + rel.z * a.pU[2];

@@ -107,6 +107,14 @@ __global__ void __launch_bounds__(256) svao_pass1_kernel(SvaoArgs a) {
         ao_store(a, (size_t)py * a.W + px, ao, aoD);
         stencil_store(a, (size_t)py * a.W + px, st);
     }
+    if (a.tileFlags) {
+        // busy 16x16 tiles for pass 2: a wave is 4 thread rows of this 16x16 group = one tile row
+        // and two tiles (threadIdx.x < 8: the left one, the 2x2 interleave spreads 16 threads over
+        // 32 pixels); one byte store per busy tile and wave
+        const uint64_t mL = __ballot(st != 0u && threadIdx.x < 8u), mR = __ballot(st != 0u && threadIdx.x >= 8u);
+        const uint32_t lane = __lane_id();
+        if ((lane == 0u && mL) || (lane == 8u && mR)) a.tileFlags[(oy / kTileEdge) * a.tilesX + ox / kTileEdge] = 1u;
+    }
 }
 
 // SVAORaster2.ps.slang:48-65 -> calcAO2 (Common.slang:523-597), stochastic-depth branch: one
@@ -177,6 +185,7 @@ __device__ __forceinline__ void svao_pass2_dir(const SvaoArgs& a, const Basic& b
 // many passes as its mean direction count (<= the old per-lane maximum).
 constexpr int kP2Tile = 16;                   // pass-2 tile edge (pixels): 16 measured 33 us, 8 35 us, 32 65 us
 constexpr int kP2Lanes = kP2Tile * kP2Tile;   // lanes per workgroup = pixels per tile
+static_assert(kP2Tile == (int)kTileEdge, "busy-tile flags are per pass-2 tile");
 template <int N, int ND>
 __global__ void __launch_bounds__(kP2Lanes) svao_pass2_kernel(SvaoArgs a) {
     constexpr uint32_t T = kP2Tile, L = kP2Lanes;
@@ -196,6 +205,10 @@ __global__ void __launch_bounds__(kP2Lanes) svao_pass2_kernel(SvaoArgs a) {
     const uint32_t x0 = blockIdx.x * T + a.guard;
     const uint32_t y0 = ((blockIdx.y / kPerGroup) * a.bandCount + a.bandIndex) * 32u + (blockIdx.y % kPerGroup) * T +
                         a.guard;
+    // busy-tile flags (pass 1): an unflagged tile holds no stencilled pixel -- the whole group returns
+    // before any barrier (SVAORaster2.ps.slang:50-52 returns per pixel on aoMask == 0)
+    uint8_t* flag = a.tileFlags ? a.tileFlags + ((y0 - a.guard) / T) * a.tilesX + blockIdx.x : nullptr;
+    if (flag && *flag == 0u) return;
     if (tid == 0) { sNPix = 0u; sNPair = 0u; }
     __syncthreads();
     {
@@ -226,6 +239,7 @@ __global__ void __launch_bounds__(kP2Lanes) svao_pass2_kernel(SvaoArgs a) {
         }
     }
     __syncthreads();
+    if (flag && tid == 0) *flag = 0u;  // consumed: the next pass 1 on this stream starts from zero
     const uint32_t nPix = sNPix, nPair = sNPair;
     for (uint32_t c = 0; c < nPair; c += L) {
         const uint32_t k = c + tid;
@@ -352,6 +366,11 @@ rsd_status snap_tables(const rsd_vao_data& vd, const float** u, const float** v)
 
 using namespace rsd;
 
+extern "C" uint32_t rsd_svao_tile_count(uint32_t width, uint32_t height, uint32_t guard_band) {
+    if (2 * guard_band >= width || 2 * guard_band >= height) return 0u;
+    return tiles_x(width, guard_band) * tiles_y(height, guard_band);
+}
+
 extern "C" rsd_status rsd_svao_clear_intervals(uint32_t* d_ray_min, uint32_t* d_ray_max, uint32_t count,
                                                rsd_stream stream) {
     if (!d_ray_min || !d_ray_max) {
@@ -418,6 +437,8 @@ rsd_status pass1_impl(const rsd_camera* cam, const rsd_vao_data* vao, const rsd_
     a.rayInterval = p->ray_interval;
     a.sdJitter = p->sd_jitter;
     a.N = p->sd_samples;
+    a.tileFlags = p->tile_flags;
+    a.tilesX = tiles_x(W, p->guard_band);
     // SVAO.cpp:347-350: nThreads = roundup32(dims - 2 guardBand), 16x16 groups
     const uint32_t nx = (W - 2 * p->guard_band + 31u) / 32u * 32u, ny = (H - 2 * p->guard_band + 31u) / 32u * 32u;
     const uint32_t groups = ny / 32u;
@@ -447,6 +468,10 @@ extern "C" rsd_status rsd_svao_pass1_rows(const rsd_camera* cam, const rsd_vao_d
                                           uint8_t* d_ao, uint8_t* d_stencil, uint32_t* d_ray_min, uint32_t* d_ray_max,
                                           uint32_t sd_w, uint32_t sd_h, uint32_t row0, uint32_t row1,
                                           rsd_stream stream) {
+    if (!p) {
+        set_error("rsd_svao_pass1_rows: null params");
+        return RSD_ERR_INVALID_ARG;
+    }
     if (row0 > row1 || row0 % 32u != 0u || (row1 % 32u != 0u && row1 + 2u * (uint32_t)p->guard_band < H)) {
         set_error("rsd_svao_pass1_rows: rows must be multiples of 32 from the first visible row (row1 may end the frame)");
         return RSD_ERR_INVALID_ARG;
@@ -496,6 +521,8 @@ rsd_status pass2_impl(const rsd_camera* cam, const rsd_vao_data* vao, const rsd_
     a.rayInterval = p->ray_interval;
     a.sdJitter = p->sd_jitter;
     a.N = N;
+    a.tileFlags = p->tile_flags;
+    a.tilesX = tiles_x(W, p->guard_band);
     const uint32_t vw = W - 2 * p->guard_band, vh = H - 2 * p->guard_band;
     const uint32_t groups = (vh + 31u) / 32u;
     const uint32_t bandGroups = std::min(n, groups > start ? (groups - start + step - 1) / step : 0u);
@@ -536,6 +563,10 @@ extern "C" rsd_status rsd_svao_pass2_rows(const rsd_camera* cam, const rsd_vao_d
                                           const float* d_depth, const uint16_t* d_normals, uint32_t W, uint32_t H,
                                           const uint8_t* d_stencil, const float* d_sd, uint32_t sd_w, uint32_t sd_h,
                                           uint8_t* d_ao, uint32_t row0, uint32_t row1, rsd_stream stream) {
+    if (!p) {
+        set_error("rsd_svao_pass2_rows: null params");
+        return RSD_ERR_INVALID_ARG;
+    }
     if (row0 > row1 || row0 % 32u != 0u || (row1 % 32u != 0u && row1 + 2u * (uint32_t)p->guard_band < H)) {
         set_error("rsd_svao_pass2_rows: rows must be multiples of 32 from the first visible row (row1 may end the frame)");
         return RSD_ERR_INVALID_ARG;

@@ -52,7 +52,13 @@ struct SvaoArgs {
     const float* snapU;  // getSnappedUV: snapU[k] = (k + 0.5f) / resolution.x for k in [0, resolution.x]
     const float* snapV;  //               snapV[k] = (k + 0.5f) / resolution.y
     const float4* nlut;  // decode_normal_2x8 of every 16-bit code (normal_lut), same bits
+    uint8_t* tileFlags;  // rsd_svao_params.tile_flags (busy 16x16 tiles) or nullptr
+    uint32_t tilesX;     // tiles per row of tileFlags
 };
+
+constexpr uint32_t kTileEdge = 16;  // busy-tile flag granularity = the pass-2 workgroup tile
+inline uint32_t tiles_x(uint32_t W, uint32_t guard) { return (W - 2 * guard + kTileEdge - 1) / kTileEdge; }
+inline uint32_t tiles_y(uint32_t H, uint32_t guard) { return (H - 2 * guard + 31u) / 32u * 32u / kTileEdge; }
 
 struct Basic {
     f3 posV;

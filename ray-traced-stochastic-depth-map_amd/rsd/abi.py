@@ -82,7 +82,8 @@ class VAOData(C.Structure):
 class SVAOParams(C.Structure):
     _fields_ = [("num_directions", C.c_uint32), ("sd_samples", C.c_uint32),
                 ("secondary_depth_mode", C.c_uint32), ("ray_interval", C.c_uint32),
-                ("sd_jitter", C.c_uint32), ("guard_band", C.c_uint32), ("dual_ao", C.c_uint32)]
+                ("sd_jitter", C.c_uint32), ("guard_band", C.c_uint32), ("dual_ao", C.c_uint32),
+                ("tile_flags", C.c_void_p)]  # ABI v4: busy 16x16 tiles (pass 1 sets, pass 2 consumes)
 
 
 class Counters(C.Structure):
@@ -105,7 +106,7 @@ WALK_KERNELS = {WALK_QUAD: ("sd_setup_kernel", "sd_trace_queue_kernel"),
 
 
 # every symbol include/rsd.h declares (checked by tests/test_abi.py)
-EXPORTS = ["rsd_abi_version", "rsd_last_error", "rsd_device_open", "rsd_device_close", "rsd_scene_upload",
+EXPORTS = ["rsd_abi_version", "rsd_svao_tile_count", "rsd_last_error", "rsd_device_open", "rsd_device_close", "rsd_scene_upload",
            "rsd_scene_info_get", "rsd_scene_release", "rsd_camera_look_at", "rsd_svao_make_vao_data",
            "rsd_gbuffer", "rsd_sd_trace", "rsd_svao_clear_intervals", "rsd_svao_pass1", "rsd_svao_pass2",
            "rsd_sd_trace_band", "rsd_svao_pass1_band", "rsd_svao_pass2_band", "rsd_gbuffer_raster",
@@ -148,6 +149,8 @@ def lib():
         L = C.CDLL(str(LIB_PATH), mode=C.RTLD_GLOBAL)  # global: render-pass plugins resolve the host's symbols
         vp, u32, i32, f32, st = C.c_void_p, C.c_uint32, C.c_int32, C.c_float, C.c_int
         L.rsd_abi_version.restype = u32
+        L.rsd_svao_tile_count.restype = u32
+        L.rsd_svao_tile_count.argtypes = [u32, u32, u32]
         L.rsd_last_error.restype = C.c_char_p
         L.rsd_device_open.restype = st
         L.rsd_device_open.argtypes = [C.c_int, C.POINTER(vp)]

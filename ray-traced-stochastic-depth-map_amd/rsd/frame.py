@@ -254,6 +254,17 @@ class Renderer:
         # Use16Bit (standalone SD pass): R16F / RG16F / RGBA16F
         self.sd = torch.empty(((N + 3) // 4, self.sd_h, self.sd_w, min(N, 4)),
                               dtype=torch.float16 if cfg.use_16bit else torch.float32, device=dv)
+        self._bind_tile_flags()
+
+    def _bind_tile_flags(self):
+        """Busy 16x16 tiles of this frame's stencil (rsd_svao_params.tile_flags, ABI v4): pass 1 sets
+        them, pass 2 visits only flagged tiles and clears them.  One set per stencil buffer (frame slot)."""
+        cfg = self.cfg
+        n = abi.lib().rsd_svao_tile_count(cfg.fb_w, cfg.fb_h, cfg.guard_band)
+        self.tile_flags = self.torch.zeros(max(1, n), dtype=self.torch.uint8, device=self.depth.device)
+        svp = abi.SVAOParams.from_buffer_copy(self.svp)
+        svp.tile_flags = self.tile_flags.data_ptr()
+        self.svp = svp
 
     def frame_slot(self, own_gbuffer: bool = False) -> "Renderer":
         """Another set of per-frame buffers (ao, stencil, intervals, SD map) over the same scene,
@@ -271,6 +282,7 @@ class Renderer:
         r.ray_minmax = t.empty_like(self.ray_minmax)
         r.ray_min, r.ray_max = r.ray_minmax[0], r.ray_minmax[1]
         r.sd = t.empty_like(self.sd)
+        r._bind_tile_flags()
         if own_gbuffer:
             r.cam = abi.Camera.from_buffer_copy(self.cam)
             r.depth = t.empty_like(self.depth)

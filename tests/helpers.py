@@ -8,9 +8,13 @@ import numpy as np
 
 
 def to_oracle(struct, oracle_cls):
-    """Byte-copy a librsd ctypes struct into the oracle's struct of identical layout."""
+    """Byte-copy a librsd ctypes struct into the oracle's struct of identical layout.  The oracle's
+    struct may be a prefix of librsd's (device-only trailing fields such as rsd_svao_params.tile_flags)."""
     out = oracle_cls()
-    assert C.sizeof(out) == C.sizeof(struct), (oracle_cls, C.sizeof(out), C.sizeof(struct))
+    names = [f[0] for f in type(struct)._fields_]
+    onames = [f[0] for f in oracle_cls._fields_]
+    assert names[:len(onames)] == onames, (oracle_cls, onames, names)
+    assert C.sizeof(out) <= C.sizeof(struct), (oracle_cls, C.sizeof(out), C.sizeof(struct))
     C.memmove(C.byref(out), C.byref(struct), C.sizeof(out))
     return out
 

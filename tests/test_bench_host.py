@@ -45,6 +45,11 @@ def test_host_cpus():
     import bench as b
     h = b.host_cpus()
     assert h["usable"] >= 1 and h["nproc"] >= h["usable"]
+    # the baseline's core count: the affinity mask capped by the cgroup quota
+    assert 1 <= h["effective"] <= h["usable"]
+    if h["cgroup_cpu_quota"] is not None:
+        import math
+        assert h["effective"] <= max(1, math.ceil(h["cgroup_cpu_quota"]))
 
 
 def test_camera_path():

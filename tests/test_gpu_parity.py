@@ -501,3 +501,47 @@ def test_dual_ao_raytraced_parity(device, oracle):
     assert np.array_equal(g["stencil"], st)
     ao = oracle.svao_pass2_raytraced(osc, cam, vao, svp, z, n, st, ao1, cull=cfg.cull_mode, ray_pipeline=1)
     assert np.array_equal(g["ao"], ao)
+
+
+@pytest.mark.parametrize("nd", [8, 16])
+def test_busy_tile_flags(device, oracle, torch_dev, nd):
+    """rsd_svao_params.tile_flags (ABI v4): pass 1 flags exactly the 16x16 tiles of the visible region
+    that hold a stencilled pixel; pass 2 visits only those and clears them; the AO equals a frame
+    without flags (every tile visited) and the oracle."""
+    cfg = small_frame_config(visible=(224, 128), guard=32, divisor=2)
+    cfg.num_directions = nd
+    r, osc = renderer("arcade_tiny", cfg, device, oracle)
+    r.gbuffer()
+    r.clear_intervals()
+    r.pass1()
+    g = r.numpy()
+    flags = r.tile_flags.cpu().numpy()
+    g_, vw, vh = cfg.guard_band, cfg.visible_w, cfg.visible_h
+    tx, ty = (vw + 15) // 16, (vh + 31) // 32 * 32 // 16
+    assert flags.size == tx * ty
+    st = g["stencil"][g_:g_ + ty * 16, g_:g_ + vw]
+    want = np.zeros((ty, tx), np.uint8)
+    for j in range(ty):
+        for i in range(tx):
+            want[j, i] = (st[16 * j:16 * j + 16, 16 * i:16 * i + 16] != 0).any()
+    assert want.any() and not want.all()
+    assert np.array_equal(flags.reshape(ty, tx), want)
+    r.sd_trace()
+    r.pass2()
+    with_flags = r.numpy()["ao"]
+    assert not r.tile_flags.cpu().numpy().any()  # consumed
+    # the same frame without flags
+    from rsd import abi
+    svp = abi.SVAOParams.from_buffer_copy(r.svp)
+    svp.tile_flags = None
+    r.svp, keep = svp, r.svp
+    r.ao.zero_()
+    r.clear_intervals()
+    r.pass1()
+    r.sd_trace()
+    r.pass2()
+    assert np.array_equal(r.numpy()["ao"], with_flags)
+    r.svp = keep
+    cam, vao, sdp, svp_o = oracle_structs(r, oracle)
+    o = oracle_frame(oracle, osc, cam, vao, sdp, svp_o, cfg.fb_w, cfg.fb_h, r.sd_w, r.sd_h)
+    assert np.array_equal(with_flags, o["ao"])

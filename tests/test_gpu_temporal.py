@@ -82,6 +82,27 @@ def test_temporal_ao_rejects_bad_arguments(torch):
     assert st == abi.ERR_INVALID_ARG
 
 
+def test_motion_vectors_background_zero(torch, oracle):
+    """Background pixels (linear depth >= farZ) get mvec (0, 0) under a moving camera, on the GPU
+    and in the oracle (GBufferRaster.cpp:176 clears mvec; GBufferRaster.3d.slang:117 writes it for
+    geometry only); geometry pixels are bit-identical to the oracle."""
+    from rsd.frame import FrameConfig, look_at
+    from rsd.temporal import motion_vectors
+    cfg = FrameConfig(visible_w=160, visible_h=96, guard_band=16)
+    c0 = look_at((0.0, 2.0, 8.0), (0.0, 1.0, 0.0), (0.0, 1.0, 0.0), cfg)
+    c1 = look_at((0.6, 2.2, 7.5), (0.1, 1.0, 0.0), (0.0, 1.0, 0.0), cfg)
+    rng = np.random.default_rng(11)
+    z = (4.0 + 20.0 * rng.random((cfg.fb_h, cfg.fb_w))).astype(np.float32)
+    z[: cfg.fb_h // 3] = c1.farZ                                    # rsd_gbuffer miss value
+    z[cfg.fb_h // 3: cfg.fb_h // 3 + 8] = np.float32(1000.2441)     # linearized raster depth 1.0
+    zt = torch.from_numpy(z).cuda()
+    mv = motion_vectors(c1, c0, zt).cpu().numpy()
+    want = oracle.motion_vectors(to_oracle(c1, oracle.Camera), to_oracle(c0, oracle.Camera), z)
+    assert np.array_equal(mv.view(np.uint32), want.view(np.uint32))
+    bg = z >= c1.farZ
+    assert (mv[bg] == 0.0).all() and (np.abs(mv[~bg]).max(axis=-1) > 0).all()
+
+
 def test_temporal_sequence_parity_and_accumulation(torch, oracle):
     """Four poses of a slowly moving camera: each frame's motion vectors and TemporalAO output
     equal the oracle's, and the history grows where the reprojection holds."""
@@ -109,6 +130,7 @@ def test_temporal_sequence_parity_and_accumulation(torch, oracle):
         oc, op = to_oracle(r.cam, oracle.Camera), to_oracle(prev_cam, oracle.Camera)
         want_mv = oracle.motion_vectors(oc, op, z)
         assert np.array_equal(mv.cpu().numpy().view(np.uint32), want_mv.view(np.uint32)), i
+        assert (want_mv[z >= oc.farZ] == 0.0).all()  # background keeps the cleared mvec
         if o_prev is None:
             H, W = z.shape
             o_prev = (np.zeros_like(z), np.zeros_like(ao_in), np.zeros_like(ao_in))

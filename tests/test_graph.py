@@ -225,6 +225,52 @@ def test_sd_pass_refuses_like_the_reference(N, use16):
     g.close()
 
 
+@pytest.mark.parametrize("fmt,name", [(abi.FMT_R32F, "R32Float"), (abi.FMT_RG32F, "RG32Float"),
+                                      (abi.FMT_RGBA32F, "RGBA32Float"), (abi.FMT_R16U, "R16Uint"),
+                                      (abi.FMT_R8U, "R8Uint"), (abi.FMT_R8UNORM, "R8Unorm"),
+                                      (abi.FMT_R32U, "R32Uint"), (abi.FMT_R16F, "R16Float"),
+                                      (abi.FMT_RG16F, "RG16Float"), (abi.FMT_RGBA16F, "RGBA16Float"),
+                                      (abi.FMT_RG8UNORM, "RG8Unorm")])
+def test_graph_input_format_round_trip(fmt, name):
+    """rsd_graph_set_input accepts every real rsd_format (dualAO's RG8Unorm included); a Switch
+    output takes the format of its external input (Switch.cpp:95-108)."""
+    g = rsdgraph.RenderGraph("fmt")
+    g.create_pass("S", "Switch", {"count": 1, "selected": 0})
+    g.mark_output("S.out")
+    buf = np.zeros(32 * 64 * 16, np.uint8)  # planned only: never read
+    g.set_input("S.i0", buf.ctypes.data, 64, 32, fmt)
+    g.plan(64, 32)
+    assert g.resources()["S.out"] == (64, 32, 1, name)
+    g.close()
+
+
+@pytest.mark.parametrize("fmt", [abi.FMT_UNKNOWN, abi.FMT_RG8UNORM + 1, 255])
+def test_graph_input_refuses_unknown_formats(fmt):
+    g = rsdgraph.RenderGraph("fmt")
+    g.create_pass("S", "Switch", {"count": 1, "selected": 0})
+    buf = np.zeros(16, np.uint8)
+    with pytest.raises(abi.RsdError):
+        g.set_input("S.i0", buf.ctypes.data, 2, 2, fmt)
+    g.close()
+
+
+def test_optional_mvec_allocated_only_when_read():
+    """GBuffer.cpp:48: mvec is an optional channel -- a graph that does not read it allocates no
+    mvec (and GBufferRaster launches no motion-vector kernels); one that reads it gets RG32Float."""
+    g = rsdgraph.RenderGraph("gb")
+    g.create_pass("GBufferRaster", "GBufferRaster", {})
+    g.mark_output("GBufferRaster.depth")
+    g.plan(64, 32)
+    assert "GBufferRaster.mvec" not in g.resources() and "GBufferRaster.depth" in g.resources()
+    g.close()
+    g = rsdgraph.RenderGraph("gb")
+    g.create_pass("GBufferRaster", "GBufferRaster", {})
+    g.mark_output("GBufferRaster.mvec")
+    g.plan(64, 32)
+    assert g.resources()["GBufferRaster.mvec"] == (64, 32, 1, "RG32Float")
+    g.close()
+
+
 def test_temporal_ao_enabled_plans():
     """TemporalAO enabled (TemporalAO.cpp:92-103): linearZ and mvec become required inputs;
     GBufferRaster declares mvec (RG32Float)."""

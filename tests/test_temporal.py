@@ -47,6 +47,20 @@ def test_motion_vectors_follow_the_camera(oracle):
     assert (behind == 2.0).all()  # every hit is behind that previous camera: off screen
 
 
+def test_motion_vectors_background_is_zero(oracle):
+    """Sky / background pixels (linear depth >= farZ: rsd_gbuffer's miss value, or a linearized
+    cleared raster depth 1.0) keep the cleared mvec (0, 0) under a moving camera, like
+    GBufferRaster (GBufferRaster.cpp:176 clear, GBufferRaster.3d.slang:117 geometry only)."""
+    c0 = _cam(oracle, pos=(0.0, 2.0, 8.0), target=(0.0, 1.0, 0.0))
+    c1 = _cam(oracle, pos=(0.5, 2.3, 7.0), target=(0.2, 1.0, 0.0))
+    z = np.full((64, 96), 8.0, F)
+    z[:20] = c1.farZ                                        # rsd_gbuffer miss
+    z[20:24] = np.float32(c1.farZ) * np.float32(1.0001)     # linearized raster depth 1.0 (> farZ)
+    mv = oracle.motion_vectors(c1, c0, z)
+    assert (mv[:24] == 0.0).all()
+    assert (np.abs(mv[24:]).max(axis=-1) > 0).all()        # geometry still moves
+
+
 def test_temporal_accumulates_to_thirty_and_resets(oracle):
     H, W, g = 64, 96, 4
     c = _cam(oracle)

@@ -1,7 +1,7 @@
 """Per-pass GPU time of one AO frame (diagnostics): pass 1, SD trace, pass 2 of a BASELINE config,
-each the median of 7 batches of 40 back-to-back launches (HIP events).  Pass 2 re-runs on the
-same stencil / SD map (it rewrites the AO image in place: timing only).
-usage: python tools/pass_time.py [config]"""
+each the median over 200 sequential frames of HIP events around the pass (clear -> pass 1 ->
+trace -> pass 2 per frame, so pass 2 always consumes the busy-tile flags of its own pass 1).
+usage: python tools/pass_time.py [config] [--frames N]"""
 import json
 import sys
 from pathlib import Path
@@ -14,31 +14,27 @@ import torch  # noqa: E402
 from rsd.frame import CONFIGS, FrameConfig, Renderer  # noqa: E402
 from rsd.scenes import make_scene  # noqa: E402
 
-
-def timeit(fn, n=40, batches=7):
-    fn()
-    torch.cuda.synchronize()
-    res = []
-    for _ in range(batches):
-        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        s.record()
-        for _ in range(n):
-            fn()
-        e.record()
-        torch.cuda.synchronize()
-        res.append(s.elapsed_time(e) / n * 1e3)
-    return float(np.median(res))
-
-
 name = next((a for a in sys.argv[1:] if not a.startswith("--")), "suntemple_1080p_q")
+frames = int(sys.argv[sys.argv.index("--frames") + 1]) if "--frames" in sys.argv else 200
 kw, sc = CONFIGS[name]
 r = Renderer(make_scene(sc), FrameConfig(**kw))
 r.gbuffer()
-r.frame()
+for _ in range(5):
+    r.frame()
 torch.cuda.synchronize()
-out = {"config": name, "pass1_us": timeit(r.pass1), "pass2_us": timeit(r.pass2)}
-iv = r.ray_minmax.clone()
-r.clear_intervals()
-r.pass1()
-out["sd_trace_us"] = timeit(lambda: r.sd_trace())
-print(json.dumps(out))
+ev = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(frames)]
+for e in ev:
+    r.clear_intervals()
+    e[0].record()
+    r.pass1()
+    e[1].record()
+    r.sd_trace()
+    e[2].record()
+    r.pass2()
+    e[3].record()
+torch.cuda.synchronize()
+t = np.array([[e[i].elapsed_time(e[i + 1]) * 1e3 for i in range(3)] for e in ev])
+med = np.median(t, axis=0)
+print(json.dumps({"config": name, "frames": frames, "pass1_us": round(float(med[0]), 2),
+                  "sd_trace_us": round(float(med[1]), 2), "pass2_us": round(float(med[2]), 2),
+                  "ao_span_us": round(float(np.median(t.sum(axis=1))), 2)}))
