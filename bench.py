@@ -28,13 +28,14 @@ The G-buffer is inside the frame's wall time but outside the AO span (BASELINE.m
 excludes the G-buffer).
 
 Multi-GPU (torchrun, one rank per GPU), sharding modes (--shard):
-  frame (default for the 1080p configs): frames are the independent units -- every rank renders
-    whole frames (its own frame stream, BVH + G-buffer replicated), no data-path collective.
-    Weak scaling.
-  band (default for the 4K configs): the north_star's screen split (rsd/shard.py HaloFrame):
-    contiguous bands; pass 1 of the rank's rows, interval halo exchange with the bands its
-    samples reach (point-to-point send / recv: ncclSend / ncclRecv under RCCL), trace of the
-    rank's SD rows, SD halo exchange, pass 2 of the rank's rows, AO all-gather.  Strong scaling.
+  band (the default for every config): the north_star's screen split (rsd/shard.py HaloFrame) --
+    each frame is split into contiguous screen bands re-balanced from the previous frame's
+    per-band time; pass 1 of the rank's rows, a SPARSE interval halo (only the SD texels its
+    samples touched, as (index, rayMin, rayMax) triples; point-to-point send / recv = ncclSend /
+    ncclRecv under RCCL), trace of the rank's SD rows, a sparse SD halo (the depths of exactly
+    those texels), pass 2 of the rank's rows, AO all-gather.  Strong scaling.
+  frame: frames are the independent units -- every rank renders whole frames (its own frame
+    stream, BVH + G-buffer replicated), no data-path collective.  Weak scaling.
   gather: round-1 v1 of band -- interleaved bands, whole-map interval all-reduce and SD all-gather.
 """
 from __future__ import annotations
@@ -72,11 +73,11 @@ def parse():
     ap.add_argument("--frames-in-flight", type=int, default=4,
                     help="throughput region: frame i runs on stream i %% F with its own frame buffers")
     ap.add_argument("--shard", choices=("frame", "band", "gather"), default=None,
-                    help="N > 1: frame = every rank renders whole frames (weak scaling, no per-frame "
-                         "collective); band = each frame split into contiguous screen bands with interval / SD "
-                         "halo exchanges (point-to-point RCCL) + AO all-gather (strong); gather = interleaved "
-                         "bands with whole-map all-reduce / all-gather (round-1 v1). Default: band for the 4K "
-                         "configs, frame otherwise")
+                    help="N > 1: band (default) = each frame split into contiguous, re-balanced screen bands "
+                         "with sparse interval / SD halo exchanges (point-to-point RCCL) + AO all-gather (strong "
+                         "scaling, the north_star split); frame = every rank renders whole frames (weak scaling, "
+                         "no per-frame collective); gather = interleaved bands with whole-map all-reduce / "
+                         "all-gather (round-1 v1)")
     ap.add_argument("--scene-file", default=None,
                     help="a .pyscene or .obj scene (rsd.pyscene / rsd.ingest) instead of the config's stand-in "
                          "scene; the config still sets the frame, SD map and N")
@@ -143,7 +144,7 @@ def main():
 
     kw, scene_name = CONFIGS[args.config]
     cfg = FrameConfig(**kw)
-    shard = args.shard or ("band" if cfg.visible_w >= 3840 else "frame")
+    shard = args.shard or "band"
     path_name = args.camera_path or DEFAULT_CAMERA_PATH.get(args.config, "static")
     poses = camera_path(path_name)
     if args.scene_file:
@@ -349,7 +350,9 @@ def main():
         # the frame's largest kernel is pass 1, bound by VALU issue rather than HBM
         "pass1_roofline": pmc_valu(valu_csv, "svao_pass1_kernel") if valu_csv and args.config == DEFAULT_CONFIG and not args.scene_file
         else None,
-        "exchange_bytes_per_frame": seq.bytes_per_frame() if shard == "band" and world > 1 else None,
+        "exchange_bytes_per_frame": dict(seq.bytes_per_frame(), dense_halo_equivalent=seq.dense_bytes_per_frame(),
+                                         final_split_groups=list(seq.gb))
+        if shard == "band" and world > 1 else None,
         "bvh_build_s": round(bvh_build_s, 3),
         "bvh_build_threads": int(r.gscene.info.build_threads),
         "cpu_baseline": cpu,

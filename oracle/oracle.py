@@ -14,11 +14,13 @@ from pathlib import Path
 import numpy as np
 
 _HERE = Path(__file__).resolve().parent
-_LIB_PATH = _HERE / "_build" / "librsd_oracle.so"
+# RSD_ORACLE_VARIANT=asan: the ASan + UBSan build (make -C oracle asan; tools/asan_cpu_suite.sh)
+_VARIANT = os.environ.get("RSD_ORACLE_VARIANT", "")
+_LIB_PATH = _HERE / "_build" / (f"librsd_oracle_{_VARIANT}.so" if _VARIANT else "librsd_oracle.so")
 
 
 def build(quiet: bool = True) -> Path:
-    subprocess.run(["make", "-C", str(_HERE)], check=True,
+    subprocess.run(["make", "-C", str(_HERE)] + ([_VARIANT] if _VARIANT else []), check=True,
                    stdout=subprocess.DEVNULL if quiet else None)
     return _LIB_PATH
 

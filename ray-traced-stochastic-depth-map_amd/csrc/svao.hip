@@ -12,7 +12,9 @@
 #include <algorithm>
 #include <cfloat>
 #include <cmath>
+#include <cstdlib>
 #include <mutex>
+#include <string>
 #include <vector>
 
 #include "rsd_device.h"
@@ -37,7 +39,69 @@ __global__ void clear_intervals_kernel(uint32_t* rmin, uint32_t* rmax, uint32_t 
     }
 }
 
-// SVAORaster.ps.slang:29-122, [numthreads(16,16,1)] with the 2x2 group interleave
+// One direction of SVAORaster.ps.slang:49-105 for one pixel (any radius, any divisor, IEEE division
+// where the host reciprocals do not apply): the reference loop body
+__device__ __forceinline__ void pass1_dir_generic(const SvaoArgs& a, float u, float v, uint32_t px, uint32_t py,
+                                                  const Basic& b, int i, float& ao, float& aoD, uint32_t& st) {
+    const rsd_vao_data& d = a.d;
+    Sample s;
+    bool ssrAbove;
+    if (!sample_init(a, u, v, b, i, s, ssrAbove)) return;
+    const bool same = a.k.samePixelInt ? (s.kx == (int)px && s.ky == (int)py)
+                                       : (fabsf(u - s.ru) < d.invResolution[0] * 0.9f &&
+                                          fabsf(v - s.rv) < d.invResolution[1] * 0.9f);
+    if (same) {
+        const float w = div_pdf(s.sphereStart - s.sphereEnd, s);  // isSamePixel
+        ao += w;
+        aoD += w;
+        return;
+    }
+    // SVAORaster.ps.slang:62-66: Raytraced mode with TRACE_OUT_OF_SCREEN (SVAO.h:104)
+    bool forceRay = a.secondary == 3u && !s.isInScreen;
+    eval_primary(a, b, s);
+    ao += s.visibility;
+    if (!s.isInScreen && d.sdGuard > 0) {
+        forceRay = true;
+        s.objectSpaceZ = 3.402823466e+38f;
+    }
+    const float constRadius = (1.0f + d.thickness) * b.radius - s.sphereStart;
+    const bool req = s.objectSpaceZ > s.sphereStart + constRadius && ssrAbove;
+    if (req || forceRay) {
+        st |= 1u << i;
+        if (a.secondary == 2u) {
+            const int sx = uv_to_sd(s.su, d.lowResolution[0], d.sdGuard);
+            const int sy = uv_to_sd(s.sv, d.lowResolution[1], d.sdGuard);
+            const size_t o = (size_t)sy * a.sdW + sx;
+            if (a.rayInterval) {
+                const float osMin = hmin(s.objectSpaceZ, b.radius + d.thickness * b.radius + s.sphereStart);
+                atomicMin(&a.rayMin[o], asuint(hmax(b.posVLength - osMin, 0.0f)));
+                atomicMax(&a.rayMax[o], asuint(hmax(b.posVLength - s.sphereEnd, 0.0f)));
+            } else {
+                a.rayMax[o] = 1u;
+            }
+        }
+    } else {
+        aoD += s.visibility;  // darkmap: the dark channel keeps directions that need no ray
+    }
+}
+
+// element idx of a device table through a 32-bit byte offset from the (uniform) base: the load
+// takes the SGPR-base + VGPR-offset form instead of 64-bit address arithmetic per lane
+template <typename T>
+__device__ __forceinline__ T ld32(const T* base, uint32_t idx) {
+    return *reinterpret_cast<const T*>(reinterpret_cast<const char*>(base) + idx * (uint32_t)sizeof(T));
+}
+
+// SVAORaster.ps.slang:29-122 with the reference 2x2 group interleave (numthreads 16x16).  The pixel's
+// per-direction work is either the generic body above or, when no lane of the wave has its AO
+// radius clamped to ssMaxRadius (the host-evaluated direction terms then apply to every lane),
+// the LEAN body: ND directions unrolled with their constants in scalar registers, branch-free up
+// to the interval atomics (every quantity is evaluated and selected: an invalid or same-pixel
+// direction adds +0, which leaves the running sums' bits unchanged), the ratio test as one float
+// compare (SvaoConsts::ratioThr), divisions by pdf / sphereHeight through div_rcp, and 32-bit table
+// offsets.  Same bits as the generic body (tests/test_gpu_parity.py: every pass-1 case runs this
+// kernel; RSD_PASS1=generic selects the generic-only kernel for A/B).
+template <int ND, bool LEAN>
 __global__ void __launch_bounds__(256) svao_pass1_kernel(SvaoArgs a) {
     const uint32_t bx = blockIdx.x, by = blockIdx.y;
     const uint32_t ox = (bx / 2u) * 32u + 2u * threadIdx.x + (bx % 2u);
@@ -49,51 +113,73 @@ __global__ void __launch_bounds__(256) svao_pass1_kernel(SvaoArgs a) {
     float ao = 0.0f, aoD = 0.0f;  // bright, dark (DUAL_AO: SVAORaster.ps.slang:13 ao_t = float2)
     uint32_t st = 0;
     Basic b;
-    if (!basic_init(a, u, v, b)) {
+    const bool ok = basic_init(a, u, v, b);
+    // the lean body needs the unclamped radius on every lane of the wave (uniform decision)
+    const bool lean = LEAN && __all(!ok || b.radius == d.radius);
+    if (!ok) {
         ao = aoD = 1.0f;
-    } else {
+    } else if (!lean) {
 #pragma unroll 1
-        for (int i = 0; i < (int)a.k.nd; ++i) {
-            Sample s;
-            bool ssrAbove;
-            if (!sample_init(a, u, v, b, i, s, ssrAbove)) continue;
-            const bool same = a.k.samePixelInt ? (s.kx == (int)px && s.ky == (int)py)
-                                               : (fabsf(u - s.ru) < d.invResolution[0] * 0.9f &&
-                                                  fabsf(v - s.rv) < d.invResolution[1] * 0.9f);
-            if (same) {
-                const float w = div_pdf(s.sphereStart - s.sphereEnd, s);  // isSamePixel
-                ao += w;
-                aoD += w;
-                continue;
-            }
-            // SVAORaster.ps.slang:62-66: Raytraced mode with TRACE_OUT_OF_SCREEN (SVAO.h:104)
-            bool forceRay = a.secondary == 3u && !s.isInScreen;
-            eval_primary(a, b, s);
-            ao += s.visibility;
-            if (!s.isInScreen && d.sdGuard > 0) {
-                forceRay = true;
-                s.objectSpaceZ = 3.402823466e+38f;
-            }
-            const float constRadius = (1.0f + d.thickness) * b.radius - s.sphereStart;
-            const bool req = s.objectSpaceZ > s.sphereStart + constRadius && ssrAbove;
-            if (req || forceRay) {
-                st |= 1u << i;
-                if (a.secondary == 2u) {
-                    const int sx = uv_to_sd(s.su, d.lowResolution[0], d.sdGuard);
-                    const int sy = uv_to_sd(s.sv, d.lowResolution[1], d.sdGuard);
-                    const size_t o = (size_t)sy * a.sdW + sx;
-                    if (a.rayInterval) {
-                        const float osMin = hmin(s.objectSpaceZ, b.radius + d.thickness * b.radius + s.sphereStart);
-                        atomicMin(&a.rayMin[o], asuint(hmax(b.posVLength - osMin, 0.0f)));
-                        atomicMax(&a.rayMax[o], asuint(hmax(b.posVLength - s.sphereEnd, 0.0f)));
-                    } else {
-                        a.rayMax[o] = 1u;
-                    }
+        for (int i = 0; i < (int)a.k.nd; ++i) pass1_dir_generic(a, u, v, px, py, b, i, ao, aoD, st);
+    } else {
+        const float nzD = make_nonzero(b.normalO.z, 0.0001f);
+        const float r1 = (1.0f + d.thickness) * b.radius;          // CONST_RADIUS term, Common.slang:37
+        const float rInt = b.radius + d.thickness * b.radius;      // the interval's r + thickness r
+        const bool offForce = d.sdGuard > 0;                       // off-screen sample -> ray (SD guard)
+        const bool rtForce = a.secondary == 3u;                    // TRACE_OUT_OF_SCREEN (Raytraced)
+        const float res0 = d.resolution[0], res1 = d.resolution[1];
+        const uint32_t W = (uint32_t)a.W, H = (uint32_t)a.H;
+#pragma unroll
+        for (int i = 0; i < ND; ++i) {
+            const float dx = a.k.dirDx[i], dy = a.k.dirDy[i], h = a.k.dirHeight[i];
+            const float yPdf = a.k.rcpPdf[i], yH = a.k.rcpHeight[i];
+            const float pdf = 2.0f * h;
+            // SampleAOData::Init (Common.slang:354-399)
+            const float zi = -(dx * b.normalO.x + dy * b.normalO.y) / nzD;
+            const float se = hmin(hmax(zi, -h), h);
+            const float n = h - se;
+            const bool valid = !(n < a.k.ratioThr[i]);
+            const f3 ip = b.posV + b.tangent * dx + b.bitangent * dy;
+            float su, sv;
+            view_to_uv(a, ip, su, sv);
+            const float ex = (u - su) * res0, ey = (v - sv) * res1;
+            const bool ssrAbove = ex * ex + ey * ey >= a.k.ssrMin2;
+            const float cu = saturate(su), cv = saturate(sv);
+            const bool inScreen = (su == cu) && (sv == cv);
+            const uint32_t kx = (uint32_t)(int)floorf(cu * res0), ky = (uint32_t)(int)floorf(cv * res1);
+            const bool same = kx == px && ky == py;  // isSamePixel on indices (SvaoConsts::samePixelInt)
+            // evalPrimaryVisibility (Common.slang:492-496) at the snapped uv (depth_center's direct fetch)
+            const float ru = ld32(a.snapU, kx), rv = ld32(a.snapV, ky);
+            const float zp = ld32(a.depth, min(ky, H - 1u) * W + min(kx, W - 1u));
+            const float oz = dot(uv_to_view(a, ru, rv, zp) - b.posV, b.normal);
+            const float sphere = div_rcp(hmax(h - hmax(se, oz), 0.0f), pdf, yPdf);
+            const float xh = oz - r1;
+            const float hr = xh >= h ? 1.0f : saturate(div_rcp(xh, h, yH));
+            const float vis = sphere + (xh > 0.0f ? div_rcp(hr * (h - se), pdf, yPdf) : 0.0f);
+            const float wSame = div_rcp(n, pdf, yPdf);
+            // requireRay (Common.slang:455-461) and the SVAORaster.ps.slang:62-80 ray forcing
+            const bool off = !inScreen && offForce;
+            const float osz = off ? 3.402823466e+38f : oz;
+            const bool req = osz > h + (r1 - h) && ssrAbove;
+            const bool need = valid && !same && (req || off || (rtForce && !inScreen));
+            ao += valid ? (same ? wSame : vis) : 0.0f;
+            aoD += (valid && !need) ? (same ? wSame : vis) : 0.0f;
+            st |= need ? (1u << i) : 0u;
+            if (need && a.secondary == 2u) {
+                const uint32_t sx = (uint32_t)uv_to_sd(su, d.lowResolution[0], d.sdGuard);
+                const uint32_t sy = (uint32_t)uv_to_sd(sv, d.lowResolution[1], d.sdGuard);
+                const uint32_t o = sy * (uint32_t)a.sdW + sx;
+                if (a.rayInterval) {
+                    const float osMin = hmin(osz, rInt + h);
+                    atomicMin(&a.rayMin[o], asuint(hmax(b.posVLength - osMin, 0.0f)));
+                    atomicMax(&a.rayMax[o], asuint(hmax(b.posVLength - se, 0.0f)));
+                } else {
+                    a.rayMax[o] = 1u;
                 }
-            } else {
-                aoD += s.visibility;  // darkmap: the dark channel keeps directions that need no ray
             }
         }
+    }
+    if (ok) {
         ao *= a.k.invNd;  // SVAORaster.ps.slang:108-109
         ao *= 2.0f;
         aoD *= a.k.invNd;
@@ -446,7 +532,21 @@ rsd_status pass1_impl(const rsd_camera* cam, const rsd_vao_data* vao, const rsd_
     a.bandIndex = start;
     a.bandCount = step;
     if (bandGroups == 0) return RSD_OK;
-    hipLaunchKernelGGL(svao_pass1_kernel, dim3(nx / 16, 2 * bandGroups), dim3(16, 16), 0, (hipStream_t)stream, a);
+    // the lean kernel needs the host reciprocals for every direction, index-based isSamePixel and
+    // depth_center's direct fetch (frames up to 4096 px); RSD_PASS1=generic forces the generic body
+    static const bool forceGeneric = [] {
+        const char* e = getenv("RSD_PASS1");
+        return e && std::string(e) == "generic";
+    }();
+    const uint32_t allDirs = a.k.nd == 32u ? 0xffffffffu : ((1u << a.k.nd) - 1u);
+    const bool lean = !forceGeneric && (a.k.fastDiv & allDirs) == allDirs && a.k.samePixelInt && W <= 4096u &&
+                      H <= 4096u;
+    const dim3 grid(nx / 16, 2 * bandGroups), block(16, 16);
+    hipStream_t s = (hipStream_t)stream;
+    if (!lean) hipLaunchKernelGGL((svao_pass1_kernel<8, false>), grid, block, 0, s, a);
+    else if (a.k.nd == 32u) hipLaunchKernelGGL((svao_pass1_kernel<32, true>), grid, block, 0, s, a);
+    else if (a.k.nd == 16u) hipLaunchKernelGGL((svao_pass1_kernel<16, true>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((svao_pass1_kernel<8, true>), grid, block, 0, s, a);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? RSD_OK : hip_fail(e, "svao_pass1_kernel launch");
 }

@@ -18,6 +18,8 @@ the same deterministic kernels, so the gathered frame is bit-identical to the 1-
 """
 from __future__ import annotations
 
+import time
+
 import torch
 
 
@@ -162,32 +164,41 @@ def halo_px(cfg, max_radius_px: float = 512.0) -> int:
     return int(np.ceil(worst)) + 4
 
 
+FLT_MAX_BITS = 0x7F7FFFFF  # asuint(FLT_MAX): a cleared rayMin (SVAO.cpp:339)
+
+
 class HaloFrame:
-    """One AO frame split into CONTIGUOUS screen bands with halo exchanges:
-    the ranks exchange only the rows within reach of each other's samples instead of
-    all-reducing / all-gathering whole maps.
+    """One AO frame split into CONTIGUOUS screen bands with SPARSE halo exchanges.
 
-    Rank r of B owns visible rows [32 g_r, 32 g_{r+1}) (32-row groups split evenly) and the SD
-    rows [S_r, S_{r+1}) under them (8-row aligned).  Per frame:
+    Rank r of B owns the visible rows of its 32-row groups [g_r, g_{r+1}) and the SD rows under
+    them (8-row aligned).  Per frame:
 
-      1. pass 1 of its own rows (rsd_svao_pass1_rows) -- its partial ray intervals land within
-         `halo` SD rows of its band (the window W_r);
-      2. interval halo exchange: the part of W_r inside band k goes to rank k, which merges it
-         with MIN / MAX (exact on the non-negative float bit patterns) -> every rank holds the
-         exact union for its own SD rows, like the 1-GPU pass 1;
+      1. pass 1 of its own rows (rsd_svao_pass1_rows).  Its interval atomics land on SD texels
+         within `halo` rows of its band (the window W_r): exactly the texels its pass 2 will read
+         (pass 1 and pass 2 place a refined direction's sample on the same SD texel, Common.slang:
+         164-168; an atomic always lowers rayMin below asuint(FLT_MAX) or sets rayMax);
+      2. sparse interval halo: the TOUCHED texels of W_r inside band k (rayMin != asuint(FLT_MAX)
+         or rayMax != 0) go to rank k as (texel index, rayMin, rayMax) triples -- one all-gather of
+         the send counts (and of the previous frame's compute time) sizes the point-to-point
+         transfers; rank k merges them with scatter MIN / MAX (exact on the non-negative float
+         bit patterns) and holds the exact 1-GPU union for its SD rows;
       3. SD trace of its own SD rows (rsd_sd_trace_rows; consume resets the whole map);
-      4. SD halo exchange: rank k sends the rows of its band inside W_r to rank r (pass 2 of
-         band r reads SD texels only inside W_r);
+      4. sparse SD halo: rank k returns the N depths of exactly the texels r sent it in step 2 (k
+         already holds r's index list, so the reply carries values only);
       5. pass 2 of its own rows (rsd_svao_pass2_rows) and an all-gather of the AO bands.
 
-    Every SD texel and AO pixel is produced by exactly one rank with the same kernels, so the
-    frame is bit-identical to the 1-GPU frame.  Data per rank and frame: 2 x 4 B per texel of
-    the interval halo rows and 4N B per texel of the SD halo rows, instead of the whole maps.
+    Load balance ("re-split from the previous frame's per-band time"): every rank
+    times its own pass 1 + trace + pass 2; the times travel with the step-2 counts, and every rank
+    computes the same new split of the 32-row groups (cost spread uniformly over each band's
+    groups, equal predicted cost per rank, moved half-way from the current split), applied from
+    the next frame.  Every SD texel and AO pixel is still produced by exactly one rank with the
+    same kernels, so the frame is bit-identical to the 1-GPU frame whatever the split.
 
     `backend` provides pass1_rows(rows), sd_trace_rows(rows, consume=...), pass2_rows(rows),
     clear_intervals(), tensors ray_minmax (int32 [2, sdH, sdW]), sd, ao, and cfg / vao / sd_h."""
 
-    def __init__(self, backend, rank: int = 0, world: int = 1, pg=None, throughput: bool = False):
+    def __init__(self, backend, rank: int = 0, world: int = 1, pg=None, throughput: bool = False,
+                 rebalance: bool = True):
         import torch.distributed as dist
         b = self.b = backend
         self.rank, self.world, self.pg = rank, world, pg
@@ -195,17 +206,33 @@ class HaloFrame:
         self.trace_kw = {"throughput": True} if throughput and getattr(b, "can_consume_intervals", False) else {}
         self._intervals_clear = False
         cfg = b.cfg
+        self.V = cfg.fb_h - 2 * cfg.guard_band
+        self.G = (self.V + 31) // 32
+        self.gb = [self.G * r // world for r in range(world + 1)]  # first split: equal group counts
+        self.rebalance = rebalance and world > 1
+        self.halo_px = halo_px(cfg, float(b.vao.ssMaxRadius))
+        self.nccl = world > 1 and dist.get_backend(pg) == "nccl"
+        self.cuda = b.sd.is_cuda
+        self._ao_cap = 0
+        self._next_gb = None
+        self._prev = None  # timing of this rank's previous frame (events or seconds)
+        self.sent = {"intervals": 0, "sd": 0, "ao": 0}
+        self.frames = 0
+        self.splits = []  # the group split of every frame (diagnostics)
+        self._plan()
+
+    # ---- the partition implied by self.gb
+    def _plan(self):
+        b, world, me = self.b, self.world, self.rank
+        cfg = b.cfg
         g, div, sdg, sdh = cfg.guard_band, cfg.divisor, int(b.vao.sdGuard), b.sd_h
-        V = cfg.fb_h - 2 * g
-        G = (V + 31) // 32
-        gb = [G * r // world for r in range(world + 1)]
+        gb, V = self.gb, self.V
         self.px_rows = [(32 * gb[r], 32 * gb[r + 1]) for r in range(world)]  # visible rows, API ranges
         # SD rows under each band: SD row of frame-buffer row y = y / div + sdGuard (SVAO.cpp:700-716)
         S = [0] + [min(sdh, ((g + 32 * gb[r]) // div + sdg) // 8 * 8) for r in range(1, world)] + [sdh]
         for r in range(1, world + 1):
             S[r] = max(S[r], S[r - 1])
         self.sd_rows = [(S[r], S[r + 1]) for r in range(world)]
-        self.halo_px = halo_px(cfg, float(b.vao.ssMaxRadius))
         self.window = []
         for r in range(world):
             a_px = g + self.px_rows[r][0] - self.halo_px
@@ -215,43 +242,51 @@ class HaloFrame:
         def overlap(a, c):
             lo, hi = max(a[0], c[0]), min(a[1], c[1])
             return (lo, hi) if lo < hi else None
-        # interval halo: my window inside band k -> rank k;  SD halo: band k inside my window <- rank k
-        me = rank
+        # candidate rows: my window inside band k (my intervals -> k, k's depths -> me), and k's
+        # window inside my band (k's intervals -> me, my depths -> k)
         self.iv_send = {k: overlap(self.window[me], self.sd_rows[k]) for k in range(world) if k != me}
         self.iv_recv = {k: overlap(self.window[k], self.sd_rows[me]) for k in range(world) if k != me}
-        self.sd_send = {k: overlap(self.window[k], self.sd_rows[me]) for k in range(world) if k != me}
-        self.sd_recv = {k: overlap(self.window[me], self.sd_rows[k]) for k in range(world) if k != me}
-        dev = b.sd.device
-        mk = lambda t, rows: torch.empty((t.shape[0], rows[1] - rows[0]) + tuple(t.shape[2:]), dtype=t.dtype,  # noqa: E731
-                                         device=dev)
-        self.iv_sbuf = {k: mk(b.ray_minmax, r) for k, r in self.iv_send.items() if r}
-        self.iv_rbuf = {k: mk(b.ray_minmax, r) for k, r in self.iv_recv.items() if r}
-        self.sd_sbuf = {k: mk(b.sd, r) for k, r in self.sd_send.items() if r}
-        self.sd_rbuf = {k: mk(b.sd, r) for k, r in self.sd_recv.items() if r}
+        self.sd_send = dict(self.iv_recv)
+        self.sd_recv = dict(self.iv_send)
         # AO bands (frame-buffer rows), padded to the largest for one all-gather.  Pass 1 dispatches
         # roundup32 of the visible rows (SVAO.cpp:347-349), so the last band also writes the AO of up
         # to 31 guard-band rows below the visible region.
         self.ao_rows = [(g + self.px_rows[r][0], min(cfg.fb_h, g + self.px_rows[r][1])) for r in range(world)]
         self.ao_max = max(hi - lo for lo, hi in self.ao_rows)
-        W = b.ao.shape[1]
-        self.ao_send = torch.zeros((self.ao_max, W), dtype=b.ao.dtype, device=dev)
-        self.ao_recv = torch.zeros((world, self.ao_max, W), dtype=b.ao.dtype, device=dev)
-        self.nccl = world > 1 and dist.get_backend(pg) == "nccl"
+        row = b.ao[0].numel()  # elements per AO row (2 with dualAO)
+        if self.ao_max > self._ao_cap:
+            self._ao_send_buf = torch.zeros(self.ao_max * row, dtype=b.ao.dtype, device=b.ao.device)
+            self._ao_recv_buf = torch.zeros(world * self.ao_max * row, dtype=b.ao.dtype, device=b.ao.device)
+            self._ao_cap = self.ao_max
+        # exact-size contiguous views of the grow-only buffers (one all-gather of ao_max rows each)
+        shape = (self.ao_max,) + tuple(b.ao.shape[1:])
+        self.ao_send = self._ao_send_buf[:self.ao_max * row].view(shape)
+        self.ao_recv = self._ao_recv_buf[:world * self.ao_max * row].view((world,) + shape)
 
-    def bytes_per_frame(self):
-        """Bytes this rank sends per frame: interval halo, SD halo, AO band."""
-        iv = sum(t.numel() * t.element_size() for t in self.iv_sbuf.values())
-        sd = sum(t.numel() * t.element_size() for t in self.sd_sbuf.values())
+    def dense_bytes_per_frame(self):
+        """What the round-2 dense halo (whole candidate rows) would send per frame from this rank."""
+        b = self.b
+        iv = sum(2 * 4 * (hi - lo) * b.sd.shape[2] for r in self.iv_send.values() if r for lo, hi in [r])
+        sd_row = b.sd[:, 0].numel() * b.sd.element_size()
+        sd = sum((hi - lo) * sd_row for r in self.sd_send.values() if r for lo, hi in [r])
         return {"intervals": iv, "sd": sd, "ao": self.ao_send.numel() * self.ao_send.element_size()}
 
+    def bytes_per_frame(self):
+        """Mean bytes this rank sent per frame so far: sparse interval halo, sparse SD halo, AO band."""
+        n = max(1, self.frames)
+        return {k: int(v // n) for k, v in self.sent.items()}
+
+    # ---- collectives
     def _exchange(self, sends, recvs):
         """Point-to-point exchange (ncclSend / ncclRecv under RCCL): sends {peer: tensor}, recvs
         {peer: tensor}; returns after every transfer completed (stream-ordered for NCCL)."""
+        sends = {k: t for k, t in sends.items() if t.numel()}
+        recvs = {k: t for k, t in recvs.items() if t.numel()}
         staged = not self.nccl and any(t.is_cuda for t in list(sends.values()) + list(recvs.values()))
         if staged:  # gloo rehearsal with device tensors (several ranks on one GPU): via host copies
             sends = {k: t.cpu() for k, t in sends.items()}
             recvs_dev, recvs = recvs, {k: torch.empty(t.shape, dtype=t.dtype) for k, t in recvs.items()}
-        ops = [self.dist.P2POp(self.dist.isend, t, k, group=self.pg) for k, t in sends.items()]
+        ops = [self.dist.P2POp(self.dist.isend, t.contiguous(), k, group=self.pg) for k, t in sends.items()]
         ops += [self.dist.P2POp(self.dist.irecv, t, k, group=self.pg) for k, t in recvs.items()]
         if ops:
             for w in self.dist.batch_isend_irecv(ops):
@@ -260,46 +295,138 @@ class HaloFrame:
             for k, t in recvs.items():
                 recvs_dev[k].copy_(t)
 
+    def _all_gather_small(self, row):
+        """All-gather one int64 row per rank -> [world, len(row)] on the host (one sync)."""
+        t = torch.tensor(row, dtype=torch.int64)
+        if self.nccl:
+            t = t.cuda()
+            out = torch.empty((self.world, t.numel()), dtype=torch.int64, device=t.device)
+            self.dist.all_gather_into_tensor(out.view(-1), t, group=self.pg)
+            return out.cpu()
+        out = [torch.empty_like(t) for _ in range(self.world)]
+        self.dist.all_gather(out, t, group=self.pg)
+        return torch.stack(out)
+
+    # ---- timing of this rank's compute (load balance)
+    def _mark(self):
+        if self.cuda:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            return e
+        return time.perf_counter()
+
+    def _span_us(self, a, c):
+        if self.cuda:
+            return a.elapsed_time(c) * 1e3
+        return (c - a) * 1e6
+
+    def _rebalanced(self, costs):
+        """The next split of the 32-row groups from every rank's measured cost of the current one:
+        cost spread uniformly over each band's groups, boundaries where the cumulative cost crosses
+        k / world of the total, moved half-way (damping), at least one group per rank."""
+        G, world, gb = self.G, self.world, self.gb
+        dens = []
+        for r in range(world):
+            n = gb[r + 1] - gb[r]
+            dens += [max(float(costs[r]), 1e-3) / max(n, 1)] * n
+        cum = [0.0]
+        for x in dens:
+            cum.append(cum[-1] + x)
+        total = cum[-1]
+        new = [0]
+        for k in range(1, world):
+            target = total * k / world
+            j = next((i for i in range(1, G + 1) if cum[i] >= target), G)
+            # the nearer of the two group boundaries around the crossing
+            if j > 0 and target - cum[j - 1] < cum[j] - target:
+                j -= 1
+            new.append(int(round(0.5 * gb[k] + 0.5 * j)))
+        new.append(G)
+        if G >= world:  # monotone, one group per rank at least
+            for k in range(1, world):
+                new[k] = min(max(new[k], new[k - 1] + 1), G - (world - k))
+        return new
+
     def frame(self, sd_events=None):
-        b, me = self.b, self.rank
+        b, me, world = self.b, self.rank, self.world
+        if self._next_gb is not None and self._next_gb != self.gb:
+            self.gb = self._next_gb
+            self._plan()
+        self._next_gb = None
+        self.splits.append(tuple(self.gb))
         consume = getattr(b, "can_consume_intervals", False) and bool(b.cfg.ray_interval)
         if not (consume and self._intervals_clear):
             b.clear_intervals()
+        t0 = self._mark()
         b.pass1_rows(self.px_rows[me])
-        if self.world > 1 and b.cfg.ray_interval:
-            for k, t in self.iv_sbuf.items():
-                lo, hi = self.iv_send[k]
-                t.copy_(b.ray_minmax[:, lo:hi])
-            self._exchange(self.iv_sbuf, self.iv_rbuf)
-            for k, t in self.iv_rbuf.items():
-                lo, hi = self.iv_recv[k]
-                torch.minimum(b.ray_minmax[0, lo:hi], t[0], out=b.ray_minmax[0, lo:hi])
-                torch.maximum(b.ray_minmax[1, lo:hi], t[1], out=b.ray_minmax[1, lo:hi])
+        t1 = self._mark()
+        mine = {}  # k -> global texel indices of my window touched by my pass 1 inside band k
+        if world > 1:
+            sdw = b.ray_minmax.shape[2]
+            iv_send = {}
+            for k, rows in self.iv_send.items():
+                if not rows:
+                    continue
+                lo, hi = rows
+                reg = b.ray_minmax[:, lo:hi].reshape(2, -1)
+                flat = ((reg[0] != FLT_MAX_BITS) | (reg[1] != 0)).nonzero().squeeze(1)
+                idx = (flat + lo * sdw).to(torch.int32)
+                mine[k] = idx.long()
+                iv_send[k] = torch.cat([idx[None], reg[:, flat]], 0)  # [3, n] int32: index, rayMin, rayMax
+            prev_us = -1
+            if self._prev is not None:
+                prev_us = int(sum(self._span_us(a, c) for a, c in self._prev))
+            counts = [int(iv_send[k].shape[1]) if k in iv_send else 0 for k in range(world)]
+            M = self._all_gather_small(counts + [prev_us])  # [world, world + 1]: send counts, previous cost
+            if self.rebalance and int(M[:, world].min()) >= 0:
+                self._next_gb = self._rebalanced([float(x) for x in M[:, world].tolist()])
+            dev = b.ray_minmax.device
+            iv_recv = {k: torch.empty((3, int(M[k, me])), dtype=torch.int32, device=dev)
+                       for k in range(world) if k != me and int(M[k, me]) > 0}
+            self._exchange(iv_send, iv_recv)
+            self.sent["intervals"] += sum(t.numel() * 4 for t in iv_send.values())
+            theirs = {}
+            for k, t in iv_recv.items():
+                idx = t[0].long()
+                theirs[k] = idx
+                if b.cfg.ray_interval:
+                    b.ray_minmax[0].view(-1).scatter_reduce_(0, idx, t[1], reduce="amin")
+                b.ray_minmax[1].view(-1).scatter_reduce_(0, idx, t[2], reduce="amax")
         if sd_events:
             sd_events[0].record()
+        t2 = self._mark()
         if consume:
             b.sd_trace_rows(self.sd_rows[me], consume=True, **self.trace_kw)
         else:
             b.sd_trace_rows(self.sd_rows[me], **self.trace_kw)
         self._intervals_clear = consume
+        t3 = self._mark()
         if sd_events:
             sd_events[1].record()
-        if self.world > 1:
-            for k, t in self.sd_sbuf.items():
-                lo, hi = self.sd_send[k]
-                t.copy_(b.sd[:, lo:hi])
-            self._exchange(self.sd_sbuf, self.sd_rbuf)
-            for k, t in self.sd_rbuf.items():
-                lo, hi = self.sd_recv[k]
-                b.sd[:, lo:hi].copy_(t)
+        if world > 1:
+            L, sdh, sdw, ch = b.sd.shape
+            flat_sd = b.sd.view(L, sdh * sdw, ch)
+            sd_send = {k: flat_sd.index_select(1, idx) for k, idx in theirs.items()}
+            sd_recv = {k: torch.empty((L, idx.numel(), ch), dtype=b.sd.dtype, device=b.sd.device)
+                       for k, idx in mine.items() if idx.numel()}
+            self._exchange(sd_send, sd_recv)
+            self.sent["sd"] += sum(t.numel() * t.element_size() for t in sd_send.values())
+            for k, t in sd_recv.items():
+                flat_sd.index_copy_(1, mine[k], t)
+        t4 = self._mark()
         b.pass2_rows(self.px_rows[me])
-        if self.world > 1:
+        t5 = self._mark()
+        self._prev = [(t0, t1), (t2, t3), (t4, t5)]
+        if world > 1:
             lo, hi = self.ao_rows[me]
-            self.ao_send[:hi - lo].copy_(b.ao[lo:hi])
+            send, recv = self.ao_send, self.ao_recv
+            send[:hi - lo].copy_(b.ao[lo:hi])
             if self.nccl:
-                self.dist.all_gather_into_tensor(self.ao_recv.view(-1), self.ao_send.view(-1), group=self.pg)
+                self.dist.all_gather_into_tensor(recv.view(-1), send.view(-1), group=self.pg)
             else:
-                self.dist.all_gather(list(self.ao_recv.unbind(0)), self.ao_send, group=self.pg)
+                self.dist.all_gather(list(recv.unbind(0)), send, group=self.pg)
+            self.sent["ao"] += send.numel() * send.element_size()
             for k, (lo, hi) in enumerate(self.ao_rows):
                 if k != me:
-                    b.ao[lo:hi].copy_(self.ao_recv[k, :hi - lo])
+                    b.ao[lo:hi].copy_(recv[k, :hi - lo])
+        self.frames += 1

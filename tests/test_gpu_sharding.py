@@ -94,11 +94,13 @@ def _worker(rank, world, port, out_dir):
     r = Renderer(make_scene(name), FrameConfig(**kw))
     r.gbuffer()
     f = HaloFrame(r, rank, world)
-    for _ in range(2):  # the second frame relies on the first trace's consume
+    for i in range(4):  # frame 2 relies on frame 1's consume; frames 3-4 run re-balanced splits
         r.ao.zero_()
         f.frame()
-    torch.cuda.synchronize()
+        torch.cuda.synchronize()
+        np.save(os.path.join(out_dir, f"ao_{rank}_{i}.npy"), r.ao.cpu().numpy())
     g = r.numpy()
+    np.save(os.path.join(out_dir, f"sdrows_{rank}.npy"), np.array(f.sd_rows))
     np.save(os.path.join(out_dir, f"ao_{rank}.npy"), g["ao"])
     np.save(os.path.join(out_dir, f"sd_{rank}.npy"), g["sd"])
     np.save(os.path.join(out_dir, f"bytes_{rank}.npy"), np.array(list(f.bytes_per_frame().values())))
@@ -125,7 +127,9 @@ def test_halo_frame_three_ranks_equals_one_gpu(tmp_path):
     mp.start_processes(_worker, args=(3, _free_port(), str(tmp_path)), nprocs=3, join=True, start_method="spawn")
     for k in range(3):
         assert np.array_equal(np.load(tmp_path / f"ao_{k}.npy"), ref["ao"]), f"rank {k} AO"
-        lo, hi = plans[k].sd_rows[k]
+        for i in range(4):
+            assert np.array_equal(np.load(tmp_path / f"ao_{k}_{i}.npy"), ref["ao"]), f"rank {k} AO frame {i}"
+        lo, hi = np.load(tmp_path / f"sdrows_{k}.npy")[k]
         assert bits_equal(np.load(tmp_path / f"sd_{k}.npy")[:, lo:hi], ref["sd"][:, lo:hi]), f"rank {k} SD rows"
         iv, sd, _ = np.load(tmp_path / f"bytes_{k}.npy")
         assert iv + sd < full  # less than the whole interval + SD maps

@@ -94,7 +94,19 @@ def _worker(rank, world, port, out_dir, mode="band"):
     f = (BandFrame if mode == "band" else HaloFrame)(be, rank, world)
     f.frame()
     if mode == "halo":
-        f.frame()  # a second frame: intervals cleared again, the exchange buffers reused
+        # more frames: intervals cleared again, buffers reused, and the split re-balanced from the
+        # measured per-rank times (a skewed first split forces a real move); every frame must still
+        # give the 1-process image
+        f.gb = [0] + [1 + k for k in range(world - 1)] + [f.G]
+        f._plan()
+        for _ in range(3):
+            be.np_ao[:] = 0
+            f.frame()
+            np.save(os.path.join(out_dir, f"ao_{rank}_{f.frames}.npy"), be.np_ao)
+        np.save(os.path.join(out_dir, f"split_{rank}.npy"), np.array(f.splits))
+        np.save(os.path.join(out_dir, f"sdrows_{rank}.npy"), np.array(f.sd_rows))
+        np.save(os.path.join(out_dir, f"bytes_{rank}.npy"), np.array([f.sent["intervals"], f.sent["sd"],
+                                                                     f.frames]))
     np.save(os.path.join(out_dir, f"ao_{rank}.npy"), be.np_ao)
     np.save(os.path.join(out_dir, f"sd_{rank}.npy"), be.np_sd)
     dist.barrier()
@@ -131,10 +143,12 @@ def _halo_cfg():
     return small_frame_config(visible=(96, 448), guard=16, divisor=2, N=2)
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 4])
 def test_halo_sharded_frame_equals_single_process(oracle, tmp_path, world):
-    """HaloFrame (contiguous bands, interval + SD halo exchange over point-to-point sends):
-    every rank ends with the single-process AO image; its own SD rows equal the reference."""
+    """HaloFrame (contiguous bands, sparse interval + SD halo exchange over point-to-point sends,
+    load-balanced re-splits): every rank ends every frame with the single-process AO image; its
+    own SD rows equal the reference; the split moved; the sparse halo moved less than the dense
+    candidate rows would have."""
     from rsd.scenes import make_scene
     from rsd.shard import BandFrame
     ref = OracleBackend(oracle, make_scene("arcade_tiny"), _halo_cfg(), HALO_REACH)
@@ -144,11 +158,20 @@ def test_halo_sharded_frame_equals_single_process(oracle, tmp_path, world):
                        start_method="spawn")
     for r in range(world):
         assert np.array_equal(np.load(tmp_path / f"ao_{r}.npy"), ref.np_ao), f"rank {r} AO"
+        for fr in (2, 3, 4):
+            assert np.array_equal(np.load(tmp_path / f"ao_{r}_{fr}.npy"), ref.np_ao), f"rank {r} AO frame {fr}"
         sd = np.load(tmp_path / f"sd_{r}.npy")
-        lo, hi = _halo_plan(oracle, world, r).sd_rows[r]
+        lo, hi = np.load(tmp_path / f"sdrows_{r}.npy")[r]
         assert np.array_equal(sd[:, lo:hi].view(np.uint32), ref.np_sd[:, lo:hi].view(np.uint32)), f"rank {r} SD"
+    splits = np.load(tmp_path / "split_0.npy")
+    assert all(np.array_equal(splits, np.load(tmp_path / f"split_{r}.npy")) for r in range(world))  # same on all
+    assert not np.array_equal(splits[1], splits[-1])  # the skewed split was re-balanced
     p = _halo_plan(oracle, world, 0)
     assert p.window[0][1] < p.b.sd_h  # rank 0 did not receive the whole map
+    sent = sum(np.load(tmp_path / f"bytes_{r}.npy")[1] / np.load(tmp_path / f"bytes_{r}.npy")[2]
+               for r in range(world))
+    dense = sum(_halo_plan(oracle, world, r).dense_bytes_per_frame()["sd"] for r in range(world))
+    assert 0 < sent < dense  # only the texels the receivers read
 
 
 def _halo_plan(oracle, world, rank):
@@ -188,6 +211,33 @@ def test_halo_plan_partitions_and_bounds(oracle):
             for k, q in enumerate(plans):
                 if k != r:
                     assert p.iv_send[k] == q.iv_recv[r] and p.sd_recv[k] == q.sd_send[r]
+
+
+def test_halo_rebalance_moves_toward_cost():
+    """The re-split: an expensive band gives up groups, the same inputs give the same
+    split on every rank, and each rank keeps at least one group."""
+    import torch.distributed as dist
+    from rsd.shard import HaloFrame
+    for world in (2, 3, 4, 8):
+        from types import SimpleNamespace
+        cfg = small_frame_config(visible=(96, 1080), guard=16, divisor=2, N=2)
+        sd_h = 600
+        be = SimpleNamespace(cfg=cfg, vao=SimpleNamespace(sdGuard=32, ssMaxRadius=24.0), sd_h=sd_h,
+                             sd=torch.zeros((1, sd_h, 64, 2)), ray_minmax=torch.zeros((2, sd_h, 64), dtype=torch.int32),
+                             ao=torch.zeros((cfg.fb_h, cfg.fb_w), dtype=torch.uint8))
+        orig = dist.get_backend
+        dist.get_backend = lambda pg=None: "gloo"
+        try:
+            f = HaloFrame(be, 0, world)
+        finally:
+            dist.get_backend = orig
+        costs = [1.0] * world
+        costs[0] = 10.0  # band 0 ten times as expensive per group
+        new = f._rebalanced(costs)
+        assert new[0] == 0 and new[-1] == f.G and all(new[k] < new[k + 1] for k in range(world))
+        assert new[1] < f.gb[1]  # band 0 shrinks
+        assert new == f._rebalanced(list(costs))  # deterministic
+        assert f._rebalanced([1.0] * world) == f.gb  # balanced costs: no move
 
 
 def test_band_rows_partition():
