@@ -122,8 +122,24 @@ def _p(a):
     return a.ctypes.data_as(C.c_void_p) if a is not None else None
 
 
+def effective_cpus():
+    """CPUs this process may use at once: the affinity mask capped by the cgroup CPU quota (a GPU box
+    shows 256 CPUs under a 16-CPU quota)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        n = os.cpu_count() or 1
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            n = min(n, max(1, -(-int(q) // int(per))))
+    except (OSError, ValueError):
+        pass
+    return max(1, n)
+
+
 def _threads(n):
-    return int(n) if n else (os.cpu_count() or 1)
+    return int(n) if n else effective_cpus()
 
 
 class Scene:

@@ -39,8 +39,7 @@ __global__ void clear_intervals_kernel(uint32_t* rmin, uint32_t* rmax, uint32_t 
     }
 }
 
-// One direction of SVAORaster.ps.slang:49-105 for one pixel (any radius, any divisor, IEEE division
-// where the host reciprocals do not apply): the reference loop body
+// One direction of SVAORaster.ps.slang:49-105 for one pixel: the reference loop body
 __device__ __forceinline__ void pass1_dir_generic(const SvaoArgs& a, float u, float v, uint32_t px, uint32_t py,
                                                   const Basic& b, int i, float& ao, float& aoD, uint32_t& st) {
     const rsd_vao_data& d = a.d;
@@ -85,23 +84,9 @@ __device__ __forceinline__ void pass1_dir_generic(const SvaoArgs& a, float u, fl
     }
 }
 
-// element idx of a device table through a 32-bit byte offset from the (uniform) base: the load
-// takes the SGPR-base + VGPR-offset form instead of 64-bit address arithmetic per lane
-template <typename T>
-__device__ __forceinline__ T ld32(const T* base, uint32_t idx) {
-    return *reinterpret_cast<const T*>(reinterpret_cast<const char*>(base) + idx * (uint32_t)sizeof(T));
-}
-
-// SVAORaster.ps.slang:29-122 with the reference 2x2 group interleave (numthreads 16x16).  The pixel's
-// per-direction work is either the generic body above or, when no lane of the wave has its AO
-// radius clamped to ssMaxRadius (the host-evaluated direction terms then apply to every lane),
-// the LEAN body: ND directions unrolled with their constants in scalar registers, branch-free up
-// to the interval atomics (every quantity is evaluated and selected: an invalid or same-pixel
-// direction adds +0, which leaves the running sums' bits unchanged), the ratio test as one float
-// compare (SvaoConsts::ratioThr), divisions by pdf / sphereHeight through div_rcp, and 32-bit table
-// offsets.  Same bits as the generic body (tests/test_gpu_parity.py: every pass-1 case runs this
-// kernel; RSD_PASS1=generic selects the generic-only kernel for A/B).
-template <int ND, bool LEAN>
+// SVAORaster.ps.slang:29-122, [numthreads(16,16,1)] with the 2x2 group interleave.  (A branch-free
+// "lean" direction body -- host constants in SGPRs, predicated updates, one float ratio compare --
+// measured 74 vs 70 us at configs[1]: more VALU per direction and 64-73 VGPRs)
 __global__ void __launch_bounds__(256) svao_pass1_kernel(SvaoArgs a) {
     const uint32_t bx = blockIdx.x, by = blockIdx.y;
     const uint32_t ox = (bx / 2u) * 32u + 2u * threadIdx.x + (bx % 2u);
@@ -113,73 +98,11 @@ __global__ void __launch_bounds__(256) svao_pass1_kernel(SvaoArgs a) {
     float ao = 0.0f, aoD = 0.0f;  // bright, dark (DUAL_AO: SVAORaster.ps.slang:13 ao_t = float2)
     uint32_t st = 0;
     Basic b;
-    const bool ok = basic_init(a, u, v, b);
-    // the lean body needs the unclamped radius on every lane of the wave (uniform decision)
-    const bool lean = LEAN && __all(!ok || b.radius == d.radius);
-    if (!ok) {
+    if (!basic_init(a, u, v, b)) {
         ao = aoD = 1.0f;
-    } else if (!lean) {
+    } else {
 #pragma unroll 1
         for (int i = 0; i < (int)a.k.nd; ++i) pass1_dir_generic(a, u, v, px, py, b, i, ao, aoD, st);
-    } else {
-        const float nzD = make_nonzero(b.normalO.z, 0.0001f);
-        const float r1 = (1.0f + d.thickness) * b.radius;          // CONST_RADIUS term, Common.slang:37
-        const float rInt = b.radius + d.thickness * b.radius;      // the interval's r + thickness r
-        const bool offForce = d.sdGuard > 0;                       // off-screen sample -> ray (SD guard)
-        const bool rtForce = a.secondary == 3u;                    // TRACE_OUT_OF_SCREEN (Raytraced)
-        const float res0 = d.resolution[0], res1 = d.resolution[1];
-        const uint32_t W = (uint32_t)a.W, H = (uint32_t)a.H;
-#pragma unroll
-        for (int i = 0; i < ND; ++i) {
-            const float dx = a.k.dirDx[i], dy = a.k.dirDy[i], h = a.k.dirHeight[i];
-            const float yPdf = a.k.rcpPdf[i], yH = a.k.rcpHeight[i];
-            const float pdf = 2.0f * h;
-            // SampleAOData::Init (Common.slang:354-399)
-            const float zi = -(dx * b.normalO.x + dy * b.normalO.y) / nzD;
-            const float se = hmin(hmax(zi, -h), h);
-            const float n = h - se;
-            const bool valid = !(n < a.k.ratioThr[i]);
-            const f3 ip = b.posV + b.tangent * dx + b.bitangent * dy;
-            float su, sv;
-            view_to_uv(a, ip, su, sv);
-            const float ex = (u - su) * res0, ey = (v - sv) * res1;
-            const bool ssrAbove = ex * ex + ey * ey >= a.k.ssrMin2;
-            const float cu = saturate(su), cv = saturate(sv);
-            const bool inScreen = (su == cu) && (sv == cv);
-            const uint32_t kx = (uint32_t)(int)floorf(cu * res0), ky = (uint32_t)(int)floorf(cv * res1);
-            const bool same = kx == px && ky == py;  // isSamePixel on indices (SvaoConsts::samePixelInt)
-            // evalPrimaryVisibility (Common.slang:492-496) at the snapped uv (depth_center's direct fetch)
-            const float ru = ld32(a.snapU, kx), rv = ld32(a.snapV, ky);
-            const float zp = ld32(a.depth, min(ky, H - 1u) * W + min(kx, W - 1u));
-            const float oz = dot(uv_to_view(a, ru, rv, zp) - b.posV, b.normal);
-            const float sphere = div_rcp(hmax(h - hmax(se, oz), 0.0f), pdf, yPdf);
-            const float xh = oz - r1;
-            const float hr = xh >= h ? 1.0f : saturate(div_rcp(xh, h, yH));
-            const float vis = sphere + (xh > 0.0f ? div_rcp(hr * (h - se), pdf, yPdf) : 0.0f);
-            const float wSame = div_rcp(n, pdf, yPdf);
-            // requireRay (Common.slang:455-461) and the SVAORaster.ps.slang:62-80 ray forcing
-            const bool off = !inScreen && offForce;
-            const float osz = off ? 3.402823466e+38f : oz;
-            const bool req = osz > h + (r1 - h) && ssrAbove;
-            const bool need = valid && !same && (req || off || (rtForce && !inScreen));
-            ao += valid ? (same ? wSame : vis) : 0.0f;
-            aoD += (valid && !need) ? (same ? wSame : vis) : 0.0f;
-            st |= need ? (1u << i) : 0u;
-            if (need && a.secondary == 2u) {
-                const uint32_t sx = (uint32_t)uv_to_sd(su, d.lowResolution[0], d.sdGuard);
-                const uint32_t sy = (uint32_t)uv_to_sd(sv, d.lowResolution[1], d.sdGuard);
-                const uint32_t o = sy * (uint32_t)a.sdW + sx;
-                if (a.rayInterval) {
-                    const float osMin = hmin(osz, rInt + h);
-                    atomicMin(&a.rayMin[o], asuint(hmax(b.posVLength - osMin, 0.0f)));
-                    atomicMax(&a.rayMax[o], asuint(hmax(b.posVLength - se, 0.0f)));
-                } else {
-                    a.rayMax[o] = 1u;
-                }
-            }
-        }
-    }
-    if (ok) {
         ao *= a.k.invNd;  // SVAORaster.ps.slang:108-109
         ao *= 2.0f;
         aoD *= a.k.invNd;
@@ -272,50 +195,49 @@ __device__ __forceinline__ void svao_pass2_dir(const SvaoArgs& a, const Basic& b
 constexpr int kP2Tile = 16;                   // pass-2 tile edge (pixels): 16 measured 33 us, 8 35 us, 32 65 us
 constexpr int kP2Lanes = kP2Tile * kP2Tile;   // lanes per workgroup = pixels per tile
 static_assert(kP2Tile == (int)kTileEdge, "busy-tile flags are per pass-2 tile");
-template <int N, int ND>
-__global__ void __launch_bounds__(kP2Lanes) svao_pass2_kernel(SvaoArgs a) {
-    constexpr uint32_t T = kP2Tile, L = kP2Lanes;
-    __shared__ uint32_t sPix[L];        // active pixel slot: local index
-    __shared__ uint16_t sPair[ND * L];  // pair: slot << 5 | direction
-    __shared__ uint16_t sFirst[L];     // first pair of each slot
-    __shared__ float sAcc[L];          // running vis of each slot (bright)
-    __shared__ float sAccD[L];         // ... dark channel (DUAL_AO)
-    __shared__ float sP[L], sR[L];
+// the LDS of one pass-2 tile (26 KB: 6 workgroups per CU)
+template <int ND>
+struct P2Shared {
+    uint32_t pix[kP2Lanes];        // active pixel slot: local index
+    uint16_t pair[ND * kP2Lanes];  // pair: slot << 5 | direction
+    uint16_t first[kP2Lanes];      // first pair of each slot
+    float acc[kP2Lanes];           // running vis of each slot (bright)
+    float accD[kP2Lanes];          // ... dark channel (DUAL_AO)
+    float p[kP2Lanes], r[kP2Lanes];
     // the pixel's BasicAOData, evaluated once per pixel, not per pair: the 16 floats pass 2 reads
-    // (posVLength, normalV, radiusInPixels stay out: 26 KB of LDS -> 6 workgroups per CU, not 5)
-    __shared__ float sBasic[L][16];
-    __shared__ uint32_t sNPix, sNPair;
+    // (posVLength, normalV, radiusInPixels stay out)
+    float basic[kP2Lanes][16];
+    uint32_t nPix, nPair;
+};
+
+// One kP2Tile^2 tile whose top-left pixel is (x0, y0); flag: its busy-tile flag (cleared) or null
+template <int N, int ND>
+__device__ __forceinline__ void pass2_tile(const SvaoArgs& a, uint32_t x0, uint32_t y0, uint8_t* flag,
+                                           P2Shared<ND>& sh) {
+    constexpr uint32_t T = kP2Tile, L = kP2Lanes;
     const uint32_t tid = threadIdx.x;
     const rsd_vao_data& d = a.d;
-    constexpr uint32_t kPerGroup = 32u / T;  // tile rows per 32-row band group
-    const uint32_t x0 = blockIdx.x * T + a.guard;
-    const uint32_t y0 = ((blockIdx.y / kPerGroup) * a.bandCount + a.bandIndex) * 32u + (blockIdx.y % kPerGroup) * T +
-                        a.guard;
-    // busy-tile flags (pass 1): an unflagged tile holds no stencilled pixel -- the whole group returns
-    // before any barrier (SVAORaster2.ps.slang:50-52 returns per pixel on aoMask == 0)
-    uint8_t* flag = a.tileFlags ? a.tileFlags + ((y0 - a.guard) / T) * a.tilesX + blockIdx.x : nullptr;
-    if (flag && *flag == 0u) return;
-    if (tid == 0) { sNPix = 0u; sNPair = 0u; }
+    if (tid == 0) { sh.nPix = 0u; sh.nPair = 0u; }
     __syncthreads();
     {
         const uint32_t px = x0 + (tid % T), py = y0 + (tid / T);
         const uint32_t m =
             (px < (uint32_t)a.W - a.guard && py < (uint32_t)a.H - a.guard) ? stencil_load(a, (size_t)py * a.W + px) : 0u;
         if (m) {
-            const uint32_t slot = atomicAdd(&sNPix, 1u), base = atomicAdd(&sNPair, (uint32_t)__popc(m));
-            sPix[slot] = tid;
-            sFirst[slot] = (uint16_t)base;
-            sAcc[slot] = 0.0f;
-            sAccD[slot] = 0.0f;
+            const uint32_t slot = atomicAdd(&sh.nPix, 1u), base = atomicAdd(&sh.nPair, (uint32_t)__popc(m));
+            sh.pix[slot] = tid;
+            sh.first[slot] = (uint16_t)base;
+            sh.acc[slot] = 0.0f;
+            sh.accD[slot] = 0.0f;
             uint32_t j = base;
             for (int i = 0; i < ND; ++i)
-                if (m & (1u << i)) sPair[j++] = (uint16_t)(slot << 5 | i);
+                if (m & (1u << i)) sh.pair[j++] = (uint16_t)(slot << 5 | i);
             // a non-zero stencil means pass 1's basic_init of this pixel succeeded (same bits)
             const float u = ((float)px + 0.5f) * d.invResolution[0];
             const float v = ((float)py + 0.5f) * d.invResolution[1];
             Basic b;
             basic_init(a, u, v, b);
-            float* q = sBasic[slot];
+            float* q = sh.basic[slot];
             q[0] = b.posV.x; q[1] = b.posV.y; q[2] = b.posV.z;
             q[3] = b.normal.x; q[4] = b.normal.y; q[5] = b.normal.z;
             q[6] = b.tangent.x; q[7] = b.tangent.y; q[8] = b.tangent.z;
@@ -326,17 +248,17 @@ __global__ void __launch_bounds__(kP2Lanes) svao_pass2_kernel(SvaoArgs a) {
     }
     __syncthreads();
     if (flag && tid == 0) *flag = 0u;  // consumed: the next pass 1 on this stream starts from zero
-    const uint32_t nPix = sNPix, nPair = sNPair;
+    const uint32_t nPix = sh.nPix, nPair = sh.nPair;
     for (uint32_t c = 0; c < nPair; c += L) {
         const uint32_t k = c + tid;
         uint32_t slot = 0;
         if (k < nPair) {
-            const uint32_t e = sPair[k];
+            const uint32_t e = sh.pair[k];
             slot = e >> 5;
-            const uint32_t lp = sPix[slot] & 255u;
+            const uint32_t lp = sh.pix[slot] & 255u;
             const float u = ((float)(x0 + lp % T) + 0.5f) * d.invResolution[0];
             const float v = ((float)(y0 + lp / T) + 0.5f) * d.invResolution[1];
-            const float* q = sBasic[slot];
+            const float* q = sh.basic[slot];
             Basic b;
             b.posV = mk(q[0], q[1], q[2]);
             b.normal = mk(q[3], q[4], q[5]);
@@ -349,26 +271,67 @@ __global__ void __launch_bounds__(kP2Lanes) svao_pass2_kernel(SvaoArgs a) {
             b.radiusInPixels = 0.0f;
             float p, r;
             svao_pass2_dir<N>(a, b, u, v, (int)(e & 31u), p, r);
-            sP[tid] = p;
-            sR[tid] = r;
+            sh.p[tid] = p;
+            sh.r[tid] = r;
         }
         __syncthreads();
         // the lane of a pixel's first pair in this chunk applies its pairs in direction order
-        if (k < nPair && k == max((uint32_t)sFirst[slot], c)) {
-            float acc = sAcc[slot], accD = sAccD[slot];
-            for (uint32_t j = k; j < nPair && j < c + L && (uint32_t)(sPair[j] >> 5) == slot; ++j) {
-                acc = (acc - sP[j - c]) + sR[j - c];  // calcAO2: visibility.x -= raster; visibility += refined
-                accD = accD + sR[j - c];
+        if (k < nPair && k == max((uint32_t)sh.first[slot], c)) {
+            float acc = sh.acc[slot], accD = sh.accD[slot];
+            for (uint32_t j = k; j < nPair && j < c + L && (uint32_t)(sh.pair[j] >> 5) == slot; ++j) {
+                acc = (acc - sh.p[j - c]) + sh.r[j - c];  // calcAO2: visibility.x -= raster; visibility += refined
+                accD = accD + sh.r[j - c];
             }
-            sAcc[slot] = acc;
-            sAccD[slot] = accD;
+            sh.acc[slot] = acc;
+            sh.accD[slot] = accD;
         }
         __syncthreads();
     }
     for (uint32_t sl = tid; sl < nPix; sl += L) {
-        const uint32_t lp = sPix[sl] & 255u;
+        const uint32_t lp = sh.pix[sl] & 255u;
         const size_t o = (size_t)(y0 + lp / T) * a.W + (x0 + lp % T);
-        ao_finish(a, o, sAcc[sl], sAccD[sl]);
+        ao_finish(a, o, sh.acc[sl], sh.accD[sl]);
+    }
+}
+
+// Pass 2 grids.  svao_pass2_tiles_kernel: one workgroup per tile of the band's 32-row groups (an
+// unflagged tile returns at once).  svao_pass2_persistent_kernel (the default with busy-tile flags):
+// a few workgroups per CU stride over the band's tiles and work only the flagged ones --
+// dispatching a workgroup for each of the ~8 K tiles of a 1080p frame costs ~12 us by itself when
+// only ~2 K hold a stencilled pixel (tools/pass2_probe.py).  The loop's invariant kernel arguments
+// would take 97 VGPRs (4 waves / SIMD); the waves-per-EU bound keeps it at 80 (6 waves / SIMD, the
+// LDS limit) with a few spilled invariants.
+template <int N, int ND>
+__device__ __forceinline__ uint32_t pass2_origin_y(const SvaoArgs& a, uint32_t ty) {
+    constexpr uint32_t kPerGroup = 32u / kP2Tile;  // tile rows per 32-row band group
+    return ((ty / kPerGroup) * a.bandCount + a.bandIndex) * 32u + (ty % kPerGroup) * kP2Tile + a.guard;
+}
+
+template <int N, int ND>
+__global__ void __launch_bounds__(kP2Lanes) svao_pass2_tiles_kernel(SvaoArgs a) {
+    __shared__ P2Shared<ND> sh;
+    const uint32_t y0 = pass2_origin_y<N, ND>(a, blockIdx.y);
+    uint8_t* flag = a.tileFlags ? a.tileFlags + ((y0 - a.guard) / kP2Tile) * a.tilesX + blockIdx.x : nullptr;
+    if (flag && *flag == 0u) return;  // uniform over the workgroup, before any barrier
+    pass2_tile<N, ND>(a, blockIdx.x * kP2Tile + a.guard, y0, flag, sh);
+}
+
+template <int N, int ND>
+__global__ void __launch_bounds__(kP2Lanes)
+#ifndef RSD_P2_NO_WPE
+__attribute__((amdgpu_waves_per_eu(6, 8)))
+#endif
+svao_pass2_persistent_kernel(SvaoArgs a, uint32_t tileRows) {
+    static_assert(ND == 8, "the persistent grid is sized for the 8-direction LDS footprint");
+    __shared__ P2Shared<ND> sh;
+    const uint32_t tilesX = (uint32_t)(a.W - 2 * (int)a.guard + (int)kP2Tile - 1) / kP2Tile, n = tilesX * tileRows;
+#pragma unroll 1
+    for (uint32_t t = blockIdx.x; t < n; t += gridDim.x) {
+        const uint32_t tx = t % tilesX, y0 = pass2_origin_y<N, ND>(a, t / tilesX);
+        uint8_t* flag = a.tileFlags + ((y0 - a.guard) / kP2Tile) * a.tilesX + tx;
+        if (*flag == 0u) continue;  // uniform over the workgroup
+        pass2_tile<N, ND>(a, tx * kP2Tile + a.guard, y0, flag, sh);
+        __syncthreads();  // the next tile reuses the LDS
     }
 }
 
@@ -532,21 +495,7 @@ rsd_status pass1_impl(const rsd_camera* cam, const rsd_vao_data* vao, const rsd_
     a.bandIndex = start;
     a.bandCount = step;
     if (bandGroups == 0) return RSD_OK;
-    // the lean kernel needs the host reciprocals for every direction, index-based isSamePixel and
-    // depth_center's direct fetch (frames up to 4096 px); RSD_PASS1=generic forces the generic body
-    static const bool forceGeneric = [] {
-        const char* e = getenv("RSD_PASS1");
-        return e && std::string(e) == "generic";
-    }();
-    const uint32_t allDirs = a.k.nd == 32u ? 0xffffffffu : ((1u << a.k.nd) - 1u);
-    const bool lean = !forceGeneric && (a.k.fastDiv & allDirs) == allDirs && a.k.samePixelInt && W <= 4096u &&
-                      H <= 4096u;
-    const dim3 grid(nx / 16, 2 * bandGroups), block(16, 16);
-    hipStream_t s = (hipStream_t)stream;
-    if (!lean) hipLaunchKernelGGL((svao_pass1_kernel<8, false>), grid, block, 0, s, a);
-    else if (a.k.nd == 32u) hipLaunchKernelGGL((svao_pass1_kernel<32, true>), grid, block, 0, s, a);
-    else if (a.k.nd == 16u) hipLaunchKernelGGL((svao_pass1_kernel<16, true>), grid, block, 0, s, a);
-    else hipLaunchKernelGGL((svao_pass1_kernel<8, true>), grid, block, 0, s, a);
+    hipLaunchKernelGGL(svao_pass1_kernel, dim3(nx / 16, 2 * bandGroups), dim3(16, 16), 0, (hipStream_t)stream, a);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? RSD_OK : hip_fail(e, "svao_pass1_kernel launch");
 }
@@ -629,13 +578,29 @@ rsd_status pass2_impl(const rsd_camera* cam, const rsd_vao_data* vao, const rsd_
     a.bandIndex = start;
     a.bandCount = step;
     if (bandGroups == 0) return RSD_OK;
-    dim3 grid((vw + kP2Tile - 1) / kP2Tile, (32 / kP2Tile) * bandGroups), block(kP2Lanes);
+    const uint32_t tileRows = (32 / kP2Tile) * bandGroups, tilesX = (vw + kP2Tile - 1) / kP2Tile;
+    static const bool tilesGrid = [] {  // RSD_P2_GRID=tiles: one workgroup per tile (A/B runs)
+        const char* e = getenv("RSD_P2_GRID");
+        return e && std::string(e) == "tiles";
+    }();
+    static const int cus = [] {
+        int dev = 0, n = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            n = 256;
+        return std::max(1, n);
+    }();
+    const bool persist = a.tileFlags && !tilesGrid;
+    // persistent: 6 resident workgroups per CU (26 KB LDS each)
+    const dim3 grid = persist ? dim3(std::min<uint32_t>(tilesX * tileRows, 6u * (uint32_t)cus)) : dim3(tilesX, tileRows);
+    const dim3 block(kP2Lanes);
     hipStream_t s = (hipStream_t)stream;
     const uint32_t nd = a.k.nd;
-#define RSD_P2(NN)                                                                                           \
-    if (nd == 32u) hipLaunchKernelGGL((svao_pass2_kernel<NN, 32>), grid, block, 0, s, a);                  \
-    else if (nd == 16u) hipLaunchKernelGGL((svao_pass2_kernel<NN, 16>), grid, block, 0, s, a);             \
-    else hipLaunchKernelGGL((svao_pass2_kernel<NN, 8>), grid, block, 0, s, a);
+    // 16 / 32 directions: the pair lists take 8 / 16 KB more LDS (4 workgroups per CU): per-tile grid
+#define RSD_P2(NN)                                                                                            \
+    if (nd == 32u) hipLaunchKernelGGL((svao_pass2_tiles_kernel<NN, 32>), dim3(tilesX, tileRows), block, 0, s, a); \
+    else if (nd == 16u) hipLaunchKernelGGL((svao_pass2_tiles_kernel<NN, 16>), dim3(tilesX, tileRows), block, 0, s, a); \
+    else if (persist) hipLaunchKernelGGL((svao_pass2_persistent_kernel<NN, 8>), grid, block, 0, s, a, tileRows); \
+    else hipLaunchKernelGGL((svao_pass2_tiles_kernel<NN, 8>), grid, block, 0, s, a);
     switch (N) {
         case 1: RSD_P2(1) break;
         case 2: RSD_P2(2) break;

@@ -27,9 +27,6 @@ struct SvaoConsts {
     // both divisors of direction i lie in [2^-30, 2^30]
     float rcpPdf[kMaxDirections], rcpHeight[kMaxDirections];
     uint32_t fastDiv;
-    // ratio_le_tenth(n, 2 h_i) as one float compare: n < ratioThr[i] <=> (double)n < M * 2 h_i, with
-    // ratioThr[i] = M * 2 h_i rounded UP to float (no float lies strictly between it and the double)
-    float ratioThr[kMaxDirections];
     uint32_t samePixelInt;  // isSamePixel decided on pixel indices (fill_consts)
     uint32_t nd;            // NUM_DIRECTIONS
     float invNd;            // 1.0 / float(NUM_DIRECTIONS) (SVAORaster.ps.slang:108, Common.slang:660)
@@ -379,10 +376,6 @@ inline void fill_consts(SvaoConsts& k, const rsd_vao_data& d, uint32_t nd) {
         k.rcpHeight[i] = (float)(1.0 / (double)h);
         const bool ok = h >= 0x1p-30f && pdf <= 0x1p30f;
         if (ok) k.fastDiv |= 1u << i;
-        const double T = ((double)0.1f + 0x1p-28) * (double)(2.0f * h);  // ratio_le_tenth's M * D
-        float t = (float)T;
-        if ((double)t < T) t = std::nextafter(t, INFINITY);
-        k.ratioThr[i] = t;
     }
 }
 
