@@ -19,7 +19,7 @@ Two timed regions, each K frames between a barrier + torch.cuda.synchronize() pa
   throughput F frames in flight (--frames-in-flight, default 4): frame i runs on HIP stream
              i % F with its own frame buffers, frames of different slots overlap (the latency-
              bound SD trace of one frame shares the machine with the VALU-bound passes of
-             others; overlapping traces use librsd's work-efficient walk, RSD_SD_THROUGHPUT).
+             others; traces are flagged RSD_SD_THROUGHPUT, which librsd may use to pick a walk).
                ms_per_step, throughput.ao_frames_per_s, throughput.frame_mrays_per_s
 
 --camera-path orbit120 (default for configs[4], bistro_4k_full_n16): every frame renders the

@@ -313,9 +313,10 @@ rsd_status rsd_sd_trace_band(rsd_scene* scene, const rsd_camera* cam, const rsd_
  * the whole map, not only the band -- so the next frame's pass 1 may run without
  * rsd_svao_clear_intervals (SVAO.cpp:334-340 folded into the trace's first kernel). */
 #define RSD_SD_CONSUME_INTERVALS 1u
-/* RSD_SD_THROUGHPUT: the caller overlaps this trace with other GPU work (frames in flight), so
- * librsd picks the work-efficient traversal (4 lanes per ray, depth-first) over the
- * latency-optimised row walk (8 lanes per ray).  Same result bits either way. */
+/* RSD_SD_THROUGHPUT: the caller overlaps this trace with other GPU work (frames in flight).  A hint:
+ * librsd measured the row walk (8 lanes per ray) ahead of the depth-first quad walk there too since
+ * the segment entry grid, so it currently picks the same walk either way.
+ * Same result bits whatever the walk. */
 #define RSD_SD_THROUGHPUT 2u
 rsd_status rsd_sd_trace_band_ex(rsd_scene* scene, const rsd_camera* cam, const rsd_sd_params* params,
                                 const float* d_linear_z, uint32_t z_w, uint32_t z_h,

@@ -144,6 +144,26 @@ __device__ __forceinline__ f3 decode_normal_2x8(uint32_t packed) {
     return normalize(n);
 }
 
+// SD-map texel addressing.  The product layout is Texture2DArray order [layer][y][x][ch]
+// (StochasticDepthMapRT.cpp:177-216).  RSD_SD_TILED (an A/B build only, SURVEY 7.3's "8x8-texel
+// tiles"): each layer is stored as 8x8-texel tiles, row-major inside a tile and tiles row-major,
+// over a map padded to whole tiles (sd_plane_texels) -- measured no faster, DESIGN.md section 4.
+__device__ __forceinline__ size_t sd_texel(int x, int y, int W) {
+#ifdef RSD_SD_TILED
+    const int tw = (W + 7) >> 3;
+    return ((size_t)((y >> 3) * tw + (x >> 3)) << 6) + (size_t)((y & 7) * 8 + (x & 7));
+#else
+    return (size_t)y * W + x;
+#endif
+}
+__device__ __forceinline__ size_t sd_plane_texels(int W, int H) {
+#ifdef RSD_SD_TILED
+    return (size_t)((W + 7) >> 3) * ((H + 7) >> 3) * 64u;
+#else
+    return (size_t)W * H;
+#endif
+}
+
 __device__ __forceinline__ uint32_t asuint(float f) { return __float_as_uint(f); }
 __device__ __forceinline__ float asfloat(uint32_t u) { return __uint_as_float(u); }
 

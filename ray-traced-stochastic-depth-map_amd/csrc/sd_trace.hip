@@ -252,8 +252,8 @@ __device__ __forceinline__ uint32_t f16_bits(float v) {
 }
 template <int N>
 __device__ __forceinline__ void sd_store(const SDArgs& a, int x, int y, const float (&depths)[N]) {
-    const size_t plane = (size_t)a.sdW * a.sdH;
-    const size_t o = (size_t)y * a.sdW + x;
+    const size_t plane = sd_plane_texels(a.sdW, a.sdH);
+    const size_t o = sd_texel(x, y, a.sdW);
     if constexpr (N <= 4) {
         if (a.f16) {
             if constexpr (N == 1) {
@@ -2052,11 +2052,13 @@ rsd_status sd_trace_impl(rsd_scene* scene, const rsd_camera* cam, const rsd_sd_p
     // (rsd_sd_trace, row vs quad: 1080p/4 0.43 M texels 92 vs 133 us; 4K/4 1.0 M texels 443 vs
     // 327 us; 1080p full 6.9 M texels 688 vs 294 us -- DESIGN.md section 4)
     const uint64_t bandTexels = (uint64_t)sd_w * std::min<uint64_t>((uint64_t)n * kTile, sd_h);
-    // RSD_SD_THROUGHPUT (frames in flight): the row walk's spare lanes are VALU time taken from
-    // the overlapping frames, so the quad walk wins there (1080p/4, 4 frames in flight: 108 vs
-    // 118 us per frame; one frame alone: 245 vs 197 us -- DESIGN.md section 4)
+    // RSD_SD_THROUGHPUT (frames in flight) no longer changes the walk: round 1 measured the quad walk
+    // ahead with frames in flight (108 vs 118 us per frame), but with the segment entry grid and the
+    // longest-first queue the row walk is ahead at every F (20-frame bench, configs[1]: F = 2/3/4/6
+    // -> 169/157/154/161 vs 200/172/162/171 us; profiles/round3/ab/walk_*.json)
+    (void)throughput;
     const bool rowWalk = a.poolSoft >= 16 && walkName != "quad" &&
-                         (walkName == "fused" || walkName == "split" || (bandTexels <= 600000u && !throughput));
+                         (walkName == "fused" || walkName == "split" || bandTexels <= 600000u);
     // default: the fused row walk; RSD_TRACE_WALK=split|quad for A/B runs
     // raster walk: triangles -> per-texel K nearest keys (split-eligible canonical traces; the near
     // clip needs the cosine bound)

@@ -14,7 +14,6 @@
 #include <cmath>
 #include <cstdlib>
 #include <mutex>
-#include <string>
 #include <vector>
 
 #include "rsd_device.h"
@@ -133,7 +132,7 @@ __device__ __forceinline__ void svao_pass2_dir(const SvaoArgs& a, const Basic& b
                                                float& r) {
     const rsd_vao_data& d = a.d;
     const float depthRange = a.cam.farZ - a.cam.nearZ, depthOffset = a.cam.nearZ;
-    const size_t plane = (size_t)a.sdW * a.sdH;
+    const size_t plane = sd_plane_texels(a.sdW, a.sdH);
     Sample s;
     bool ssrAbove;
     sample_init(a, u, v, b, i, s, ssrAbove);
@@ -145,7 +144,7 @@ __device__ __forceinline__ void svao_pass2_dir(const SvaoArgs& a, const Basic& b
     sd_jitter((uint32_t)cx, (uint32_t)cy, a.sdJitter != 0u, jx, jy);
     const float su = ((float)(cx - d.sdGuard) + jx) / d.lowResolution[0];
     const float sv = ((float)(cy - d.sdGuard) + jy) / d.lowResolution[1];
-    const size_t so = (size_t)cy * a.sdW + cx;
+    const size_t so = sd_texel(cx, cy, a.sdW);
     float dep[N];
     if constexpr (N == 1) {
         dep[0] = a.sd[so];
@@ -294,45 +293,19 @@ __device__ __forceinline__ void pass2_tile(const SvaoArgs& a, uint32_t x0, uint3
     }
 }
 
-// Pass 2 grids.  svao_pass2_tiles_kernel: one workgroup per tile of the band's 32-row groups (an
-// unflagged tile returns at once).  svao_pass2_persistent_kernel (the default with busy-tile flags):
-// a few workgroups per CU stride over the band's tiles and work only the flagged ones --
-// dispatching a workgroup for each of the ~8 K tiles of a 1080p frame costs ~12 us by itself when
-// only ~2 K hold a stencilled pixel (tools/pass2_probe.py).  The loop's invariant kernel arguments
-// would take 97 VGPRs (4 waves / SIMD); the waves-per-EU bound keeps it at 80 (6 waves / SIMD, the
-// LDS limit) with a few spilled invariants.
+// One workgroup per tile of the band's 32-row groups; an unflagged tile (busy-tile flags of pass 1)
+// returns before any barrier.  (A persistent grid of 6 workgroups per CU striding over the flagged
+// tiles measured 48-51 vs 36-38 us at configs[1]: the busy tiles cluster, so some workgroups
+// serialise several dependent tile chains -- tools/pass2_probe.py)
 template <int N, int ND>
-__device__ __forceinline__ uint32_t pass2_origin_y(const SvaoArgs& a, uint32_t ty) {
+__global__ void __launch_bounds__(kP2Lanes) svao_pass2_kernel(SvaoArgs a) {
     constexpr uint32_t kPerGroup = 32u / kP2Tile;  // tile rows per 32-row band group
-    return ((ty / kPerGroup) * a.bandCount + a.bandIndex) * 32u + (ty % kPerGroup) * kP2Tile + a.guard;
-}
-
-template <int N, int ND>
-__global__ void __launch_bounds__(kP2Lanes) svao_pass2_tiles_kernel(SvaoArgs a) {
     __shared__ P2Shared<ND> sh;
-    const uint32_t y0 = pass2_origin_y<N, ND>(a, blockIdx.y);
+    const uint32_t y0 = ((blockIdx.y / kPerGroup) * a.bandCount + a.bandIndex) * 32u + (blockIdx.y % kPerGroup) * kP2Tile +
+                        a.guard;
     uint8_t* flag = a.tileFlags ? a.tileFlags + ((y0 - a.guard) / kP2Tile) * a.tilesX + blockIdx.x : nullptr;
-    if (flag && *flag == 0u) return;  // uniform over the workgroup, before any barrier
+    if (flag && *flag == 0u) return;  // uniform over the workgroup
     pass2_tile<N, ND>(a, blockIdx.x * kP2Tile + a.guard, y0, flag, sh);
-}
-
-template <int N, int ND>
-__global__ void __launch_bounds__(kP2Lanes)
-#ifndef RSD_P2_NO_WPE
-__attribute__((amdgpu_waves_per_eu(6, 8)))
-#endif
-svao_pass2_persistent_kernel(SvaoArgs a, uint32_t tileRows) {
-    static_assert(ND == 8, "the persistent grid is sized for the 8-direction LDS footprint");
-    __shared__ P2Shared<ND> sh;
-    const uint32_t tilesX = (uint32_t)(a.W - 2 * (int)a.guard + (int)kP2Tile - 1) / kP2Tile, n = tilesX * tileRows;
-#pragma unroll 1
-    for (uint32_t t = blockIdx.x; t < n; t += gridDim.x) {
-        const uint32_t tx = t % tilesX, y0 = pass2_origin_y<N, ND>(a, t / tilesX);
-        uint8_t* flag = a.tileFlags + ((y0 - a.guard) / kP2Tile) * a.tilesX + tx;
-        if (*flag == 0u) continue;  // uniform over the workgroup
-        pass2_tile<N, ND>(a, tx * kP2Tile + a.guard, y0, flag, sh);
-        __syncthreads();  // the next tile reuses the LDS
-    }
 }
 
 }  // namespace rsd
@@ -495,7 +468,18 @@ rsd_status pass1_impl(const rsd_camera* cam, const rsd_vao_data* vao, const rsd_
     a.bandIndex = start;
     a.bandCount = step;
     if (bandGroups == 0) return RSD_OK;
-    hipLaunchKernelGGL(svao_pass1_kernel, dim3(nx / 16, 2 * bandGroups), dim3(16, 16), 0, (hipStream_t)stream, a);
+    // Residency cap (frames in flight): pass 1 alone fills all 8 wave slots of every SIMD (63 VGPRs),
+    // so the latency-bound SD traces and pass 2 of the other frames find no slot while it runs.
+    // RSD_PASS1_WG_PER_CU=k reserves LDS so that at most k pass-1 workgroups (k waves per SIMD)
+    // share a CU with the other frames' waves (A/B knob; 0 / unset = no cap).
+    static const uint32_t capLds = [] {
+        const char* e = getenv("RSD_PASS1_WG_PER_CU");
+        const int k = e ? atoi(e) : 0;
+        // k workgroups of L bytes fit the 160 KB of a CU and a (k + 1)-th does not, leaving >= 12 KB
+        // for a trace wave's LDS stack: L = floor(148 / k) KB (> 160 / (k + 1) KB for k = 1..7)
+        return k > 0 && k < 8 ? 148u / (uint32_t)k * 1024u : 0u;
+    }();
+    hipLaunchKernelGGL(svao_pass1_kernel, dim3(nx / 16, 2 * bandGroups), dim3(16, 16), capLds, (hipStream_t)stream, a);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? RSD_OK : hip_fail(e, "svao_pass1_kernel launch");
 }
@@ -578,29 +562,13 @@ rsd_status pass2_impl(const rsd_camera* cam, const rsd_vao_data* vao, const rsd_
     a.bandIndex = start;
     a.bandCount = step;
     if (bandGroups == 0) return RSD_OK;
-    const uint32_t tileRows = (32 / kP2Tile) * bandGroups, tilesX = (vw + kP2Tile - 1) / kP2Tile;
-    static const bool tilesGrid = [] {  // RSD_P2_GRID=tiles: one workgroup per tile (A/B runs)
-        const char* e = getenv("RSD_P2_GRID");
-        return e && std::string(e) == "tiles";
-    }();
-    static const int cus = [] {
-        int dev = 0, n = 0;
-        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-            n = 256;
-        return std::max(1, n);
-    }();
-    const bool persist = a.tileFlags && !tilesGrid;
-    // persistent: 6 resident workgroups per CU (26 KB LDS each)
-    const dim3 grid = persist ? dim3(std::min<uint32_t>(tilesX * tileRows, 6u * (uint32_t)cus)) : dim3(tilesX, tileRows);
-    const dim3 block(kP2Lanes);
+    dim3 grid((vw + kP2Tile - 1) / kP2Tile, (32 / kP2Tile) * bandGroups), block(kP2Lanes);
     hipStream_t s = (hipStream_t)stream;
     const uint32_t nd = a.k.nd;
-    // 16 / 32 directions: the pair lists take 8 / 16 KB more LDS (4 workgroups per CU): per-tile grid
-#define RSD_P2(NN)                                                                                            \
-    if (nd == 32u) hipLaunchKernelGGL((svao_pass2_tiles_kernel<NN, 32>), dim3(tilesX, tileRows), block, 0, s, a); \
-    else if (nd == 16u) hipLaunchKernelGGL((svao_pass2_tiles_kernel<NN, 16>), dim3(tilesX, tileRows), block, 0, s, a); \
-    else if (persist) hipLaunchKernelGGL((svao_pass2_persistent_kernel<NN, 8>), grid, block, 0, s, a, tileRows); \
-    else hipLaunchKernelGGL((svao_pass2_tiles_kernel<NN, 8>), grid, block, 0, s, a);
+#define RSD_P2(NN)                                                                                           \
+    if (nd == 32u) hipLaunchKernelGGL((svao_pass2_kernel<NN, 32>), grid, block, 0, s, a);                  \
+    else if (nd == 16u) hipLaunchKernelGGL((svao_pass2_kernel<NN, 16>), grid, block, 0, s, a);             \
+    else hipLaunchKernelGGL((svao_pass2_kernel<NN, 8>), grid, block, 0, s, a);
     switch (N) {
         case 1: RSD_P2(1) break;
         case 2: RSD_P2(2) break;

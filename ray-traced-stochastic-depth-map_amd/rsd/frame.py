@@ -17,6 +17,7 @@ from __future__ import annotations
 
 import ctypes as C
 import dataclasses
+import os
 
 import numpy as np
 
@@ -252,7 +253,10 @@ class Renderer:
         self.ray_minmax = torch.empty((2, self.sd_h, self.sd_w), dtype=torch.int32, device=dv)
         self.ray_min, self.ray_max = self.ray_minmax[0], self.ray_minmax[1]
         # Use16Bit (standalone SD pass): R16F / RG16F / RGBA16F
-        self.sd = torch.empty(((N + 3) // 4, self.sd_h, self.sd_w, min(N, 4)),
+        # the tiled-layout A/B build (RSD_LIB_VARIANT=sdtiled) stores whole 8x8 tiles: pad the rows
+        tiled = os.environ.get("RSD_LIB_VARIANT") == "sdtiled"
+        sh, sw = ((self.sd_h + 7) // 8 * 8, (self.sd_w + 7) // 8 * 8) if tiled else (self.sd_h, self.sd_w)
+        self.sd = torch.empty(((N + 3) // 4, sh, sw, min(N, 4)),
                               dtype=torch.float16 if cfg.use_16bit else torch.float32, device=dv)
         self._bind_tile_flags()
 

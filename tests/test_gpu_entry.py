@@ -91,7 +91,7 @@ def test_entry_grid_cuts_node_visits(device, monkeypatch):
 
 def test_entry_grid_no_interval_and_throughput(device, monkeypatch):
     """Without ray intervals every segment runs to farZ: longer than the scene, the walk starts at
-    the root; the quad walk under RSD_SD_THROUGHPUT gives the same bits as the row walk."""
+    the root; the depth-first quad walk (RSD_SD_THROUGHPUT) gives the same bits as the row walk."""
     from rsd.frame import Renderer
     s, gs = gpu_scene("arcade_tiny", device)
     cfg = small_frame_config(visible=(128, 128), guard=0, divisor=1, N=4, max_count=8)
@@ -101,7 +101,7 @@ def test_entry_grid_no_interval_and_throughput(device, monkeypatch):
     r.gbuffer()
     a, _ = trace(r, monkeypatch, "on", None)
     b, _ = trace(r, monkeypatch, "off", None)
-    c, _ = trace(r, monkeypatch, "on", None, throughput=True)
+    c, _ = trace(r, monkeypatch, "on", "quad", throughput=True)
     assert np.array_equal(a, b) and np.array_equal(a, c)
 
 

@@ -52,9 +52,9 @@ def test_fullsize_config_parity(oracle, config):
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("config,flight", [("suntemple_1080p_q", 2), ("suntemple_1080p_q", 3),
-                                           ("emerald_4k_q", 2)])
-def test_frames_in_flight_equal_sequential(config, flight):
+@pytest.mark.parametrize("config,flight,walk", [("suntemple_1080p_q", 2, None), ("suntemple_1080p_q", 3, "quad"),
+                                                ("suntemple_1080p_q", 4, None), ("emerald_4k_q", 2, None)])
+def test_frames_in_flight_equal_sequential(monkeypatch, config, flight, walk):
     """bench.py's frames in flight: F frame slots on F streams, frames overlapping across slots
     (each slot consuming its own interval maps), give the sequential frame bit-for-bit in every
     slot -- librsd's SD-trace scratch is per (scene, stream), so concurrent traces of one scene
@@ -72,7 +72,9 @@ def test_frames_in_flight_equal_sequential(config, flight):
     for s in slots:
         s.sd.zero_()
         s.ao.zero_()
-    frames = [BandFrame(s, throughput=flight != 2) for s in slots]  # both trace walks
+    if walk:  # the depth-first quad walk (the default is the row walk, with or without RSD_SD_THROUGHPUT)
+        monkeypatch.setenv("RSD_TRACE_WALK", walk)
+    frames = [BandFrame(s, throughput=True) for s in slots]
     streams = [torch.cuda.Stream() for _ in slots]
     for st in streams:
         st.wait_stream(torch.cuda.current_stream())
