@@ -12,7 +12,6 @@
 #include <algorithm>
 #include <cfloat>
 #include <cmath>
-#include <cstdlib>
 #include <mutex>
 #include <vector>
 
@@ -38,7 +37,9 @@ __global__ void clear_intervals_kernel(uint32_t* rmin, uint32_t* rmax, uint32_t 
     }
 }
 
-// One direction of SVAORaster.ps.slang:49-105 for one pixel: the reference loop body
+// One direction of SVAORaster.ps.slang:49-105 for one pixel: the reference loop body.  (Issuing the
+// reads of 2 or 4 directions before their bodies measured 77 / 91 vs 70 us: 77 / 105 VGPRs, 6 / 4 waves
+// per SIMD -- DESIGN.md section 4.)
 __device__ __forceinline__ void pass1_dir_generic(const SvaoArgs& a, float u, float v, uint32_t px, uint32_t py,
                                                   const Basic& b, int i, float& ao, float& aoD, uint32_t& st) {
     const rsd_vao_data& d = a.d;
@@ -468,18 +469,7 @@ rsd_status pass1_impl(const rsd_camera* cam, const rsd_vao_data* vao, const rsd_
     a.bandIndex = start;
     a.bandCount = step;
     if (bandGroups == 0) return RSD_OK;
-    // Residency cap (frames in flight): pass 1 alone fills all 8 wave slots of every SIMD (63 VGPRs),
-    // so the latency-bound SD traces and pass 2 of the other frames find no slot while it runs.
-    // RSD_PASS1_WG_PER_CU=k reserves LDS so that at most k pass-1 workgroups (k waves per SIMD)
-    // share a CU with the other frames' waves (A/B knob; 0 / unset = no cap).
-    static const uint32_t capLds = [] {
-        const char* e = getenv("RSD_PASS1_WG_PER_CU");
-        const int k = e ? atoi(e) : 0;
-        // k workgroups of L bytes fit the 160 KB of a CU and a (k + 1)-th does not, leaving >= 12 KB
-        // for a trace wave's LDS stack: L = floor(148 / k) KB (> 160 / (k + 1) KB for k = 1..7)
-        return k > 0 && k < 8 ? 148u / (uint32_t)k * 1024u : 0u;
-    }();
-    hipLaunchKernelGGL(svao_pass1_kernel, dim3(nx / 16, 2 * bandGroups), dim3(16, 16), capLds, (hipStream_t)stream, a);
+    hipLaunchKernelGGL(svao_pass1_kernel, dim3(nx / 16, 2 * bandGroups), dim3(16, 16), 0, (hipStream_t)stream, a);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? RSD_OK : hip_fail(e, "svao_pass1_kernel launch");
 }
