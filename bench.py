@@ -57,7 +57,7 @@ for p in (str(ROOT), str(PKG)):
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8 TB/s (spec)
 DEFAULT_CONFIG = "suntemple_1080p_q"
 # committed rocprofv3 passes of the default bench (newest round first)
-PROFILE_DIRS = [ROOT / "profiles" / "round2", ROOT / "profiles" / "round1"]
+PROFILE_DIRS = [ROOT / "profiles" / "round3", ROOT / "profiles" / "round2", ROOT / "profiles" / "round1"]
 
 
 def parse():
@@ -84,6 +84,10 @@ def parse():
     ap.add_argument("--pmc-csv", nargs="*", default=None,
                     help="rocprofv3 --pmc counter_collection.csv file(s) with FETCH_SIZE / WRITE_SIZE for "
                          "roofline.traffic (default: the committed passes of the default config)")
+    ap.add_argument("--timing-events", choices=("hip", "torch", "off"), default="hip",
+                    help="per-kernel timing events: hip = fence-free timing events (rsd.timing, default); "
+                         "torch = torch.cuda.Event (a system-scope fence per record); off = none in the "
+                         "throughput region (the latency region still needs them for value)")
     return ap.parse_args()
 
 
@@ -211,8 +215,13 @@ def main():
         return wall
 
     # ---- latency region: one frame in flight, the latency-optimised trace walk
-    mk_ev = lambda n: [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))  # noqa: E731
-                       for _ in range(n)]
+    # per-kernel timing: fence-free HIP events by default -- a torch.cuda.Event record carries a
+    # system-scope release fence that left ~5 us bubbles in the stream it sat in (rsd/timing.py)
+    if args.timing_events == "torch":
+        new_ev = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
+    else:
+        from rsd.timing import TimingEvent as new_ev
+    mk_ev = lambda n: [(new_ev(), new_ev()) for _ in range(n)]  # noqa: E731
     ev_sd, ev_ao = mk_ev(args.steps), mk_ev(args.steps)
 
     def run_seq(n, timed_ev=True):
@@ -235,9 +244,10 @@ def main():
     streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(F - 1)]
     for st in streams[1:]:
         st.wait_stream(streams[0])
-    ev_thr = mk_ev(args.steps)
+    thr_ev = args.timing_events != "off"
+    ev_thr = mk_ev(args.steps) if thr_ev else None
 
-    def run_thr(n, timed_ev=True):
+    def run_thr(n, timed_ev=thr_ev):
         for i in range(n):
             with torch.cuda.stream(streams[i % F]):
                 pose(slots[i % F].b, i)
@@ -245,7 +255,7 @@ def main():
 
     run_thr(args.warmup, timed_ev=False)
     wall_thr = timed(run_thr, args.steps)
-    thr_sd_ms = float(np.mean([a.elapsed_time(b) for a, b in ev_thr]))
+    thr_sd_ms = float(np.mean([a.elapsed_time(b) for a, b in ev_thr])) if thr_ev else float("nan")
 
     if dist:  # per-kernel times: the slowest rank
         t = torch.tensor([seq_sd_ms, seq_ao_ms, thr_sd_ms], device="cuda")
@@ -331,7 +341,8 @@ def main():
         "throughput": {"frames_in_flight": F, "frames": frames_thr, "ms_per_frame": round(wall_thr / args.steps * 1e3, 4),
                        "ao_frames_per_s": round(frames_thr / wall_thr, 2),
                        "frame_mrays_per_s": round(rays * frames_thr / wall_thr / 1e6, 2),
-                       "sd_kernel_ms_overlapped": round(thr_sd_ms, 4),
+                       "sd_kernel_ms_overlapped": round(thr_sd_ms, 4) if thr_ev else None,
+                       "timing_events": args.timing_events,
                        "walk": abi.WALK_NAMES[walk_thr]},
         "traversal": {"nodes_per_ray": round(nodes_seq / rays / units, 3),
                       "tris_per_ray": round(tris_seq / rays / units, 3),

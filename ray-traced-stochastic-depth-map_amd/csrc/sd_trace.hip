@@ -44,26 +44,6 @@ constexpr int kQctlWords = 3 * (int)kQueueParts + 32;
 constexpr int kQctlLiveTiles = 2 * (int)kQueueParts;
 constexpr int kQctlShort = 2 * (int)kQueueParts + 32;  // lpt: short-ray counts (filled from the partition's end)
 constexpr int kSetupWaves = 4;  // sd_setup_kernel: tiles (waves) per workgroup
-constexpr int kQctlExit = 2 * (int)kQueueParts + 1;  // persistent waves that finished the trace's last kernel
-
-// End of a trace's LAST kernel (every persistent wave, converged): the wave that finishes last
-// zeroes the queue-control words of this trace, so the buffer is clean for the next trace on the
-// stream (the setup kernel's zeroing of the other buffer stays; a captured graph replays one
-// buffer and relies on this).  A wave's reads of qctl (counts, heads) all complete before its
-// increment: their values steer its loop.
-__device__ __forceinline__ void qctl_release(uint32_t* qctl) {
-    uint32_t last = 0u;
-    if (threadIdx.x == 0) {
-        __threadfence();
-        last = atomicAdd(&qctl[kQctlExit], 1u) == gridDim.x * gridDim.y - 1u ? 1u : 0u;
-    }
-    last = __shfl(last, 0);
-    if (last) {
-        __threadfence();
-        for (int w = (int)threadIdx.x; w < kQctlWords; w += (int)blockDim.x) qctl[w] = 0u;
-    }
-}
-
 struct SDArgs {
     const float4* nodes;  // BVH base (wide nodes, then triangle records)
     const float4* tris;   // = nodes + triOff
@@ -751,7 +731,6 @@ __global__ void __launch_bounds__(kBlock) sd_trace_queue_kernel(SDArgs a, const 
         atomicMax(&a.counters[8], maxCycles);
         atomicAdd(&a.counters[9], (unsigned long long)(q == 0 ? st.leaves : 0u));
     }
-    qctl_release(qctl);
 }
 
 // ------------------------------------------------------------------------------------
@@ -903,7 +882,6 @@ __global__ void __launch_bounds__(kBlock) sd_trace_ordered_kernel(SDArgs a, cons
         atomicMax(&a.counters[6], (unsigned long long)maxSteps);
         atomicAdd(&a.counters[9], (unsigned long long)(q == 0 ? st.leaves : 0u));
     }
-    qctl_release(qctl);
 }
 
 // ------------------------------------------------------------------------------------
@@ -1560,7 +1538,6 @@ __global__ void __launch_bounds__(kBlock) sd_trace_row_kernel(SDArgs a, const fl
         atomicAdd(&a.counters[17], tComp);
         atomicAdd(&a.counters[18], tPool);
     }
-    if constexpr (!SPLIT) qctl_release(qctl);  // the split walk releases in its resolve kernel
 }
 
 // Phase 3 of the split trace: anyHit -> algorithm over the K nearest keys of every live ray
@@ -1616,7 +1593,6 @@ __global__ void __launch_bounds__(kBlock) sd_resolve_row_kernel(SDArgs a, const 
         }
     }
     if (a.counters && l == 0 && delivered) atomicAdd(&a.counters[4], (unsigned long long)delivered);
-    qctl_release(qctl);  // the last kernel of the split / raster walk
 }
 
 // ------------------------------------------------------------------------------------

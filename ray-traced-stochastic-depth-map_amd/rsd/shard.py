@@ -309,8 +309,12 @@ class HaloFrame:
 
     # ---- timing of this rank's compute (load balance)
     def _mark(self):
-        if self.cuda:
-            e = torch.cuda.Event(enable_timing=True)
+        """A timestamp for the re-balancing cost (None when nothing re-balances: world 1)."""
+        if not self.rebalance:
+            return None
+        if self.cuda:  # fence-free timing event (rsd/timing.py): no stream bubble per mark
+            from .timing import TimingEvent
+            e = TimingEvent()
             e.record()
             return e
         return time.perf_counter()
@@ -416,7 +420,7 @@ class HaloFrame:
         t4 = self._mark()
         b.pass2_rows(self.px_rows[me])
         t5 = self._mark()
-        self._prev = [(t0, t1), (t2, t3), (t4, t5)]
+        self._prev = [(t0, t1), (t2, t3), (t4, t5)] if self.rebalance else None
         if world > 1:
             lo, hi = self.ao_rows[me]
             send, recv = self.ao_send, self.ao_recv

@@ -13,6 +13,7 @@ import torch  # noqa: E402
 
 from rsd.frame import CONFIGS, FrameConfig, Renderer  # noqa: E402
 from rsd.scenes import make_scene  # noqa: E402
+from rsd.timing import TimingEvent  # noqa: E402
 
 name = next((a for a in sys.argv[1:] if not a.startswith("--")), "suntemple_1080p_q")
 frames = int(sys.argv[sys.argv.index("--frames") + 1]) if "--frames" in sys.argv else 200
@@ -22,7 +23,7 @@ r.gbuffer()
 for _ in range(5):
     r.frame()
 torch.cuda.synchronize()
-ev = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(frames)]
+ev = [[TimingEvent() for _ in range(4)] for _ in range(frames)]  # fence-free (rsd/timing.py)
 for e in ev:
     r.clear_intervals()
     e[0].record()
