@@ -206,7 +206,7 @@ struct P2Shared {
     float p[kP2Lanes], r[kP2Lanes];
     // the pixel's BasicAOData, evaluated once per pixel, not per pair: the 16 floats pass 2 reads
     // (posVLength, normalV, radiusInPixels stay out)
-    float basic[kP2Lanes][16];
+    alignas(16) float basic[kP2Lanes][16];
     uint32_t nPix, nPair;
 };
 

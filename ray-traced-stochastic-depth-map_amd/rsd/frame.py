@@ -267,7 +267,8 @@ class Renderer:
         n = abi.lib().rsd_svao_tile_count(cfg.fb_w, cfg.fb_h, cfg.guard_band)
         self.tile_flags = self.torch.zeros(max(1, n), dtype=self.torch.uint8, device=self.depth.device)
         svp = abi.SVAOParams.from_buffer_copy(self.svp)
-        svp.tile_flags = self.tile_flags.data_ptr()
+        # RSD_TILE_FLAGS=off: no flags (pass 2 visits every tile) -- A/B runs only
+        svp.tile_flags = None if os.environ.get("RSD_TILE_FLAGS") == "off" else self.tile_flags.data_ptr()
         self.svp = svp
 
     def frame_slot(self, own_gbuffer: bool = False) -> "Renderer":
