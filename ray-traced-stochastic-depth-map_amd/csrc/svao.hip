@@ -12,12 +12,18 @@
 #include <algorithm>
 #include <cfloat>
 #include <cmath>
+#include <cstdlib>
+#include <cstring>
 #include <mutex>
 #include <vector>
 
 #include "rsd_device.h"
 #include "rsd_internal.h"
 #include "svao_math.h"
+
+#ifndef RSD_P1_UNROLL
+#define RSD_P1_UNROLL 1
+#endif
 
 namespace rsd {
 
@@ -39,16 +45,19 @@ __global__ void clear_intervals_kernel(uint32_t* rmin, uint32_t* rmax, uint32_t 
 
 // One direction of SVAORaster.ps.slang:49-105 for one pixel: the reference loop body.  (Issuing the
 // reads of 2 or 4 directions before their bodies measured 77 / 91 vs 70 us: 77 / 105 VGPRs, 6 / 4 waves
-// per SIMD -- DESIGN.md section 4.)
+// per SIMD -- DESIGN.md section 4.)  SPEC: the specialised kernel of the StochasticDepth frame with ray
+// intervals, an SD guard band, pixel-index isSamePixel and a frame of at most 4096 x 4096 (every
+// BASELINE config) -- the run-time tests of those settings are compile-time constants there.
+template <bool SPEC, bool ALLFAST = false>
 __device__ __forceinline__ void pass1_dir_generic(const SvaoArgs& a, float u, float v, uint32_t px, uint32_t py,
                                                   const Basic& b, int i, float& ao, float& aoD, uint32_t& st) {
     const rsd_vao_data& d = a.d;
     Sample s;
     bool ssrAbove;
-    if (!sample_init(a, u, v, b, i, s, ssrAbove)) return;
-    const bool same = a.k.samePixelInt ? (s.kx == (int)px && s.ky == (int)py)
-                                       : (fabsf(u - s.ru) < d.invResolution[0] * 0.9f &&
-                                          fabsf(v - s.rv) < d.invResolution[1] * 0.9f);
+    if (!sample_init<ALLFAST>(a, u, v, b, i, s, ssrAbove)) return;
+    const bool same = (SPEC || a.k.samePixelInt) ? (s.kx == (int)px && s.ky == (int)py)
+                                                 : (fabsf(u - s.ru) < d.invResolution[0] * 0.9f &&
+                                                    fabsf(v - s.rv) < d.invResolution[1] * 0.9f);
     if (same) {
         const float w = div_pdf(s.sphereStart - s.sphereEnd, s);  // isSamePixel
         ao += w;
@@ -56,10 +65,10 @@ __device__ __forceinline__ void pass1_dir_generic(const SvaoArgs& a, float u, fl
         return;
     }
     // SVAORaster.ps.slang:62-66: Raytraced mode with TRACE_OUT_OF_SCREEN (SVAO.h:104)
-    bool forceRay = a.secondary == 3u && !s.isInScreen;
-    eval_primary(a, b, s);
+    bool forceRay = !SPEC && a.secondary == 3u && !s.isInScreen;
+    eval_primary<SPEC>(a, b, s);
     ao += s.visibility;
-    if (!s.isInScreen && d.sdGuard > 0) {
+    if (!s.isInScreen && (SPEC || d.sdGuard > 0)) {
         forceRay = true;
         s.objectSpaceZ = 3.402823466e+38f;
     }
@@ -67,11 +76,11 @@ __device__ __forceinline__ void pass1_dir_generic(const SvaoArgs& a, float u, fl
     const bool req = s.objectSpaceZ > s.sphereStart + constRadius && ssrAbove;
     if (req || forceRay) {
         st |= 1u << i;
-        if (a.secondary == 2u) {
+        if (SPEC || a.secondary == 2u) {
             const int sx = uv_to_sd(s.su, d.lowResolution[0], d.sdGuard);
             const int sy = uv_to_sd(s.sv, d.lowResolution[1], d.sdGuard);
             const size_t o = (size_t)sy * a.sdW + sx;
-            if (a.rayInterval) {
+            if (SPEC || a.rayInterval) {
                 const float osMin = hmin(s.objectSpaceZ, b.radius + d.thickness * b.radius + s.sphereStart);
                 atomicMin(&a.rayMin[o], asuint(hmax(b.posVLength - osMin, 0.0f)));
                 atomicMax(&a.rayMax[o], asuint(hmax(b.posVLength - s.sphereEnd, 0.0f)));
@@ -87,6 +96,8 @@ __device__ __forceinline__ void pass1_dir_generic(const SvaoArgs& a, float u, fl
 // SVAORaster.ps.slang:29-122, [numthreads(16,16,1)] with the 2x2 group interleave.  (A branch-free
 // "lean" direction body -- host constants in SGPRs, predicated updates, one float ratio compare --
 // measured 74 vs 70 us at configs[1]: more VALU per direction and 64-73 VGPRs)
+// ND > 0: NUM_DIRECTIONS known at compile time (the specialised kernel); 0: a.k.nd
+template <bool SPEC, int ND>
 __global__ void __launch_bounds__(256) svao_pass1_kernel(SvaoArgs a) {
     const uint32_t bx = blockIdx.x, by = blockIdx.y;
     const uint32_t ox = (bx / 2u) * 32u + 2u * threadIdx.x + (bx % 2u);
@@ -98,16 +109,28 @@ __global__ void __launch_bounds__(256) svao_pass1_kernel(SvaoArgs a) {
     float ao = 0.0f, aoD = 0.0f;  // bright, dark (DUAL_AO: SVAORaster.ps.slang:13 ao_t = float2)
     uint32_t st = 0;
     Basic b;
-    if (!basic_init(a, u, v, b)) {
+    if (!basic_init<SPEC>(a, u, v, b)) {
         ao = aoD = 1.0f;
     } else {
-#pragma unroll 1
-        for (int i = 0; i < (int)a.k.nd; ++i) pass1_dir_generic(a, u, v, px, py, b, i, ao, aoD, st);
+        const int nd = ND > 0 ? ND : (int)a.k.nd;
+        // every lane of the wave at the unclamped AO radius (all but the pixels nearest the camera):
+        // the host terms and div_rcp for all, no per-lane choice of path (the specialised kernel runs
+        // only when every direction's fastDiv bit is set), and the per-direction zi division by the
+        // pixel's make_nonzero(normalO.z) through its refined reciprocal (div_unscaled)
+        const float nzd = make_nonzero(b.normalO.z, 0.0001f);
+        if (SPEC && __ballot(b.radius != d.radius || !div_unscaled_den_ok(nzd)) == 0u) {
+            b.nzRcp = rcp_refined(nzd);
+#pragma unroll RSD_P1_UNROLL
+            for (int i = 0; i < nd; ++i) pass1_dir_generic<SPEC, true>(a, u, v, px, py, b, i, ao, aoD, st);
+        } else {
+#pragma unroll RSD_P1_UNROLL
+            for (int i = 0; i < nd; ++i) pass1_dir_generic<SPEC>(a, u, v, px, py, b, i, ao, aoD, st);
+        }
         ao *= a.k.invNd;  // SVAORaster.ps.slang:108-109
         ao *= 2.0f;
         aoD *= a.k.invNd;
         aoD *= 2.0f;
-        if (a.secondary == 0u || st == 0u) {
+        if ((!SPEC && a.secondary == 0u) || st == 0u) {
             ao = acc_pow(ao, d.exponent);
             aoD = acc_pow(aoD, d.exponent);
         }
@@ -469,7 +492,18 @@ rsd_status pass1_impl(const rsd_camera* cam, const rsd_vao_data* vao, const rsd_
     a.bandIndex = start;
     a.bandCount = step;
     if (bandGroups == 0) return RSD_OK;
-    hipLaunchKernelGGL(svao_pass1_kernel, dim3(nx / 16, 2 * bandGroups), dim3(16, 16), 0, (hipStream_t)stream, a);
+    // the specialised kernel for the StochasticDepth frame (every BASELINE config); RSD_PASS1=generic
+    // forces the generic one (A/B runs)
+    const char* p1Env = std::getenv("RSD_PASS1");
+    const uint32_t allDirs = a.k.nd == 32u ? 0xffffffffu : (1u << a.k.nd) - 1u;
+    const bool spec = !(p1Env && std::strcmp(p1Env, "generic") == 0) && a.secondary == 2u && a.rayInterval &&
+                      a.k.samePixelInt && a.d.sdGuard > 0 && W <= 4096u && H <= 4096u &&
+                      (a.k.fastDiv & allDirs) == allDirs;
+    const dim3 grid(nx / 16, 2 * bandGroups), block(16, 16);
+    hipStream_t s = (hipStream_t)stream;
+    if (spec && a.k.nd == 8u) hipLaunchKernelGGL((svao_pass1_kernel<true, 8>), grid, block, 0, s, a);
+    else if (spec) hipLaunchKernelGGL((svao_pass1_kernel<true, 0>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((svao_pass1_kernel<false, 0>), grid, block, 0, s, a);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? RSD_OK : hip_fail(e, "svao_pass1_kernel launch");
 }

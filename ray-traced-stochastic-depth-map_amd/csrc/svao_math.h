@@ -65,6 +65,7 @@ struct Basic {
     float posVLength;
     f3 normal, tangent, bitangent, normalO, normalV;
     float radiusInPixels, radius;
+    float nzRcp;  // rcp_refined(make_nonzero(normalO.z, 1e-4)): set by the all-fast pass-1 loop only
 };
 
 struct Sample {
@@ -92,6 +93,34 @@ __device__ __forceinline__ float div_rcp(float a, float b, float y) {
     const float q1 = __builtin_fmaf(r0, y, q0);
     const float r1 = __builtin_fmaf(-q1, b, a);
     return __builtin_fmaf(r1, y, q1);
+}
+
+// The gfx950 IEEE binary32 division a / b is: v_div_scale of a and of b, v_rcp of the scaled b, two FMAs
+// refining it (y1), q0 = a y1, two residual steps and v_div_fmas, then v_div_fixup.  Where neither the
+// scaling nor the fixup acts -- b normal, |b| in [2^-20, 2^20], and a = 0 or |a| in [2^-100, 2^70]
+// (exponent difference < 96, a / b and 1 / b normal, |a| >= 2^-103; finite normal operands) -- the
+// quotient is that sequence's own value without them: div_unscaled(a, b, rcp_refined(b)), with the
+// sign of q0 (the fixup's sign(a) ^ sign(b), which the residual steps lose for a = -0).  Same
+// operations, same bits as a / b; a per-pixel divisor pays v_rcp and its refinement once.
+__device__ __forceinline__ float rcp_refined(float b) {
+    const float y0 = __builtin_amdgcn_rcpf(b);
+    return __builtin_fmaf(__builtin_fmaf(-b, y0, 1.0f), y0, y0);
+}
+__device__ __forceinline__ float div_unscaled(float a, float b, float y1) {
+    const float q0 = a * y1;
+    const float r0 = __builtin_fmaf(-q0, b, a);
+    const float q1 = __builtin_fmaf(r0, y1, q0);
+    const float r1 = __builtin_fmaf(-q1, b, a);
+    return __builtin_copysignf(__builtin_fmaf(r1, y1, q1), q0);
+}
+// the numerator range of div_unscaled (false for NaN / inf)
+__device__ __forceinline__ bool div_unscaled_num_ok(float a) {
+    const float m = fabsf(a);
+    return (m >= 0x1p-100f && m < 0x1p70f) || a == 0.0f;
+}
+__device__ __forceinline__ bool div_unscaled_den_ok(float b) {
+    const float m = fabsf(b);
+    return m >= 0x1p-20f && m <= 0x1p20f;
 }
 
 // n / pdf for n = 0 or n in (0, 2 * sphereHeight]: max(ss - max(se, oz), 0) (>= ulp(ss) / 2 when
@@ -127,8 +156,10 @@ __device__ __forceinline__ float depth_sample(const SvaoArgs& a, float u, float 
 // (kx + 0.5) +- size * 2^-22, and an offset below 1/512 rounds the 8-bit weights to 0 (or to
 // 256 of the next texel, tex_bilinear's carry), so for frames up to 4096 px the fetch is
 // direct -- no dependency on the uv arithmetic or the snap-table loads.
+// SMALL: the caller guarantees W, H <= 4096 (a specialised kernel: no run-time size test)
+template <bool SMALL = false>
 __device__ __forceinline__ float depth_center(const SvaoArgs& a, float u, float v, int kx, int ky) {
-    if (a.W <= 4096 && a.H <= 4096)
+    if (SMALL || (a.W <= 4096 && a.H <= 4096))
         return a.depth[(size_t)min(max(ky, 0), a.H - 1) * a.W + min(max(kx, 0), a.W - 1)];
     return depth_sample(a, u, v);
 }
@@ -173,9 +204,10 @@ __device__ __forceinline__ void stencil_store(const SvaoArgs& a, size_t o, uint3
 }
 
 // Common.slang:285-324
+template <bool SMALL = false>
 __device__ __forceinline__ bool basic_init(const SvaoArgs& a, float u, float v, Basic& b) {
     const rsd_vao_data& d = a.d;
-    const float z = depth_center(a, u, v, (int)(u * d.resolution[0]), (int)(v * d.resolution[1]));
+    const float z = depth_center<SMALL>(a, u, v, (int)(u * d.resolution[0]), (int)(v * d.resolution[1]));
     const float rux = (d.radius * a.cam.focalLength) / (a.cam.frameWidth * z);
     const float ruy = (d.radius * a.cam.focalLength) / (a.cam.frameHeight * z);
     const float pa = rux * d.resolution[0], pb = ruy * d.resolution[1];
@@ -219,13 +251,24 @@ __device__ __forceinline__ bool ratio_le_tenth(float n, float D) {
     return (double)n < M * (double)D;
 }
 
-// ssrAbove = (screenSpaceRadius > ssRadiusCutoff), decided on the squared radius (no sqrt)
+// ssrAbove = (screenSpaceRadius > ssRadiusCutoff), decided on the squared radius (no sqrt).
+// ALLFAST: the caller guarantees b.radius == VAOData.radius and every fastDiv bit (the host terms
+// and div_rcp apply; a wave-uniform case of the specialised pass 1)
+template <bool ALLFAST = false>
 __device__ __forceinline__ bool sample_init(const SvaoArgs& a, float u, float v, const Basic& b, int i, Sample& s,
                                             bool& ssrAbove) {
     const rsd_vao_data& d = a.d;
     float radius, dx, dy, sphereHeight;
     s.fast = false;
-    if (b.radius == d.radius) {  // the host-evaluated terms (same operations, same bits)
+    if (ALLFAST) {
+        radius = a.k.dirRadius[i];
+        dx = a.k.dirDx[i];
+        dy = a.k.dirDy[i];
+        sphereHeight = a.k.dirHeight[i];
+        s.fast = true;
+        s.yPdf = a.k.rcpPdf[i];
+        s.yHeight = a.k.rcpHeight[i];
+    } else if (b.radius == d.radius) {  // the host-evaluated terms (same operations, same bits)
         radius = a.k.dirRadius[i];
         dx = a.k.dirDx[i];
         dy = a.k.dirDy[i];
@@ -241,7 +284,13 @@ __device__ __forceinline__ bool sample_init(const SvaoArgs& a, float u, float v,
     }
     s.pdf = 2.0f * sphereHeight;
     s.sphereStart = sphereHeight;
-    const float zi = -(dx * b.normalO.x + dy * b.normalO.y) / make_nonzero(b.normalO.z, 0.0001f);
+    float zi;
+    if (ALLFAST) {  // the pixel's divisor is in div_unscaled's range (checked with ALLFAST)
+        const float num = -(dx * b.normalO.x + dy * b.normalO.y), den = make_nonzero(b.normalO.z, 0.0001f);
+        zi = __ballot(!div_unscaled_num_ok(num)) == 0u ? div_unscaled(num, den, b.nzRcp) : num / den;
+    } else {
+        zi = -(dx * b.normalO.x + dy * b.normalO.y) / make_nonzero(b.normalO.z, 0.0001f);
+    }
     s.sphereEnd = hmin(hmax(zi, -sphereHeight), sphereHeight);
     if (ratio_le_tenth(s.sphereStart - s.sphereEnd, 2.0f * sphereHeight)) return false;
     const f3 ip = b.posV + b.tangent * dx + b.bitangent * dy;
@@ -295,8 +344,9 @@ __device__ __forceinline__ void add_sample(const SvaoArgs& a, const Basic& b, Sa
 }
 
 // Common.slang:492-496
+template <bool SMALL = false>
 __device__ __forceinline__ void eval_primary(const SvaoArgs& a, const Basic& b, Sample& s) {
-    const float z = depth_center(a, s.ru, s.rv, s.kx, s.ky);
+    const float z = depth_center<SMALL>(a, s.ru, s.rv, s.kx, s.ky);
     add_sample(a, b, s, uv_to_view(a, s.ru, s.rv, z), true);
 }
 
