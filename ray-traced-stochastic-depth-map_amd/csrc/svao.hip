@@ -151,23 +151,29 @@ __global__ void __launch_bounds__(256) svao_pass1_kernel(SvaoArgs a) {
 
 // SVAORaster2.ps.slang:48-65 -> calcAO2 (Common.slang:523-597), stochastic-depth branch: one
 // refined direction i of a pixel -> its primary visibility p (subtracted) and refined r (added)
-template <int N>
+// SPEC / ALLFAST as in pass 1 (the specialised kernel: frame <= 4096 x 4096, every fastDiv bit, SD map
+// width / height in [1, 2^20]; ALLFAST: every lane's pixel at the unclamped radius with b.nzRcp set).
+// (ylx, yly) = rcp_refined of the SD resolution: the texel-centre uv divisions (cx - guard + jx) / low
+// go through div_unscaled -- the numerator is never 0 and >= 0.0037 in magnitude (the jitter table
+// lies in (0.0037, 0.9963), or 0.5 without jitter), so its preconditions hold.
+template <int N, bool SPEC = false, bool ALLFAST = false>
 __device__ __forceinline__ void svao_pass2_dir(const SvaoArgs& a, const Basic& b, float u, float v, int i, float& p,
-                                               float& r) {
+                                               float& r, float ylx = 0.0f, float yly = 0.0f) {
     const rsd_vao_data& d = a.d;
     const float depthRange = a.cam.farZ - a.cam.nearZ, depthOffset = a.cam.nearZ;
     const size_t plane = sd_plane_texels(a.sdW, a.sdH);
     Sample s;
     bool ssrAbove;
-    sample_init(a, u, v, b, i, s, ssrAbove);
-    eval_primary(a, b, s);
+    sample_init<ALLFAST>(a, u, v, b, i, s, ssrAbove);
+    eval_primary<SPEC>(a, b, s);
     p = s.visibility;
     const int cx = uv_to_sd(s.su, d.lowResolution[0], d.sdGuard);
     const int cy = uv_to_sd(s.sv, d.lowResolution[1], d.sdGuard);
     float jx, jy;
     sd_jitter((uint32_t)cx, (uint32_t)cy, a.sdJitter != 0u, jx, jy);
-    const float su = ((float)(cx - d.sdGuard) + jx) / d.lowResolution[0];
-    const float sv = ((float)(cy - d.sdGuard) + jy) / d.lowResolution[1];
+    const float nu = (float)(cx - d.sdGuard) + jx, nv = (float)(cy - d.sdGuard) + jy;
+    const float su = SPEC ? div_unscaled(nu, d.lowResolution[0], ylx) : nu / d.lowResolution[0];
+    const float sv = SPEC ? div_unscaled(nv, d.lowResolution[1], yly) : nv / d.lowResolution[1];
     const size_t so = sd_texel(cx, cy, a.sdW);
     float dep[N];
     if constexpr (N == 1) {
@@ -234,7 +240,7 @@ struct P2Shared {
 };
 
 // One kP2Tile^2 tile whose top-left pixel is (x0, y0); flag: its busy-tile flag (cleared) or null
-template <int N, int ND>
+template <int N, int ND, bool SPEC>
 __device__ __forceinline__ void pass2_tile(const SvaoArgs& a, uint32_t x0, uint32_t y0, uint8_t* flag,
                                            P2Shared<ND>& sh) {
     constexpr uint32_t T = kP2Tile, L = kP2Lanes;
@@ -293,7 +299,18 @@ __device__ __forceinline__ void pass2_tile(const SvaoArgs& a, uint32_t x0, uint3
             b.normalV = b.normal;
             b.radiusInPixels = 0.0f;
             float p, r;
-            svao_pass2_dir<N>(a, b, u, v, (int)(e & 31u), p, r);
+            if constexpr (SPEC) {
+                const float nzd = make_nonzero(b.normalO.z, 0.0001f);
+                const float ylx = rcp_refined(d.lowResolution[0]), yly = rcp_refined(d.lowResolution[1]);
+                if (__ballot(b.radius != d.radius || !div_unscaled_den_ok(nzd)) == 0u) {
+                    b.nzRcp = rcp_refined(nzd);
+                    svao_pass2_dir<N, true, true>(a, b, u, v, (int)(e & 31u), p, r, ylx, yly);
+                } else {
+                    svao_pass2_dir<N, true, false>(a, b, u, v, (int)(e & 31u), p, r, ylx, yly);
+                }
+            } else {
+                svao_pass2_dir<N>(a, b, u, v, (int)(e & 31u), p, r);
+            }
             sh.p[tid] = p;
             sh.r[tid] = r;
         }
@@ -321,7 +338,7 @@ __device__ __forceinline__ void pass2_tile(const SvaoArgs& a, uint32_t x0, uint3
 // returns before any barrier.  (A persistent grid of 6 workgroups per CU striding over the flagged
 // tiles measured 48-51 vs 36-38 us at configs[1]: the busy tiles cluster, so some workgroups
 // serialise several dependent tile chains -- tools/pass2_probe.py)
-template <int N, int ND>
+template <int N, int ND, bool SPEC = false>
 __global__ void __launch_bounds__(kP2Lanes) svao_pass2_kernel(SvaoArgs a) {
     constexpr uint32_t kPerGroup = 32u / kP2Tile;  // tile rows per 32-row band group
     __shared__ P2Shared<ND> sh;
@@ -329,7 +346,7 @@ __global__ void __launch_bounds__(kP2Lanes) svao_pass2_kernel(SvaoArgs a) {
                         a.guard;
     uint8_t* flag = a.tileFlags ? a.tileFlags + ((y0 - a.guard) / kP2Tile) * a.tilesX + blockIdx.x : nullptr;
     if (flag && *flag == 0u) return;  // uniform over the workgroup
-    pass2_tile<N, ND>(a, blockIdx.x * kP2Tile + a.guard, y0, flag, sh);
+    pass2_tile<N, ND, SPEC>(a, blockIdx.x * kP2Tile + a.guard, y0, flag, sh);
 }
 
 }  // namespace rsd
@@ -589,9 +606,15 @@ rsd_status pass2_impl(const rsd_camera* cam, const rsd_vao_data* vao, const rsd_
     dim3 grid((vw + kP2Tile - 1) / kP2Tile, (32 / kP2Tile) * bandGroups), block(kP2Lanes);
     hipStream_t s = (hipStream_t)stream;
     const uint32_t nd = a.k.nd;
+    // the specialised kernel (8 directions; RSD_PASS2=generic forces the generic one for A/B runs)
+    const char* p2Env = std::getenv("RSD_PASS2");
+    const bool spec = !(p2Env && std::strcmp(p2Env, "generic") == 0) && nd == 8u && W <= 4096u && H <= 4096u &&
+                      (a.k.fastDiv & 0xffu) == 0xffu && a.d.lowResolution[0] >= 1.0f &&
+                      a.d.lowResolution[0] <= 0x1p20f && a.d.lowResolution[1] >= 1.0f && a.d.lowResolution[1] <= 0x1p20f;
 #define RSD_P2(NN)                                                                                           \
     if (nd == 32u) hipLaunchKernelGGL((svao_pass2_kernel<NN, 32>), grid, block, 0, s, a);                  \
     else if (nd == 16u) hipLaunchKernelGGL((svao_pass2_kernel<NN, 16>), grid, block, 0, s, a);             \
+    else if (spec) hipLaunchKernelGGL((svao_pass2_kernel<NN, 8, true>), grid, block, 0, s, a);             \
     else hipLaunchKernelGGL((svao_pass2_kernel<NN, 8>), grid, block, 0, s, a);
     switch (N) {
         case 1: RSD_P2(1) break;
