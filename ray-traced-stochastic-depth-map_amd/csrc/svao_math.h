@@ -26,6 +26,9 @@ struct SvaoConsts {
     // RN(1 / pdf_i) and RN(1 / sphereHeight_i) of those terms (div_rcp); bit i of fastDiv set when
     // both divisors of direction i lie in [2^-30, 2^30]
     float rcpPdf[kMaxDirections], rcpHeight[kMaxDirections];
+    // ratioMin[i]: the least float >= M * 2 dirHeight[i] (ratio_le_tenth's exact bound): at the
+    // unclamped radius a direction is valid iff sphereStart - sphereEnd >= ratioMin[i]
+    float ratioMin[kMaxDirections];
     uint32_t fastDiv;
     uint32_t samePixelInt;  // isSamePixel decided on pixel indices (fill_consts)
     uint32_t nd;            // NUM_DIRECTIONS
@@ -284,7 +287,7 @@ __device__ __forceinline__ bool sample_init(const SvaoArgs& a, float u, float v,
     }
     s.pdf = 2.0f * sphereHeight;
     s.sphereStart = sphereHeight;
-    float zi;
+    float zi;  // ALLFAST: the validity test below is one compare against the host bound ratioMin
     if (ALLFAST) {  // the pixel's divisor is in div_unscaled's range (checked with ALLFAST)
         const float num = -(dx * b.normalO.x + dy * b.normalO.y), den = make_nonzero(b.normalO.z, 0.0001f);
         zi = __ballot(!div_unscaled_num_ok(num)) == 0u ? div_unscaled(num, den, b.nzRcp) : num / den;
@@ -292,7 +295,10 @@ __device__ __forceinline__ bool sample_init(const SvaoArgs& a, float u, float v,
         zi = -(dx * b.normalO.x + dy * b.normalO.y) / make_nonzero(b.normalO.z, 0.0001f);
     }
     s.sphereEnd = hmin(hmax(zi, -sphereHeight), sphereHeight);
-    if (ratio_le_tenth(s.sphereStart - s.sphereEnd, 2.0f * sphereHeight)) return false;
+    // (sphereStart - sphereEnd is never NaN: hmax maps a NaN zi to -sphereHeight)
+    if (ALLFAST ? !(s.sphereStart - s.sphereEnd >= a.k.ratioMin[i])
+                : ratio_le_tenth(s.sphereStart - s.sphereEnd, 2.0f * sphereHeight))
+        return false;
     const f3 ip = b.posV + b.tangent * dx + b.bitangent * dy;
     s.ip = ip;
     view_to_uv(a, ip, s.su, s.sv);
@@ -426,6 +432,12 @@ inline void fill_consts(SvaoConsts& k, const rsd_vao_data& d, uint32_t nd) {
         k.rcpHeight[i] = (float)(1.0 / (double)h);
         const bool ok = h >= 0x1p-30f && pdf <= 0x1p30f;
         if (ok) k.fastDiv |= 1u << i;
+        // ratio_le_tenth(n, D) is n < M D in exact arithmetic (M D exact in double): valid iff
+        // n >= M D iff n >= the least float >= M D
+        const double bound = ((double)0.1f + 0x1p-28) * (double)pdf;
+        float t = (float)bound;
+        if ((double)t < bound) t = std::nextafter(t, INFINITY);
+        k.ratioMin[i] = t;
     }
 }
 
