@@ -50,11 +50,12 @@ __global__ void clear_intervals_kernel(uint32_t* rmin, uint32_t* rmax, uint32_t 
 // BASELINE config) -- the run-time tests of those settings are compile-time constants there.
 template <bool SPEC, bool ALLFAST = false>
 __device__ __forceinline__ void pass1_dir_generic(const SvaoArgs& a, float u, float v, uint32_t px, uint32_t py,
-                                                  const Basic& b, int i, float& ao, float& aoD, uint32_t& st) {
+                                                  const Basic& b, int i, float& ao, float& aoD, uint32_t& st,
+                                                  const P1Bufs* bf = nullptr) {
     const rsd_vao_data& d = a.d;
     Sample s;
     bool ssrAbove;
-    if (!sample_init<ALLFAST>(a, u, v, b, i, s, ssrAbove)) return;
+    if (!sample_init<ALLFAST>(a, u, v, b, i, s, ssrAbove, bf)) return;
     const bool same = (SPEC || a.k.samePixelInt) ? (s.kx == (int)px && s.ky == (int)py)
                                                  : (fabsf(u - s.ru) < d.invResolution[0] * 0.9f &&
                                                     fabsf(v - s.rv) < d.invResolution[1] * 0.9f);
@@ -66,7 +67,7 @@ __device__ __forceinline__ void pass1_dir_generic(const SvaoArgs& a, float u, fl
     }
     // SVAORaster.ps.slang:62-66: Raytraced mode with TRACE_OUT_OF_SCREEN (SVAO.h:104)
     bool forceRay = !SPEC && a.secondary == 3u && !s.isInScreen;
-    eval_primary<SPEC>(a, b, s);
+    eval_primary<SPEC>(a, b, s, bf);
     ao += s.visibility;
     if (!s.isInScreen && (SPEC || d.sdGuard > 0)) {
         forceRay = true;
@@ -109,6 +110,7 @@ __global__ void __launch_bounds__(256) svao_pass1_kernel(SvaoArgs a) {
     float ao = 0.0f, aoD = 0.0f;  // bright, dark (DUAL_AO: SVAORaster.ps.slang:13 ao_t = float2)
     uint32_t st = 0;
     Basic b;
+    const P1Bufs bf = p1_bufs(a);  // uniform: built before any divergent branch
     if (!basic_init<SPEC>(a, u, v, b)) {
         ao = aoD = 1.0f;
     } else {
@@ -118,10 +120,11 @@ __global__ void __launch_bounds__(256) svao_pass1_kernel(SvaoArgs a) {
         // only when every direction's fastDiv bit is set), and the per-direction zi division by the
         // pixel's make_nonzero(normalO.z) through its refined reciprocal (div_unscaled)
         const float nzd = make_nonzero(b.normalO.z, 0.0001f);
-        if (SPEC && __ballot(b.radius != d.radius || !div_unscaled_den_ok(nzd)) == 0u) {
+        const bool posOk = fabsf(b.posV.x) < 0x1p60f && fabsf(b.posV.y) < 0x1p60f;  // (div_unscaled bounds)
+        if (SPEC && __ballot(b.radius != d.radius || !div_unscaled_den_ok(nzd) || !posOk) == 0u) {
             b.nzRcp = rcp_refined(nzd);
 #pragma unroll RSD_P1_UNROLL
-            for (int i = 0; i < nd; ++i) pass1_dir_generic<SPEC, true>(a, u, v, px, py, b, i, ao, aoD, st);
+            for (int i = 0; i < nd; ++i) pass1_dir_generic<SPEC, true>(a, u, v, px, py, b, i, ao, aoD, st, &bf);
         } else {
 #pragma unroll RSD_P1_UNROLL
             for (int i = 0; i < nd; ++i) pass1_dir_generic<SPEC>(a, u, v, px, py, b, i, ao, aoD, st);
@@ -302,7 +305,8 @@ __device__ __forceinline__ void pass2_tile(const SvaoArgs& a, uint32_t x0, uint3
             if constexpr (SPEC) {
                 const float nzd = make_nonzero(b.normalO.z, 0.0001f);
                 const float ylx = rcp_refined(d.lowResolution[0]), yly = rcp_refined(d.lowResolution[1]);
-                if (__ballot(b.radius != d.radius || !div_unscaled_den_ok(nzd)) == 0u) {
+                const bool posOk = fabsf(b.posV.x) < 0x1p60f && fabsf(b.posV.y) < 0x1p60f;
+                if (__ballot(b.radius != d.radius || !div_unscaled_den_ok(nzd) || !posOk) == 0u) {
                     b.nzRcp = rcp_refined(nzd);
                     svao_pass2_dir<N, true, true>(a, b, u, v, (int)(e & 31u), p, r, ylx, yly);
                 } else {
@@ -515,7 +519,7 @@ rsd_status pass1_impl(const rsd_camera* cam, const rsd_vao_data* vao, const rsd_
     const uint32_t allDirs = a.k.nd == 32u ? 0xffffffffu : (1u << a.k.nd) - 1u;
     const bool spec = !(p1Env && std::strcmp(p1Env, "generic") == 0) && a.secondary == 2u && a.rayInterval &&
                       a.k.samePixelInt && a.d.sdGuard > 0 && W <= 4096u && H <= 4096u &&
-                      (a.k.fastDiv & allDirs) == allDirs;
+                      (a.k.fastDiv & allDirs) == allDirs && a.d.radius < 0x1p58f;
     const dim3 grid(nx / 16, 2 * bandGroups), block(16, 16);
     hipStream_t s = (hipStream_t)stream;
     if (spec && a.k.nd == 8u) hipLaunchKernelGGL((svao_pass1_kernel<true, 8>), grid, block, 0, s, a);
@@ -610,7 +614,8 @@ rsd_status pass2_impl(const rsd_camera* cam, const rsd_vao_data* vao, const rsd_
     const char* p2Env = std::getenv("RSD_PASS2");
     const bool spec = !(p2Env && std::strcmp(p2Env, "generic") == 0) && nd == 8u && W <= 4096u && H <= 4096u &&
                       (a.k.fastDiv & 0xffu) == 0xffu && a.d.lowResolution[0] >= 1.0f &&
-                      a.d.lowResolution[0] <= 0x1p20f && a.d.lowResolution[1] >= 1.0f && a.d.lowResolution[1] <= 0x1p20f;
+                      a.d.lowResolution[0] <= 0x1p20f && a.d.lowResolution[1] >= 1.0f && a.d.lowResolution[1] <= 0x1p20f &&
+                      a.d.radius < 0x1p58f;
 #define RSD_P2(NN)                                                                                           \
     if (nd == 32u) hipLaunchKernelGGL((svao_pass2_kernel<NN, 32>), grid, block, 0, s, a);                  \
     else if (nd == 16u) hipLaunchKernelGGL((svao_pass2_kernel<NN, 16>), grid, block, 0, s, a);             \

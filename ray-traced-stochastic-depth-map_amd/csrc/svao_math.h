@@ -52,6 +52,7 @@ struct SvaoArgs {
     uint32_t dual;  // DUAL_AO: ao holds (bright, dark) byte pairs (RG8Unorm)
     uint32_t bandIndex, bandCount;  // 32-row groups g (offset space) with g % count == index
     float isx, isy;  // imageScale (Common.slang:142), hoisted: 0.5 * (frameW / focal), same bits
+    float pzLo, pzHi;  // |p.z| in [pzLo, pzHi] keeps isx p.z and isy p.z in [2^-20, 2^20] (fill_scale)
     const float* snapU;  // getSnappedUV: snapU[k] = (k + 0.5f) / resolution.x for k in [0, resolution.x]
     const float* snapV;  //               snapV[k] = (k + 0.5f) / resolution.y
     const float4* nlut;  // decode_normal_2x8 of every 16-bit code (normal_lut), same bits
@@ -116,6 +117,14 @@ __device__ __forceinline__ float div_unscaled(float a, float b, float y1) {
     const float r1 = __builtin_fmaf(-q1, b, a);
     return __builtin_copysignf(__builtin_fmaf(r1, y1, q1), q0);
 }
+// div_unscaled without the sign fix of a zero quotient (callers for which +-0 give the same result)
+__device__ __forceinline__ float div_unscaled_tail(float a, float b, float y1) {
+    const float q0 = a * y1;
+    const float r0 = __builtin_fmaf(-q0, b, a);
+    const float q1 = __builtin_fmaf(r0, y1, q0);
+    const float r1 = __builtin_fmaf(-q1, b, a);
+    return __builtin_fmaf(r1, y1, q1);
+}
 // the numerator range of div_unscaled (false for NaN / inf)
 __device__ __forceinline__ bool div_unscaled_num_ok(float a) {
     const float m = fabsf(a);
@@ -165,6 +174,34 @@ __device__ __forceinline__ float depth_center(const SvaoArgs& a, float u, float 
     if (SMALL || (a.W <= 4096 && a.H <= 4096))
         return a.depth[(size_t)min(max(ky, 0), a.H - 1) * a.W + min(max(kx, 0), a.W - 1)];
     return depth_sample(a, u, v);
+}
+
+// Buffer resources of the specialised pass-1 direction loop (gfx9 raw buffers, CK's word-3 flags): the
+// snap-table and depth gathers take a 32-bit byte offset from one VALU op instead of 64-bit address
+// arithmetic.  The offsets are always inside the buffers (kx in [0, resolution.x], clamped depth texel).
+struct P1Bufs {
+    __amdgpu_buffer_rsrc_t depth, snapU, snapV;
+};
+// (the record count only bounds offsets, which are in range here: the maximum keeps the descriptor a
+// function of the kernel-argument pointer alone, i.e. in SGPRs -- a count computed in VALU made the
+// compiler wrap every load in a readfirstlane loop)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t raw_buffer(const void* p) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, 0x7fffffff, 0x00020000);
+}
+__device__ __forceinline__ float buf_load(__amdgpu_buffer_rsrc_t r, uint32_t byteOff) {
+    return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (int)byteOff, 0, 0));
+}
+__device__ __forceinline__ P1Bufs p1_bufs(const SvaoArgs& a) {
+    P1Bufs b;
+    b.depth = raw_buffer(a.depth);
+    b.snapU = raw_buffer(a.snapU);
+    b.snapV = raw_buffer(a.snapV);
+    return b;
+}
+// depth_center of the specialised kernels (W, H <= 4096): kx, ky >= 0 (floor of a saturated uv)
+__device__ __forceinline__ float depth_center_buf(const SvaoArgs& a, const P1Bufs& bf, int kx, int ky) {
+    const uint32_t x = min((uint32_t)kx, (uint32_t)a.W - 1u), y = min((uint32_t)ky, (uint32_t)a.H - 1u);
+    return buf_load(bf.depth, (y * (uint32_t)a.W + x) * 4u);
 }
 
 // the AO of pixel o: one R8Unorm byte, or the (bright, dark) RG8Unorm pair with DUAL_AO
@@ -259,7 +296,7 @@ __device__ __forceinline__ bool ratio_le_tenth(float n, float D) {
 // and div_rcp apply; a wave-uniform case of the specialised pass 1)
 template <bool ALLFAST = false>
 __device__ __forceinline__ bool sample_init(const SvaoArgs& a, float u, float v, const Basic& b, int i, Sample& s,
-                                            bool& ssrAbove) {
+                                            bool& ssrAbove, const P1Bufs* bf = nullptr) {
     const rsd_vao_data& d = a.d;
     float radius, dx, dy, sphereHeight;
     s.fast = false;
@@ -301,18 +338,38 @@ __device__ __forceinline__ bool sample_init(const SvaoArgs& a, float u, float v,
         return false;
     const f3 ip = b.posV + b.tangent * dx + b.bitangent * dy;
     s.ip = ip;
-    view_to_uv(a, ip, s.su, s.sv);
+    // ALLFAST: the two view-to-uv divisions through div_unscaled when every lane's p.z keeps both
+    // divisors in [2^-20, 2^20].  Exact for |p.x|, |p.y| in [2^-100, 2^70] (|posV| < 2^60 per pixel, the
+    // sample offset < radius); a smaller numerator gives |x / den| < 2^-80, and then u = x / den * -0.5 +
+    // 0.5 rounds to 0.5 whichever tiny quotient the sequence returns, and su is all that is used of it.
+    if (ALLFAST && __ballot(!(fabsf(ip.z) >= a.pzLo && fabsf(ip.z) <= a.pzHi)) == 0u) {
+        const float dx2 = a.isx * ip.z, dy2 = a.isy * ip.z;
+        const float ndcx = div_unscaled_tail(ip.x, dx2, rcp_refined(dx2));
+        const float ndcy = div_unscaled_tail(ip.y, dy2, rcp_refined(dy2));
+        s.su = ndcx * -0.5f + 0.5f;
+        s.sv = ndcy * 0.5f + 0.5f;
+    } else {
+        view_to_uv(a, ip, s.su, s.sv);
+    }
     s.visibility = 0.0f;
     s.objectSpaceZ = 0.0f;
     const float ex = (u - s.su) * d.resolution[0], ey = (v - s.sv) * d.resolution[1];
     ssrAbove = ex * ex + ey * ey >= a.k.ssrMin2;
-    const float cu = saturate(s.su), cv = saturate(s.sv);
+    // ALLFAST: saturate as fmin(fmax(x, 0), 1) (NaN -> 0 as well); it may differ from saturate only in
+    // the sign of a zero, which neither use of cu below can see (-0 == +0; floor(+-0 * res) = 0)
+    const float cu = ALLFAST ? fminf(fmaxf(s.su, 0.0f), 1.0f) : saturate(s.su);
+    const float cv = ALLFAST ? fminf(fmaxf(s.sv, 0.0f), 1.0f) : saturate(s.sv);
     s.isInScreen = (s.su == cu) && (s.sv == cv);
     // getSnappedUV (Common.slang:116-120): (floor(uv * res) + 0.5) / res from the host table
     s.kx = (int)floorf(cu * d.resolution[0]);
     s.ky = (int)floorf(cv * d.resolution[1]);
-    s.ru = a.snapU[s.kx];
-    s.rv = a.snapV[s.ky];
+    if (bf) {
+        s.ru = buf_load(bf->snapU, (uint32_t)s.kx * 4u);
+        s.rv = buf_load(bf->snapV, (uint32_t)s.ky * 4u);
+    } else {
+        s.ru = a.snapU[s.kx];
+        s.rv = a.snapV[s.ky];
+    }
     return true;
 }
 
@@ -351,8 +408,8 @@ __device__ __forceinline__ void add_sample(const SvaoArgs& a, const Basic& b, Sa
 
 // Common.slang:492-496
 template <bool SMALL = false>
-__device__ __forceinline__ void eval_primary(const SvaoArgs& a, const Basic& b, Sample& s) {
-    const float z = depth_center<SMALL>(a, s.ru, s.rv, s.kx, s.ky);
+__device__ __forceinline__ void eval_primary(const SvaoArgs& a, const Basic& b, Sample& s, const P1Bufs* bf = nullptr) {
+    const float z = bf ? depth_center_buf(a, *bf, s.kx, s.ky) : depth_center<SMALL>(a, s.ru, s.rv, s.kx, s.ky);
     add_sample(a, b, s, uv_to_view(a, s.ru, s.rv, z), true);
 }
 
@@ -367,6 +424,11 @@ inline void fill_scale(SvaoArgs& a) {
     // Common.slang:142/150 imageScale, evaluated once on the host (IEEE float, same bits)
     a.isx = 0.5f * (a.cam.frameWidth / a.cam.focalLength);
     a.isy = 0.5f * (a.cam.frameHeight / a.cam.focalLength);
+    // with a factor-2 margin for the rounding of isx * p.z (0 when the scales are not finite and positive)
+    const double lo = std::min(a.isx, a.isy), hi = std::max(a.isx, a.isy);
+    const bool ok = lo > 0.0 && hi < 1e30;
+    a.pzLo = ok ? (float)(0x1p-19 / lo) : INFINITY;
+    a.pzHi = ok ? (float)(0x1p19 / hi) : 0.0f;
 }
 
 inline void fill_consts(SvaoConsts& k, const rsd_vao_data& d, uint32_t nd) {
