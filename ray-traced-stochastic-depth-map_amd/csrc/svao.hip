@@ -236,6 +236,7 @@ struct P2Shared {
     float acc[kP2Lanes];           // running vis of each slot (bright)
     float accD[kP2Lanes];          // ... dark channel (DUAL_AO)
     float p[kP2Lanes], r[kP2Lanes];
+    uchar2 aoPrev[kP2Lanes];       // the pixel's pass-1 AO (bright, dark), read with the stencil
     // the pixel's BasicAOData, evaluated once per pixel, not per pair: the 16 floats pass 2 reads
     // (posVLength, normalV, radiusInPixels stay out)
     alignas(16) float basic[kP2Lanes][16];
@@ -252,9 +253,25 @@ __device__ __forceinline__ void pass2_tile(const SvaoArgs& a, uint32_t x0, uint3
     if (tid == 0) { sh.nPix = 0u; sh.nPair = 0u; }
     __syncthreads();
     {
+        // every read of the tile's pixels is issued at once, independent of the stencil: the stencil, the
+        // pixel's depth and packed normal (basic_init's reads) and the pass-1 AO the finish adds to; then
+        // the normal-table read.  (Round 2 read the stencil first and the rest behind it: two more
+        // dependent memory round trips per tile.)
         const uint32_t px = x0 + (tid % T), py = y0 + (tid / T);
-        const uint32_t m =
-            (px < (uint32_t)a.W - a.guard && py < (uint32_t)a.H - a.guard) ? stencil_load(a, (size_t)py * a.W + px) : 0u;
+        const bool inb = px < (uint32_t)a.W - a.guard && py < (uint32_t)a.H - a.guard;
+        const size_t po = (size_t)py * a.W + px;
+        const float u = ((float)px + 0.5f) * d.invResolution[0];
+        const float v = ((float)py + 0.5f) * d.invResolution[1];
+        uint32_t m = 0u, packed = 0u;
+        float z = 0.0f;
+        uchar2 prev = make_uchar2(0, 0);
+        if (inb) {
+            m = stencil_load(a, po);
+            basic_reads<SPEC>(a, u, v, z, packed);
+            if (a.dual) prev = reinterpret_cast<const uchar2*>(a.ao)[po];
+            else prev.x = a.ao[po];
+        }
+        const float4 nl = a.nlut[packed];
         if (m) {
             const uint32_t slot = atomicAdd(&sh.nPix, 1u), base = atomicAdd(&sh.nPair, (uint32_t)__popc(m));
             sh.pix[slot] = tid;
@@ -265,10 +282,9 @@ __device__ __forceinline__ void pass2_tile(const SvaoArgs& a, uint32_t x0, uint3
             for (int i = 0; i < ND; ++i)
                 if (m & (1u << i)) sh.pair[j++] = (uint16_t)(slot << 5 | i);
             // a non-zero stencil means pass 1's basic_init of this pixel succeeded (same bits)
-            const float u = ((float)px + 0.5f) * d.invResolution[0];
-            const float v = ((float)py + 0.5f) * d.invResolution[1];
             Basic b;
-            basic_init(a, u, v, b);
+            basic_from(a, u, v, z, nl, b);
+            sh.aoPrev[slot] = prev;
             float* q = sh.basic[slot];
             q[0] = b.posV.x; q[1] = b.posV.y; q[2] = b.posV.z;
             q[3] = b.normal.x; q[4] = b.normal.y; q[5] = b.normal.z;
@@ -334,7 +350,7 @@ __device__ __forceinline__ void pass2_tile(const SvaoArgs& a, uint32_t x0, uint3
     for (uint32_t sl = tid; sl < nPix; sl += L) {
         const uint32_t lp = sh.pix[sl] & 255u;
         const size_t o = (size_t)(y0 + lp / T) * a.W + (x0 + lp % T);
-        ao_finish(a, o, sh.acc[sl], sh.accD[sl]);
+        ao_finish(a, o, sh.acc[sl], sh.accD[sl], sh.aoPrev[sl]);
     }
 }
 

@@ -209,19 +209,18 @@ __device__ __forceinline__ void ao_store(const SvaoArgs& a, size_t o, float brig
     if (a.dual) reinterpret_cast<uchar2*>(a.ao)[o] = make_uchar2(unorm8(bright), unorm8(dark));
     else a.ao[o] = unorm8(bright);
 }
-// pass 2's (and the Raytraced pass 2's) end of a refined pixel, SVAORaster2.ps.slang:60-64: the
+// pass 2's (and the Raytraced pass 2's) end of a refined pixel; prev = its pass-1 AO bytes, SVAORaster2.ps.slang:60-64: the
 // direction sums (bright: sum of refined - raster visibility; dark: sum of refined) scaled by
 // 2 / NUM_DIRECTIONS (Common.slang:660-661), plus the pass-1 AO, dark = min(bright, dark), finalize
-__device__ __forceinline__ void ao_finish(const SvaoArgs& a, size_t o, float accB, float accD) {
+__device__ __forceinline__ void ao_finish(const SvaoArgs& a, size_t o, float accB, float accD, uchar2 prev) {
     float vb = accB;
     vb *= a.k.invNd;
     vb *= 2.0f;
     if (!a.dual) {
-        vb += unorm8_to_float(a.ao[o]);
+        vb += unorm8_to_float(prev.x);
         a.ao[o] = unorm8(acc_pow(vb, a.d.exponent));
         return;
     }
-    const uchar2 prev = reinterpret_cast<const uchar2*>(a.ao)[o];
     float vd = accD;
     vd *= a.k.invNd;
     vd *= 2.0f;
@@ -243,11 +242,29 @@ __device__ __forceinline__ void stencil_store(const SvaoArgs& a, size_t o, uint3
     else a.stencil[o] = (uint8_t)m;
 }
 
+// the reads of basic_init: the pixel's depth and its packed normal (0 outside the frame)
+template <bool SMALL = false>
+__device__ __forceinline__ void basic_reads(const SvaoArgs& a, float u, float v, float& z, uint32_t& packed) {
+    const rsd_vao_data& d = a.d;
+    z = depth_center<SMALL>(a, u, v, (int)(u * d.resolution[0]), (int)(v * d.resolution[1]));
+    const uint32_t ix = (uint32_t)(u * d.resolution[0]), iy = (uint32_t)(v * d.resolution[1]);
+    packed = (ix < (uint32_t)a.W && iy < (uint32_t)a.H) ? a.normals[(size_t)iy * a.W + ix] : 0u;
+}
+
+// Common.slang:285-324 from the reads above (z, nl = decode_normal_2x8(packed) from the device table)
+__device__ __forceinline__ bool basic_from(const SvaoArgs& a, float u, float v, float z, float4 nl, Basic& b);
+
 // Common.slang:285-324
 template <bool SMALL = false>
 __device__ __forceinline__ bool basic_init(const SvaoArgs& a, float u, float v, Basic& b) {
+    float z;
+    uint32_t packed;
+    basic_reads<SMALL>(a, u, v, z, packed);
+    return basic_from(a, u, v, z, a.nlut[packed], b);  // nlut = decode_normal_2x8, tabulated on the device
+}
+
+__device__ __forceinline__ bool basic_from(const SvaoArgs& a, float u, float v, float z, float4 nl, Basic& b) {
     const rsd_vao_data& d = a.d;
-    const float z = depth_center<SMALL>(a, u, v, (int)(u * d.resolution[0]), (int)(v * d.resolution[1]));
     const float rux = (d.radius * a.cam.focalLength) / (a.cam.frameWidth * z);
     const float ruy = (d.radius * a.cam.focalLength) / (a.cam.frameHeight * z);
     const float pa = rux * d.resolution[0], pb = ruy * d.resolution[1];
@@ -261,9 +278,6 @@ __device__ __forceinline__ bool basic_init(const SvaoArgs& a, float u, float v, 
     if (b.radiusInPixels < 0.5f) return false;
     b.posV = uv_to_view(a, u, v, z);
     b.posVLength = length(b.posV);
-    const uint32_t ix = (uint32_t)(u * d.resolution[0]), iy = (uint32_t)(v * d.resolution[1]);
-    const uint32_t packed = (ix < (uint32_t)a.W && iy < (uint32_t)a.H) ? a.normals[(size_t)iy * a.W + ix] : 0u;
-    const float4 nl = a.nlut[packed];  // = decode_normal_2x8(packed), tabulated on the device
     b.normalV = mk(nl.x, nl.y, nl.z);
     if (dot(b.posV, b.normalV) > 0.0f) b.normalV = -b.normalV;
     const float nu = u * d.noiseScale[0], nv = v * d.noiseScale[1];

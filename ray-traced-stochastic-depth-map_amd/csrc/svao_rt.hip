@@ -251,7 +251,8 @@ __global__ void __launch_bounds__(64) svao_pass2_rt_kernel(RtArgs ra) {
     if (lane < nPix) {
         const uint32_t lp = sPix[lane] & 63u;
         const size_t o = (size_t)(y0 + lp / 8u) * a.W + (x0 + lp % 8u);
-        ao_finish(a, o, sAcc[lane], sAccD[lane]);
+        const uchar2 prev = a.dual ? reinterpret_cast<const uchar2*>(a.ao)[o] : make_uchar2(a.ao[o], 0);
+        ao_finish(a, o, sAcc[lane], sAccD[lane], prev);
     }
 }
 
