@@ -209,9 +209,10 @@ __device__ __forceinline__ void ao_store(const SvaoArgs& a, size_t o, float brig
     if (a.dual) reinterpret_cast<uchar2*>(a.ao)[o] = make_uchar2(unorm8(bright), unorm8(dark));
     else a.ao[o] = unorm8(bright);
 }
-// pass 2's (and the Raytraced pass 2's) end of a refined pixel; prev = its pass-1 AO bytes, SVAORaster2.ps.slang:60-64: the
+// pass 2's (and the Raytraced pass 2's) end of a refined pixel, SVAORaster2.ps.slang:60-64: the
 // direction sums (bright: sum of refined - raster visibility; dark: sum of refined) scaled by
-// 2 / NUM_DIRECTIONS (Common.slang:660-661), plus the pass-1 AO, dark = min(bright, dark), finalize
+// 2 / NUM_DIRECTIONS (Common.slang:660-661), plus the pass-1 AO (prev: the pixel's (bright, dark)
+// bytes as pass 1 stored them), dark = min(bright, dark), finalize
 __device__ __forceinline__ void ao_finish(const SvaoArgs& a, size_t o, float accB, float accD, uchar2 prev) {
     float vb = accB;
     vb *= a.k.invNd;
