@@ -262,10 +262,11 @@ __device__ __forceinline__ void sd_store(const SDArgs& a, int x, int y, const fl
 // anyHit -> algorithm (Common.slangh:102-254) for ONE delivered hit: hash `rng` of its
 // barycentrics, normalized view depth `z`, `af` = the alpha test failed.  Returns the commit
 // decision (true: the any-hit shader accepts the hit, DXR TMax = t).
-template <int N>
-__device__ __forceinline__ bool sd_any_hit(const SDArgs& a, float rng, float z, bool af, float (&depths)[N],
-                                           uint32_t& cnt) {
-    if (a.impl == 1u) {  // CoverageMask, Common.slangh:117-131, 189-209
+template <int N, int IMPL>
+__device__ __forceinline__ bool sd_any_hit_impl(const SDArgs& a, float rng, float z, bool af, float (&depths)[N],
+                                                uint32_t& cnt) {
+    // IMPL >= 0: the implementation known at compile time (the specialised row walk: 0 = Default)
+    if (IMPL < 0 && a.impl == 1u) {  // CoverageMask, Common.slangh:117-131, 189-209
         const int R = (int)floorf(a.alpha * (float)N + rng);
         uint32_t mask = 0u;
         if (R >= N) mask = 0xffffu;
@@ -282,7 +283,7 @@ __device__ __forceinline__ bool sd_any_hit(const SDArgs& a, float rng, float z, 
             maxT = hmax(maxT, depths[i]);
         }
         return !(z < maxT);
-    } else if (a.impl == 3u) {  // KBuffer, Common.slangh:132-135, 211-232
+    } else if (IMPL < 0 && a.impl == 3u) {  // KBuffer, Common.slangh:132-135, 211-232
         if (z >= depths[N - 1]) return true;
         cnt++;
         if (af) return cnt >= a.maxCount;
@@ -299,6 +300,11 @@ __device__ __forceinline__ bool sd_any_hit(const SDArgs& a, float rng, float z, 
             if ((uint32_t)i == slot && !(depths[i] <= z) && !af) depths[i] = z;
         return cnt >= a.maxCount;
     }
+}
+template <int N>
+__device__ __forceinline__ bool sd_any_hit(const SDArgs& a, float rng, float z, bool af, float (&depths)[N],
+                                           uint32_t& cnt) {
+    return sd_any_hit_impl<N, -1>(a, rng, z, af, depths, cnt);
 }
 
 // ------------------------------------------------------------------------------------
@@ -1156,7 +1162,7 @@ __device__ __forceinline__ int row_prefix(int v, int l, int base, int& total) {
 // anyHit -> algorithm (Common.slangh:102-254) over `found` keys in ascending (t, prim) order;
 // lane j of the row holds key j's hash `rng` and normalized view depth `z`.  Every lane of
 // the row ends with the same depths / cnt / commit.
-template <int K, int N>
+template <int K, int N, int IMPL = -1>
 __device__ __forceinline__ bool sd_algorithm_row(const SDArgs& a, float rng, float z, bool afl, int found,
                                                  int base, float (&depths)[N], uint32_t& cnt, uint32_t& delivered) {
     bool commit = false;
@@ -1168,7 +1174,7 @@ __device__ __forceinline__ bool sd_algorithm_row(const SDArgs& a, float rng, flo
         const bool af = (afm >> (base + j)) & 1u;
         if (commit || j >= found) continue;
         delivered++;
-        commit = sd_any_hit<N>(a, rj, zj, af, depths, cnt);
+        commit = sd_any_hit_impl<N, IMPL>(a, rj, zj, af, depths, cnt);
     }
     return commit;
 }
@@ -1194,7 +1200,10 @@ __device__ __forceinline__ void sd_hit_terms(const SDArgs& a, const RayCtx& r, f
 // per queue slot); sd_resolve_row_kernel runs the algorithm.  Valid when one chunk of K keys
 // always decides the texel: Default / KBuffer with MaxCount <= K.  Otherwise the algorithm
 // runs here and the walk continues after the K-th key while it has not committed.
-template <int K, int N, int ROW, bool SPLIT, bool CNT, int POOL = kPoolCap>
+// SPEC: the specialised fused walk of the common trace -- the Default reservoir with MaxCount <= K (a
+// commit by the K-th key, so no second chunk of keys) and no alpha-tested triangles: the lower-bound
+// (useLB) tests, the alpha test, the other implementations and the chunk continuation compile away.
+template <int K, int N, int ROW, bool SPLIT, bool CNT, int POOL = kPoolCap, bool SPEC = false>
 __global__ void __launch_bounds__(kBlock) sd_trace_row_kernel(SDArgs a, const float4* __restrict__ queue,
                                                               uint32_t* __restrict__ qctl, uint2* __restrict__ keys) {
     static_assert(K <= ROW, "one key per lane");
@@ -1290,6 +1299,7 @@ __global__ void __launch_bounds__(kBlock) sd_trace_row_kernel(SDArgs a, const fl
         if (phase != kTrace) continue;
 
         // ---- one traversal step of this row
+        if constexpr (SPEC) useLB = false;
         const float tlo = useLB ? fmaxf(TMin, lbT) : TMin;
         float kthT = row_bcastf<ROW, K - 1>(kt, l, base);
         uint32_t kthP = row_bcast<ROW, K - 1>(kp, l, base);
@@ -1467,7 +1477,7 @@ __global__ void __launch_bounds__(kBlock) sd_trace_row_kernel(SDArgs a, const fl
         float rng = 0.0f, z = 0.0f;
         bool af = false;
         if (l < found) {
-            if (a.alphaTest) {
+            if (!SPEC && a.alphaTest) {
                 sd_hit_terms(a, r, cosT, a.primRec[kp], rng, z, af);
             } else {
                 rng = sd_hash(ku, kv);
@@ -1476,10 +1486,10 @@ __global__ void __launch_bounds__(kBlock) sd_trace_row_kernel(SDArgs a, const fl
             }
         }
         uint32_t delivered = 0;
-        const bool commit = sd_algorithm_row<K, N>(a, rng, z, af, found, base, depths, cnt, delivered);
+        const bool commit = sd_algorithm_row<K, N, SPEC ? 0 : -1>(a, rng, z, af, found, base, depths, cnt, delivered);
         if (l == 0) hitsDelivered += delivered;
         if (CNT && l == 0) tResolve += __builtin_amdgcn_s_memtime() - tS1;
-        if (!commit && found == K) {
+        if (!SPEC && !commit && found == K) {
             // the stream continues after the K-th key: trace the next chunk of K keys
             useLB = true;
             lbT = __shfl(kt, base + K - 1);
@@ -1693,7 +1703,12 @@ static hipError_t launch_sd_kn(const SDArgs& a, dim3 grid, uint32_t persistentBl
         if ((e = hipGetLastError()) != hipSuccess) return e;
         hipLaunchKernelGGL((sd_resolve_row_kernel<K, N, ROW, true>), pg, wb, 0, s, a, queue, qctl, keys);
     } else if (walk == 1) {
+        // the specialised walk (RSD_TRACE_SPEC=off: the generic one, A/B runs)
+        const char* specEnv = std::getenv("RSD_TRACE_SPEC");
+        const bool spec = !(specEnv && std::string(specEnv) == "off") && !a.alphaTest && a.impl != 1u &&
+                          a.impl != 3u && a.maxCount <= (uint32_t)K && pool == kPoolCap;
         if (a.counters) hipLaunchKernelGGL((sd_trace_row_kernel<K, N, ROW, false, true>), pg, wb, 0, s, a, queue, qctl, keys);
+        else if (spec) hipLaunchKernelGGL((sd_trace_row_kernel<K, N, ROW, false, false, kPoolCap, true>), pg, wb, 0, s, a, queue, qctl, keys);
         else hipLaunchKernelGGL((sd_trace_row_kernel<K, N, ROW, false, false>), pg, wb, 0, s, a, queue, qctl, keys);
     } else {
         hipLaunchKernelGGL((sd_trace_queue_kernel<K, N>), dim3(persistentBlocks), dim3(kBlock), 0, s, a, queue, qctl);
