@@ -1706,8 +1706,9 @@ static hipError_t launch_sd_kn(const SDArgs& a, dim3 grid, uint32_t persistentBl
         // the specialised walk (RSD_TRACE_SPEC=off: the generic one, A/B runs)
         const char* specEnv = std::getenv("RSD_TRACE_SPEC");
         const bool spec = !(specEnv && std::string(specEnv) == "off") && !a.alphaTest && a.impl != 1u &&
-                          a.impl != 3u && a.maxCount <= (uint32_t)K && pool == kPoolCap;
+                          a.impl != 3u && a.maxCount <= (uint32_t)K;
         if (a.counters) hipLaunchKernelGGL((sd_trace_row_kernel<K, N, ROW, false, true>), pg, wb, 0, s, a, queue, qctl, keys);
+        else if (spec && pool == 128) hipLaunchKernelGGL((sd_trace_row_kernel<K, N, ROW, false, false, 128, true>), pg, wb, 0, s, a, queue, qctl, keys);
         else if (spec) hipLaunchKernelGGL((sd_trace_row_kernel<K, N, ROW, false, false, kPoolCap, true>), pg, wb, 0, s, a, queue, qctl, keys);
         else hipLaunchKernelGGL((sd_trace_row_kernel<K, N, ROW, false, false>), pg, wb, 0, s, a, queue, qctl, keys);
     } else {
@@ -2031,9 +2032,13 @@ rsd_status sd_trace_impl(rsd_scene* scene, const rsd_camera* cam, const rsd_sd_p
     // bound (kPoolCap >= poolSoft + 48 + 3 * depth), or RSD_TRACE_WALK=quad asks for the
     // depth-first quad walk (A/B measurements)
     const int depth = (int)std::max(1u, scene->stats.wide_depth);
-    // experiments: RSD_TRACE_POOL=128 halves the row walk's LDS pool (8 KB per wave: 20 waves / CU)
+    // the row walk's LDS pool: 128 entries per ray (8 KB per wave) wherever the tree depth allows it
+    // (the pool bound above), else 256; with the specialised walk the smaller pool measured faster alone
+    // (75.7 vs 78.3 us at configs[1]) and leaves more LDS to the other frames' passes
+    // (profiles/round3/ab/trace_pool/).  RSD_TRACE_POOL=256 forces the large pool (A/B runs); the
+    // instrumented (counters) walk always uses 256.
     static const char* poolEnv = std::getenv("RSD_TRACE_POOL");
-    int pool = poolEnv && std::atoi(poolEnv) == 128 && !counters ? 128 : kPoolCap;
+    int pool = (poolEnv && std::atoi(poolEnv) == 256) || counters ? kPoolCap : 128;
     if (pool - 48 - 3 * depth < 16) pool = kPoolCap;
     a.poolSoft = std::min(pool - 48 - 3 * depth, 160);
     const char* walkEnv = std::getenv("RSD_TRACE_WALK");  // read per call: tests cover every walk
