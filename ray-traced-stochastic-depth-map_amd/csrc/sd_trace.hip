@@ -454,7 +454,7 @@ __device__ __forceinline__ int trace_knearest_quad(const float4* __restrict__ bv
 
 // TraceRay + anyHit -> algorithm (Common.slangh:102-254) over the canonical hit stream,
 // for the ray of this quad.  All 4 lanes end with identical depths.
-template <int K, int N>
+template <int K, int N, bool SPEC = false>
 __device__ __forceinline__ void sd_resolve(const SDArgs& a, f3 d, float TMin, float TMax, float cosT, float (&depths)[N],
                                            uint32_t* sItem, float* sT, int q, int quadBase, TraceStats& st,
                                            uint32_t& hitsDelivered, const uint32_t* ent = nullptr,
@@ -469,7 +469,8 @@ __device__ __forceinline__ void sd_resolve(const SDArgs& a, f3 d, float TMin, fl
     uint32_t lbP = 0u;
     constexpr int J = (K + 3) / 4;  // hits per lane in the epilogue
     while (!commit) {
-        const int found = trace_knearest_quad<K>(a.nodes, a.triOff, r, TMin, TMax, a.cull, useLB, lbT, lbP, kl, sItem,
+        // SPEC (as the row walk's): one chunk of K keys decides the texel -- no lower bound, no alpha test
+        const int found = trace_knearest_quad<K>(a.nodes, a.triOff, r, TMin, TMax, a.cull, SPEC ? false : useLB, lbT, lbP, kl, sItem,
                                                  sT, q, quadBase, st, ent, nEnt);
         // barycentrics + hash of hit j are computed by lane j % 4 (re-running the identical
         // triangle test on the hit's record), then shared with the quad
@@ -492,7 +493,7 @@ __device__ __forceinline__ void sd_resolve(const SDArgs& a, f3 d, float TMin, fl
                 float z = t * cosT;  // RayToViewDepth
                 if (a.normalize) z = saturate((z - c.nearZ) / (c.farZ - c.nearZ));
                 zL[i] = z;
-                if (a.alphaTest && (__float_as_uint(v1.w) & 4u) &&
+                if (!SPEC && a.alphaTest && (__float_as_uint(v1.w) & 4u) &&
                     alpha_test_fails(a.alphaData, __float_as_uint(v0.w), v0, v1, v2, bu, bv, true, t, r.d))
                     afL |= 1u << i;
             }
@@ -504,9 +505,9 @@ __device__ __forceinline__ void sd_resolve(const SDArgs& a, f3 d, float TMin, fl
             const bool af = (qselu(afL, j % 4) >> (j / 4)) & 1u;
             if (commit || j >= found) continue;
             hitsDelivered++;
-            commit = sd_any_hit<N>(a, rng, z, af, depths, count);
+            commit = sd_any_hit_impl<N, SPEC ? 0 : -1>(a, rng, z, af, depths, count);
         }
-        if (found < K) break;  // stream exhausted
+        if (SPEC || found < K) break;  // stream exhausted (SPEC: a commit by the K-th key)
         useLB = true;
         lbT = kl.t[K - 1];
         lbP = kl.p[K - 1];
@@ -676,7 +677,7 @@ __global__ void __launch_bounds__(kSetupWaves * kBlock) sd_setup_kernel(SDArgs a
 // The first chunk of each wave is static (blockIdx); later ones come from one atomic head
 // that starts after the static range, so a wave with no static chunk exits without an
 // atomic (one head word serialises ~90 dequeues/us, MI355X_MICROARCH.md "dequeue").
-template <int K, int N>
+template <int K, int N, bool SPEC = false>
 __global__ void __launch_bounds__(kBlock) sd_trace_queue_kernel(SDArgs a, const float4* __restrict__ queue,
                                                                 uint32_t* __restrict__ qctl) {
     __shared__ uint32_t sItem[kQuadStack * kQuadRays];
@@ -707,7 +708,7 @@ __global__ void __launch_bounds__(kBlock) sd_trace_queue_kernel(SDArgs a, const 
             for (int i = 0; i < N; ++i) depths[i] = DEFAULT;
             const uint32_t n0 = st.nodes, l0 = st.leaves;
             const unsigned long long c0 = a.counters ? __builtin_amdgcn_s_memtime() : 0ull;
-            sd_resolve<K, N>(a, d, TMin, TMax, cosT, depths, &sItem[quad], &sT[quad], q, quadBase, st,
+            sd_resolve<K, N, SPEC>(a, d, TMin, TMax, cosT, depths, &sItem[quad], &sT[quad], q, quadBase, st,
                              hitsDelivered, a.entOn ? a.entQ + (size_t)slot * kEntryCap : nullptr, nEnt);
             if (q == 0) {
                 if (a.counters) {
@@ -1712,7 +1713,12 @@ static hipError_t launch_sd_kn(const SDArgs& a, dim3 grid, uint32_t persistentBl
         else if (spec) hipLaunchKernelGGL((sd_trace_row_kernel<K, N, ROW, false, false, kPoolCap, true>), pg, wb, 0, s, a, queue, qctl, keys);
         else hipLaunchKernelGGL((sd_trace_row_kernel<K, N, ROW, false, false>), pg, wb, 0, s, a, queue, qctl, keys);
     } else {
-        hipLaunchKernelGGL((sd_trace_queue_kernel<K, N>), dim3(persistentBlocks), dim3(kBlock), 0, s, a, queue, qctl);
+        // the specialised quad walk (the row walk's conditions; RSD_TRACE_SPEC=off: the generic one)
+        const char* specEnv = std::getenv("RSD_TRACE_SPEC");
+        const bool spec = !(specEnv && std::string(specEnv) == "off") && !a.alphaTest && a.impl != 1u &&
+                          a.impl != 3u && a.maxCount <= (uint32_t)K && !a.counters;
+        if (spec) hipLaunchKernelGGL((sd_trace_queue_kernel<K, N, true>), dim3(persistentBlocks), dim3(kBlock), 0, s, a, queue, qctl);
+        else hipLaunchKernelGGL((sd_trace_queue_kernel<K, N>), dim3(persistentBlocks), dim3(kBlock), 0, s, a, queue, qctl);
     }
     return hipGetLastError();
 }
