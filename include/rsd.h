@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define RSD_ABI_VERSION 4
+#define RSD_ABI_VERSION 5
 
 typedef enum {
     RSD_OK = 0,
@@ -171,7 +171,16 @@ typedef struct {
                                       visits only flagged tiles and clears the flags it consumed (the
                                       reference's pass 2 returns on aoMask == 0, SVAORaster2.ps.slang:50-52).
                                       Pass 2 must get the flags of the pass 1 that wrote d_stencil. */
+    uint32_t numerics;             /* ABI v5: rsd_numerics of pass 1 and pass 2 (DESIGN.md 2 "Numerics") */
 } rsd_svao_params;
+/* Arithmetic of the SVAO passes ("AO 1", "AO 2"; the SD trace is always exact).
+ *   FAST   FMA contraction, v_rcp_f32-based division, hardware sqrt / rsq, float32 denormals flushed:
+ *          what D3D allows the reference's HLSL (mad may fuse, '/' within 2.5 ulp, denormals flushed).
+ *          Graded against the CPU oracle by BASELINE.md section 4's AO tolerance (MAE <= 1/255 over the
+ *          visible pixels, |diff| <= 2/255 on >= 99.5 %).  The default (zero-initialised params).
+ *   EXACT  binary32 round-to-nearest operation by operation, correctly rounded '/' and sqrt: bit-identical
+ *          to the CPU oracle (oracle/rsd_oracle.c), at a higher instruction count. */
+typedef enum { RSD_NUMERICS_FAST = 0, RSD_NUMERICS_EXACT = 1 } rsd_numerics;
 /* Bytes of rsd_svao_params.tile_flags for a width x height frame buffer with guard_band: one per 16x16
  * tile of the visible region rounded up to 32 rows (the padded pass-1 dispatch, SVAO.cpp:347-350). */
 uint32_t rsd_svao_tile_count(uint32_t width, uint32_t height, uint32_t guard_band);

@@ -26,6 +26,7 @@
 // the script connects and does no work, so the scripts build and run unchanged.
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 
 #include "graph.h"
 #include "../../../include/rsd_graph.h"
@@ -62,6 +63,14 @@ const std::initializer_list<const char*> kDepthModeNames = {"SingleDepth", "Dual
 const std::initializer_list<const char*> kImplNames = {"Default", "CoverageMask", "ReservoirSampling",
                                                        "KBuffer"};  // StochasticDepthImplementation.h
 const std::initializer_list<const char*> kHitOrderNames = {"Canonical", "Traversal"};  // rsd.h rsd_hit_order
+const std::initializer_list<const char*> kNumericsNames = {"Fast", "Exact"};  // rsd.h rsd_numerics
+
+// the SVAO passes' arithmetic when the graph does not set "numerics": RSD_NUMERICS=exact in the
+// environment selects the oracle-exact kernels (tests), otherwise the fast default (rsd.h rsd_numerics)
+uint32_t defaultNumerics() {
+    const char* e = std::getenv("RSD_NUMERICS");
+    return (e && std::string(e) == "exact") ? (uint32_t)RSD_NUMERICS_EXACT : (uint32_t)RSD_NUMERICS_FAST;
+}
 
 const SceneRef* requireScene(const SceneRef* s, const std::string& who) {
     if (!s || !s->scene) throw std::runtime_error(who + ": no scene set");
@@ -294,7 +303,8 @@ private:
 // :192-455 execute.  Members the reference sets only from its GUI (SVAO.h:90-126) are
 // accepted as extra Properties with the same defaults: stochSamples, stochMaxCount,
 // stochGuardBand, stochJitter, rayInterval, cullMode, sampleCount, stochImplementation; and the
-// librsd extension stochHitOrder (rsd_hit_order, passed on as the SD pass's HitOrder).
+// librsd extensions stochHitOrder (rsd_hit_order, passed on as the SD pass's HitOrder) and numerics
+// ("Fast" / "Exact", rsd_numerics of the two SVAO passes; default RSD_NUMERICS from the environment, else Fast).
 class SVAOPass : public RenderPass {
 public:
     explicit SVAOPass(const Properties& p) {
@@ -317,6 +327,7 @@ public:
         impl_ = enumProp(p, "stochImplementation", kImplNames, 0);
         hitOrder_ = enumProp(p, "stochHitOrder", kHitOrderNames, 0);  // librsd extension (rsd_hit_order)
         rayPipeline_ = p.getBool("rayPipeline", true);  // SVAO.h:101
+        numerics_ = enumProp(p, "numerics", kNumericsNames, defaultNumerics());  // librsd extension (rsd_numerics)
     }
     void checkSupported() const {
         if (primary_ != 0) throw Unsupported("SVAO: primaryDepthMode other than SingleDepth is not implemented");
@@ -367,7 +378,7 @@ public:
         height_ = cd.defaultHeight;
         sdSize(width_, height_, &vao_, &sdW_, &sdH_);
         svp_ = rsd_svao_params{directions_, samples_, secondary_, (uint32_t)rayInterval_, (uint32_t)jitter_, 0,
-                               (uint32_t)dualAo_};
+                               (uint32_t)dualAo_, nullptr, numerics_};
         sdGraph_.reset();
         if (secondary_ != 2) return;
         // SVAO.cpp:157-189: the nested "Stochastic Depth" graph
@@ -459,7 +470,7 @@ public:
 private:
     const SceneRef* scene_ = nullptr;
     float radius_, exponent_, thickness_;
-    uint32_t primary_, secondary_, divisor_, samples_, maxCount_, cull_, directions_, impl_, hitOrder_;
+    uint32_t primary_, secondary_, divisor_, samples_, maxCount_, cull_, directions_, impl_, hitOrder_, numerics_;
     int32_t guardPx_;
     bool dualAo_, alphaTest_, jitter_, rayInterval_, rayPipeline_;
     uint32_t width_ = 0, height_ = 0, sdW_ = 0, sdH_ = 0;

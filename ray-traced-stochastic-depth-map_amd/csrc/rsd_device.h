@@ -30,7 +30,11 @@ __device__ __forceinline__ f3 cross(f3 a, f3 b) {
     return mk(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
 }
 __device__ __forceinline__ f3 normalize(f3 v) {
+#ifdef RSD_FAST_NUMERICS  // svao_fast.hip (svao_math.h): the hardware reciprocal square root, 1 ulp
+    float inv = __builtin_amdgcn_rsqf(dot(v, v));
+#else
     float inv = 1.0f / sqrtf(dot(v, v));
+#endif
     return v * inv;
 }
 __device__ __forceinline__ float length(f3 v) { return sqrtf(dot(v, v)); }

@@ -84,6 +84,24 @@ struct Sample {
     float yPdf, yHeight;   // RN(1 / pdf), RN(1 / sphereStart)
 };
 
+// RSD_FAST_NUMERICS (svao_fast.hip, svao_kernels.h): the division helpers below become one multiply by
+// the hardware reciprocal (v_rcp_f32, 1 ulp) and their range tests constant true; the compiler contracts
+// a * b + c into FMAs, '/' and sqrtf lower to v_rcp_f32 / v_sqrt_f32 and float32 denormals flush -- the
+// arithmetic D3D permits the reference's HLSL.  Without it (svao.hip, svao_rt.hip): the exact contract.
+#ifdef RSD_FAST_NUMERICS
+constexpr bool kFastNumerics = true;
+#else
+constexpr bool kFastNumerics = false;
+#endif
+
+#ifdef RSD_FAST_NUMERICS
+__device__ __forceinline__ float div_rcp(float a, float b, float y) { return a * y; }
+__device__ __forceinline__ float rcp_refined(float b) { return __builtin_amdgcn_rcpf(b); }
+__device__ __forceinline__ float div_unscaled(float a, float b, float y1) { return a * y1; }
+__device__ __forceinline__ float div_unscaled_tail(float a, float b, float y1) { return a * y1; }
+__device__ __forceinline__ bool div_unscaled_num_ok(float) { return true; }
+__device__ __forceinline__ bool div_unscaled_den_ok(float) { return true; }
+#else
 // RN(a / b) for b > 0 given y = RN(1 / b), in five operations instead of the IEEE division's
 // eleven (v_div_scale x2, v_rcp, 6 fma/mul, v_div_fmas, v_div_fixup).  q0 = RN(a y) is within
 // 1.5 ulp of a / b; one residual step (r0 = a - b q0 exact by FMA) brings q1 within 1 ulp; then
@@ -134,6 +152,7 @@ __device__ __forceinline__ bool div_unscaled_den_ok(float b) {
     const float m = fabsf(b);
     return m >= 0x1p-20f && m <= 0x1p20f;
 }
+#endif  // RSD_FAST_NUMERICS
 
 // n / pdf for n = 0 or n in (0, 2 * sphereHeight]: max(ss - max(se, oz), 0) (>= ulp(ss) / 2 when
 // non-zero), ss - se (> 0.2 h after the validity test), saturate(x / ss) * (ss - se)
@@ -302,8 +321,12 @@ __device__ __forceinline__ float make_nonzero(float v, float eps) {
 // for D > 0 q < M <=> n < M * D, a product of 25- and 24-bit significands: exact in double.
 // D = 0 gives +inf / NaN in the reference (never <= 0.1): n < 0 is false here as well.
 __device__ __forceinline__ bool ratio_le_tenth(float n, float D) {
+#ifdef RSD_FAST_NUMERICS
+    return n * __builtin_amdgcn_rcpf(D) <= 0.1f;  // the reference's (n / D) <= 0.1 with a 1-ulp '/'
+#else
     constexpr double M = (double)0.1f + 0x1p-28;
     return (double)n < M * (double)D;
+#endif
 }
 
 // ssrAbove = (screenSpaceRadius > ssRadiusCutoff), decided on the squared radius (no sqrt).
@@ -342,7 +365,7 @@ __device__ __forceinline__ bool sample_init(const SvaoArgs& a, float u, float v,
     float zi;  // ALLFAST: the validity test below is one compare against the host bound ratioMin
     if (ALLFAST) {  // the pixel's divisor is in div_unscaled's range (checked with ALLFAST)
         const float num = -(dx * b.normalO.x + dy * b.normalO.y), den = make_nonzero(b.normalO.z, 0.0001f);
-        zi = __ballot(!div_unscaled_num_ok(num)) == 0u ? div_unscaled(num, den, b.nzRcp) : num / den;
+        zi = (kFastNumerics || __ballot(!div_unscaled_num_ok(num)) == 0u) ? div_unscaled(num, den, b.nzRcp) : num / den;
     } else {
         zi = -(dx * b.normalO.x + dy * b.normalO.y) / make_nonzero(b.normalO.z, 0.0001f);
     }
@@ -357,7 +380,7 @@ __device__ __forceinline__ bool sample_init(const SvaoArgs& a, float u, float v,
     // divisors in [2^-20, 2^20].  Exact for |p.x|, |p.y| in [2^-100, 2^70] (|posV| < 2^60 per pixel, the
     // sample offset < radius); a smaller numerator gives |x / den| < 2^-80, and then u = x / den * -0.5 +
     // 0.5 rounds to 0.5 whichever tiny quotient the sequence returns, and su is all that is used of it.
-    if (ALLFAST && __ballot(!(fabsf(ip.z) >= a.pzLo && fabsf(ip.z) <= a.pzHi)) == 0u) {
+    if (ALLFAST && (kFastNumerics || __ballot(!(fabsf(ip.z) >= a.pzLo && fabsf(ip.z) <= a.pzHi)) == 0u)) {
         const float dx2 = a.isx * ip.z, dy2 = a.isy * ip.z;
         const float ndcx = div_unscaled_tail(ip.x, dx2, rcp_refined(dx2));
         const float ndcy = div_unscaled_tail(ip.y, dy2, rcp_refined(dy2));
@@ -533,6 +556,10 @@ inline rsd_status check_common(const rsd_camera* cam, const rsd_vao_data* vao, c
         // Common.slang:51-58 holds sample radii for 8, 16 and 32 directions only
         set_error(std::string(who) + ": NUM_DIRECTIONS must be 8, 16 or 32");
         return RSD_ERR_UNSUPPORTED;
+    }
+    if (p->numerics != RSD_NUMERICS_FAST && p->numerics != RSD_NUMERICS_EXACT) {
+        set_error(std::string(who) + ": numerics must be RSD_NUMERICS_FAST or RSD_NUMERICS_EXACT");
+        return RSD_ERR_INVALID_ARG;
     }
     if (2 * p->guard_band >= W || 2 * p->guard_band >= H) {
         set_error(std::string(who) + ": guard band leaves no visible region");

@@ -83,7 +83,12 @@ class SVAOParams(C.Structure):
     _fields_ = [("num_directions", C.c_uint32), ("sd_samples", C.c_uint32),
                 ("secondary_depth_mode", C.c_uint32), ("ray_interval", C.c_uint32),
                 ("sd_jitter", C.c_uint32), ("guard_band", C.c_uint32), ("dual_ao", C.c_uint32),
-                ("tile_flags", C.c_void_p)]  # ABI v4: busy 16x16 tiles (pass 1 sets, pass 2 consumes)
+                ("tile_flags", C.c_void_p),  # ABI v4: busy 16x16 tiles (pass 1 sets, pass 2 consumes)
+                ("numerics", C.c_uint32)]    # ABI v5: rsd_numerics of pass 1 / pass 2
+
+
+NUMERICS_FAST, NUMERICS_EXACT = 0, 1  # rsd.h rsd_numerics
+NUMERICS = {"fast": NUMERICS_FAST, "exact": NUMERICS_EXACT}
 
 
 class Counters(C.Structure):

@@ -53,6 +53,10 @@ class FrameConfig:
     sd_guard_px: int = 512
     num_directions: int = 8
     dual_ao: bool = False                  # SVAO dualAO (SVAO.cpp:130): ao is RG8Unorm (bright, dark)
+    # arithmetic of the SVAO passes (rsd.h rsd_numerics): "fast" (the product default, AO graded by
+    # BASELINE.md section 4's tolerance) or "exact" (bit-identical to the oracle); the environment's
+    # RSD_NUMERICS sets the default
+    numerics: str = dataclasses.field(default_factory=lambda: os.environ.get("RSD_NUMERICS", "fast"))
     focal_length: float = 21.0
     frame_height: float = 24.0
     near: float = 0.1
@@ -145,8 +149,10 @@ def sd_params(cfg: FrameConfig, sd_guard: int) -> abi.SDParams:
 
 
 def svao_params(cfg: FrameConfig) -> abi.SVAOParams:
+    if cfg.numerics not in abi.NUMERICS:
+        raise ValueError(f"numerics must be one of {sorted(abi.NUMERICS)}, not {cfg.numerics!r}")
     return abi.SVAOParams(cfg.num_directions, cfg.sd_samples, cfg.secondary, int(cfg.ray_interval), int(cfg.jitter),
-                          cfg.guard_band, int(cfg.dual_ao))
+                          cfg.guard_band, int(cfg.dual_ao), None, abi.NUMERICS[cfg.numerics])
 
 
 class Device:
