@@ -369,6 +369,38 @@ rsd_status rsd_svao_pass2_raytraced_band(rsd_scene* scene, const rsd_camera* cam
                                          uint32_t ray_pipeline, uint32_t alpha_test, uint32_t band_index,
                                          uint32_t band_count, rsd_stream stream);
 
+/* --- one whole frame per call (SVAO::execute, SVAO.cpp:192-456) ---------------------
+ * The frame's dispatch sequence on one stream, issued from C++: the interval clear (SVAO.cpp:
+ * 330-341; skipped with RSD_FRAME_INTERVALS_CLEAR when the previous frame's trace on these maps
+ * consumed them) -> "AO 1" -> (StochasticDepth) the SD trace, which consumes the interval maps when
+ * RayInterval is on -> "AO 2"; (Raytraced) "AO 1" -> the Raytraced "AO 2"; (SingleDepth) "AO 1".
+ * The same kernels and bits as the separate calls; one ABI crossing per frame instead of four
+ * (the host issue cost of a frame).
+ * events: NULL or 4 hipEvent_t (each may be NULL) recorded on the stream before "AO 1", before the
+ * SD trace, after the SD trace and after "AO 2" (per-pass timing without host round trips). */
+typedef struct {
+    rsd_scene* scene;               /* StochasticDepth / Raytraced modes */
+    const rsd_camera* cam;
+    const rsd_vao_data* vao;
+    const rsd_svao_params* svao;    /* secondary_depth_mode selects the sequence */
+    const rsd_sd_params* sd;        /* the nested SD pass (StochasticDepth); cull_mode / alpha_test of the
+                                       Raytraced pass */
+    const float* d_depth;           /* linear Z, width x height */
+    const uint16_t* d_normals;      /* 2x8 octahedral view-space normals */
+    uint32_t width, height;
+    uint8_t* d_ao;
+    uint8_t* d_stencil;
+    uint32_t* d_ray_min;            /* sd_w x sd_h (StochasticDepth) */
+    uint32_t* d_ray_max;
+    float* d_sd;                    /* the SD map (StochasticDepth) */
+    uint32_t sd_w, sd_h;
+    uint32_t ray_pipeline;          /* Raytraced mode: SVAO rayPipeline (rsd_svao_pass2_raytraced) */
+} rsd_svao_frame_desc;
+#define RSD_FRAME_INTERVALS_CLEAR 4u  /* the interval maps hold the cleared state: no clear launch */
+#define RSD_FRAME_KEEP_INTERVALS 8u   /* the trace leaves the interval maps as pass 1 wrote them (no consume) */
+/* flags: RSD_FRAME_INTERVALS_CLEAR | RSD_FRAME_KEEP_INTERVALS | RSD_SD_THROUGHPUT */
+rsd_status rsd_svao_frame(const rsd_svao_frame_desc* frame, uint32_t flags, void* const* events, rsd_stream stream);
+
 #ifdef __cplusplus
 }
 #endif

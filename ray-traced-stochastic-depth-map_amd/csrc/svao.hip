@@ -130,6 +130,32 @@ rsd_status snap_tables(const rsd_vao_data& vd, const float** u, const float** v)
 
 using namespace rsd;
 
+namespace {
+// fill_consts of (VAOData, NUM_DIRECTIONS), cached per host thread: the ~50 double sin / cos and the
+// ssRadiusCutoff search are host work every pass-1 / pass-2 call would otherwise repeat per frame
+void cached_consts(SvaoConsts& k, const rsd_vao_data& d, uint32_t nd) {
+    struct Entry {
+        rsd_vao_data d;
+        uint32_t nd;
+        SvaoConsts k;
+    };
+    thread_local Entry cache[4];
+    thread_local int used = 0, next = 0;
+    for (int i = 0; i < used; ++i)
+        if (cache[i].nd == nd && std::memcmp(&cache[i].d, &d, sizeof(d)) == 0) {
+            k = cache[i].k;
+            return;
+        }
+    fill_consts(k, d, nd);
+    Entry& e = cache[next];
+    e.d = d;
+    e.nd = nd;
+    e.k = k;
+    next = (next + 1) % 4;
+    used = used < 4 ? used + 1 : 4;
+}
+}  // namespace
+
 extern "C" uint32_t rsd_svao_tile_count(uint32_t width, uint32_t height, uint32_t guard_band) {
     if (2 * guard_band >= width || 2 * guard_band >= height) return 0u;
     return tiles_x(width, guard_band) * tiles_y(height, guard_band);
@@ -178,7 +204,7 @@ rsd_status pass1_impl(const rsd_camera* cam, const rsd_vao_data* vao, const rsd_
     SvaoArgs a{};
     a.cam = *cam;
     a.d = *vao;
-    fill_consts(a.k, a.d, p->num_directions);
+    cached_consts(a.k, a.d, p->num_directions);
     {
         rsd_status ts = snap_tables(a.d, &a.snapU, &a.snapV);
         if (ts == RSD_OK) ts = normal_lut(&a.nlut);
@@ -273,7 +299,7 @@ rsd_status pass2_impl(const rsd_camera* cam, const rsd_vao_data* vao, const rsd_
     SvaoArgs a{};
     a.cam = *cam;
     a.d = *vao;
-    fill_consts(a.k, a.d, p->num_directions);
+    cached_consts(a.k, a.d, p->num_directions);
     {
         rsd_status ts = snap_tables(a.d, &a.snapU, &a.snapV);
         if (ts == RSD_OK) ts = normal_lut(&a.nlut);

@@ -127,7 +127,11 @@ __global__ void __launch_bounds__(256) svao_pass1_kernel(SvaoArgs a) {
         // busy 16x16 tiles for pass 2: a wave is 4 thread rows of this 16x16 group = one tile row
         // and two tiles (threadIdx.x < 8: the left one, the 2x2 interleave spreads 16 threads over
         // 32 pixels); one byte store per busy tile and wave
-        const uint64_t mL = __ballot(st != 0u && threadIdx.x < 8u), mR = __ballot(st != 0u && threadIdx.x >= 8u);
+        // only visible pixels vote: the padded dispatch (roundup32 of the visible size) also runs up to 31
+        // columns / rows beyond it, whose tile index would alias the next row's first tile (or lie past
+        // the last flag byte) when the visible width is not a multiple of 16
+        const bool vote = st != 0u && ox < (uint32_t)a.W - 2u * a.guard && oy < (uint32_t)a.H - 2u * a.guard;
+        const uint64_t mL = __ballot(vote && threadIdx.x < 8u), mR = __ballot(vote && threadIdx.x >= 8u);
         const uint32_t lane = __lane_id();
         if ((lane == 0u && mL) || (lane == 8u && mR)) a.tileFlags[(oy / kTileEdge) * a.tilesX + ox / kTileEdge] = 1u;
     }

@@ -91,6 +91,18 @@ NUMERICS_FAST, NUMERICS_EXACT = 0, 1  # rsd.h rsd_numerics
 NUMERICS = {"fast": NUMERICS_FAST, "exact": NUMERICS_EXACT}
 
 
+class FrameDesc(C.Structure):  # rsd_svao_frame_desc
+    _fields_ = [("scene", C.c_void_p), ("cam", C.c_void_p), ("vao", C.c_void_p), ("svao", C.c_void_p),
+                ("sd", C.c_void_p), ("d_depth", C.c_void_p), ("d_normals", C.c_void_p), ("width", C.c_uint32),
+                ("height", C.c_uint32), ("d_ao", C.c_void_p), ("d_stencil", C.c_void_p), ("d_ray_min", C.c_void_p),
+                ("d_ray_max", C.c_void_p), ("d_sd", C.c_void_p), ("sd_w", C.c_uint32), ("sd_h", C.c_uint32),
+                ("ray_pipeline", C.c_uint32)]
+
+
+FRAME_INTERVALS_CLEAR = 4  # rsd.h RSD_FRAME_INTERVALS_CLEAR
+FRAME_KEEP_INTERVALS = 8   # rsd.h RSD_FRAME_KEEP_INTERVALS
+
+
 class Counters(C.Structure):
     _fields_ = [("rays_dispatched", C.c_uint64), ("rays_active", C.c_uint64), ("nodes_visited", C.c_uint64),
                 ("tris_tested", C.c_uint64), ("hits_delivered", C.c_uint64), ("max_nodes_per_ray", C.c_uint64),
@@ -117,7 +129,7 @@ EXPORTS = ["rsd_abi_version", "rsd_svao_tile_count", "rsd_last_error", "rsd_devi
            "rsd_sd_trace_band", "rsd_svao_pass1_band", "rsd_svao_pass2_band", "rsd_gbuffer_raster",
            "rsd_linearize_depth", "rsd_compress_normals", "rsd_svao_pass2_raytraced", "rsd_svao_pass2_raytraced_band",
            "rsd_scene_upload_alpha", "rsd_ray_cone_spread", "rsd_sd_trace_band_ex", "rsd_scene_export_bvh",
-           "rsd_bvh_build", "rsd_svao_pass1_rows", "rsd_svao_pass2_rows", "rsd_sd_trace_rows"]
+           "rsd_bvh_build", "rsd_svao_pass1_rows", "rsd_svao_pass2_rows", "rsd_sd_trace_rows", "rsd_svao_frame"]
 
 SD_CONSUME_INTERVALS = 1
 SD_THROUGHPUT = 2  # frames in flight: the work-efficient traversal (rsd.h RSD_SD_THROUGHPUT)
@@ -210,6 +222,8 @@ def lib():
         L.rsd_sd_trace_rows.restype = st
         L.rsd_sd_trace_rows.argtypes = [vp, C.POINTER(Camera), C.POINTER(SDParams), vp, u32, u32, vp, vp, vp, u32,
                                         u32, u32, u32, u32, C.POINTER(Counters), vp]
+        L.rsd_svao_frame.restype = st
+        L.rsd_svao_frame.argtypes = [C.POINTER(FrameDesc), u32, vp, vp]
         L.rsd_svao_pass2_raytraced.restype = st
         L.rsd_svao_pass2_raytraced.argtypes = [vp, C.POINTER(Camera), C.POINTER(VAOData), C.POINTER(SVAOParams), vp, vp,
                                                u32, u32, vp, vp, u32, u32, u32, vp]

@@ -288,6 +288,7 @@ class Renderer:
         t = self.torch
         r = copy.copy(self)
         r._slot = True
+        r._desc_key = None  # the slot's own buffers
         r.ao = t.zeros_like(self.ao)
         r.stencil = t.zeros_like(self.stencil)
         r.ray_minmax = t.empty_like(self.ray_minmax)
@@ -388,17 +389,43 @@ class Renderer:
                                                           int(self.cfg.alpha_test), band[0], band[1], self.stream),
                   "rsd_svao_pass2_raytraced_band")
 
+    def _frame_desc(self):
+        """The rsd_svao_frame_desc of this renderer's buffers (cached; rebuilt when the camera or the
+        parameter structs are replaced, e.g. by set_pose)."""
+        key = (id(self.cam), id(self.svp), id(self.sdp), id(self.vao))
+        if getattr(self, "_desc_key", None) != key:
+            cfg = self.cfg
+            p = lambda t: t.data_ptr()  # noqa: E731
+            self._desc = abi.FrameDesc(self.gscene.h, C.addressof(self.cam), C.addressof(self.vao),
+                                       C.addressof(self.svp), C.addressof(self.sdp), p(self.depth), p(self.normals),
+                                       cfg.fb_w, cfg.fb_h, p(self.ao), p(self.stencil), p(self.ray_min),
+                                       p(self.ray_max), p(self.sd), self.sd_w, self.sd_h, int(cfg.ray_pipeline))
+            self._desc_key = key
+            self._events = (C.c_void_p * 4)()
+        return self._desc
+
+    def svao_frame(self, intervals_clear: bool = False, keep_intervals: bool = False, throughput: bool = False,
+                   events=None):
+        """One AO frame in ONE librsd call (rsd_svao_frame: clear -> "AO 1" -> SD trace -> "AO 2" issued
+        from C++ on the current stream).  intervals_clear: the interval maps are known to be cleared
+        (the previous trace consumed them), so no clear launch; keep_intervals: the trace does not
+        consume them; events: None or 4 TimingEvents / None recorded before pass 1, before and after
+        the SD trace and after pass 2."""
+        d = self._frame_desc()
+        flags = ((abi.FRAME_INTERVALS_CLEAR if intervals_clear else 0) |
+                 (abi.FRAME_KEEP_INTERVALS if keep_intervals else 0) | (abi.SD_THROUGHPUT if throughput else 0))
+        ev = None
+        if events is not None:
+            ev = self._events
+            for i, e in enumerate(events):
+                ev[i] = e.h.value if e is not None else None
+        abi.check(abi.lib().rsd_svao_frame(C.byref(d), flags, ev, self.stream), "rsd_svao_frame")
+
     def frame(self):
         """One AO frame: the span of the reference's "AO 1" + "AORefine" profile scopes
-        (SVAO.cpp:327-455) for the configured secondary depth mode."""
-        if self.cfg.secondary == abi.DEPTH_STOCHASTIC:
-            self.clear_intervals()
-        self.pass1()
-        if self.cfg.secondary == abi.DEPTH_STOCHASTIC:
-            self.sd_trace()
-            self.pass2()
-        elif self.cfg.secondary == abi.DEPTH_RAYTRACED:
-            self.pass2_raytraced()
+        (SVAO.cpp:327-455) for the configured secondary depth mode, in one librsd call; the interval
+        maps keep what pass 1 wrote (tests read them)."""
+        self.svao_frame(keep_intervals=True)
 
     def numpy(self):
         t = self.torch

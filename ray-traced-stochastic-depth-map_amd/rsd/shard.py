@@ -91,6 +91,8 @@ class BandFrame:
     def frame(self, sd_events=None):
         """One AO frame.  sd_events: optional (start, end) torch.cuda.Event pair recorded
         around this rank's SD trace (per-kernel timing in bench.py)."""
+        if self.world == 1 and _one_call_frame(self, sd_events):
+            return
         self.front()
         self.back(sd_events)
 
@@ -134,6 +136,21 @@ class BandFrame:
         b.pass2(band=band)
         if self.world > 1:
             self._gather_rows(b.ao, self.ao_rows, self.ao_send, self.ao_recv, 0, self.ao_unpack)
+
+
+def _one_call_frame(fr, sd_events) -> bool:
+    """The 1-rank frame of a BandFrame / HaloFrame as ONE librsd call (rsd_svao_frame: the same
+    kernels and bits as the per-pass calls, issued from C++).  False when the backend has no such
+    entry (the CPU oracle backend of the tests) or the SD events are not HIP timing events."""
+    b = fr.b
+    if not hasattr(b, "svao_frame") or (sd_events and not all(hasattr(e, "h") for e in sd_events)):
+        return False
+    consume = getattr(b, "can_consume_intervals", False) and bool(b.cfg.ray_interval)
+    ev = [None, sd_events[0], sd_events[1], None] if sd_events else None
+    b.svao_frame(intervals_clear=consume and fr._intervals_clear, keep_intervals=not consume,
+                 throughput=bool(fr.trace_kw), events=ev)
+    fr._intervals_clear = consume
+    return True
 
 
 def halo_px(cfg, max_radius_px: float = 512.0) -> int:
@@ -353,6 +370,10 @@ class HaloFrame:
 
     def frame(self, sd_events=None):
         b, me, world = self.b, self.rank, self.world
+        if world == 1 and _one_call_frame(self, sd_events):
+            self.splits.append(tuple(self.gb))
+            self.frames += 1
+            return
         if self._next_gb is not None and self._next_gb != self.gb:
             self.gb = self._next_gb
             self._plan()

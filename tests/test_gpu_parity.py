@@ -503,12 +503,14 @@ def test_dual_ao_raytraced_parity(device, oracle):
     assert np.array_equal(g["ao"], ao)
 
 
-@pytest.mark.parametrize("nd", [8, 16])
-def test_busy_tile_flags(device, oracle, torch_dev, nd):
+@pytest.mark.parametrize("nd,visible", [(8, (224, 128)), (16, (224, 128)), (8, (200, 120)), (8, (1000, 72))])
+def test_busy_tile_flags(device, oracle, torch_dev, nd, visible):
     """rsd_svao_params.tile_flags (ABI v4): pass 1 flags exactly the 16x16 tiles of the visible region
-    that hold a stencilled pixel; pass 2 visits only those and clears them; the AO equals a frame
-    without flags (every tile visited) and the oracle."""
-    cfg = small_frame_config(visible=(224, 128), guard=32, divisor=2)
+    that hold a stencilled VISIBLE pixel; pass 2 visits only those and clears them; the AO equals a
+    frame without flags (every tile visited) and the oracle.  Widths 200 and 1000 (width % 32 in
+    [1, 16]): pass 1's padded dispatch runs 16 columns right of the last tile, whose pixels must not
+    vote (they would flag the next row's first tile, or write past the buffer on the last row)."""
+    cfg = small_frame_config(visible=visible, guard=32, divisor=2)
     cfg.num_directions = nd
     r, osc = renderer("arcade_tiny", cfg, device, oracle)
     r.gbuffer()
@@ -519,7 +521,8 @@ def test_busy_tile_flags(device, oracle, torch_dev, nd):
     g_, vw, vh = cfg.guard_band, cfg.visible_w, cfg.visible_h
     tx, ty = (vw + 15) // 16, (vh + 31) // 32 * 32 // 16
     assert flags.size == tx * ty
-    st = g["stencil"][g_:g_ + ty * 16, g_:g_ + vw]
+    st = np.zeros((ty * 16, tx * 16), g["stencil"].dtype)
+    st[:vh, :vw] = g["stencil"][g_:g_ + vh, g_:g_ + vw]  # visible pixels only
     want = np.zeros((ty, tx), np.uint8)
     for j in range(ty):
         for i in range(tx):

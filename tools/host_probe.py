@@ -47,7 +47,8 @@ for n in (frames, 10 * frames):
     out[f"issue_us_per_frame_{n}"] = round((t1 - t0) / n * 1e6, 1)
     out[f"wall_us_per_frame_{n}"] = round((t2 - t0) / n * 1e6, 1)
 # per-call host cost (the GPU queue kept short: synchronize between batches)
-calls = {"pass1": r.pass1, "sd_trace": lambda: r.sd_trace(throughput=True), "pass2": r.pass2,
+calls = {"svao_frame": lambda: r.svao_frame(throughput=True), "pass1": r.pass1,
+         "sd_trace": lambda: r.sd_trace(throughput=True), "pass2": r.pass2,
          "stream_ctx": lambda: torch.cuda.stream(streams[1]).__enter__(), "event_record": lambda: torch.cuda.Event().record()}
 for k, fn in calls.items():
     ts = []
