@@ -84,6 +84,9 @@ def parse():
     ap.add_argument("--pmc-csv", nargs="*", default=None,
                     help="rocprofv3 --pmc counter_collection.csv file(s) with FETCH_SIZE / WRITE_SIZE for "
                          "roofline.traffic (default: the committed passes of the default config)")
+    ap.add_argument("--hit-order-record", type=int, default=1,
+                    help="1: add the hit_order_traversal sub-record (the latency region again with the DXR-like "
+                         "traversal-order any-hit stream, rsd_hit_order TRAVERSAL); 0: skip it")
     ap.add_argument("--timing-events", choices=("hip", "torch", "off"), default="hip",
                     help="per-kernel timing events: hip = fence-free timing events (rsd.timing, default); "
                          "torch = torch.cuda.Event (a system-scope fence per record); off = none in the "
@@ -284,6 +287,7 @@ def main():
     alg_bytes = rays * (16 + 8 + 4 * N) + 128 * nodes_seq + 48 * tris_seq + entry_bytes
     achieved = alg_bytes / (seq_sd_ms * 1e-3) / 1e9
     kernels_seq = abi.WALK_KERNELS[walk_seq]
+    lat = latency_floor(cnt_seq, seq_sd_ms)
     pmc = args.pmc_csv
     if pmc is None and args.config == DEFAULT_CONFIG and not poses and not args.scene_file:
         for d in PROFILE_DIRS:
@@ -294,6 +298,14 @@ def main():
     pmc = [p for p in (pmc or []) if Path(p).exists()]
     traffic = pmc_traffic(pmc, kernels_seq)
     valu_csv = next((d / "pmc_sq_valu.csv" for d in PROFILE_DIRS if (d / "pmc_sq_valu.csv").exists()), None)
+
+    # DXR-like any-hit order (rsd_hit_order TRAVERSAL): the same latency region with
+    # the traversal-order hit stream -- the mode closest to the reference's DXR semantics
+    # (Common.slangh:137-151: the reservoir samples among the hits in traversal order)
+    hit_trav = None
+    if world == 1 and args.hit_order_record:
+        hit_trav = hit_order_record(r, HaloFrame, new_ev, min(args.steps, 50), min(args.warmup, 5), pose,
+                                    rays, rays_active)
 
     if rank != 0:
         if dist:
@@ -357,13 +369,15 @@ def main():
                      "note": "achieved = SURVEY 8(d) algorithmic bytes of one trace / its HIP-event duration in "
                              "the latency region; traffic = FETCH_SIZE + WRITE_SIZE of the same kernels "
                              "(per launch, committed rocprofv3 --pmc passes)",
-                     "traffic_source": ", ".join(rel(p) for p in pmc) or None},
+                     "traffic_source": ", ".join(rel(p) for p in pmc) or None,
+                     **lat},
         # the frame's largest kernel is pass 1, bound by VALU issue rather than HBM
         "pass1_roofline": pmc_valu(valu_csv, "svao_pass1_kernel") if valu_csv and args.config == DEFAULT_CONFIG and not args.scene_file
         else None,
         "exchange_bytes_per_frame": dict(seq.bytes_per_frame(), dense_halo_equivalent=seq.dense_bytes_per_frame(),
                                          final_split_groups=list(seq.gb))
         if shard == "band" and world > 1 else None,
+        "hit_order_traversal": hit_trav,
         "bvh_build_s": round(bvh_build_s, 3),
         "bvh_build_threads": int(r.gscene.info.build_threads),
         "cpu_baseline": cpu,
@@ -371,6 +385,70 @@ def main():
     print(json.dumps(line))
     if dist:
         dist.destroy_process_group()
+
+
+def hit_order_record(r, frame_cls, new_ev, steps, warmup, pose, rays, rays_active):
+    """The latency region with the traversal-order hit stream (rsd.h RSD_HIT_ORDER_TRAVERSAL: a
+    depth-first walk of the 4-wide BVH delivering each triangle once in leaf order, a commit shrinking
+    TMax -- DXR's any-hit semantics, StochasticDepthMapRT.rt.slang:83-88): SD-trace time, dispatched /
+    active Mrays/s and the AO span over `steps` frames, one in flight."""
+    import numpy as np
+    import torch
+
+    from rsd import abi
+    keep = r.sdp
+    sdp = abi.SDParams.from_buffer_copy(keep)
+    sdp.hit_order = abi.HIT_ORDER_TRAVERSAL
+    r.sdp = sdp
+    try:
+        fr = frame_cls(r)
+        ev_sd = [(new_ev(), new_ev()) for _ in range(steps)]
+        ev_ao = [(new_ev(), new_ev()) for _ in range(steps)]
+        for i in range(warmup):
+            pose(r, i)
+            fr.frame()
+        for i in range(steps):
+            pose(r, i)
+            ev_ao[i][0].record()
+            fr.frame(sd_events=ev_sd[i])
+            ev_ao[i][1].record()
+        torch.cuda.synchronize()
+        sd_ms = float(np.mean([a.elapsed_time(b) for a, b in ev_sd]))
+        ao_ms = float(np.mean([a.elapsed_time(b) for a, b in ev_ao]))
+    finally:
+        r.sdp = keep
+    return {"frames": steps, "walk": "ordered", "sd_kernel_ms": round(sd_ms, 4),
+            "mrays_per_s": round(rays / (sd_ms * 1e-3) / 1e6, 1),
+            "active_mrays_per_s": round(rays_active / (sd_ms * 1e-3) / 1e6, 2),
+            "ao_span_ms": round(ao_ms, 4), "ao_frames_per_s": round(1e3 / ao_ms, 1),
+            "note": "latency region with rsd_sd_params.hit_order = RSD_HIT_ORDER_TRAVERSAL (DXR-like any-hit "
+                    "order, sd_trace_ordered_kernel); the headline value keeps the canonical order"}
+
+
+def latency_floor(cnts, trace_ms):
+    """Latency roofline of the SD walk: the slowest ray is a chain of
+    max_steps_per_ray dependent row-steps (LDS pop -> node / leaf fetch -> box or triangle tests ->
+    row merge -> push); its floor is max_steps x the mean step time measured by the instrumented
+    walk under the same load (rsd_counters.step_*_clocks over row_steps, s_memtime converted with
+    the launch's measured clock).  latency_frac = floor / the trace's HIP-event duration (setup +
+    walk): near 1 means the trace lasts as long as its slowest ray's dependency chain."""
+    import numpy as np
+    c = [x for x in cnts if x.row_steps and x.shader_clock_mhz > 0]
+    if not c:
+        return {"latency_floor_us": None}
+    mhz = float(np.mean([x.shader_clock_mhz for x in c]))
+    steps = sum(x.row_steps for x in c)
+    fetch = sum(x.step_fetch_clocks for x in c) / steps / mhz
+    comp = sum(x.step_compute_clocks for x in c) / steps / mhz
+    pool = sum(x.step_pool_clocks for x in c) / steps / mhz
+    ms = max(x.max_steps_per_ray for x in c)
+    floor = ms * (fetch + comp + pool)
+    return {"latency_floor_us": round(floor, 2), "latency_frac": round(floor / (trace_ms * 1e3), 3),
+            "latency_floor_fetch_only_us": round(ms * fetch, 2),
+            "step_us": {"fetch": round(fetch, 3), "tests_merge": round(comp, 3), "pool": round(pool, 3)},
+            "max_steps_per_ray": int(ms), "shader_clock_mhz": round(mhz, 1),
+            "latency_note": "floor = max_steps_per_ray x mean row-step time of the instrumented walk "
+                            "(fetch wait + tests/merge + LDS pool); latency_frac = floor / trace duration"}
 
 
 def pmc_traffic(csv_paths, kernel_substrs):

@@ -200,6 +200,16 @@ typedef struct {
     uint64_t walk;              /* traversal walk of the trace: RSD_WALK_* */
     uint64_t entry_lookups;     /* segment entry-grid lookups (one 16-B hash slot each, first probe) */
     uint64_t entry_items;       /* frontier items tested by the setup kernel (32 B each) */
+    /* ABI v5, the instrumented row walk (RSD_WALK_FUSED; 0 for the other walks): per row-step clock
+     * sums of lane 0 of every row -- the step's dependent fetch (the instrumented build waits for it),
+     * its box / triangle tests and merges, its LDS pool pops and pushes -- and the steps walked; the
+     * s_memtime rate of the launch (MHz) converts them to time.  Latency roofline of the walk (bench.py
+     * roofline.latency_floor_us): max_steps_per_ray x the mean step time. */
+    uint64_t step_fetch_clocks;
+    uint64_t step_compute_clocks;
+    uint64_t step_pool_clocks;
+    uint64_t row_steps;
+    double shader_clock_mhz;
 } rsd_counters;
 /* rsd_counters.walk: which kernels an rsd_sd_trace launched (besides sd_setup_kernel) */
 #define RSD_WALK_QUAD 0u   /* sd_trace_queue_kernel: depth-first, 4 lanes per ray */

@@ -1250,6 +1250,15 @@ __global__ void __launch_bounds__(kBlock) sd_trace_row_kernel(SDArgs a, const fl
 
     unsigned long long tFetch = 0, tStep = 0, tResolve = 0, nStep = 0, nLoop = 0, tS0 = 0, tS1 = 0;
     unsigned long long tMem = 0, tComp = 0, tPool = 0, tMark = 0;  // step split (instrumented build)
+    // clock calibration (instrumented build): the first wave's span in s_memtime ticks and in the
+    // 100 MHz s_memrealtime ticks converts the step clocks to microseconds (rsd_counters.shader_clock_mhz)
+    unsigned long long cal0 = 0, calR0 = 0;
+    if constexpr (CNT) {
+        if (blockIdx.x == 0) {
+            cal0 = __builtin_amdgcn_s_memtime();
+            calR0 = __builtin_amdgcn_s_memrealtime();
+        }
+    }
     while (__ballot(phase != kExit) != 0ull) {
         if constexpr (CNT) { tS0 = __builtin_amdgcn_s_memtime(); nLoop += lane == 0; }
         const bool fetching = phase == kFetch;
@@ -1548,6 +1557,11 @@ __global__ void __launch_bounds__(kBlock) sd_trace_row_kernel(SDArgs a, const fl
         atomicAdd(&a.counters[16], tMem);
         atomicAdd(&a.counters[17], tComp);
         atomicAdd(&a.counters[18], tPool);
+        if (blockIdx.x == 0 && lane == 0) {
+            const unsigned long long cal1 = __builtin_amdgcn_s_memtime(), calR1 = __builtin_amdgcn_s_memrealtime();
+            atomicMax(&a.counters[21], cal1 - cal0);
+            atomicMax(&a.counters[22], calR1 - calR0);
+        }
     }
 }
 
@@ -2154,6 +2168,12 @@ rsd_status sd_trace_impl(rsd_scene* scene, const rsd_camera* cam, const rsd_sd_p
         counters->walk = (uint64_t)walk;
         counters->entry_lookups = h[19];
         counters->entry_items = h[20];
+        // row walk (instrumented): per-step clock sums and the clock of the instrumented launch
+        counters->step_fetch_clocks = h[16];
+        counters->step_compute_clocks = h[17];
+        counters->step_pool_clocks = h[18];
+        counters->row_steps = h[14];
+        counters->shader_clock_mhz = h[22] ? (double)h[21] / ((double)h[22] * 0.01) : 0.0;  // 100 MHz realtime
         if (const char* dbg = std::getenv("RSD_TRACE_PHASES"))
             if (*dbg) std::fprintf(stderr, "[rsd] row walk phase clocks: fetch %llu step %llu resolve %llu steps %llu loops %llu"
                                    " | step split: mem %llu compute %llu pool %llu\n",

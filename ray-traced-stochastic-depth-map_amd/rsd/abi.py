@@ -108,7 +108,8 @@ class Counters(C.Structure):
                 ("tris_tested", C.c_uint64), ("hits_delivered", C.c_uint64), ("max_nodes_per_ray", C.c_uint64),
                 ("max_steps_per_ray", C.c_uint64), ("sum_ray_clocks", C.c_uint64), ("max_ray_clocks", C.c_uint64),
                 ("leaves_visited", C.c_uint64), ("walk", C.c_uint64), ("entry_lookups", C.c_uint64),
-                ("entry_items", C.c_uint64)]
+                ("entry_items", C.c_uint64), ("step_fetch_clocks", C.c_uint64), ("step_compute_clocks", C.c_uint64),
+                ("step_pool_clocks", C.c_uint64), ("row_steps", C.c_uint64), ("shader_clock_mhz", C.c_double)]
 
 
 WALK_QUAD, WALK_FUSED, WALK_SPLIT, WALK_ORDERED, WALK_RASTER = 0, 1, 2, 3, 4
