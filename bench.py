@@ -250,11 +250,31 @@ def main():
     thr_ev = args.timing_events != "off"
     ev_thr = mk_ev(args.steps) if thr_ev else None
 
+    # N > 1 band frames: back() of frame i is issued after front() of the next F - 1 frames, so the
+    # host reads frame i's exchange counts once they are long complete (HaloFrame: no host wait
+    # drains the frames in flight); 1 rank: one rsd_svao_frame call per frame
+    lag = F - 1 if shard == "band" and world > 1 else 0
+
     def run_thr(n, timed_ev=thr_ev):
+        pending = []
+
+        def finish(j):
+            with torch.cuda.stream(streams[j % F]):
+                slots[j % F].back(sd_events=ev_thr[j] if timed_ev else None)
+
         for i in range(n):
             with torch.cuda.stream(streams[i % F]):
                 pose(slots[i % F].b, i)
-                slots[i % F].frame(sd_events=ev_thr[i] if timed_ev else None)
+                if lag:
+                    slots[i % F].front()
+                else:
+                    slots[i % F].frame(sd_events=ev_thr[i] if timed_ev else None)
+            if lag:
+                pending.append(i)
+                if len(pending) > lag:
+                    finish(pending.pop(0))
+        while pending:
+            finish(pending.pop(0))
 
     run_thr(args.warmup, timed_ev=False)
     wall_thr = timed(run_thr, args.steps)

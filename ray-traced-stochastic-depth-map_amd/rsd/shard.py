@@ -184,42 +184,167 @@ def halo_px(cfg, max_radius_px: float = 512.0) -> int:
 FLT_MAX_BITS = 0x7F7FFFFF  # asuint(FLT_MAX): a cleared rayMin (SVAO.cpp:339)
 
 
+class DistComm:
+    """HaloFrame's collectives over torch.distributed: RCCL under backend "nccl" (one GPU per rank;
+    point-to-point send / recv = ncclSend / ncclRecv, stream-ordered, no host wait), gloo for the CPU
+    rehearsals (and several ranks sharing one GPU, staged through host copies)."""
+
+    def __init__(self, pg=None):
+        import torch.distributed as dist
+        self.dist, self.pg = dist, pg
+        self.nccl = dist.get_backend(pg) == "nccl"
+
+    def all_gather(self, out, inp):
+        """out [world, *inp.shape] <- every rank's inp."""
+        if self.nccl:
+            self.dist.all_gather_into_tensor(out.view(-1), inp.reshape(-1), group=self.pg)
+        else:
+            self.dist.all_gather(list(out.unbind(0)), inp.contiguous(), group=self.pg)
+
+    def exchange(self, sends, recvs):
+        """Point-to-point: sends {peer: tensor}, recvs {peer: tensor} (sizes agreed beforehand)."""
+        sends = {k: t for k, t in sends.items() if t.numel()}
+        recvs = {k: t for k, t in recvs.items() if t.numel()}
+        staged = not self.nccl and any(t.is_cuda for t in list(sends.values()) + list(recvs.values()))
+        if staged:  # gloo rehearsal with device tensors (several ranks on one GPU): via host copies
+            sends = {k: t.cpu() for k, t in sends.items()}
+            recvs_dev, recvs = recvs, {k: torch.empty(t.shape, dtype=t.dtype) for k, t in recvs.items()}
+        ops = [self.dist.P2POp(self.dist.isend, t.contiguous(), k, group=self.pg) for k, t in sends.items()]
+        ops += [self.dist.P2POp(self.dist.irecv, t, k, group=self.pg) for k, t in recvs.items()]
+        if ops:
+            for w in self.dist.batch_isend_irecv(ops):
+                w.wait()  # NCCL: the current stream waits for the transfer (no host wait)
+        if staged:
+            for k, t in recvs.items():
+                recvs_dev[k].copy_(t)
+
+
+class LocalHub:
+    """Rendezvous of LocalComm ranks: `world` host threads of one process, one HIP stream each."""
+
+    def __init__(self, world: int):
+        import threading
+        self.world = world
+        self.cv = threading.Condition()
+        self.posts = {}
+
+
+class LocalComm:
+    """HaloFrame's collectives between host threads of one process on one GPU, with the semantics of
+    stream-ordered RCCL and no host synchronisation: a rank posts its tensors with an event recorded
+    on its stream; every reader makes ITS stream wait for that event and copies (device to device),
+    then posts a done event that the writer's stream waits for before it may touch the tensors
+    again.  The threads only rendezvous on Python conditions; the GPU work stays asynchronous.  A
+    rehearsal device for the sync-free N > 1 frame (tests/test_gpu_sharding.py)."""
+
+    def __init__(self, hub: LocalHub, rank: int):
+        self.hub, self.rank, self.seq = hub, rank, 0
+
+    def _post(self, key, value):
+        with self.hub.cv:
+            self.hub.posts.setdefault(key, {})[self.rank] = value
+            self.hub.cv.notify_all()
+
+    def _wait(self, key, ranks):
+        with self.hub.cv:
+            self.hub.cv.wait_for(lambda: all(r in self.hub.posts.get(key, {}) for r in ranks), timeout=120)
+            got = dict(self.hub.posts.get(key, {}))
+        if not all(r in got for r in ranks):
+            raise RuntimeError(f"LocalComm: rank {self.rank} timed out in {key}")
+        return got
+
+    def _event(self):
+        e = torch.cuda.Event()
+        e.record(torch.cuda.current_stream())
+        return e
+
+    def _finish(self, key, readers):
+        """After reading: post my done event, then wait (on my stream) for the readers of my tensors."""
+        self._post(("done",) + key, self._event())
+        done = self._wait(("done",) + key, readers)
+        st = torch.cuda.current_stream()
+        for r in readers:
+            if r != self.rank:
+                st.wait_event(done[r])
+
+    def all_gather(self, out, inp):
+        key = ("ag", self.seq)
+        self.seq += 1
+        world = range(self.hub.world)
+        self._post(key, (inp, self._event()))
+        got = self._wait(key, world)
+        st = torch.cuda.current_stream()
+        for k in world:
+            t, e = got[k]
+            if k != self.rank:
+                st.wait_event(e)
+            out[k].copy_(t.view(out[k].shape))
+        self._finish(key, world)
+
+    def exchange(self, sends, recvs):
+        key = ("x", self.seq)
+        self.seq += 1
+        world = range(self.hub.world)
+        self._post(key, ({k: t for k, t in sends.items()}, self._event()))
+        got = self._wait(key, world)
+        st = torch.cuda.current_stream()
+        for k, t in recvs.items():
+            src, e = got[k]
+            if t.numel():
+                st.wait_event(e)
+                t.copy_(src[self.rank].view(t.shape))
+        self._finish(key, world)
+
+
 class HaloFrame:
-    """One AO frame split into CONTIGUOUS screen bands with SPARSE halo exchanges (SURVEY 8(e) v3).
+    """One AO frame split into CONTIGUOUS screen bands with SPARSE halo exchanges (SURVEY 8(e) v4).
 
     Rank r of B owns the visible rows of its 32-row groups [g_r, g_{r+1}) and the SD rows under
-    them (8-row aligned).  Per frame:
+    them (8-row aligned).  A frame is front() then back():
 
-      1. pass 1 of its own rows (rsd_svao_pass1_rows).  Its interval atomics land on SD texels
-         within `halo` rows of its band (the window W_r): exactly the texels its pass 2 will read
-         (pass 1 and pass 2 place a refined direction's sample on the same SD texel, Common.slang:
-         164-168; an atomic always lowers rayMin below asuint(FLT_MAX) or sets rayMax);
-      2. sparse interval halo: the TOUCHED texels of W_r inside band k (rayMin != asuint(FLT_MAX)
-         or rayMax != 0) go to rank k as (texel index, rayMin, rayMax) triples -- one all-gather of
-         the send counts (and of the previous frame's compute time) sizes the point-to-point
-         transfers; rank k merges them with scatter MIN / MAX (exact on the non-negative float
-         bit patterns) and holds the exact 1-GPU union for its SD rows;
-      3. SD trace of its own SD rows (rsd_sd_trace_rows; consume resets the whole map);
-      4. sparse SD halo: rank k returns the N depths of exactly the texels r sent it in step 2 (k
-         already holds r's index list, so the reply carries values only);
-      5. pass 2 of its own rows (rsd_svao_pass2_rows) and an all-gather of the AO bands.
+      front  1. pass 1 of its own rows (rsd_svao_pass1_rows).  Its interval atomics land on SD texels
+                within `halo` rows of its band (the window W_r): exactly the texels its pass 2 will
+                read (pass 1 and pass 2 place a refined direction's sample on the same SD texel,
+                Common.slang:164-168; an atomic always lowers rayMin below asuint(FLT_MAX) or sets
+                rayMax);
+             2. ON THE DEVICE: the TOUCHED texels of W_r inside each band k (rayMin != asuint(FLT_MAX)
+                or rayMax != 0) are compacted into a fixed-capacity buffer of (texel index, rayMin,
+                rayMax) int32 triples (cumulative-sum positions, one scatter; the capacity is the
+                candidate region, so it never overflows), and their counts -- with the compute time
+                of this rank's previous frame -- are all-gathered as a device tensor, then copied to
+                pinned host memory without waiting (one event marks the copy).
+      back   3. the host reads the counts once that event has completed -- with frames in flight
+                (bench.py issues back() of frame i after front() of the next frames) it completed
+                long before, so the GPU never drains -- and sizes the point-to-point transfers of the
+                triples' prefixes; rank k merges them with scatter MIN / MAX (exact on the
+                non-negative float bit patterns) and holds the exact 1-GPU union for its SD rows;
+             4. SD trace of its own SD rows (rsd_sd_trace_rows; consume resets the whole map);
+             5. sparse SD halo: rank k returns the N depths of exactly the texels r sent it in step 3
+                (k holds r's index list, so the reply carries values only);
+             6. pass 2 of its own rows (rsd_svao_pass2_rows) and an all-gather of the AO bands.
+
+    No step synchronises the host with the GPU except the event wait of step 3 (no
+    nonzero(), no .cpu(), no .item(); tests/test_gpu_sharding.py runs it under
+    torch.cuda.set_sync_debug_mode("error")).
 
     Load balance ("re-split from the previous frame's per-band time"): every rank
-    times its own pass 1 + trace + pass 2; the times travel with the step-2 counts, and every rank
-    computes the same new split of the 32-row groups (cost spread uniformly over each band's
-    groups, equal predicted cost per rank, moved half-way from the current split), applied from
-    the next frame.  Every SD texel and AO pixel is still produced by exactly one rank with the
-    same kernels, so the frame is bit-identical to the 1-GPU frame whatever the split.
+    times its own pass 1 + trace + pass 2 (HIP events, read only once complete); the times travel
+    with the step-2 counts, and every rank computes the same new split of the 32-row groups (cost
+    spread uniformly over each band's groups, equal predicted cost per rank, moved half-way from the
+    current split), applied from this object's next frame.  Every SD texel and AO pixel is still
+    produced by exactly one rank with the same kernels, so the frame is bit-identical to the 1-GPU
+    frame whatever the split.
 
     `backend` provides pass1_rows(rows), sd_trace_rows(rows, consume=...), pass2_rows(rows),
-    clear_intervals(), tensors ray_minmax (int32 [2, sdH, sdW]), sd, ao, and cfg / vao / sd_h."""
+    clear_intervals(), tensors ray_minmax (int32 [2, sdH, sdW]), sd, ao, and cfg / vao / sd_h.
+    `comm`: DistComm (default; torch.distributed) or LocalComm (threads on one GPU)."""
 
     def __init__(self, backend, rank: int = 0, world: int = 1, pg=None, throughput: bool = False,
-                 rebalance: bool = True):
-        import torch.distributed as dist
+                 rebalance: bool = True, comm=None):
         b = self.b = backend
         self.rank, self.world, self.pg = rank, world, pg
-        self.dist = dist if world > 1 else None
+        self.comm = comm if comm is not None else (DistComm(pg) if world > 1 else None)
+        self.nccl = bool(getattr(self.comm, "nccl", False))
         self.trace_kw = {"throughput": True} if throughput and getattr(b, "can_consume_intervals", False) else {}
         self._intervals_clear = False
         cfg = b.cfg
@@ -228,13 +353,14 @@ class HaloFrame:
         self.gb = [self.G * r // world for r in range(world + 1)]  # first split: equal group counts
         self.rebalance = rebalance and world > 1
         self.halo_px = halo_px(cfg, float(b.vao.ssMaxRadius))
-        self.nccl = world > 1 and dist.get_backend(pg) == "nccl"
         self.cuda = b.sd.is_cuda
         self._ao_cap = 0
         self._next_gb = None
-        self._prev = None  # timing of this rank's previous frame (events or seconds)
+        self._prev = None  # timing events of this object's previous frame
+        self._open = None  # state of the frame between front() and back()
         self.sent = {"intervals": 0, "sd": 0, "ao": 0}
         self.frames = 0
+        self.blocked_waits = 0  # back() calls whose counts were not yet on the host (frames in flight: ~0)
         self.splits = []  # the group split of every frame (diagnostics)
         self._plan()
 
@@ -279,6 +405,22 @@ class HaloFrame:
         shape = (self.ao_max,) + tuple(b.ao.shape[1:])
         self.ao_send = self._ao_send_buf[:self.ao_max * row].view(shape)
         self.ao_recv = self._ao_recv_buf[:world * self.ao_max * row].view((world,) + shape)
+        # device compaction of the touched texels: per peer, the candidate region's texel indices and a
+        # [3, cap + 1] int32 buffer (column cap collects the untouched texels' scatter writes)
+        if world > 1:
+            dev = b.ray_minmax.device
+            sdw = b.ray_minmax.shape[2]
+            self._cand = {}
+            for k, rows in self.iv_send.items():
+                if rows:
+                    lo, hi = rows
+                    n = (hi - lo) * sdw
+                    self._cand[k] = (lo, hi, torch.arange(lo * sdw, hi * sdw, dtype=torch.int32, device=dev),
+                                     torch.empty((3, n + 1), dtype=torch.int32, device=dev))
+            self._row = torch.zeros(world + 1, dtype=torch.int64, device=dev)
+            self._M_dev = torch.zeros((world, world + 1), dtype=torch.int64, device=dev)
+            self._M_host = torch.zeros((world, world + 1), dtype=torch.int64,
+                                       pin_memory=self.cuda and torch.cuda.is_available())
 
     def dense_bytes_per_frame(self):
         """What the round-2 dense halo (whole candidate rows) would send per frame from this rank."""
@@ -293,37 +435,6 @@ class HaloFrame:
         n = max(1, self.frames)
         return {k: int(v // n) for k, v in self.sent.items()}
 
-    # ---- collectives
-    def _exchange(self, sends, recvs):
-        """Point-to-point exchange (ncclSend / ncclRecv under RCCL): sends {peer: tensor}, recvs
-        {peer: tensor}; returns after every transfer completed (stream-ordered for NCCL)."""
-        sends = {k: t for k, t in sends.items() if t.numel()}
-        recvs = {k: t for k, t in recvs.items() if t.numel()}
-        staged = not self.nccl and any(t.is_cuda for t in list(sends.values()) + list(recvs.values()))
-        if staged:  # gloo rehearsal with device tensors (several ranks on one GPU): via host copies
-            sends = {k: t.cpu() for k, t in sends.items()}
-            recvs_dev, recvs = recvs, {k: torch.empty(t.shape, dtype=t.dtype) for k, t in recvs.items()}
-        ops = [self.dist.P2POp(self.dist.isend, t.contiguous(), k, group=self.pg) for k, t in sends.items()]
-        ops += [self.dist.P2POp(self.dist.irecv, t, k, group=self.pg) for k, t in recvs.items()]
-        if ops:
-            for w in self.dist.batch_isend_irecv(ops):
-                w.wait()
-        if staged:
-            for k, t in recvs.items():
-                recvs_dev[k].copy_(t)
-
-    def _all_gather_small(self, row):
-        """All-gather one int64 row per rank -> [world, len(row)] on the host (one sync)."""
-        t = torch.tensor(row, dtype=torch.int64)
-        if self.nccl:
-            t = t.cuda()
-            out = torch.empty((self.world, t.numel()), dtype=torch.int64, device=t.device)
-            self.dist.all_gather_into_tensor(out.view(-1), t, group=self.pg)
-            return out.cpu()
-        out = [torch.empty_like(t) for _ in range(self.world)]
-        self.dist.all_gather(out, t, group=self.pg)
-        return torch.stack(out)
-
     # ---- timing of this rank's compute (load balance)
     def _mark(self):
         """A timestamp for the re-balancing cost (None when nothing re-balances: world 1)."""
@@ -336,10 +447,16 @@ class HaloFrame:
             return e
         return time.perf_counter()
 
-    def _span_us(self, a, c):
+    def _prev_cost_us(self):
+        """This object's previous frame's compute time (us), or -1 while its events are incomplete
+        (never waits: every rank then sees the -1 and nobody re-balances this frame)."""
+        if self._prev is None:
+            return -1
         if self.cuda:
-            return a.elapsed_time(c) * 1e3
-        return (c - a) * 1e6
+            if not all(c.query() for _, c in self._prev):
+                return -1
+            return int(sum(a.elapsed_time(c) * 1e3 for a, c in self._prev))
+        return int(sum((c - a) * 1e6 for a, c in self._prev))
 
     def _rebalanced(self, costs):
         """The next split of the 32-row groups from every rank's measured cost of the current one:
@@ -374,6 +491,14 @@ class HaloFrame:
             self.splits.append(tuple(self.gb))
             self.frames += 1
             return
+        self.front()
+        self.back(sd_events)
+
+    def front(self):
+        """Steps 1-2: pass 1 of this rank's rows, the device compaction of the touched texels per
+        peer and the all-gather of the counts (device tensors; the copy to the host is not waited for)."""
+        assert self._open is None, "HaloFrame: front() twice without back()"
+        b, me, world = self.b, self.rank, self.world
         if self._next_gb is not None and self._next_gb != self.gb:
             self.gb = self._next_gb
             self._plan()
@@ -382,50 +507,67 @@ class HaloFrame:
         consume = getattr(b, "can_consume_intervals", False) and bool(b.cfg.ray_interval)
         if not (consume and self._intervals_clear):
             b.clear_intervals()
-        t0 = self._mark()
+        st = {"consume": consume, "t": [self._mark()]}
+        prev_us = self._prev_cost_us() if self.rebalance else -1
         b.pass1_rows(self.px_rows[me])
-        t1 = self._mark()
-        mine = {}  # k -> global texel indices of my window touched by my pass 1 inside band k
+        st["t"].append(self._mark())
         if world > 1:
-            sdw = b.ray_minmax.shape[2]
-            iv_send = {}
-            for k, rows in self.iv_send.items():
-                if not rows:
-                    continue
-                lo, hi = rows
+            row = self._row
+            row.zero_()
+            for k, (lo, hi, idx, buf) in self._cand.items():
                 reg = b.ray_minmax[:, lo:hi].reshape(2, -1)
-                flat = ((reg[0] != FLT_MAX_BITS) | (reg[1] != 0)).nonzero().squeeze(1)
-                idx = (flat + lo * sdw).to(torch.int32)
-                mine[k] = idx.long()
-                iv_send[k] = torch.cat([idx[None], reg[:, flat]], 0)  # [3, n] int32: index, rayMin, rayMax
-            prev_us = -1
-            if self._prev is not None:
-                prev_us = int(sum(self._span_us(a, c) for a, c in self._prev))
-            counts = [int(iv_send[k].shape[1]) if k in iv_send else 0 for k in range(world)]
-            M = self._all_gather_small(counts + [prev_us])  # [world, world + 1]: send counts, previous cost
+                touched = (reg[0] != FLT_MAX_BITS) | (reg[1] != 0)
+                pos = torch.cumsum(touched, 0)  # int64: 1-based position of each touched texel
+                dst = torch.where(touched, pos - 1, torch.full_like(pos, buf.shape[1] - 1))
+                buf.scatter_(1, dst.expand(3, -1), torch.stack((idx, reg[0], reg[1])))
+                row[k:k + 1].copy_(pos[-1:])
+            row[world] = prev_us
+            self.comm.all_gather(self._M_dev, row)
+            self._M_host.copy_(self._M_dev, non_blocking=True)
+            if self.cuda:
+                ev = torch.cuda.Event()
+                ev.record()
+                st["ev"] = ev
+        self._open = st
+
+    def back(self, sd_events=None):
+        """Steps 3-6 of the frame opened by front()."""
+        assert self._open is not None, "HaloFrame: back() without front()"
+        st, self._open = self._open, None
+        b, me, world = self.b, self.rank, self.world
+        t = st["t"]
+        mine, theirs = {}, {}
+        if world > 1:
+            if self.cuda:
+                if not st["ev"].query():
+                    self.blocked_waits += 1
+                st["ev"].synchronize()  # the counts of THIS frame on the host (lagged: already there)
+            M = self._M_host.numpy().copy()
             if self.rebalance and int(M[:, world].min()) >= 0:
-                self._next_gb = self._rebalanced([float(x) for x in M[:, world].tolist()])
+                self._next_gb = self._rebalanced([float(x) for x in M[:, world]])
             dev = b.ray_minmax.device
+            iv_send = {k: self._cand[k][3][:, :int(M[me, k])] for k in self._cand if M[me, k] > 0}
             iv_recv = {k: torch.empty((3, int(M[k, me])), dtype=torch.int32, device=dev)
-                       for k in range(world) if k != me and int(M[k, me]) > 0}
-            self._exchange(iv_send, iv_recv)
-            self.sent["intervals"] += sum(t.numel() * 4 for t in iv_send.values())
-            theirs = {}
-            for k, t in iv_recv.items():
-                idx = t[0].long()
+                       for k in range(world) if k != me and M[k, me] > 0}
+            self.comm.exchange(iv_send, iv_recv)
+            self.sent["intervals"] += sum(x.numel() * 4 for x in iv_send.values())
+            for k, x in iv_send.items():
+                mine[k] = x[0].long()
+            for k, x in iv_recv.items():
+                idx = x[0].long()
                 theirs[k] = idx
                 if b.cfg.ray_interval:
-                    b.ray_minmax[0].view(-1).scatter_reduce_(0, idx, t[1], reduce="amin")
-                b.ray_minmax[1].view(-1).scatter_reduce_(0, idx, t[2], reduce="amax")
+                    b.ray_minmax[0].view(-1).scatter_reduce_(0, idx, x[1], reduce="amin")
+                b.ray_minmax[1].view(-1).scatter_reduce_(0, idx, x[2], reduce="amax")
         if sd_events:
             sd_events[0].record()
-        t2 = self._mark()
-        if consume:
+        t.append(self._mark())
+        if st["consume"]:
             b.sd_trace_rows(self.sd_rows[me], consume=True, **self.trace_kw)
         else:
             b.sd_trace_rows(self.sd_rows[me], **self.trace_kw)
-        self._intervals_clear = consume
-        t3 = self._mark()
+        self._intervals_clear = st["consume"]
+        t.append(self._mark())
         if sd_events:
             sd_events[1].record()
         if world > 1:
@@ -434,22 +576,19 @@ class HaloFrame:
             sd_send = {k: flat_sd.index_select(1, idx) for k, idx in theirs.items()}
             sd_recv = {k: torch.empty((L, idx.numel(), ch), dtype=b.sd.dtype, device=b.sd.device)
                        for k, idx in mine.items() if idx.numel()}
-            self._exchange(sd_send, sd_recv)
-            self.sent["sd"] += sum(t.numel() * t.element_size() for t in sd_send.values())
-            for k, t in sd_recv.items():
-                flat_sd.index_copy_(1, mine[k], t)
-        t4 = self._mark()
+            self.comm.exchange(sd_send, sd_recv)
+            self.sent["sd"] += sum(x.numel() * x.element_size() for x in sd_send.values())
+            for k, x in sd_recv.items():
+                flat_sd.index_copy_(1, mine[k], x)
+        t.append(self._mark())
         b.pass2_rows(self.px_rows[me])
-        t5 = self._mark()
-        self._prev = [(t0, t1), (t2, t3), (t4, t5)] if self.rebalance else None
+        t.append(self._mark())
+        self._prev = [(t[0], t[1]), (t[2], t[3]), (t[4], t[5])] if self.rebalance else None
         if world > 1:
             lo, hi = self.ao_rows[me]
             send, recv = self.ao_send, self.ao_recv
             send[:hi - lo].copy_(b.ao[lo:hi])
-            if self.nccl:
-                self.dist.all_gather_into_tensor(recv.view(-1), send.view(-1), group=self.pg)
-            else:
-                self.dist.all_gather(list(recv.unbind(0)), send, group=self.pg)
+            self.comm.all_gather(recv, send)
             self.sent["ao"] += send.numel() * send.element_size()
             for k, (lo, hi) in enumerate(self.ao_rows):
                 if k != me:

@@ -34,6 +34,7 @@ def _hip():
         L.hipEventRecord.argtypes = [C.c_void_p, C.c_void_p]
         L.hipEventElapsedTime.argtypes = [C.POINTER(C.c_float), C.c_void_p, C.c_void_p]
         L.hipEventDestroy.argtypes = [C.c_void_p]
+        L.hipEventQuery.argtypes = [C.c_void_p]
         _HIP = L
     return _HIP
 
@@ -53,6 +54,10 @@ class TimingEvent:
         s = (stream or torch.cuda.current_stream()).cuda_stream
         if self._L.hipEventRecord(self.h, C.c_void_p(s)) != 0:
             raise RuntimeError("hipEventRecord failed")
+
+    def query(self) -> bool:
+        """True when the event has completed (hipEventQuery; never blocks)."""
+        return self._L.hipEventQuery(self.h) == 0
 
     def elapsed_time(self, end: "TimingEvent") -> float:
         ms = C.c_float()

@@ -133,3 +133,88 @@ def test_halo_frame_three_ranks_equals_one_gpu(tmp_path):
         assert bits_equal(np.load(tmp_path / f"sd_{k}.npy")[:, lo:hi], ref["sd"][:, lo:hi]), f"rank {k} SD rows"
         iv, sd, _ = np.load(tmp_path / f"bytes_{k}.npy")
         assert iv + sd < full  # less than the whole interval + SD maps
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("world", [2, 3])
+def test_halo_frame_sync_free_threads(world):
+    """The N > 1 frame without host synchronisation: HaloFrame over LocalComm -- `world`
+    host threads on this GPU, one HIP stream and one librsd device each, exchanges as device-to-device
+    copies ordered by events (the stream semantics of RCCL) -- runs 4 frames per rank, two frame slots
+    interleaved like bench.py's frames in flight (back() of a frame after front() of the next), under
+    torch.cuda.set_sync_debug_mode("error"): no torch op of front() / back() waits for the GPU (the
+    only host wait is the event of a frame's counts, one frame later).  Every frame of every rank
+    equals the 1-GPU AO image; each rank's own SD rows equal the 1-GPU SD map."""
+    import threading
+
+    import torch
+    from rsd.frame import CONFIGS, FrameConfig, Renderer
+    from rsd.scenes import make_scene
+    from rsd.shard import HaloFrame, LocalComm, LocalHub
+    kw, name = CONFIGS[CONFIG]
+    scene = make_scene(name)
+    r = Renderer(scene, FrameConfig(**kw))
+    r.gbuffer()
+    r.frame()
+    ref = r.numpy()
+    r.close()
+    hub = LocalHub(world)
+    ranks = []
+    for k in range(world):  # setup (allocations, uploads, G-buffers) before the sync check
+        slots = []
+        comm = LocalComm(hub, k)  # one communicator per rank, shared by its frame slots
+        for _ in range(2):
+            rr = Renderer(scene, FrameConfig(**kw))
+            st = torch.cuda.Stream()
+            with torch.cuda.stream(st):
+                rr.gbuffer()
+            slots.append((rr, st, HaloFrame(rr, k, world, comm=comm)))
+        ranks.append(slots)
+    torch.cuda.synchronize()
+    out, errors = {}, []
+
+    def run(k):
+        try:
+            slots = ranks[k]
+            pending = []
+
+            def finish(j):
+                rr, st, f = slots[j % 2]
+                with torch.cuda.stream(st):
+                    f.back()
+                    out[(k, j)] = rr.ao.clone()
+
+            for i in range(4):
+                rr, st, f = slots[i % 2]
+                with torch.cuda.stream(st):
+                    rr.ao.zero_()
+                    f.front()
+                pending.append(i)
+                if len(pending) > 1:
+                    finish(pending.pop(0))
+            finish(pending.pop(0))
+        except Exception as e:  # noqa: BLE001 -- reported by the main thread
+            errors.append((k, repr(e)))
+
+    torch.cuda.set_sync_debug_mode("error")
+    try:
+        threads = [threading.Thread(target=run, args=(k,)) for k in range(world)]
+        for t in threads:
+            t.start()
+        for t in threads:
+            t.join(timeout=240)
+    finally:
+        torch.cuda.set_sync_debug_mode("default")
+    torch.cuda.synchronize()
+    assert not errors, errors
+    for k in range(world):
+        for j in range(4):
+            assert np.array_equal(out[(k, j)].cpu().numpy(), ref["ao"]), f"rank {k} frame {j}"
+        f = ranks[k][1][2]
+        lo, hi = f.sd_rows[k]
+        g = ranks[k][1][0].numpy()
+        assert bits_equal(g["sd"][:, lo:hi], ref["sd"][:, lo:hi]), f"rank {k} SD rows"
+        assert f.frames == 2 and sum(f.bytes_per_frame().values()) > 0
+    for slots in ranks:
+        for rr, _, _ in slots:
+            rr.close()

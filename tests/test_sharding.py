@@ -90,6 +90,11 @@ def _worker(rank, world, port, out_dir, mode="band"):
     from rsd.shard import BandFrame, HaloFrame
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     cfg = _cfg() if mode == "band" else _halo_cfg()
+    if mode == "halo_lag":
+        _lag_frames(O, cfg, rank, world, out_dir)
+        dist.barrier()
+        dist.destroy_process_group()
+        return
     be = OracleBackend(O, make_scene("arcade_tiny"), cfg, None if mode == "band" else HALO_REACH)
     f = (BandFrame if mode == "band" else HaloFrame)(be, rank, world)
     f.frame()
@@ -111,6 +116,33 @@ def _worker(rank, world, port, out_dir, mode="band"):
     np.save(os.path.join(out_dir, f"sd_{rank}.npy"), be.np_sd)
     dist.barrier()
     dist.destroy_process_group()
+
+
+def _lag_frames(O, cfg, rank, world, out_dir):
+    """bench.py's frames in flight at N > 1: two frame slots (own buffers), back() of each frame issued
+    after front() of the next one, so the collectives of different frames interleave -- in the same
+    order on every rank.  Every frame must still give the 1-process image."""
+    from rsd.scenes import make_scene
+    from rsd.shard import HaloFrame
+    slots = []
+    for _ in range(2):
+        be = OracleBackend(O, make_scene("arcade_tiny"), cfg, HALO_REACH)
+        slots.append((be, HaloFrame(be, rank, world)))
+    pending = []
+
+    def finish(j):
+        be, f = slots[j % 2]
+        f.back()
+        np.save(os.path.join(out_dir, f"lag_{rank}_{j}.npy"), be.np_ao)
+
+    for i in range(5):
+        be, f = slots[i % 2]
+        be.np_ao[:] = 0
+        f.front()
+        pending.append(i)
+        if len(pending) > 1:
+            finish(pending.pop(0))
+    finish(pending.pop(0))
 
 
 def _free_port():
@@ -293,3 +325,18 @@ def test_band_frame_throughput_and_consume_plumbing():
     bf.frame()
     assert [c for c in plain.calls if c[0] == "trace"] == [("trace", (0, 1), ())] * 2
     assert plain.calls.count(("clear",)) == 2
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_halo_frames_in_flight_interleaved(oracle, tmp_path, world):
+    """HaloFrame.front() / back() with frames in flight (the counts of a frame are read on the host one
+    frame later): 5 frames over 2 slots, every rank ends every frame with the 1-process AO image."""
+    from rsd.scenes import make_scene
+    from rsd.shard import BandFrame
+    ref = OracleBackend(oracle, make_scene("arcade_tiny"), _halo_cfg(), HALO_REACH)
+    BandFrame(ref, 0, 1).frame()
+    mp.start_processes(_worker, args=(world, _free_port(), str(tmp_path), "halo_lag"), nprocs=world, join=True,
+                       start_method="spawn")
+    for r in range(world):
+        for j in range(5):
+            assert np.array_equal(np.load(tmp_path / f"lag_{r}_{j}.npy"), ref.np_ao), f"rank {r} frame {j}"
