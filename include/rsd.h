@@ -172,7 +172,20 @@ typedef struct {
                                       reference's pass 2 returns on aoMask == 0, SVAORaster2.ps.slang:50-52).
                                       Pass 2 must get the flags of the pass 1 that wrote d_stencil. */
     uint32_t numerics;             /* ABI v5: rsd_numerics of pass 1 and pass 2 (DESIGN.md 2 "Numerics") */
+    uint32_t ao_kernel;            /* ABI v5: AO_KERNEL (SVAO.cpp:233, AOKernel.h): rsd_ao_kernel */
+    uint32_t primary_depth_mode;   /* ABI v5: PRIMARY_DEPTH_MODE (SVAO.cpp:222, DepthMode.h): 0 SingleDepth,
+                                      1 DualDepth (the second depth layer d_depth2 refines the raster samples,
+                                      SVAORaster.ps.slang:69-70, Common.slang:498-505, :555-558) */
+    const float* d_depth2;         /* ABI v5: DualDepth: gDepthTex2, linear depth of the second layer
+                                      (DepthPeeling / TemporalDepthPeel), width x height R32F */
 } rsd_svao_params;
+/* SVAO's AO kernel (SVAO::mKernel, a UI dropdown in the reference, SVAO.cpp:615-620):
+ *   VAO   volumetric obscurance: visibility = min over the samples of the sphere + halo terms (default);
+ *   HBAO  horizon-based: visibility = max over the samples of saturate(HBAOKernel / pdf), pdf =
+ *         0.9 (1 - r_i)^1.5, AO = saturate(1 - 2 avg)^exponent (Common.slang:60-66, 326-330, 362-365,
+ *         421-430, 455-488).  The reference's UI scales the world radius by 1.5 on switching to HBAO
+ *         (SVAO.cpp:617-620); callers pass the radius they want.  Raytraced secondary mode: VAO only. */
+typedef enum { RSD_AO_KERNEL_VAO = 0, RSD_AO_KERNEL_HBAO = 1 } rsd_ao_kernel;
 /* Arithmetic of the SVAO passes ("AO 1", "AO 2"; the SD trace is always exact).
  *   FAST   FMA contraction, v_rcp_f32-based division, hardware sqrt / rsq, float32 denormals flushed:
  *          what D3D allows the reference's HLSL (mad may fuse, '/' within 2.5 ulp, denormals flushed).

@@ -51,7 +51,9 @@ class VAOData(C.Structure):
 class SVAOParams(C.Structure):
     _fields_ = [("num_directions", C.c_uint32), ("sd_samples", C.c_uint32),
                 ("secondary_depth_mode", C.c_uint32), ("ray_interval", C.c_uint32),
-                ("sd_jitter", C.c_uint32), ("guard_band", C.c_uint32), ("dual_ao", C.c_uint32)]
+                ("sd_jitter", C.c_uint32), ("guard_band", C.c_uint32), ("dual_ao", C.c_uint32),
+                ("tile_flags_unused", C.c_void_p), ("numerics_unused", C.c_uint32), ("ao_kernel", C.c_uint32),
+                ("primary_depth_mode", C.c_uint32), ("depth2", C.c_void_p)]
 
 
 _lib = None
@@ -109,6 +111,8 @@ def lib():
         L.ocpu_noise_texture.argtypes = [vp]
         L.ocpu_sample_radius.restype = f32
         L.ocpu_sample_radius.argtypes = [u32, u32]
+        L.ocpu_sample_radius_kernel.restype = f32
+        L.ocpu_sample_radius_kernel.argtypes = [u32, u32, u32]
         L.ocpu_encode_normal_2x8.restype = u32
         L.ocpu_encode_normal_2x8.argtypes = [vp]
         L.ocpu_decode_normal_2x8.argtypes = [u32, vp]
@@ -273,8 +277,25 @@ def stencil_dtype(num_directions):
     return {8: np.uint8, 16: np.uint16, 32: np.uint32}[int(num_directions)]
 
 
-def svao_pass1(cam, vao: VAOData, p: SVAOParams, depth, normals, sdW, sdH):
+def _host_params(p, depth2=None):
+    """A copy of the SVAO params whose DualDepth layer points at host memory (a struct copied from
+    librsd carries a device pointer there): `depth2` (float32 H x W) or none; the array must outlive
+    the call (the caller holds it)."""
+    q = SVAOParams.from_buffer_copy(p)
+    q.tile_flags_unused = None
+    if q.primary_depth_mode == 1:
+        if depth2 is None:
+            raise ValueError("DualDepth (primary_depth_mode 1) needs the host depth2 layer")
+        q.depth2 = depth2.ctypes.data
+    else:
+        q.depth2 = None
+    return q
+
+
+def svao_pass1(cam, vao: VAOData, p: SVAOParams, depth, normals, sdW, sdH, depth2=None):
     H, W = depth.shape
+    d2 = None if depth2 is None else np.ascontiguousarray(depth2, np.float32)
+    p = _host_params(p, d2)
     ao = np.zeros((H, W, 2) if p.dual_ao else (H, W), np.uint8)  # dualAO: RG8Unorm (bright, dark)
     st = np.zeros((H, W), stencil_dtype(p.num_directions))
     rmin = np.zeros((sdH, sdW), np.uint32)
@@ -285,8 +306,10 @@ def svao_pass1(cam, vao: VAOData, p: SVAOParams, depth, normals, sdW, sdH):
     return ao, st, rmin, rmax
 
 
-def svao_pass2(cam, vao: VAOData, p: SVAOParams, depth, normals, stencil, sd, ao, threads=None):
+def svao_pass2(cam, vao: VAOData, p: SVAOParams, depth, normals, stencil, sd, ao, threads=None, depth2=None):
     H, W = depth.shape
+    d2 = None if depth2 is None else np.ascontiguousarray(depth2, np.float32)
+    p = _host_params(p, d2)
     ao = np.array(ao, np.uint8, copy=True)
     sdH, sdW = sd.shape[1], sd.shape[2]
     sdc = np.ascontiguousarray(sd, np.float32)
@@ -302,7 +325,11 @@ def ray_cone_spread(focal_length, height):
 
 def svao_pass2_raytraced(scene: Scene, cam, vao: VAOData, p: SVAOParams, depth, normals, stencil, ao, cull=1,
                          ray_pipeline=0, band=(0, 1), threads=None, alpha_test=1):
-    """SVAO "AO 2" in the Raytraced secondary mode; returns the updated AO image."""
+    """SVAO "AO 2" in the Raytraced secondary mode; returns the updated AO image (VAO kernel, SingleDepth
+    primary visibility: the modes librsd's Raytraced pass supports)."""
+    if p.ao_kernel != 0 or p.primary_depth_mode != 0:
+        raise NotImplementedError("Raytraced AO 2: VAO kernel with SingleDepth primary visibility only")
+    p = _host_params(p)
     H, W = depth.shape
     ao = np.array(ao, np.uint8, copy=True)
     lib().ocpu_svao_pass2_rt_band(scene.h, C.byref(cam), C.byref(vao), C.byref(p), _p(depth), _p(normals), W, H,
@@ -335,8 +362,9 @@ def noise_texture():
     return out
 
 
-def sample_radius(nd, i):
-    return lib().ocpu_sample_radius(nd, i)
+def sample_radius(nd, i, kernel=0):
+    """Common.slang:51-66: the sample radius of direction i (kernel 0 VAO, 1 HBAO)."""
+    return lib().ocpu_sample_radius_kernel(nd, i, kernel)
 
 
 def encode_normal(n):
@@ -364,6 +392,7 @@ def svao_clear(rmin, rmax):
 
 
 def svao_pass1_into(cam, vao, p, depth, normals, ao, st, rmin, rmax, band=(0, 1)):
+    p = _host_params(p)
     H, W = depth.shape
     sdH, sdW = rmin.shape
     lib().ocpu_svao_pass1_band(C.byref(cam), C.byref(vao), C.byref(p), _p(depth), _p(normals), W, H, _p(ao), _p(st),
@@ -372,6 +401,7 @@ def svao_pass1_into(cam, vao, p, depth, normals, ao, st, rmin, rmax, band=(0, 1)
 
 def svao_pass1_rows_into(cam, vao, p, depth, normals, ao, st, rmin, rmax, rows):
     """Pass 1 of the visible rows [rows[0], rows[1]) (a contiguous screen band)."""
+    p = _host_params(p)
     H, W = depth.shape
     sdH, sdW = rmin.shape
     lib().ocpu_svao_pass1_rows(C.byref(cam), C.byref(vao), C.byref(p), _p(depth), _p(normals), W, H, _p(ao), _p(st),
@@ -379,6 +409,7 @@ def svao_pass1_rows_into(cam, vao, p, depth, normals, ao, st, rmin, rmax, rows):
 
 
 def svao_pass2_rows_into(cam, vao, p, depth, normals, stencil, sd, ao, rows, threads=None):
+    p = _host_params(p)
     H, W = depth.shape
     sdc = np.ascontiguousarray(sd, np.float32)
     sdH, sdW = sdc.shape[1], sdc.shape[2]
@@ -406,6 +437,7 @@ def sd_trace_into(scene, cam, params, linearZ, rmin, rmax, sd, band=(0, 1), thre
 
 
 def svao_pass2_into(cam, vao, p, depth, normals, stencil, sd, ao, band=(0, 1), threads=None):
+    p = _host_params(p)
     H, W = depth.shape
     sdH, sdW = sd.shape[1], sd.shape[2]
     lib().ocpu_svao_pass2_band(C.byref(cam), C.byref(vao), C.byref(p), _p(depth), _p(normals), W, H, _p(stencil),

@@ -89,10 +89,31 @@ static const float k_radius32[32] = {
     0.878233108646881, 0.5303115209931901, 0.7032256306171377, 0.3099952198410562,
     0.7873133907642258, 0.43130429537268, 0.6190581352335289, 0.10219580968897692,
 };
-static const float* o_radius_table(uint32_t nd)
+/* SVAO/Common.slang:60-66 -- HBAO sample radii (AO_KERNEL == AO_KERNEL_HBAO), double literals there */
+static const float k_hbao8[8] = {0.019897607325877215, 0.3239192018939078, 0.15013283288204182, 0.5608856339193332,
+                                 0.07874804859295396, 0.4306374970658152, 0.23159241868180838, 0.74770696488701};
+static const float k_hbao16[16] = {
+    0.008364792005390745, 0.29968419137477154, 0.13131974798930376, 0.5251597224509892,
+    0.06264063727314514, 0.40226410430222115, 0.21027995621089465, 0.6906178807859765,
+    0.03303993608633204, 0.34903099295095424, 0.16956281924775551, 0.5996160679614535,
+    0.09559795810145842, 0.46040865279052423, 0.25357218870257175, 0.8218290863578166,
+};
+static const float k_hbao32[32] = {
+    0.0035168784979124203, 0.28787249889929795, 0.12214740408236834, 0.5082189968610005,
+    0.05489041689357717, 0.38854375322009427, 0.19986558164830323, 0.6656225173745592,
+    0.02630214826181389, 0.33636038195532914, 0.15977097044845298, 0.579825376399601,
+    0.08708424832212604, 0.44533522627083877, 0.24249692822679572, 0.7816464549941924,
+    0.013886447731081395, 0.3116969449839127, 0.14064876764650994, 0.5426920213922799,
+    0.07059703986067731, 0.41628837439340993, 0.22085459126773643, 0.7177502077720759,
+    0.04006955250785802, 0.36194276200351894, 0.17950859741413544, 0.6203897476558216,
+    0.10428292232859922, 0.47588885313824597, 0.2648228762567681, 0.8740952987729764,
+};
+static const float* o_radius_table_k(uint32_t nd, uint32_t kernel)
 {
+    if (kernel == 1) return nd == 32 ? k_hbao32 : nd == 16 ? k_hbao16 : k_hbao8;
     return nd == 32 ? k_radius32 : nd == 16 ? k_radius16 : k_radius8;
 }
+static const float* o_radius_table(uint32_t nd) { return o_radius_table_k(nd, 0); }
 
 /* Jitter.slangh:27-50 randomJitter */
 void ocpu_jitter(uint32_t x, uint32_t y, float* jx, float* jy)
@@ -106,6 +127,14 @@ float ocpu_sample_radius(uint32_t num_directions, uint32_t i)
 {
     if ((num_directions == 8 || num_directions == 16 || num_directions == 32) && i < num_directions)
         return o_radius_table(num_directions)[i];
+    return 0.0f;
+}
+
+/* the sample radius of direction i for AO_KERNEL `kernel` (0 VAO, 1 HBAO) */
+float ocpu_sample_radius_kernel(uint32_t num_directions, uint32_t i, uint32_t kernel)
+{
+    if ((num_directions == 8 || num_directions == 16 || num_directions == 32) && i < num_directions && kernel <= 1)
+        return o_radius_table_k(num_directions, kernel)[i];
     return 0.0f;
 }
 
@@ -1276,6 +1305,9 @@ typedef struct {
     float sinNoise[16], cosNoise[16];
     uint32_t nd;  /* NUM_DIRECTIONS: 8, 16, 32 */
     float sinDir[32], cosDir[32];
+    uint32_t hbao;  /* AO_KERNEL == AO_KERNEL_HBAO */
+    uint32_t dual;  /* PRIMARY_DEPTH_MODE == DEPTH_MODE_DUAL (gDepthTex2 = p->depth2) */
+    float hbaoPdf[32]; /* HBAO pdf of direction i: 0.9 * pow(1 - sampleRadius[i], 1.5) (Common.slang:364) */
 } octx;
 
 /* the SVAO stencil texel (SVAO.cpp:132-134): R8Uint / R16Uint / R32Uint for 8 / 16 / 32 directions,
@@ -1321,10 +1353,13 @@ static void o_ctx_init(octx* x, const ocam* c, const ovao* d, const osvao_params
         x->cosNoise[i] = o_cos(rr);
     }
     x->nd = p->num_directions == 16 || p->num_directions == 32 ? p->num_directions : 8u;
+    x->hbao = p->ao_kernel == 1;
+    x->dual = p->primary_depth_mode == 1 && p->depth2;
     for (uint32_t i = 0; i < x->nd; ++i) {
         float a = ((float)i / (float)x->nd) * 2.0f * 3.141f; /* Common.slang:357 */
         x->sinDir[i] = o_sin(a);
         x->cosDir[i] = o_cos(a);
+        x->hbaoPdf[i] = 0.9f * o_pow(1.0f - o_radius_table_k(x->nd, 1)[i], 1.5f);
     }
 }
 
@@ -1405,10 +1440,10 @@ static float o_make_nonzero(float v, float eps)
 static int o_sample_init(const octx* x, float u, float v, const obasic* b, uint32_t i, osample* s)
 {
     const ovao* d = x->d;
-    s->radius = o_radius_table(x->nd)[i] * b->radius;
+    s->radius = o_radius_table_k(x->nd, x->hbao)[i] * b->radius;
     float dir[2] = {s->radius * x->sinDir[i], s->radius * x->cosDir[i]};
     float sphereHeight = sqrtf(b->radius * b->radius - s->radius * s->radius);
-    s->pdf = 2.0f * sphereHeight;
+    s->pdf = x->hbao ? x->hbaoPdf[i] : 2.0f * sphereHeight; /* Common.slang:362-365 */
     s->sphereStart = sphereHeight;
     s->sphereEnd = -sphereHeight;
     float zi = -(dir[0] * b->normalO[0] + dir[1] * b->normalO[1]) / o_make_nonzero(b->normalO[2], 0.0001f);
@@ -1438,14 +1473,41 @@ static float o_calc_visibility(const ovao* d, float oz, float ss, float se, floa
     return sphere + halo;
 }
 
-/* Common.slang:463-483 addSample (VAO) */
+/* Common.slang:421-430 HBAOKernel (gData.radius: the VAOData radius, not the pixel's clamped one) */
+static float o_hbao_kernel(const octx* x, const obasic* b, const float S[3])
+{
+    float V[3] = {S[0] - b->posV[0], S[1] - b->posV[1], S[2] - b->posV[2]};
+    const float NdotVBias = 0.1f;
+    float nV[3];
+    o_normalize(V, nV);
+    float angleTerm = o_saturate(o_dot(b->normalV, nV) - NdotVBias);
+    float distanceTerm = o_saturate(1.0f - o_dot(V, V) / (x->d->radius * x->d->radius));
+    return angleTerm * distanceTerm;
+}
+
+/* Common.slang:463-483 addSample: VAO (min of calcVisibility) or HBAO (max of the kernel / pdf) */
 static void o_add_sample(const octx* x, const obasic* b, osample* s, const float spV[3], int init)
 {
     float diff[3] = {spV[0] - b->posV[0], spV[1] - b->posV[1], spV[2] - b->posV[2]};
     float oz = o_dot(diff, b->normal);
     s->objectSpaceZ = init ? oz : o_min(s->objectSpaceZ, oz);
+    if (x->hbao) {
+        float v = o_saturate(o_hbao_kernel(x, b, spV) / s->pdf);
+        s->visibility = init ? v : o_max(s->visibility, v);
+        return;
+    }
     float vis = o_calc_visibility(x->d, oz, s->sphereStart, s->sphereEnd, s->pdf, b->radius);
     s->visibility = init ? vis : o_min(s->visibility, vis);
+}
+
+/* Common.slang:455-461 requireRay (VAO with CONST_RADIUS, Common.slang:37; HBAO) */
+static int o_require_ray(const octx* x, const obasic* b, const osample* s)
+{
+    const ovao* d = x->d;
+    if (x->hbao)
+        return s->objectSpaceZ > o_max(s->sphereStart, b->radius * 0.1f) && s->screenSpaceRadius > d->ssRadiusCutoff;
+    float constRadius = (1.0f + d->thickness) * b->radius - s->sphereStart;
+    return s->objectSpaceZ > s->sphereStart + constRadius && s->screenSpaceRadius > d->ssRadiusCutoff;
 }
 
 /* Common.slang:492-496 evalPrimaryVisibility */
@@ -1455,6 +1517,24 @@ static void o_eval_primary(const octx* x, const obasic* b, osample* s)
     float spV[3];
     o_uv_to_view(x, s->rasterSamplePosUV[0], s->rasterSamplePosUV[1], z, spV);
     o_add_sample(x, b, s, spV, 1);
+}
+
+/* Common.slang:498-505 evalDualVisibility: the second depth layer (gDepthTex2) at the same texel,
+ * only where the sample still requires a ray */
+static void o_eval_dual(const octx* x, const obasic* b, osample* s, int init)
+{
+    if (!o_require_ray(x, b, s)) return;
+    float z = o_bilinear(x->p->depth2, (int)x->W, (int)x->H, s->rasterSamplePosUV[0], s->rasterSamplePosUV[1], 0);
+    float spV[3];
+    o_uv_to_view(x, s->rasterSamplePosUV[0], s->rasterSamplePosUV[1], z, spV);
+    o_add_sample(x, b, s, spV, init);
+}
+
+/* Common.slang:326-330 finalize */
+static float o_finalize(const octx* x, float avgAO)
+{
+    if (x->hbao) avgAO = o_saturate(1.0f - 2.0f * avgAO);
+    return o_pow(avgAO, x->d->exponent);
 }
 
 /* Common.slang:164-168 UVToSDPixel */
@@ -1538,22 +1618,23 @@ static void o_pass1_impl(const ocam* cam, const ovao* d, const osvao_params* p,
                     /* isSamePixel, Common.slang:129-134 */
                     if (fabsf(u - s.rasterSamplePosUV[0]) < d->invResolution[0] * 0.9f &&
                         fabsf(v - s.rasterSamplePosUV[1]) < d->invResolution[1] * 0.9f) {
-                        float w = (s.sphereStart - s.sphereEnd) / s.pdf;
-                        aoOut += w;
-                        aoD += w;
+                        if (!x.hbao) { /* SVAORaster.ps.slang:57-58: HBAO adds 0 */
+                            float w = (s.sphereStart - s.sphereEnd) / s.pdf;
+                            aoOut += w;
+                            aoD += w;
+                        }
                         continue;
                     }
                     /* SVAORaster.ps.slang:62-66: Raytraced mode with TRACE_OUT_OF_SCREEN (SVAO.h:104) */
                     int forceRay = p->secondary_depth_mode == 3 && !s.isInScreen;
                     o_eval_primary(&x, &b, &s);
+                    if (x.dual) o_eval_dual(&x, &b, &s, 0); /* SVAORaster.ps.slang:69-70 */
                     aoOut += s.visibility;
                     if (!s.isInScreen && d->sdGuard > 0) {
                         forceRay = 1;
                         s.objectSpaceZ = O_FLT_MAX;
                     }
-                    /* requireRay (VAO), Common.slang:455-461 with CONST_RADIUS (Common.slang:37) */
-                    float constRadius = (1.0f + d->thickness) * b.radius - s.sphereStart;
-                    int req = s.objectSpaceZ > s.sphereStart + constRadius && s.screenSpaceRadius > d->ssRadiusCutoff;
+                    int req = o_require_ray(&x, &b, &s);
                     if (req || forceRay) {
                         st |= 1u << i;
                         if (p->secondary_depth_mode == 2) {
@@ -1561,7 +1642,9 @@ static void o_pass1_impl(const ocam* cam, const ovao* d, const osvao_params* p,
                             o_uv_to_sd_pixel(d, s.samplePosUV, pix);
                             size_t o = (size_t)pix[1] * sdW + pix[0];
                             if (p->ray_interval) {
-                                float osMin = o_min(s.objectSpaceZ, b.radius + d->thickness * b.radius + s.sphereStart);
+                                /* SVAORaster.ps.slang:90-91 */
+                                float osMin = x.hbao ? o_min(s.objectSpaceZ, s.sphereStart)
+                                                     : o_min(s.objectSpaceZ, b.radius + d->thickness * b.radius + s.sphereStart);
                                 uint32_t rmin = o_asuint(o_max(b.posVLength - osMin, 0.0f));
                                 uint32_t rmax = o_asuint(o_max(b.posVLength - s.sphereEnd, 0.0f));
                                 if (rmin < rayMin[o]) rayMin[o] = rmin;
@@ -1574,13 +1657,15 @@ static void o_pass1_impl(const ocam* cam, const ovao* d, const osvao_params* p,
                         aoD += s.visibility; /* darkmap, SVAORaster.ps.slang:101-104 */
                     }
                 }
-                aoOut *= 1.0f / (float)x.nd;  /* SVAORaster.ps.slang:108-109 */
-                aoOut *= 2.0f;
+                aoOut *= 1.0f / (float)x.nd;  /* SVAORaster.ps.slang:108-109 (x 2: VAO only) */
                 aoD *= 1.0f / (float)x.nd;
-                aoD *= 2.0f;
+                if (!x.hbao) {
+                    aoOut *= 2.0f;
+                    aoD *= 2.0f;
+                }
                 if (p->secondary_depth_mode == 0 || st == 0) {
-                    aoOut = o_pow(aoOut, d->exponent);
-                    aoD = o_pow(aoD, d->exponent);
+                    aoOut = o_finalize(&x, aoOut);
+                    aoD = o_finalize(&x, aoD);
                 }
             }
             if (px < W && py < H) {
@@ -1600,21 +1685,20 @@ static void o_pass1_impl(const ocam* cam, const ovao* d, const osvao_params* p,
  * the pass-1 AO, dark = min(bright, dark) (DUAL_AO), finalize, store */
 static void o_ao_finish(const octx* x, uint8_t* ao, size_t o, float vis, float visD)
 {
-    const float e = x->d->exponent;
     vis *= 1.0f / (float)x->nd;
-    vis *= 2.0f;
+    if (!x->hbao) vis *= 2.0f; /* Common.slang:660-661 */
     if (!x->p->dual_ao) {
         vis += o_unorm8_to_float(ao[o]);
-        ao[o] = o_unorm8(o_pow(vis, e));
+        ao[o] = o_unorm8(o_finalize(x, vis));
         return;
     }
     visD *= 1.0f / (float)x->nd;
-    visD *= 2.0f;
+    if (!x->hbao) visD *= 2.0f;
     vis += o_unorm8_to_float(ao[2 * o]);
     visD += o_unorm8_to_float(ao[2 * o + 1]);
     visD = o_min(vis, visD);
-    ao[2 * o] = o_unorm8(o_pow(vis, e));
-    ao[2 * o + 1] = o_unorm8(o_pow(visD, e));
+    ao[2 * o] = o_unorm8(o_finalize(x, vis));
+    ao[2 * o + 1] = o_unorm8(o_finalize(x, visD));
 }
 
 /* SVAORaster2.ps.slang:48-65 -> calcAO2 (Common.slang:523-663), stochastic branch */
@@ -1647,15 +1731,22 @@ static void* o_pass2_rows(void* arg)
                 if (!(mask & (1u << i))) continue;
                 osample s;
                 o_sample_init(x, u, v, &b, i, &s);
-                o_eval_primary(x, &b, &s);
+                if (x->dual) o_eval_dual(x, &b, &s, 1); /* Common.slang:555-558 (force init) */
+                else o_eval_primary(x, &b, &s);
                 vis -= s.visibility;
+                if (x->p->secondary_depth_mode != 2) {
+                    /* secondary DualDepth: calcAO2 has no branch for it (Common.slang:562-651) */
+                    vis += s.visibility;
+                    visD += s.visibility;
+                    continue;
+                }
                 int pc[2];
                 o_uv_to_sd_pixel(d, s.samplePosUV, pc);
                 float jx = 0.5f, jy = 0.5f;
                 if (x->p->sd_jitter) ocpu_jitter((uint32_t)pc[0], (uint32_t)pc[1], &jx, &jy);
                 float su = ((float)(pc[0] - d->sdGuard) + jx) / d->lowResolution[0];
                 float sv = ((float)(pc[1] - d->sdGuard) + jy) / d->lowResolution[1];
-                if (!s.isInScreen) { s.visibility = 1.0f; s.objectSpaceZ = O_FLT_MAX; } /* resetSample */
+                if (!s.isInScreen) { s.visibility = x->hbao ? 0.0f : 1.0f; s.objectSpaceZ = O_FLT_MAX; } /* resetSample */
                 for (uint32_t k = 0; k < N; ++k) {
                     size_t so = ((((size_t)(k / 4) * j->sdH) + (size_t)pc[1]) * j->sdW + (size_t)pc[0]) * ch + (k % 4);
                     float lz = j->sd[so] * depthRange + depthOffset;
@@ -1773,7 +1864,7 @@ static void* o_pass2_rt_rows(void* arg)
                 const float tCRS = (pl - b.radius - d->thickness * b.radius) * L / pl;
                 const float tSS = (pl - s.sphereStart) * L / pl;
                 float TMin = o_max(halo, 0.0f), TMax = inside;
-                if (!s.isInScreen) { s.visibility = 1.0f; s.objectSpaceZ = O_FLT_MAX; } /* resetSample */
+                if (!s.isInScreen) { s.visibility = x->hbao ? 0.0f : 1.0f; s.objectSpaceZ = O_FLT_MAX; } /* resetSample */
                 const float eps = b.radius * 0.01f;
                 if (s.isInScreen) TMin = o_max(TMin, (pl - s.objectSpaceZ) * L / pl + eps);
                 if (TMin <= TMax) {

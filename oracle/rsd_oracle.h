@@ -85,6 +85,12 @@ typedef struct {
     uint32_t sd_jitter;        /* SD_JITTER */
     uint32_t guard_band;       /* frame-buffer guard band (GuardBand pass) */
     uint32_t dual_ao;          /* DUAL_AO: ao is RG8Unorm (bright, dark), 2 bytes per pixel */
+    /* the layout of librsd's rsd_svao_params continues (tests copy the common prefix): */
+    void* tile_flags_unused;   /* librsd's busy-tile flags (device only) */
+    uint32_t numerics_unused;  /* librsd's fast / exact arithmetic (the oracle is the exact one) */
+    uint32_t ao_kernel;        /* AO_KERNEL (SVAO.cpp:233, AOKernel.h): 0 VAO, 1 HBAO */
+    uint32_t primary_depth_mode; /* PRIMARY_DEPTH_MODE (DepthMode.h): 0 SingleDepth, 1 DualDepth */
+    const float* depth2;       /* DualDepth: gDepthTex2, the second linear-depth layer (W x H) */
 } osvao_params;
 
 typedef struct oscene oscene;
@@ -185,6 +191,7 @@ void ocpu_jitter(uint32_t x, uint32_t y, float* jx, float* jy);
 void ocpu_stratified_lut(int n, int32_t* indices /* n+1 */, uint32_t* lut /* 2^n */);
 void ocpu_noise_texture(uint8_t out[16]);
 float ocpu_sample_radius(uint32_t num_directions, uint32_t i);
+float ocpu_sample_radius_kernel(uint32_t num_directions, uint32_t i, uint32_t kernel); /* 0 VAO, 1 HBAO */
 uint32_t ocpu_encode_normal_2x8(const float n[3]);
 void ocpu_decode_normal_2x8(uint32_t packed, float out[3]);
 /* returns 1 on hit; outputs t, DXR barycentrics (u,v) and det */

@@ -64,6 +64,7 @@ const std::initializer_list<const char*> kImplNames = {"Default", "CoverageMask"
                                                        "KBuffer"};  // StochasticDepthImplementation.h
 const std::initializer_list<const char*> kHitOrderNames = {"Canonical", "Traversal"};  // rsd.h rsd_hit_order
 const std::initializer_list<const char*> kNumericsNames = {"Fast", "Exact"};  // rsd.h rsd_numerics
+const std::initializer_list<const char*> kAoKernelNames = {"VAO", "HBAO"};    // AOKernel.h -> rsd_ao_kernel
 
 // the SVAO passes' arithmetic when the graph does not set "numerics": RSD_NUMERICS=exact in the
 // environment selects the oracle-exact kernels (tests), otherwise the fast default (rsd.h rsd_numerics)
@@ -328,10 +329,16 @@ public:
         hitOrder_ = enumProp(p, "stochHitOrder", kHitOrderNames, 0);  // librsd extension (rsd_hit_order)
         rayPipeline_ = p.getBool("rayPipeline", true);  // SVAO.h:101
         numerics_ = enumProp(p, "numerics", kNumericsNames, defaultNumerics());  // librsd extension (rsd_numerics)
+        // AO kernel (SVAO::mKernel, a UI dropdown in the reference, SVAO.cpp:615-620; librsd accepts it as a
+        // Property).  The UI scales the radius by 1.5 when it switches to HBAO: a graph that selects HBAO
+        // gets that scaled radius unless it sets "radius" itself.
+        aoKernel_ = enumProp(p, "aoKernel", kAoKernelNames, 0);
+        if (aoKernel_ == RSD_AO_KERNEL_HBAO && !p.has("radius")) radius_ *= 1.5f;
     }
     void checkSupported() const {
-        if (primary_ != 0) throw Unsupported("SVAO: primaryDepthMode other than SingleDepth is not implemented");
-        if (secondary_ == 1) throw Unsupported("SVAO: secondaryDepthMode DualDepth is not implemented (SURVEY 8(f))");
+        if (primary_ > 1) throw Unsupported("SVAO: primaryDepthMode must be SingleDepth or DualDepth");
+        if (secondary_ == 3 && (primary_ != 0 || aoKernel_ != 0))
+            throw Unsupported("SVAO: the Raytraced secondary mode supports the VAO kernel with SingleDepth only");
         // Common.slang:51-58 holds sample radii for 8, 16 and 32 directions only
         if (directions_ != 8 && directions_ != 16 && directions_ != 32)
             throw Unsupported("SVAO: sampleCount must be 8, 16 or 32");
@@ -378,7 +385,7 @@ public:
         height_ = cd.defaultHeight;
         sdSize(width_, height_, &vao_, &sdW_, &sdH_);
         svp_ = rsd_svao_params{directions_, samples_, secondary_, (uint32_t)rayInterval_, (uint32_t)jitter_, 0,
-                               (uint32_t)dualAo_, nullptr, numerics_};
+                               (uint32_t)dualAo_, nullptr, numerics_, aoKernel_, primary_, nullptr};
         sdGraph_.reset();
         if (secondary_ != 2) return;
         // SVAO.cpp:157-189: the nested "Stochastic Depth" graph
@@ -421,6 +428,13 @@ public:
             guard = std::get<int64_t>(it->second);
         svp_.guard_band = (uint32_t)guard;
         svp_.tile_flags = nullptr;
+        svp_.d_depth2 = nullptr;
+        if (primary_ == 1) {  // DualDepth: the second depth layer (SVAO.cpp:201, gDepthTex2)
+            Texture* depth2 = rd["depth2"];
+            if (!depth2 || depth2->width != width_ || depth2->height != height_ || depth2->format != Format::R32Float)
+                throw std::runtime_error("SVAO: primaryDepthMode DualDepth needs 'depth2' (R32Float, the frame size)");
+            svp_.d_depth2 = (const float*)depth2->ptr;
+        }
         if (secondary_ == 2) {
             // busy 16x16 tiles of this pass's stencil (rsd_svao_params.tile_flags): pass 1 sets, pass 2
             // consumes; sized by the guard band of this frame, zeroed once per allocation
@@ -443,6 +457,13 @@ public:
                              (uint32_t*)rmax->ptr, sdW_, sdH_, ctx.stream),
               "SVAO AO 1");
         if (secondary_ == 0) return;  // SVAO.cpp:355
+        if (secondary_ == 1) {  // DualDepth: "AO 2" refines nothing (no calcAO2 branch); it finalizes the AO
+            check(rsd_svao_pass2(&s->camera, &vao_, &svp_, (const float*)depth->ptr, (const uint16_t*)normals->ptr,
+                                 width_, height_, (const uint8_t*)stencil->ptr, nullptr, 0, 0, (uint8_t*)ao->ptr,
+                                 ctx.stream),
+                  "SVAO AO 2 (DualDepth)");
+            return;
+        }
         if (secondary_ == 3) {  // SVAO.cpp:408-455: refine by tracing the scene
             check(rsd_svao_pass2_raytraced(s->scene, &s->camera, &vao_, &svp_, (const float*)depth->ptr,
                                            (const uint16_t*)normals->ptr, width_, height_, (const uint8_t*)stencil->ptr,
@@ -470,7 +491,8 @@ public:
 private:
     const SceneRef* scene_ = nullptr;
     float radius_, exponent_, thickness_;
-    uint32_t primary_, secondary_, divisor_, samples_, maxCount_, cull_, directions_, impl_, hitOrder_, numerics_;
+    uint32_t primary_, secondary_, divisor_, samples_, maxCount_, cull_, directions_, impl_, hitOrder_, numerics_,
+        aoKernel_ = 0;
     int32_t guardPx_;
     bool dualAo_, alphaTest_, jitter_, rayInterval_, rayPipeline_;
     uint32_t width_ = 0, height_ = 0, sdW_ = 0, sdH_ = 0;

@@ -29,12 +29,12 @@ extern "C" rsd_status rsd_svao_frame(const rsd_svao_frame_desc* f, uint32_t flag
         return RSD_ERR_INVALID_ARG;
     }
     const uint32_t mode = f->svao->secondary_depth_mode;
-    if (mode != 0 && mode != 2 && mode != 3) {
-        rsd::set_error("rsd_svao_frame: secondary_depth_mode must be 0 (SingleDepth), 2 (StochasticDepth) or 3 "
-                       "(Raytraced)");
+    if (mode > 3) {
+        rsd::set_error("rsd_svao_frame: secondary_depth_mode must be 0 (SingleDepth), 1 (DualDepth), 2 (StochasticDepth)"
+                       " or 3 (Raytraced)");
         return RSD_ERR_UNSUPPORTED;
     }
-    if (mode != 0 && (!f->scene || !f->sd)) {
+    if ((mode == 2 || mode == 3) && (!f->scene || !f->sd)) {
         rsd::set_error("rsd_svao_frame: the StochasticDepth and Raytraced modes need a scene and SD params");
         return RSD_ERR_INVALID_ARG;
     }
@@ -58,7 +58,7 @@ extern "C" rsd_status rsd_svao_frame(const rsd_svao_frame_desc* f, uint32_t flag
         if (st != RSD_OK) return st;
     }
     if ((st = record(events, 2, stream)) != RSD_OK) return st;
-    if (stochastic) {
+    if (stochastic || mode == 1) {
         st = rsd_svao_pass2(f->cam, f->vao, f->svao, f->d_depth, f->d_normals, f->width, f->height, f->d_stencil,
                             f->d_sd, f->sd_w, f->sd_h, f->d_ao, stream);
     } else if (mode == 3) {

@@ -133,23 +133,24 @@ using namespace rsd;
 namespace {
 // fill_consts of (VAOData, NUM_DIRECTIONS), cached per host thread: the ~50 double sin / cos and the
 // ssRadiusCutoff search are host work every pass-1 / pass-2 call would otherwise repeat per frame
-void cached_consts(SvaoConsts& k, const rsd_vao_data& d, uint32_t nd) {
+void cached_consts(SvaoConsts& k, const rsd_vao_data& d, uint32_t nd, uint32_t kernel) {
     struct Entry {
         rsd_vao_data d;
-        uint32_t nd;
+        uint32_t nd, kernel;
         SvaoConsts k;
     };
     thread_local Entry cache[4];
     thread_local int used = 0, next = 0;
     for (int i = 0; i < used; ++i)
-        if (cache[i].nd == nd && std::memcmp(&cache[i].d, &d, sizeof(d)) == 0) {
+        if (cache[i].nd == nd && cache[i].kernel == kernel && std::memcmp(&cache[i].d, &d, sizeof(d)) == 0) {
             k = cache[i].k;
             return;
         }
-    fill_consts(k, d, nd);
+    fill_consts(k, d, nd, kernel);
     Entry& e = cache[next];
     e.d = d;
     e.nd = nd;
+    e.kernel = kernel;
     e.k = k;
     next = (next + 1) % 4;
     used = used < 4 ? used + 1 : 4;
@@ -204,7 +205,7 @@ rsd_status pass1_impl(const rsd_camera* cam, const rsd_vao_data* vao, const rsd_
     SvaoArgs a{};
     a.cam = *cam;
     a.d = *vao;
-    cached_consts(a.k, a.d, p->num_directions);
+    cached_consts(a.k, a.d, p->num_directions, p->ao_kernel);
     {
         rsd_status ts = snap_tables(a.d, &a.snapU, &a.snapV);
         if (ts == RSD_OK) ts = normal_lut(&a.nlut);
@@ -229,6 +230,8 @@ rsd_status pass1_impl(const rsd_camera* cam, const rsd_vao_data* vao, const rsd_
     a.N = p->sd_samples;
     a.tileFlags = p->tile_flags;
     a.tilesX = tiles_x(W, p->guard_band);
+    a.dualDepth = p->primary_depth_mode == 1u ? 1u : 0u;
+    a.depth2 = p->d_depth2;
     // SVAO.cpp:347-350: nThreads = roundup32(dims - 2 guardBand), 16x16 groups
     const uint32_t nx = (W - 2 * p->guard_band + 31u) / 32u * 32u, ny = (H - 2 * p->guard_band + 31u) / 32u * 32u;
     const uint32_t groups = ny / 32u;
@@ -241,6 +244,7 @@ rsd_status pass1_impl(const rsd_camera* cam, const rsd_vao_data* vao, const rsd_
     const char* p1Env = std::getenv("RSD_PASS1");
     const uint32_t allDirs = a.k.nd == 32u ? 0xffffffffu : (1u << a.k.nd) - 1u;
     const bool spec = !(p1Env && std::strcmp(p1Env, "generic") == 0) && a.secondary == 2u && a.rayInterval &&
+                      !a.k.hbao && !a.dualDepth &&
                       a.k.samePixelInt && a.d.sdGuard > 0 && W <= 4096u && H <= 4096u &&
                       (a.k.fastDiv & allDirs) == allDirs && a.d.radius < 0x1p58f;
     const dim3 grid(nx / 16, 2 * bandGroups), block(16, 16);
@@ -287,8 +291,15 @@ rsd_status pass2_impl(const rsd_camera* cam, const rsd_vao_data* vao, const rsd_
                       rsd_stream stream) {
     rsd_status st = check_common(cam, vao, p, d_depth, d_normals, W, H, "rsd_svao_pass2");
     if (st != RSD_OK) return st;
-    if (!d_stencil || !d_sd || !d_ao || !sd_w || !sd_h) {
+    // secondary DualDepth (1) refines nothing and reads no SD map; StochasticDepth (2) needs it
+    const bool needSd = p->secondary_depth_mode != 1u;
+    if (!d_stencil || !d_ao || (needSd && (!d_sd || !sd_w || !sd_h))) {
         set_error("rsd_svao_pass2: null buffer");
+        return RSD_ERR_INVALID_ARG;
+    }
+    if (p->secondary_depth_mode != 1u && p->secondary_depth_mode != 2u) {
+        set_error("rsd_svao_pass2: secondary_depth_mode must be 2 (StochasticDepth) or 1 (DualDepth); Raytraced is "
+                  "rsd_svao_pass2_raytraced");
         return RSD_ERR_INVALID_ARG;
     }
     const uint32_t N = p->sd_samples;
@@ -299,7 +310,7 @@ rsd_status pass2_impl(const rsd_camera* cam, const rsd_vao_data* vao, const rsd_
     SvaoArgs a{};
     a.cam = *cam;
     a.d = *vao;
-    cached_consts(a.k, a.d, p->num_directions);
+    cached_consts(a.k, a.d, p->num_directions, p->ao_kernel);
     {
         rsd_status ts = snap_tables(a.d, &a.snapU, &a.snapV);
         if (ts == RSD_OK) ts = normal_lut(&a.nlut);
@@ -323,6 +334,8 @@ rsd_status pass2_impl(const rsd_camera* cam, const rsd_vao_data* vao, const rsd_
     a.N = N;
     a.tileFlags = p->tile_flags;
     a.tilesX = tiles_x(W, p->guard_band);
+    a.dualDepth = p->primary_depth_mode == 1u ? 1u : 0u;
+    a.depth2 = p->d_depth2;
     const uint32_t vw = W - 2 * p->guard_band, vh = H - 2 * p->guard_band;
     const uint32_t groups = (vh + 31u) / 32u;
     const uint32_t bandGroups = std::min(n, groups > start ? (groups - start + step - 1) / step : 0u);
@@ -335,6 +348,7 @@ rsd_status pass2_impl(const rsd_camera* cam, const rsd_vao_data* vao, const rsd_
     // the specialised kernel (8 directions; RSD_PASS2=generic forces the generic one for A/B runs)
     const char* p2Env = std::getenv("RSD_PASS2");
     const bool spec = !(p2Env && std::strcmp(p2Env, "generic") == 0) && nd == 8u && W <= 4096u && H <= 4096u &&
+                      !a.k.hbao && !a.dualDepth && a.secondary == 2u &&
                       (a.k.fastDiv & 0xffu) == 0xffu && a.d.lowResolution[0] >= 1.0f &&
                       a.d.lowResolution[0] <= 0x1p20f && a.d.lowResolution[1] >= 1.0f && a.d.lowResolution[1] <= 0x1p20f &&
                       a.d.radius < 0x1p58f;

@@ -41,21 +41,29 @@ __device__ __forceinline__ void pass1_dir_generic(const SvaoArgs& a, float u, fl
                                                  : (fabsf(u - s.ru) < d.invResolution[0] * 0.9f &&
                                                     fabsf(v - s.rv) < d.invResolution[1] * 0.9f);
     if (same) {
-        const float w = div_pdf(s.sphereStart - s.sphereEnd, s);  // isSamePixel
-        ao += w;
-        aoD += w;
+        if (SPEC || !a.k.hbao) {  // isSamePixel (SVAORaster.ps.slang:55-60: HBAO adds 0)
+            const float w = div_pdf(s.sphereStart - s.sphereEnd, s);
+            ao += w;
+            aoD += w;
+        }
         return;
     }
     // SVAORaster.ps.slang:62-66: Raytraced mode with TRACE_OUT_OF_SCREEN (SVAO.h:104)
     bool forceRay = !SPEC && a.secondary == 3u && !s.isInScreen;
     eval_primary<SPEC>(a, b, s, bf);
+    if (!SPEC && a.dualDepth) eval_dual(a, b, s, ssrAbove, false);  // SVAORaster.ps.slang:69-70
     ao += s.visibility;
     if (!s.isInScreen && (SPEC || d.sdGuard > 0)) {
         forceRay = true;
         s.objectSpaceZ = 3.402823466e+38f;
     }
-    const float constRadius = (1.0f + d.thickness) * b.radius - s.sphereStart;
-    const bool req = s.objectSpaceZ > s.sphereStart + constRadius && ssrAbove;
+    bool req;
+    if (SPEC) {
+        const float constRadius = (1.0f + d.thickness) * b.radius - s.sphereStart;
+        req = s.objectSpaceZ > s.sphereStart + constRadius && ssrAbove;
+    } else {
+        req = require_ray(a, b, s, ssrAbove);
+    }
     if (req || forceRay) {
         st |= 1u << i;
         if (SPEC || a.secondary == 2u) {
@@ -63,7 +71,9 @@ __device__ __forceinline__ void pass1_dir_generic(const SvaoArgs& a, float u, fl
             const int sy = uv_to_sd(s.sv, d.lowResolution[1], d.sdGuard);
             const size_t o = (size_t)sy * a.sdW + sx;
             if (SPEC || a.rayInterval) {
-                const float osMin = hmin(s.objectSpaceZ, b.radius + d.thickness * b.radius + s.sphereStart);
+                // SVAORaster.ps.slang:90-91
+                const float osMin = (!SPEC && a.k.hbao) ? hmin(s.objectSpaceZ, s.sphereStart)
+                                                        : hmin(s.objectSpaceZ, b.radius + d.thickness * b.radius + s.sphereStart);
                 atomicMin(&a.rayMin[o], asuint(hmax(b.posVLength - osMin, 0.0f)));
                 atomicMax(&a.rayMax[o], asuint(hmax(b.posVLength - s.sphereEnd, 0.0f)));
             } else {
@@ -110,13 +120,15 @@ __global__ void __launch_bounds__(256) svao_pass1_kernel(SvaoArgs a) {
 #pragma unroll RSD_P1_UNROLL
             for (int i = 0; i < nd; ++i) pass1_dir_generic<SPEC>(a, u, v, px, py, b, i, ao, aoD, st);
         }
-        ao *= a.k.invNd;  // SVAORaster.ps.slang:108-109
-        ao *= 2.0f;
+        ao *= a.k.invNd;  // SVAORaster.ps.slang:108-109 (x 2: VAO only)
         aoD *= a.k.invNd;
-        aoD *= 2.0f;
+        if (SPEC || !a.k.hbao) {
+            ao *= 2.0f;
+            aoD *= 2.0f;
+        }
         if ((!SPEC && a.secondary == 0u) || st == 0u) {
-            ao = acc_pow(ao, d.exponent);
-            aoD = acc_pow(aoD, d.exponent);
+            ao = SPEC ? acc_pow(ao, d.exponent) : ao_finalize(a, ao);
+            aoD = SPEC ? acc_pow(aoD, d.exponent) : ao_finalize(a, aoD);
         }
     }
     if (px < (uint32_t)a.W && py < (uint32_t)a.H) {
@@ -153,8 +165,15 @@ __device__ __forceinline__ void svao_pass2_dir(const SvaoArgs& a, const Basic& b
     Sample s;
     bool ssrAbove;
     sample_init<ALLFAST>(a, u, v, b, i, s, ssrAbove);
-    eval_primary<SPEC>(a, b, s);
+    if (!SPEC && a.dualDepth) eval_dual(a, b, s, ssrAbove, true);  // Common.slang:555-558 (force init)
+    else eval_primary<SPEC>(a, b, s);
     p = s.visibility;
+    if (!SPEC && a.secondary == 1u) {
+        // secondary DualDepth: calcAO2 has no branch for it (Common.slang:562-651), so the raster
+        // visibility is subtracted and added back unchanged
+        r = p;
+        return;
+    }
     const int cx = uv_to_sd(s.su, d.lowResolution[0], d.sdGuard);
     const int cy = uv_to_sd(s.sv, d.lowResolution[1], d.sdGuard);
     float jx, jy;
@@ -176,7 +195,16 @@ __device__ __forceinline__ void svao_pass2_dir(const SvaoArgs& a, const Basic& b
             dep[4 * l] = t.x; dep[4 * l + 1] = t.y; dep[4 * l + 2] = t.z; dep[4 * l + 3] = t.w;
         }
     }
-    if (!s.isInScreen) { s.visibility = 1.0f; s.objectSpaceZ = 3.402823466e+38f; }  // resetSample
+    if (!s.isInScreen) {  // resetSample (Common.slang:485-490)
+        s.visibility = (!SPEC && a.k.hbao) ? 0.0f : 1.0f;
+        s.objectSpaceZ = 3.402823466e+38f;
+    }
+    if (!SPEC && a.k.hbao) {  // addSample x N, HBAO: the max of saturate(HBAOKernel / pdf)
+#pragma unroll
+        for (int k = 0; k < N; ++k) add_sample(a, b, s, uv_to_view(a, su, sv, dep[k] * depthRange + depthOffset), false);
+        r = s.visibility;
+        return;
+    }
     // addSample x N (Common.slang:583-596): visibility = min over k of sphere_k + halo_k.
     // Where halo_k is exactly +0 the term is RN(y_k / pdf), monotone in y_k, so those k
     // share ONE division of their least numerator (the result is the same float).
@@ -213,7 +241,7 @@ constexpr int kP2Tile = 16;                   // pass-2 tile edge (pixels): 16 m
 constexpr int kP2Lanes = kP2Tile * kP2Tile;   // lanes per workgroup = pixels per tile
 static_assert(kP2Tile == (int)kTileEdge, "busy-tile flags are per pass-2 tile");
 // the LDS of one pass-2 tile (26 KB: 6 workgroups per CU)
-template <int ND>
+template <int ND, int NB = 16>
 struct P2Shared {
     uint32_t pix[kP2Lanes];        // active pixel slot: local index
     uint16_t pair[ND * kP2Lanes];  // pair: slot << 5 | direction
@@ -223,15 +251,15 @@ struct P2Shared {
     float p[kP2Lanes], r[kP2Lanes];
     uchar2 aoPrev[kP2Lanes];       // the pixel's pass-1 AO (bright, dark), read with the stencil
     // the pixel's BasicAOData, evaluated once per pixel, not per pair: the 16 floats pass 2 reads
-    // (posVLength, normalV, radiusInPixels stay out)
-    alignas(16) float basic[kP2Lanes][16];
+    // (posVLength, radiusInPixels stay out; normalV too, except in the generic kernels, NB = 20: HBAO)
+    alignas(16) float basic[kP2Lanes][NB];
     uint32_t nPix, nPair;
 };
 
 // One kP2Tile^2 tile whose top-left pixel is (x0, y0); flag: its busy-tile flag (cleared) or null
-template <int N, int ND, bool SPEC>
+template <int N, int ND, bool SPEC, int NB>
 __device__ __forceinline__ void pass2_tile(const SvaoArgs& a, uint32_t x0, uint32_t y0, uint8_t* flag,
-                                           P2Shared<ND>& sh) {
+                                           P2Shared<ND, NB>& sh) {
     constexpr uint32_t T = kP2Tile, L = kP2Lanes;
     const uint32_t tid = threadIdx.x;
     const rsd_vao_data& d = a.d;
@@ -277,6 +305,7 @@ __device__ __forceinline__ void pass2_tile(const SvaoArgs& a, uint32_t x0, uint3
             q[9] = b.bitangent.x; q[10] = b.bitangent.y; q[11] = b.bitangent.z;
             q[12] = b.normalO.x; q[13] = b.normalO.y; q[14] = b.normalO.z;
             q[15] = b.radius;
+            if constexpr (NB > 16) { q[16] = b.normalV.x; q[17] = b.normalV.y; q[18] = b.normalV.z; }
         }
     }
     __syncthreads();
@@ -300,7 +329,8 @@ __device__ __forceinline__ void pass2_tile(const SvaoArgs& a, uint32_t x0, uint3
             b.normalO = mk(q[12], q[13], q[14]);
             b.radius = q[15];
             b.posVLength = 0.0f;  // not read by pass 2
-            b.normalV = b.normal;
+            if constexpr (NB > 16) b.normalV = mk(q[16], q[17], q[18]);  // HBAOKernel
+            else b.normalV = b.normal;  // not read by the VAO kernel
             b.radiusInPixels = 0.0f;
             float p, r;
             if constexpr (SPEC) {
@@ -346,12 +376,12 @@ __device__ __forceinline__ void pass2_tile(const SvaoArgs& a, uint32_t x0, uint3
 template <int N, int ND, bool SPEC = false>
 __global__ void __launch_bounds__(kP2Lanes) svao_pass2_kernel(SvaoArgs a) {
     constexpr uint32_t kPerGroup = 32u / kP2Tile;  // tile rows per 32-row band group
-    __shared__ P2Shared<ND> sh;
+    __shared__ P2Shared<ND, SPEC ? 16 : 20> sh;
     const uint32_t y0 = ((blockIdx.y / kPerGroup) * a.bandCount + a.bandIndex) * 32u + (blockIdx.y % kPerGroup) * kP2Tile +
                         a.guard;
     uint8_t* flag = a.tileFlags ? a.tileFlags + ((y0 - a.guard) / kP2Tile) * a.tilesX + blockIdx.x : nullptr;
     if (flag && *flag == 0u) return;  // uniform over the workgroup
-    pass2_tile<N, ND, SPEC>(a, blockIdx.x * kP2Tile + a.guard, y0, flag, sh);
+    pass2_tile<N, ND, SPEC, SPEC ? 16 : 20>(a, blockIdx.x * kP2Tile + a.guard, y0, flag, sh);
 }
 
 // ---- host launchers of this TU's kernels (svao.hip picks the TU by rsd_svao_params.numerics)

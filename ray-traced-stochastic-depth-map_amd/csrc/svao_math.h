@@ -33,6 +33,8 @@ struct SvaoConsts {
     uint32_t samePixelInt;  // isSamePixel decided on pixel indices (fill_consts)
     uint32_t nd;            // NUM_DIRECTIONS
     float invNd;            // 1.0 / float(NUM_DIRECTIONS) (SVAORaster.ps.slang:108, Common.slang:660)
+    uint32_t hbao;          // AO_KERNEL == AO_KERNEL_HBAO (rsd_ao_kernel)
+    float pdfHbao[kMaxDirections];  // HBAO pdf of direction i: 0.9 pow(1 - sampleRadius[i], 1.5) (Common.slang:364)
 };
 
 struct SvaoArgs {
@@ -58,6 +60,8 @@ struct SvaoArgs {
     const float4* nlut;  // decode_normal_2x8 of every 16-bit code (normal_lut), same bits
     uint8_t* tileFlags;  // rsd_svao_params.tile_flags (busy 16x16 tiles) or nullptr
     uint32_t tilesX;     // tiles per row of tileFlags
+    uint32_t dualDepth;  // PRIMARY_DEPTH_MODE == DualDepth: depth2 refines the raster samples
+    const float* depth2; // gDepthTex2 (DualDepth), W x H linear depth
 };
 
 constexpr uint32_t kTileEdge = 16;  // busy-tile flag granularity = the pass-2 workgroup tile
@@ -228,6 +232,12 @@ __device__ __forceinline__ void ao_store(const SvaoArgs& a, size_t o, float brig
     if (a.dual) reinterpret_cast<uchar2*>(a.ao)[o] = make_uchar2(unorm8(bright), unorm8(dark));
     else a.ao[o] = unorm8(bright);
 }
+// Common.slang:326-330 finalize: HBAO maps the average to saturate(1 - 2 avg), then pow(exponent)
+__device__ __forceinline__ float ao_finalize(const SvaoArgs& a, float avg) {
+    if (a.k.hbao) avg = saturate(1.0f - 2.0f * avg);
+    return acc_pow(avg, a.d.exponent);
+}
+
 // pass 2's (and the Raytraced pass 2's) end of a refined pixel, SVAORaster2.ps.slang:60-64: the
 // direction sums (bright: sum of refined - raster visibility; dark: sum of refined) scaled by
 // 2 / NUM_DIRECTIONS (Common.slang:660-661), plus the pass-1 AO (prev: the pixel's (bright, dark)
@@ -235,19 +245,19 @@ __device__ __forceinline__ void ao_store(const SvaoArgs& a, size_t o, float brig
 __device__ __forceinline__ void ao_finish(const SvaoArgs& a, size_t o, float accB, float accD, uchar2 prev) {
     float vb = accB;
     vb *= a.k.invNd;
-    vb *= 2.0f;
+    if (!a.k.hbao) vb *= 2.0f;  // Common.slang:661: VAO only
     if (!a.dual) {
         vb += unorm8_to_float(prev.x);
-        a.ao[o] = unorm8(acc_pow(vb, a.d.exponent));
+        a.ao[o] = unorm8(ao_finalize(a, vb));
         return;
     }
     float vd = accD;
     vd *= a.k.invNd;
-    vd *= 2.0f;
+    if (!a.k.hbao) vd *= 2.0f;
     vb += unorm8_to_float(prev.x);
     vd += unorm8_to_float(prev.y);
     vd = hmin(vb, vd);
-    reinterpret_cast<uchar2*>(a.ao)[o] = make_uchar2(unorm8(acc_pow(vb, a.d.exponent)), unorm8(acc_pow(vd, a.d.exponent)));
+    reinterpret_cast<uchar2*>(a.ao)[o] = make_uchar2(unorm8(ao_finalize(a, vb)), unorm8(ao_finalize(a, vd)));
 }
 
 // the stencil bitmask of pixel o (one bit per direction)
@@ -360,7 +370,7 @@ __device__ __forceinline__ bool sample_init(const SvaoArgs& a, float u, float v,
         dy = radius * a.k.cosDir[i];
         sphereHeight = sqrtf(b.radius * b.radius - radius * radius);
     }
-    s.pdf = 2.0f * sphereHeight;
+    s.pdf = a.k.hbao ? a.k.pdfHbao[i] : 2.0f * sphereHeight;  // Common.slang:362-365
     s.sphereStart = sphereHeight;
     float zi;  // ALLFAST: the validity test below is one compare against the host bound ratioMin
     if (ALLFAST) {  // the pixel's divisor is in div_unscaled's range (checked with ALLFAST)
@@ -436,13 +446,44 @@ __device__ __forceinline__ float sample_visibility(const rsd_vao_data& d, float 
     return sphere + halo;
 }
 
-// Common.slang:463-483
+// Common.slang:421-430 HBAOKernel (gData.radius: the VAOData radius, not the pixel's clamped one)
+__device__ __forceinline__ float hbao_kernel(const SvaoArgs& a, const Basic& b, f3 S) {
+    const f3 V = S - b.posV;
+    const float angleTerm = saturate(dot(b.normalV, normalize(V)) - 0.1f);  // NdotVBias
+    const float distanceTerm = saturate(1.0f - dot(V, V) / (a.d.radius * a.d.radius));
+    return angleTerm * distanceTerm;
+}
+
+// Common.slang:463-483: VAO -- min of calcVisibility; HBAO -- max of saturate(HBAOKernel / pdf)
 __device__ __forceinline__ void add_sample(const SvaoArgs& a, const Basic& b, Sample& s, f3 spV, bool init) {
     const float oz = dot(spV - b.posV, b.normal);
     s.objectSpaceZ = init ? oz : hmin(s.objectSpaceZ, oz);
+    if (a.k.hbao) {
+        const float v = saturate(hbao_kernel(a, b, spV) / s.pdf);
+        s.visibility = init ? v : hmax(s.visibility, v);
+        return;
+    }
     const float vis = sample_visibility(a.d, oz, s, b.radius);
     s.visibility = init ? vis : hmin(s.visibility, vis);
 }
+
+// Common.slang:455-461 requireRay: VAO (CONST_RADIUS, Common.slang:37) or HBAO
+__device__ __forceinline__ bool require_ray(const SvaoArgs& a, const Basic& b, const Sample& s, bool ssrAbove) {
+    if (a.k.hbao) return s.objectSpaceZ > hmax(s.sphereStart, b.radius * 0.1f) && ssrAbove;
+    const float constRadius = (1.0f + a.d.thickness) * b.radius - s.sphereStart;
+    return s.objectSpaceZ > s.sphereStart + constRadius && ssrAbove;
+}
+
+// Common.slang:498-505 evalDualVisibility: the second depth layer at the raster sample's texel, only
+// where the sample still requires a ray
+__device__ __forceinline__ void eval_dual(const SvaoArgs& a, const Basic& b, Sample& s, bool ssrAbove, bool init) {
+    if (!require_ray(a, b, s, ssrAbove)) return;
+    const float z = (a.W <= 4096 && a.H <= 4096)
+                        ? a.depth2[(size_t)min(max(s.ky, 0), a.H - 1) * a.W + min(max(s.kx, 0), a.W - 1)]
+                        : tex_bilinear(a.depth2, a.W, a.H, s.ru, s.rv, false);
+    add_sample(a, b, s, uv_to_view(a, s.ru, s.rv, z), init);
+}
+
 
 // Common.slang:492-496
 template <bool SMALL = false>
@@ -469,7 +510,7 @@ inline void fill_scale(SvaoArgs& a) {
     a.pzHi = ok ? (float)(0x1p19 / hi) : 0.0f;
 }
 
-inline void fill_consts(SvaoConsts& k, const rsd_vao_data& d, uint32_t nd) {
+inline void fill_consts(SvaoConsts& k, const rsd_vao_data& d, uint32_t nd, uint32_t kernel = RSD_AO_KERNEL_VAO) {
     // SVAO.cpp:670-684 -> R8Unorm noise; Common.slang:311-312 randRotation, :357 alpha
     static const float dither[16] = {0.0f, 8.0f, 2.0f, 10.0f, 12.0f, 4.0f, 14.0f, 6.0f,
                                      3.0f, 11.0f, 1.0f, 9.0f, 15.0f, 7.0f, 13.0f, 5.0f};
@@ -498,9 +539,30 @@ inline void fill_consts(SvaoConsts& k, const rsd_vao_data& d, uint32_t nd) {
         0.878233108646881, 0.5303115209931901, 0.7032256306171377, 0.3099952198410562,
         0.7873133907642258, 0.43130429537268, 0.6190581352335289, 0.10219580968897692,
     };
+    // Common.slang:60-66 (HBAO kernel), double literals rounded to float
+    static const float hbao8[8] = {0.019897607325877215, 0.3239192018939078, 0.15013283288204182, 0.5608856339193332,
+                                   0.07874804859295396, 0.4306374970658152, 0.23159241868180838, 0.74770696488701};
+    static const float hbao16[16] = {
+        0.008364792005390745, 0.29968419137477154, 0.13131974798930376, 0.5251597224509892,
+        0.06264063727314514, 0.40226410430222115, 0.21027995621089465, 0.6906178807859765,
+        0.03303993608633204, 0.34903099295095424, 0.16956281924775551, 0.5996160679614535,
+        0.09559795810145842, 0.46040865279052423, 0.25357218870257175, 0.8218290863578166,
+    };
+    static const float hbao32[32] = {
+        0.0035168784979124203, 0.28787249889929795, 0.12214740408236834, 0.5082189968610005,
+        0.05489041689357717, 0.38854375322009427, 0.19986558164830323, 0.6656225173745592,
+        0.02630214826181389, 0.33636038195532914, 0.15977097044845298, 0.579825376399601,
+        0.08708424832212604, 0.44533522627083877, 0.24249692822679572, 0.7816464549941924,
+        0.013886447731081395, 0.3116969449839127, 0.14064876764650994, 0.5426920213922799,
+        0.07059703986067731, 0.41628837439340993, 0.22085459126773643, 0.7177502077720759,
+        0.04006955250785802, 0.36194276200351894, 0.17950859741413544, 0.6203897476558216,
+        0.10428292232859922, 0.47588885313824597, 0.2648228762567681, 0.8740952987729764,
+    };
     k.nd = nd == 16u || nd == 32u ? nd : 8u;
     k.invNd = 1.0f / (float)k.nd;
-    const float* radius = k.nd == 32u ? radius32 : k.nd == 16u ? radius16 : radius8;
+    k.hbao = kernel == RSD_AO_KERNEL_HBAO ? 1u : 0u;
+    const float* radius = k.hbao ? (k.nd == 32u ? hbao32 : k.nd == 16u ? hbao16 : hbao8)
+                                 : (k.nd == 32u ? radius32 : k.nd == 16u ? radius16 : radius8);
     for (int i = 0; i < (int)k.nd; ++i) {
         const float al = ((float)i / (float)k.nd) * 2.0f * 3.141f;  // Common.slang:357
         k.sinDir[i] = (float)std::sin((double)al);
@@ -511,6 +573,8 @@ inline void fill_consts(SvaoConsts& k, const rsd_vao_data& d, uint32_t nd) {
         k.dirDx[i] = k.dirRadius[i] * k.sinDir[i];
         k.dirDy[i] = k.dirRadius[i] * k.cosDir[i];
         k.dirHeight[i] = std::sqrt(d.radius * d.radius - k.dirRadius[i] * k.dirRadius[i]);
+        // pow of a float in double, rounded once (rsd_device.h numerics contract)
+        k.pdfHbao[i] = 0.9f * (float)std::pow((double)(1.0f - k.sampleRadius[i]), 1.5);
     }
     // sqrtf is correctly rounded and monotone: the least x with sqrtf(x) > c
     const float c = d.ssRadiusCutoff;
@@ -530,7 +594,8 @@ inline void fill_consts(SvaoConsts& k, const rsd_vao_data& d, uint32_t nd) {
         const float pdf = 2.0f * k.dirHeight[i], h = k.dirHeight[i];
         k.rcpPdf[i] = (float)(1.0 / (double)pdf);
         k.rcpHeight[i] = (float)(1.0 / (double)h);
-        const bool ok = h >= 0x1p-30f && pdf <= 0x1p30f;
+        // (HBAO divides by its own pdf and takes no div_rcp path: no fast bits)
+        const bool ok = !k.hbao && h >= 0x1p-30f && pdf <= 0x1p30f;
         if (ok) k.fastDiv |= 1u << i;
         // ratio_le_tenth(n, D) is n < M D in exact arithmetic (M D exact in double): valid iff
         // n >= M D iff n >= the least float >= M D
@@ -556,6 +621,14 @@ inline rsd_status check_common(const rsd_camera* cam, const rsd_vao_data* vao, c
         // Common.slang:51-58 holds sample radii for 8, 16 and 32 directions only
         set_error(std::string(who) + ": NUM_DIRECTIONS must be 8, 16 or 32");
         return RSD_ERR_UNSUPPORTED;
+    }
+    if (p->ao_kernel != RSD_AO_KERNEL_VAO && p->ao_kernel != RSD_AO_KERNEL_HBAO) {
+        set_error(std::string(who) + ": ao_kernel must be RSD_AO_KERNEL_VAO or RSD_AO_KERNEL_HBAO");
+        return RSD_ERR_INVALID_ARG;
+    }
+    if (p->primary_depth_mode > 1 || (p->primary_depth_mode == 1 && !p->d_depth2)) {
+        set_error(std::string(who) + ": primary_depth_mode must be 0 (SingleDepth) or 1 (DualDepth with d_depth2)");
+        return RSD_ERR_INVALID_ARG;
     }
     if (p->numerics != RSD_NUMERICS_FAST && p->numerics != RSD_NUMERICS_EXACT) {
         set_error(std::string(who) + ": numerics must be RSD_NUMERICS_FAST or RSD_NUMERICS_EXACT");

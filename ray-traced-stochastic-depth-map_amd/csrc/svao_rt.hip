@@ -276,6 +276,12 @@ extern "C" rsd_status rsd_svao_pass2_raytraced_band(rsd_scene* scene, const rsd_
         set_error("rsd_svao_pass2_raytraced: null argument or bad cull mode");
         return RSD_ERR_INVALID_ARG;
     }
+    if (p->ao_kernel != RSD_AO_KERNEL_VAO || p->primary_depth_mode != 0) {
+        // the HBAO ray (a committed closest hit, SVAORaster2.ps.slang:12-15, 42-45) and the DualDepth
+        // primary mode are implemented for the raster and StochasticDepth passes only
+        set_error("rsd_svao_pass2_raytraced: only the VAO kernel with SingleDepth primary visibility");
+        return RSD_ERR_UNSUPPORTED;
+    }
     RtArgs ra{};
     SvaoArgs& a = ra.s;
     a.cam = *cam;

@@ -84,7 +84,12 @@ class SVAOParams(C.Structure):
                 ("secondary_depth_mode", C.c_uint32), ("ray_interval", C.c_uint32),
                 ("sd_jitter", C.c_uint32), ("guard_band", C.c_uint32), ("dual_ao", C.c_uint32),
                 ("tile_flags", C.c_void_p),  # ABI v4: busy 16x16 tiles (pass 1 sets, pass 2 consumes)
-                ("numerics", C.c_uint32)]    # ABI v5: rsd_numerics of pass 1 / pass 2
+                ("numerics", C.c_uint32),    # ABI v5: rsd_numerics of pass 1 / pass 2
+                ("ao_kernel", C.c_uint32),   # ABI v5: rsd_ao_kernel (VAO / HBAO)
+                ("primary_depth_mode", C.c_uint32),  # ABI v5: 0 SingleDepth, 1 DualDepth
+                ("d_depth2", C.c_void_p)]    # ABI v5: DualDepth's second depth layer
+AO_KERNEL_VAO, AO_KERNEL_HBAO = 0, 1  # rsd.h rsd_ao_kernel
+AO_KERNELS = {"vao": AO_KERNEL_VAO, "hbao": AO_KERNEL_HBAO}
 
 
 NUMERICS_FAST, NUMERICS_EXACT = 0, 1  # rsd.h rsd_numerics

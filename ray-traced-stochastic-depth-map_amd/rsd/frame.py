@@ -46,7 +46,9 @@ class FrameConfig:
     cull_mode: int = abi.CULL_BACK
     radius: float = 0.2
     exponent: float = 2.0
-    secondary: int = abi.DEPTH_STOCHASTIC  # SVAO secondaryDepthMode: 0 Single, 2 StochasticDepth, 3 Raytraced
+    secondary: int = abi.DEPTH_STOCHASTIC  # SVAO secondaryDepthMode: 0 Single, 1 Dual, 2 StochasticDepth, 3 Raytraced
+    primary: int = abi.DEPTH_SINGLE        # SVAO primaryDepthMode: 0 Single, 1 Dual (needs Renderer.depth2)
+    ao_kernel: str = "vao"                 # SVAO AO kernel (rsd_ao_kernel): "vao" or "hbao" (SVAO.cpp:233)
     ray_pipeline: bool = True              # SVAO rayPipeline (SVAO.h:101): pass-2 extent in Raytraced mode
     alpha_test: bool = True                # SVAO alphaTest (SVAO.h:104) -> SD AlphaTest; no-op on opaque scenes
     thickness: float = 0.0
@@ -151,8 +153,11 @@ def sd_params(cfg: FrameConfig, sd_guard: int) -> abi.SDParams:
 def svao_params(cfg: FrameConfig) -> abi.SVAOParams:
     if cfg.numerics not in abi.NUMERICS:
         raise ValueError(f"numerics must be one of {sorted(abi.NUMERICS)}, not {cfg.numerics!r}")
+    if cfg.ao_kernel not in abi.AO_KERNELS:
+        raise ValueError(f"ao_kernel must be one of {sorted(abi.AO_KERNELS)}, not {cfg.ao_kernel!r}")
     return abi.SVAOParams(cfg.num_directions, cfg.sd_samples, cfg.secondary, int(cfg.ray_interval), int(cfg.jitter),
-                          cfg.guard_band, int(cfg.dual_ao), None, abi.NUMERICS[cfg.numerics])
+                          cfg.guard_band, int(cfg.dual_ao), None, abi.NUMERICS[cfg.numerics],
+                          abi.AO_KERNELS[cfg.ao_kernel], cfg.primary, None)
 
 
 class Device:
@@ -250,6 +255,9 @@ class Renderer:
         dv = torch.device("cuda", self.dev.index)
         self.depth = torch.empty((H, W), dtype=torch.float32, device=dv)
         self.normals = torch.empty((H, W), dtype=torch.int16, device=dv)
+        # DualDepth primary mode: the second depth layer (gDepthTex2; DepthPeeling / TemporalDepthPeel in
+        # the reference's graphs -- the caller fills it)
+        self.depth2 = torch.zeros((H, W), dtype=torch.float32, device=dv) if cfg.primary == abi.DEPTH_DUAL else None
         # SVAO.cpp:307 clears on first use; dualAO: RG8Unorm (bright, dark)
         self.ao = torch.zeros((H, W, 2) if cfg.dual_ao else (H, W), dtype=torch.uint8, device=dv)
         # SVAO.cpp:132-134: R8Uint / R16Uint / R32Uint for 8 / 16 / 32 directions
@@ -275,6 +283,7 @@ class Renderer:
         svp = abi.SVAOParams.from_buffer_copy(self.svp)
         # RSD_TILE_FLAGS=off: no flags (pass 2 visits every tile) -- A/B runs only
         svp.tile_flags = None if os.environ.get("RSD_TILE_FLAGS") == "off" else self.tile_flags.data_ptr()
+        svp.d_depth2 = self.depth2.data_ptr() if self.depth2 is not None else None
         self.svp = svp
 
     def frame_slot(self, own_gbuffer: bool = False) -> "Renderer":
@@ -299,6 +308,9 @@ class Renderer:
             r.cam = abi.Camera.from_buffer_copy(self.cam)
             r.depth = t.empty_like(self.depth)
             r.normals = t.empty_like(self.normals)
+            if self.depth2 is not None:
+                r.depth2 = t.empty_like(self.depth2)
+                r._bind_tile_flags()
         return r
 
     def set_pose(self, pos, target, up):

@@ -12,7 +12,9 @@ def to_oracle(struct, oracle_cls):
     struct may be a prefix of librsd's (device-only trailing fields such as rsd_svao_params.tile_flags)."""
     out = oracle_cls()
     names = [f[0] for f in type(struct)._fields_]
-    onames = [f[0] for f in oracle_cls._fields_]
+    # a field the oracle does not use keeps librsd's name with an "_unused" suffix
+    onames = [f[0].removesuffix("_unused") for f in oracle_cls._fields_]
+    names = [n.removeprefix("d_") for n in names]  # librsd's device pointers vs the oracle's host pointers
     assert names[:len(onames)] == onames, (oracle_cls, onames, names)
     assert C.sizeof(out) <= C.sizeof(struct), (oracle_cls, C.sizeof(out), C.sizeof(struct))
     C.memmove(C.byref(out), C.byref(struct), C.sizeof(out))

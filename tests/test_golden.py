@@ -24,13 +24,15 @@ def test_jitter_table_matches_reference(oracle):
 
 
 @pytest.mark.parametrize("n", [8, 16, 32])
-def test_sample_radius_matches_reference(oracle, n):
-    # SVAO/Common.slang:52-58 (NUM_DIRECTIONS = 8 / 16 / 32, VAO kernel; the shader's float constants)
-    table = GOLDEN["sampleRadius"]["VAO"][str(n)]
+@pytest.mark.parametrize("kernel", ["VAO", "HBAO"])
+def test_sample_radius_matches_reference(oracle, n, kernel):
+    # SVAO/Common.slang:52-58 (VAO) and :60-66 (HBAO), NUM_DIRECTIONS = 8 / 16 / 32 (the shader's constants)
+    table = GOLDEN["sampleRadius"][kernel][str(n)]
+    k = 0 if kernel == "VAO" else 1
     assert len(table) == n
     for i, r in enumerate(table):
-        assert oracle.sample_radius(n, i) == f32(r)
-    assert oracle.sample_radius(n, n) == 0.0  # out of range
+        assert oracle.sample_radius(n, i, k) == f32(r)
+    assert oracle.sample_radius(n, n, k) == 0.0  # out of range
 
 
 def vdc(n, base=2):

@@ -94,11 +94,11 @@ def test_reference_raytraced_svao_script_plans():
 
 
 @pytest.mark.skipif(not REF_SCRIPTS.is_dir(), reason="reference scripts not present (GPU box)")
-def test_reference_dual_depth_svao_is_reported_unsupported():
+def test_reference_dual_depth_svao_plans():
+    """scripts/SVAO_depth.py: SVAO with primaryDepthMode DualDepth (the second layer from DepthSelect) next
+    to the Raytraced reference pass -- both SVAO modes are built since round 4, so the graph plans."""
     g = next(iter(rsdgraph.load_script(REF_SCRIPTS / "SVAO_depth.py").values()))
-    with pytest.raises(abi.RsdError) as e:
-        g.plan(1920 + 128, 1080 + 128)
-    assert e.value.status == 2 and "primaryDepthMode" in str(e.value)  # SVAO primaryDepthMode DualDepth
+    g.plan(1920 + 128, 1080 + 128)
 
 
 def test_graph_errors():

@@ -298,3 +298,59 @@ def test_oracle_dual_ao(oracle):
     assert np.array_equal(ao1[..., 0], res[False][0]) and np.array_equal(ao2[..., 0], res[False][2])
     assert np.array_equal(ao1[..., 0][st == 0], ao1[..., 1][st == 0])
     assert (st != 0).any() and (ao2[..., 1] <= ao2[..., 0]).all()
+
+
+def _flat_floor_scene():
+    """One 200 x 200 quad at y = 0 under a camera looking down at 45 degrees."""
+    from rsd.scenes import Scene
+    pos = np.array([[-100, 0, -100], [100, 0, -100], [100, 0, 100], [-100, 0, 100]], np.float32)
+    ind = np.array([[0, 2, 1], [0, 3, 2]], np.uint32)
+    cam = {"pos": [0.0, 3.0, 6.0], "target": [0.0, 0.0, 0.0], "up": [0.0, 1.0, 0.0]}
+    return Scene("flat", pos, ind, np.zeros(2, np.uint32), cam)
+
+
+def test_oracle_hbao_flat_floor_is_unoccluded(oracle):
+    """HBAO (Common.slang:421-430): every sample of a flat floor lies in the pixel's tangent plane, so
+    the angle term saturate(dot(n, V) - 0.1) is 0 and the AO saturate(1 - 2 * 0)^2 = 1 everywhere."""
+    from rsd.frame import FrameConfig, make_camera, make_vao, svao_params
+    from helpers import to_oracle
+    scene = _flat_floor_scene()
+    osc = oracle.Scene(scene.positions, scene.indices, scene.flags)
+    cfg = FrameConfig(visible_w=128, visible_h=96, guard_band=16, divisor=2, sd_guard_px=64, radius=1.0,
+                      secondary=0, ao_kernel="hbao", cull_mode=0)
+    cam = to_oracle(make_camera(scene, cfg), oracle.Camera)
+    vao, sdw, sdh = make_vao(cfg)
+    z, nrm = oracle.gbuffer(osc, cam, cfg.fb_w, cfg.fb_h, 0, threads=4)
+    assert (z < 1000.0).mean() > 0.3  # the floor covers the lower part of the frame
+    ao, st, _, _ = oracle.svao_pass1(cam, to_oracle(vao, oracle.VAOData), to_oracle(svao_params(cfg), oracle.SVAOParams),
+                                     z, nrm, sdw, sdh)
+    g = cfg.guard_band
+    assert (ao[g:-g, g:-g] == 255).all()
+
+
+def test_oracle_dual_depth_equal_layers_is_single_depth(oracle):
+    """DualDepth (SVAORaster.ps.slang:69-70): a second layer equal to the first adds the same sample
+    again (min / max of equal values), so pass 1 equals the SingleDepth pass 1 bit for bit; a layer
+    behind the first changes the AO of some refined directions."""
+    import dataclasses
+    from rsd.frame import FrameConfig, make_camera, make_vao, svao_params
+    from rsd.scenes import make_scene
+    from helpers import to_oracle
+    scene = make_scene("arcade_tiny")
+    osc = oracle.Scene(scene.positions, scene.indices, scene.flags)
+    for kernel in ("vao", "hbao"):
+        cfg = FrameConfig(visible_w=160, visible_h=96, guard_band=16, divisor=2, sd_guard_px=64, radius=1.0,
+                          secondary=0, ao_kernel=kernel)
+        cam = to_oracle(make_camera(scene, cfg), oracle.Camera)
+        vao, sdw, sdh = make_vao(cfg)
+        vao = to_oracle(vao, oracle.VAOData)
+        z, nrm = oracle.gbuffer(osc, cam, cfg.fb_w, cfg.fb_h, 1, threads=4)
+        single = oracle.svao_pass1(cam, vao, to_oracle(svao_params(cfg), oracle.SVAOParams), z, nrm, sdw, sdh)
+        dcfg = dataclasses.replace(cfg, primary=1)
+        svp = to_oracle(svao_params(dcfg), oracle.SVAOParams)
+        same = oracle.svao_pass1(cam, vao, svp, z, nrm, sdw, sdh, depth2=z.copy())
+        assert np.array_equal(single[0], same[0]) and np.array_equal(single[1], same[1]), kernel
+        behind = oracle.svao_pass1(cam, vao, svp, z, nrm, sdw, sdh, depth2=z * np.float32(1.1) + np.float32(0.25))
+        assert not np.array_equal(single[0], behind[0]), kernel
+        with pytest.raises(ValueError):
+            oracle.svao_pass1(cam, vao, svp, z, nrm, sdw, sdh)  # DualDepth without the second layer
