@@ -125,6 +125,11 @@ rsd_status rsd_temporal_ao(const uint8_t* d_ao_in, const float* d_linear_z, cons
  * primary hit (from the linear depth) projected with the previous camera, prevUV - uv (RG32F). */
 rsd_status rsd_motion_vectors(const rsd_camera* cam, const rsd_camera* prev_cam, const float* d_linear_z,
                               uint32_t width, uint32_t height, float* d_mvec, rsd_stream stream);
+/* The same from GBufferRaster's non-linear depth (the GBufferRaster pass's mvec channel): linearised
+ * in-kernel like rsd_linearize_depth, background classified on the raw value (d >= 1, the cleared
+ * depth, GBufferRaster.cpp:176) -> mvec (0, 0) whatever near / far do to its linearisation. */
+rsd_status rsd_motion_vectors_raster(const rsd_camera* cam, const rsd_camera* prev_cam, const float* d_depth,
+                                     uint32_t width, uint32_t height, float* d_mvec, rsd_stream stream);
 /* ImageEquation (ImageEquation.cpp:134-160, ImageEquation.ps.slang): `formula` is the HLSL
  * expression of `float4 result = (FORMULA)` over I0..I3[xy].  Compile on the host (syntax
  * errors -> RSD_ERR_INVALID_ARG, message in rsd_last_error), run on a stream: inputs[4]

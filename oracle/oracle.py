@@ -99,6 +99,7 @@ def lib():
         L.ocpu_cross_bilateral_blur.argtypes = [vp, vp, u32, u32, vp, vp, u32, u32, u32, u32, u32]
         L.ocpu_temporal_ao.argtypes = [vp, vp, vp, vp, vp, vp, vp, u32, u32, u32, vp, vp, vp, vp]
         L.ocpu_motion_vectors.argtypes = [vp, vp, vp, u32, u32, vp]
+        L.ocpu_motion_vectors_raster.argtypes = [vp, vp, vp, u32, u32, vp]
         L.ocpu_taa.argtypes = [vp, vp, vp, u32, u32, f32, f32, u32, vp]
         L.ocpu_ao_flicker_mask.argtypes = [vp, vp, u32, u32, vp, vp]
         L.ocpu_binary_dilation.argtypes = [vp, u32, u32, u32, vp]
@@ -470,6 +471,14 @@ def motion_vectors(cam, prev_cam, linear_z):
     z = np.ascontiguousarray(linear_z, np.float32)
     out = np.zeros(z.shape + (2,), np.float32)
     lib().ocpu_motion_vectors(C.byref(cam), C.byref(prev_cam), _p(z), z.shape[1], z.shape[0], _p(out))
+    return out
+
+
+def motion_vectors_raster(cam, prev_cam, depth):
+    """GBufferRaster.mvec from the non-linear raster depth (background: d >= 1)."""
+    d = np.ascontiguousarray(depth, np.float32)
+    out = np.zeros(d.shape + (2,), np.float32)
+    lib().ocpu_motion_vectors_raster(C.byref(cam), C.byref(prev_cam), _p(d), d.shape[1], d.shape[0], _p(out))
     return out
 
 

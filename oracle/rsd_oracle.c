@@ -2083,6 +2083,18 @@ void ocpu_motion_vectors(const ocam* c, const ocam* prev, const float* z, uint32
         }
 }
 
+/* rsd_motion_vectors_raster: GBufferRaster's non-linear depth linearised like LinearizeDepth, the
+ * cleared depth (d >= 1, GBufferRaster.cpp:176) classified as background on the raw value */
+void ocpu_motion_vectors_raster(const ocam* c, const ocam* prev, const float* d, uint32_t W, uint32_t H, float* mvec)
+{
+    const size_t n = (size_t)W * H;
+    float* z = (float*)malloc(n * sizeof(float));
+    for (size_t i = 0; i < n; ++i)
+        z[i] = d[i] < 1.0f ? c->nearZ * c->farZ / (c->farZ + d[i] * (c->nearZ - c->farZ)) : INFINITY;
+    ocpu_motion_vectors(c, prev, z, W, H, mvec);
+    free(z);
+}
+
 /* ------------------------------------------------------------------ TAA
  * TAA.ps.slang:78-150 (TAA.cpp:99-124); librsd's definitions where HLSL leaves them open:
  * lerp(x, y, s) = x + s * (y - x), Load outside the texture = 0, gSampler = linear + wrap with

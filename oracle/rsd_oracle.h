@@ -213,6 +213,8 @@ void ocpu_temporal_ao(const uint8_t* aoIn, const float* z, const float* mvec, co
                       uint32_t H, uint32_t g, const ocam* cam, const float m[16], uint8_t* aoOut,
                       uint8_t* nOut);
 void ocpu_motion_vectors(const ocam* c, const ocam* prev, const float* z, uint32_t W, uint32_t H, float* mvec);
+void ocpu_motion_vectors_raster(const ocam* c, const ocam* prev, const float* depth, uint32_t W, uint32_t H,
+                                float* mvec);
 void ocpu_ao_flicker_mask(const float* z, const float* nw, uint32_t W, uint32_t H, const ocam* cam, uint8_t* mask);
 void ocpu_binary_dilation(const uint8_t* in, uint32_t W, uint32_t H, uint32_t opMax, uint8_t* out);
 void ocpu_taa(const float* color, const float* mvec, const float* prev, uint32_t W, uint32_t H, float alpha,

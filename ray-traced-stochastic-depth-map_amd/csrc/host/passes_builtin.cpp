@@ -3,7 +3,7 @@
 //
 //   GuardBand             GuardBand.cpp:38-64        dict["guardBand"]
 //   GBufferRaster         GBufferRaster.cpp:86-230   depth + faceNormalW (rsd_gbuffer_raster),
-//                                                    mvec when connected (rsd_motion_vectors)
+//                                                    mvec when connected (rsd_motion_vectors_raster)
 //   LinearizeDepth        LinearizeDepth.cpp:73-96   rsd_linearize_depth
 //   CompressNormals       CompressNormals.cpp:70-96  rsd_compress_normals (viewSpace, 16 bit)
 //   StochasticDepthMapRT  StochasticDepthMapRT.cpp   rsd_sd_trace            (the hot path)
@@ -122,7 +122,6 @@ public:
         mv.optional = true;  // GBuffer.cpp:48: mvec is an optional channel, computed only when read
         return r;
     }
-    ~GBufferRasterPass() override { (void)hipFree(linZ_); }
     void setScene(Context&, const SceneRef* s) override {
         scene_ = s;
         hasPrev_ = false;
@@ -143,19 +142,9 @@ public:
         if (!mv) return;  // nothing reads mvec: no linearize / motion-vector launches, no scratch
         if (mv->format != Format::RG32Float || mv->width != d->width || mv->height != d->height)
             throw Unsupported("GBufferRaster: mvec must be RG32Float at the depth size");
-        const size_t px = (size_t)d->width * d->height;
-        if (px > linZCap_) {
-            (void)hipFree(linZ_);
-            linZ_ = nullptr;
-            linZCap_ = 0;
-            if (hipMalloc(&linZ_, px * sizeof(float)) != hipSuccess)
-                throw std::runtime_error("GBufferRaster: mvec scratch allocation failed");
-            linZCap_ = px;
-        }
-        check(rsd_linearize_depth((const float*)d->ptr, linZ_, (uint32_t)px, scene_->camera.nearZ,
-                                  scene_->camera.farZ, ctx.stream),
-              "GBufferRaster mvec");
-        check(rsd_motion_vectors(&scene_->camera, &prev, linZ_, d->width, d->height, (float*)mv->ptr, ctx.stream),
+        // background decided on the raw raster depth (the cleared 1.0), not on its linearisation
+        check(rsd_motion_vectors_raster(&scene_->camera, &prev, (const float*)d->ptr, d->width, d->height,
+                                        (float*)mv->ptr, ctx.stream),
               "GBufferRaster mvec");
     }
     // further channels (posW, normW, ...) feed passes outside the hot path
@@ -166,8 +155,6 @@ private:
     uint32_t cull_;
     rsd_camera prevCam_{};
     bool hasPrev_ = false;
-    float* linZ_ = nullptr;
-    size_t linZCap_ = 0;
 };
 
 // ------------------------------------------------------------------------------ LinearizeDepth

@@ -417,6 +417,7 @@ __global__ void __launch_bounds__(kPostW * kPostH) temporal_ao_kernel(TaoArgs a)
 struct MvecArgs {
     rsd_camera cam, prev;
     const float* z;
+    const float* rawD;  // rsd_motion_vectors_raster: the non-linear raster depth (z unused)
     float2* mvec;
     int W, H;
     float pU[3], pV[3], pW[3];  // prev U / |U|^2, V / |V|^2, W / |W|^2
@@ -427,10 +428,22 @@ __global__ void __launch_bounds__(kPostW * kPostH) motion_vector_kernel(MvecArgs
     if (x >= a.W || y >= a.H) return;
     const rsd_camera& c = a.cam;
     const float u = ((float)x + 0.5f) / (float)a.W, v = ((float)y + 0.5f) / (float)a.H;
-    const float z = a.z[(size_t)y * a.W + x];
-    if (!(z < c.farZ)) {
-        a.mvec[(size_t)y * a.W + x] = make_float2(0.0f, 0.0f);
-        return;
+    float z;
+    if (a.rawD) {
+        // GBufferRaster's own depth: background is the cleared depth 1.0 (GBufferRaster.cpp:176), decided
+        // on the raw value -- its linearisation can round either side of farZ (near 0.1 / far 10: 9.99996)
+        const float dr = a.rawD[(size_t)y * a.W + x];
+        if (!(dr < 1.0f)) {
+            a.mvec[(size_t)y * a.W + x] = make_float2(0.0f, 0.0f);
+            return;
+        }
+        z = c.nearZ * c.farZ / (c.farZ + dr * (c.nearZ - c.farZ));  // LinearizeDepth (rsd_linearize_depth)
+    } else {
+        z = a.z[(size_t)y * a.W + x];
+        if (!(z < c.farZ)) {
+            a.mvec[(size_t)y * a.W + x] = make_float2(0.0f, 0.0f);
+            return;
+        }
     }
     const f3 wn = normalize(mk(c.W[0], c.W[1], c.W[2]));
     const f3 d = normalize(mk((2.0f * u + -1.0f) * c.U[0] + (-2.0f * v + 1.0f) * c.V[0] + c.W[0],
@@ -802,9 +815,10 @@ extern "C" rsd_status rsd_temporal_ao(const uint8_t* d_ao_in, const float* d_lin
     return e == hipSuccess ? RSD_OK : hip_fail(e, "temporal_ao_kernel launch");
 }
 
-extern "C" rsd_status rsd_motion_vectors(const rsd_camera* cam, const rsd_camera* prev_cam, const float* d_linear_z,
-                                         uint32_t width, uint32_t height, float* d_mvec, rsd_stream stream) {
-    if (!cam || !prev_cam || !d_linear_z || !d_mvec || width == 0 || height == 0) {
+namespace {
+rsd_status motion_vectors_impl(const rsd_camera* cam, const rsd_camera* prev_cam, const float* d_linear_z,
+                               const float* d_raw, uint32_t width, uint32_t height, float* d_mvec, rsd_stream stream) {
+    if (!cam || !prev_cam || !(d_linear_z || d_raw) || !d_mvec || width == 0 || height == 0) {
         set_error("rsd_motion_vectors: invalid argument");
         return RSD_ERR_INVALID_ARG;
     }
@@ -812,6 +826,7 @@ extern "C" rsd_status rsd_motion_vectors(const rsd_camera* cam, const rsd_camera
     a.cam = *cam;
     a.prev = *prev_cam;
     a.z = d_linear_z;
+    a.rawD = d_raw;
     a.mvec = reinterpret_cast<float2*>(d_mvec);
     a.W = (int)width;
     a.H = (int)height;
@@ -827,6 +842,25 @@ extern "C" rsd_status rsd_motion_vectors(const rsd_camera* cam, const rsd_camera
     hipLaunchKernelGGL(motion_vector_kernel, grid, dim3(kPostW, kPostH), 0, (hipStream_t)stream, a);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? RSD_OK : hip_fail(e, "motion_vector_kernel launch");
+}
+}  // namespace
+
+extern "C" rsd_status rsd_motion_vectors(const rsd_camera* cam, const rsd_camera* prev_cam, const float* d_linear_z,
+                                         uint32_t width, uint32_t height, float* d_mvec, rsd_stream stream) {
+    if (!d_linear_z) {
+        set_error("rsd_motion_vectors: null linear depth");
+        return RSD_ERR_INVALID_ARG;
+    }
+    return motion_vectors_impl(cam, prev_cam, d_linear_z, nullptr, width, height, d_mvec, stream);
+}
+
+extern "C" rsd_status rsd_motion_vectors_raster(const rsd_camera* cam, const rsd_camera* prev_cam, const float* d_depth,
+                                                uint32_t width, uint32_t height, float* d_mvec, rsd_stream stream) {
+    if (!d_depth) {
+        set_error("rsd_motion_vectors_raster: null depth");
+        return RSD_ERR_INVALID_ARG;
+    }
+    return motion_vectors_impl(cam, prev_cam, nullptr, d_depth, width, height, d_mvec, stream);
 }
 
 extern "C" rsd_status rsd_image_equation_run(const rsd_image_program* prog, const rsd_texture* inputs,

@@ -62,15 +62,31 @@ extern "C" rsd_status rsd_device_open(int hip_device, rsd_device** out) {
 extern "C" void rsd_device_close(rsd_device* dev) { delete dev; }
 
 namespace {
-// Host threads of the BVH build: every CPU this process may run on (its affinity mask, which is
-// what a container or `taskset` grants), or RSD_BUILD_THREADS.
+// cgroup v2 CPU quota of this process ("max 100000" = none): ceil(quota / period) CPUs, or 0
+unsigned cgroup_cpu_quota() {
+    FILE* f = std::fopen("/sys/fs/cgroup/cpu.max", "r");
+    if (!f) return 0;
+    char q[32] = {0};
+    long long period = 0;
+    const int n = std::fscanf(f, "%31s %lld", q, &period);
+    std::fclose(f);
+    if (n != 2 || period <= 0 || std::strcmp(q, "max") == 0) return 0;
+    const long long quota = std::atoll(q);
+    return quota > 0 ? (unsigned)((quota + period - 1) / period) : 0;
+}
+
+// Host threads of the BVH build: the CPUs this process may actually use -- its affinity mask (what a
+// container or `taskset` grants) capped by the cgroup CPU quota (a GPU box shows 256 CPUs under a
+// 16-CPU quota; bench.py's cpu_baseline counts cores the same way) -- or RSD_BUILD_THREADS.
 unsigned build_threads() {
     if (const char* env = std::getenv("RSD_BUILD_THREADS"))
         if (int n = std::atoi(env); n > 0) return (unsigned)n;
+    unsigned n = std::max(1u, std::thread::hardware_concurrency());
     cpu_set_t set;
     CPU_ZERO(&set);
-    if (sched_getaffinity(0, sizeof(set), &set) == 0 && CPU_COUNT(&set) > 0) return (unsigned)CPU_COUNT(&set);
-    return std::max(1u, std::thread::hardware_concurrency());
+    if (sched_getaffinity(0, sizeof(set), &set) == 0 && CPU_COUNT(&set) > 0) n = (unsigned)CPU_COUNT(&set);
+    if (const unsigned q = cgroup_cpu_quota()) n = std::min(n, q);
+    return std::max(1u, n);
 }
 }  // namespace
 

@@ -148,7 +148,7 @@ GRAPH_EXPORTS = ["rsd_graph_create", "rsd_graph_destroy", "rsd_graph_create_pass
                  "rsd_graph_get_dict_int", "rsd_graph_pass_count", "rsd_plugin_set_dir", "rsd_plugin_types",
                  "rsd_cross_bilateral_blur", "rsd_image_equation_compile", "rsd_image_equation_info",
                  "rsd_image_equation_run", "rsd_image_equation_release", "rsd_temporal_ao",
-                 "rsd_motion_vectors", "rsd_taa", "rsd_ao_flicker_mask", "rsd_binary_dilation",
+                 "rsd_motion_vectors", "rsd_motion_vectors_raster", "rsd_taa", "rsd_ao_flicker_mask", "rsd_binary_dilation",
                  "rsd_deinterleave", "rsd_interleave", "rsd_ray_min_max_length"]
 
 FMT_R32F, FMT_RG32F, FMT_RGBA32F, FMT_R16U, FMT_R8U, FMT_R8UNORM, FMT_R32U, FMT_UNKNOWN = range(8)
@@ -283,6 +283,8 @@ def lib():
         L.rsd_taa.argtypes = [vp, vp, vp, u32, u32, f32, f32, u32, vp, vp]
         L.rsd_motion_vectors.restype = st
         L.rsd_motion_vectors.argtypes = [C.POINTER(Camera), C.POINTER(Camera), vp, u32, u32, vp, vp]
+        L.rsd_motion_vectors_raster.restype = st
+        L.rsd_motion_vectors_raster.argtypes = [C.POINTER(Camera), C.POINTER(Camera), vp, u32, u32, vp, vp]
         L.rsd_image_equation_compile.restype = st
         L.rsd_image_equation_compile.argtypes = [C.c_char_p, C.POINTER(vp)]
         L.rsd_image_equation_info.restype = st

@@ -103,6 +103,34 @@ def test_motion_vectors_background_zero(torch, oracle):
     assert (mv[bg] == 0.0).all() and (np.abs(mv[~bg]).max(axis=-1) > 0).all()
 
 
+@pytest.mark.parametrize("near,far", [(0.1, 1000.0), (0.1, 10.0)])
+def test_motion_vectors_raster_background_from_raw_depth(torch, oracle, near, far):
+    """rsd_motion_vectors_raster (the GBufferRaster pass's mvec): background is the cleared raster depth
+    1.0 decided on the raw value, so it stays (0, 0) even where its linearisation lands below farZ
+    (near 0.1 / far 10: 9.99996 -- ADVICE r3); geometry bit-identical to the oracle."""
+    from rsd import abi
+    from rsd.frame import FrameConfig, look_at
+    cfg = FrameConfig(visible_w=160, visible_h=96, guard_band=16, near=near, far=far)
+    c0 = look_at((0.0, 2.0, 8.0), (0.0, 1.0, 0.0), (0.0, 1.0, 0.0), cfg)
+    c1 = look_at((0.6, 2.2, 7.5), (0.1, 1.0, 0.0), (0.0, 1.0, 0.0), cfg)
+    rng = np.random.default_rng(12)
+    d = rng.uniform(0.5, 0.99, (cfg.fb_h, cfg.fb_w)).astype(np.float32)  # non-linear depth of geometry
+    d[: cfg.fb_h // 3] = 1.0  # cleared
+    lin = (np.float32(near) * np.float32(far) / (np.float32(far) + np.float32(1.0) * (np.float32(near) -
+                                                                                       np.float32(far))))
+    if far == 10.0:
+        assert lin < np.float32(far)  # the case the linear-depth classification gets wrong
+    dt = torch.from_numpy(d).cuda()
+    mv = torch.zeros((cfg.fb_h, cfg.fb_w, 2), dtype=torch.float32, device="cuda")
+    abi.check(abi.lib().rsd_motion_vectors_raster(C.byref(c1), C.byref(c0), _p(dt), cfg.fb_w, cfg.fb_h, _p(mv),
+                                                  C.c_void_p(torch.cuda.current_stream().cuda_stream)),
+              "rsd_motion_vectors_raster")
+    got = mv.cpu().numpy()
+    want = oracle.motion_vectors_raster(to_oracle(c1, oracle.Camera), to_oracle(c0, oracle.Camera), d)
+    assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
+    assert (got[: cfg.fb_h // 3] == 0.0).all() and (np.abs(got[cfg.fb_h // 3:]).max(axis=-1) > 0).all()
+
+
 def test_temporal_sequence_parity_and_accumulation(torch, oracle):
     """Four poses of a slowly moving camera: each frame's motion vectors and TemporalAO output
     equal the oracle's, and the history grows where the reprojection holds."""

@@ -198,3 +198,17 @@ def test_ray_min_max_length_oracle():
     mx[1] = 0
     got = ray_min_max_length(mn, mx)
     assert got.tolist() == [1.0, 0.0, 0.0, 0.0, 0.0, 0.0]
+
+
+def test_motion_vectors_raster_near_far_ten(oracle):
+    """The raster variant classifies the cleared depth 1.0 as background on the raw value: with near
+    0.1 / far 10 its linearisation (9.99996) is below farZ and the linear-depth variant would move it."""
+    c0 = _cam(oracle, pos=(0.0, 2.0, 8.0), target=(0.0, 1.0, 0.0))
+    c1 = _cam(oracle, pos=(0.5, 2.3, 7.0), target=(0.2, 1.0, 0.0))
+    c0.nearZ, c0.farZ, c1.nearZ, c1.farZ = 0.1, 10.0, 0.1, 10.0
+    d = np.full((64, 96), 0.9, F)
+    d[:20] = 1.0
+    mv = oracle.motion_vectors_raster(c1, c0, d)
+    assert (mv[:20] == 0.0).all() and (np.abs(mv[20:]).max(axis=-1) > 0).all()
+    lin = oracle.linearize_depth(d, 0.1, 10.0)
+    assert (lin[:20] < 10.0).all()  # the linear depth alone cannot tell the cleared depth from geometry
