@@ -1,0 +1,150 @@
+#!/usr/bin/env python3
+"""Predicted per-rank frame time of the N > 1 band split (rsd/shard.py HaloFrame) from measurements
+on ONE GPU (a model the driver's 8-GPU run can be judged against).
+
+For a config and N in --worlds, on the real frame (fast numerics, the product default):
+
+  * per rank k of HaloFrame's first (equal-groups) split: the GPU time of its pass 1
+    (rsd_svao_pass1_rows), its SD trace given the 1-GPU interval union (rsd_sd_trace_rows) and its
+    pass 2 given the 1-GPU SD map (rsd_svao_pass2_rows), each the median of --reps runs between
+    fence-free HIP events, one launch in flight;
+  * the bytes it sends per frame (sparse interval triples to the bands it touches, the depths it
+    returns, its AO band), as tools/halo_plan.py computes them;
+  * the host time of HaloFrame.front() + back() for that rank with the collectives stubbed out (the
+    Python + torch + librsd issue cost of one frame; the results of those frames are not used).
+
+Model (stated assumptions, checked by the driver's run): one frame in flight,
+  T(N) = max_k (pass1_k + trace_k + pass2_k) + 4 x L_coll + max_k bytes_k / B_link
+with L_coll = 12 us per small collective / point-to-point round (--coll-us) and B_link = 50 GB/s
+per xGMI peer link (--link-gbs); with F frames in flight the GPU part overlaps across frames as at
+N = 1 (factor --overlap = ms_per_step(F = 4) / one-frame GPU time, measured at N = 1 here), and the
+frame rate is bounded by max(overlapped GPU time, host issue time).
+usage: python tools/scaling_model.py [config] [--worlds 2,4,8] [--reps 15] [--pose i]"""
+import json
+import statistics
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path[:0] = [str(ROOT), str(ROOT / "ray-traced-stochastic-depth-map_amd")]
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+from rsd.frame import CONFIGS, DEFAULT_CAMERA_PATH, FrameConfig, Renderer, camera_path  # noqa: E402
+from rsd.scenes import make_scene  # noqa: E402
+from rsd.shard import FLT_MAX_BITS, HaloFrame  # noqa: E402
+from rsd.timing import TimingEvent  # noqa: E402
+
+
+def arg(flag, default):
+    return sys.argv[sys.argv.index(flag) + 1] if flag in sys.argv else default
+
+
+name = next((a for a in sys.argv[1:] if not a.startswith("--") and a in CONFIGS), "suntemple_1080p_q")
+worlds = [int(x) for x in arg("--worlds", "2,4,8").split(",")]
+reps = int(arg("--reps", "15"))
+pose = int(arg("--pose", "0"))
+coll_us, link_gbs = float(arg("--coll-us", "12")), float(arg("--link-gbs", "50"))
+kw, sc = CONFIGS[name]
+r = Renderer(make_scene(sc), FrameConfig(**kw))
+poses = camera_path(DEFAULT_CAMERA_PATH.get(name, "static"))
+if poses:
+    r.set_pose(*poses[pose % len(poses)])
+r.gbuffer()
+N = r.cfg.sd_samples
+
+
+def timed(fn, prep=None):
+    ts = []
+    for _ in range(reps):
+        if prep:
+            prep()
+        a, b = TimingEvent(), TimingEvent()
+        a.record()
+        fn()
+        b.record()
+        torch.cuda.synchronize()
+        ts.append(a.elapsed_time(b) * 1e3)
+    return statistics.median(ts)
+
+
+# the 1-GPU frame: interval union, stencil, SD map
+for _ in range(3):
+    r.frame()
+r.clear_intervals()
+r.pass1()
+torch.cuda.synchronize()
+union = r.ray_minmax.clone()
+r.sd_trace()
+torch.cuda.synchronize()
+sd_full = r.sd.clone()
+one = {"pass1_us": timed(r.pass1, r.clear_intervals),
+       "trace_us": timed(lambda: r.sd_trace(), lambda: r.ray_minmax.copy_(union)),
+       "pass2_us": timed(r.pass2, lambda: (r.clear_intervals(), r.pass1()))}
+one["gpu_us"] = one["pass1_us"] + one["trace_us"] + one["pass2_us"]
+overlap = float(arg("--overlap", "0") or 0) or None
+
+dist.get_backend = lambda pg=None: "gloo"  # plans only: no process group
+
+
+class NoComm:
+    """Collectives stubbed out: host issue cost only (frame results unused)."""
+    nccl = False
+
+    def all_gather(self, out, inp):
+        out[0].copy_(inp.view(out[0].shape))
+
+    def exchange(self, sends, recvs):
+        pass
+
+
+out = {"config": name, "pose": pose, "reps": reps, "one_gpu": {k: round(v, 2) for k, v in one.items()},
+       "assumptions": {"coll_us": coll_us, "link_gbs": link_gbs, "collectives_per_frame": 4}, "worlds": {}}
+for world in worlds:
+    plans = [HaloFrame(r, k, world, rebalance=False) for k in range(world)]
+    ranks = []
+    touched = []
+    for k, p in enumerate(plans):
+        r.clear_intervals()
+        r.pass1_rows(p.px_rows[k])
+        m = (r.ray_minmax[0] != FLT_MAX_BITS) | (r.ray_minmax[1] != 0)
+        touched.append([int(m[lo:hi].sum()) if j != k else 0 for j, (lo, hi) in enumerate(p.sd_rows)])
+    for k, p in enumerate(plans):
+        t1 = timed(lambda: r.pass1_rows(p.px_rows[k]), r.clear_intervals)
+        r.sd.copy_(sd_full)
+        t2 = timed(lambda: r.sd_trace_rows(p.sd_rows[k]), lambda: r.ray_minmax.copy_(union))
+        r.sd.copy_(sd_full)
+        t3 = timed(lambda: r.pass2_rows(p.px_rows[k]), lambda: (r.clear_intervals(), r.pass1()))
+        iv = 12 * sum(touched[k])
+        sdb = 4 * N * sum(touched[j][k] for j in range(world))
+        ao = p.ao_max * r.ao[0].numel() * r.ao.element_size()
+        ranks.append({"pass1_us": round(t1, 2), "trace_us": round(t2, 2), "pass2_us": round(t3, 2),
+                      "gpu_us": round(t1 + t2 + t3, 2), "bytes": iv + sdb + ao,
+                      "px_rows": p.px_rows[k], "sd_rows": p.sd_rows[k]})
+    # host issue of one rank's frame (rank 0 and the middle rank), collectives stubbed
+    host = []
+    for k in sorted({0, world // 2}):
+        f = HaloFrame(r, k, world, rebalance=False, comm=NoComm())
+        for _ in range(3):
+            f.front()
+            f.back()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        n = 20
+        for _ in range(n):
+            f.front()
+            f.back()
+        host.append((time.perf_counter() - t0) / n * 1e6)
+        torch.cuda.synchronize()
+    gpu = max(x["gpu_us"] for x in ranks)
+    xfer = max(x["bytes"] for x in ranks) / (link_gbs * 1e3)  # bytes / (GB/s) in us
+    lat = gpu + 4 * coll_us + xfer
+    out["worlds"][str(world)] = {
+        "ranks": ranks, "max_rank_gpu_us": round(gpu, 2), "max_rank_bytes": max(x["bytes"] for x in ranks),
+        "host_issue_us_per_frame": round(max(host), 1),
+        "predicted_latency_us": round(lat, 1),
+        "predicted_speedup_latency": round((one["gpu_us"]) / lat, 2),
+        "note": "latency = max-rank GPU time + 4 collective latencies + max-rank bytes / link bandwidth; with "
+                "frames in flight the frame interval is bounded below by host_issue_us_per_frame"}
+print(json.dumps(out))
