@@ -57,7 +57,8 @@ for p in (str(ROOT), str(PKG)):
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8 TB/s (spec)
 DEFAULT_CONFIG = "suntemple_1080p_q"
 # committed rocprofv3 passes of the default bench (newest round first)
-PROFILE_DIRS = [ROOT / "profiles" / "round3", ROOT / "profiles" / "round2", ROOT / "profiles" / "round1"]
+PROFILE_DIRS = [ROOT / "profiles" / "round4", ROOT / "profiles" / "round3", ROOT / "profiles" / "round2",
+                ROOT / "profiles" / "round1"]
 
 
 def parse():
@@ -309,10 +310,16 @@ def main():
     kernels_seq = abi.WALK_KERNELS[walk_seq]
     lat = latency_floor(cnt_seq, seq_sd_ms)
     pmc = args.pmc_csv
-    if pmc is None and args.config == DEFAULT_CONFIG and not poses and not args.scene_file:
+    if pmc is None and not args.scene_file:
+        # the committed passes of this config (tools/config_measure.sh -> profiles/roundN/configs/<config>/),
+        # or of the default config (tools/round_measure.sh -> profiles/roundN/)
         for d in PROFILE_DIRS:
-            cand = [d / "pmc_fetch_size.csv", d / "pmc_write_size.csv"]
-            if all(p.exists() for p in cand):
+            dd = d / "configs" / args.config
+            cands = [[dd / "pmc_fetch_size.csv", dd / "pmc_write_size.csv"]]
+            if args.config == DEFAULT_CONFIG and not poses:
+                cands.append([d / "pmc_fetch_size.csv", d / "pmc_write_size.csv"])
+            cand = next((c for c in cands if all(p.exists() for p in c)), None)
+            if cand:
                 pmc = [str(p) for p in cand]
                 break
     pmc = [p for p in (pmc or []) if Path(p).exists()]
@@ -473,11 +480,13 @@ def latency_floor(cnts, trace_ms):
 
 def pmc_traffic(csv_paths, kernel_substrs):
     """HBM bytes of one SD trace from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (KB units;
-    FETCH_SIZE doubled on gfx950 per MI355X_MICROARCH.md section HBM): per kernel, the mean over
-    its launches (the instrumented counter launches excluded); summed over the kernels of ONE
-    trace of the given walk."""
+    FETCH_SIZE doubled on gfx950 per MI355X_MICROARCH.md section HBM): per kernel, the median over
+    its launches (the instrumented counter launches of the row walk -- CNT = true in its name --
+    excluded; the quad walk's instrumented launches are a minority the median ignores); summed over
+    the kernels of ONE trace of the given walk."""
     import csv
     import re
+    import statistics
     if not csv_paths:
         return None
     per = {}  # (kernel, counter) -> values
@@ -486,13 +495,16 @@ def pmc_traffic(csv_paths, kernel_substrs):
             for row in csv.DictReader(f):
                 name = row.get("Kernel_Name", "")
                 k = next((s for s in kernel_substrs if s in name), None)
-                if k is None or re.search(r", (true|false), true>", name):  # skip the instrumented launch
+                if k is None:
                     continue
+                m = re.search(r"sd_trace_row_kernel<([^>]*)>", name)
+                if m and [x.strip() for x in m.group(1).split(",")][4:5] == ["true"]:
+                    continue  # the instrumented row walk (template parameter CNT)
                 per.setdefault((k, row.get("Counter_Name")), []).append(float(row.get("Counter_Value", 0)))
     if not per:
         return None
-    mean = lambda k, c: (sum(per[(k, c)]) / len(per[(k, c)])) if (k, c) in per else 0.0  # noqa: E731
-    return int(sum(2 * mean(k, "FETCH_SIZE") + mean(k, "WRITE_SIZE") for k in kernel_substrs) * 1024)
+    med = lambda k, c: statistics.median(per[(k, c)]) if (k, c) in per else 0.0  # noqa: E731
+    return int(sum(2 * med(k, "FETCH_SIZE") + med(k, "WRITE_SIZE") for k in kernel_substrs) * 1024)
 
 
 # VALU issue peak of MI355X (MI355X_MICROARCH.md: a wave64 VALU instruction issues over 2 cycles,
