@@ -165,12 +165,15 @@ typedef struct {
     uint32_t guard_band;           /* dict["guardBand"] from the GuardBand pass */
     uint32_t dual_ao;              /* DUAL_AO (SVAO dualAO, SVAO.cpp:130): d_ao is RG8Unorm -- R bright, G dark
                                       (SVAORaster.ps.slang:103, SVAORaster2.ps.slang:62), 2 bytes per pixel */
-    uint8_t* tile_flags;           /* ABI v4, optional (NULL = none): busy-tile flags, one byte per 16x16 tile
-                                      of the visible region (rsd_svao_tile_count), caller-owned, zeroed once.
-                                      Pass 1 sets the flag of every tile holding a stencilled pixel; pass 2
-                                      visits only flagged tiles and clears the flags it consumed (the
-                                      reference's pass 2 returns on aoMask == 0, SVAORaster2.ps.slang:50-52).
-                                      Pass 2 must get the flags of the pass 1 that wrote d_stencil. */
+    uint8_t* tile_flags;           /* ABI v4 (layout v5), optional (NULL = none): busy-tile state of the 16x16
+                                      tiles of the visible region, rsd_svao_tile_count bytes, caller-owned,
+                                      zeroed once.  Pass 1 flags every tile holding a stencilled pixel and
+                                      appends it to a list; a whole-frame pass 2 walks the list (no workgroup
+                                      for an empty tile), a band / row-range pass 2 visits the flagged tiles
+                                      of its rows; both clear what they consumed, so the buffer is clean for
+                                      the next pass 1 (the reference's pass 2 returns on aoMask == 0,
+                                      SVAORaster2.ps.slang:50-52).  Pass 2 must get the buffer of the pass 1
+                                      that wrote d_stencil. */
     uint32_t numerics;             /* ABI v5: rsd_numerics of pass 1 and pass 2 (DESIGN.md 2 "Numerics") */
     uint32_t ao_kernel;            /* ABI v5: AO_KERNEL (SVAO.cpp:233, AOKernel.h): rsd_ao_kernel */
     uint32_t primary_depth_mode;   /* ABI v5: PRIMARY_DEPTH_MODE (SVAO.cpp:222, DepthMode.h): 0 SingleDepth,
@@ -194,8 +197,9 @@ typedef enum { RSD_AO_KERNEL_VAO = 0, RSD_AO_KERNEL_HBAO = 1 } rsd_ao_kernel;
  *   EXACT  binary32 round-to-nearest operation by operation, correctly rounded '/' and sqrt: bit-identical
  *          to the CPU oracle (oracle/rsd_oracle.c), at a higher instruction count. */
 typedef enum { RSD_NUMERICS_FAST = 0, RSD_NUMERICS_EXACT = 1 } rsd_numerics;
-/* Bytes of rsd_svao_params.tile_flags for a width x height frame buffer with guard_band: one per 16x16
- * tile of the visible region rounded up to 32 rows (the padded pass-1 dispatch, SVAO.cpp:347-350). */
+/* Bytes of rsd_svao_params.tile_flags for a width x height frame buffer with guard_band: for the T 16x16
+ * tiles of the visible region rounded up to 32 rows (the padded pass-1 dispatch, SVAO.cpp:347-350), T flag
+ * words, a 16-byte list header and T list entries (8 T + 16 bytes; ABI v4 had T bytes). */
 uint32_t rsd_svao_tile_count(uint32_t width, uint32_t height, uint32_t guard_band);
 
 /* Traversal counters of the last instrumented trace (roofline bytes) */

@@ -48,7 +48,8 @@ __global__ void clear_intervals_kernel(uint32_t* rmin, uint32_t* rmax, uint32_t 
 namespace rsd {
 namespace fast {  // svao_fast.hip: the same kernels with fast numerics (RSD_NUMERICS_FAST)
 void launch_pass1(const SvaoArgs& a, int variant, dim3 grid, dim3 block, hipStream_t s);
-void launch_pass2(const SvaoArgs& a, uint32_t N, uint32_t nd, bool spec, dim3 grid, dim3 block, hipStream_t s);
+void launch_pass2(const SvaoArgs& a, uint32_t N, uint32_t nd, bool spec, dim3 grid, dim3 block, hipStream_t s,
+                  bool list);
 }  // namespace fast
 }  // namespace rsd
 
@@ -159,7 +160,7 @@ void cached_consts(SvaoConsts& k, const rsd_vao_data& d, uint32_t nd, uint32_t k
 
 extern "C" uint32_t rsd_svao_tile_count(uint32_t width, uint32_t height, uint32_t guard_band) {
     if (2 * guard_band >= width || 2 * guard_band >= height) return 0u;
-    return tiles_x(width, guard_band) * tiles_y(height, guard_band);
+    return tile_buffer_bytes(tiles_x(width, guard_band) * tiles_y(height, guard_band));
 }
 
 extern "C" rsd_status rsd_svao_clear_intervals(uint32_t* d_ray_min, uint32_t* d_ray_max, uint32_t count,
@@ -228,7 +229,8 @@ rsd_status pass1_impl(const rsd_camera* cam, const rsd_vao_data* vao, const rsd_
     a.rayInterval = p->ray_interval;
     a.sdJitter = p->sd_jitter;
     a.N = p->sd_samples;
-    a.tileFlags = p->tile_flags;
+    tile_layout(p->tile_flags, tiles_x(W, p->guard_band) * tiles_y(H, p->guard_band), a.tileFlags, a.tileCount,
+                a.tileList);
     a.tilesX = tiles_x(W, p->guard_band);
     a.dualDepth = p->primary_depth_mode == 1u ? 1u : 0u;
     a.depth2 = p->d_depth2;
@@ -332,7 +334,8 @@ rsd_status pass2_impl(const rsd_camera* cam, const rsd_vao_data* vao, const rsd_
     a.rayInterval = p->ray_interval;
     a.sdJitter = p->sd_jitter;
     a.N = N;
-    a.tileFlags = p->tile_flags;
+    tile_layout(p->tile_flags, tiles_x(W, p->guard_band) * tiles_y(H, p->guard_band), a.tileFlags, a.tileCount,
+                a.tileList);
     a.tilesX = tiles_x(W, p->guard_band);
     a.dualDepth = p->primary_depth_mode == 1u ? 1u : 0u;
     a.depth2 = p->d_depth2;
@@ -352,8 +355,16 @@ rsd_status pass2_impl(const rsd_camera* cam, const rsd_vao_data* vao, const rsd_
                       (a.k.fastDiv & 0xffu) == 0xffu && a.d.lowResolution[0] >= 1.0f &&
                       a.d.lowResolution[0] <= 0x1p20f && a.d.lowResolution[1] >= 1.0f && a.d.lowResolution[1] <= 0x1p20f &&
                       a.d.radius < 0x1p58f;
-    if (p->numerics == RSD_NUMERICS_EXACT) exact::launch_pass2(a, N, nd, spec, grid, block, s);
-    else fast::launch_pass2(a, N, nd, spec, grid, block, s);
+    // the whole frame with busy-tile flags: walk pass 1's list of busy tiles with a third of the tile
+    // count in workgroups (a workgroup takes a second tile only beyond 33 % busy tiles; configs[1]: 21 %)
+    // instead of one workgroup per tile (RSD_PASS2_LIST=off: the flag grid, A/B runs)
+    const uint32_t T = tiles_x(W, p->guard_band) * tiles_y(H, p->guard_band);
+    const char* listEnv = std::getenv("RSD_PASS2_LIST");
+    const bool list = a.tileFlags && start == 0u && step == 1u && bandGroups == groups &&
+                      !(listEnv && std::strcmp(listEnv, "off") == 0);
+    if (list) grid = dim3(std::min(T, std::max(256u, (T + 2u) / 3u)));
+    if (p->numerics == RSD_NUMERICS_EXACT) exact::launch_pass2(a, N, nd, spec, grid, block, s, list);
+    else fast::launch_pass2(a, N, nd, spec, grid, block, s, list);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? RSD_OK : hip_fail(e, "svao_pass2_kernel launch");
 }

@@ -145,7 +145,11 @@ __global__ void __launch_bounds__(256) svao_pass1_kernel(SvaoArgs a) {
         const bool vote = st != 0u && ox < (uint32_t)a.W - 2u * a.guard && oy < (uint32_t)a.H - 2u * a.guard;
         const uint64_t mL = __ballot(vote && threadIdx.x < 8u), mR = __ballot(vote && threadIdx.x >= 8u);
         const uint32_t lane = __lane_id();
-        if ((lane == 0u && mL) || (lane == 8u && mR)) a.tileFlags[(oy / kTileEdge) * a.tilesX + ox / kTileEdge] = 1u;
+        if ((lane == 0u && mL) || (lane == 8u && mR)) {
+            // the first wave to flag a tile appends it to the busy-tile list pass 2 walks
+            const uint32_t t = (oy / kTileEdge) * a.tilesX + ox / kTileEdge;
+            if (atomicExch(&a.tileFlags[t], 1u) == 0u) a.tileList[atomicAdd(a.tileCount, 1u)] = t;
+        }
     }
 }
 
@@ -258,7 +262,7 @@ struct P2Shared {
 
 // One kP2Tile^2 tile whose top-left pixel is (x0, y0); flag: its busy-tile flag (cleared) or null
 template <int N, int ND, bool SPEC, int NB>
-__device__ __forceinline__ void pass2_tile(const SvaoArgs& a, uint32_t x0, uint32_t y0, uint8_t* flag,
+__device__ __forceinline__ void pass2_tile(const SvaoArgs& a, uint32_t x0, uint32_t y0, uint32_t* flag,
                                            P2Shared<ND, NB>& sh) {
     constexpr uint32_t T = kP2Tile, L = kP2Lanes;
     const uint32_t tid = threadIdx.x;
@@ -379,9 +383,43 @@ __global__ void __launch_bounds__(kP2Lanes) svao_pass2_kernel(SvaoArgs a) {
     __shared__ P2Shared<ND, SPEC ? 16 : 20> sh;
     const uint32_t y0 = ((blockIdx.y / kPerGroup) * a.bandCount + a.bandIndex) * 32u + (blockIdx.y % kPerGroup) * kP2Tile +
                         a.guard;
-    uint8_t* flag = a.tileFlags ? a.tileFlags + ((y0 - a.guard) / kP2Tile) * a.tilesX + blockIdx.x : nullptr;
-    if (flag && *flag == 0u) return;  // uniform over the workgroup
-    pass2_tile<N, ND, SPEC, SPEC ? 16 : 20>(a, blockIdx.x * kP2Tile + a.guard, y0, flag, sh);
+    uint32_t* flag = a.tileFlags ? a.tileFlags + ((y0 - a.guard) / kP2Tile) * a.tilesX + blockIdx.x : nullptr;
+    if (!flag || *flag != 0u) pass2_tile<N, ND, SPEC, SPEC ? 16 : 20>(a, blockIdx.x * kP2Tile + a.guard, y0, flag, sh);
+    if (flag && threadIdx.x == 0) {
+        // this pass consumed the flags, not the list pass 1 also appended: the last workgroup resets it
+        const uint32_t k = __hip_atomic_fetch_add(a.tileCount + 1, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        if (k == gridDim.x * gridDim.y - 1u) {
+            __hip_atomic_store(a.tileCount, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(a.tileCount + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
+// Whole-frame pass 2 over the busy-tile list pass 1 appended (tile_flags, ABI v5): gridDim.x workgroups
+// stride over the list, so no workgroup is dispatched for an empty tile -- the flag-grid kernel above
+// dispatches one per tile of the frame (8160 at configs[1], 21 % busy), and each holds its 26 KB of LDS
+// until its flag load returns.  The workgroup that finishes last resets the list for the next pass 1.
+template <int N, int ND, bool SPEC = false>
+__global__ void __launch_bounds__(kP2Lanes) svao_pass2_list_kernel(SvaoArgs a) {
+    __shared__ P2Shared<ND, SPEC ? 16 : 20> sh;
+    __shared__ uint32_t sCount;
+    if (threadIdx.x == 0) sCount = __hip_atomic_load(a.tileCount, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const uint32_t n = sCount;
+    for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
+        const uint32_t t = a.tileList[i];
+        pass2_tile<N, ND, SPEC, SPEC ? 16 : 20>(a, (t % a.tilesX) * kP2Tile + a.guard, (t / a.tilesX) * kP2Tile + a.guard,
+                                                a.tileFlags + t, sh);
+        __syncthreads();  // the tile's LDS is reused by the next one
+    }
+    if (threadIdx.x == 0) {
+        // every workgroup read the count before its ticket: the last ticket may reset the list
+        const uint32_t k = __hip_atomic_fetch_add(a.tileCount + 1, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        if (k == gridDim.x - 1u) {
+            __hip_atomic_store(a.tileCount, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(a.tileCount + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
 }
 
 // ---- host launchers of this TU's kernels (svao.hip picks the TU by rsd_svao_params.numerics)
@@ -392,13 +430,21 @@ void launch_pass1(const SvaoArgs& a, int variant, dim3 grid, dim3 block, hipStre
     else hipLaunchKernelGGL((svao_pass1_kernel<false, 0>), grid, block, 0, s, a);
 }
 
-// pass 2: N SD samples, nd directions; spec: the specialised 8-direction kernel
-void launch_pass2(const SvaoArgs& a, uint32_t N, uint32_t nd, bool spec, dim3 grid, dim3 block, hipStream_t s) {
+// pass 2: N SD samples, nd directions; spec: the specialised 8-direction kernel; list: the busy-tile
+// list kernel (grid.x workgroups striding over the list) instead of one workgroup per tile
+void launch_pass2(const SvaoArgs& a, uint32_t N, uint32_t nd, bool spec, dim3 grid, dim3 block, hipStream_t s,
+                  bool list) {
+#define RSD_P2K(K, NN, D, SP) hipLaunchKernelGGL((K<NN, D, SP>), grid, block, 0, s, a)
 #define RSD_P2(NN)                                                                                           \
-    if (nd == 32u) hipLaunchKernelGGL((svao_pass2_kernel<NN, 32>), grid, block, 0, s, a);                  \
-    else if (nd == 16u) hipLaunchKernelGGL((svao_pass2_kernel<NN, 16>), grid, block, 0, s, a);             \
-    else if (spec) hipLaunchKernelGGL((svao_pass2_kernel<NN, 8, true>), grid, block, 0, s, a);             \
-    else hipLaunchKernelGGL((svao_pass2_kernel<NN, 8>), grid, block, 0, s, a);
+    if (list) {                                                                                              \
+        if (nd == 32u) RSD_P2K(svao_pass2_list_kernel, NN, 32, false);                                       \
+        else if (nd == 16u) RSD_P2K(svao_pass2_list_kernel, NN, 16, false);                                  \
+        else if (spec) RSD_P2K(svao_pass2_list_kernel, NN, 8, true);                                          \
+        else RSD_P2K(svao_pass2_list_kernel, NN, 8, false);                                                   \
+    } else if (nd == 32u) RSD_P2K(svao_pass2_kernel, NN, 32, false);                                         \
+    else if (nd == 16u) RSD_P2K(svao_pass2_kernel, NN, 16, false);                                           \
+    else if (spec) RSD_P2K(svao_pass2_kernel, NN, 8, true);                                                   \
+    else RSD_P2K(svao_pass2_kernel, NN, 8, false);
     switch (N) {
         case 1: RSD_P2(1) break;
         case 2: RSD_P2(2) break;
@@ -407,6 +453,7 @@ void launch_pass2(const SvaoArgs& a, uint32_t N, uint32_t nd, bool spec, dim3 gr
         default: RSD_P2(16) break;
     }
 #undef RSD_P2
+#undef RSD_P2K
 }
 
 }  // namespace RSD_SVAO_NS

@@ -517,10 +517,14 @@ def test_busy_tile_flags(device, oracle, torch_dev, nd, visible):
     r.clear_intervals()
     r.pass1()
     g = r.numpy()
-    flags = r.tile_flags.cpu().numpy()
+    buf = r.tile_flags.cpu().numpy().view(np.uint32)
     g_, vw, vh = cfg.guard_band, cfg.visible_w, cfg.visible_h
     tx, ty = (vw + 15) // 16, (vh + 31) // 32 * 32 // 16
-    assert flags.size == tx * ty
+    T = tx * ty
+    assert buf.size == 2 * T + 4  # T flag words, {count, ticket, -, -}, T list entries (ABI v5)
+    flags, count, lst = buf[:T], int(buf[T]), buf[T + 4:T + 4 + int(buf[T])]
+    # the list holds every flagged tile once
+    assert count == int(flags.sum()) and sorted(lst.tolist()) == np.flatnonzero(flags).tolist()
     st = np.zeros((ty * 16, tx * 16), g["stencil"].dtype)
     st[:vh, :vw] = g["stencil"][g_:g_ + vh, g_:g_ + vw]  # visible pixels only
     want = np.zeros((ty, tx), np.uint8)
@@ -532,7 +536,7 @@ def test_busy_tile_flags(device, oracle, torch_dev, nd, visible):
     r.sd_trace()
     r.pass2()
     with_flags = r.numpy()["ao"]
-    assert not r.tile_flags.cpu().numpy().any()  # consumed
+    assert not r.tile_flags.cpu().numpy().view(np.uint32)[:T + 2].any()  # flags and list consumed
     # the same frame without flags
     from rsd import abi
     svp = abi.SVAOParams.from_buffer_copy(r.svp)
@@ -548,3 +552,27 @@ def test_busy_tile_flags(device, oracle, torch_dev, nd, visible):
     cam, vao, sdp, svp_o = oracle_structs(r, oracle)
     o = oracle_frame(oracle, osc, cam, vao, sdp, svp_o, cfg.fb_w, cfg.fb_h, r.sd_w, r.sd_h)
     assert np.array_equal(with_flags, o["ao"])
+
+
+def test_busy_tile_list_and_flag_grid_agree(device, oracle, torch_dev):
+    """The whole-frame pass 2 walks pass 1's busy-tile list; a row-range pass 2 (HaloFrame's bands)
+    visits the flagged tiles of its rows.  Both give the same AO, and both leave the tile buffer
+    clean (flags, list count and ticket zero) for the next pass 1."""
+    cfg = small_frame_config(visible=(224, 128), guard=32, divisor=2)
+    r, osc = renderer("arcade_tiny", cfg, device, oracle)
+    r.gbuffer()
+    out = []
+    for mode in ("list", "rows"):
+        r.ao.zero_()
+        r.clear_intervals()
+        r.pass1()
+        r.sd_trace()
+        if mode == "list":
+            r.pass2()
+        else:
+            r.pass2_rows((0, 64))
+            r.pass2_rows((64, cfg.visible_h))
+        g = r.numpy()
+        out.append(g["ao"])
+        assert not r.tile_flags.cpu().numpy().view(np.uint32).any(), mode
+    assert np.array_equal(out[0], out[1])
