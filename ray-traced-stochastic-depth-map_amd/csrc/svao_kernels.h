@@ -36,7 +36,7 @@ __device__ __forceinline__ void pass1_dir_generic(const SvaoArgs& a, float u, fl
     const rsd_vao_data& d = a.d;
     Sample s;
     bool ssrAbove;
-    if (!sample_init<ALLFAST>(a, u, v, b, i, s, ssrAbove, bf)) return;
+    if (!sample_init<ALLFAST, SPEC>(a, u, v, b, i, s, ssrAbove, bf)) return;
     const bool same = (SPEC || a.k.samePixelInt) ? (s.kx == (int)px && s.ky == (int)py)
                                                  : (fabsf(u - s.ru) < d.invResolution[0] * 0.9f &&
                                                     fabsf(v - s.rv) < d.invResolution[1] * 0.9f);
@@ -50,7 +50,7 @@ __device__ __forceinline__ void pass1_dir_generic(const SvaoArgs& a, float u, fl
     }
     // SVAORaster.ps.slang:62-66: Raytraced mode with TRACE_OUT_OF_SCREEN (SVAO.h:104)
     bool forceRay = !SPEC && a.secondary == 3u && !s.isInScreen;
-    eval_primary<SPEC>(a, b, s, bf);
+    eval_primary<SPEC, SPEC>(a, b, s, bf);
     if (!SPEC && a.dualDepth) eval_dual(a, b, s, ssrAbove, false);  // SVAORaster.ps.slang:69-70
     ao += s.visibility;
     if (!s.isInScreen && (SPEC || d.sdGuard > 0)) {
@@ -168,9 +168,9 @@ __device__ __forceinline__ void svao_pass2_dir(const SvaoArgs& a, const Basic& b
     const size_t plane = sd_plane_texels(a.sdW, a.sdH);
     Sample s;
     bool ssrAbove;
-    sample_init<ALLFAST>(a, u, v, b, i, s, ssrAbove);
+    sample_init<ALLFAST, SPEC>(a, u, v, b, i, s, ssrAbove);
     if (!SPEC && a.dualDepth) eval_dual(a, b, s, ssrAbove, true);  // Common.slang:555-558 (force init)
-    else eval_primary<SPEC>(a, b, s);
+    else eval_primary<SPEC, SPEC>(a, b, s);
     p = s.visibility;
     if (!SPEC && a.secondary == 1u) {
         // secondary DualDepth: calcAO2 has no branch for it (Common.slang:562-651), so the raster

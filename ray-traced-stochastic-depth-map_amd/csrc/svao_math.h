@@ -353,7 +353,8 @@ __device__ __forceinline__ bool ratio_le_tenth(float n, float D) {
 // ssrAbove = (screenSpaceRadius > ssRadiusCutoff), decided on the squared radius (no sqrt).
 // ALLFAST: the caller guarantees b.radius == VAOData.radius and every fastDiv bit (the host terms
 // and div_rcp apply; a wave-uniform case of the specialised pass 1)
-template <bool ALLFAST = false>
+// VAO: the caller is a VAO-only (specialised) kernel -- the HBAO branches compile away
+template <bool ALLFAST = false, bool VAO = false>
 __device__ __forceinline__ bool sample_init(const SvaoArgs& a, float u, float v, const Basic& b, int i, Sample& s,
                                             bool& ssrAbove, const P1Bufs* bf = nullptr) {
     const rsd_vao_data& d = a.d;
@@ -381,7 +382,7 @@ __device__ __forceinline__ bool sample_init(const SvaoArgs& a, float u, float v,
         dy = radius * a.k.cosDir[i];
         sphereHeight = sqrtf(b.radius * b.radius - radius * radius);
     }
-    s.pdf = a.k.hbao ? a.k.pdfHbao[i] : 2.0f * sphereHeight;  // Common.slang:362-365
+    s.pdf = (!VAO && a.k.hbao) ? a.k.pdfHbao[i] : 2.0f * sphereHeight;  // Common.slang:362-365
     s.sphereStart = sphereHeight;
     float zi;  // ALLFAST: the validity test below is one compare against the host bound ratioMin
     if (ALLFAST) {  // the pixel's divisor is in div_unscaled's range (checked with ALLFAST)
@@ -422,7 +423,10 @@ __device__ __forceinline__ bool sample_init(const SvaoArgs& a, float u, float v,
     // getSnappedUV (Common.slang:116-120): (floor(uv * res) + 0.5) / res from the host table
     s.kx = (int)floorf(cu * d.resolution[0]);
     s.ky = (int)floorf(cv * d.resolution[1]);
-    if (bf) {
+    if (kFastNumerics) {  // (k + 0.5) / res with the hardware reciprocal: no table loads
+        s.ru = ((float)s.kx + 0.5f) * d.invResolution[0];
+        s.rv = ((float)s.ky + 0.5f) * d.invResolution[1];
+    } else if (bf) {
         s.ru = buf_load(bf->snapU, (uint32_t)s.kx * 4u);
         s.rv = buf_load(bf->snapV, (uint32_t)s.ky * 4u);
     } else {
@@ -466,10 +470,11 @@ __device__ __forceinline__ float hbao_kernel(const SvaoArgs& a, const Basic& b, 
 }
 
 // Common.slang:463-483: VAO -- min of calcVisibility; HBAO -- max of saturate(HBAOKernel / pdf)
+template <bool VAO = false>
 __device__ __forceinline__ void add_sample(const SvaoArgs& a, const Basic& b, Sample& s, f3 spV, bool init) {
     const float oz = dot(spV - b.posV, b.normal);
     s.objectSpaceZ = init ? oz : hmin(s.objectSpaceZ, oz);
-    if (a.k.hbao) {
+    if (!VAO && a.k.hbao) {
         const float v = saturate(hbao_kernel(a, b, spV) / s.pdf);
         s.visibility = init ? v : hmax(s.visibility, v);
         return;
@@ -497,10 +502,10 @@ __device__ __forceinline__ void eval_dual(const SvaoArgs& a, const Basic& b, Sam
 
 
 // Common.slang:492-496
-template <bool SMALL = false>
+template <bool SMALL = false, bool VAO = false>
 __device__ __forceinline__ void eval_primary(const SvaoArgs& a, const Basic& b, Sample& s, const P1Bufs* bf = nullptr) {
     const float z = bf ? depth_center_buf(a, *bf, s.kx, s.ky) : depth_center<SMALL>(a, s.ru, s.rv, s.kx, s.ky);
-    add_sample(a, b, s, uv_to_view(a, s.ru, s.rv, z), true);
+    add_sample<VAO>(a, b, s, uv_to_view(a, s.ru, s.rv, z), true);
 }
 
 // Common.slang:164-168
