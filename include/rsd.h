@@ -199,7 +199,8 @@ typedef enum { RSD_AO_KERNEL_VAO = 0, RSD_AO_KERNEL_HBAO = 1 } rsd_ao_kernel;
 typedef enum { RSD_NUMERICS_FAST = 0, RSD_NUMERICS_EXACT = 1 } rsd_numerics;
 /* Bytes of rsd_svao_params.tile_flags for a width x height frame buffer with guard_band: for the T 16x16
  * tiles of the visible region rounded up to 32 rows (the padded pass-1 dispatch, SVAO.cpp:347-350), T flag
- * words, a 16-byte list header and T list entries (8 T + 16 bytes; ABI v4 had T bytes). */
+ * words, a 16-byte list header (two list counts: frames alternate between them, so no pass resets the
+ * list on the device) and T list entries (8 T + 16 bytes; ABI v4 had T bytes). */
 uint32_t rsd_svao_tile_count(uint32_t width, uint32_t height, uint32_t guard_band);
 
 /* Traversal counters of the last instrumented trace (roofline bytes) */

@@ -156,6 +156,45 @@ void cached_consts(SvaoConsts& k, const rsd_vao_data& d, uint32_t nd, uint32_t k
     next = (next + 1) % 4;
     used = used < 4 ? used + 1 : 4;
 }
+// The busy-tile list's generation per tile buffer.  Pass 1 of generation g appends to count[g & 1] and
+// zeroes count[(g + 1) & 1]; the whole-frame pass 2 walks count[g & 1]; the first pass 2 after a pass 1
+// (whatever its rows) moves the buffer to g + 1.  Stream order makes every step see the previous one:
+// the zeroing of pass 1 (g + 1) lands after pass 2 (g) read that count, so no kernel resets the list
+// and no workgroup waits for the others (a per-workgroup completion ticket on one address serialised
+// pass 2: 150-240 us at configs[1]).  Host-side state, one lock, a few entries per process.
+struct TileGen {
+    uint32_t gen = 0;
+    bool appended = false;  // a pass 1 ran since the last pass 2
+};
+std::mutex g_tile_mutex;
+std::vector<std::pair<const void*, TileGen>> g_tile_gen;
+
+TileGen& tile_gen_locked(const void* buf) {
+    for (auto& e : g_tile_gen)
+        if (e.first == buf) return e.second;
+    g_tile_gen.push_back({buf, TileGen{}});
+    return g_tile_gen.back().second;
+}
+
+uint32_t tile_gen_pass1(const void* buf) {
+    if (!buf) return 0u;
+    std::lock_guard<std::mutex> lock(g_tile_mutex);
+    TileGen& t = tile_gen_locked(buf);
+    t.appended = true;
+    return t.gen & 1u;
+}
+
+uint32_t tile_gen_pass2(const void* buf) {
+    if (!buf) return 0u;
+    std::lock_guard<std::mutex> lock(g_tile_mutex);
+    TileGen& t = tile_gen_locked(buf);
+    const uint32_t g = t.gen & 1u;
+    if (t.appended) {
+        ++t.gen;
+        t.appended = false;
+    }
+    return g;
+}
 }  // namespace
 
 extern "C" uint32_t rsd_svao_tile_count(uint32_t width, uint32_t height, uint32_t guard_band) {
@@ -241,6 +280,7 @@ rsd_status pass1_impl(const rsd_camera* cam, const rsd_vao_data* vao, const rsd_
     a.bandIndex = start;
     a.bandCount = step;
     if (bandGroups == 0) return RSD_OK;
+    a.tileGen = tile_gen_pass1(a.tileFlags);
     // the specialised kernel for the StochasticDepth frame (every BASELINE config); RSD_PASS1=generic
     // forces the generic one (A/B runs)
     const char* p1Env = std::getenv("RSD_PASS1");
@@ -355,14 +395,15 @@ rsd_status pass2_impl(const rsd_camera* cam, const rsd_vao_data* vao, const rsd_
                       (a.k.fastDiv & 0xffu) == 0xffu && a.d.lowResolution[0] >= 1.0f &&
                       a.d.lowResolution[0] <= 0x1p20f && a.d.lowResolution[1] >= 1.0f && a.d.lowResolution[1] <= 0x1p20f &&
                       a.d.radius < 0x1p58f;
-    // the whole frame with busy-tile flags: walk pass 1's list of busy tiles with a third of the tile
-    // count in workgroups (a workgroup takes a second tile only beyond 33 % busy tiles; configs[1]: 21 %)
-    // instead of one workgroup per tile (RSD_PASS2_LIST=off: the flag grid, A/B runs)
+    // the whole frame with busy-tile flags: pass 1's list of busy tiles, list entry i in workgroup i (one
+    // per tile of the frame: the count is on the device; the empty tail retires at once), instead of
+    // the flag grid (RSD_PASS2_LIST=off, A/B runs)
     const uint32_t T = tiles_x(W, p->guard_band) * tiles_y(H, p->guard_band);
     const char* listEnv = std::getenv("RSD_PASS2_LIST");
     const bool list = a.tileFlags && start == 0u && step == 1u && bandGroups == groups &&
                       !(listEnv && std::strcmp(listEnv, "off") == 0);
-    if (list) grid = dim3(std::min(T, std::max(256u, (T + 2u) / 3u)));
+    if (list) grid = dim3(T);
+    a.tileGen = tile_gen_pass2(a.tileFlags);
     if (p->numerics == RSD_NUMERICS_EXACT) exact::launch_pass2(a, N, nd, spec, grid, block, s, list);
     else fast::launch_pass2(a, N, nd, spec, grid, block, s, list);
     hipError_t e = hipGetLastError();

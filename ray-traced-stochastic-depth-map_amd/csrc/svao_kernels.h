@@ -148,8 +148,12 @@ __global__ void __launch_bounds__(256) svao_pass1_kernel(SvaoArgs a) {
         if ((lane == 0u && mL) || (lane == 8u && mR)) {
             // the first wave to flag a tile appends it to the busy-tile list pass 2 walks
             const uint32_t t = (oy / kTileEdge) * a.tilesX + ox / kTileEdge;
-            if (atomicExch(&a.tileFlags[t], 1u) == 0u) a.tileList[atomicAdd(a.tileCount, 1u)] = t;
+            if (atomicExch(&a.tileFlags[t], 1u) == 0u) a.tileList[atomicAdd(a.tileCount + a.tileGen, 1u)] = t;
         }
+        // the other list count (read by the previous frame's pass 2, earlier on this stream) starts the
+        // next frame's list at zero: no workgroup of pass 2 has to reset anything (svao.hip tile_gen)
+        if (blockIdx.x == 0u && blockIdx.y == 0u && threadIdx.x == 0u && threadIdx.y == 0u)
+            a.tileCount[a.tileGen ^ 1u] = 0u;
     }
 }
 
@@ -385,41 +389,25 @@ __global__ void __launch_bounds__(kP2Lanes) svao_pass2_kernel(SvaoArgs a) {
                         a.guard;
     uint32_t* flag = a.tileFlags ? a.tileFlags + ((y0 - a.guard) / kP2Tile) * a.tilesX + blockIdx.x : nullptr;
     if (!flag || *flag != 0u) pass2_tile<N, ND, SPEC, SPEC ? 16 : 20>(a, blockIdx.x * kP2Tile + a.guard, y0, flag, sh);
-    if (flag && threadIdx.x == 0) {
-        // this pass consumed the flags, not the list pass 1 also appended: the last workgroup resets it
-        const uint32_t k = __hip_atomic_fetch_add(a.tileCount + 1, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-        if (k == gridDim.x * gridDim.y - 1u) {
-            __hip_atomic_store(a.tileCount, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(a.tileCount + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
 }
 
-// Whole-frame pass 2 over the busy-tile list pass 1 appended (tile_flags, ABI v5): gridDim.x workgroups
-// stride over the list, so no workgroup is dispatched for an empty tile -- the flag-grid kernel above
-// dispatches one per tile of the frame (8160 at configs[1], 21 % busy), and each holds its 26 KB of LDS
-// until its flag load returns.  The workgroup that finishes last resets the list for the next pass 1.
+// Whole-frame pass 2 over the busy-tile list pass 1 appended (tile_flags, ABI v5): workgroup i takes list
+// entry i, so the busy tiles' workgroups are dispatched first and the empty ones (i >= count) form the
+// tail, retiring at once while the busy ones run.  The flag-grid kernel above interleaves them (8160
+// workgroups at configs[1], 21 % busy), and each holds its LDS until its own flag load returns.  One
+// tile per workgroup: a grid-stride loop over the list keeps the loop-invariant tile set-up in registers
+// (105-109 VGPRs, occupancy 4, vs 78 and 6).
 template <int N, int ND, bool SPEC = false>
 __global__ void __launch_bounds__(kP2Lanes) svao_pass2_list_kernel(SvaoArgs a) {
     __shared__ P2Shared<ND, SPEC ? 16 : 20> sh;
-    __shared__ uint32_t sCount;
-    if (threadIdx.x == 0) sCount = __hip_atomic_load(a.tileCount, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __syncthreads();
-    const uint32_t n = sCount;
-    for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
-        const uint32_t t = a.tileList[i];
-        pass2_tile<N, ND, SPEC, SPEC ? 16 : 20>(a, (t % a.tilesX) * kP2Tile + a.guard, (t / a.tilesX) * kP2Tile + a.guard,
-                                                a.tileFlags + t, sh);
-        __syncthreads();  // the tile's LDS is reused by the next one
-    }
-    if (threadIdx.x == 0) {
-        // every workgroup read the count before its ticket: the last ticket may reset the list
-        const uint32_t k = __hip_atomic_fetch_add(a.tileCount + 1, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-        if (k == gridDim.x - 1u) {
-            __hip_atomic_store(a.tileCount, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(a.tileCount + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
+    // the count of this frame's list (pass 1 of the same generation appended to it; the next pass 1
+    // appends to the other one): read-only here, no reset and no completion ticket
+    const uint32_t n = __builtin_amdgcn_readfirstlane(a.tileCount[a.tileGen]);
+    if (blockIdx.x >= n) return;
+    // uniform: the tile origin stays in scalar registers like blockIdx in the flag-grid kernel
+    const uint32_t t = __builtin_amdgcn_readfirstlane(a.tileList[blockIdx.x]);
+    pass2_tile<N, ND, SPEC, SPEC ? 16 : 20>(a, (t % a.tilesX) * kP2Tile + a.guard, (t / a.tilesX) * kP2Tile + a.guard,
+                                            a.tileFlags + t, sh);
 }
 
 // ---- host launchers of this TU's kernels (svao.hip picks the TU by rsd_svao_params.numerics)
@@ -431,7 +419,7 @@ void launch_pass1(const SvaoArgs& a, int variant, dim3 grid, dim3 block, hipStre
 }
 
 // pass 2: N SD samples, nd directions; spec: the specialised 8-direction kernel; list: the busy-tile
-// list kernel (grid.x workgroups striding over the list) instead of one workgroup per tile
+// list kernel (workgroup i: list entry i) instead of the flag grid
 void launch_pass2(const SvaoArgs& a, uint32_t N, uint32_t nd, bool spec, dim3 grid, dim3 block, hipStream_t s,
                   bool list) {
 #define RSD_P2K(K, NN, D, SP) hipLaunchKernelGGL((K<NN, D, SP>), grid, block, 0, s, a)

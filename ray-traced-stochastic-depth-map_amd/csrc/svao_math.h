@@ -59,7 +59,8 @@ struct SvaoArgs {
     const float* snapV;  //               snapV[k] = (k + 0.5f) / resolution.y
     const float4* nlut;  // decode_normal_2x8 of every 16-bit code (normal_lut), same bits
     uint32_t* tileFlags;  // rsd_svao_params.tile_flags: one word per busy 16x16 tile (tile_layout), or nullptr
-    uint32_t* tileCount;  // {count, done ticket} of the busy-tile list (after the flags)
+    uint32_t* tileCount;  // the two list counts (after the flags): frame generations alternate between them
+    uint32_t tileGen;     // 0 / 1: the count this pass appends to (pass 1) or walks (pass 2), svao.hip tile_gen
     uint32_t* tileList;   // busy tiles in the order pass 1 found them (after the count)
     uint32_t tilesX;      // tiles per row of tileFlags
     uint32_t dualDepth;  // PRIMARY_DEPTH_MODE == DualDepth: depth2 refines the raster samples
@@ -69,7 +70,7 @@ struct SvaoArgs {
 constexpr uint32_t kTileEdge = 16;  // busy-tile flag granularity = the pass-2 workgroup tile
 inline uint32_t tiles_x(uint32_t W, uint32_t guard) { return (W - 2 * guard + kTileEdge - 1) / kTileEdge; }
 inline uint32_t tiles_y(uint32_t H, uint32_t guard) { return (H - 2 * guard + 31u) / 32u * 32u / kTileEdge; }
-// the rsd_svao_params.tile_flags buffer (ABI v5) for T tiles: T flag words, {count, done ticket}, T list
+// the rsd_svao_params.tile_flags buffer (ABI v5) for T tiles: T flag words, {count[2], -, -}, T list
 // entries -- rsd_svao_tile_count bytes, zeroed once by its owner
 inline uint32_t tile_buffer_bytes(uint32_t T) { return T ? 8u * T + 16u : 0u; }
 inline void tile_layout(uint8_t* base, uint32_t T, uint32_t*& flags, uint32_t*& count, uint32_t*& list) {

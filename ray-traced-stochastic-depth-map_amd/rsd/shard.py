@@ -521,7 +521,7 @@ class HaloFrame:
                 dst = torch.where(touched, pos - 1, torch.full_like(pos, buf.shape[1] - 1))
                 buf.scatter_(1, dst.expand(3, -1), torch.stack((idx, reg[0], reg[1])))
                 row[k:k + 1].copy_(pos[-1:])
-            row[world] = prev_us
+            row[world:].fill_(prev_us)  # a kernel argument (row[world] = x is a synchronous host-to-device copy)
             self.comm.all_gather(self._M_dev, row)
             self._M_host.copy_(self._M_dev, non_blocking=True)
             if self.cuda:

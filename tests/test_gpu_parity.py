@@ -521,8 +521,11 @@ def test_busy_tile_flags(device, oracle, torch_dev, nd, visible):
     g_, vw, vh = cfg.guard_band, cfg.visible_w, cfg.visible_h
     tx, ty = (vw + 15) // 16, (vh + 31) // 32 * 32 // 16
     T = tx * ty
-    assert buf.size == 2 * T + 4  # T flag words, {count, ticket, -, -}, T list entries (ABI v5)
-    flags, count, lst = buf[:T], int(buf[T]), buf[T + 4:T + 4 + int(buf[T])]
+    assert buf.size == 2 * T + 4  # T flag words, {count[2], -, -}, T list entries (ABI v5)
+    # frames alternate between the two counts; pass 1 zeroes the one it does not append to
+    assert buf[T] == 0 or buf[T + 1] == 0
+    count = int(buf[T]) + int(buf[T + 1])
+    flags, lst = buf[:T], buf[T + 4:T + 4 + count]
     # the list holds every flagged tile once
     assert count == int(flags.sum()) and sorted(lst.tolist()) == np.flatnonzero(flags).tolist()
     st = np.zeros((ty * 16, tx * 16), g["stencil"].dtype)
@@ -536,7 +539,7 @@ def test_busy_tile_flags(device, oracle, torch_dev, nd, visible):
     r.sd_trace()
     r.pass2()
     with_flags = r.numpy()["ao"]
-    assert not r.tile_flags.cpu().numpy().view(np.uint32)[:T + 2].any()  # flags and list consumed
+    assert not r.tile_flags.cpu().numpy().view(np.uint32)[:T].any()  # flags consumed
     # the same frame without flags
     from rsd import abi
     svp = abi.SVAOParams.from_buffer_copy(r.svp)
@@ -556,23 +559,29 @@ def test_busy_tile_flags(device, oracle, torch_dev, nd, visible):
 
 def test_busy_tile_list_and_flag_grid_agree(device, oracle, torch_dev):
     """The whole-frame pass 2 walks pass 1's busy-tile list; a row-range pass 2 (HaloFrame's bands)
-    visits the flagged tiles of its rows.  Both give the same AO, and both leave the tile buffer
-    clean (flags, list count and ticket zero) for the next pass 1."""
+    visits the flagged tiles of its rows.  Both give the same AO and consume every flag; any sequence
+    of the two keeps the alternating list counts consistent (svao.hip tile_gen), including two pass 1
+    runs before one pass 2 (the flags OR, the list holds each tile once)."""
     cfg = small_frame_config(visible=(224, 128), guard=32, divisor=2)
     r, osc = renderer("arcade_tiny", cfg, device, oracle)
     r.gbuffer()
+    vw, vh = cfg.visible_w, cfg.visible_h
+    T = ((vw + 15) // 16) * ((vh + 31) // 32 * 2)
     out = []
-    for mode in ("list", "rows"):
+    for mode in ("list", "rows", "rows", "list", "list", "twice", "rows", "list"):
         r.ao.zero_()
         r.clear_intervals()
         r.pass1()
+        if mode == "twice":
+            r.clear_intervals()
+            r.pass1()
         r.sd_trace()
-        if mode == "list":
-            r.pass2()
-        else:
+        if mode == "rows":
             r.pass2_rows((0, 64))
-            r.pass2_rows((64, cfg.visible_h))
-        g = r.numpy()
-        out.append(g["ao"])
-        assert not r.tile_flags.cpu().numpy().view(np.uint32).any(), mode
-    assert np.array_equal(out[0], out[1])
+            r.pass2_rows((64, vh))
+        else:
+            r.pass2()
+        out.append(r.numpy()["ao"])
+        assert not r.tile_flags.cpu().numpy().view(np.uint32)[:T].any(), mode
+    for mode, ao in zip(("list", "rows", "rows", "list", "list", "twice", "rows", "list"), out):
+        assert np.array_equal(out[0], ao), mode

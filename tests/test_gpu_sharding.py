@@ -193,8 +193,9 @@ def test_halo_frame_sync_free_threads(world):
                 if len(pending) > 1:
                     finish(pending.pop(0))
             finish(pending.pop(0))
-        except Exception as e:  # noqa: BLE001 -- reported by the main thread
-            errors.append((k, repr(e)))
+        except Exception:  # noqa: BLE001 -- reported by the main thread, with the line that synchronised
+            import traceback
+            errors.append((k, traceback.format_exc()))
 
     torch.cuda.set_sync_debug_mode("error")
     try:

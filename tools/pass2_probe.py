@@ -20,10 +20,8 @@ r = Renderer(make_scene(sc), FrameConfig(**kw))
 r.gbuffer()
 r.clear_intervals()
 r.pass1()
-flags = r.tile_flags.clone()
 r.sd_trace()
 torch.cuda.synchronize()
-ao1 = r.ao.clone()
 st = r.stencil.clone()
 g = r.cfg.guard_band
 s = st.cpu().numpy()[g:g + (r.cfg.visible_h + 31) // 32 * 32, g:r.cfg.fb_w - g].astype(np.uint32)
@@ -49,10 +47,15 @@ def timeit(prep, n=60):
     return round(float(np.median(ts)), 2)
 
 
-def restore(stencil=st, fl=flags):
-    r.ao.copy_(ao1)
-    r.stencil.copy_(stencil)
-    r.tile_flags.copy_(fl)
+def restore(stencil=None, no_busy=False):
+    """pass 1 again (the busy-tile list belongs to the pass 1 before each pass 2, svao.hip tile_gen;
+    the SD map is unchanged), then optionally a different stencil / no busy tiles"""
+    r.clear_intervals()
+    r.pass1()
+    if stencil is not None:
+        r.stencil.copy_(stencil)
+    if no_busy:
+        r.tile_flags.zero_()
 
 
 out = {"config": name, "tiles": int(pt.size), "busy_tiles": int(busy.size), "pairs": int(pairs.sum()),
@@ -70,6 +73,5 @@ r.svp = svp_flags
 # only the lowest refined direction of each pixel: the per-pair share of the time
 st1 = torch.from_numpy((lambda a: a & (~a + 1))(st.cpu().numpy().astype(np.int32)).astype(np.uint8)).cuda()
 out["pass2_us_one_dir_per_pixel"] = timeit(lambda: restore(st1))
-zero_fl = torch.zeros_like(flags)
-out["pass2_us_no_busy_tiles"] = timeit(lambda: restore(st, zero_fl))
+out["pass2_us_no_busy_tiles"] = timeit(lambda: restore(no_busy=True))
 print(json.dumps(out))
