@@ -20,6 +20,15 @@
 #ifndef RSD_P1_UNROLL
 #define RSD_P1_UNROLL 1
 #endif
+// fast numerics: clamped-radius pixels take the SCALED all-fast loops (sample_init); 0 = the per-lane
+// generic loops as in the exact build (A/B builds: make variant V=noscaled DEFS=-DRSD_SCALED_ALLFAST=0)
+// fast numerics: the all-fast pass-1 loops take 2 directions at a time (pass1_dir_pair); 1 = one at a time
+#ifndef RSD_P1_BATCH
+#define RSD_P1_BATCH 2
+#endif
+#ifndef RSD_SCALED_ALLFAST
+#define RSD_SCALED_ALLFAST 1
+#endif
 
 namespace rsd {
 namespace RSD_SVAO_NS {
@@ -29,14 +38,14 @@ namespace RSD_SVAO_NS {
 // per SIMD -- DESIGN.md section 4.)  SPEC: the specialised kernel of the StochasticDepth frame with ray
 // intervals, an SD guard band, pixel-index isSamePixel and a frame of at most 4096 x 4096 (every
 // BASELINE config) -- the run-time tests of those settings are compile-time constants there.
-template <bool SPEC, bool ALLFAST = false>
+template <bool SPEC, bool ALLFAST = false, bool SCALED = false>
 __device__ __forceinline__ void pass1_dir_generic(const SvaoArgs& a, float u, float v, uint32_t px, uint32_t py,
                                                   const Basic& b, int i, float& ao, float& aoD, uint32_t& st,
                                                   const P1Bufs* bf = nullptr) {
     const rsd_vao_data& d = a.d;
     Sample s;
     bool ssrAbove;
-    if (!sample_init<ALLFAST, SPEC>(a, u, v, b, i, s, ssrAbove, bf)) return;
+    if (!sample_init<ALLFAST, SPEC, SCALED>(a, u, v, b, i, s, ssrAbove, bf)) return;
     const bool same = (SPEC || a.k.samePixelInt) ? (s.kx == (int)px && s.ky == (int)py)
                                                  : (fabsf(u - s.ru) < d.invResolution[0] * 0.9f &&
                                                     fabsf(v - s.rv) < d.invResolution[1] * 0.9f);
@@ -85,6 +94,57 @@ __device__ __forceinline__ void pass1_dir_generic(const SvaoArgs& a, float u, fl
     }
 }
 
+// The second half of pass1_dir_generic<true, true, SCALED> (fast numerics), given the depth at the
+// sample's texel: the batched loop below issues the depth reads of two directions before either body.
+template <bool SCALED>
+__device__ __forceinline__ void pass1_dir_finish(const SvaoArgs& a, const Basic& b, int i, Sample& s, bool ssrAbove,
+                                                 bool same, float z, float& ao, float& aoD, uint32_t& st) {
+    const rsd_vao_data& d = a.d;
+    if (same) {  // isSamePixel (SVAORaster.ps.slang:55-60)
+        const float w = div_pdf(s.sphereStart - s.sphereEnd, s);
+        ao += w;
+        aoD += w;
+        return;
+    }
+    add_sample<true>(a, b, s, uv_to_view(a, s.ru, s.rv, z), true);  // evalPrimaryVisibility
+    ao += s.visibility;
+    bool forceRay = false;
+    if (!s.isInScreen) {
+        forceRay = true;
+        s.objectSpaceZ = 3.402823466e+38f;
+    }
+    const float constRadius = (1.0f + d.thickness) * b.radius - s.sphereStart;
+    if ((s.objectSpaceZ > s.sphereStart + constRadius && ssrAbove) || forceRay) {
+        st |= 1u << i;
+        const int sx = uv_to_sd(s.su, d.lowResolution[0], d.sdGuard);
+        const int sy = uv_to_sd(s.sv, d.lowResolution[1], d.sdGuard);
+        const size_t o = (size_t)sy * a.sdW + sx;
+        const float osMin = hmin(s.objectSpaceZ, b.radius + d.thickness * b.radius + s.sphereStart);
+        atomicMin(&a.rayMin[o], asuint(hmax(b.posVLength - osMin, 0.0f)));
+        atomicMax(&a.rayMax[o], asuint(hmax(b.posVLength - s.sphereEnd, 0.0f)));
+    } else {
+        aoD += s.visibility;
+    }
+}
+
+// Two directions of the fast all-fast loop at a time: both samples' set-up, both depth reads issued back
+// to back (one memory wait instead of two), then both bodies in direction order.  The reads are always
+// in bounds (depth_center_buf clamps; an invalid direction reads texel 0 and discards it).
+template <bool SCALED>
+__device__ __forceinline__ void pass1_dir_pair(const SvaoArgs& a, float u, float v, uint32_t px, uint32_t py,
+                                               const Basic& b, int i, float& ao, float& aoD, uint32_t& st,
+                                               const P1Bufs& bf) {
+    Sample s0, s1;
+    bool r0 = false, r1 = false;
+    s0.kx = s0.ky = s1.kx = s1.ky = 0;
+    const bool ok0 = sample_init<true, true, SCALED>(a, u, v, b, i, s0, r0, &bf);
+    const bool ok1 = sample_init<true, true, SCALED>(a, u, v, b, i + 1, s1, r1, &bf);
+    const float z0 = depth_center_buf(a, bf, s0.kx, s0.ky);
+    const float z1 = depth_center_buf(a, bf, s1.kx, s1.ky);
+    if (ok0) pass1_dir_finish<SCALED>(a, b, i, s0, r0, s0.kx == (int)px && s0.ky == (int)py, z0, ao, aoD, st);
+    if (ok1) pass1_dir_finish<SCALED>(a, b, i + 1, s1, r1, s1.kx == (int)px && s1.ky == (int)py, z1, ao, aoD, st);
+}
+
 // SVAORaster.ps.slang:29-122, [numthreads(16,16,1)] with the 2x2 group interleave.  (A branch-free
 // "lean" direction body -- host constants in SGPRs, predicated updates, one float ratio compare --
 // measured 74 vs 70 us at configs[1]: more VALU per direction and 64-73 VGPRs)
@@ -114,8 +174,26 @@ __global__ void __launch_bounds__(256) svao_pass1_kernel(SvaoArgs a) {
         const bool posOk = kFastNumerics || (fabsf(b.posV.x) < 0x1p60f && fabsf(b.posV.y) < 0x1p60f);  // (div_unscaled bounds)
         if (SPEC && __ballot(b.radius != d.radius || !div_unscaled_den_ok(nzd) || !posOk) == 0u) {
             b.nzRcp = rcp_refined(nzd);
+            if constexpr (SPEC && kFastNumerics && RSD_P1_BATCH == 2) {
 #pragma unroll RSD_P1_UNROLL
-            for (int i = 0; i < nd; ++i) pass1_dir_generic<SPEC, true>(a, u, v, px, py, b, i, ao, aoD, st, &bf);
+                for (int i = 0; i < nd; i += 2) pass1_dir_pair<false>(a, u, v, px, py, b, i, ao, aoD, st, bf);
+            } else {
+#pragma unroll RSD_P1_UNROLL
+                for (int i = 0; i < nd; ++i) pass1_dir_generic<SPEC, true>(a, u, v, px, py, b, i, ao, aoD, st, &bf);
+            }
+        } else if (SPEC && kFastNumerics && RSD_SCALED_ALLFAST) {
+            // fast numerics: a wave with clamped-radius pixels (nearest the camera) takes the same lean
+            // loop with the direction terms scaled per pixel instead of the per-lane IEEE paths
+            b.nzRcp = rcp_refined(nzd);
+            set_radius_scale(a, b);
+            if constexpr (RSD_P1_BATCH == 2) {
+#pragma unroll RSD_P1_UNROLL
+                for (int i = 0; i < nd; i += 2) pass1_dir_pair<true>(a, u, v, px, py, b, i, ao, aoD, st, bf);
+            } else {
+#pragma unroll RSD_P1_UNROLL
+                for (int i = 0; i < nd; ++i)
+                    pass1_dir_generic<SPEC, true, true>(a, u, v, px, py, b, i, ao, aoD, st, &bf);
+            }
         } else {
 #pragma unroll RSD_P1_UNROLL
             for (int i = 0; i < nd; ++i) pass1_dir_generic<SPEC>(a, u, v, px, py, b, i, ao, aoD, st);
@@ -164,7 +242,7 @@ __global__ void __launch_bounds__(256) svao_pass1_kernel(SvaoArgs a) {
 // (ylx, yly) = rcp_refined of the SD resolution: the texel-centre uv divisions (cx - guard + jx) / low
 // go through div_unscaled -- the numerator is never 0 and >= 0.0037 in magnitude (the jitter table
 // lies in (0.0037, 0.9963), or 0.5 without jitter), so its preconditions hold.
-template <int N, bool SPEC = false, bool ALLFAST = false>
+template <int N, bool SPEC = false, bool ALLFAST = false, bool SCALED = false>
 __device__ __forceinline__ void svao_pass2_dir(const SvaoArgs& a, const Basic& b, float u, float v, int i, float& p,
                                                float& r, float ylx = 0.0f, float yly = 0.0f) {
     const rsd_vao_data& d = a.d;
@@ -172,7 +250,7 @@ __device__ __forceinline__ void svao_pass2_dir(const SvaoArgs& a, const Basic& b
     const size_t plane = sd_plane_texels(a.sdW, a.sdH);
     Sample s;
     bool ssrAbove;
-    sample_init<ALLFAST, SPEC>(a, u, v, b, i, s, ssrAbove);
+    sample_init<ALLFAST, SPEC, SCALED>(a, u, v, b, i, s, ssrAbove);
     if (!SPEC && a.dualDepth) eval_dual(a, b, s, ssrAbove, true);  // Common.slang:555-558 (force init)
     else eval_primary<SPEC, SPEC>(a, b, s);
     p = s.visibility;
@@ -348,6 +426,10 @@ __device__ __forceinline__ void pass2_tile(const SvaoArgs& a, uint32_t x0, uint3
                 if (__ballot(b.radius != d.radius || !div_unscaled_den_ok(nzd) || !posOk) == 0u) {
                     b.nzRcp = rcp_refined(nzd);
                     svao_pass2_dir<N, true, true>(a, b, u, v, (int)(e & 31u), p, r, ylx, yly);
+                } else if (kFastNumerics && RSD_SCALED_ALLFAST) {  // clamped-radius pixels: the scaled lean path (pass 1's)
+                    b.nzRcp = rcp_refined(nzd);
+                    set_radius_scale(a, b);
+                    svao_pass2_dir<N, true, true, true>(a, b, u, v, (int)(e & 31u), p, r, ylx, yly);
                 } else {
                     svao_pass2_dir<N, true, false>(a, b, u, v, (int)(e & 31u), p, r, ylx, yly);
                 }

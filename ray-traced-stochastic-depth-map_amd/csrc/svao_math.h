@@ -35,6 +35,7 @@ struct SvaoConsts {
     float invNd;            // 1.0 / float(NUM_DIRECTIONS) (SVAORaster.ps.slang:108, Common.slang:660)
     uint32_t hbao;          // AO_KERNEL == AO_KERNEL_HBAO (rsd_ao_kernel)
     float pdfHbao[kMaxDirections];  // HBAO pdf of direction i: 0.9 pow(1 - sampleRadius[i], 1.5) (Common.slang:364)
+    float rcpRadius;                // 1 / VAOData.radius (fast numerics: the clamped pixels' scale, sample_init)
 };
 
 struct SvaoArgs {
@@ -86,6 +87,7 @@ struct Basic {
     f3 normal, tangent, bitangent, normalO, normalV;
     float radiusInPixels, radius;
     float nzRcp;  // rcp_refined(make_nonzero(normalO.z, 1e-4)): set by the all-fast pass-1 loop only
+    float rScale, rScaleInv;  // fast numerics, SCALED all-fast loop: radius / VAOData.radius and its inverse
 };
 
 struct Sample {
@@ -332,6 +334,13 @@ __device__ __forceinline__ bool basic_from(const SvaoArgs& a, float u, float v, 
     return true;
 }
 
+// the SCALED all-fast loop's per-pixel factors (fast numerics): exactly 1 for an unclamped pixel
+__device__ __forceinline__ void set_radius_scale(const SvaoArgs& a, Basic& b) {
+    const bool unclamped = b.radius == a.d.radius;
+    b.rScale = unclamped ? 1.0f : b.radius * a.k.rcpRadius;
+    b.rScaleInv = unclamped ? 1.0f : a.d.radius * __builtin_amdgcn_rcpf(b.radius);
+}
+
 __device__ __forceinline__ float make_nonzero(float v, float eps) {
     const float av = hmax(fabsf(v), eps);
     return v >= 0.0f ? av : -av;
@@ -355,7 +364,12 @@ __device__ __forceinline__ bool ratio_le_tenth(float n, float D) {
 // ALLFAST: the caller guarantees b.radius == VAOData.radius and every fastDiv bit (the host terms
 // and div_rcp apply; a wave-uniform case of the specialised pass 1)
 // VAO: the caller is a VAO-only (specialised) kernel -- the HBAO branches compile away
-template <bool ALLFAST = false, bool VAO = false>
+// SCALED (fast numerics only, with ALLFAST): the pixel's radius may be clamped to ssMaxRadius; every
+// radius-dependent term of the direction is linear in it (Common.slang:358-365: radius_i = r_i R,
+// sphereHeight = R sqrt(1 - r_i^2), pdf = 2 sphereHeight), so the host terms at VAOData.radius are
+// scaled by b.rScale = R / VAOData.radius (1 exactly when unclamped) -- the rounding differs from the
+// reference's order of operations by a few ulp, inside the fast-numerics tolerance
+template <bool ALLFAST = false, bool VAO = false, bool SCALED = false>
 __device__ __forceinline__ bool sample_init(const SvaoArgs& a, float u, float v, const Basic& b, int i, Sample& s,
                                             bool& ssrAbove, const P1Bufs* bf = nullptr) {
     const rsd_vao_data& d = a.d;
@@ -369,6 +383,13 @@ __device__ __forceinline__ bool sample_init(const SvaoArgs& a, float u, float v,
         s.fast = true;
         s.yPdf = a.k.rcpPdf[i];
         s.yHeight = a.k.rcpHeight[i];
+        if constexpr (SCALED) {
+            dx *= b.rScale;
+            dy *= b.rScale;
+            sphereHeight *= b.rScale;
+            s.yPdf *= b.rScaleInv;
+            s.yHeight *= b.rScaleInv;
+        }
     } else if (b.radius == d.radius) {  // the host-evaluated terms (same operations, same bits)
         radius = a.k.dirRadius[i];
         dx = a.k.dirDx[i];
@@ -394,7 +415,7 @@ __device__ __forceinline__ bool sample_init(const SvaoArgs& a, float u, float v,
     }
     s.sphereEnd = hmin(hmax(zi, -sphereHeight), sphereHeight);
     // (sphereStart - sphereEnd is never NaN: hmax maps a NaN zi to -sphereHeight)
-    if (ALLFAST ? !(s.sphereStart - s.sphereEnd >= a.k.ratioMin[i])
+    if (ALLFAST ? !(s.sphereStart - s.sphereEnd >= (SCALED ? a.k.ratioMin[i] * b.rScale : a.k.ratioMin[i]))
                 : ratio_le_tenth(s.sphereStart - s.sphereEnd, 2.0f * sphereHeight))
         return false;
     const f3 ip = b.posV + b.tangent * dx + b.bitangent * dy;
@@ -606,6 +627,7 @@ inline void fill_consts(SvaoConsts& k, const rsd_vao_data& d, uint32_t nd, uint3
     // holds exactly when the pixel indices agree (difference < 2^-21 << 0.9 / res) and fails when
     // they differ (difference >= 1 / res - 2^-21 > 0.9 / res) for res <= 2^18
     k.samePixelInt = d.resolution[0] <= 262144.0f && d.resolution[1] <= 262144.0f;
+    k.rcpRadius = d.radius > 0.0f ? (float)(1.0 / (double)d.radius) : 0.0f;
     k.fastDiv = 0u;
     for (int i = 0; i < (int)k.nd; ++i) {
         const float pdf = 2.0f * k.dirHeight[i], h = k.dirHeight[i];

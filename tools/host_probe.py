@@ -1,7 +1,13 @@
 """Host-side cost of issuing frames (diagnostics): how long the Python + librsd host path takes to
 enqueue the frames-in-flight loop of bench.py, per frame and per ABI call, against the GPU time per
 frame.  If issuing a frame costs about as much host time as the GPU spends on it, the GPU starves.
-usage: python tools/host_probe.py [config] [--frames N]"""
+usage: python tools/host_probe.py [config] [--frames N]
+
+svao_frame_python_only is the same ctypes call with a description librsd rejects at once: the Python +
+ctypes + current-stream part of svao_frame; the rest is librsd's host code and the HIP runtime's launch
+path (tools/launch_floor.hip measures the runtime alone).  svao_frame issues 5 launches (interval clear,
+pass 1, SD setup, walk, pass 2), svao_frame_cleared 4 (the previous trace consumed the intervals, the
+bench's steady state)."""
 import json
 import sys
 import time
@@ -47,7 +53,16 @@ for n in (frames, 10 * frames):
     out[f"issue_us_per_frame_{n}"] = round((t1 - t0) / n * 1e6, 1)
     out[f"wall_us_per_frame_{n}"] = round((t2 - t0) / n * 1e6, 1)
 # per-call host cost (the GPU queue kept short: synchronize between batches)
-calls = {"svao_frame": lambda: r.svao_frame(throughput=True), "pass1": r.pass1,
+from rsd import abi  # noqa: E402
+import ctypes as C  # noqa: E402
+
+null_desc = abi.FrameDesc()  # cam == NULL: rsd_svao_frame returns at its first check (no HIP call)
+calls = {"svao_frame": lambda: r.svao_frame(throughput=True),
+         "svao_frame_cleared": lambda: r.svao_frame(intervals_clear=True, throughput=True),
+         # the host path around the C++ work: Python + ctypes marshalling + torch's current stream
+         "svao_frame_python_only": lambda: abi.lib().rsd_svao_frame(C.byref(null_desc), 0, None, r.stream),
+         "current_stream": lambda: r.stream, "frame_desc": r._frame_desc,
+         "pass1": r.pass1,
          "sd_trace": lambda: r.sd_trace(throughput=True), "pass2": r.pass2,
          "stream_ctx": lambda: torch.cuda.stream(streams[1]).__enter__(), "event_record": lambda: torch.cuda.Event().record()}
 for k, fn in calls.items():

@@ -1,0 +1,78 @@
+// launch_floor.hip -- the HIP runtime's own host cost per kernel launch on this box (diagnostics for
+// tools/host_probe.py: what part of rsd_svao_frame's host time is librsd and what part is the
+// runtime).  Empty kernels with a 64-byte and a 2048-byte argument struct (SvaoArgs is ~2 KB),
+// launched back to back on one non-blocking stream, plus hipEventRecord; the GPU queue is drained
+// between batches so the host never blocks on a full queue.
+// build + run on the GPU box: hipcc --offload-arch=gfx950 -O2 tools/launch_floor.hip -o /tmp/lf && /tmp/lf
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cstdio>
+
+struct Small {
+    float v[16];
+};
+struct Big {
+    float v[512];
+};
+
+__global__ void k_small(Small s, float* out) {
+    if (threadIdx.x == 0 && blockIdx.x == 0 && s.v[0] < -1.0f) out[0] = s.v[1];
+}
+__global__ void k_big(Big s, float* out) {
+    if (threadIdx.x == 0 && blockIdx.x == 0 && s.v[0] < -1.0f) out[0] = s.v[511];
+}
+
+#define CHECK(x)                                                              \
+    do {                                                                      \
+        hipError_t e_ = (x);                                                  \
+        if (e_ != hipSuccess) {                                               \
+            std::fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e_));      \
+            return 1;                                                         \
+        }                                                                     \
+    } while (0)
+
+template <class F>
+double per_call_us(hipStream_t s, F&& fn) {
+    double best = 1e30;
+    for (int rep = 0; rep < 7; ++rep) {
+        if (hipStreamSynchronize(s) != hipSuccess) return -1.0;
+        const auto t0 = std::chrono::steady_clock::now();
+        for (int i = 0; i < 64; ++i) fn();
+        const auto t1 = std::chrono::steady_clock::now();
+        const double us = std::chrono::duration<double, std::micro>(t1 - t0).count() / 64.0;
+        best = us < best ? us : best;
+    }
+    return best;
+}
+
+int main() {
+    hipStream_t s;
+    CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    float* out = nullptr;
+    CHECK(hipMalloc(&out, 4));
+    Small sm{};
+    Big bg{};
+    hipEvent_t ev;
+    CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    hipEvent_t evt;
+    CHECK(hipEventCreate(&evt));
+    // warm-up: code objects loaded, queues created
+    for (int i = 0; i < 100; ++i) {
+        hipLaunchKernelGGL(k_small, dim3(1), dim3(64), 0, s, sm, out);
+        hipLaunchKernelGGL(k_big, dim3(1), dim3(64), 0, s, bg, out);
+    }
+    CHECK(hipStreamSynchronize(s));
+    const double small = per_call_us(s, [&] { hipLaunchKernelGGL(k_small, dim3(8160), dim3(256), 0, s, sm, out); });
+    const double big = per_call_us(s, [&] { hipLaunchKernelGGL(k_big, dim3(8160), dim3(256), 0, s, bg, out); });
+    const double rec = per_call_us(s, [&] { (void)hipEventRecord(ev, s); });
+    const double rect = per_call_us(s, [&] { (void)hipEventRecord(evt, s); });
+    const double gle = per_call_us(s, [&] { (void)hipGetLastError(); });
+    int dev = 0;
+    const double gd = per_call_us(s, [&] { (void)hipGetDevice(&dev); });
+    CHECK(hipStreamSynchronize(s));
+    std::printf("{\"launch_us_args64\": %.2f, \"launch_us_args2048\": %.2f, \"event_record_us\": %.2f, "
+                "\"event_record_timing_us\": %.2f, \"get_last_error_us\": %.3f, \"get_device_us\": %.3f}\n",
+                small, big, rec, rect, gle, gd);
+    return 0;
+}
