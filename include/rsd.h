@@ -390,6 +390,49 @@ rsd_status rsd_sd_trace_rows(rsd_scene* scene, const rsd_camera* cam, const rsd_
                              float* d_sd_out, uint32_t sd_w, uint32_t sd_h,
                              uint32_t row0, uint32_t row1, uint32_t flags, rsd_counters* counters, rsd_stream stream);
 
+/* --- sparse halo exchange of the band split (rsd/shard.py HaloFrame) ----------
+ * Device-side steps around the point-to-point transfers, one call each instead of a dozen small torch
+ * ops per peer (the host issue cost of an N > 1 frame).  No host synchronisation.
+ *
+ * rsd_halo_compact: for each region r (SD rows [row0, row1) of the interval maps), the touched texels
+ * (rayMin != asuint(FLT_MAX) or rayMax != 0; SVAO.cpp:334-340's cleared state) are written as int32
+ * triples -- texel index, rayMin bits, rayMax bits -- to out[r] (three rows of `stride` int32:
+ * out[r][0 .. n), out[r][stride ..], out[r][2 stride ..]; stride >= the region's texel count) in an
+ * unspecified order, and their number to counts[r] (int64, overwritten).  The merge below is
+ * order-independent (min / max), so the order does not change a result bit. */
+typedef struct {
+    uint32_t row0, row1;  /* SD-map rows of the region */
+    int32_t* out;         /* 3 x stride int32 (device) */
+    uint32_t stride;
+    uint32_t pad;
+    int64_t* count;       /* device int64, overwritten */
+} rsd_halo_region;
+rsd_status rsd_halo_compact(const uint32_t* d_ray_min, const uint32_t* d_ray_max, uint32_t sd_w, uint32_t sd_h,
+                            const rsd_halo_region* regions, uint32_t n_regions, rsd_stream stream);
+/* rsd_halo_merge: atomicMin / atomicMax of received triples (per list: n triples in three rows of `stride`
+ * int32, as above) into the interval maps -- the exact union (non-negative float bit patterns order like
+ * the floats); ray_interval = 0 (no RayInterval): rayMin is not merged.  All lists in one launch. */
+typedef struct {
+    const int32_t* triples;
+    uint32_t n;
+    uint32_t stride;
+} rsd_halo_list;
+rsd_status rsd_halo_merge(uint32_t* d_ray_min, uint32_t* d_ray_max, uint32_t sd_w, uint32_t sd_h,
+                          const rsd_halo_list* lists, uint32_t n_lists, uint32_t ray_interval, rsd_stream stream);
+/* rsd_halo_sd_gather / _scatter: the SD depths of n texels per list (int32 texel indices of the sd_w x sd_h
+ * plane) between the map (layers x texels x ch floats, Texture2DArray order) and the list's packed buffer
+ * (layers x n x ch floats) -- the sparse SD halo's reply.  All lists in one launch; at most 64 lists. */
+typedef struct {
+    const int32_t* idx;
+    float* buf;
+    uint32_t n;
+    uint32_t pad;
+} rsd_halo_sd_list;
+rsd_status rsd_halo_sd_gather(const float* d_sd, uint32_t layers, uint32_t sd_w, uint32_t sd_h, uint32_t ch,
+                              const rsd_halo_sd_list* lists, uint32_t n_lists, rsd_stream stream);
+rsd_status rsd_halo_sd_scatter(float* d_sd, uint32_t layers, uint32_t sd_w, uint32_t sd_h, uint32_t ch,
+                               const rsd_halo_sd_list* lists, uint32_t n_lists, rsd_stream stream);
+
 rsd_status rsd_svao_pass2_raytraced_band(rsd_scene* scene, const rsd_camera* cam, const rsd_vao_data* vao,
                                          const rsd_svao_params* params, const float* d_depth,
                                          const uint16_t* d_normals, uint32_t width, uint32_t height,

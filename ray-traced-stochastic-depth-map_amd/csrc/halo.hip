@@ -1,0 +1,231 @@
+// halo.hip -- device steps of the band split's sparse halo exchange (rsd/shard.py HaloFrame,
+// DESIGN.md section 6; include/rsd.h rsd_halo_*).
+//
+// each rank owns contiguous screen bands; the SD texels its pass 1 touched inside another
+// rank's band travel as (texel, rayMin, rayMax) triples and their N depths come back.  These kernels
+// are the device side of those steps: the compaction of the touched texels (one ballot + one atomic per
+// wave and region), the order-independent merge (atomicMin / atomicMax, the union SVAO.cpp:334-340's
+// atomics would have produced on one GPU), and the SD-depth gather / scatter of the reply.  All are
+// HBM-streaming: bytes per texel = 8 (read both words) + 12 per touched texel; per triple 12 + 2 atomics.
+#include <hip/hip_runtime.h>
+
+#include <string>
+
+#include "rsd_internal.h"
+
+namespace rsd {
+namespace {
+
+constexpr uint32_t kHaloBlock = 256;
+constexpr uint32_t kFltMaxBits = 0x7f7fffffu;  // asuint(FLT_MAX): a cleared rayMin (SVAO.cpp:339)
+constexpr uint32_t kMaxRegions = 64;
+
+struct HaloRegions {
+    uint32_t n;
+    uint32_t first[kMaxRegions + 1];  // first texel of each region (flattened grid of all regions' texels)
+    uint32_t row0[kMaxRegions];
+    uint32_t stride[kMaxRegions];
+    int32_t* out[kMaxRegions];
+    unsigned long long* count[kMaxRegions];
+};
+
+__global__ void halo_zero_kernel(HaloRegions R) {
+    if (threadIdx.x < R.n) *R.count[threadIdx.x] = 0ull;
+}
+
+__global__ void __launch_bounds__(kHaloBlock) halo_compact_kernel(const uint32_t* __restrict__ rmin,
+                                                                   const uint32_t* __restrict__ rmax, uint32_t sdW,
+                                                                   HaloRegions R) {
+    const uint32_t g = blockIdx.x * kHaloBlock + threadIdx.x;
+    const bool in = g < R.first[R.n];
+    uint32_t r = 0;
+    while (in && g >= R.first[r + 1]) ++r;
+    const uint32_t t = in ? R.row0[r] * sdW + (g - R.first[r]) : 0u;
+    const uint32_t lo = in ? rmin[t] : kFltMaxBits, hi = in ? rmax[t] : 0u;
+    const bool touched = lo != kFltMaxBits || hi != 0u;
+    // one atomic per (wave, region) the wave's touched texels fall in
+    const uint32_t lane = __lane_id();
+    uint64_t pending = __ballot(touched);
+    while (pending != 0ull) {
+        const int leader = __ffsll((long long)pending) - 1;
+        const uint32_t rl = (uint32_t)__shfl((int)r, leader);
+        const uint64_t grp = __ballot(touched && r == rl);
+        unsigned long long base = 0ull;
+        if (lane == (uint32_t)leader) base = atomicAdd(R.count[rl], (unsigned long long)__popcll(grp));
+        base = __shfl(base, leader);
+        if (touched && r == rl) {
+            const uint32_t k = (uint32_t)base + (uint32_t)__popcll(grp & ((1ull << lane) - 1ull));
+            int32_t* o = R.out[rl];
+            const uint32_t st = R.stride[rl];
+            o[k] = (int32_t)t;
+            o[st + k] = (int32_t)lo;
+            o[2u * st + k] = (int32_t)hi;
+        }
+        pending &= ~grp;
+    }
+}
+
+// flattened work of up to kMaxRegions lists: list l covers items [first[l], first[l + 1])
+struct HaloLists {
+    uint32_t n;
+    uint32_t first[kMaxRegions + 1];
+    const int32_t* idx[kMaxRegions];  // merge: the triples; SD: the texel indices
+    float* buf[kMaxRegions];          // SD: the packed depths
+    uint32_t stride[kMaxRegions];     // merge: the triples' row stride
+};
+
+__device__ __forceinline__ uint32_t list_of(const HaloLists& H, uint32_t g) {
+    uint32_t l = 0;
+    while (g >= H.first[l + 1]) ++l;
+    return l;
+}
+
+__global__ void __launch_bounds__(kHaloBlock) halo_merge_kernel(uint32_t* __restrict__ rmin, uint32_t* __restrict__ rmax,
+                                                                 HaloLists H, uint32_t total, uint32_t interval) {
+    const uint32_t g = blockIdx.x * kHaloBlock + threadIdx.x;
+    if (g >= H.first[H.n]) return;
+    const uint32_t l = list_of(H, g), k = g - H.first[l];
+    const int32_t* tr = H.idx[l];
+    const uint32_t t = (uint32_t)tr[k];
+    if (t >= total) return;  // never: the sender's indices lie in the map
+    if (interval) atomicMin(&rmin[t], (uint32_t)tr[H.stride[l] + k]);
+    atomicMax(&rmax[t], (uint32_t)tr[2u * H.stride[l] + k]);
+}
+
+// one lane per (list item, layer, channel): item-major within a list, so a list's lanes read its
+// index once per layer and channel (the L x n x ch packed layout is written / read in order per layer)
+template <bool GATHER>
+__global__ void __launch_bounds__(kHaloBlock) halo_sd_kernel(float* __restrict__ sd, HaloLists H, uint32_t layers,
+                                                              uint32_t texels, uint32_t ch) {
+    const uint32_t g = blockIdx.x * kHaloBlock + threadIdx.x;  // over sum_l layers * n_l * ch
+    if (g >= H.first[H.n]) return;
+    const uint32_t l = list_of(H, g), e = g - H.first[l];
+    const uint32_t n = (H.first[l + 1] - H.first[l]) / (layers * ch);
+    const uint32_t per = n * ch, L = e / per, rem = e % per, k = rem / ch, c = rem % ch;
+    const uint32_t t = (uint32_t)H.idx[l][k];
+    if (t >= texels) return;
+    const size_t so = ((size_t)L * texels + t) * ch + c;
+    if (GATHER) H.buf[l][e] = sd[so];
+    else sd[so] = H.buf[l][e];
+}
+
+rsd_status launch_check(const char* what) {
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? RSD_OK : hip_fail(e, what);
+}
+
+}  // namespace
+}  // namespace rsd
+
+using namespace rsd;
+
+extern "C" rsd_status rsd_halo_compact(const uint32_t* d_ray_min, const uint32_t* d_ray_max, uint32_t sd_w,
+                                       uint32_t sd_h, const rsd_halo_region* regions, uint32_t n_regions,
+                                       rsd_stream stream) {
+    if (!d_ray_min || !d_ray_max || (n_regions && !regions) || n_regions > kMaxRegions) {
+        set_error("rsd_halo_compact: null buffer or more than 64 regions");
+        return RSD_ERR_INVALID_ARG;
+    }
+    HaloRegions R{};
+    R.n = n_regions;
+    uint32_t total = 0;
+    hipStream_t s = (hipStream_t)stream;
+    for (uint32_t r = 0; r < n_regions; ++r) {
+        const rsd_halo_region& g = regions[r];
+        const uint64_t texels = (uint64_t)(g.row1 - g.row0) * sd_w;
+        if (g.row0 > g.row1 || g.row1 > sd_h || !g.out || !g.count || g.stride < texels ||
+            (uint64_t)total + texels > 0xffffffffull) {
+            set_error("rsd_halo_compact: region rows outside the map, null output, or stride below its texel count");
+            return RSD_ERR_INVALID_ARG;
+        }
+        R.first[r] = total;
+        R.row0[r] = g.row0;
+        R.stride[r] = g.stride;
+        R.out[r] = g.out;
+        R.count[r] = reinterpret_cast<unsigned long long*>(g.count);
+        total += (uint32_t)texels;
+    }
+    R.first[n_regions] = total;
+    if (n_regions == 0) return RSD_OK;
+    // the counts start at zero (one launch for all regions), then one compaction launch
+    hipLaunchKernelGGL(halo_zero_kernel, dim3(1), dim3(64), 0, s, R);
+    if (total == 0) return launch_check("halo_zero_kernel launch");
+    hipLaunchKernelGGL(halo_compact_kernel, dim3((total + kHaloBlock - 1) / kHaloBlock), dim3(kHaloBlock), 0, s,
+                       d_ray_min, d_ray_max, sd_w, R);
+    return launch_check("halo_compact_kernel launch");
+}
+
+extern "C" rsd_status rsd_halo_merge(uint32_t* d_ray_min, uint32_t* d_ray_max, uint32_t sd_w, uint32_t sd_h,
+                                     const rsd_halo_list* lists, uint32_t n_lists, uint32_t ray_interval,
+                                     rsd_stream stream) {
+    if (!d_ray_min || !d_ray_max || (n_lists && !lists) || n_lists > kMaxRegions) {
+        set_error("rsd_halo_merge: null buffer or more than 64 lists");
+        return RSD_ERR_INVALID_ARG;
+    }
+    HaloLists H{};
+    H.n = n_lists;
+    uint32_t total = 0;
+    for (uint32_t l = 0; l < n_lists; ++l) {
+        if ((lists[l].n && !lists[l].triples) || lists[l].stride < lists[l].n) {
+            set_error("rsd_halo_merge: null triples or stride below n");
+            return RSD_ERR_INVALID_ARG;
+        }
+        H.first[l] = total;
+        H.idx[l] = lists[l].triples;
+        H.stride[l] = lists[l].stride;
+        total += lists[l].n;
+    }
+    H.first[n_lists] = total;
+    if (total == 0) return RSD_OK;
+    hipLaunchKernelGGL(halo_merge_kernel, dim3((total + kHaloBlock - 1) / kHaloBlock), dim3(kHaloBlock), 0,
+                       (hipStream_t)stream, d_ray_min, d_ray_max, H, sd_w * sd_h, ray_interval ? 1u : 0u);
+    return launch_check("halo_merge_kernel launch");
+}
+
+namespace {
+rsd_status halo_sd(bool gather, float* sd, uint32_t layers, uint32_t sd_w, uint32_t sd_h, uint32_t ch,
+                   const rsd_halo_sd_list* lists, uint32_t n_lists, rsd_stream stream, const char* who) {
+    if (!sd || (n_lists && !lists) || n_lists > kMaxRegions || !layers || !ch || ch > 4) {
+        set_error(std::string(who) + ": null buffer, more than 64 lists, or layers / channels out of range");
+        return RSD_ERR_INVALID_ARG;
+    }
+    HaloLists H{};
+    H.n = n_lists;
+    uint64_t total = 0;
+    for (uint32_t l = 0; l < n_lists; ++l) {
+        if (lists[l].n && (!lists[l].idx || !lists[l].buf)) {
+            set_error(std::string(who) + ": null index list or buffer");
+            return RSD_ERR_INVALID_ARG;
+        }
+        H.first[l] = (uint32_t)total;
+        H.idx[l] = lists[l].idx;
+        H.buf[l] = lists[l].buf;
+        total += (uint64_t)lists[l].n * layers * ch;
+        if (total > 0xffffffffull) {
+            set_error(std::string(who) + ": more than 2^32 values");
+            return RSD_ERR_INVALID_ARG;
+        }
+    }
+    H.first[n_lists] = (uint32_t)total;
+    if (total == 0) return RSD_OK;
+    const dim3 grid((uint32_t)((total + kHaloBlock - 1) / kHaloBlock));
+    if (gather)
+        hipLaunchKernelGGL(halo_sd_kernel<true>, grid, dim3(kHaloBlock), 0, (hipStream_t)stream, sd, H, layers,
+                           sd_w * sd_h, ch);
+    else
+        hipLaunchKernelGGL(halo_sd_kernel<false>, grid, dim3(kHaloBlock), 0, (hipStream_t)stream, sd, H, layers,
+                           sd_w * sd_h, ch);
+    return launch_check(who);
+}
+}  // namespace
+
+extern "C" rsd_status rsd_halo_sd_gather(const float* d_sd, uint32_t layers, uint32_t sd_w, uint32_t sd_h, uint32_t ch,
+                                         const rsd_halo_sd_list* lists, uint32_t n_lists, rsd_stream stream) {
+    return halo_sd(true, const_cast<float*>(d_sd), layers, sd_w, sd_h, ch, lists, n_lists, stream,
+                   "rsd_halo_sd_gather");
+}
+
+extern "C" rsd_status rsd_halo_sd_scatter(float* d_sd, uint32_t layers, uint32_t sd_w, uint32_t sd_h, uint32_t ch,
+                                          const rsd_halo_sd_list* lists, uint32_t n_lists, rsd_stream stream) {
+    return halo_sd(false, d_sd, layers, sd_w, sd_h, ch, lists, n_lists, stream, "rsd_halo_sd_scatter");
+}

@@ -22,10 +22,6 @@
 #endif
 // fast numerics: clamped-radius pixels take the SCALED all-fast loops (sample_init); 0 = the per-lane
 // generic loops as in the exact build (A/B builds: make variant V=noscaled DEFS=-DRSD_SCALED_ALLFAST=0)
-// fast numerics: the all-fast pass-1 loops take 2 directions at a time (pass1_dir_pair); 1 = one at a time
-#ifndef RSD_P1_BATCH
-#define RSD_P1_BATCH 2
-#endif
 #ifndef RSD_SCALED_ALLFAST
 #define RSD_SCALED_ALLFAST 1
 #endif
@@ -35,7 +31,8 @@ namespace RSD_SVAO_NS {
 
 // One direction of SVAORaster.ps.slang:49-105 for one pixel: the reference loop body.  (Issuing the
 // reads of 2 or 4 directions before their bodies measured 77 / 91 vs 70 us: 77 / 105 VGPRs, 6 / 4 waves
-// per SIMD -- DESIGN.md section 4.)  SPEC: the specialised kernel of the StochasticDepth frame with ray
+// per SIMD -- DESIGN.md section 4; in the fast build 2 directions at 62 VGPRs, 8 waves, measured 48.7-49.0
+// vs 47.5 us, and 2-3 us per frame slower with frames in flight, profiles/round4/ab_pass/.)  SPEC: the specialised kernel of the StochasticDepth frame with ray
 // intervals, an SD guard band, pixel-index isSamePixel and a frame of at most 4096 x 4096 (every
 // BASELINE config) -- the run-time tests of those settings are compile-time constants there.
 template <bool SPEC, bool ALLFAST = false, bool SCALED = false>
@@ -94,57 +91,6 @@ __device__ __forceinline__ void pass1_dir_generic(const SvaoArgs& a, float u, fl
     }
 }
 
-// The second half of pass1_dir_generic<true, true, SCALED> (fast numerics), given the depth at the
-// sample's texel: the batched loop below issues the depth reads of two directions before either body.
-template <bool SCALED>
-__device__ __forceinline__ void pass1_dir_finish(const SvaoArgs& a, const Basic& b, int i, Sample& s, bool ssrAbove,
-                                                 bool same, float z, float& ao, float& aoD, uint32_t& st) {
-    const rsd_vao_data& d = a.d;
-    if (same) {  // isSamePixel (SVAORaster.ps.slang:55-60)
-        const float w = div_pdf(s.sphereStart - s.sphereEnd, s);
-        ao += w;
-        aoD += w;
-        return;
-    }
-    add_sample<true>(a, b, s, uv_to_view(a, s.ru, s.rv, z), true);  // evalPrimaryVisibility
-    ao += s.visibility;
-    bool forceRay = false;
-    if (!s.isInScreen) {
-        forceRay = true;
-        s.objectSpaceZ = 3.402823466e+38f;
-    }
-    const float constRadius = (1.0f + d.thickness) * b.radius - s.sphereStart;
-    if ((s.objectSpaceZ > s.sphereStart + constRadius && ssrAbove) || forceRay) {
-        st |= 1u << i;
-        const int sx = uv_to_sd(s.su, d.lowResolution[0], d.sdGuard);
-        const int sy = uv_to_sd(s.sv, d.lowResolution[1], d.sdGuard);
-        const size_t o = (size_t)sy * a.sdW + sx;
-        const float osMin = hmin(s.objectSpaceZ, b.radius + d.thickness * b.radius + s.sphereStart);
-        atomicMin(&a.rayMin[o], asuint(hmax(b.posVLength - osMin, 0.0f)));
-        atomicMax(&a.rayMax[o], asuint(hmax(b.posVLength - s.sphereEnd, 0.0f)));
-    } else {
-        aoD += s.visibility;
-    }
-}
-
-// Two directions of the fast all-fast loop at a time: both samples' set-up, both depth reads issued back
-// to back (one memory wait instead of two), then both bodies in direction order.  The reads are always
-// in bounds (depth_center_buf clamps; an invalid direction reads texel 0 and discards it).
-template <bool SCALED>
-__device__ __forceinline__ void pass1_dir_pair(const SvaoArgs& a, float u, float v, uint32_t px, uint32_t py,
-                                               const Basic& b, int i, float& ao, float& aoD, uint32_t& st,
-                                               const P1Bufs& bf) {
-    Sample s0, s1;
-    bool r0 = false, r1 = false;
-    s0.kx = s0.ky = s1.kx = s1.ky = 0;
-    const bool ok0 = sample_init<true, true, SCALED>(a, u, v, b, i, s0, r0, &bf);
-    const bool ok1 = sample_init<true, true, SCALED>(a, u, v, b, i + 1, s1, r1, &bf);
-    const float z0 = depth_center_buf(a, bf, s0.kx, s0.ky);
-    const float z1 = depth_center_buf(a, bf, s1.kx, s1.ky);
-    if (ok0) pass1_dir_finish<SCALED>(a, b, i, s0, r0, s0.kx == (int)px && s0.ky == (int)py, z0, ao, aoD, st);
-    if (ok1) pass1_dir_finish<SCALED>(a, b, i + 1, s1, r1, s1.kx == (int)px && s1.ky == (int)py, z1, ao, aoD, st);
-}
-
 // SVAORaster.ps.slang:29-122, [numthreads(16,16,1)] with the 2x2 group interleave.  (A branch-free
 // "lean" direction body -- host constants in SGPRs, predicated updates, one float ratio compare --
 // measured 74 vs 70 us at configs[1]: more VALU per direction and 64-73 VGPRs)
@@ -162,7 +108,15 @@ __global__ void __launch_bounds__(256) svao_pass1_kernel(SvaoArgs a) {
     uint32_t st = 0;
     Basic b;
     const P1Bufs bf = p1_bufs(a);  // uniform: built before any divergent branch
-    if (!basic_init<SPEC>(a, u, v, b)) {
+    // the specialised kernels: the 16 noise sines and cosines in LDS (a lane's noise index is its own, so the
+    // kernel-argument table would be a per-lane vector load, one more dependent round trip per pixel)
+    __shared__ float sNoise[SPEC ? 32 : 1];
+    if constexpr (SPEC) {
+        const uint32_t t = threadIdx.y * 16u + threadIdx.x;
+        if (t < 32u) sNoise[t] = t < 16u ? a.k.sinNoise[t] : a.k.cosNoise[t - 16u];
+        __syncthreads();
+    }
+    if (!basic_init<SPEC>(a, u, v, b, SPEC ? sNoise : nullptr)) {
         ao = aoD = 1.0f;
     } else {
         const int nd = ND > 0 ? ND : (int)a.k.nd;
@@ -174,26 +128,15 @@ __global__ void __launch_bounds__(256) svao_pass1_kernel(SvaoArgs a) {
         const bool posOk = kFastNumerics || (fabsf(b.posV.x) < 0x1p60f && fabsf(b.posV.y) < 0x1p60f);  // (div_unscaled bounds)
         if (SPEC && __ballot(b.radius != d.radius || !div_unscaled_den_ok(nzd) || !posOk) == 0u) {
             b.nzRcp = rcp_refined(nzd);
-            if constexpr (SPEC && kFastNumerics && RSD_P1_BATCH == 2) {
 #pragma unroll RSD_P1_UNROLL
-                for (int i = 0; i < nd; i += 2) pass1_dir_pair<false>(a, u, v, px, py, b, i, ao, aoD, st, bf);
-            } else {
-#pragma unroll RSD_P1_UNROLL
-                for (int i = 0; i < nd; ++i) pass1_dir_generic<SPEC, true>(a, u, v, px, py, b, i, ao, aoD, st, &bf);
-            }
+            for (int i = 0; i < nd; ++i) pass1_dir_generic<SPEC, true>(a, u, v, px, py, b, i, ao, aoD, st, &bf);
         } else if (SPEC && kFastNumerics && RSD_SCALED_ALLFAST) {
             // fast numerics: a wave with clamped-radius pixels (nearest the camera) takes the same lean
             // loop with the direction terms scaled per pixel instead of the per-lane IEEE paths
             b.nzRcp = rcp_refined(nzd);
             set_radius_scale(a, b);
-            if constexpr (RSD_P1_BATCH == 2) {
 #pragma unroll RSD_P1_UNROLL
-                for (int i = 0; i < nd; i += 2) pass1_dir_pair<true>(a, u, v, px, py, b, i, ao, aoD, st, bf);
-            } else {
-#pragma unroll RSD_P1_UNROLL
-                for (int i = 0; i < nd; ++i)
-                    pass1_dir_generic<SPEC, true, true>(a, u, v, px, py, b, i, ao, aoD, st, &bf);
-            }
+            for (int i = 0; i < nd; ++i) pass1_dir_generic<SPEC, true, true>(a, u, v, px, py, b, i, ao, aoD, st, &bf);
         } else {
 #pragma unroll RSD_P1_UNROLL
             for (int i = 0; i < nd; ++i) pass1_dir_generic<SPEC>(a, u, v, px, py, b, i, ao, aoD, st);
@@ -242,31 +185,36 @@ __global__ void __launch_bounds__(256) svao_pass1_kernel(SvaoArgs a) {
 // (ylx, yly) = rcp_refined of the SD resolution: the texel-centre uv divisions (cx - guard + jx) / low
 // go through div_unscaled -- the numerator is never 0 and >= 0.0037 in magnitude (the jitter table
 // lies in (0.0037, 0.9963), or 0.5 without jitter), so its preconditions hold.
-template <int N, bool SPEC = false, bool ALLFAST = false, bool SCALED = false>
+// KL > 0 (the specialised all-fast kernels): kl = the tile's LDS copy of the direction terms (sample_init)
+// followed by the 16 SD jitter pairs (rsd_device.h kJitter); the pair's reads -- the primary depth and the
+// N SD depths, no table -- are issued back to back, the depth first (vmcnt returns in order, so waiting for
+// the depth leaves the SD reads in flight)
+template <int N, bool SPEC = false, bool ALLFAST = false, bool SCALED = false, int KL = 0>
 __device__ __forceinline__ void svao_pass2_dir(const SvaoArgs& a, const Basic& b, float u, float v, int i, float& p,
-                                               float& r, float ylx = 0.0f, float yly = 0.0f) {
+                                               float& r, float ylx = 0.0f, float yly = 0.0f,
+                                               const float* kl = nullptr) {
     const rsd_vao_data& d = a.d;
     const float depthRange = a.cam.farZ - a.cam.nearZ, depthOffset = a.cam.nearZ;
     const size_t plane = sd_plane_texels(a.sdW, a.sdH);
     Sample s;
     bool ssrAbove;
-    sample_init<ALLFAST, SPEC, SCALED>(a, u, v, b, i, s, ssrAbove);
-    if (!SPEC && a.dualDepth) eval_dual(a, b, s, ssrAbove, true);  // Common.slang:555-558 (force init)
-    else eval_primary<SPEC, SPEC>(a, b, s);
-    p = s.visibility;
-    if (!SPEC && a.secondary == 1u) {
-        // secondary DualDepth: calcAO2 has no branch for it (Common.slang:562-651), so the raster
-        // visibility is subtracted and added back unchanged
-        r = p;
-        return;
+    sample_init<ALLFAST, SPEC, SCALED, KL>(a, u, v, b, i, s, ssrAbove, nullptr, kl);
+    float zp = 0.0f;
+    if constexpr (SPEC) {
+        zp = depth_center<true>(a, s.ru, s.rv, s.kx, s.ky);  // evalPrimaryVisibility's read, issued first
+    } else {
+        if (a.dualDepth) eval_dual(a, b, s, ssrAbove, true);  // Common.slang:555-558 (force init)
+        else eval_primary<SPEC, SPEC>(a, b, s);
+        p = s.visibility;
+        if (a.secondary == 1u) {
+            // secondary DualDepth: calcAO2 has no branch for it (Common.slang:562-651), so the raster
+            // visibility is subtracted and added back unchanged
+            r = p;
+            return;
+        }
     }
     const int cx = uv_to_sd(s.su, d.lowResolution[0], d.sdGuard);
     const int cy = uv_to_sd(s.sv, d.lowResolution[1], d.sdGuard);
-    float jx, jy;
-    sd_jitter((uint32_t)cx, (uint32_t)cy, a.sdJitter != 0u, jx, jy);
-    const float nu = (float)(cx - d.sdGuard) + jx, nv = (float)(cy - d.sdGuard) + jy;
-    const float su = SPEC ? div_unscaled(nu, d.lowResolution[0], ylx) : nu / d.lowResolution[0];
-    const float sv = SPEC ? div_unscaled(nv, d.lowResolution[1], yly) : nv / d.lowResolution[1];
     const size_t so = sd_texel(cx, cy, a.sdW);
     float dep[N];
     if constexpr (N == 1) {
@@ -281,6 +229,21 @@ __device__ __forceinline__ void svao_pass2_dir(const SvaoArgs& a, const Basic& b
             dep[4 * l] = t.x; dep[4 * l + 1] = t.y; dep[4 * l + 2] = t.z; dep[4 * l + 3] = t.w;
         }
     }
+    float jx, jy;
+    if constexpr (KL > 0) {
+        const uint32_t ji = ((uint32_t)(cy & 3) * 4u + (uint32_t)(cx & 3)) * 2u;
+        jx = a.sdJitter ? kl[6 * KL + ji] : 0.5f;
+        jy = a.sdJitter ? kl[6 * KL + ji + 1] : 0.5f;
+    } else {
+        sd_jitter((uint32_t)cx, (uint32_t)cy, a.sdJitter != 0u, jx, jy);
+    }
+    if constexpr (SPEC) {
+        add_sample<true>(a, b, s, uv_to_view(a, s.ru, s.rv, zp), true);  // evalPrimaryVisibility
+        p = s.visibility;
+    }
+    const float nu = (float)(cx - d.sdGuard) + jx, nv = (float)(cy - d.sdGuard) + jy;
+    const float su = SPEC ? div_unscaled(nu, d.lowResolution[0], ylx) : nu / d.lowResolution[0];
+    const float sv = SPEC ? div_unscaled(nv, d.lowResolution[1], yly) : nv / d.lowResolution[1];
     if (!s.isInScreen) {  // resetSample (Common.slang:485-490)
         s.visibility = (!SPEC && a.k.hbao) ? 0.0f : 1.0f;
         s.objectSpaceZ = 3.402823466e+38f;
@@ -327,8 +290,13 @@ constexpr int kP2Tile = 16;                   // pass-2 tile edge (pixels): 16 m
 constexpr int kP2Lanes = kP2Tile * kP2Tile;   // lanes per workgroup = pixels per tile
 static_assert(kP2Tile == (int)kTileEdge, "busy-tile flags are per pass-2 tile");
 // the LDS of one pass-2 tile (26 KB: 6 workgroups per CU)
-template <int ND, int NB = 16>
+template <int ND, int NB = 16, int KC = 0>
 struct P2Shared {
+    // the specialised kernels (KC = 6 ND + 64): the direction terms and SD jitter pairs sample_init and
+    // svao_pass2_dir read per pair (kl, KL = ND) and the noise terms basic_from reads per pixel, copied
+    // from the kernel arguments once per tile (per-lane indices: vector loads of kernel-argument memory,
+    // one dependent round trip each, otherwise)
+    float kc[KC > 0 ? KC : 1];
     uint32_t pix[kP2Lanes];        // active pixel slot: local index
     uint16_t pair[ND * kP2Lanes];  // pair: slot << 5 | direction
     uint16_t first[kP2Lanes];      // first pair of each slot
@@ -343,13 +311,23 @@ struct P2Shared {
 };
 
 // One kP2Tile^2 tile whose top-left pixel is (x0, y0); flag: its busy-tile flag (cleared) or null
-template <int N, int ND, bool SPEC, int NB>
+template <int N, int ND, bool SPEC, int NB, int KC>
 __device__ __forceinline__ void pass2_tile(const SvaoArgs& a, uint32_t x0, uint32_t y0, uint32_t* flag,
-                                           P2Shared<ND, NB>& sh) {
+                                           P2Shared<ND, NB, KC>& sh) {
     constexpr uint32_t T = kP2Tile, L = kP2Lanes;
     const uint32_t tid = threadIdx.x;
     const rsd_vao_data& d = a.d;
     if (tid == 0) { sh.nPix = 0u; sh.nPair = 0u; }
+    if constexpr (KC > 0) {
+        static_assert(KC == 6 * ND + 64, "kc layout: 6 direction tables of ND, 16 jitter pairs, 16 + 16 noise terms");
+        if (tid < (uint32_t)KC) {
+            const uint32_t t = tid % ND, w = tid / ND, j = tid - 6u * ND;
+            const float* src = w == 0 ? a.k.dirDx : w == 1 ? a.k.dirDy : w == 2 ? a.k.dirHeight
+                             : w == 3 ? a.k.rcpPdf : w == 4 ? a.k.rcpHeight : a.k.ratioMin;
+            sh.kc[tid] = tid < 6u * ND ? src[t] : j < 32u ? kJitter[j] : j < 48u ? a.k.sinNoise[j - 32u]
+                                                                                  : a.k.cosNoise[j - 48u];
+        }
+    }
     __syncthreads();
     {
         // every read of the tile's pixels is issued at once, independent of the stencil: the stencil, the
@@ -382,7 +360,7 @@ __device__ __forceinline__ void pass2_tile(const SvaoArgs& a, uint32_t x0, uint3
                 if (m & (1u << i)) sh.pair[j++] = (uint16_t)(slot << 5 | i);
             // a non-zero stencil means pass 1's basic_init of this pixel succeeded (same bits)
             Basic b;
-            basic_from(a, u, v, z, nl, b);
+            basic_from(a, u, v, z, nl, b, KC > 0 ? sh.kc + 6 * ND + 32 : nullptr);
             sh.aoPrev[slot] = prev;
             float* q = sh.basic[slot];
             q[0] = b.posV.x; q[1] = b.posV.y; q[2] = b.posV.z;
@@ -423,13 +401,15 @@ __device__ __forceinline__ void pass2_tile(const SvaoArgs& a, uint32_t x0, uint3
                 const float nzd = make_nonzero(b.normalO.z, 0.0001f);
                 const float ylx = rcp_refined(d.lowResolution[0]), yly = rcp_refined(d.lowResolution[1]);
                 const bool posOk = kFastNumerics || (fabsf(b.posV.x) < 0x1p60f && fabsf(b.posV.y) < 0x1p60f);
-                if (__ballot(b.radius != d.radius || !div_unscaled_den_ok(nzd) || !posOk) == 0u) {
-                    b.nzRcp = rcp_refined(nzd);
-                    svao_pass2_dir<N, true, true>(a, b, u, v, (int)(e & 31u), p, r, ylx, yly);
-                } else if (kFastNumerics && RSD_SCALED_ALLFAST) {  // clamped-radius pixels: the scaled lean path (pass 1's)
+                if (kFastNumerics && RSD_SCALED_ALLFAST) {
+                    // fast numerics: every pair through the scaled lean path (pass 1's SCALED loop; the
+                    // scale is exactly 1 for an unclamped pixel) -- one copy of the pair body, no vote
                     b.nzRcp = rcp_refined(nzd);
                     set_radius_scale(a, b);
-                    svao_pass2_dir<N, true, true, true>(a, b, u, v, (int)(e & 31u), p, r, ylx, yly);
+                    svao_pass2_dir<N, true, true, true, ND>(a, b, u, v, (int)(e & 31u), p, r, ylx, yly, sh.kc);
+                } else if (__ballot(b.radius != d.radius || !div_unscaled_den_ok(nzd) || !posOk) == 0u) {
+                    b.nzRcp = rcp_refined(nzd);
+                    svao_pass2_dir<N, true, true, false, ND>(a, b, u, v, (int)(e & 31u), p, r, ylx, yly, sh.kc);
                 } else {
                     svao_pass2_dir<N, true, false>(a, b, u, v, (int)(e & 31u), p, r, ylx, yly);
                 }
@@ -466,11 +446,11 @@ __device__ __forceinline__ void pass2_tile(const SvaoArgs& a, uint32_t x0, uint3
 template <int N, int ND, bool SPEC = false>
 __global__ void __launch_bounds__(kP2Lanes) svao_pass2_kernel(SvaoArgs a) {
     constexpr uint32_t kPerGroup = 32u / kP2Tile;  // tile rows per 32-row band group
-    __shared__ P2Shared<ND, SPEC ? 16 : 20> sh;
+    __shared__ P2Shared<ND, SPEC ? 16 : 20, SPEC ? 6 * ND + 64 : 0> sh;
     const uint32_t y0 = ((blockIdx.y / kPerGroup) * a.bandCount + a.bandIndex) * 32u + (blockIdx.y % kPerGroup) * kP2Tile +
                         a.guard;
     uint32_t* flag = a.tileFlags ? a.tileFlags + ((y0 - a.guard) / kP2Tile) * a.tilesX + blockIdx.x : nullptr;
-    if (!flag || *flag != 0u) pass2_tile<N, ND, SPEC, SPEC ? 16 : 20>(a, blockIdx.x * kP2Tile + a.guard, y0, flag, sh);
+    if (!flag || *flag != 0u) pass2_tile<N, ND, SPEC, SPEC ? 16 : 20, SPEC ? 6 * ND + 64 : 0>(a, blockIdx.x * kP2Tile + a.guard, y0, flag, sh);
 }
 
 // Whole-frame pass 2 over the busy-tile list pass 1 appended (tile_flags, ABI v5): workgroup i takes list
@@ -481,14 +461,14 @@ __global__ void __launch_bounds__(kP2Lanes) svao_pass2_kernel(SvaoArgs a) {
 // (105-109 VGPRs, occupancy 4, vs 78 and 6).
 template <int N, int ND, bool SPEC = false>
 __global__ void __launch_bounds__(kP2Lanes) svao_pass2_list_kernel(SvaoArgs a) {
-    __shared__ P2Shared<ND, SPEC ? 16 : 20> sh;
+    __shared__ P2Shared<ND, SPEC ? 16 : 20, SPEC ? 6 * ND + 64 : 0> sh;
     // the count of this frame's list (pass 1 of the same generation appended to it; the next pass 1
     // appends to the other one): read-only here, no reset and no completion ticket
     const uint32_t n = __builtin_amdgcn_readfirstlane(a.tileCount[a.tileGen]);
     if (blockIdx.x >= n) return;
     // uniform: the tile origin stays in scalar registers like blockIdx in the flag-grid kernel
     const uint32_t t = __builtin_amdgcn_readfirstlane(a.tileList[blockIdx.x]);
-    pass2_tile<N, ND, SPEC, SPEC ? 16 : 20>(a, (t % a.tilesX) * kP2Tile + a.guard, (t / a.tilesX) * kP2Tile + a.guard,
+    pass2_tile<N, ND, SPEC, SPEC ? 16 : 20, SPEC ? 6 * ND + 64 : 0>(a, (t % a.tilesX) * kP2Tile + a.guard, (t / a.tilesX) * kP2Tile + a.guard,
                                             a.tileFlags + t, sh);
 }
 

@@ -296,18 +296,21 @@ __device__ __forceinline__ void basic_reads(const SvaoArgs& a, float u, float v,
 }
 
 // Common.slang:285-324 from the reads above (z, nl = decode_normal_2x8(packed) from the device table)
-__device__ __forceinline__ bool basic_from(const SvaoArgs& a, float u, float v, float z, float4 nl, Basic& b);
+// noise: null, or an LDS copy of the 16 noise sines then the 16 cosines (pass 2's specialised tiles)
+__device__ __forceinline__ bool basic_from(const SvaoArgs& a, float u, float v, float z, float4 nl, Basic& b,
+                                           const float* noise = nullptr);
 
 // Common.slang:285-324
 template <bool SMALL = false>
-__device__ __forceinline__ bool basic_init(const SvaoArgs& a, float u, float v, Basic& b) {
+__device__ __forceinline__ bool basic_init(const SvaoArgs& a, float u, float v, Basic& b, const float* noise = nullptr) {
     float z;
     uint32_t packed;
     basic_reads<SMALL>(a, u, v, z, packed);
-    return basic_from(a, u, v, z, a.nlut[packed], b);  // nlut = decode_normal_2x8, tabulated on the device
+    return basic_from(a, u, v, z, a.nlut[packed], b, noise);  // nlut = decode_normal_2x8, tabulated on the device
 }
 
-__device__ __forceinline__ bool basic_from(const SvaoArgs& a, float u, float v, float z, float4 nl, Basic& b) {
+__device__ __forceinline__ bool basic_from(const SvaoArgs& a, float u, float v, float z, float4 nl, Basic& b,
+                                           const float* noise) {
     const rsd_vao_data& d = a.d;
     const float rux = (d.radius * a.cam.focalLength) / (a.cam.frameWidth * z);
     const float ruy = (d.radius * a.cam.focalLength) / (a.cam.frameHeight * z);
@@ -326,7 +329,8 @@ __device__ __forceinline__ bool basic_from(const SvaoArgs& a, float u, float v, 
     if (dot(b.posV, b.normalV) > 0.0f) b.normalV = -b.normalV;
     const float nu = u * d.noiseScale[0], nv = v * d.noiseScale[1];
     const int ni = ((int)floorf(nu * 4.0f)) & 3, nj = ((int)floorf(nv * 4.0f)) & 3;
-    const f3 rd = mk(a.k.sinNoise[nj * 4 + ni], a.k.cosNoise[nj * 4 + ni], 0.0f);
+    const f3 rd = noise ? mk(noise[nj * 4 + ni], noise[16 + nj * 4 + ni], 0.0f)
+                        : mk(a.k.sinNoise[nj * 4 + ni], a.k.cosNoise[nj * 4 + ni], 0.0f);
     b.normal = mk(-b.posV.x / b.posVLength, -b.posV.y / b.posVLength, -b.posV.z / b.posVLength);
     b.bitangent = normalize(cross(b.normal, rd));
     b.tangent = cross(b.bitangent, b.normal);
@@ -369,26 +373,41 @@ __device__ __forceinline__ bool ratio_le_tenth(float n, float D) {
 // sphereHeight = R sqrt(1 - r_i^2), pdf = 2 sphereHeight), so the host terms at VAOData.radius are
 // scaled by b.rScale = R / VAOData.radius (1 exactly when unclamped) -- the rounding differs from the
 // reference's order of operations by a few ulp, inside the fast-numerics tolerance
-template <bool ALLFAST = false, bool VAO = false, bool SCALED = false>
+// KL > 0 (with ALLFAST): the direction terms come from an LDS copy kl[6][KL] (dirDx, dirDy, dirHeight, rcpPdf,
+// rcpHeight, ratioMin) -- pass 2, whose lanes hold different directions: the kernel-argument tables would be
+// per-lane vector loads, one more dependent memory round trip per pair
+template <bool ALLFAST = false, bool VAO = false, bool SCALED = false, int KL = 0>
 __device__ __forceinline__ bool sample_init(const SvaoArgs& a, float u, float v, const Basic& b, int i, Sample& s,
-                                            bool& ssrAbove, const P1Bufs* bf = nullptr) {
+                                            bool& ssrAbove, const P1Bufs* bf = nullptr, const float* kl = nullptr) {
     const rsd_vao_data& d = a.d;
     float radius, dx, dy, sphereHeight;
     s.fast = false;
+    float ratioMin = 0.0f;
     if (ALLFAST) {
         radius = a.k.dirRadius[i];
-        dx = a.k.dirDx[i];
-        dy = a.k.dirDy[i];
-        sphereHeight = a.k.dirHeight[i];
         s.fast = true;
-        s.yPdf = a.k.rcpPdf[i];
-        s.yHeight = a.k.rcpHeight[i];
+        if constexpr (KL > 0) {
+            dx = kl[i];
+            dy = kl[KL + i];
+            sphereHeight = kl[2 * KL + i];
+            s.yPdf = kl[3 * KL + i];
+            s.yHeight = kl[4 * KL + i];
+            ratioMin = kl[5 * KL + i];
+        } else {
+            dx = a.k.dirDx[i];
+            dy = a.k.dirDy[i];
+            sphereHeight = a.k.dirHeight[i];
+            s.yPdf = a.k.rcpPdf[i];
+            s.yHeight = a.k.rcpHeight[i];
+            ratioMin = a.k.ratioMin[i];
+        }
         if constexpr (SCALED) {
             dx *= b.rScale;
             dy *= b.rScale;
             sphereHeight *= b.rScale;
             s.yPdf *= b.rScaleInv;
             s.yHeight *= b.rScaleInv;
+            ratioMin *= b.rScale;
         }
     } else if (b.radius == d.radius) {  // the host-evaluated terms (same operations, same bits)
         radius = a.k.dirRadius[i];
@@ -415,7 +434,7 @@ __device__ __forceinline__ bool sample_init(const SvaoArgs& a, float u, float v,
     }
     s.sphereEnd = hmin(hmax(zi, -sphereHeight), sphereHeight);
     // (sphereStart - sphereEnd is never NaN: hmax maps a NaN zi to -sphereHeight)
-    if (ALLFAST ? !(s.sphereStart - s.sphereEnd >= (SCALED ? a.k.ratioMin[i] * b.rScale : a.k.ratioMin[i]))
+    if (ALLFAST ? !(s.sphereStart - s.sphereEnd >= ratioMin)
                 : ratio_le_tenth(s.sphereStart - s.sphereEnd, 2.0f * sphereHeight))
         return false;
     const f3 ip = b.posV + b.tangent * dx + b.bitangent * dy;

@@ -96,6 +96,19 @@ NUMERICS_FAST, NUMERICS_EXACT = 0, 1  # rsd.h rsd_numerics
 NUMERICS = {"fast": NUMERICS_FAST, "exact": NUMERICS_EXACT}
 
 
+class HaloRegion(C.Structure):  # rsd_halo_region
+    _fields_ = [("row0", C.c_uint32), ("row1", C.c_uint32), ("out", C.c_void_p), ("stride", C.c_uint32),
+                ("pad", C.c_uint32), ("count", C.c_void_p)]
+
+
+class HaloList(C.Structure):  # rsd_halo_list
+    _fields_ = [("triples", C.c_void_p), ("n", C.c_uint32), ("stride", C.c_uint32)]
+
+
+class HaloSdList(C.Structure):  # rsd_halo_sd_list
+    _fields_ = [("idx", C.c_void_p), ("buf", C.c_void_p), ("n", C.c_uint32), ("pad", C.c_uint32)]
+
+
 class FrameDesc(C.Structure):  # rsd_svao_frame_desc
     _fields_ = [("scene", C.c_void_p), ("cam", C.c_void_p), ("vao", C.c_void_p), ("svao", C.c_void_p),
                 ("sd", C.c_void_p), ("d_depth", C.c_void_p), ("d_normals", C.c_void_p), ("width", C.c_uint32),
@@ -135,7 +148,8 @@ EXPORTS = ["rsd_abi_version", "rsd_svao_tile_count", "rsd_last_error", "rsd_devi
            "rsd_sd_trace_band", "rsd_svao_pass1_band", "rsd_svao_pass2_band", "rsd_gbuffer_raster",
            "rsd_linearize_depth", "rsd_compress_normals", "rsd_svao_pass2_raytraced", "rsd_svao_pass2_raytraced_band",
            "rsd_scene_upload_alpha", "rsd_ray_cone_spread", "rsd_sd_trace_band_ex", "rsd_scene_export_bvh",
-           "rsd_bvh_build", "rsd_svao_pass1_rows", "rsd_svao_pass2_rows", "rsd_sd_trace_rows", "rsd_svao_frame"]
+           "rsd_bvh_build", "rsd_svao_pass1_rows", "rsd_svao_pass2_rows", "rsd_sd_trace_rows", "rsd_svao_frame",
+           "rsd_halo_compact", "rsd_halo_merge", "rsd_halo_sd_gather", "rsd_halo_sd_scatter"]
 
 SD_CONSUME_INTERVALS = 1
 SD_THROUGHPUT = 2  # frames in flight: the work-efficient traversal (rsd.h RSD_SD_THROUGHPUT)
@@ -230,6 +244,14 @@ def lib():
                                         u32, u32, u32, u32, C.POINTER(Counters), vp]
         L.rsd_svao_frame.restype = st
         L.rsd_svao_frame.argtypes = [C.POINTER(FrameDesc), u32, vp, vp]
+        L.rsd_halo_compact.restype = st
+        L.rsd_halo_compact.argtypes = [vp, vp, u32, u32, C.POINTER(HaloRegion), u32, vp]
+        L.rsd_halo_merge.restype = st
+        L.rsd_halo_merge.argtypes = [vp, vp, u32, u32, C.POINTER(HaloList), u32, u32, vp]
+        L.rsd_halo_sd_gather.restype = st
+        L.rsd_halo_sd_gather.argtypes = [vp, u32, u32, u32, u32, C.POINTER(HaloSdList), u32, vp]
+        L.rsd_halo_sd_scatter.restype = st
+        L.rsd_halo_sd_scatter.argtypes = [vp, u32, u32, u32, u32, C.POINTER(HaloSdList), u32, vp]
         L.rsd_svao_pass2_raytraced.restype = st
         L.rsd_svao_pass2_raytraced.argtypes = [vp, C.POINTER(Camera), C.POINTER(VAOData), C.POINTER(SVAOParams), vp, vp,
                                                u32, u32, vp, vp, u32, u32, u32, vp]

@@ -354,6 +354,9 @@ class HaloFrame:
         self.rebalance = rebalance and world > 1
         self.halo_px = halo_px(cfg, float(b.vao.ssMaxRadius))
         self.cuda = b.sd.is_cuda
+        # the halo's device steps through librsd (rsd_halo_*: one call each instead of a dozen torch ops
+        # per peer); the CPU rehearsal backends (gloo tests) keep the torch formulation of the same steps
+        self.native = self.cuda and hasattr(b, "stream")
         self._ao_cap = 0
         self._next_gb = None
         self._prev = None  # timing events of this object's previous frame
@@ -405,6 +408,16 @@ class HaloFrame:
         shape = (self.ao_max,) + tuple(b.ao.shape[1:])
         self.ao_send = self._ao_send_buf[:self.ao_max * row].view(shape)
         self.ao_recv = self._ao_recv_buf[:world * self.ao_max * row].view((world,) + shape)
+        # the other bands' rows of the gathered AO: one index_select + one index_copy per frame
+        # (built by device arange kernels: a host list copied to the device would be a synchronous copy)
+        aod = b.ao.device
+        others = [(k, lo, hi) for k, (lo, hi) in enumerate(self.ao_rows) if k != me and hi > lo]
+        self._ao_dst = torch.cat([torch.arange(lo, hi, dtype=torch.int64, device=aod) for _, lo, hi in others]) \
+            if others else torch.zeros(0, dtype=torch.int64, device=aod)
+        self._ao_src = torch.cat([torch.arange(k * self.ao_max, k * self.ao_max + hi - lo, dtype=torch.int64, device=aod)
+                                  for k, lo, hi in others]) if others else torch.zeros(0, dtype=torch.int64, device=aod)
+        if not hasattr(self, "_bufs"):
+            self._bufs = {}  # grow-only per-peer exchange buffers (_buf)
         # device compaction of the touched texels: per peer, the candidate region's texel indices and a
         # [3, cap + 1] int32 buffer (column cap collects the untouched texels' scatter writes)
         if world > 1:
@@ -415,12 +428,19 @@ class HaloFrame:
                 if rows:
                     lo, hi = rows
                     n = (hi - lo) * sdw
-                    self._cand[k] = (lo, hi, torch.arange(lo * sdw, hi * sdw, dtype=torch.int32, device=dev),
-                                     torch.empty((3, n + 1), dtype=torch.int32, device=dev))
+                    # the device path (librsd rsd_halo_compact) needs no index list
+                    idx = None if self.native else torch.arange(lo * sdw, hi * sdw, dtype=torch.int32, device=dev)
+                    self._cand[k] = (lo, hi, idx, torch.empty((3, n + 1), dtype=torch.int32, device=dev))
             self._row = torch.zeros(world + 1, dtype=torch.int64, device=dev)
             self._M_dev = torch.zeros((world, world + 1), dtype=torch.int64, device=dev)
             self._M_host = torch.zeros((world, world + 1), dtype=torch.int64,
                                        pin_memory=self.cuda and torch.cuda.is_available())
+            if self.native:
+                from . import abi
+                regs = [abi.HaloRegion(lo, hi, buf.data_ptr(), buf.shape[1], 0, self._row.data_ptr() + 8 * k)
+                        for k, (lo, hi, _, buf) in self._cand.items()]
+                self._regions = (abi.HaloRegion * max(1, len(regs)))(*regs)
+                self._n_regions = len(regs)
 
     def dense_bytes_per_frame(self):
         """What the round-2 dense halo (whole candidate rows) would send per frame from this rank."""
@@ -434,6 +454,19 @@ class HaloFrame:
         """Mean bytes this rank sent per frame so far: sparse interval halo, sparse SD halo, AO band."""
         n = max(1, self.frames)
         return {k: int(v // n) for k, v in self.sent.items()}
+
+    def _buf(self, kind, k, shape, dtype, device):
+        """A contiguous tensor of `shape` carved from a grow-only flat buffer per (kind, peer): the exchange
+        buffers of a frame are the previous frame's memory (stream-ordered reuse; the comm's handshakes
+        order the peers' reads), so steady state allocates nothing."""
+        n = 1
+        for x in shape:
+            n *= x
+        cur = self._bufs.get((kind, k))
+        if cur is None or cur.numel() < n or cur.dtype != dtype:
+            cur = torch.empty(max(n, 1) * 3 // 2 + 64, dtype=dtype, device=device)
+            self._bufs[(kind, k)] = cur
+        return cur[:n].view(shape)
 
     # ---- timing of this rank's compute (load balance)
     def _mark(self):
@@ -462,19 +495,16 @@ class HaloFrame:
         """The next split of the 32-row groups from every rank's measured cost of the current one:
         cost spread uniformly over each band's groups, boundaries where the cumulative cost crosses
         k / world of the total, moved half-way (damping), at least one group per rank."""
+        import numpy as np
         G, world, gb = self.G, self.world, self.gb
-        dens = []
-        for r in range(world):
-            n = gb[r + 1] - gb[r]
-            dens += [max(float(costs[r]), 1e-3) / max(n, 1)] * n
-        cum = [0.0]
-        for x in dens:
-            cum.append(cum[-1] + x)
+        n = np.diff(np.asarray(gb))
+        dens = np.repeat(np.maximum(np.asarray(costs, dtype=np.float64), 1e-3) / np.maximum(n, 1), n)
+        cum = np.concatenate(([0.0], np.cumsum(dens)))  # left-to-right float64 sums, as a Python loop adds
         total = cum[-1]
         new = [0]
         for k in range(1, world):
             target = total * k / world
-            j = next((i for i in range(1, G + 1) if cum[i] >= target), G)
+            j = min(int(np.searchsorted(cum[1:], target, side="left")) + 1, G)  # first i >= 1 with cum[i] >= target
             # the nearer of the two group boundaries around the crossing
             if j > 0 and target - cum[j - 1] < cum[j] - target:
                 j -= 1
@@ -513,14 +543,22 @@ class HaloFrame:
         st["t"].append(self._mark())
         if world > 1:
             row = self._row
-            row.zero_()
-            for k, (lo, hi, idx, buf) in self._cand.items():
-                reg = b.ray_minmax[:, lo:hi].reshape(2, -1)
-                touched = (reg[0] != FLT_MAX_BITS) | (reg[1] != 0)
-                pos = torch.cumsum(touched, 0)  # int64: 1-based position of each touched texel
-                dst = torch.where(touched, pos - 1, torch.full_like(pos, buf.shape[1] - 1))
-                buf.scatter_(1, dst.expand(3, -1), torch.stack((idx, reg[0], reg[1])))
-                row[k:k + 1].copy_(pos[-1:])
+            if self.native:
+                # rsd_halo_compact: every peer's touched texels as triples and their counts in row[k] (the other
+                # entries of row stay 0); triple order unspecified -- the receiver's min / max merge is exact
+                from . import abi
+                _, sdh, sdw = b.ray_minmax.shape
+                abi.check(abi.lib().rsd_halo_compact(b.ray_minmax[0].data_ptr(), b.ray_minmax[1].data_ptr(), sdw, sdh,
+                                                     self._regions, self._n_regions, b.stream), "rsd_halo_compact")
+            else:
+                row.zero_()
+                for k, (lo, hi, idx, buf) in self._cand.items():
+                    reg = b.ray_minmax[:, lo:hi].reshape(2, -1)
+                    touched = (reg[0] != FLT_MAX_BITS) | (reg[1] != 0)
+                    pos = torch.cumsum(touched, 0)  # int64: 1-based position of each touched texel
+                    dst = torch.where(touched, pos - 1, torch.full_like(pos, buf.shape[1] - 1))
+                    buf.scatter_(1, dst.expand(3, -1), torch.stack((idx, reg[0], reg[1])))
+                    row[k:k + 1].copy_(pos[-1:])
             row[world:].fill_(prev_us)  # a kernel argument (row[world] = x is a synchronous host-to-device copy)
             self.comm.all_gather(self._M_dev, row)
             self._M_host.copy_(self._M_dev, non_blocking=True)
@@ -547,18 +585,33 @@ class HaloFrame:
                 self._next_gb = self._rebalanced([float(x) for x in M[:, world]])
             dev = b.ray_minmax.device
             iv_send = {k: self._cand[k][3][:, :int(M[me, k])] for k in self._cand if M[me, k] > 0}
-            iv_recv = {k: torch.empty((3, int(M[k, me])), dtype=torch.int32, device=dev)
+            iv_recv = {k: self._buf("iv", k, (3, int(M[k, me])), torch.int32, dev)
                        for k in range(world) if k != me and M[k, me] > 0}
             self.comm.exchange(iv_send, iv_recv)
             self.sent["intervals"] += sum(x.numel() * 4 for x in iv_send.values())
-            for k, x in iv_send.items():
-                mine[k] = x[0].long()
-            for k, x in iv_recv.items():
-                idx = x[0].long()
-                theirs[k] = idx
-                if b.cfg.ray_interval:
-                    b.ray_minmax[0].view(-1).scatter_reduce_(0, idx, x[1], reduce="amin")
-                b.ray_minmax[1].view(-1).scatter_reduce_(0, idx, x[2], reduce="amax")
+            if self.native:
+                from . import abi
+                L_ = abi.lib()
+                _, sdh, sdw = b.ray_minmax.shape
+                for k, x in iv_send.items():
+                    mine[k] = x[0]  # int32 texel indices (row 0 of the persistent triple buffer)
+                for k, x in iv_recv.items():
+                    theirs[k] = x[0]
+                if iv_recv:  # every peer's triples in one launch
+                    lists = (abi.HaloList * len(iv_recv))(*[abi.HaloList(x.data_ptr(), x.shape[1], x.shape[1])
+                                                            for x in iv_recv.values()])
+                    abi.check(L_.rsd_halo_merge(b.ray_minmax[0].data_ptr(), b.ray_minmax[1].data_ptr(), sdw, sdh,
+                                                lists, len(iv_recv), int(bool(b.cfg.ray_interval)), b.stream),
+                              "rsd_halo_merge")
+            else:
+                for k, x in iv_send.items():
+                    mine[k] = x[0].long()
+                for k, x in iv_recv.items():
+                    idx = x[0].long()
+                    theirs[k] = idx
+                    if b.cfg.ray_interval:
+                        b.ray_minmax[0].view(-1).scatter_reduce_(0, idx, x[1], reduce="amin")
+                    b.ray_minmax[1].view(-1).scatter_reduce_(0, idx, x[2], reduce="amax")
         if sd_events:
             sd_events[0].record()
         t.append(self._mark())
@@ -573,13 +626,31 @@ class HaloFrame:
         if world > 1:
             L, sdh, sdw, ch = b.sd.shape
             flat_sd = b.sd.view(L, sdh * sdw, ch)
-            sd_send = {k: flat_sd.index_select(1, idx) for k, idx in theirs.items()}
-            sd_recv = {k: torch.empty((L, idx.numel(), ch), dtype=b.sd.dtype, device=b.sd.device)
+            if self.native:
+                from . import abi
+                L_ = abi.lib()
+                sd_send = {k: self._buf("sds", k, (L, idx.numel(), ch), b.sd.dtype, b.sd.device)
+                           for k, idx in theirs.items()}
+                if sd_send:  # every peer's reply in one launch
+                    lists = (abi.HaloSdList * len(sd_send))(*[abi.HaloSdList(theirs[k].data_ptr(), x.data_ptr(),
+                                                                             x.shape[1], 0) for k, x in sd_send.items()])
+                    abi.check(L_.rsd_halo_sd_gather(b.sd.data_ptr(), L, sdw, sdh, ch, lists, len(sd_send), b.stream),
+                              "rsd_halo_sd_gather")
+            else:
+                sd_send = {k: flat_sd.index_select(1, idx) for k, idx in theirs.items()}
+            sd_recv = {k: self._buf("sdr", k, (L, idx.numel(), ch), b.sd.dtype, b.sd.device)
                        for k, idx in mine.items() if idx.numel()}
             self.comm.exchange(sd_send, sd_recv)
             self.sent["sd"] += sum(x.numel() * x.element_size() for x in sd_send.values())
-            for k, x in sd_recv.items():
-                flat_sd.index_copy_(1, mine[k], x)
+            if self.native:
+                if sd_recv:
+                    lists = (abi.HaloSdList * len(sd_recv))(*[abi.HaloSdList(mine[k].data_ptr(), x.data_ptr(),
+                                                                             x.shape[1], 0) for k, x in sd_recv.items()])
+                    abi.check(L_.rsd_halo_sd_scatter(b.sd.data_ptr(), L, sdw, sdh, ch, lists, len(sd_recv), b.stream),
+                              "rsd_halo_sd_scatter")
+            else:
+                for k, x in sd_recv.items():
+                    flat_sd.index_copy_(1, mine[k], x)
         t.append(self._mark())
         b.pass2_rows(self.px_rows[me])
         t.append(self._mark())
@@ -590,7 +661,6 @@ class HaloFrame:
             send[:hi - lo].copy_(b.ao[lo:hi])
             self.comm.all_gather(recv, send)
             self.sent["ao"] += send.numel() * send.element_size()
-            for k, (lo, hi) in enumerate(self.ao_rows):
-                if k != me:
-                    b.ao[lo:hi].copy_(recv[k, :hi - lo])
+            if self._ao_dst.numel():
+                b.ao.index_copy_(0, self._ao_dst, recv.view((-1,) + tuple(b.ao.shape[1:])).index_select(0, self._ao_src))
         self.frames += 1

@@ -47,7 +47,9 @@ def test_struct_layouts_match_header(abi, tmp_path):
     structs = {"rsd_scene_desc": abi.SceneDesc, "rsd_scene_info": abi.SceneInfo, "rsd_camera": abi.Camera,
                "rsd_sd_params": abi.SDParams, "rsd_vao_data": abi.VAOData, "rsd_svao_params": abi.SVAOParams,
                "rsd_counters": abi.Counters, "rsd_texture": abi.Texture,
-               "rsd_alpha_texture": abi.AlphaTexture, "rsd_material": abi.Material, "rsd_alpha_desc": abi.AlphaDesc}
+               "rsd_alpha_texture": abi.AlphaTexture, "rsd_material": abi.Material, "rsd_alpha_desc": abi.AlphaDesc,
+               "rsd_svao_frame_desc": abi.FrameDesc, "rsd_halo_region": abi.HaloRegion,
+               "rsd_halo_list": abi.HaloList, "rsd_halo_sd_list": abi.HaloSdList}
     src = "#include <stdio.h>\n#include \"rsd_graph.h\"\nint main(void){\n"
     for name in structs:
         src += f'printf("%zu\\n", sizeof({name}));\n'
