@@ -190,7 +190,9 @@ def main():
             # pass 1 over the whole frame = the exact interval union a band frame all-reduces
             r.clear_intervals()
             r.pass1()
-            if shard == "band":
+            if shard == "band" and seq.sd_band is not None:  # N > 1: this rank's round-robin SD tiles
+                acc.append(r.sd_trace(counters=True, band=seq.sd_band, throughput=thr))
+            elif shard == "band":
                 acc.append(r.sd_trace_rows(seq.sd_rows[rank], counters=True, throughput=thr))
             else:
                 acc.append(r.sd_trace(counters=True, throughput=thr, band=bw))

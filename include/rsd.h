@@ -394,17 +394,20 @@ rsd_status rsd_sd_trace_rows(rsd_scene* scene, const rsd_camera* cam, const rsd_
  * Device-side steps around the point-to-point transfers, one call each instead of a dozen small torch
  * ops per peer (the host issue cost of an N > 1 frame).  No host synchronisation.
  *
- * rsd_halo_compact: for each region r (SD rows [row0, row1) of the interval maps), the touched texels
- * (rayMin != asuint(FLT_MAX) or rayMax != 0; SVAO.cpp:334-340's cleared state) are written as int32
- * triples -- texel index, rayMin bits, rayMax bits -- to out[r] (three rows of `stride` int32:
- * out[r][0 .. n), out[r][stride ..], out[r][2 stride ..]; stride >= the region's texel count) in an
- * unspecified order, and their number to counts[r] (int64, overwritten).  The merge below is
- * order-independent (min / max), so the order does not change a result bit. */
+ * rsd_halo_compact: for each region r, the touched texels (rayMin != asuint(FLT_MAX) or rayMax != 0;
+ * SVAO.cpp:334-340's cleared state) are written as int32 triples -- texel index, rayMin bits, rayMax
+ * bits -- to out[r] (three rows of `stride` int32: out[r][0 .. n), out[r][stride ..], out[r][2 stride ..];
+ * stride >= the region's texel count) in an unspecified order, and their number to *count[r] (int64,
+ * overwritten; regions may share an output and a count).  The merge below is order-independent
+ * (min / max), so the order does not change a result bit.
+ * A region is SD rows [row0, row1) (period <= 1), or (period > 1; row0 a multiple of 8) the 8-row SD
+ * tiles t = row0 / 8 + j period that start below row1 -- one rank's tiles when the SD trace's tiles
+ * are dealt round-robin to the ranks (rsd_sd_trace_band_ex with band_count = period). */
 typedef struct {
     uint32_t row0, row1;  /* SD-map rows of the region */
     int32_t* out;         /* 3 x stride int32 (device) */
     uint32_t stride;
-    uint32_t pad;
+    uint32_t period;      /* 0 / 1: rows [row0, row1); > 1: every period-th 8-row tile from row0 */
     int64_t* count;       /* device int64, overwritten */
 } rsd_halo_region;
 rsd_status rsd_halo_compact(const uint32_t* d_ray_min, const uint32_t* d_ray_max, uint32_t sd_w, uint32_t sd_h,

@@ -20,10 +20,14 @@ constexpr uint32_t kHaloBlock = 256;
 constexpr uint32_t kFltMaxBits = 0x7f7fffffu;  // asuint(FLT_MAX): a cleared rayMin (SVAO.cpp:339)
 constexpr uint32_t kMaxRegions = 64;
 
+constexpr uint32_t kSdTile = 8;  // SD trace tile rows (sd_trace.hip kTile): the round-robin unit of the tiled split
+
 struct HaloRegions {
     uint32_t n;
     uint32_t first[kMaxRegions + 1];  // first texel of each region (flattened grid of all regions' texels)
     uint32_t row0[kMaxRegions];
+    uint32_t row1[kMaxRegions];
+    uint32_t period[kMaxRegions];     // 1: contiguous rows; > 1: every period-th 8-row tile from row0
     uint32_t stride[kMaxRegions];
     int32_t* out[kMaxRegions];
     unsigned long long* count[kMaxRegions];
@@ -37,10 +41,22 @@ __global__ void __launch_bounds__(kHaloBlock) halo_compact_kernel(const uint32_t
                                                                    const uint32_t* __restrict__ rmax, uint32_t sdW,
                                                                    HaloRegions R) {
     const uint32_t g = blockIdx.x * kHaloBlock + threadIdx.x;
-    const bool in = g < R.first[R.n];
+    bool in = g < R.first[R.n];
     uint32_t r = 0;
     while (in && g >= R.first[r + 1]) ++r;
-    const uint32_t t = in ? R.row0[r] * sdW + (g - R.first[r]) : 0u;
+    uint32_t t = 0u;
+    if (in) {
+        const uint32_t e = g - R.first[r];
+        uint32_t row;
+        if (R.period[r] <= 1u) {
+            row = R.row0[r] + e / sdW;
+        } else {  // tile j of the region: SD tile row0 / 8 + j period (whole tiles; rows past row1 skipped)
+            const uint32_t per = kSdTile * sdW, j = e / per;
+            row = R.row0[r] + j * R.period[r] * kSdTile + (e % per) / sdW;
+        }
+        in = row < R.row1[r];
+        t = row * sdW + e % sdW;
+    }
     const uint32_t lo = in ? rmin[t] : kFltMaxBits, hi = in ? rmax[t] : 0u;
     const bool touched = lo != kFltMaxBits || hi != 0u;
     // one atomic per (wave, region) the wave's touched texels fall in
@@ -132,14 +148,21 @@ extern "C" rsd_status rsd_halo_compact(const uint32_t* d_ray_min, const uint32_t
     hipStream_t s = (hipStream_t)stream;
     for (uint32_t r = 0; r < n_regions; ++r) {
         const rsd_halo_region& g = regions[r];
-        const uint64_t texels = (uint64_t)(g.row1 - g.row0) * sd_w;
+        const uint32_t period = g.period > 1u ? g.period : 1u;
+        // the flattened texels of the region: its rows, or its whole tiles (rows past row1 masked)
+        const uint64_t tiles = period > 1u && g.row1 > g.row0
+                                   ? ((g.row1 - g.row0 + kSdTile - 1) / kSdTile + period - 1) / period : 0u;
+        const uint64_t texels = period > 1u ? tiles * kSdTile * sd_w : (uint64_t)(g.row1 - g.row0) * sd_w;
         if (g.row0 > g.row1 || g.row1 > sd_h || !g.out || !g.count || g.stride < texels ||
-            (uint64_t)total + texels > 0xffffffffull) {
-            set_error("rsd_halo_compact: region rows outside the map, null output, or stride below its texel count");
+            (period > 1u && g.row0 % kSdTile != 0u) || (uint64_t)total + texels > 0xffffffffull) {
+            set_error("rsd_halo_compact: region rows outside the map, null output, stride below its texel count, "
+                      "or a tiled region not starting on an 8-row tile");
             return RSD_ERR_INVALID_ARG;
         }
         R.first[r] = total;
         R.row0[r] = g.row0;
+        R.row1[r] = g.row1;
+        R.period[r] = period;
         R.stride[r] = g.stride;
         R.out[r] = g.out;
         R.count[r] = reinterpret_cast<unsigned long long*>(g.count);

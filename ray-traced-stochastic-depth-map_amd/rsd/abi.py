@@ -98,7 +98,7 @@ NUMERICS = {"fast": NUMERICS_FAST, "exact": NUMERICS_EXACT}
 
 class HaloRegion(C.Structure):  # rsd_halo_region
     _fields_ = [("row0", C.c_uint32), ("row1", C.c_uint32), ("out", C.c_void_p), ("stride", C.c_uint32),
-                ("pad", C.c_uint32), ("count", C.c_void_p)]
+                ("period", C.c_uint32), ("count", C.c_void_p)]
 
 
 class HaloList(C.Structure):  # rsd_halo_list

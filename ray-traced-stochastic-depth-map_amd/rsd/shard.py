@@ -340,9 +340,16 @@ class HaloFrame:
     `comm`: DistComm (default; torch.distributed) or LocalComm (threads on one GPU)."""
 
     def __init__(self, backend, rank: int = 0, world: int = 1, pg=None, throughput: bool = False,
-                 rebalance: bool = True, comm=None):
+                 rebalance: bool = True, comm=None, sd_split: str = "tiles"):
         b = self.b = backend
         self.rank, self.world, self.pg = rank, world, pg
+        if sd_split not in ("tiles", "rows"):
+            raise ValueError("HaloFrame sd_split must be 'tiles' or 'rows'")
+        # who traces which SD texel: "tiles" deals the 8-row SD tiles round-robin to the ranks (tile t to
+        # rank t % world), so every rank traces a share of the frame's long rays -- the trace is
+        # latency-bound by its slowest rays, which cluster on the screen (DESIGN.md section 6); "rows":
+        # the SD rows under each rank's pass-1 band (HaloFrame v4)
+        self.sd_split = sd_split if world > 1 else "rows"
         self.comm = comm if comm is not None else (DistComm(pg) if world > 1 else None)
         self.nccl = bool(getattr(self.comm, "nccl", False))
         self.trace_kw = {"throughput": True} if throughput and getattr(b, "can_consume_intervals", False) else {}
@@ -379,6 +386,7 @@ class HaloFrame:
         for r in range(1, world + 1):
             S[r] = max(S[r], S[r - 1])
         self.sd_rows = [(S[r], S[r + 1]) for r in range(world)]
+        self.sd_band = (me, world) if self.sd_split == "tiles" else None  # rsd_sd_trace_band_ex's tiles
         self.window = []
         for r in range(world):
             a_px = g + self.px_rows[r][0] - self.halo_px
@@ -389,9 +397,20 @@ class HaloFrame:
             lo, hi = max(a[0], c[0]), min(a[1], c[1])
             return (lo, hi) if lo < hi else None
         # candidate rows: my window inside band k (my intervals -> k, k's depths -> me), and k's
-        # window inside my band (k's intervals -> me, my depths -> k)
-        self.iv_send = {k: overlap(self.window[me], self.sd_rows[k]) for k in range(world) if k != me}
-        self.iv_recv = {k: overlap(self.window[k], self.sd_rows[me]) for k in range(world) if k != me}
+        # window inside my band (k's intervals -> me, my depths -> k); tiles: my window's tiles of rank k
+        # (from the first tile of k at or after the window's first tile, every world-th tile, rows below
+        # the window's end) -- a region (row0, row1, period = world) of rsd_halo_compact
+        if self.sd_split == "tiles":
+            def tiles_of(k, win):
+                lo, hi = win
+                t = lo // 8
+                t += (k - t) % world
+                return (8 * t, hi) if 8 * t < hi else None
+            self.iv_send = {k: tiles_of(k, self.window[me]) for k in range(world) if k != me}
+            self.iv_recv = {k: tiles_of(me, self.window[k]) for k in range(world) if k != me}
+        else:
+            self.iv_send = {k: overlap(self.window[me], self.sd_rows[k]) for k in range(world) if k != me}
+            self.iv_recv = {k: overlap(self.window[k], self.sd_rows[me]) for k in range(world) if k != me}
         self.sd_send = dict(self.iv_recv)
         self.sd_recv = dict(self.iv_send)
         # AO bands (frame-buffer rows), padded to the largest for one all-gather.  Pass 1 dispatches
@@ -424,30 +443,64 @@ class HaloFrame:
             dev = b.ray_minmax.device
             sdw = b.ray_minmax.shape[2]
             self._cand = {}
+            period = world if self.sd_split == "tiles" else 1
             for k, rows in self.iv_send.items():
                 if rows:
                     lo, hi = rows
-                    n = (hi - lo) * sdw
-                    # the device path (librsd rsd_halo_compact) needs no index list
-                    idx = None if self.native else torch.arange(lo * sdw, hi * sdw, dtype=torch.int32, device=dev)
-                    self._cand[k] = (lo, hi, idx, torch.empty((3, n + 1), dtype=torch.int32, device=dev))
+                    rl = self._region_rows(lo, hi, period)
+                    n = (((hi - lo + 7) // 8 + period - 1) // period) * 8 * sdw if period > 1 else (hi - lo) * sdw
+                    # the device path (librsd rsd_halo_compact) needs no index list; the torch path gathers
+                    # the region's rows and their texel indices
+                    idx = rsel = None
+                    if not self.native:
+                        rsel = torch.tensor(rl, dtype=torch.int64, device=dev)
+                        idx = (rsel[:, None] * sdw + torch.arange(sdw, device=dev)).reshape(-1).to(torch.int32)
+                    self._cand[k] = (lo, hi, idx, torch.empty((3, n + 1), dtype=torch.int32, device=dev), rsel)
             self._row = torch.zeros(world + 1, dtype=torch.int64, device=dev)
             self._M_dev = torch.zeros((world, world + 1), dtype=torch.int64, device=dev)
             self._M_host = torch.zeros((world, world + 1), dtype=torch.int64,
                                        pin_memory=self.cuda and torch.cuda.is_available())
             if self.native:
                 from . import abi
-                regs = [abi.HaloRegion(lo, hi, buf.data_ptr(), buf.shape[1], 0, self._row.data_ptr() + 8 * k)
-                        for k, (lo, hi, _, buf) in self._cand.items()]
+                regs = [abi.HaloRegion(lo, hi, buf.data_ptr(), buf.shape[1], period, self._row.data_ptr() + 8 * k)
+                        for k, (lo, hi, _, buf, _) in self._cand.items()]
                 self._regions = (abi.HaloRegion * max(1, len(regs)))(*regs)
                 self._n_regions = len(regs)
+
+    @staticmethod
+    def _region_rows(lo, hi, period):
+        """The SD rows of a compaction region: [lo, hi), or every period-th 8-row tile from lo."""
+        if period <= 1:
+            return list(range(lo, hi))
+        return [y for t0 in range(lo, hi, 8 * period) for y in range(t0, min(t0 + 8, hi))]
+
+    def owned_sd_rows(self, rank=None):
+        """The SD row ranges `rank` traces (default: this rank): its contiguous rows, or its tiles."""
+        rank = self.rank if rank is None else rank
+        if self.sd_split != "tiles":
+            return [self.sd_rows[rank]]
+        sdh = self.b.sd_h
+        return [(y, min(y + 8, sdh)) for y in range(8 * rank, sdh, 8 * self.world)]
+
+    def trace(self, consume=False, counters=False):
+        """The SD trace of this rank's texels (rsd_sd_trace_band_ex over its tiles, or rsd_sd_trace_rows)."""
+        b, kw = self.b, dict(self.trace_kw)
+        if consume:
+            kw["consume"] = True
+        if counters:
+            kw["counters"] = True
+        if self.sd_band is not None:
+            return b.sd_trace(band=self.sd_band, **kw)
+        return b.sd_trace_rows(self.sd_rows[self.rank], **kw)
 
     def dense_bytes_per_frame(self):
         """What the round-2 dense halo (whole candidate rows) would send per frame from this rank."""
         b = self.b
-        iv = sum(2 * 4 * (hi - lo) * b.sd.shape[2] for r in self.iv_send.values() if r for lo, hi in [r])
+        period = self.world if self.sd_split == "tiles" else 1
+        nrows = lambda r: len(self._region_rows(r[0], r[1], period)) if r else 0  # noqa: E731
+        iv = sum(2 * 4 * nrows(r) * b.sd.shape[2] for r in self.iv_send.values())
         sd_row = b.sd[:, 0].numel() * b.sd.element_size()
-        sd = sum((hi - lo) * sd_row for r in self.sd_send.values() if r for lo, hi in [r])
+        sd = sum(nrows(r) * sd_row for r in self.sd_send.values())
         return {"intervals": iv, "sd": sd, "ao": self.ao_send.numel() * self.ao_send.element_size()}
 
     def bytes_per_frame(self):
@@ -552,8 +605,8 @@ class HaloFrame:
                                                      self._regions, self._n_regions, b.stream), "rsd_halo_compact")
             else:
                 row.zero_()
-                for k, (lo, hi, idx, buf) in self._cand.items():
-                    reg = b.ray_minmax[:, lo:hi].reshape(2, -1)
+                for k, (lo, hi, idx, buf, rsel) in self._cand.items():
+                    reg = b.ray_minmax.index_select(1, rsel).reshape(2, -1)
                     touched = (reg[0] != FLT_MAX_BITS) | (reg[1] != 0)
                     pos = torch.cumsum(touched, 0)  # int64: 1-based position of each touched texel
                     dst = torch.where(touched, pos - 1, torch.full_like(pos, buf.shape[1] - 1))
@@ -615,10 +668,7 @@ class HaloFrame:
         if sd_events:
             sd_events[0].record()
         t.append(self._mark())
-        if st["consume"]:
-            b.sd_trace_rows(self.sd_rows[me], consume=True, **self.trace_kw)
-        else:
-            b.sd_trace_rows(self.sd_rows[me], **self.trace_kw)
+        self.trace(consume=st["consume"])
         self._intervals_clear = st["consume"]
         t.append(self._mark())
         if sd_events:

@@ -61,6 +61,12 @@ def test_row_ranges_union_equals_full_frame():
     g = r.numpy()
     assert bits_equal(g["sd"], ref["sd"])
     assert np.array_equal(g["ao"], ref["ao"])
+    # the tiled split (HaloFrame's default): every rank's round-robin 8-row tiles, traced as bands
+    r.sd.zero_()
+    for p in plans:
+        assert p.sd_split == "tiles"
+        p.trace()
+    assert bits_equal(r.numpy()["sd"], ref["sd"])
     # consume: a band trace resets the WHOLE interval map
     r.sd_trace_rows(plans[2].sd_rows[2], consume=True)
     g = r.numpy()
@@ -100,7 +106,7 @@ def _worker(rank, world, port, out_dir):
         torch.cuda.synchronize()
         np.save(os.path.join(out_dir, f"ao_{rank}_{i}.npy"), r.ao.cpu().numpy())
     g = r.numpy()
-    np.save(os.path.join(out_dir, f"sdrows_{rank}.npy"), np.array(f.sd_rows))
+    np.save(os.path.join(out_dir, f"sdrows_{rank}.npy"), np.array(f.owned_sd_rows()))
     np.save(os.path.join(out_dir, f"ao_{rank}.npy"), g["ao"])
     np.save(os.path.join(out_dir, f"sd_{rank}.npy"), g["sd"])
     np.save(os.path.join(out_dir, f"bytes_{rank}.npy"), np.array(list(f.bytes_per_frame().values())))
@@ -129,8 +135,9 @@ def test_halo_frame_three_ranks_equals_one_gpu(tmp_path):
         assert np.array_equal(np.load(tmp_path / f"ao_{k}.npy"), ref["ao"]), f"rank {k} AO"
         for i in range(4):
             assert np.array_equal(np.load(tmp_path / f"ao_{k}_{i}.npy"), ref["ao"]), f"rank {k} AO frame {i}"
-        lo, hi = np.load(tmp_path / f"sdrows_{k}.npy")[k]
-        assert bits_equal(np.load(tmp_path / f"sd_{k}.npy")[:, lo:hi], ref["sd"][:, lo:hi]), f"rank {k} SD rows"
+        sd = np.load(tmp_path / f"sd_{k}.npy")
+        for lo, hi in np.load(tmp_path / f"sdrows_{k}.npy"):  # the SD rows (tiles) rank k traced
+            assert bits_equal(sd[:, lo:hi], ref["sd"][:, lo:hi]), f"rank {k} SD rows {lo}-{hi}"
         iv, sd, _ = np.load(tmp_path / f"bytes_{k}.npy")
         assert iv + sd < full  # less than the whole interval + SD maps
 
@@ -212,9 +219,9 @@ def test_halo_frame_sync_free_threads(world):
         for j in range(4):
             assert np.array_equal(out[(k, j)].cpu().numpy(), ref["ao"]), f"rank {k} frame {j}"
         f = ranks[k][1][2]
-        lo, hi = f.sd_rows[k]
         g = ranks[k][1][0].numpy()
-        assert bits_equal(g["sd"][:, lo:hi], ref["sd"][:, lo:hi]), f"rank {k} SD rows"
+        for lo, hi in f.owned_sd_rows():
+            assert bits_equal(g["sd"][:, lo:hi], ref["sd"][:, lo:hi]), f"rank {k} SD rows {lo}-{hi}"
         assert f.frames == 2 and sum(f.bytes_per_frame().values()) > 0
     for slots in ranks:
         for rr, _, _ in slots:

@@ -76,7 +76,7 @@ def _cfg():
     return small_frame_config(visible=(192, 104), guard=16, divisor=2, N=4)
 
 
-def _worker(rank, world, port, out_dir, mode="band"):
+def _worker(rank, world, port, out_dir, mode="band", sd_split="tiles"):
     import sys
     from pathlib import Path
     root = Path(__file__).resolve().parents[1]
@@ -96,7 +96,7 @@ def _worker(rank, world, port, out_dir, mode="band"):
         dist.destroy_process_group()
         return
     be = OracleBackend(O, make_scene("arcade_tiny"), cfg, None if mode == "band" else HALO_REACH)
-    f = (BandFrame if mode == "band" else HaloFrame)(be, rank, world)
+    f = BandFrame(be, rank, world) if mode == "band" else HaloFrame(be, rank, world, sd_split=sd_split)
     f.frame()
     if mode == "halo":
         # more frames: intervals cleared again, buffers reused, and the split re-balanced from the
@@ -109,7 +109,7 @@ def _worker(rank, world, port, out_dir, mode="band"):
             f.frame()
             np.save(os.path.join(out_dir, f"ao_{rank}_{f.frames}.npy"), be.np_ao)
         np.save(os.path.join(out_dir, f"split_{rank}.npy"), np.array(f.splits))
-        np.save(os.path.join(out_dir, f"sdrows_{rank}.npy"), np.array(f.sd_rows))
+        np.save(os.path.join(out_dir, f"sdrows_{rank}.npy"), np.array(f.owned_sd_rows()))
         np.save(os.path.join(out_dir, f"bytes_{rank}.npy"), np.array([f.sent["intervals"], f.sent["sd"],
                                                                      f.frames]))
     np.save(os.path.join(out_dir, f"ao_{rank}.npy"), be.np_ao)
@@ -175,26 +175,26 @@ def _halo_cfg():
     return small_frame_config(visible=(96, 448), guard=16, divisor=2, N=2)
 
 
-@pytest.mark.parametrize("world", [2, 3, 4])
-def test_halo_sharded_frame_equals_single_process(oracle, tmp_path, world):
+@pytest.mark.parametrize("world,sd_split", [(2, "tiles"), (3, "tiles"), (4, "tiles"), (3, "rows")])
+def test_halo_sharded_frame_equals_single_process(oracle, tmp_path, world, sd_split):
     """HaloFrame (contiguous bands, sparse interval + SD halo exchange over point-to-point sends,
-    load-balanced re-splits): every rank ends every frame with the single-process AO image; its
-    own SD rows equal the reference; the split moved; the sparse halo moved less than the dense
-    candidate rows would have."""
+    load-balanced re-splits; the SD trace split into round-robin 8-row tiles, or the rows under each
+    band): every rank ends every frame with the single-process AO image; the SD rows it traced equal
+    the reference; the split moved; the sparse halo moved less than the dense candidate rows would have."""
     from rsd.scenes import make_scene
     from rsd.shard import BandFrame
     ref = OracleBackend(oracle, make_scene("arcade_tiny"), _halo_cfg(), HALO_REACH)
     BandFrame(ref, 0, 1).frame()
     assert (ref.np_st != 0).any()
-    mp.start_processes(_worker, args=(world, _free_port(), str(tmp_path), "halo"), nprocs=world, join=True,
+    mp.start_processes(_worker, args=(world, _free_port(), str(tmp_path), "halo", sd_split), nprocs=world, join=True,
                        start_method="spawn")
     for r in range(world):
         assert np.array_equal(np.load(tmp_path / f"ao_{r}.npy"), ref.np_ao), f"rank {r} AO"
         for fr in (2, 3, 4):
             assert np.array_equal(np.load(tmp_path / f"ao_{r}_{fr}.npy"), ref.np_ao), f"rank {r} AO frame {fr}"
         sd = np.load(tmp_path / f"sd_{r}.npy")
-        lo, hi = np.load(tmp_path / f"sdrows_{r}.npy")[r]
-        assert np.array_equal(sd[:, lo:hi].view(np.uint32), ref.np_sd[:, lo:hi].view(np.uint32)), f"rank {r} SD"
+        for lo, hi in np.load(tmp_path / f"sdrows_{r}.npy"):
+            assert np.array_equal(sd[:, lo:hi].view(np.uint32), ref.np_sd[:, lo:hi].view(np.uint32)), f"rank {r} SD"
     splits = np.load(tmp_path / "split_0.npy")
     assert all(np.array_equal(splits, np.load(tmp_path / f"split_{r}.npy")) for r in range(world))  # same on all
     assert not np.array_equal(splits[1], splits[-1])  # the skewed split was re-balanced
@@ -235,8 +235,18 @@ def test_halo_plan_partitions_and_bounds(oracle):
         assert p0.px_rows[0][0] == 0 and all(p0.px_rows[r][1] == p0.px_rows[r + 1][0] for r in range(world - 1))
         assert p0.sd_rows[0][0] == 0 and p0.sd_rows[-1][1] == plans[0].b.sd_h
         assert all(p0.sd_rows[r][1] == p0.sd_rows[r + 1][0] for r in range(world - 1))
+        # the tiled SD split: the ranks' round-robin tiles partition the map's rows
+        owned = sorted(y for p in plans for lo, hi in p.owned_sd_rows() for y in range(lo, hi))
+        assert owned == list(range(p0.b.sd_h))
         for r, p in enumerate(plans):
             assert p.window[r][0] < p.window[r][1]
+            # what r scans for k: every row of r's window in k's tiles, plus at most the rows of the
+            # window's first tile below it (whole tiles; r's pass 1 never touches those)
+            for k, reg in p.iv_send.items():
+                got = set(p._region_rows(reg[0], reg[1], world)) if reg else set()
+                lo, hi = p.window[r]
+                want = {y for y in range(lo, hi) if (y // 8) % world == k}
+                assert want <= got <= {y for y in range(lo // 8 * 8, hi) if (y // 8) % world == k}, (world, r, k)
             if world >= 3:  # the halo is a real restriction: a window leaves rows of the map out
                 assert any(q.window[k] != (0, q.b.sd_h) for k, q in enumerate(plans))
             # what r sends to k is what k expects from r (same row ranges on both sides)

@@ -36,7 +36,8 @@ for world in worlds:
         r.clear_intervals()
         r.pass1_rows(p.px_rows[k])
         m = (r.ray_minmax[0] != FLT_MAX_BITS) | (r.ray_minmax[1] != 0)
-        touched.append([int(m[lo:hi].sum()) if j != k else 0 for j, (lo, hi) in enumerate(p.sd_rows)])
+        touched.append([sum(int(m[lo:hi].sum()) for lo, hi in p.owned_sd_rows(j)) if j != k else 0
+                        for j in range(world)])
     torch.cuda.synchronize()
     ranks = []
     for k, p in enumerate(plans):

@@ -5,7 +5,8 @@ on ONE GPU (a model the driver's 8-GPU run can be judged against)
 For a config and N in --worlds, on the real frame (fast numerics, the product default):
 
   * per rank k of HaloFrame's first (equal-groups) split: the GPU time of its pass 1
-    (rsd_svao_pass1_rows), its SD trace given the 1-GPU interval union (rsd_sd_trace_rows) and its
+    (rsd_svao_pass1_rows), its SD trace given the 1-GPU interval union (its round-robin SD tiles,
+    rsd_sd_trace_band_ex, or with --sd-split rows the rows under its band, rsd_sd_trace_rows) and its
     pass 2 given the 1-GPU SD map (rsd_svao_pass2_rows), each the median of --reps runs between
     fence-free HIP events, one launch in flight;
   * the bytes it sends per frame (sparse interval triples to the bands it touches, the depths it
@@ -19,7 +20,7 @@ with L_coll = 12 us per small collective / point-to-point round (--coll-us) and 
 per xGMI peer link (--link-gbs); with F frames in flight the GPU part overlaps across frames as at
 N = 1 (factor --overlap = ms_per_step(F = 4) / one-frame GPU time, measured at N = 1 here), and the
 frame rate is bounded by max(overlapped GPU time, host issue time).
-usage: python tools/scaling_model.py [config] [--worlds 2,4,8] [--reps 15] [--pose i]"""
+usage: python tools/scaling_model.py [config] [--worlds 2,4,8] [--reps 15] [--pose i] [--sd-split tiles|rows]"""
 import json
 import statistics
 import sys
@@ -46,6 +47,7 @@ worlds = [int(x) for x in arg("--worlds", "2,4,8").split(",")]
 reps = int(arg("--reps", "15"))
 pose = int(arg("--pose", "0"))
 coll_us, link_gbs = float(arg("--coll-us", "12")), float(arg("--link-gbs", "50"))
+sd_split = arg("--sd-split", "tiles")  # HaloFrame's SD trace split: round-robin tiles (default) or rows
 kw, sc = CONFIGS[name]
 r = Renderer(make_scene(sc), FrameConfig(**kw))
 poses = camera_path(DEFAULT_CAMERA_PATH.get(name, "static"))
@@ -99,21 +101,22 @@ class NoComm:
         pass
 
 
-out = {"config": name, "pose": pose, "reps": reps, "one_gpu": {k: round(v, 2) for k, v in one.items()},
+out = {"config": name, "sd_split": sd_split, "pose": pose, "reps": reps, "one_gpu": {k: round(v, 2) for k, v in one.items()},
        "assumptions": {"coll_us": coll_us, "link_gbs": link_gbs, "collectives_per_frame": 4}, "worlds": {}}
 for world in worlds:
-    plans = [HaloFrame(r, k, world, rebalance=False) for k in range(world)]
+    plans = [HaloFrame(r, k, world, rebalance=False, sd_split=sd_split) for k in range(world)]
     ranks = []
     touched = []
     for k, p in enumerate(plans):
         r.clear_intervals()
         r.pass1_rows(p.px_rows[k])
         m = (r.ray_minmax[0] != FLT_MAX_BITS) | (r.ray_minmax[1] != 0)
-        touched.append([int(m[lo:hi].sum()) if j != k else 0 for j, (lo, hi) in enumerate(p.sd_rows)])
+        touched.append([sum(int(m[lo:hi].sum()) for lo, hi in p.owned_sd_rows(j)) if j != k else 0
+                        for j in range(world)])
     for k, p in enumerate(plans):
         t1 = timed(lambda: r.pass1_rows(p.px_rows[k]), r.clear_intervals)
         r.sd.copy_(sd_full)
-        t2 = timed(lambda: r.sd_trace_rows(p.sd_rows[k]), lambda: r.ray_minmax.copy_(union))
+        t2 = timed(p.trace, lambda: r.ray_minmax.copy_(union))  # its SD tiles (or rows)
         r.sd.copy_(sd_full)
         t3 = timed(lambda: r.pass2_rows(p.px_rows[k]), lambda: (r.clear_intervals(), r.pass1()))
         iv = 12 * sum(touched[k])
@@ -121,11 +124,11 @@ for world in worlds:
         ao = p.ao_max * r.ao[0].numel() * r.ao.element_size()
         ranks.append({"pass1_us": round(t1, 2), "trace_us": round(t2, 2), "pass2_us": round(t3, 2),
                       "gpu_us": round(t1 + t2 + t3, 2), "bytes": iv + sdb + ao,
-                      "px_rows": p.px_rows[k], "sd_rows": p.sd_rows[k]})
+                      "px_rows": p.px_rows[k], "sd_split": p.sd_split})
     # host issue of one rank's frame (rank 0 and the middle rank), collectives stubbed
     host = []
     for k in sorted({0, world // 2}):
-        f = HaloFrame(r, k, world, rebalance=False, comm=NoComm())
+        f = HaloFrame(r, k, world, rebalance=False, comm=NoComm(), sd_split=sd_split)
         for _ in range(3):
             f.front()
             f.back()
