@@ -22,6 +22,11 @@
 #endif
 // fast numerics: clamped-radius pixels take the SCALED all-fast loops (sample_init); 0 = the per-lane
 // generic loops as in the exact build (A/B builds: make variant V=noscaled DEFS=-DRSD_SCALED_ALLFAST=0)
+// diagnostic builds only (make variant V=noatom DEFS=-DRSD_DIAG_P1_NOATOM=1; results wrong by design): pass 1
+// without its interval atomics, to price them
+#ifndef RSD_DIAG_P1_NOATOM
+#define RSD_DIAG_P1_NOATOM 0
+#endif
 #ifndef RSD_SCALED_ALLFAST
 #define RSD_SCALED_ALLFAST 1
 #endif
@@ -80,8 +85,10 @@ __device__ __forceinline__ void pass1_dir_generic(const SvaoArgs& a, float u, fl
                 // SVAORaster.ps.slang:90-91
                 const float osMin = (!SPEC && a.k.hbao) ? hmin(s.objectSpaceZ, s.sphereStart)
                                                         : hmin(s.objectSpaceZ, b.radius + d.thickness * b.radius + s.sphereStart);
-                atomicMin(&a.rayMin[o], asuint(hmax(b.posVLength - osMin, 0.0f)));
-                atomicMax(&a.rayMax[o], asuint(hmax(b.posVLength - s.sphereEnd, 0.0f)));
+                if (!RSD_DIAG_P1_NOATOM) {
+                    atomicMin(&a.rayMin[o], asuint(hmax(b.posVLength - osMin, 0.0f)));
+                    atomicMax(&a.rayMax[o], asuint(hmax(b.posVLength - s.sphereEnd, 0.0f)));
+                }
             } else {
                 a.rayMax[o] = 1u;
             }

@@ -340,15 +340,20 @@ class HaloFrame:
     `comm`: DistComm (default; torch.distributed) or LocalComm (threads on one GPU)."""
 
     def __init__(self, backend, rank: int = 0, world: int = 1, pg=None, throughput: bool = False,
-                 rebalance: bool = True, comm=None, sd_split: str = "tiles"):
+                 rebalance: bool = True, comm=None, sd_split: str = "auto"):
         b = self.b = backend
         self.rank, self.world, self.pg = rank, world, pg
-        if sd_split not in ("tiles", "rows"):
-            raise ValueError("HaloFrame sd_split must be 'tiles' or 'rows'")
+        if sd_split not in ("tiles", "rows", "auto"):
+            raise ValueError("HaloFrame sd_split must be 'tiles', 'rows' or 'auto'")
         # who traces which SD texel: "tiles" deals the 8-row SD tiles round-robin to the ranks (tile t to
         # rank t % world), so every rank traces a share of the frame's long rays -- the trace is
-        # latency-bound by its slowest rays, which cluster on the screen (DESIGN.md section 6); "rows":
-        # the SD rows under each rank's pass-1 band (HaloFrame v4)
+        # latency-bound by its slowest rays, which cluster on the screen; "rows": the SD rows under each
+        # rank's pass-1 band (HaloFrame v4), which sends only the texels beyond a band's edge.  "auto":
+        # tiles for reduced-resolution SD maps (few touched texels per pixel row: the extra exchange is
+        # small), rows for full-resolution maps, whose touched sets are dense (configs[4]: 14.9 vs 2.9 MB
+        # per rank and frame at N = 8) -- DESIGN.md section 6, profiles/round4/multigpu/
+        if sd_split == "auto":
+            sd_split = "tiles" if backend.cfg.divisor > 1 else "rows"
         self.sd_split = sd_split if world > 1 else "rows"
         self.comm = comm if comm is not None else (DistComm(pg) if world > 1 else None)
         self.nccl = bool(getattr(self.comm, "nccl", False))
@@ -455,11 +460,14 @@ class HaloFrame:
                     if not self.native:
                         rsel = torch.tensor(rl, dtype=torch.int64, device=dev)
                         idx = (rsel[:, None] * sdw + torch.arange(sdw, device=dev)).reshape(-1).to(torch.int32)
-                    self._cand[k] = (lo, hi, idx, torch.empty((3, n + 1), dtype=torch.int32, device=dev), rsel)
-            self._row = torch.zeros(world + 1, dtype=torch.int64, device=dev)
-            self._M_dev = torch.zeros((world, world + 1), dtype=torch.int64, device=dev)
-            self._M_host = torch.zeros((world, world + 1), dtype=torch.int64,
-                                       pin_memory=self.cuda and torch.cuda.is_available())
+                    self._cand[k] = (lo, hi, idx, self._buf("cand", k, (3, n + 1), torch.int32, dev), rsel)
+            if not hasattr(self, "_row"):  # shapes fixed by world: allocated once (a re-plan allocates nothing)
+                self._row = torch.zeros(world + 1, dtype=torch.int64, device=dev)
+                self._M_dev = torch.zeros((world, world + 1), dtype=torch.int64, device=dev)
+                self._M_host = torch.zeros((world, world + 1), dtype=torch.int64,
+                                           pin_memory=self.cuda and torch.cuda.is_available())
+            else:
+                self._row.zero_()  # the peers of the new plan write their counts; the others stay 0
             if self.native:
                 from . import abi
                 regs = [abi.HaloRegion(lo, hi, buf.data_ptr(), buf.shape[1], period, self._row.data_ptr() + 8 * k)
@@ -566,6 +574,11 @@ class HaloFrame:
         if G >= world:  # monotone, one group per rank at least
             for k in range(1, world):
                 new[k] = min(max(new[k], new[k - 1] + 1), G - (world - k))
+        # hysteresis: keep the split unless the cost model predicts the slowest band at least 3 % faster (a
+        # re-split re-plans the exchange regions: host work every frame for a split that only oscillates)
+        pred = max(cum[new[k + 1]] - cum[new[k]] for k in range(world))
+        if pred > 0.97 * max(cum[gb[k + 1]] - cum[gb[k]] for k in range(world)):
+            return list(gb)
         return new
 
     def frame(self, sd_events=None):

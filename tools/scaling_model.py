@@ -20,7 +20,7 @@ with L_coll = 12 us per small collective / point-to-point round (--coll-us) and 
 per xGMI peer link (--link-gbs); with F frames in flight the GPU part overlaps across frames as at
 N = 1 (factor --overlap = ms_per_step(F = 4) / one-frame GPU time, measured at N = 1 here), and the
 frame rate is bounded by max(overlapped GPU time, host issue time).
-usage: python tools/scaling_model.py [config] [--worlds 2,4,8] [--reps 15] [--pose i] [--sd-split tiles|rows]"""
+usage: python tools/scaling_model.py [config] [--worlds 2,4,8] [--reps 15] [--pose i] [--sd-split auto|tiles|rows]"""
 import json
 import statistics
 import sys
@@ -47,7 +47,7 @@ worlds = [int(x) for x in arg("--worlds", "2,4,8").split(",")]
 reps = int(arg("--reps", "15"))
 pose = int(arg("--pose", "0"))
 coll_us, link_gbs = float(arg("--coll-us", "12")), float(arg("--link-gbs", "50"))
-sd_split = arg("--sd-split", "tiles")  # HaloFrame's SD trace split: round-robin tiles (default) or rows
+sd_split = arg("--sd-split", "auto")  # HaloFrame's SD trace split: auto (its default), tiles or rows
 kw, sc = CONFIGS[name]
 r = Renderer(make_scene(sc), FrameConfig(**kw))
 poses = camera_path(DEFAULT_CAMERA_PATH.get(name, "static"))
@@ -101,7 +101,8 @@ class NoComm:
         pass
 
 
-out = {"config": name, "sd_split": sd_split, "pose": pose, "reps": reps, "one_gpu": {k: round(v, 2) for k, v in one.items()},
+out = {"config": name, "sd_split": HaloFrame(r, 0, 2, rebalance=False, sd_split=sd_split).sd_split, "pose": pose,
+       "reps": reps, "one_gpu": {k: round(v, 2) for k, v in one.items()},
        "assumptions": {"coll_us": coll_us, "link_gbs": link_gbs, "collectives_per_frame": 4}, "worlds": {}}
 for world in worlds:
     plans = [HaloFrame(r, k, world, rebalance=False, sd_split=sd_split) for k in range(world)]
