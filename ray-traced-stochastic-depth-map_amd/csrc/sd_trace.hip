@@ -1250,6 +1250,7 @@ __global__ void __launch_bounds__(kBlock) sd_trace_row_kernel(SDArgs a, const fl
 
     unsigned long long tFetch = 0, tStep = 0, tResolve = 0, nStep = 0, nLoop = 0, tS0 = 0, tS1 = 0;
     unsigned long long tMem = 0, tComp = 0, tPool = 0, tMark = 0;  // step split (instrumented build)
+    unsigned long long tBox = 0, tTri = 0, tB = 0, tT = 0;  // compute split: box tests + sort, triangle tests
     // clock calibration (instrumented build): the first wave's span in s_memtime ticks and in the
     // 100 MHz s_memrealtime ticks converts the step clocks to microseconds (rsd_counters.shader_clock_mhz)
     unsigned long long cal0 = 0, calR0 = 0;
@@ -1365,6 +1366,7 @@ __global__ void __launch_bounds__(kBlock) sd_trace_row_kernel(SDArgs a, const fl
             cswap(ck[1], ci[1], ck[3], ci[3]);
             cswap(ck[1], ci[1], ck[2], ci[2]);
         }
+        if constexpr (CNT) { tB = __builtin_amdgcn_s_memtime(); tT = tB; }
         // ---- leaves: every triangle test of the step first (independent dependency chains), then
         //      the row merges the accepted hits into its k-list, one insert each (the merge
         //      re-checks each hit against the current K-th key)
@@ -1392,6 +1394,7 @@ __global__ void __launch_bounds__(kBlock) sd_trace_row_kernel(SDArgs a, const fl
                     }
                 }
             }
+            if constexpr (CNT) tT = __builtin_amdgcn_s_memtime();
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 for (uint32_t m = row_bits<ROW>(aj[j], base); m; m &= m - 1u) {
@@ -1426,7 +1429,11 @@ __global__ void __launch_bounds__(kBlock) sd_trace_row_kernel(SDArgs a, const fl
         }
         if constexpr (CNT) {
             const unsigned long long t = __builtin_amdgcn_s_memtime();
-            if (l == 0) tComp += t - tMark;
+            if (l == 0) {
+                tComp += t - tMark;
+                tBox += tB - tMark;
+                tTri += tT - tB;
+            }
             tMark = t;
         }
 #pragma unroll
@@ -1557,6 +1564,8 @@ __global__ void __launch_bounds__(kBlock) sd_trace_row_kernel(SDArgs a, const fl
         atomicAdd(&a.counters[16], tMem);
         atomicAdd(&a.counters[17], tComp);
         atomicAdd(&a.counters[18], tPool);
+        atomicAdd(&a.counters[23], tBox);
+        atomicAdd(&a.counters[24], tTri);
         if (blockIdx.x == 0 && lane == 0) {
             const unsigned long long cal1 = __builtin_amdgcn_s_memtime(), calR1 = __builtin_amdgcn_s_memrealtime();
             atomicMax(&a.counters[21], cal1 - cal0);
@@ -1779,7 +1788,7 @@ rsd_status sd_workspace(rsd_scene* scene, hipStream_t s, SdWorkspace** out) {
     SdWorkspace* w = new SdWorkspace();
     w->stream = s;
     hipError_t e = hipMalloc(&w->qctl, 2 * kQctlWords * sizeof(uint32_t));
-    if (e == hipSuccess) e = hipMalloc(&w->counters, 24 * sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipMalloc(&w->counters, 32 * sizeof(unsigned long long));
     if (e != hipSuccess) {
         (void)hipFree(w->qctl);
         delete w;
@@ -2006,7 +2015,7 @@ rsd_status sd_trace_impl(rsd_scene* scene, const rsd_camera* cam, const rsd_sd_p
     }
     if (counters) {
         // per (scene, stream): concurrent instrumented traces on other streams keep their own
-        RSD_HIP(hipMemsetAsync(ws->counters, 0, 24 * sizeof(unsigned long long), s));
+        RSD_HIP(hipMemsetAsync(ws->counters, 0, 32 * sizeof(unsigned long long), s));
         a.counters = ws->counters;
     }
     const char* rayLogPath = counters ? std::getenv("RSD_TRACE_RAYLOG") : nullptr;  // diagnostics only
@@ -2152,7 +2161,7 @@ rsd_status sd_trace_impl(rsd_scene* scene, const rsd_camera* cam, const rsd_sd_p
     }
     if (grid.y != 0) ws->qctl_gen++;
     if (counters) {
-        unsigned long long h[24];
+        unsigned long long h[32];
         RSD_HIP(hipMemcpyAsync(h, ws->counters, sizeof(h), hipMemcpyDeviceToHost, s));
         RSD_HIP(hipStreamSynchronize(s));
         counters->rays_dispatched = h[0];
@@ -2176,8 +2185,10 @@ rsd_status sd_trace_impl(rsd_scene* scene, const rsd_camera* cam, const rsd_sd_p
         counters->shader_clock_mhz = h[22] ? (double)h[21] / ((double)h[22] * 0.01) : 0.0;  // 100 MHz realtime
         if (const char* dbg = std::getenv("RSD_TRACE_PHASES"))
             if (*dbg) std::fprintf(stderr, "[rsd] row walk phase clocks: fetch %llu step %llu resolve %llu steps %llu loops %llu"
-                                   " | step split: mem %llu compute %llu pool %llu\n",
-                                   h[11], h[12], h[13], h[14], h[15], h[16], h[17], h[18]);
+                                   " | step split: mem %llu compute %llu pool %llu | compute split: box+sort %llu"
+                                   " tri-tests %llu merge+push %llu\n",
+                                   h[11], h[12], h[13], h[14], h[15], h[16], h[17], h[18], h[23], h[24],
+                                   h[17] - h[23] - h[24]);
         if (a.rayLog) {
             std::vector<uint32_t> lg(rayLogBytes / 4);
             RSD_HIP(hipMemcpy(lg.data(), a.rayLog, rayLogBytes, hipMemcpyDeviceToHost));

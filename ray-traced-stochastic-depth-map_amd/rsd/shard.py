@@ -531,12 +531,18 @@ class HaloFrame:
 
     # ---- timing of this rank's compute (load balance)
     def _mark(self):
-        """A timestamp for the re-balancing cost (None when nothing re-balances: world 1)."""
+        """A timestamp for the re-balancing cost (None when nothing re-balances: world 1).  Device: the next
+        event of this frame's set of six fence-free timing events (rsd/timing.py); two sets alternate, so the
+        previous frame's events stay readable while this frame records (no event is created per frame)."""
         if not self.rebalance:
             return None
-        if self.cuda:  # fence-free timing event (rsd/timing.py): no stream bubble per mark
-            from .timing import TimingEvent
-            e = TimingEvent()
+        if self.cuda:
+            if not hasattr(self, "_evsets"):
+                from .timing import TimingEvent
+                self._evsets = [[TimingEvent() for _ in range(6)] for _ in range(2)]
+                self._evn = 0
+            e = self._evsets[(self._evn // 6) % 2][self._evn % 6]
+            self._evn += 1
             e.record()
             return e
         return time.perf_counter()
@@ -629,9 +635,11 @@ class HaloFrame:
             self.comm.all_gather(self._M_dev, row)
             self._M_host.copy_(self._M_dev, non_blocking=True)
             if self.cuda:
-                ev = torch.cuda.Event()
-                ev.record()
-                st["ev"] = ev
+                if not hasattr(self, "_cnt_ev"):  # one event per object: front() / back() strictly alternate
+                    from .timing import TimingEvent
+                    self._cnt_ev = TimingEvent()
+                self._cnt_ev.record()
+                st["ev"] = self._cnt_ev
         self._open = st
 
     def back(self, sd_events=None):
@@ -647,7 +655,8 @@ class HaloFrame:
                     self.blocked_waits += 1
                 st["ev"].synchronize()  # the counts of THIS frame on the host (lagged: already there)
             M = self._M_host.numpy().copy()
-            if self.rebalance and int(M[:, world].min()) >= 0:
+            # re-split on every second frame (each rank sees the same counts, so all skip or all re-split)
+            if self.rebalance and self.frames % 2 == 0 and int(M[:, world].min()) >= 0:
                 self._next_gb = self._rebalanced([float(x) for x in M[:, world]])
             dev = b.ray_minmax.device
             iv_send = {k: self._cand[k][3][:, :int(M[me, k])] for k in self._cand if M[me, k] > 0}

@@ -51,9 +51,17 @@ class TimingEvent:
 
     def record(self, stream=None):
         import torch
-        s = (stream or torch.cuda.current_stream()).cuda_stream
+        if stream is not None:
+            s = stream.cuda_stream
+        else:  # torch's raw accessor: no Python Stream object per record (3 us each through current_stream())
+            s = torch._C._cuda_getCurrentRawStream(torch._C._cuda_getDevice())
         if self._L.hipEventRecord(self.h, C.c_void_p(s)) != 0:
             raise RuntimeError("hipEventRecord failed")
+
+    def synchronize(self):
+        """Block the host until the event has completed (hipEventSynchronize)."""
+        if self._L.hipEventSynchronize(self.h) != 0:
+            raise RuntimeError("hipEventSynchronize failed")
 
     def query(self) -> bool:
         """True when the event has completed (hipEventQuery; never blocks)."""
