@@ -55,6 +55,7 @@ struct SvaoArgs {
     uint32_t dual;  // DUAL_AO: ao holds (bright, dark) byte pairs (RG8Unorm)
     uint32_t bandIndex, bandCount;  // 32-row groups g (offset space) with g % count == index
     float isx, isy;  // imageScale (Common.slang:142), hoisted: 0.5 * (frameW / focal), same bits
+    float risx, risy;  // 1 / isx, 1 / isy (fast numerics: view-to-uv through one reciprocal of p.z)
     float pzLo, pzHi;  // |p.z| in [pzLo, pzHi] keeps isx p.z and isy p.z in [2^-20, 2^20] (fill_scale)
     const float* snapU;  // getSnappedUV: snapU[k] = (k + 0.5f) / resolution.x for k in [0, resolution.x]
     const float* snapV;  //               snapV[k] = (k + 0.5f) / resolution.y
@@ -312,8 +313,15 @@ __device__ __forceinline__ bool basic_init(const SvaoArgs& a, float u, float v, 
 __device__ __forceinline__ bool basic_from(const SvaoArgs& a, float u, float v, float z, float4 nl, Basic& b,
                                            const float* noise) {
     const rsd_vao_data& d = a.d;
-    const float rux = (d.radius * a.cam.focalLength) / (a.cam.frameWidth * z);
-    const float ruy = (d.radius * a.cam.focalLength) / (a.cam.frameHeight * z);
+    float rux, ruy;
+    if constexpr (kFastNumerics) {  // one hardware reciprocal of the pixel's depth for both radii
+        const float rz = __builtin_amdgcn_rcpf(z);
+        rux = (d.radius * a.cam.focalLength) * __builtin_amdgcn_rcpf(a.cam.frameWidth) * rz;
+        ruy = (d.radius * a.cam.focalLength) * __builtin_amdgcn_rcpf(a.cam.frameHeight) * rz;
+    } else {
+        rux = (d.radius * a.cam.focalLength) / (a.cam.frameWidth * z);
+        ruy = (d.radius * a.cam.focalLength) / (a.cam.frameHeight * z);
+    }
     const float pa = rux * d.resolution[0], pb = ruy * d.resolution[1];
     b.radiusInPixels = pa + 0.5f * (pb - pa);
     b.radius = d.radius;
@@ -331,7 +339,12 @@ __device__ __forceinline__ bool basic_from(const SvaoArgs& a, float u, float v, 
     const int ni = ((int)floorf(nu * 4.0f)) & 3, nj = ((int)floorf(nv * 4.0f)) & 3;
     const f3 rd = noise ? mk(noise[nj * 4 + ni], noise[16 + nj * 4 + ni], 0.0f)
                         : mk(a.k.sinNoise[nj * 4 + ni], a.k.cosNoise[nj * 4 + ni], 0.0f);
-    b.normal = mk(-b.posV.x / b.posVLength, -b.posV.y / b.posVLength, -b.posV.z / b.posVLength);
+    if constexpr (kFastNumerics) {
+        const float il = __builtin_amdgcn_rcpf(b.posVLength);
+        b.normal = mk(-b.posV.x * il, -b.posV.y * il, -b.posV.z * il);
+    } else {
+        b.normal = mk(-b.posV.x / b.posVLength, -b.posV.y / b.posVLength, -b.posV.z / b.posVLength);
+    }
     b.bitangent = normalize(cross(b.normal, rd));
     b.tangent = cross(b.bitangent, b.normal);
     b.normalO = mk(dot(b.normalV, b.tangent), dot(b.normalV, b.bitangent), dot(b.normalV, b.normal));
@@ -443,7 +456,11 @@ __device__ __forceinline__ bool sample_init(const SvaoArgs& a, float u, float v,
     // divisors in [2^-20, 2^20].  Exact for |p.x|, |p.y| in [2^-100, 2^70] (|posV| < 2^60 per pixel, the
     // sample offset < radius); a smaller numerator gives |x / den| < 2^-80, and then u = x / den * -0.5 +
     // 0.5 rounds to 0.5 whichever tiny quotient the sequence returns, and su is all that is used of it.
-    if (ALLFAST && (kFastNumerics || __ballot(!(fabsf(ip.z) >= a.pzLo && fabsf(ip.z) <= a.pzHi)) == 0u)) {
+    if (ALLFAST && kFastNumerics) {  // x / (isx z) = x (1 / isx) (1 / z): one hardware reciprocal for both
+        const float rz = __builtin_amdgcn_rcpf(ip.z);
+        s.su = (ip.x * a.risx * rz) * -0.5f + 0.5f;
+        s.sv = (ip.y * a.risy * rz) * 0.5f + 0.5f;
+    } else if (ALLFAST && __ballot(!(fabsf(ip.z) >= a.pzLo && fabsf(ip.z) <= a.pzHi)) == 0u) {
         const float dx2 = a.isx * ip.z, dy2 = a.isy * ip.z;
         const float ndcx = div_unscaled_tail(ip.x, dx2, rcp_refined(dx2));
         const float ndcy = div_unscaled_tail(ip.y, dy2, rcp_refined(dy2));
@@ -560,6 +577,8 @@ inline void fill_scale(SvaoArgs& a) {
     // Common.slang:142/150 imageScale, evaluated once on the host (IEEE float, same bits)
     a.isx = 0.5f * (a.cam.frameWidth / a.cam.focalLength);
     a.isy = 0.5f * (a.cam.frameHeight / a.cam.focalLength);
+    a.risx = a.isx != 0.0f ? 1.0f / a.isx : 0.0f;
+    a.risy = a.isy != 0.0f ? 1.0f / a.isy : 0.0f;
     // with a factor-2 margin for the rounding of isx * p.z (0 when the scales are not finite and positive)
     const double lo = std::min(a.isx, a.isy), hi = std::max(a.isx, a.isy);
     const bool ok = lo > 0.0 && hi < 1e30;

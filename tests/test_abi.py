@@ -116,3 +116,23 @@ def test_sd_map_sizes_of_the_baseline_configs(abi):
         cfg = FrameConfig(visible_w=vis[0], visible_h=vis[1], divisor=div)
         _, w, h = make_vao(cfg)
         assert (w, h) == want
+
+
+def test_halo_arguments_are_validated_before_any_gpu_work(abi):
+    """The rsd_halo_* entries check their arguments on the host (no HIP call on a bad request)."""
+    L, dummy = abi.lib(), C.c_void_p(16)
+    one = abi.HaloRegion(0, 8, 16, 10, 1, 16)  # 8 rows x 4 columns = 32 texels > stride 10
+    arr = (abi.HaloRegion * 1)(one)
+    assert L.rsd_halo_compact(dummy, dummy, 4, 8, arr, 1, None) == abi.ERR_INVALID_ARG  # stride below the texels
+    tiled = (abi.HaloRegion * 1)(abi.HaloRegion(3, 8, 16, 1000, 2, 16))
+    assert L.rsd_halo_compact(dummy, dummy, 4, 8, tiled, 1, None) == abi.ERR_INVALID_ARG  # tiles off the 8-row grid
+    past = (abi.HaloRegion * 1)(abi.HaloRegion(0, 9, 16, 1000, 1, 16))
+    assert L.rsd_halo_compact(dummy, dummy, 4, 8, past, 1, None) == abi.ERR_INVALID_ARG  # rows past the map
+    many = (abi.HaloRegion * 65)(*[abi.HaloRegion(0, 1, 16, 1000, 1, 16) for _ in range(65)])
+    assert L.rsd_halo_compact(dummy, dummy, 4, 8, many, 65, None) == abi.ERR_INVALID_ARG  # > 64 regions
+    lists = (abi.HaloList * 1)(abi.HaloList(16, 10, 5))
+    assert L.rsd_halo_merge(dummy, dummy, 4, 8, lists, 1, 1, None) == abi.ERR_INVALID_ARG  # stride below n
+    sdl = (abi.HaloSdList * 1)(abi.HaloSdList(None, 16, 3, 0))
+    assert L.rsd_halo_sd_gather(dummy, 1, 4, 8, 4, sdl, 1, None) == abi.ERR_INVALID_ARG  # null index list
+    assert L.rsd_halo_sd_scatter(dummy, 1, 4, 8, 5, sdl, 0, None) == abi.ERR_INVALID_ARG  # 5 channels
+    assert L.rsd_halo_merge(dummy, dummy, 4, 8, None, 0, 1, None) == abi.RSD_OK  # nothing to merge
