@@ -190,8 +190,9 @@ typedef struct {
  *         (SVAO.cpp:617-620); callers pass the radius they want.  Raytraced secondary mode: VAO only. */
 typedef enum { RSD_AO_KERNEL_VAO = 0, RSD_AO_KERNEL_HBAO = 1 } rsd_ao_kernel;
 /* Arithmetic of the SVAO passes ("AO 1", "AO 2"; the SD trace is always exact).
- *   FAST   FMA contraction, v_rcp_f32-based division, hardware sqrt / rsq, float32 denormals flushed:
- *          what D3D allows the reference's HLSL (mad may fuse, '/' within 2.5 ulp, denormals flushed).
+ *   FAST   FMA contraction, v_rcp_f32-based division, hardware sqrt / rsq, float32 denormals flushed, no
+ *          NaN operands assumed: what D3D allows the reference's HLSL (mad may fuse, '/' within 2.5 ulp,
+ *          denormals flushed, min / max without signalling-NaN quieting).
  *          Graded against the CPU oracle by BASELINE.md section 4's AO tolerance (MAE <= 1/255 over the
  *          visible pixels, |diff| <= 2/255 on >= 99.5 %).  The default (zero-initialised params).
  *   EXACT  binary32 round-to-nearest operation by operation, correctly rounded '/' and sqrt: bit-identical
