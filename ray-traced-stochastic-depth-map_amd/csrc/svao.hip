@@ -49,7 +49,7 @@ namespace rsd {
 namespace fast {  // svao_fast.hip: the same kernels with fast numerics (RSD_NUMERICS_FAST)
 void launch_pass1(const SvaoArgs& a, int variant, dim3 grid, dim3 block, hipStream_t s);
 void launch_pass2(const SvaoArgs& a, uint32_t N, uint32_t nd, bool spec, dim3 grid, dim3 block, hipStream_t s,
-                  bool list);
+                  bool list, bool loop);
 }  // namespace fast
 }  // namespace rsd
 
@@ -403,9 +403,13 @@ rsd_status pass2_impl(const rsd_camera* cam, const rsd_vao_data* vao, const rsd_
     const bool list = a.tileFlags && start == 0u && step == 1u && bandGroups == groups &&
                       !(listEnv && std::strcmp(listEnv, "off") == 0);
     if (list) grid = dim3(T);
+    // the specialised list strides over its tiles in the resident grid (RSD_PASS2_LOOP=off: one workgroup
+    // per tile of the frame, A/B runs)
+    const char* loopEnv = std::getenv("RSD_PASS2_LOOP");  // read per call: a test compares both
+    const bool loop = list && spec && !(loopEnv && std::strcmp(loopEnv, "off") == 0);
     a.tileGen = tile_gen_pass2(a.tileFlags);
-    if (p->numerics == RSD_NUMERICS_EXACT) exact::launch_pass2(a, N, nd, spec, grid, block, s, list);
-    else fast::launch_pass2(a, N, nd, spec, grid, block, s, list);
+    if (p->numerics == RSD_NUMERICS_EXACT) exact::launch_pass2(a, N, nd, spec, grid, block, s, list, loop);
+    else fast::launch_pass2(a, N, nd, spec, grid, block, s, list, loop);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? RSD_OK : hip_fail(e, "svao_pass2_kernel launch");
 }

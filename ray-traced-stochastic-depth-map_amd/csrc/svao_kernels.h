@@ -320,9 +320,8 @@ struct P2Shared {
 // One kP2Tile^2 tile whose top-left pixel is (x0, y0); flag: its busy-tile flag (cleared) or null
 template <int N, int ND, bool SPEC, int NB, int KC>
 __device__ __forceinline__ void pass2_tile(const SvaoArgs& a, uint32_t x0, uint32_t y0, uint32_t* flag,
-                                           P2Shared<ND, NB, KC>& sh) {
+                                           P2Shared<ND, NB, KC>& sh, uint32_t tid = threadIdx.x) {
     constexpr uint32_t T = kP2Tile, L = kP2Lanes;
-    const uint32_t tid = threadIdx.x;
     const rsd_vao_data& d = a.d;
     if (tid == 0) { sh.nPix = 0u; sh.nPair = 0u; }
     if constexpr (KC > 0) {
@@ -479,6 +478,36 @@ __global__ void __launch_bounds__(kP2Lanes) svao_pass2_list_kernel(SvaoArgs a) {
                                             a.tileFlags + t, sh);
 }
 
+// The specialised kernel's busy-tile list in a grid of the resident workgroups (launch_pass2: occupancy x
+// CUs): workgroup i takes list entries i, i + grid, ..., so the empty tail is never dispatched -- with
+// frames in flight its ~6 K empty workgroups held dispatch slots the other frames' passes wait for
+// (configs[1], 200 frames with 4 in flight: 77.5-78.1 -> 74.5-75.2 us per frame; pass 2 alone 23.0-23.2
+// -> 22.7-23.0 us; profiles/round4/pass2_loop/).  Only for frames of at most 8 tiles per resident
+// workgroup (1080p): at 4K (~6 busy tiles per workgroup) the static stride serialises clustered busy
+// tiles and one workgroup per tile is faster (pass 2 62.8 vs 73.6 us at configs[3]).  90 VGPRs (5 waves
+// per SIMD) with the two opaque re-reads below; a 6-wave target spills.
+template <int N, int ND, bool SPEC = false>
+__global__ void __launch_bounds__(kP2Lanes) svao_pass2_loop_kernel(SvaoArgs a) {
+    __shared__ P2Shared<ND, SPEC ? 16 : 20, SPEC ? 6 * ND + 64 : 0> sh;
+    const uint32_t n = __builtin_amdgcn_readfirstlane(a.tileCount[a.tileGen]);
+#pragma nounroll
+    for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
+        // the arguments re-read from the kernel-argument segment per tile through an opaque pointer: values
+        // derived from them cannot be hoisted out of the loop into registers (111 VGPRs otherwise)
+        const __attribute__((address_space(4))) SvaoArgs* ka =
+            (const __attribute__((address_space(4))) SvaoArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+        asm volatile("" : "+s"(ka));
+        const SvaoArgs& aa = *(const SvaoArgs*)ka;
+        uint32_t tid = threadIdx.x;  // likewise the lane's LDS and pixel addresses
+        asm volatile("" : "+v"(tid));
+        const uint32_t t = __builtin_amdgcn_readfirstlane(aa.tileList[i]);
+        pass2_tile<N, ND, SPEC, SPEC ? 16 : 20, SPEC ? 6 * ND + 64 : 0>(aa, (t % aa.tilesX) * kP2Tile + aa.guard,
+                                                                        (t / aa.tilesX) * kP2Tile + aa.guard, aa.tileFlags + t, sh,
+                                                                        tid);
+        __syncthreads();  // the tile's last LDS reads before the next tile's writes
+    }
+}
+
 // ---- host launchers of this TU's kernels (svao.hip picks the TU by rsd_svao_params.numerics)
 // pass 1: variant 0 = generic, 1 = specialised with NUM_DIRECTIONS = 8, 2 = specialised, any count
 void launch_pass1(const SvaoArgs& a, int variant, dim3 grid, dim3 block, hipStream_t s) {
@@ -487,15 +516,33 @@ void launch_pass1(const SvaoArgs& a, int variant, dim3 grid, dim3 block, hipStre
     else hipLaunchKernelGGL((svao_pass1_kernel<false, 0>), grid, block, 0, s, a);
 }
 
+// the loop kernel's resident workgroups (its occupancy x CUs; 0 if unknown)
+template <int N>
+static uint32_t loop_resident() {
+    static const uint32_t g = [] {
+        int dev = 0, cus = 0, nb = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, svao_pass2_loop_kernel<N, 8, true>, kP2Lanes, 0) != hipSuccess)
+            return 0u;
+        return (uint32_t)(std::max(nb, 0) * std::max(cus, 0));
+    }();
+    return g;
+}
+
 // pass 2: N SD samples, nd directions; spec: the specialised 8-direction kernel; list: the busy-tile
-// list kernel (workgroup i: list entry i) instead of the flag grid
+// list kernel (workgroup i: list entry i) instead of the flag grid; loop: the specialised list in the
+// resident grid (svao_pass2_loop_kernel)
 void launch_pass2(const SvaoArgs& a, uint32_t N, uint32_t nd, bool spec, dim3 grid, dim3 block, hipStream_t s,
-                  bool list) {
+                  bool list, bool loop) {
 #define RSD_P2K(K, NN, D, SP) hipLaunchKernelGGL((K<NN, D, SP>), grid, block, 0, s, a)
 #define RSD_P2(NN)                                                                                           \
     if (list) {                                                                                              \
         if (nd == 32u) RSD_P2K(svao_pass2_list_kernel, NN, 32, false);                                       \
         else if (nd == 16u) RSD_P2K(svao_pass2_list_kernel, NN, 16, false);                                  \
+        else if (spec && loop && loop_resident<NN>() && grid.x <= 8u * loop_resident<NN>())                  \
+            hipLaunchKernelGGL((svao_pass2_loop_kernel<NN, 8, true>), dim3(std::min(grid.x, loop_resident<NN>())),  \
+                               block, 0, s, a);                                                              \
         else if (spec) RSD_P2K(svao_pass2_list_kernel, NN, 8, true);                                          \
         else RSD_P2K(svao_pass2_list_kernel, NN, 8, false);                                                   \
     } else if (nd == 32u) RSD_P2K(svao_pass2_kernel, NN, 32, false);                                         \

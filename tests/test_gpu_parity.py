@@ -585,3 +585,32 @@ def test_busy_tile_list_and_flag_grid_agree(device, oracle, torch_dev):
         assert not r.tile_flags.cpu().numpy().view(np.uint32)[:T].any(), mode
     for mode, ao in zip(("list", "rows", "rows", "list", "list", "twice", "rows", "list"), out):
         assert np.array_equal(out[0], ao), mode
+
+
+def test_busy_tile_loop_matches_one_workgroup_per_tile(monkeypatch, torch_dev):
+    """At 1080p the specialised pass 2 strides the resident workgroups over the busy-tile list
+    (svao_pass2_loop_kernel, ~1.3 busy tiles per workgroup at configs[1]); RSD_PASS2_LOOP=off gives every
+    list entry its own workgroup.  Same AO bits, every flag consumed, over frames of a camera path."""
+    from rsd.frame import CONFIGS, FrameConfig, Renderer, camera_path
+    from rsd.scenes import make_scene
+    kw, sc = CONFIGS["suntemple_1080p_q"]
+    r = Renderer(make_scene(sc), FrameConfig(**kw))
+    vw, vh = r.cfg.visible_w, r.cfg.visible_h
+    T = ((vw + 15) // 16) * ((vh + 31) // 32 * 2)  # the flags; the list and its counts follow them
+    poses = [None] + camera_path("orbit120")[::50]
+    for frame, pose in enumerate(poses):
+        if pose is not None:
+            r.set_pose(*pose)
+        r.gbuffer()
+        aos = []
+        for loop in ("on", "off"):
+            monkeypatch.setenv("RSD_PASS2_LOOP", loop)
+            r.ao.zero_()
+            r.clear_intervals()
+            r.pass1()
+            r.sd_trace()
+            r.pass2()
+            aos.append(r.numpy()["ao"])
+            assert not r.tile_flags.cpu().numpy().view(np.uint32)[:T].any(), (frame, loop)
+        assert np.array_equal(aos[0], aos[1]), frame
+        assert (aos[0] != aos[0].flat[0]).any()  # a non-trivial AO image
