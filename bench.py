@@ -79,6 +79,10 @@ def parse():
                          "scaling, the north_star split); frame = every rank renders whole frames (weak scaling, "
                          "no per-frame collective); gather = interleaved bands with whole-map all-reduce / "
                          "all-gather (round-1 v1)")
+    ap.add_argument("--frame-impl", choices=("native", "python"), default="native",
+                    help="N > 1 band frames: native = rsd_band_frame (the frame's passes and exchanges issued from C++, "
+                         "RCCL communicators driven by librsd: one per frame slot); python = rsd/shard.py HaloFrame "
+                         "(torch.distributed collectives; also the gloo rehearsal's path)")
     ap.add_argument("--scene-file", default=None,
                     help="a .pyscene or .obj scene (rsd.pyscene / rsd.ingest) instead of the config's stand-in "
                          "scene; the config still sets the frame, SD map and N")
@@ -131,12 +135,13 @@ def main():
     from rsd import abi
     from rsd.frame import CONFIGS, DEFAULT_CAMERA_PATH, FrameConfig, Renderer, camera_path
     from rsd.scenes import make_scene
-    from rsd.shard import BandFrame, HaloFrame
+    from rsd.shard import BandFrame, HaloFrame, NativeComm, NativeHaloFrame
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    backend = None
     if world > 1:
         import torch.distributed as dist
         # RSD_BENCH_BACKEND=gloo: rehearsal of the N > 1 code paths with several ranks on one GPU
@@ -165,9 +170,15 @@ def main():
     bvh_build_s = r.gscene.info.build_ms * 1e-3
     bw = (rank, world) if shard == "gather" else (0, 1)
     F = max(1, args.frames_in_flight)
+    # N > 1 band frames issued from C++ (rsd_band_frame) over librsd's own RCCL communicators -- one per frame
+    # slot, so every communicator's operations stay on one stream; the gloo rehearsal keeps HaloFrame
+    native = shard == "band" and world > 1 and backend == "nccl" and args.frame_impl == "native"
+    comms = [NativeComm.rccl(rank, world, device=torch.device("cuda", local)) for _ in range(F)] if native else []
 
-    def make_frame(rend, throughput=False):
+    def make_frame(rend, throughput=False, slot=0):
         if shard == "band":
+            if native:
+                return NativeHaloFrame(rend, comms[slot], throughput=throughput)
             return HaloFrame(rend, rank, world, throughput=throughput)
         return BandFrame(rend, *bw, throughput=throughput)
 
@@ -192,8 +203,8 @@ def main():
             r.pass1()
             if shard == "band" and seq.sd_band is not None:  # N > 1: this rank's round-robin SD tiles
                 acc.append(r.sd_trace(counters=True, band=seq.sd_band, throughput=thr))
-            elif shard == "band":
-                acc.append(r.sd_trace_rows(seq.sd_rows[rank], counters=True, throughput=thr))
+            elif shard == "band":  # the SD rows under this rank's band
+                acc.append(r.sd_trace_rows(seq.owned_sd_rows()[0], counters=True, throughput=thr))
             else:
                 acc.append(r.sd_trace(counters=True, throughput=thr, band=bw))
     torch.cuda.synchronize()
@@ -246,7 +257,7 @@ def main():
 
     # ---- throughput region: F frames in flight on F streams
     slots = [make_frame(r, throughput=F > 1)] + \
-        [make_frame(r.frame_slot(own_gbuffer=bool(poses)), throughput=True) for _ in range(F - 1)]
+        [make_frame(r.frame_slot(own_gbuffer=bool(poses)), throughput=True, slot=j) for j in range(1, F)]
     streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(F - 1)]
     for st in streams[1:]:
         st.wait_stream(streams[0])
@@ -337,6 +348,7 @@ def main():
                                     rays, rays_active)
 
     if rank != 0:
+        close_frames([seq] + slots, comms)
         if dist:
             dist.destroy_process_group()
         return
@@ -366,6 +378,8 @@ def main():
                    "stoch_map_divisor": cfg.divisor, "camera_path": path_name,
                    "parallelism": {"band": f"screen-band+halo x{world}", "gather": f"screen-band+allgather x{world}",
                                    "frame": f"frame-parallel x{world}"}[shard],
+                   "frame_impl": ("native (rsd_band_frame, librsd RCCL communicators)" if native else
+                                  "python (rsd/shard.py)") if shard == "band" and world > 1 else "rsd_svao_frame",
                    "frames_in_flight": F},
         "value_definition": "dispatched SD rays / SD-kernel time (HIP events around every rsd_sd_trace of the "
                             "latency region; BASELINE.md section 4), summed over ranks",
@@ -412,8 +426,18 @@ def main():
         "cpu_baseline": cpu,
     }
     print(json.dumps(line))
+    close_frames([seq] + slots, comms)
     if dist:
         dist.destroy_process_group()
+
+
+def close_frames(frames, comms):
+    """Release the native band frames before their communicators (each waits for its stream)."""
+    for f in frames:
+        if hasattr(f, "close"):
+            f.close()
+    for c in comms:
+        c.close()
 
 
 def hit_order_record(r, frame_cls, new_ev, steps, warmup, pose, rays, rays_active):

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define RSD_ABI_VERSION 5
+#define RSD_ABI_VERSION 6
 
 typedef enum {
     RSD_OK = 0,
@@ -187,7 +187,8 @@ typedef struct {
  *   HBAO  horizon-based: visibility = max over the samples of saturate(HBAOKernel / pdf), pdf =
  *         0.9 (1 - r_i)^1.5, AO = saturate(1 - 2 avg)^exponent (Common.slang:60-66, 326-330, 362-365,
  *         421-430, 455-488).  The reference's UI scales the world radius by 1.5 on switching to HBAO
- *         (SVAO.cpp:617-620); callers pass the radius they want.  Raytraced secondary mode: VAO only. */
+ *         (SVAO.cpp:617-620); callers pass the radius they want.  Every secondary mode takes either kernel
+ *         (Raytraced HBAO: a closest-hit ray over [sphereStart, sphereEnd], Common.slang:622-650). */
 typedef enum { RSD_AO_KERNEL_VAO = 0, RSD_AO_KERNEL_HBAO = 1 } rsd_ao_kernel;
 /* Arithmetic of the SVAO passes ("AO 1", "AO 2"; the SD trace is always exact).
  *   FAST   FMA contraction, v_rcp_f32-based division, hardware sqrt / rsq, float32 denormals flushed, no
@@ -475,6 +476,99 @@ typedef struct {
 #define RSD_FRAME_KEEP_INTERVALS 8u   /* the trace leaves the interval maps as pass 1 wrote them (no consume) */
 /* flags: RSD_FRAME_INTERVALS_CLEAR | RSD_FRAME_KEEP_INTERVALS | RSD_SD_THROUGHPUT */
 rsd_status rsd_svao_frame(const rsd_svao_frame_desc* frame, uint32_t flags, void* const* events, rsd_stream stream);
+
+/* --- communicators of the band frame (ABI v6; multi-GPU) ---------------
+ * The exchanges of a screen-band frame, stream-ordered (no host wait for the GPU):
+ *   RCCL   one process per GPU (north_star: "final AO image all-gathered over RCCL/xGMI"): ncclAllGather,
+ *          ncclSend / ncclRecv in one ncclGroupStart / End on the caller's stream.  librccl.so.1 is loaded
+ *          on first use (the copy torch loaded, when it did).  rsd_comm_rccl_create is collective: every
+ *          rank calls it with the id rank 0 got from rsd_comm_rccl_unique_id, on its own GPU (the HIP
+ *          device current on the calling thread).
+ *   LOCAL  `world` host threads of one process sharing a GPU, one stream each (one-GPU tests of the N > 1
+ *          frame): device-to-device copies ordered by events; a hub is the threads' rendezvous.
+ * The reference renders on one GPU (no counterpart); the split's geometry follows SVAO.cpp:700-723 and
+ * VAOData.slang:44. */
+typedef struct rsd_comm rsd_comm;
+typedef struct rsd_comm_hub rsd_comm_hub;
+#define RSD_COMM_UNIQUE_ID_BYTES 128
+#define RSD_COMM_RCCL 1u
+#define RSD_COMM_LOCAL 2u
+#define RSD_COMM_NULL 3u   /* moves nothing: host-cost probes of one rank's frame (diagnostics only) */
+rsd_status rsd_comm_rccl_unique_id(uint8_t id[RSD_COMM_UNIQUE_ID_BYTES]);
+rsd_status rsd_comm_rccl_create(const uint8_t id[RSD_COMM_UNIQUE_ID_BYTES], uint32_t world, uint32_t rank,
+                                rsd_comm** out);
+rsd_status rsd_comm_hub_create(uint32_t world, rsd_comm_hub** out);
+void rsd_comm_hub_release(rsd_comm_hub* hub); /* after every rsd_comm of the hub */
+rsd_status rsd_comm_local_create(rsd_comm_hub* hub, uint32_t rank, rsd_comm** out);
+rsd_status rsd_comm_null_create(uint32_t world, uint32_t rank, rsd_comm** out);
+void rsd_comm_release(rsd_comm* comm);
+rsd_status rsd_comm_info(const rsd_comm* comm, uint32_t* kind, uint32_t* rank, uint32_t* world);
+/* d_recv = world x bytes (rank k's d_send at offset k x bytes) */
+rsd_status rsd_comm_all_gather(rsd_comm* comm, const void* d_send, void* d_recv, uint64_t bytes, rsd_stream stream);
+/* One group of point-to-point transfers (sizes agreed beforehand; a peer may be the rank itself) */
+typedef struct {
+    void* buf;
+    uint64_t bytes;
+    uint32_t peer;
+    uint32_t pad;
+} rsd_comm_xfer;
+rsd_status rsd_comm_exchange(rsd_comm* comm, const rsd_comm_xfer* sends, uint32_t n_sends, const rsd_comm_xfer* recvs,
+                             uint32_t n_recvs, rsd_stream stream);
+
+/* --- the screen-band frame (ABI v6) ---------------------------------
+ * One rank's share of SVAO::execute (SVAO.cpp:192-456) split into contiguous screen bands, issued from
+ * C++ on the caller's stream.  Rank r of the communicator's world:
+ *   front  the interval clear (skipped when the previous trace of this object consumed them) -> "AO 1" of
+ *          its visible rows (rsd_svao_pass1_rows) -> the SD texels its samples touched inside every other
+ *          rank's SD share, compacted on the device as (texel, rayMin, rayMax) triples -> an all-gather of
+ *          the per-peer counts (+ this object's previous frame time) -> an async copy of the count matrix
+ *          to pinned host memory;
+ *   back   the host reads the counts (one event; with frames in flight it completed long before) ->
+ *          point-to-point transfer of the triples -> atomic min / max merge (the exact 1-GPU interval
+ *          union on the rank's SD share) -> the SD trace of its share (round-robin 8-row tiles, or the SD
+ *          rows under its band: rsd_band_params.sd_split) -> the depths of exactly the texels each peer
+ *          sent come back to it -> "AO 2" of its rows -> an all-gather of the AO bands into d_ao.
+ * Every SD texel and AO pixel is produced by exactly one rank with the same kernels: each rank's AO
+ * image and its own SD share are bit-identical to the 1-GPU frame (rsd_svao_frame), whatever the split.
+ * The split of the 32-row groups is re-balanced every second frame from the ranks' measured pass-1 +
+ * trace + pass-2 times (same decision on every rank).  The frame description's buffers are used in
+ * place; its camera / params structs are copied (rsd_band_frame_front may pass a new camera).
+ * StochasticDepth mode with RayInterval only (the north_star's path). */
+#define RSD_SD_SPLIT_AUTO 0u   /* tiles for reduced-resolution SD maps (divisor > 1), rows at full resolution */
+#define RSD_SD_SPLIT_TILES 1u  /* the SD map's 8-row tiles dealt round-robin (tile t to rank t mod world) */
+#define RSD_SD_SPLIT_ROWS 2u   /* the SD rows under each rank's pass-1 band */
+typedef struct {
+    uint32_t divisor;     /* stochMapDivisor of the SD map (SVAO.cpp:143-150) */
+    uint32_t sd_split;    /* RSD_SD_SPLIT_* */
+    uint32_t rebalance;   /* 1: re-split from the measured per-rank time (needs world > 1) */
+    uint32_t throughput;  /* 1: traces flagged RSD_SD_THROUGHPUT (this frame overlaps others) */
+} rsd_band_params;
+typedef struct rsd_band_frame rsd_band_frame;
+rsd_status rsd_band_frame_create(const rsd_svao_frame_desc* frame, const rsd_band_params* params, rsd_comm* comm,
+                                 rsd_band_frame** out);
+/* cam: NULL or the camera of this frame (an animated camera; copied) */
+rsd_status rsd_band_frame_front(rsd_band_frame* bf, const rsd_camera* cam, rsd_stream stream);
+/* events: NULL or 2 hipEvent_t (each may be NULL) recorded before and after this rank's SD trace */
+rsd_status rsd_band_frame_back(rsd_band_frame* bf, void* const* events, rsd_stream stream);
+typedef struct {
+    uint32_t rank, world;
+    uint32_t sd_split;          /* RSD_SD_SPLIT_TILES or _ROWS (resolved) */
+    uint32_t groups;            /* 32-row groups of the visible rows */
+    uint32_t split[65];         /* group boundaries of the current split: rank k owns [split[k], split[k+1]) */
+    uint32_t sd_row0, sd_row1;  /* SD rows under this rank's band (sd_split ROWS: the rows it traces) */
+    uint32_t halo_px;           /* vertical reach of a sample in frame-buffer pixels (the window's margin) */
+    uint64_t frames;            /* back() calls */
+    uint64_t blocked_waits;     /* back() calls whose counts had not reached the host yet */
+    uint64_t resplits;          /* applied re-splits */
+    uint64_t bytes_intervals;   /* bytes sent so far: interval triples, SD replies, AO bands */
+    uint64_t bytes_sd;
+    uint64_t bytes_ao;
+    uint64_t dense_intervals;   /* what the dense halo (whole candidate regions) would send per frame */
+    uint64_t dense_sd;
+    uint64_t growth_syncs;      /* exchange buffers grown (each waits for this stream once) */
+} rsd_band_stats;
+rsd_status rsd_band_frame_stats(const rsd_band_frame* bf, rsd_band_stats* out);
+void rsd_band_frame_release(rsd_band_frame* bf); /* waits for the frame's stream work to finish */
 
 #ifdef __cplusplus
 }

@@ -325,12 +325,11 @@ def ray_cone_spread(focal_length, height):
 
 
 def svao_pass2_raytraced(scene: Scene, cam, vao: VAOData, p: SVAOParams, depth, normals, stencil, ao, cull=1,
-                         ray_pipeline=0, band=(0, 1), threads=None, alpha_test=1):
-    """SVAO "AO 2" in the Raytraced secondary mode; returns the updated AO image (VAO kernel, SingleDepth
-    primary visibility: the modes librsd's Raytraced pass supports)."""
-    if p.ao_kernel != 0 or p.primary_depth_mode != 0:
-        raise NotImplementedError("Raytraced AO 2: VAO kernel with SingleDepth primary visibility only")
-    p = _host_params(p)
+                         ray_pipeline=0, band=(0, 1), threads=None, alpha_test=1, depth2=None):
+    """SVAO "AO 2" in the Raytraced secondary mode; returns the updated AO image (VAO or HBAO kernel;
+    SingleDepth, or DualDepth primary visibility with the host `depth2` layer)."""
+    d2 = None if depth2 is None else np.ascontiguousarray(depth2, np.float32)
+    p = _host_params(p, d2)
     H, W = depth.shape
     ao = np.array(ao, np.uint8, copy=True)
     lib().ocpu_svao_pass2_rt_band(scene.h, C.byref(cam), C.byref(vao), C.byref(p), _p(depth), _p(normals), W, H,

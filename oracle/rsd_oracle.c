@@ -1813,9 +1813,9 @@ void ocpu_svao_pass2_band(const ocam* cam, const ovao* d, const osvao_params* p,
 
 /* ------------------------------------------------------------------ SVAO pass 2, Raytraced */
 /* calcAO2 DEPTH_MODE_RAYTRACING (Common.slang:598-651), traceAORay (SVAORaster2.ps.slang:9-46,
- * Ray.rt.slang:46-58) and aoAnyHit (Common.slang:679-718, VAO kernel), replayed literally over
- * the canonical any-hit stream: every hit in [TMin, TMax] (culling applied) in ascending
- * (t, prim) order, TMax shrinking on a commit. */
+ * Ray.rt.slang:46-58) and aoAnyHit (Common.slang:679-718), replayed literally over the canonical any-hit
+ * stream: every hit in [TMin, TMax] (culling applied) in ascending (t, prim) order, TMax shrinking on a
+ * commit.  VAO and HBAO kernels; SingleDepth or DualDepth primary visibility. */
 typedef struct {
     const oscene* s; const octx* x; const uint8_t* stencil; uint8_t* ao;
     uint32_t cull, rayPipeline, alphaTest;
@@ -1847,7 +1847,8 @@ static void* o_pass2_rt_rows(void* arg)
                 if (!(mask & (1u << i))) continue;
                 osample s;
                 o_sample_init(x, u, v, &b, i, &s);
-                o_eval_primary(x, &b, &s);
+                if (x->dual) o_eval_dual(x, &b, &s, 1); /* Common.slang:555-558 (force init) */
+                else o_eval_primary(x, &b, &s);
                 vis -= s.visibility;
                 /* getSnappedUV(samplePosUV): Common.slang:116-125, no clamp */
                 float suv[2] = {(floorf(s.samplePosUV[0] * d->resolution[0]) + 0.5f) / d->resolution[0],
@@ -1858,6 +1859,36 @@ static void* o_pass2_rt_rows(void* arg)
                 for (int k = 0; k < 3; ++k)
                     dw[k] = j->invView[k * 3 + 0] * dv[0] + j->invView[k * 3 + 1] * dv[1] + j->invView[k * 3 + 2] * dv[2];
                 const float L = s.initialSamplePosLength, pl = b.posVLength;
+                if (x->hbao) {
+                    /* Common.slang:622-628: the ray spans [sphereStart, sphereEnd]; no RAY_FLAG_FORCE_NON_OPAQUE, so
+                     * opaque triangles commit as closest hits and alpha-masked ones pass aoAnyHit (alpha test, then
+                     * ACCEPT whatever the face, :695-697, 715-717): tFirst = the nearest hit of the stream */
+                    float TMin = (pl - s.sphereStart) * L / pl;
+                    const float TMax = (pl - s.sphereEnd) * L / pl;
+                    if (!s.isInScreen) { s.visibility = 0.0f; s.objectSpaceZ = O_FLT_MAX; } /* resetSample (HBAO) */
+                    const float eps = b.radius * 0.01f;
+                    if (s.isInScreen) TMin = o_max(TMin, (pl - s.objectSpaceZ) * L / pl + eps);
+                    float tFirst = 0.0f; /* rayData.tFirst = 0.0: a miss leaves the ray origin */
+                    if (TMin <= TMax) {
+                        oray r;
+                        o_ray_setup(&r, c->posW, dw);
+                        ohits hs = {0};
+                        hs.limit = 1; /* the nearest hit only */
+                        o_collect(j->s, &r, TMin, TMax, j->cull, (int)j->alphaTest, &hs);
+                        if (hs.n) tFirst = hs.h[0].t; /* CommittedRayT (SVAORaster2.ps.slang:42-45) */
+                        free(hs.h);
+                    }
+                    /* Common.slang:647-649: samplePosW = origin + dir tFirst, samplePosV = mul(viewMat, (samplePosW, 1)) */
+                    float pw[3], pv[3];
+                    for (int k = 0; k < 3; ++k) pw[k] = c->posW[k] + dw[k] * tFirst;
+                    for (int k = 0; k < 3; ++k)
+                        pv[k] = ((c->viewMat[k * 4 + 0] * pw[0] + c->viewMat[k * 4 + 1] * pw[1]) + c->viewMat[k * 4 + 2] * pw[2]) +
+                                c->viewMat[k * 4 + 3];
+                    o_add_sample(x, &b, &s, pv, 0);
+                    vis += s.visibility;
+                    visD += s.visibility;
+                    continue;
+                }
                 /* RayData init, Common.slang:614-620 */
                 float halo = (pl - s.sphereStart - b.radius - d->thickness * b.radius) * L / pl;
                 float inside = (pl - s.sphereEnd) * L / pl;

@@ -9,8 +9,10 @@
 // HBM-streaming: bytes per texel = 8 (read both words) + 12 per touched texel; per triple 12 + 2 atomics.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <string>
 
+#include "comm.h"
 #include "rsd_internal.h"
 
 namespace rsd {
@@ -31,10 +33,18 @@ struct HaloRegions {
     uint32_t stride[kMaxRegions];
     int32_t* out[kMaxRegions];
     unsigned long long* count[kMaxRegions];
+    uint32_t ilv;                     // 1: interleaved triples out[3k + c] (the band frame's), 0: rows of `stride`
+    long long* row;                   // optional count row: row[0, rowN) zeroed, row[rowN] = extra
+    uint32_t rowN;
+    long long extra;
 };
 
 __global__ void halo_zero_kernel(HaloRegions R) {
     if (threadIdx.x < R.n) *R.count[threadIdx.x] = 0ull;
+    if (R.row) {
+        for (uint32_t i = threadIdx.x; i < R.rowN; i += blockDim.x) R.row[i] = 0;
+        if (threadIdx.x == 0) R.row[R.rowN] = R.extra;
+    }
 }
 
 __global__ void __launch_bounds__(kHaloBlock) halo_compact_kernel(const uint32_t* __restrict__ rmin,
@@ -72,10 +82,16 @@ __global__ void __launch_bounds__(kHaloBlock) halo_compact_kernel(const uint32_t
         if (touched && r == rl) {
             const uint32_t k = (uint32_t)base + (uint32_t)__popcll(grp & ((1ull << lane) - 1ull));
             int32_t* o = R.out[rl];
-            const uint32_t st = R.stride[rl];
-            o[k] = (int32_t)t;
-            o[st + k] = (int32_t)lo;
-            o[2u * st + k] = (int32_t)hi;
+            if (R.ilv) {
+                o[3u * k] = (int32_t)t;
+                o[3u * k + 1u] = (int32_t)lo;
+                o[3u * k + 2u] = (int32_t)hi;
+            } else {
+                const uint32_t st = R.stride[rl];
+                o[k] = (int32_t)t;
+                o[st + k] = (int32_t)lo;
+                o[2u * st + k] = (int32_t)hi;
+            }
         }
         pending &= ~grp;
     }
@@ -88,6 +104,7 @@ struct HaloLists {
     const int32_t* idx[kMaxRegions];  // merge: the triples; SD: the texel indices
     float* buf[kMaxRegions];          // SD: the packed depths
     uint32_t stride[kMaxRegions];     // merge: the triples' row stride
+    uint32_t ilv;                     // 1: interleaved triples {texel, rayMin, rayMax} (merge; SD: index stride 3)
 };
 
 __device__ __forceinline__ uint32_t list_of(const HaloLists& H, uint32_t g) {
@@ -102,10 +119,11 @@ __global__ void __launch_bounds__(kHaloBlock) halo_merge_kernel(uint32_t* __rest
     if (g >= H.first[H.n]) return;
     const uint32_t l = list_of(H, g), k = g - H.first[l];
     const int32_t* tr = H.idx[l];
-    const uint32_t t = (uint32_t)tr[k];
+    const uint32_t i0 = H.ilv ? 3u * k : k, st = H.ilv ? 1u : H.stride[l];
+    const uint32_t t = (uint32_t)tr[i0];
     if (t >= total) return;  // never: the sender's indices lie in the map
-    if (interval) atomicMin(&rmin[t], (uint32_t)tr[H.stride[l] + k]);
-    atomicMax(&rmax[t], (uint32_t)tr[2u * H.stride[l] + k]);
+    if (interval) atomicMin(&rmin[t], (uint32_t)tr[i0 + st]);
+    atomicMax(&rmax[t], (uint32_t)tr[i0 + 2u * st]);
 }
 
 // one lane per (list item, layer, channel): item-major within a list, so a list's lanes read its
@@ -118,7 +136,7 @@ __global__ void __launch_bounds__(kHaloBlock) halo_sd_kernel(float* __restrict__
     const uint32_t l = list_of(H, g), e = g - H.first[l];
     const uint32_t n = (H.first[l + 1] - H.first[l]) / (layers * ch);
     const uint32_t per = n * ch, L = e / per, rem = e % per, k = rem / ch, c = rem % ch;
-    const uint32_t t = (uint32_t)H.idx[l][k];
+    const uint32_t t = (uint32_t)H.idx[l][H.ilv ? 3u * k : k];
     if (t >= texels) return;
     const size_t so = ((size_t)L * texels + t) * ch + c;
     if (GATHER) H.buf[l][e] = sd[so];
@@ -130,22 +148,73 @@ rsd_status launch_check(const char* what) {
     return e == hipSuccess ? RSD_OK : hip_fail(e, what);
 }
 
+// a batch of byte copies (the band frame's AO band packing / unpacking, the in-process communicator):
+// 16-B lanes where a segment's source, destination and size are 16-B aligned, bytes otherwise
+struct CopySegs {
+    uint32_t n;
+    uint64_t first[kMaxCopySegs + 1];  // first work item of each segment
+    const uint8_t* src[kMaxCopySegs];
+    uint8_t* dst[kMaxCopySegs];
+    uint64_t bytes[kMaxCopySegs];
+    uint32_t vec[kMaxCopySegs];        // 1: 16-B items
+};
+
+__global__ void __launch_bounds__(kHaloBlock) copy_segments_kernel(CopySegs S) {
+    const uint64_t total = S.first[S.n];
+    for (uint64_t g = (uint64_t)blockIdx.x * kHaloBlock + threadIdx.x; g < total;
+         g += (uint64_t)gridDim.x * kHaloBlock) {
+        uint32_t l = 0;
+        while (g >= S.first[l + 1]) ++l;
+        const uint64_t e = g - S.first[l];
+        if (S.vec[l]) reinterpret_cast<uint4*>(S.dst[l])[e] = reinterpret_cast<const uint4*>(S.src[l])[e];
+        else S.dst[l][e] = S.src[l][e];
+    }
+}
+
 }  // namespace
-}  // namespace rsd
 
-using namespace rsd;
+rsd_status copy_segments(const CopySeg* segs, uint32_t n, hipStream_t s) {
+    if (n > kMaxCopySegs) {
+        set_error("copy_segments: more than 16 segments");
+        return RSD_ERR_INVALID_ARG;
+    }
+    CopySegs S{};
+    uint64_t total = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        const uintptr_t a = reinterpret_cast<uintptr_t>(segs[i].src) | reinterpret_cast<uintptr_t>(segs[i].dst) |
+                            (uintptr_t)segs[i].bytes;
+        S.vec[S.n] = (a & 15u) == 0u ? 1u : 0u;
+        S.src[S.n] = static_cast<const uint8_t*>(segs[i].src);
+        S.dst[S.n] = static_cast<uint8_t*>(segs[i].dst);
+        S.bytes[S.n] = segs[i].bytes;
+        S.first[S.n] = total;
+        total += S.vec[S.n] ? segs[i].bytes / 16u : segs[i].bytes;
+        if (segs[i].bytes) ++S.n;
+    }
+    S.first[S.n] = total;
+    if (total == 0) return RSD_OK;
+    const uint64_t blocks = std::min<uint64_t>((total + kHaloBlock - 1) / kHaloBlock, 4096u);
+    hipLaunchKernelGGL(copy_segments_kernel, dim3((uint32_t)blocks), dim3(kHaloBlock), 0, s, S);
+    return launch_check("copy_segments_kernel launch");
+}
 
-extern "C" rsd_status rsd_halo_compact(const uint32_t* d_ray_min, const uint32_t* d_ray_max, uint32_t sd_w,
-                                       uint32_t sd_h, const rsd_halo_region* regions, uint32_t n_regions,
-                                       rsd_stream stream) {
-    if (!d_ray_min || !d_ray_max || (n_regions && !regions) || n_regions > kMaxRegions) {
+// The compaction of rsd_halo_compact; ilv = 1 writes interleaved triples (the band frame's layout: a
+// peer's prefix is one contiguous transfer); row (optional): a count row whose [0, rowN) is zeroed and
+// row[rowN] = extra in the same launch that zeroes the counts (the counts may point into it).
+rsd_status halo_compact_impl(const uint32_t* d_ray_min, const uint32_t* d_ray_max, uint32_t sd_w, uint32_t sd_h,
+                             const rsd_halo_region* regions, uint32_t n_regions, bool ilv, int64_t* row,
+                             uint32_t row_n, int64_t extra, hipStream_t s) {
+    if (!d_ray_min || !d_ray_max || (n_regions && !regions) || n_regions > kMaxRegions || row_n > 64u) {
         set_error("rsd_halo_compact: null buffer or more than 64 regions");
         return RSD_ERR_INVALID_ARG;
     }
     HaloRegions R{};
     R.n = n_regions;
+    R.ilv = ilv ? 1u : 0u;
+    R.row = reinterpret_cast<long long*>(row);
+    R.rowN = row_n;
+    R.extra = (long long)extra;
     uint32_t total = 0;
-    hipStream_t s = (hipStream_t)stream;
     for (uint32_t r = 0; r < n_regions; ++r) {
         const rsd_halo_region& g = regions[r];
         const uint32_t period = g.period > 1u ? g.period : 1u;
@@ -169,8 +238,8 @@ extern "C" rsd_status rsd_halo_compact(const uint32_t* d_ray_min, const uint32_t
         total += (uint32_t)texels;
     }
     R.first[n_regions] = total;
-    if (n_regions == 0) return RSD_OK;
-    // the counts start at zero (one launch for all regions), then one compaction launch
+    if (n_regions == 0 && !row) return RSD_OK;
+    // the counts (and the count row) start at zero (one launch for all regions), then one compaction launch
     hipLaunchKernelGGL(halo_zero_kernel, dim3(1), dim3(64), 0, s, R);
     if (total == 0) return launch_check("halo_zero_kernel launch");
     hipLaunchKernelGGL(halo_compact_kernel, dim3((total + kHaloBlock - 1) / kHaloBlock), dim3(kHaloBlock), 0, s,
@@ -178,18 +247,19 @@ extern "C" rsd_status rsd_halo_compact(const uint32_t* d_ray_min, const uint32_t
     return launch_check("halo_compact_kernel launch");
 }
 
-extern "C" rsd_status rsd_halo_merge(uint32_t* d_ray_min, uint32_t* d_ray_max, uint32_t sd_w, uint32_t sd_h,
-                                     const rsd_halo_list* lists, uint32_t n_lists, uint32_t ray_interval,
-                                     rsd_stream stream) {
+rsd_status halo_merge_impl(uint32_t* d_ray_min, uint32_t* d_ray_max, uint32_t sd_w, uint32_t sd_h,
+                           const rsd_halo_list* lists, uint32_t n_lists, uint32_t ray_interval, bool ilv,
+                           hipStream_t s) {
     if (!d_ray_min || !d_ray_max || (n_lists && !lists) || n_lists > kMaxRegions) {
         set_error("rsd_halo_merge: null buffer or more than 64 lists");
         return RSD_ERR_INVALID_ARG;
     }
     HaloLists H{};
     H.n = n_lists;
+    H.ilv = ilv ? 1u : 0u;
     uint32_t total = 0;
     for (uint32_t l = 0; l < n_lists; ++l) {
-        if ((lists[l].n && !lists[l].triples) || lists[l].stride < lists[l].n) {
+        if ((lists[l].n && !lists[l].triples) || (!ilv && lists[l].stride < lists[l].n)) {
             set_error("rsd_halo_merge: null triples or stride below n");
             return RSD_ERR_INVALID_ARG;
         }
@@ -200,20 +270,20 @@ extern "C" rsd_status rsd_halo_merge(uint32_t* d_ray_min, uint32_t* d_ray_max, u
     }
     H.first[n_lists] = total;
     if (total == 0) return RSD_OK;
-    hipLaunchKernelGGL(halo_merge_kernel, dim3((total + kHaloBlock - 1) / kHaloBlock), dim3(kHaloBlock), 0,
-                       (hipStream_t)stream, d_ray_min, d_ray_max, H, sd_w * sd_h, ray_interval ? 1u : 0u);
+    hipLaunchKernelGGL(halo_merge_kernel, dim3((total + kHaloBlock - 1) / kHaloBlock), dim3(kHaloBlock), 0, s,
+                       d_ray_min, d_ray_max, H, sd_w * sd_h, ray_interval ? 1u : 0u);
     return launch_check("halo_merge_kernel launch");
 }
 
-namespace {
-rsd_status halo_sd(bool gather, float* sd, uint32_t layers, uint32_t sd_w, uint32_t sd_h, uint32_t ch,
-                   const rsd_halo_sd_list* lists, uint32_t n_lists, rsd_stream stream, const char* who) {
+rsd_status halo_sd_impl(bool gather, float* sd, uint32_t layers, uint32_t sd_w, uint32_t sd_h, uint32_t ch,
+                        const rsd_halo_sd_list* lists, uint32_t n_lists, bool ilv, hipStream_t s, const char* who) {
     if (!sd || (n_lists && !lists) || n_lists > kMaxRegions || !layers || !ch || ch > 4) {
         set_error(std::string(who) + ": null buffer, more than 64 lists, or layers / channels out of range");
         return RSD_ERR_INVALID_ARG;
     }
     HaloLists H{};
     H.n = n_lists;
+    H.ilv = ilv ? 1u : 0u;
     uint64_t total = 0;
     for (uint32_t l = 0; l < n_lists; ++l) {
         if (lists[l].n && (!lists[l].idx || !lists[l].buf)) {
@@ -233,22 +303,37 @@ rsd_status halo_sd(bool gather, float* sd, uint32_t layers, uint32_t sd_w, uint3
     if (total == 0) return RSD_OK;
     const dim3 grid((uint32_t)((total + kHaloBlock - 1) / kHaloBlock));
     if (gather)
-        hipLaunchKernelGGL(halo_sd_kernel<true>, grid, dim3(kHaloBlock), 0, (hipStream_t)stream, sd, H, layers,
-                           sd_w * sd_h, ch);
+        hipLaunchKernelGGL(halo_sd_kernel<true>, grid, dim3(kHaloBlock), 0, s, sd, H, layers, sd_w * sd_h, ch);
     else
-        hipLaunchKernelGGL(halo_sd_kernel<false>, grid, dim3(kHaloBlock), 0, (hipStream_t)stream, sd, H, layers,
-                           sd_w * sd_h, ch);
+        hipLaunchKernelGGL(halo_sd_kernel<false>, grid, dim3(kHaloBlock), 0, s, sd, H, layers, sd_w * sd_h, ch);
     return launch_check(who);
 }
-}  // namespace
+
+}  // namespace rsd
+
+using namespace rsd;
+
+extern "C" rsd_status rsd_halo_compact(const uint32_t* d_ray_min, const uint32_t* d_ray_max, uint32_t sd_w,
+                                       uint32_t sd_h, const rsd_halo_region* regions, uint32_t n_regions,
+                                       rsd_stream stream) {
+    return halo_compact_impl(d_ray_min, d_ray_max, sd_w, sd_h, regions, n_regions, false, nullptr, 0u, 0,
+                             (hipStream_t)stream);
+}
+
+extern "C" rsd_status rsd_halo_merge(uint32_t* d_ray_min, uint32_t* d_ray_max, uint32_t sd_w, uint32_t sd_h,
+                                     const rsd_halo_list* lists, uint32_t n_lists, uint32_t ray_interval,
+                                     rsd_stream stream) {
+    return halo_merge_impl(d_ray_min, d_ray_max, sd_w, sd_h, lists, n_lists, ray_interval, false, (hipStream_t)stream);
+}
 
 extern "C" rsd_status rsd_halo_sd_gather(const float* d_sd, uint32_t layers, uint32_t sd_w, uint32_t sd_h, uint32_t ch,
                                          const rsd_halo_sd_list* lists, uint32_t n_lists, rsd_stream stream) {
-    return halo_sd(true, const_cast<float*>(d_sd), layers, sd_w, sd_h, ch, lists, n_lists, stream,
-                   "rsd_halo_sd_gather");
+    return halo_sd_impl(true, const_cast<float*>(d_sd), layers, sd_w, sd_h, ch, lists, n_lists, false,
+                        (hipStream_t)stream, "rsd_halo_sd_gather");
 }
 
 extern "C" rsd_status rsd_halo_sd_scatter(float* d_sd, uint32_t layers, uint32_t sd_w, uint32_t sd_h, uint32_t ch,
                                           const rsd_halo_sd_list* lists, uint32_t n_lists, rsd_stream stream) {
-    return halo_sd(false, d_sd, layers, sd_w, sd_h, ch, lists, n_lists, stream, "rsd_halo_sd_scatter");
+    return halo_sd_impl(false, d_sd, layers, sd_w, sd_h, ch, lists, n_lists, false, (hipStream_t)stream,
+                        "rsd_halo_sd_scatter");
 }

@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -76,6 +77,7 @@ struct rsd_scene {
     uint64_t bvh_bytes = 0;      // the d_nodes allocation (nodes + triangle records + pad)
     uint32_t* d_prim_rec = nullptr;  // primitive id -> triangle record index (raster walk's keys)
     std::vector<rsd::SdWorkspace*> sd_ws;  // one per stream that traced this scene (few: linear lookup)
+    std::mutex ws_mutex;                   // sd_ws: host threads may trace one scene on their own streams
     void* d_alpha = nullptr;       // alpha data (rsd_scene_upload_alpha), one allocation
     rsd::AlphaData alpha;          // device pointers into d_alpha
     // segment entry grid (entry_grid.h): one allocation, hash slots (uint4) then entry items
@@ -89,6 +91,19 @@ struct rsd_scene {
 namespace rsd {
 void set_error(const std::string& msg);
 rsd_status hip_fail(hipError_t e, const char* what);
+
+// halo.hip: the sparse-halo steps with the band frame's options (csrc/band_frame.cpp).  ilv: interleaved
+// triples {texel, rayMin, rayMax} (a peer's prefix is one contiguous transfer); the SD lists then index
+// with stride 3 (their idx points at the triples).  row: a count row zeroed ([0, row_n)) with
+// row[row_n] = extra in the launch that zeroes the region counts.
+rsd_status halo_compact_impl(const uint32_t* d_ray_min, const uint32_t* d_ray_max, uint32_t sd_w, uint32_t sd_h,
+                             const rsd_halo_region* regions, uint32_t n_regions, bool ilv, int64_t* row,
+                             uint32_t row_n, int64_t extra, hipStream_t s);
+rsd_status halo_merge_impl(uint32_t* d_ray_min, uint32_t* d_ray_max, uint32_t sd_w, uint32_t sd_h,
+                           const rsd_halo_list* lists, uint32_t n_lists, uint32_t ray_interval, bool ilv,
+                           hipStream_t s);
+rsd_status halo_sd_impl(bool gather, float* sd, uint32_t layers, uint32_t sd_w, uint32_t sd_h, uint32_t ch,
+                        const rsd_halo_sd_list* lists, uint32_t n_lists, bool ilv, hipStream_t s, const char* who);
 }  // namespace rsd
 
 #define RSD_HIP(call)                                                   \

@@ -1774,9 +1774,12 @@ constexpr int kLutDevices = 64;
 LutCache g_lut[kLutDevices][17];
 std::mutex g_lut_mutex;
 
-// the SD-trace workspace of (scene, stream); created on the stream's first trace
-constexpr size_t kMaxWorkspaces = 16;
+// the SD-trace workspace of (scene, stream); created on the stream's first trace.  Host threads may trace
+// one scene on their own streams (the band frame's rank threads): the list is locked; a workspace is only
+// used by its stream's calls, which the caller orders
+constexpr size_t kMaxWorkspaces = 64;
 rsd_status sd_workspace(rsd_scene* scene, hipStream_t s, SdWorkspace** out) {
+    std::lock_guard<std::mutex> lock(scene->ws_mutex);
     for (SdWorkspace* w : scene->sd_ws)
         if (w->stream == s) { *out = w; return RSD_OK; }
     if (scene->sd_ws.size() >= kMaxWorkspaces) {

@@ -4,7 +4,17 @@
 //
 // Reference: calcAO2 DEPTH_MODE_RAYTRACING (SVAO/Common.slang:598-651), traceAORay
 // (SVAORaster2.ps.slang:9-46 RayQuery, Ray.rt.slang:46-58 TraceRay) and aoAnyHit
-// (Common.slang:679-718, VAO kernel); dispatch SVAO.cpp:408-455.
+// (Common.slang:679-718); dispatch SVAO.cpp:408-455.  Both AO kernels and both primary depth modes:
+// the raster sample p of a refined direction comes from evalPrimaryVisibility, or with DualDepth from
+// evalDualVisibility(data, true) (Common.slang:555-558).
+//
+// HBAO (Common.slang:622-628, 646-650): the ray spans [sphereStart, sphereEnd] (TMin raised to the
+// depth buffer + epsilon on screen) WITHOUT RAY_FLAG_FORCE_NON_OPAQUE, so opaque triangles commit as
+// closest hits directly and alpha-masked ones pass aoAnyHit (alpha test, then ACCEPT whatever the face,
+// Common.slang:695-697, 715-717): tFirst = the nearest non-culled hit that passes the alpha test (0 when
+// the ray misses, SVAORaster2.ps.slang:42-45 / Ray.rt.slang:37-43), and the sample point
+// mul(viewMat, posW + dir tFirst) goes through addSample (max of saturate(HBAOKernel / pdf)).  The
+// traversal below finds that hit with tCRS = -inf: every accepted hit then terminates, so A = tFirst.
 //
 // Any-hit order.  As for the SD trace, the hit stream is canonical: ascending t, each
 // triangle once.  aoAnyHit over that stream (accepted = front face, or double-sided, or
@@ -44,7 +54,7 @@ struct RtArgs {
 __device__ __forceinline__ void trace_ao(const float4* __restrict__ bvh, uint32_t triOff, const RayCtx& r, float tmin,
                                          float tmax, uint32_t cull, float tCRS, float tSS, float& A, float& B,
                                          uint32_t* __restrict__ ldsItem, float* __restrict__ ldsT, bool alphaOn,
-                                         const AlphaData& alpha) {
+                                         const AlphaData& alpha, bool anyFace) {
     A = INFINITY;
     B = -INFINITY;
     uint32_t spillItem[kStackTotal - kLdsStack];
@@ -68,9 +78,10 @@ __device__ __forceinline__ void trace_ao(const float4* __restrict__ bvh, uint32_
                 if (!(t >= tmin && t <= thi)) continue;
                 const uint32_t flags = __float_as_uint(q[3 * j + 1].w);
                 if (culled(det, flags, cull)) continue;
-                // aoAnyHit: frontFace || isDoubleSided || isAlphaTested (Common.slang:695-697)
+                // aoAnyHit: frontFace || isDoubleSided || isAlphaTested (Common.slang:695-697); HBAO's opaque
+                // triangles never reach it (closest hit without RAY_FLAG_FORCE_NON_OPAQUE)
                 const bool front = (det > 0.0f) != ((flags & RSD_TRI_FRONT_CW) != 0u);
-                if (!(front || (flags & (RSD_TRI_DOUBLE_SIDED | RSD_TRI_ALPHA_MASK)))) continue;
+                if (!anyFace && !(front || (flags & (RSD_TRI_DOUBLE_SIDED | RSD_TRI_ALPHA_MASK)))) continue;
                 // USE_ALPHA_TEST: alpha test at LOD 0 (Common.slang:683-691) -> AO_HIT_IGNORE
                 if (alphaOn && (flags & RSD_TRI_ALPHA_MASK) &&
                     alpha_test_fails(alpha, __float_as_uint(q[3 * j].w), q[3 * j], q[3 * j + 1], q[3 * j + 2], bu, bv,
@@ -140,7 +151,8 @@ __device__ __forceinline__ void rt_dir(const RtArgs& ra, const Basic& b, float u
     Sample s;
     bool ssrAbove;
     sample_init(a, u, v, b, i, s, ssrAbove);
-    eval_primary(a, b, s);
+    if (a.dualDepth) eval_dual(a, b, s, ssrAbove, true);  // Common.slang:555-558 (force init)
+    else eval_primary(a, b, s);
     p = s.visibility;
     // getSnappedUV (Common.slang:116-125), not clamped: rays may leave the screen
     const float su = (floorf(s.su * d.resolution[0]) + 0.5f) / d.resolution[0];
@@ -150,6 +162,31 @@ __device__ __forceinline__ void rt_dir(const RtArgs& ra, const Basic& b, float u
                      M[6] * dv.x + M[7] * dv.y + M[8] * dv.z);
     const float initLen = length(s.ip);
     const float pl = b.posVLength;
+    if (a.k.hbao) {  // Common.slang:622-628, 637-638, 646-650
+        float TMin = (pl - s.sphereStart) * initLen / pl;
+        const float TMax = (pl - s.sphereEnd) * initLen / pl;
+        if (!s.isInScreen) { s.visibility = 0.0f; s.objectSpaceZ = 3.402823466e+38f; }  // resetSample (HBAO)
+        const float eps = b.radius * 0.01f;
+        if (s.isInScreen) TMin = hmax(TMin, (pl - s.objectSpaceZ) * initLen / pl + eps);
+        float tFirst = 0.0f;
+        if (TMin <= TMax) {
+            RayCtx r;
+            ray_setup(r, camPos, dw);
+            float A, B;
+            trace_ao(ra.nodes, ra.triOff, r, TMin, TMax, ra.cull, -INFINITY, INFINITY, A, B, ldsItem, ldsT,
+                     ra.alphaTest != 0u, ra.alpha, true);
+            if (A != INFINITY) tFirst = A;
+        }
+        // samplePosW = ray.Origin + ray.Direction tFirst; samplePosV = mul(viewMat, float4(samplePosW, 1))
+        const f3 pw = mk(camPos.x + dw.x * tFirst, camPos.y + dw.y * tFirst, camPos.z + dw.z * tFirst);
+        const float* V = a.cam.viewMat;
+        const f3 pv = mk(((V[0] * pw.x + V[1] * pw.y) + V[2] * pw.z) + V[3],
+                         ((V[4] * pw.x + V[5] * pw.y) + V[6] * pw.z) + V[7],
+                         ((V[8] * pw.x + V[9] * pw.y) + V[10] * pw.z) + V[11]);
+        add_sample(a, b, s, pv, false);
+        rOut = s.visibility;
+        return;
+    }
     const float tHalo0 = (pl - s.sphereStart - b.radius - d.thickness * b.radius) * initLen / pl;
     const float tInside0 = (pl - s.sphereEnd) * initLen / pl;
     const float tCRS = (pl - b.radius - d.thickness * b.radius) * initLen / pl;
@@ -165,7 +202,7 @@ __device__ __forceinline__ void rt_dir(const RtArgs& ra, const Basic& b, float u
         ray_setup(r, camPos, dw);
         float A, B;
         trace_ao(ra.nodes, ra.triOff, r, TMin, TMax, ra.cull, tCRS, tSS, A, B, ldsItem, ldsT, ra.alphaTest != 0u,
-                 ra.alpha);
+                 ra.alpha, false);
         if (B != -INFINITY) halo = hmax(halo, B);
         if (A != INFINITY) {
             if (A <= tSS) halo = hmax(halo, A);
@@ -276,17 +313,16 @@ extern "C" rsd_status rsd_svao_pass2_raytraced_band(rsd_scene* scene, const rsd_
         set_error("rsd_svao_pass2_raytraced: null argument or bad cull mode");
         return RSD_ERR_INVALID_ARG;
     }
-    if (p->ao_kernel != RSD_AO_KERNEL_VAO || p->primary_depth_mode != 0) {
-        // the HBAO ray (a committed closest hit, SVAORaster2.ps.slang:12-15, 42-45) and the DualDepth
-        // primary mode are implemented for the raster and StochasticDepth passes only
-        set_error("rsd_svao_pass2_raytraced: only the VAO kernel with SingleDepth primary visibility");
-        return RSD_ERR_UNSUPPORTED;
+    if (p->ao_kernel > RSD_AO_KERNEL_HBAO || p->primary_depth_mode > 1u || (p->primary_depth_mode == 1u && !p->d_depth2)) {
+        set_error("rsd_svao_pass2_raytraced: ao_kernel must be VAO or HBAO, primary_depth_mode 0 or 1 (DualDepth needs "
+                  "d_depth2)");
+        return RSD_ERR_INVALID_ARG;
     }
     RtArgs ra{};
     SvaoArgs& a = ra.s;
     a.cam = *cam;
     a.d = *vao;
-    fill_consts(a.k, a.d, p->num_directions);
+    fill_consts(a.k, a.d, p->num_directions, p->ao_kernel);
     {
         rsd_status ts = snap_tables(a.d, &a.snapU, &a.snapV);
         if (ts == RSD_OK) ts = normal_lut(&a.nlut);
@@ -304,6 +340,8 @@ extern "C" rsd_status rsd_svao_pass2_raytraced_band(rsd_scene* scene, const rsd_
     a.dual = p->dual_ao ? 1u : 0u;
     a.bandIndex = band_index;
     a.bandCount = band_count;
+    a.dualDepth = p->primary_depth_mode == 1u ? 1u : 0u;
+    a.depth2 = p->d_depth2;
     ra.nodes = scene->d_nodes;
     ra.triOff = scene->tri_offset;
     ra.cull = cull_mode;

@@ -117,6 +117,30 @@ class FrameDesc(C.Structure):  # rsd_svao_frame_desc
                 ("ray_pipeline", C.c_uint32)]
 
 
+class CommXfer(C.Structure):  # rsd_comm_xfer
+    _fields_ = [("buf", C.c_void_p), ("bytes", C.c_uint64), ("peer", C.c_uint32), ("pad", C.c_uint32)]
+
+
+COMM_RCCL, COMM_LOCAL, COMM_NULL = 1, 2, 3  # rsd.h RSD_COMM_*
+COMM_UNIQUE_ID_BYTES = 128
+SD_SPLIT_AUTO, SD_SPLIT_TILES, SD_SPLIT_ROWS = 0, 1, 2  # rsd.h RSD_SD_SPLIT_*
+SD_SPLITS = {"auto": SD_SPLIT_AUTO, "tiles": SD_SPLIT_TILES, "rows": SD_SPLIT_ROWS}
+
+
+class BandParams(C.Structure):  # rsd_band_params
+    _fields_ = [("divisor", C.c_uint32), ("sd_split", C.c_uint32), ("rebalance", C.c_uint32),
+                ("throughput", C.c_uint32)]
+
+
+class BandStats(C.Structure):  # rsd_band_stats
+    _fields_ = [("rank", C.c_uint32), ("world", C.c_uint32), ("sd_split", C.c_uint32), ("groups", C.c_uint32),
+                ("split", C.c_uint32 * 65), ("sd_row0", C.c_uint32), ("sd_row1", C.c_uint32),
+                ("halo_px", C.c_uint32), ("frames", C.c_uint64), ("blocked_waits", C.c_uint64),
+                ("resplits", C.c_uint64), ("bytes_intervals", C.c_uint64), ("bytes_sd", C.c_uint64),
+                ("bytes_ao", C.c_uint64), ("dense_intervals", C.c_uint64), ("dense_sd", C.c_uint64),
+                ("growth_syncs", C.c_uint64)]
+
+
 FRAME_INTERVALS_CLEAR = 4  # rsd.h RSD_FRAME_INTERVALS_CLEAR
 FRAME_KEEP_INTERVALS = 8   # rsd.h RSD_FRAME_KEEP_INTERVALS
 
@@ -149,7 +173,11 @@ EXPORTS = ["rsd_abi_version", "rsd_svao_tile_count", "rsd_last_error", "rsd_devi
            "rsd_linearize_depth", "rsd_compress_normals", "rsd_svao_pass2_raytraced", "rsd_svao_pass2_raytraced_band",
            "rsd_scene_upload_alpha", "rsd_ray_cone_spread", "rsd_sd_trace_band_ex", "rsd_scene_export_bvh",
            "rsd_bvh_build", "rsd_svao_pass1_rows", "rsd_svao_pass2_rows", "rsd_sd_trace_rows", "rsd_svao_frame",
-           "rsd_halo_compact", "rsd_halo_merge", "rsd_halo_sd_gather", "rsd_halo_sd_scatter"]
+           "rsd_halo_compact", "rsd_halo_merge", "rsd_halo_sd_gather", "rsd_halo_sd_scatter",
+           "rsd_comm_rccl_unique_id", "rsd_comm_rccl_create", "rsd_comm_hub_create", "rsd_comm_hub_release",
+           "rsd_comm_local_create", "rsd_comm_null_create", "rsd_comm_release", "rsd_comm_info", "rsd_comm_all_gather", "rsd_comm_exchange",
+           "rsd_band_frame_create", "rsd_band_frame_front", "rsd_band_frame_back", "rsd_band_frame_stats",
+           "rsd_band_frame_release"]
 
 SD_CONSUME_INTERVALS = 1
 SD_THROUGHPUT = 2  # frames in flight: the work-efficient traversal (rsd.h RSD_SD_THROUGHPUT)
@@ -252,6 +280,36 @@ def lib():
         L.rsd_halo_sd_gather.argtypes = [vp, u32, u32, u32, u32, C.POINTER(HaloSdList), u32, vp]
         L.rsd_halo_sd_scatter.restype = st
         L.rsd_halo_sd_scatter.argtypes = [vp, u32, u32, u32, u32, C.POINTER(HaloSdList), u32, vp]
+        L.rsd_comm_rccl_unique_id.restype = st
+        L.rsd_comm_rccl_unique_id.argtypes = [vp]
+        L.rsd_comm_rccl_create.restype = st
+        L.rsd_comm_rccl_create.argtypes = [vp, u32, u32, C.POINTER(vp)]
+        L.rsd_comm_hub_create.restype = st
+        L.rsd_comm_hub_create.argtypes = [u32, C.POINTER(vp)]
+        L.rsd_comm_hub_release.restype = None
+        L.rsd_comm_hub_release.argtypes = [vp]
+        L.rsd_comm_local_create.restype = st
+        L.rsd_comm_local_create.argtypes = [vp, u32, C.POINTER(vp)]
+        L.rsd_comm_null_create.restype = st
+        L.rsd_comm_null_create.argtypes = [u32, u32, C.POINTER(vp)]
+        L.rsd_comm_release.restype = None
+        L.rsd_comm_release.argtypes = [vp]
+        L.rsd_comm_info.restype = st
+        L.rsd_comm_info.argtypes = [vp, C.POINTER(u32), C.POINTER(u32), C.POINTER(u32)]
+        L.rsd_comm_all_gather.restype = st
+        L.rsd_comm_all_gather.argtypes = [vp, vp, vp, C.c_uint64, vp]
+        L.rsd_comm_exchange.restype = st
+        L.rsd_comm_exchange.argtypes = [vp, C.POINTER(CommXfer), u32, C.POINTER(CommXfer), u32, vp]
+        L.rsd_band_frame_create.restype = st
+        L.rsd_band_frame_create.argtypes = [C.POINTER(FrameDesc), C.POINTER(BandParams), vp, C.POINTER(vp)]
+        L.rsd_band_frame_front.restype = st
+        L.rsd_band_frame_front.argtypes = [vp, C.POINTER(Camera), vp]
+        L.rsd_band_frame_back.restype = st
+        L.rsd_band_frame_back.argtypes = [vp, vp, vp]
+        L.rsd_band_frame_stats.restype = st
+        L.rsd_band_frame_stats.argtypes = [vp, C.POINTER(BandStats)]
+        L.rsd_band_frame_release.restype = None
+        L.rsd_band_frame_release.argtypes = [vp]
         L.rsd_svao_pass2_raytraced.restype = st
         L.rsd_svao_pass2_raytraced.argtypes = [vp, C.POINTER(Camera), C.POINTER(VAOData), C.POINTER(SVAOParams), vp, vp,
                                                u32, u32, vp, vp, u32, u32, u32, vp]

@@ -415,8 +415,13 @@ class Renderer:
     def _frame_desc(self):
         """The rsd_svao_frame_desc of this renderer's buffers (cached; rebuilt when the camera or the
         parameter structs are replaced, e.g. by set_pose)."""
-        key = (id(self.cam), id(self.svp), id(self.sdp), id(self.vao))
-        if getattr(self, "_desc_key", None) != key:
+        # the key holds the structs themselves (compared with `is`: a held object's id cannot be reused by a
+        # new one, as a freed Camera's could) and the buffers' device addresses (a reassigned tensor)
+        objs = (self.cam, self.svp, self.sdp, self.vao, self.gscene)
+        ptrs = tuple(t.data_ptr() for t in (self.depth, self.normals, self.ao, self.stencil, self.ray_minmax, self.sd))
+        key = getattr(self, "_desc_key", None)
+        if key is None or key[1] != ptrs or any(a is not b for a, b in zip(key[0], objs)):
+            key = (objs, ptrs)
             cfg = self.cfg
             p = lambda t: t.data_ptr()  # noqa: E731
             self._desc = abi.FrameDesc(self.gscene.h, C.addressof(self.cam), C.addressof(self.vao),

@@ -736,3 +736,219 @@ class HaloFrame:
             if self._ao_dst.numel():
                 b.ao.index_copy_(0, self._ao_dst, recv.view((-1,) + tuple(b.ao.shape[1:])).index_select(0, self._ao_src))
         self.frames += 1
+
+
+# ---- the native band frame (include/rsd.h rsd_comm_* / rsd_band_frame_*; csrc/band_frame.cpp) --------------
+
+class NativeHub:
+    """rsd_comm_hub: the rendezvous of in-process communicators (`world` host threads sharing one GPU)."""
+
+    def __init__(self, world: int):
+        import ctypes as C
+
+        from . import abi
+        self.h = C.c_void_p()
+        abi.check(abi.lib().rsd_comm_hub_create(world, C.byref(self.h)), "rsd_comm_hub_create")
+        self.world = world
+
+    def close(self):
+        from . import abi
+        if self.h:
+            abi.lib().rsd_comm_hub_release(self.h)
+            self.h = None
+
+
+class NativeComm:
+    """rsd_comm: the band frame's collectives in librsd -- RCCL (one process per GPU; ncclAllGather,
+    ncclSend / ncclRecv on the caller's stream) or in-process (threads of one process sharing a GPU)."""
+
+    def __init__(self, h):
+        import ctypes as C
+
+        from . import abi
+        self.h = h
+        k, r, w = C.c_uint32(), C.c_uint32(), C.c_uint32()
+        abi.check(abi.lib().rsd_comm_info(h, C.byref(k), C.byref(r), C.byref(w)), "rsd_comm_info")
+        self.kind, self.rank, self.world = k.value, r.value, w.value
+
+    @classmethod
+    def rccl(cls, rank: int, world: int, pg=None, device=None):
+        """An RCCL communicator over the ranks of torch.distributed's group: rank 0's id travels over the
+        group (a broadcast), then every rank joins (ncclCommInitRank on its current GPU)."""
+        import ctypes as C
+
+        import torch
+        import torch.distributed as dist
+
+        from . import abi
+        L = abi.lib()
+        uid = (C.c_uint8 * abi.COMM_UNIQUE_ID_BYTES)()
+        if rank == 0:
+            abi.check(L.rsd_comm_rccl_unique_id(uid), "rsd_comm_rccl_unique_id")
+        if world > 1:
+            on_gpu = dist.get_backend(pg) == "nccl"
+            t = torch.tensor(list(bytes(uid)), dtype=torch.uint8, device=device if on_gpu else "cpu")
+            dist.broadcast(t, src=0, group=pg)
+            uid = (C.c_uint8 * abi.COMM_UNIQUE_ID_BYTES)(*t.cpu().tolist())
+        h = C.c_void_p()
+        abi.check(L.rsd_comm_rccl_create(uid, world, rank, C.byref(h)), "rsd_comm_rccl_create")
+        return cls(h)
+
+    @classmethod
+    def local(cls, hub: NativeHub, rank: int):
+        import ctypes as C
+
+        from . import abi
+        h = C.c_void_p()
+        abi.check(abi.lib().rsd_comm_local_create(hub.h, rank, C.byref(h)), "rsd_comm_local_create")
+        return cls(h)
+
+    @classmethod
+    def null(cls, rank: int, world: int):
+        """A communicator that moves nothing (rsd_comm_null_create): host-cost probes of one rank's frame."""
+        import ctypes as C
+
+        from . import abi
+        h = C.c_void_p()
+        abi.check(abi.lib().rsd_comm_null_create(world, rank, C.byref(h)), "rsd_comm_null_create")
+        return cls(h)
+
+    def all_gather(self, out, inp, stream=None):
+        """out [world, *inp.shape] <- every rank's inp (device tensors), on torch's current stream."""
+        from . import abi
+        import torch
+        s = stream if stream is not None else torch.cuda.current_stream().cuda_stream
+        abi.check(abi.lib().rsd_comm_all_gather(self.h, inp.data_ptr(), out.data_ptr(),
+                                                inp.numel() * inp.element_size(), s), "rsd_comm_all_gather")
+
+    def exchange(self, sends, recvs, stream=None):
+        """Point-to-point: sends {peer: tensor}, recvs {peer: tensor} (sizes agreed beforehand)."""
+        from . import abi
+        import torch
+        s = stream if stream is not None else torch.cuda.current_stream().cuda_stream
+        xs = [abi.CommXfer(t.data_ptr(), t.numel() * t.element_size(), k, 0) for k, t in sends.items()]
+        xr = [abi.CommXfer(t.data_ptr(), t.numel() * t.element_size(), k, 0) for k, t in recvs.items()]
+        S = (abi.CommXfer * max(1, len(xs)))(*xs)
+        R = (abi.CommXfer * max(1, len(xr)))(*xr)
+        abi.check(abi.lib().rsd_comm_exchange(self.h, S, len(xs), R, len(xr), s), "rsd_comm_exchange")
+
+    def close(self):
+        from . import abi
+        if self.h:
+            abi.lib().rsd_comm_release(self.h)
+            self.h = None
+
+
+class NativeHaloFrame:
+    """HaloFrame's band split issued from C++ (rsd_band_frame): front() / back() are ONE librsd call each --
+    pass 1 of the rank's rows, the device compaction of the touched texels, the count all-gather and its
+    copy to the host (front); the count read, the interval triples' point-to-point transfer and merge, the
+    trace of the rank's SD share, the SD replies, pass 2 of its rows and the AO all-gather (back) -- with the
+    exchanges on `comm` (NativeComm: RCCL, or in-process threads).  Same kernels, same bits as HaloFrame
+    and as the 1-GPU frame; the re-balancing rule is HaloFrame._rebalanced's.  `backend` is a Renderer (or
+    a frame slot of one): its buffers are used in place, its current camera is passed on every front()."""
+
+    def __init__(self, backend, comm: NativeComm, throughput: bool = False, rebalance: bool = True,
+                 sd_split: str = "auto"):
+        import ctypes as C
+
+        from . import abi
+        self.b, self.comm = backend, comm
+        self.rank, self.world = comm.rank, comm.world
+        desc = abi.FrameDesc.from_buffer_copy(backend._frame_desc())
+        bp = abi.BandParams(int(backend.cfg.divisor), abi.SD_SPLITS[sd_split], int(bool(rebalance)),
+                            int(bool(throughput)))
+        self.h = C.c_void_p()
+        abi.check(abi.lib().rsd_band_frame_create(C.byref(desc), C.byref(bp), comm.h, C.byref(self.h)),
+                  "rsd_band_frame_create")
+        self.throughput = bool(throughput)
+        self._ev = (C.c_void_p * 2)()
+        self._L = abi.lib()
+
+    def front(self):
+        import ctypes as C
+        b = self.b
+        st = self._L.rsd_band_frame_front(self.h, C.byref(b.cam), b.stream)
+        if st:
+            from . import abi
+            abi.check(st, "rsd_band_frame_front")
+
+    def back(self, sd_events=None):
+        ev = None
+        if sd_events:
+            ev = self._ev
+            ev[0] = sd_events[0].h.value if sd_events[0] is not None else None
+            ev[1] = sd_events[1].h.value if sd_events[1] is not None else None
+        st = self._L.rsd_band_frame_back(self.h, ev, self.b.stream)
+        if st:
+            from . import abi
+            abi.check(st, "rsd_band_frame_back")
+
+    def frame(self, sd_events=None):
+        self.front()
+        self.back(sd_events)
+
+    def stats(self):
+        import ctypes as C
+
+        from . import abi
+        s = abi.BandStats()
+        abi.check(self._L.rsd_band_frame_stats(self.h, C.byref(s)), "rsd_band_frame_stats")
+        return s
+
+    # ---- HaloFrame's descriptive surface (bench.py, tests)
+    @property
+    def sd_split(self):
+        return "tiles" if self.stats().sd_split == 1 else "rows"
+
+    @property
+    def sd_band(self):
+        return (self.rank, self.world) if self.sd_split == "tiles" else None
+
+    @property
+    def gb(self):
+        s = self.stats()
+        return [int(x) for x in s.split[:s.world + 1]]
+
+    @property
+    def frames(self):
+        return int(self.stats().frames)
+
+    @property
+    def blocked_waits(self):
+        return int(self.stats().blocked_waits)
+
+    def owned_sd_rows(self):
+        s = self.stats()
+        if s.sd_split != 1:
+            return [(int(s.sd_row0), int(s.sd_row1))]
+        sdh = self.b.sd_h
+        return [(y, min(y + 8, sdh)) for y in range(8 * self.rank, sdh, 8 * self.world)]
+
+    def trace(self, consume=False, counters=False):
+        """The SD trace of this rank's share alone (rsd_sd_trace_band_ex / _rows): the instrumented traces
+        of bench.py's roofline."""
+        kw = {"throughput": True} if self.throughput else {}
+        if consume:
+            kw["consume"] = True
+        if counters:
+            kw["counters"] = True
+        if self.sd_band is not None:
+            return self.b.sd_trace(band=self.sd_band, **kw)
+        s = self.stats()
+        return self.b.sd_trace_rows((int(s.sd_row0), int(s.sd_row1)), **kw)
+
+    def bytes_per_frame(self):
+        s = self.stats()
+        n = max(1, int(s.frames))
+        return {"intervals": int(s.bytes_intervals) // n, "sd": int(s.bytes_sd) // n, "ao": int(s.bytes_ao) // n}
+
+    def dense_bytes_per_frame(self):
+        s = self.stats()
+        n = max(1, int(s.frames))
+        return {"intervals": int(s.dense_intervals), "sd": int(s.dense_sd), "ao": int(s.bytes_ao) // n}
+
+    def close(self):
+        if self.h:
+            self._L.rsd_band_frame_release(self.h)
+            self.h = None

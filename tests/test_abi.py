@@ -40,7 +40,7 @@ def test_library_exports_every_header_symbol(abi):
     exported = set(re.findall(r"\bT (rsd_\w+)", out))
     missing = [f for f in header_functions() if f not in exported]
     assert not missing, missing
-    assert abi.lib().rsd_abi_version() == 5
+    assert abi.lib().rsd_abi_version() == 6
 
 
 def test_struct_layouts_match_header(abi, tmp_path):
@@ -49,7 +49,8 @@ def test_struct_layouts_match_header(abi, tmp_path):
                "rsd_counters": abi.Counters, "rsd_texture": abi.Texture,
                "rsd_alpha_texture": abi.AlphaTexture, "rsd_material": abi.Material, "rsd_alpha_desc": abi.AlphaDesc,
                "rsd_svao_frame_desc": abi.FrameDesc, "rsd_halo_region": abi.HaloRegion,
-               "rsd_halo_list": abi.HaloList, "rsd_halo_sd_list": abi.HaloSdList}
+               "rsd_halo_list": abi.HaloList, "rsd_halo_sd_list": abi.HaloSdList, "rsd_comm_xfer": abi.CommXfer,
+               "rsd_band_params": abi.BandParams, "rsd_band_stats": abi.BandStats}
     src = "#include <stdio.h>\n#include \"rsd_graph.h\"\nint main(void){\n"
     for name in structs:
         src += f'printf("%zu\\n", sizeof({name}));\n'
@@ -67,6 +68,26 @@ def test_device_open_without_gpu_is_an_error_not_a_crash(abi):
     h = C.c_void_p()
     st = abi.lib().rsd_device_open(0, C.byref(h))
     assert st == 5 and b"no HIP device" in abi.lib().rsd_last_error()
+
+
+def test_comm_and_band_frame_arguments_are_checked(abi):
+    """The band frame's C ABI refuses bad arguments with a status and a message, without a GPU."""
+    L = abi.lib()
+    hub = C.c_void_p()
+    assert L.rsd_comm_hub_create(0, C.byref(hub)) == 1 and b"world" in L.rsd_last_error()
+    assert L.rsd_comm_hub_create(2, C.byref(hub)) == 0 and hub.value
+    comm = C.c_void_p()
+    assert L.rsd_comm_local_create(hub, 2, C.byref(comm)) == 1 and b"rank >= world" in L.rsd_last_error()
+    assert L.rsd_comm_rccl_create(None, 1, 0, C.byref(comm)) == 1
+    assert L.rsd_comm_all_gather(None, None, None, 0, None) == 1 and b"null communicator" in L.rsd_last_error()
+    assert L.rsd_comm_exchange(None, None, 0, None, 0, None) == 1
+    assert L.rsd_band_frame_create(None, None, None, C.byref(comm)) == 1
+    assert L.rsd_band_frame_front(None, None, None) == 1 and b"null frame" in L.rsd_last_error()
+    assert L.rsd_band_frame_back(None, None, None) == 1
+    assert L.rsd_band_frame_stats(None, None) == 1
+    L.rsd_band_frame_release(None)
+    L.rsd_comm_release(None)
+    L.rsd_comm_hub_release(hub)
 
 
 def test_invalid_arguments_are_reported(abi):

@@ -168,3 +168,54 @@ def test_exact_numerics_still_bit_identical(oracle):
     assert not np.array_equal(gf["ray_min"], ge["ray_min"]), "the fast kernels ran the exact arithmetic"
     fa.close()
     ex.close()
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("kernel,primary", [("vao", 0), ("hbao", 0), ("vao", 1), ("hbao", 1)])
+def test_fast_numerics_degenerate_inputs(oracle, kernel, primary):
+    """The fast build assumes no NaN operands (-fno-honor-nans): inputs that produce NaN / inf
+    inside the SVAO arithmetic must still give AO within the tolerance of the exact oracle frame.  The
+    G-buffer gets patches of background depth exactly at farZ, zero depth (a pixel at the camera: posV = 0,
+    zero-length view vectors), +inf, NaN and negative depth; with DualDepth the second layer is left at its
+    zero initialisation (Common.slang:285-330 Init / finalize; :498-505 evalDualVisibility)."""
+    import dataclasses
+
+    import torch
+    from rsd.frame import Renderer
+    from rsd.scenes import make_scene
+    from helpers import small_frame_config
+    cfg = dataclasses.replace(small_frame_config(visible=(320, 192)), numerics="fast", ao_kernel=kernel,
+                              primary=primary)
+    scene = make_scene("arcade_tiny")
+    r = Renderer(scene, cfg)
+    r.gbuffer()
+    g0 = cfg.guard_band
+    d = r.depth
+    d[g0 + 20:g0 + 40, g0 + 30:g0 + 90] = cfg.far                 # background at exactly farZ
+    d[g0 + 60:g0 + 70, g0 + 120:g0 + 170] = 0.0                    # at the camera
+    d[g0 + 90:g0 + 100, g0 + 20:g0 + 40] = float("inf")
+    d[g0 + 110:g0 + 112, g0 + 200:g0 + 260] = float("nan")
+    d[g0 + 130:g0 + 140, g0 + 60:g0 + 80] = -1.0
+    torch.cuda.synchronize()
+    r.clear_intervals()
+    r.pass1()
+    r.sd_trace()
+    r.pass2()
+    g = r.numpy()
+    d2 = np.zeros_like(g["depth"]) if primary == 1 else None
+    cam, vao = to_oracle(r.cam, oracle.Camera), to_oracle(r.vao, oracle.VAOData)
+    sdp, svp = to_oracle(r.sdp, oracle.SDParams), to_oracle(r.svp, oracle.SVAOParams)
+    osc = oracle.Scene(scene.positions, scene.indices, scene.flags, scene.alpha)
+    ao1, st, rmin, rmax = oracle.svao_pass1(cam, vao, svp, g["depth"], g["normals"], r.sd_w, r.sd_h, depth2=d2)
+    sd, _ = oracle.sd_trace(osc, cam, sdp, g["depth"], rmin, rmax, r.sd_w, r.sd_h)
+    ao = oracle.svao_pass2(cam, vao, svp, g["depth"], g["normals"], st, sd, ao1, depth2=d2)
+    gv = slice(cfg.guard_band, cfg.fb_h - cfg.guard_band), slice(cfg.guard_band, cfg.fb_w - cfg.guard_band)
+    s = _ao_stats(g["ao"], ao, gv)
+    bad = ~np.isfinite(g["depth"][gv]) | (g["depth"][gv] <= 0.0) | (g["depth"][gv] >= cfg.far)
+    dp = np.abs(g["ao"][gv].astype(np.int32) - ao[gv].astype(np.int32))[bad]
+    _report(f"degenerate_{kernel}_p{primary}", frame_ao=s, degenerate_px=int(bad.sum()),
+            degenerate_px_max_diff=int(dp.max()), degenerate_px_exact=float((dp == 0).mean()))
+    assert bad.sum() > 2000
+    _check_ao(s, ("degenerate inputs", kernel, primary))
+    assert int(dp.max()) <= AO_P2, ("the degenerate pixels themselves", int(dp.max()))
+    r.close()

@@ -3,7 +3,9 @@
 with the collectives stubbed out (as tools/scaling_model.py's host measurement), under cProfile, and
 the per-call host time of each librsd entry / torch op it issues.
 
-usage: python tools/halo_host_profile.py [config] [--world 8] [--rank 3] [--frames 100]"""
+usage: python tools/halo_host_profile.py [config] [--world 8] [--rank 3] [--frames 100]
+
+The last section times the native band frame (rsd_band_frame) of the same rank over the null communicator."""
 import cProfile
 import io
 import pstats
@@ -68,3 +70,28 @@ for rebalance in (False, True):
     s = io.StringIO()
     pstats.Stats(pr, stream=s).sort_stats("tottime").print_stats(30)
     print(s.getvalue())
+
+# ---- the native band frame (rsd_band_frame): front() + back() are one librsd call each; the null communicator
+#      (rsd_comm_null_create) stands in for RCCL, so this is librsd's host issue of one rank's frame
+from rsd.shard import NativeComm, NativeHaloFrame  # noqa: E402
+
+for rebalance in (False, True):
+    comm = NativeComm.null(rank, world)
+    f = NativeHaloFrame(r, comm, rebalance=rebalance)
+    for _ in range(5):
+        f.front()
+        f.back()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    tf = 0.0
+    for _ in range(frames):
+        a = time.perf_counter()
+        f.front()
+        tf += time.perf_counter() - a
+        f.back()
+    host = (time.perf_counter() - t0) / frames * 1e6
+    torch.cuda.synchronize()
+    print(f"native rebalance={rebalance}: host {host:.1f} us per frame (front {tf / frames * 1e6:.1f} + back; "
+          f"collectives stubbed), blocked waits {f.blocked_waits} of {f.frames}")
+    f.close()
+    comm.close()
