@@ -480,10 +480,10 @@ def hit_order_record(r, frame_cls, new_ev, steps, warmup, pose, rays, rays_activ
 
 def latency_floor(cnts, trace_ms):
     """Latency roofline of the SD walk: the slowest ray is a chain of
-    max_steps_per_ray dependent row-steps (LDS pop -> node / leaf fetch -> box or triangle tests ->
-    row merge -> push); its floor is max_steps x the mean step time measured by the instrumented
-    walk under the same load (rsd_counters.step_*_clocks over row_steps, s_memtime converted with
-    the launch's measured clock).  latency_frac = floor / the trace's HIP-event duration (setup +
+    max_steps_per_ray dependent steps (row walk: LDS pop -> node / leaf fetch -> box or triangle tests
+    -> row merge -> push; quad walk: one iteration of the ray's quad, fetch -> tests -> stack); its
+    floor is max_steps x the mean step time measured by the instrumented walk under the same load
+    (rsd_counters.step_*_clocks over row_steps, s_memtime converted with the launch's measured clock).  latency_frac = floor / the trace's HIP-event duration (setup +
     walk): near 1 means the trace lasts as long as its slowest ray's dependency chain."""
     import numpy as np
     c = [x for x in cnts if x.row_steps and x.shader_clock_mhz > 0]
@@ -500,8 +500,10 @@ def latency_floor(cnts, trace_ms):
             "latency_floor_fetch_only_us": round(ms * fetch, 2),
             "step_us": {"fetch": round(fetch, 3), "tests_merge": round(comp, 3), "pool": round(pool, 3)},
             "max_steps_per_ray": int(ms), "shader_clock_mhz": round(mhz, 1),
-            "latency_note": "floor = max_steps_per_ray x mean row-step time of the instrumented walk "
-                            "(fetch wait + tests/merge + LDS pool); latency_frac = floor / trace duration"}
+            "latency_note": "floor = max_steps_per_ray x mean step time of the instrumented walk (row walk: one row "
+                            "step = fetch wait + tests/merge + LDS pool; quad walk, maps above 0.6 M texels: one quad "
+                            "iteration = own fetch wait + own tests and the wave's other branch + stack); "
+                            "latency_frac = floor / trace duration"}
 
 
 def pmc_traffic(csv_paths, kernel_substrs):

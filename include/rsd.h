@@ -527,11 +527,14 @@ rsd_status rsd_comm_exchange(rsd_comm* comm, const rsd_comm_xfer* sends, uint32_
  *          point-to-point transfer of the triples -> atomic min / max merge (the exact 1-GPU interval
  *          union on the rank's SD share) -> the SD trace of its share (round-robin 8-row tiles, or the SD
  *          rows under its band: rsd_band_params.sd_split) -> the depths of exactly the texels each peer
- *          sent come back to it -> "AO 2" of its rows -> an all-gather of the AO bands into d_ao.
+ *          sent come back to it -> "AO 2" of its rows -> its AO band to every other rank, theirs into d_ao
+ *          (point-to-point, image to image).
  * Every SD texel and AO pixel is produced by exactly one rank with the same kernels: each rank's AO
  * image and its own SD share are bit-identical to the 1-GPU frame (rsd_svao_frame), whatever the split.
- * The split of the 32-row groups is re-balanced every second frame from the ranks' measured pass-1 +
- * trace + pass-2 times (same decision on every rank).  The frame description's buffers are used in
+ * The split of the 32-row groups is re-balanced every fourth frame from the ranks' measured pass-1 +
+ * trace + pass-2 times (same decision on every rank).  The count matrix reaches the host through pinned
+ * memory written by a kernel (a sequence word the host polls): front and back of a frame must be issued on
+ * the same stream.  The frame description's buffers are used in
  * place; its camera / params structs are copied (rsd_band_frame_front may pass a new camera).
  * StochasticDepth mode with RayInterval only (the north_star's path). */
 #define RSD_SD_SPLIT_AUTO 0u   /* tiles for reduced-resolution SD maps (divisor > 1), rows at full resolution */
@@ -560,12 +563,15 @@ typedef struct {
     uint64_t frames;            /* back() calls */
     uint64_t blocked_waits;     /* back() calls whose counts had not reached the host yet */
     uint64_t resplits;          /* applied re-splits */
-    uint64_t bytes_intervals;   /* bytes sent so far: interval triples, SD replies, AO bands */
+    uint64_t bytes_intervals;   /* bytes sent so far: interval triples, SD replies, AO band (to every peer) */
     uint64_t bytes_sd;
     uint64_t bytes_ao;
     uint64_t dense_intervals;   /* what the dense halo (whole candidate regions) would send per frame */
     uint64_t dense_sd;
     uint64_t growth_syncs;      /* exchange buffers grown (each waits for this stream once) */
+    uint64_t host_front_ns;     /* host time inside rsd_band_frame_front / _back so far (issue cost), and the */
+    uint64_t host_back_ns;      /*   part of _back spent waiting for the count matrix (0 with frames in flight */
+    uint64_t host_wait_ns;      /*   once the counts are long complete) */
 } rsd_band_stats;
 rsd_status rsd_band_frame_stats(const rsd_band_frame* bf, rsd_band_stats* out);
 void rsd_band_frame_release(rsd_band_frame* bf); /* waits for the frame's stream work to finish */

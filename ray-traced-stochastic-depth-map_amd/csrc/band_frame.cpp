@@ -14,8 +14,11 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <cmath>
 #include <cstring>
+#include <thread>
 #include <string>
 #include <vector>
 
@@ -112,11 +115,10 @@ struct Region {
 class BandFrame {
 public:
     ~BandFrame() {
-        for (DevBuf* b : {&cand_all_, &row_, &mdev_, &ao_send_, &ao_recv_}) b->release();
+        for (DevBuf* b : {&cand_all_, &row_, &mdev_}) b->release();
         for (auto* v : {&recv_tr_, &sd_send_, &sd_recv_})
             for (DevBuf& b : *v) b.release();
         if (mhost_) (void)hipHostFree(mhost_);
-        if (cnt_ev_) (void)hipEventDestroy(cnt_ev_);
         for (auto& set : ev_)
             for (hipEvent_t& e : set)
                 if (e) (void)hipEventDestroy(e);
@@ -159,17 +161,30 @@ private:
     std::vector<rsd_halo_region> regions_;       // compaction regions (peers with a candidate region)
     std::vector<uint32_t> region_peer_;
     std::vector<DevBuf> recv_tr_, sd_send_, sd_recv_;
-    DevBuf row_, mdev_, ao_send_, ao_recv_;
-    int64_t* mhost_ = nullptr;
-    hipEvent_t cnt_ev_ = nullptr;
+    DevBuf row_, mdev_;         // two count rows (frames alternate), the all-gathered matrix
+    int64_t* mhost_ = nullptr;  // pinned: [0] sequence number, then the matrix (publish_counts)
+    int64_t* mhost_dev_ = nullptr;
+    int64_t seq_ = 0;
     hipEvent_t ev_[2][6] = {};
     uint32_t evn_ = 0;
     bool prev_valid_ = false;
     uint32_t prev_set_ = 0;
+    // timed_: this frame records the six timing events -- only the frames whose cost a re-split reads (every
+    // fourth: frames 4j + 3; the back() of frames 4j decides from them), 1.5 event records per frame on average
+    bool timed_ = false;
     bool open_ = false;
     hipStream_t last_ = nullptr;
     // statistics
     uint64_t frames_ = 0, blocked_ = 0, resplits_ = 0, b_iv_ = 0, b_sd_ = 0, b_ao_ = 0, growth_ = 0;
+    uint64_t ns_front_ = 0, ns_back_ = 0, ns_wait_ = 0;
+
+public:
+    static uint64_t now_ns() {
+        return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+                   std::chrono::steady_clock::now().time_since_epoch()).count();
+    }
+    void add_front_ns(uint64_t ns) { ns_front_ += ns; }
+    void add_back_ns(uint64_t ns) { ns_back_ += ns; }
 };
 
 rsd_status BandFrame::init(const rsd_svao_frame_desc& f, const rsd_band_params& bp, Comm* comm) {
@@ -224,16 +239,16 @@ rsd_status BandFrame::init(const rsd_svao_frame_desc& f, const rsd_band_params& 
     gb_.resize(world_ + 1);
     for (uint32_t r = 0; r <= world_; ++r) gb_[r] = (uint32_t)((uint64_t)G_ * r / world_);
     ao_row_bytes_ = (size_t)f.width * (svp_.dual_ao ? 2u : 1u);
-    RSD_HIP(hipEventCreateWithFlags(&cnt_ev_, hipEventDisableTiming));
     for (auto& set : ev_)
         for (hipEvent_t& e : set) RSD_HIP(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
-    RSD_HIP(hipHostMalloc((void**)&mhost_, sizeof(int64_t) * world_ * (world_ + 1), hipHostMallocDefault));
-    std::memset(mhost_, 0, sizeof(int64_t) * world_ * (world_ + 1));
+    RSD_HIP(hipHostMalloc((void**)&mhost_, sizeof(int64_t) * (1 + world_ * (world_ + 1)), hipHostMallocDefault));
+    std::memset(mhost_, 0, sizeof(int64_t) * (1 + world_ * (world_ + 1)));
+    RSD_HIP(hipHostGetDevicePointer((void**)&mhost_dev_, mhost_, 0));
     recv_tr_.resize(world_);
     sd_send_.resize(world_);
     sd_recv_.resize(world_);
-    RSD_HIP(hipMalloc(&row_.p, sizeof(int64_t) * (world_ + 1)));
-    row_.cap = sizeof(int64_t) * (world_ + 1);
+    RSD_HIP(hipMalloc(&row_.p, 2 * sizeof(int64_t) * (world_ + 1)));
+    row_.cap = 2 * sizeof(int64_t) * (world_ + 1);
     RSD_HIP(hipMalloc(&mdev_.p, sizeof(int64_t) * world_ * (world_ + 1)));
     mdev_.cap = sizeof(int64_t) * world_ * (world_ + 1);
     RSD_HIP(hipMemset(row_.p, 0, row_.cap));
@@ -306,9 +321,6 @@ rsd_status BandFrame::plan(hipStream_t s) {
         ao_rows_[r] = {g + px_rows_[r].first, std::min(fbh, g + px_rows_[r].second)};
         ao_max_ = std::max(ao_max_, ao_rows_[r].second - ao_rows_[r].first);
     }
-    rsd_status st = ao_recv_.ensure((size_t)world_ * ao_max_ * ao_row_bytes_, s, &growth_);
-    if (st == RSD_OK) st = ao_send_.ensure((size_t)ao_max_ * ao_row_bytes_, s, &growth_);
-    if (st != RSD_OK) return st;
     // the compaction's output: one allocation, each peer's candidate capacity in interleaved triples
     cand_off_.assign(world_, 0);
     size_t total = 0;
@@ -316,7 +328,7 @@ rsd_status BandFrame::plan(hipStream_t s) {
         cand_off_[k] = total;
         if (iv_send_[k].valid) total += 3 * iv_send_[k].texels;
     }
-    st = cand_all_.ensure(std::max<size_t>(total, 1) * sizeof(int32_t), s, &growth_);
+    rsd_status st = cand_all_.ensure(std::max<size_t>(total, 1) * sizeof(int32_t), s, &growth_);
     if (st != RSD_OK) return st;
     regions_.clear();
     region_peer_.clear();
@@ -338,7 +350,7 @@ rsd_status BandFrame::plan(hipStream_t s) {
 }
 
 rsd_status BandFrame::mark(hipStream_t s) {
-    if (!rebalance_) return RSD_OK;
+    if (!timed_) return RSD_OK;
     const uint32_t set = (evn_ / 6) % 2, i = evn_ % 6;
     ++evn_;
     RSD_HIP(hipEventRecord(ev_[set][i], s));
@@ -350,8 +362,7 @@ rsd_status BandFrame::mark(hipStream_t s) {
 int64_t BandFrame::prev_cost_us() const {
     if (!rebalance_ || !prev_valid_) return -1;
     const hipEvent_t* e = ev_[prev_set_];
-    for (int i = 1; i < 6; i += 2)
-        if (hipEventQuery(e[i]) != hipSuccess) return -1;
+    if (hipEventQuery(e[5]) != hipSuccess) return -1;  // the last of the six (one stream: the others came first)
     double us = 0.0;
     for (int i = 0; i < 6; i += 2) {
         float ms = 0.0f;
@@ -416,21 +427,29 @@ rsd_status BandFrame::front(const rsd_camera* cam, hipStream_t s) {
         st = rsd_svao_clear_intervals(f_.d_ray_min, f_.d_ray_max, f_.sd_w * f_.sd_h, s);
         if (st != RSD_OK) return st;
     }
-    const int64_t prev_us = prev_cost_us();
+    // the cost entry of the count row: this object's last timed frame, read by the back() of frames 4j
+    const int64_t prev_us = frames_ % 4 == 0 ? prev_cost_us() : -1;
+    timed_ = rebalance_ && frames_ % 4 == 3;
     if ((st = mark(s)) != RSD_OK) return st;
     st = rsd_svao_pass1_rows(&cam_, &vao_, &svp_, f_.d_depth, f_.d_normals, f_.width, f_.height, f_.d_ao, f_.d_stencil,
                              f_.d_ray_min, f_.d_ray_max, f_.sd_w, f_.sd_h, px_rows_[me_].first, px_rows_[me_].second, s);
     if (st != RSD_OK) return st;
     if ((st = mark(s)) != RSD_OK) return st;
-    // every peer's touched texels as interleaved triples, their counts in row[k] (row[me] stays 0) and
-    // this object's previous compute time in row[world], in two launches
+    // every peer's touched texels as interleaved triples, their counts in this frame's count row (row[me]
+    // stays 0; the previous frame's compaction zeroed it) and this object's last compute time in row[world],
+    // one launch, which also zeroes the other row for the next frame
+    int64_t* rows = static_cast<int64_t*>(row_.p);
+    int64_t* row = rows + (frames_ % 2) * (world_ + 1);
+    int64_t* other = rows + ((frames_ + 1) % 2) * (world_ + 1);
+    for (size_t i = 0; i < regions_.size(); ++i) regions_[i].count = row + region_peer_[i];
     st = halo_compact_impl(f_.d_ray_min, f_.d_ray_max, f_.sd_w, f_.sd_h, regions_.data(), (uint32_t)regions_.size(),
-                           true, static_cast<int64_t*>(row_.p), world_, prev_us, s);
+                           true, row, world_, prev_us, s, true, other);
     if (st != RSD_OK) return st;
-    st = comm_->all_gather(row_.p, mdev_.p, sizeof(int64_t) * (world_ + 1), s);
+    st = comm_->all_gather(row, mdev_.p, sizeof(int64_t) * (world_ + 1), s);
     if (st != RSD_OK) return st;
-    RSD_HIP(hipMemcpyAsync(mhost_, mdev_.p, sizeof(int64_t) * world_ * (world_ + 1), hipMemcpyDeviceToHost, s));
-    RSD_HIP(hipEventRecord(cnt_ev_, s));
+    // the matrix to the host, with a sequence number the host polls in back() (no copy engine, no event)
+    st = publish_counts(static_cast<const int64_t*>(mdev_.p), mhost_dev_, world_ * (world_ + 1), ++seq_, s);
+    if (st != RSD_OK) return st;
     open_ = true;
     return RSD_OK;
 }
@@ -444,12 +463,26 @@ rsd_status BandFrame::back(void* const* events, hipStream_t s) {
     last_ = s;
     const uint32_t W = world_, me = me_;
     // the counts of THIS frame on the host (with frames in flight: long complete)
-    if (hipEventQuery(cnt_ev_) != hipSuccess) ++blocked_;
-    RSD_HIP(hipEventSynchronize(cnt_ev_));
-    std::vector<int64_t> M(mhost_, mhost_ + (size_t)W * (W + 1));
+    volatile const int64_t* pub = mhost_;
+    if (pub[0] != seq_) {
+        ++blocked_;
+        const uint64_t w0 = now_ns();
+        for (uint64_t spin = 0; pub[0] != seq_; ++spin) {
+            if (spin > 64) std::this_thread::yield();
+            if ((spin & 1023u) == 1023u && now_ns() - w0 > 60000000000ull) {
+                set_error("rsd_band_frame_back: the count matrix did not arrive within 60 s (a failed kernel or "
+                          "collective on this stream?)");
+                return RSD_ERR_HIP;
+            }
+        }
+        ns_wait_ += now_ns() - w0;
+    }
+    std::atomic_thread_fence(std::memory_order_acquire);
+    std::vector<int64_t> M((size_t)W * (W + 1));
+    for (size_t i = 0; i < M.size(); ++i) M[i] = pub[1 + i];
     auto cnt = [&](uint32_t from, uint32_t to) { return (uint64_t)std::max<int64_t>(0, M[(size_t)from * (W + 1) + to]); };
     // re-split on every second frame (every rank sees the same counts: all skip or all re-split)
-    if (rebalance_ && frames_ % 2 == 0) {
+    if (rebalance_ && frames_ % 4 == 0) {
         std::vector<double> costs(W);
         bool ok = true;
         for (uint32_t k = 0; k < W; ++k) {
@@ -539,31 +572,28 @@ rsd_status BandFrame::back(void* const* events, hipStream_t s) {
                              f_.sd_w, f_.sd_h, f_.d_ao, px_rows_[me].first, px_rows_[me].second, s);
     if (st != RSD_OK) return st;
     if ((st = mark(s)) != RSD_OK) return st;
-    if (rebalance_) {
+    if (timed_) {
         prev_set_ = ((evn_ - 1) / 6) % 2;
         prev_valid_ = true;
     }
-    // AO bands: one all-gather of ao_max rows per rank (sent in place when the band's padded rows lie in
-    // the image), then every other band's rows into the image in one launch
+    // AO bands: every rank's rows straight from its image into every other rank's image (point-to-point:
+    // each xGMI link carries one band; no gather buffer, no unpack launch)
     uint8_t* ao = f_.d_ao;
-    const size_t band = (size_t)ao_max_ * ao_row_bytes_;
     const auto mine = ao_rows_[me];
-    const void* send = ao + (size_t)mine.first * ao_row_bytes_;
-    if (mine.first + ao_max_ > f_.height) {
-        const CopySeg pack{send, ao_send_.p, (size_t)(mine.second - mine.first) * ao_row_bytes_};
-        if ((st = copy_segments(&pack, 1, s)) != RSD_OK) return st;
-        send = ao_send_.p;
+    const uint64_t mineBytes = (uint64_t)(mine.second - mine.first) * ao_row_bytes_;
+    sends.clear();
+    recvs.clear();
+    for (uint32_t k = 0; k < W; ++k) {
+        if (k == me) continue;
+        if (mineBytes) sends.push_back({ao + (size_t)mine.first * ao_row_bytes_, mineBytes, k});
+        const uint64_t kb = (uint64_t)(ao_rows_[k].second - ao_rows_[k].first) * ao_row_bytes_;
+        if (kb) recvs.push_back({ao + (size_t)ao_rows_[k].first * ao_row_bytes_, kb, k});
     }
-    if ((st = comm_->all_gather(send, ao_recv_.p, band, s)) != RSD_OK) return st;
-    b_ao_ += band;
-    std::vector<CopySeg> unpack;
-    for (uint32_t k = 0; k < W; ++k)
-        if (k != me && ao_rows_[k].second > ao_rows_[k].first)
-            unpack.push_back({static_cast<const uint8_t*>(ao_recv_.p) + k * band, ao + (size_t)ao_rows_[k].first * ao_row_bytes_,
-                              (size_t)(ao_rows_[k].second - ao_rows_[k].first) * ao_row_bytes_});
-    for (size_t i = 0; i < unpack.size(); i += kMaxCopySegs)
-        if ((st = copy_segments(unpack.data() + i, (uint32_t)std::min<size_t>(kMaxCopySegs, unpack.size() - i), s)) != RSD_OK)
+    if (!sends.empty() || !recvs.empty()) {
+        if ((st = comm_->exchange(sends.data(), (uint32_t)sends.size(), recvs.data(), (uint32_t)recvs.size(), s)) != RSD_OK)
             return st;
+    }
+    b_ao_ += mineBytes * (W - 1);
     ++frames_;
     return RSD_OK;
 }
@@ -590,6 +620,9 @@ void BandFrame::stats(rsd_band_stats& o) const {
         if (iv_recv_[k].valid) o.dense_sd += iv_recv_[k].rows * sd_row;
     }
     o.growth_syncs = growth_;
+    o.host_front_ns = ns_front_;
+    o.host_back_ns = ns_back_;
+    o.host_wait_ns = ns_wait_;
 }
 
 }  // namespace rsd
@@ -621,7 +654,10 @@ extern "C" rsd_status rsd_band_frame_front(rsd_band_frame* bf, const rsd_camera*
         set_error("rsd_band_frame_front: null frame");
         return RSD_ERR_INVALID_ARG;
     }
-    return bf->impl->front(cam, (hipStream_t)stream);
+    const uint64_t t0 = BandFrame::now_ns();
+    const rsd_status st = bf->impl->front(cam, (hipStream_t)stream);
+    bf->impl->add_front_ns(BandFrame::now_ns() - t0);
+    return st;
 }
 
 extern "C" rsd_status rsd_band_frame_back(rsd_band_frame* bf, void* const* events, rsd_stream stream) {
@@ -629,7 +665,10 @@ extern "C" rsd_status rsd_band_frame_back(rsd_band_frame* bf, void* const* event
         set_error("rsd_band_frame_back: null frame");
         return RSD_ERR_INVALID_ARG;
     }
-    return bf->impl->back(events, (hipStream_t)stream);
+    const uint64_t t0 = BandFrame::now_ns();
+    const rsd_status st = bf->impl->back(events, (hipStream_t)stream);
+    bf->impl->add_back_ns(BandFrame::now_ns() - t0);
+    return st;
 }
 
 extern "C" rsd_status rsd_band_frame_stats(const rsd_band_frame* bf, rsd_band_stats* out) {

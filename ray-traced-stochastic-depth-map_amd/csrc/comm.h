@@ -46,7 +46,8 @@ struct CopySeg {
     void* dst;
     uint64_t bytes;
 };
-rsd_status copy_segments(const CopySeg* segs, uint32_t n, hipStream_t s);
+// zero (optional): zero_n 64-bit words set to 0 by the same launch (a side job, e.g. the band frame's count row)
+rsd_status copy_segments(const CopySeg* segs, uint32_t n, hipStream_t s, uint64_t* zero = nullptr, uint32_t zero_n = 0);
 constexpr uint32_t kMaxCopySegs = 16;
 
 }  // namespace rsd

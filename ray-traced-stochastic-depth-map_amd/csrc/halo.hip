@@ -37,6 +37,9 @@ struct HaloRegions {
     long long* row;                   // optional count row: row[0, rowN) zeroed, row[rowN] = extra
     uint32_t rowN;
     long long extra;
+    uint32_t extraInCompact;          // 1: the counts are already zero; the compaction writes row[rowN] = extra
+    long long* zeroRow;               // optional: a second row [0, rowN] cleared in the same launch (the next
+                                      // frame's, double-buffered count rows of the band frame)
 };
 
 __global__ void halo_zero_kernel(HaloRegions R) {
@@ -45,12 +48,16 @@ __global__ void halo_zero_kernel(HaloRegions R) {
         for (uint32_t i = threadIdx.x; i < R.rowN; i += blockDim.x) R.row[i] = 0;
         if (threadIdx.x == 0) R.row[R.rowN] = R.extra;
     }
+    if (R.zeroRow)
+        for (uint32_t i = threadIdx.x; i <= R.rowN; i += blockDim.x) R.zeroRow[i] = 0;
 }
 
 __global__ void __launch_bounds__(kHaloBlock) halo_compact_kernel(const uint32_t* __restrict__ rmin,
                                                                    const uint32_t* __restrict__ rmax, uint32_t sdW,
                                                                    HaloRegions R) {
     const uint32_t g = blockIdx.x * kHaloBlock + threadIdx.x;
+    if (R.extraInCompact && g == 0u) R.row[R.rowN] = R.extra;
+    if (R.zeroRow && g <= R.rowN) R.zeroRow[g] = 0;
     bool in = g < R.first[R.n];
     uint32_t r = 0;
     while (in && g >= R.first[r + 1]) ++r;
@@ -157,9 +164,12 @@ struct CopySegs {
     uint8_t* dst[kMaxCopySegs];
     uint64_t bytes[kMaxCopySegs];
     uint32_t vec[kMaxCopySegs];        // 1: 16-B items
+    unsigned long long* zero;          // optional: zero[0, zeroN) set to 0 by the first lanes (a side job)
+    uint32_t zeroN;
 };
 
 __global__ void __launch_bounds__(kHaloBlock) copy_segments_kernel(CopySegs S) {
+    if (S.zero && blockIdx.x == 0 && threadIdx.x < S.zeroN) S.zero[threadIdx.x] = 0ull;
     const uint64_t total = S.first[S.n];
     for (uint64_t g = (uint64_t)blockIdx.x * kHaloBlock + threadIdx.x; g < total;
          g += (uint64_t)gridDim.x * kHaloBlock) {
@@ -171,14 +181,33 @@ __global__ void __launch_bounds__(kHaloBlock) copy_segments_kernel(CopySegs S) {
     }
 }
 
+// The band frame's count matrix to the host without a copy engine or an event: one wave writes the n values
+// to host-visible (pinned, fine-grained) memory after the sequence word's slot, each lane's stores released
+// at system scope, then the sequence number with a system-scope release store -- the host polls that word.
+__global__ void __launch_bounds__(64) publish_kernel(const long long* __restrict__ src, long long* dst, uint32_t n,
+                                                      long long seq) {
+    for (uint32_t i = threadIdx.x; i < n; i += 64u) dst[1u + i] = src[i];
+    __threadfence_system();
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(&dst[0], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 }  // namespace
 
-rsd_status copy_segments(const CopySeg* segs, uint32_t n, hipStream_t s) {
-    if (n > kMaxCopySegs) {
-        set_error("copy_segments: more than 16 segments");
+rsd_status publish_counts(const int64_t* d_src, int64_t* dst_host_dev, uint32_t n, int64_t seq, hipStream_t s) {
+    hipLaunchKernelGGL(publish_kernel, dim3(1), dim3(64), 0, s, reinterpret_cast<const long long*>(d_src),
+                       reinterpret_cast<long long*>(dst_host_dev), n, (long long)seq);
+    return launch_check("publish_kernel launch");
+}
+
+rsd_status copy_segments(const CopySeg* segs, uint32_t n, hipStream_t s, uint64_t* zero, uint32_t zero_n) {
+    if (n > kMaxCopySegs || zero_n > kHaloBlock) {
+        set_error("copy_segments: more than 16 segments or 256 words to zero");
         return RSD_ERR_INVALID_ARG;
     }
     CopySegs S{};
+    S.zero = reinterpret_cast<unsigned long long*>(zero);
+    S.zeroN = zero ? zero_n : 0u;
     uint64_t total = 0;
     for (uint32_t i = 0; i < n; ++i) {
         const uintptr_t a = reinterpret_cast<uintptr_t>(segs[i].src) | reinterpret_cast<uintptr_t>(segs[i].dst) |
@@ -192,8 +221,8 @@ rsd_status copy_segments(const CopySeg* segs, uint32_t n, hipStream_t s) {
         if (segs[i].bytes) ++S.n;
     }
     S.first[S.n] = total;
-    if (total == 0) return RSD_OK;
-    const uint64_t blocks = std::min<uint64_t>((total + kHaloBlock - 1) / kHaloBlock, 4096u);
+    if (total == 0 && S.zeroN == 0) return RSD_OK;
+    const uint64_t blocks = std::max<uint64_t>(1u, std::min<uint64_t>((total + kHaloBlock - 1) / kHaloBlock, 4096u));
     hipLaunchKernelGGL(copy_segments_kernel, dim3((uint32_t)blocks), dim3(kHaloBlock), 0, s, S);
     return launch_check("copy_segments_kernel launch");
 }
@@ -203,7 +232,7 @@ rsd_status copy_segments(const CopySeg* segs, uint32_t n, hipStream_t s) {
 // row[rowN] = extra in the same launch that zeroes the counts (the counts may point into it).
 rsd_status halo_compact_impl(const uint32_t* d_ray_min, const uint32_t* d_ray_max, uint32_t sd_w, uint32_t sd_h,
                              const rsd_halo_region* regions, uint32_t n_regions, bool ilv, int64_t* row,
-                             uint32_t row_n, int64_t extra, hipStream_t s) {
+                             uint32_t row_n, int64_t extra, hipStream_t s, bool zeroed, int64_t* zero_row) {
     if (!d_ray_min || !d_ray_max || (n_regions && !regions) || n_regions > kMaxRegions || row_n > 64u) {
         set_error("rsd_halo_compact: null buffer or more than 64 regions");
         return RSD_ERR_INVALID_ARG;
@@ -214,6 +243,7 @@ rsd_status halo_compact_impl(const uint32_t* d_ray_min, const uint32_t* d_ray_ma
     R.row = reinterpret_cast<long long*>(row);
     R.rowN = row_n;
     R.extra = (long long)extra;
+    R.zeroRow = reinterpret_cast<long long*>(zero_row);
     uint32_t total = 0;
     for (uint32_t r = 0; r < n_regions; ++r) {
         const rsd_halo_region& g = regions[r];
@@ -239,6 +269,12 @@ rsd_status halo_compact_impl(const uint32_t* d_ray_min, const uint32_t* d_ray_ma
     }
     R.first[n_regions] = total;
     if (n_regions == 0 && !row) return RSD_OK;
+    if (zeroed && row && total > 0) {  // the caller zeroed the counts: the compaction alone, writing row[row_n]
+        R.extraInCompact = 1u;
+        hipLaunchKernelGGL(halo_compact_kernel, dim3((total + kHaloBlock - 1) / kHaloBlock), dim3(kHaloBlock), 0, s,
+                           d_ray_min, d_ray_max, sd_w, R);
+        return launch_check("halo_compact_kernel launch");
+    }
     // the counts (and the count row) start at zero (one launch for all regions), then one compaction launch
     hipLaunchKernelGGL(halo_zero_kernel, dim3(1), dim3(64), 0, s, R);
     if (total == 0) return launch_check("halo_zero_kernel launch");
@@ -317,7 +353,7 @@ extern "C" rsd_status rsd_halo_compact(const uint32_t* d_ray_min, const uint32_t
                                        uint32_t sd_h, const rsd_halo_region* regions, uint32_t n_regions,
                                        rsd_stream stream) {
     return halo_compact_impl(d_ray_min, d_ray_max, sd_w, sd_h, regions, n_regions, false, nullptr, 0u, 0,
-                             (hipStream_t)stream);
+                             (hipStream_t)stream, false, nullptr);
 }
 
 extern "C" rsd_status rsd_halo_merge(uint32_t* d_ray_min, uint32_t* d_ray_max, uint32_t sd_w, uint32_t sd_h,

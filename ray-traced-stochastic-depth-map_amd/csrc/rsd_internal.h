@@ -95,10 +95,16 @@ rsd_status hip_fail(hipError_t e, const char* what);
 // halo.hip: the sparse-halo steps with the band frame's options (csrc/band_frame.cpp).  ilv: interleaved
 // triples {texel, rayMin, rayMax} (a peer's prefix is one contiguous transfer); the SD lists then index
 // with stride 3 (their idx points at the triples).  row: a count row zeroed ([0, row_n)) with
-// row[row_n] = extra in the launch that zeroes the region counts.
+// row[row_n] = extra in the launch that zeroes the region counts; zeroed: the counts are already zero
+// (the previous frame's compaction cleared them through zero_row), so the compaction launch alone writes
+// row[row_n] and clears zero_row[0, row_n].
 rsd_status halo_compact_impl(const uint32_t* d_ray_min, const uint32_t* d_ray_max, uint32_t sd_w, uint32_t sd_h,
                              const rsd_halo_region* regions, uint32_t n_regions, bool ilv, int64_t* row,
-                             uint32_t row_n, int64_t extra, hipStream_t s);
+                             uint32_t row_n, int64_t extra, hipStream_t s, bool zeroed = false,
+                             int64_t* zero_row = nullptr);
+// the band frame's count matrix (n int64) to host-visible memory dst[1..n], then dst[0] = seq (system-scope
+// release): the host polls dst[0] instead of waiting on an event
+rsd_status publish_counts(const int64_t* d_src, int64_t* dst_host_dev, uint32_t n, int64_t seq, hipStream_t s);
 rsd_status halo_merge_impl(uint32_t* d_ray_min, uint32_t* d_ray_max, uint32_t sd_w, uint32_t sd_h,
                            const rsd_halo_list* lists, uint32_t n_lists, uint32_t ray_interval, bool ilv,
                            hipStream_t s);

@@ -92,6 +92,10 @@ struct SDArgs {
     // partition, the others to its back, so the expensive rays are dequeued first
     uint32_t lpt;
     float lptLen;
+    // spread (row and quad walks): the static first rays of the persistent waves are dealt row-major over
+    // the partition's waves (queue index i -> wave i % waves, row i / waves), so the longest-first rays land
+    // one per wave instead of eight to a wave; 0: wave-major (index i -> wave i / rows, row i % rows)
+    uint32_t spread;
     // segment entry grid (entry_grid.h, canonical walks): the setup kernel looks up the frontier of
     // each live ray's segment and copies its items to entQ[slot * kEntryCap ..]
     uint32_t entOn;
@@ -353,14 +357,26 @@ __device__ __forceinline__ void quad_cx(float& k, uint32_t& it, bool low) {
     it = takeOther ? oi : it;
 }
 
+// Step clocks of the instrumented quad walk (rsd_counters.step_*; the latency floor of bench.py): per
+// step of a ray -- one iteration of its quad's loop -- the wait for the step's own fetch (the
+// instrumented build waits right after issuing it), its own box / triangle tests and merge, the stack
+// push / pop from the point where the quad's branches reconverge, and the whole iteration from loop top
+// to loop top (the remainder is the other branch of the wave: divergence).  s_memtime is wave-uniform;
+// every quad's lane 0 accumulates its own ray's steps.
+struct QuadClk {
+    unsigned long long fetch = 0, tests = 0, stack = 0, total = 0, steps = 0;
+};
+
 template <int K>
 __device__ __forceinline__ int trace_knearest_quad(const float4* __restrict__ bvh, uint32_t triOff, const RayCtx& r,
                                                    float tmin, float tmax, uint32_t cull, bool useLB, float lbT,
                                                    uint32_t lbP, KList<K>& kl, uint32_t* __restrict__ sItem,
                                                    float* __restrict__ sT, int q, int quadBase, TraceStats& st,
-                                                   const uint32_t* __restrict__ ent, uint32_t nEnt) {
+                                                   const uint32_t* __restrict__ ent, uint32_t nEnt,
+                                                   QuadClk* clk = nullptr) {
     kl.clear();
     int sp = 0, found = 0;
+    unsigned long long tTop = clk ? __builtin_amdgcn_s_memtime() : 0ull, tA = 0ull, tF = 0ull;
     uint32_t item = 0;
     if (nEnt) {
         // the segment's entry-grid frontier (entry_grid.h): item 0 first, the rest on the stack
@@ -378,15 +394,26 @@ __device__ __forceinline__ int trace_knearest_quad(const float4* __restrict__ bv
     while (true) {
         const uint32_t off = item & kOffMask;
         uint32_t next = kNoItem;
+        if (clk) tA = __builtin_amdgcn_s_memtime();
         if (item & kLeafBit) {
             st.leaves++;
             const uint32_t cnt = ((item >> 29) & 3u) + 1u;
             bool acc = false;
             float t = 0.0f;
             uint32_t prim = 0u;
+            float4 va = make_float4(0.0f, 0.0f, 0.0f, 0.0f), vb = va, vc = va;
             if ((uint32_t)q < cnt) {
                 const float4* tp = bvh + off + 3u * (uint32_t)q;
-                const float4 va = tp[0], vb = tp[1], vc = tp[2];
+                va = tp[0];
+                vb = tp[1];
+                vc = tp[2];
+            }
+            if (clk) {  // the step's fetch (the instrumented build waits here)
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                tF = __builtin_amdgcn_s_memtime();
+                if (q == 0) clk->fetch += tF - tA;
+            }
+            if ((uint32_t)q < cnt) {
                 st.tris++;
                 float bu, bv, det;
                 if (intersect_tri(r, va, vb, vc, t, bu, bv, det) && t >= tmin && t <= tmax) {
@@ -407,6 +434,7 @@ __device__ __forceinline__ int trace_knearest_quad(const float4* __restrict__ bv
                     found = found < K ? found + 1 : K;
                 }
             }
+            if (clk && q == 0) clk->tests += __builtin_amdgcn_s_memtime() - tF;
         } else {
             st.nodes++;
             const float thi = fminf(tmax, kl.t[K - 1]);
@@ -414,6 +442,11 @@ __device__ __forceinline__ int trace_knearest_quad(const float4* __restrict__ bv
             const float lox = nb[q], hix = nb[4 + q], loy = nb[8 + q], hiy = nb[12 + q], loz = nb[16 + q],
                         hiz = nb[20 + q];
             const uint32_t ref = __float_as_uint(nb[24 + q]), cnt = __float_as_uint(nb[28 + q]);
+            if (clk) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                tF = __builtin_amdgcn_s_memtime();
+                if (q == 0) clk->fetch += tF - tA;
+            }
             float tn;
             const bool hit = ref != kNoItem && box_hit(r, lox, hix, loy, hiy, loz, hiz, tlo, thi, tn);
             float k = hit ? tn : INFINITY;
@@ -431,6 +464,7 @@ __device__ __forceinline__ int trace_knearest_quad(const float4* __restrict__ bv
                 it = takeOther ? oi : it;
             }
             next = qbcu<0>(it);
+            if (clk && q == 0) clk->tests += __builtin_amdgcn_s_memtime() - tF;
             if (q >= 1 && q < m) {
                 const int slot = sp + (m - 1 - q);  // farthest deepest
                 sItem[slot * kQuadRays] = it;
@@ -438,6 +472,7 @@ __device__ __forceinline__ int trace_knearest_quad(const float4* __restrict__ bv
             }
             sp += m > 0 ? m - 1 : 0;
         }
+        if (clk) tA = __builtin_amdgcn_s_memtime();  // the branches reconverged
         if (next == kNoItem) {
             const float thi = fminf(tmax, kl.t[K - 1]);
             while (sp > 0) {
@@ -445,8 +480,18 @@ __device__ __forceinline__ int trace_knearest_quad(const float4* __restrict__ bv
                 const float tt = sT[sp * kQuadRays];
                 if (tt <= thi) { next = sItem[sp * kQuadRays]; break; }
             }
-            if (next == kNoItem) break;
         }
+        if (clk) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            const unsigned long long t = __builtin_amdgcn_s_memtime();
+            if (q == 0) {
+                clk->stack += t - tA;
+                clk->total += t - tTop;
+                clk->steps++;
+            }
+            tTop = t;
+        }
+        if (next == kNoItem) break;
         item = next;
     }
     return found;
@@ -458,7 +503,7 @@ template <int K, int N, bool SPEC = false>
 __device__ __forceinline__ void sd_resolve(const SDArgs& a, f3 d, float TMin, float TMax, float cosT, float (&depths)[N],
                                            uint32_t* sItem, float* sT, int q, int quadBase, TraceStats& st,
                                            uint32_t& hitsDelivered, const uint32_t* ent = nullptr,
-                                           uint32_t nEnt = 0u) {
+                                           uint32_t nEnt = 0u, QuadClk* clk = nullptr) {
     const rsd_camera& c = a.cam;
     RayCtx r;
     ray_setup(r, mk(c.posW[0], c.posW[1], c.posW[2]), d);
@@ -471,7 +516,7 @@ __device__ __forceinline__ void sd_resolve(const SDArgs& a, f3 d, float TMin, fl
     while (!commit) {
         // SPEC (as the row walk's): one chunk of K keys decides the texel -- no lower bound, no alpha test
         const int found = trace_knearest_quad<K>(a.nodes, a.triOff, r, TMin, TMax, a.cull, SPEC ? false : useLB, lbT, lbP, kl, sItem,
-                                                 sT, q, quadBase, st, ent, nEnt);
+                                                 sT, q, quadBase, st, ent, nEnt, SPEC ? nullptr : clk);
         // barycentrics + hash of hit j are computed by lane j % 4 (re-running the identical
         // triangle test on the hit's record), then shared with the quad
         float rngL[J], zL[J];
@@ -677,7 +722,7 @@ __global__ void __launch_bounds__(kSetupWaves * kBlock) sd_setup_kernel(SDArgs a
 // The first chunk of each wave is static (blockIdx); later ones come from one atomic head
 // that starts after the static range, so a wave with no static chunk exits without an
 // atomic (one head word serialises ~90 dequeues/us, MI355X_MICROARCH.md "dequeue").
-template <int K, int N, bool SPEC = false>
+template <int K, int N, bool SPEC = false, bool CNT = false>
 __global__ void __launch_bounds__(kBlock) sd_trace_queue_kernel(SDArgs a, const float4* __restrict__ queue,
                                                                 uint32_t* __restrict__ qctl) {
     __shared__ uint32_t sItem[kQuadStack * kQuadRays];
@@ -692,9 +737,21 @@ __global__ void __launch_bounds__(kBlock) sd_trace_queue_kernel(SDArgs a, const 
     TraceStats st{0u, 0u, 0u};
     uint32_t active = 0, hitsDelivered = 0, maxNodes = 0, maxSteps = 0;
     unsigned long long sumCycles = 0, maxCycles = 0;
+    // instrumented traces (counters): the step clocks of every ray (QuadClk) and the clock calibration of
+    // the first wave (s_memtime ticks against the 100 MHz s_memrealtime), as the row walk's
+    QuadClk clk;
+    unsigned long long cal0 = 0, calR0 = 0;
+    if (CNT && blockIdx.x == 0) {
+        cal0 = __builtin_amdgcn_s_memtime();
+        calR0 = __builtin_amdgcn_s_memrealtime();
+    }
     uint32_t base = (blockIdx.x / kQueueParts) * (uint32_t)kQuadRays;
-    while (base < count) {
-        const uint32_t qi = base + (uint32_t)quad;
+    bool firstChunk = true;
+    while (base < count || (firstChunk && a.spread)) {
+        // the static first chunk (spread: quad q of the partition's wave w takes index q * waves + w)
+        const uint32_t qi = firstChunk && a.spread ? (uint32_t)quad * wavesPerPart + blockIdx.x / kQueueParts
+                                                   : base + (uint32_t)quad;
+        firstChunk = false;
         if (qi < count) {
             f3 d;
             float TMin, TMax, cosT;
@@ -709,7 +766,8 @@ __global__ void __launch_bounds__(kBlock) sd_trace_queue_kernel(SDArgs a, const 
             const uint32_t n0 = st.nodes, l0 = st.leaves;
             const unsigned long long c0 = a.counters ? __builtin_amdgcn_s_memtime() : 0ull;
             sd_resolve<K, N, SPEC>(a, d, TMin, TMax, cosT, depths, &sItem[quad], &sT[quad], q, quadBase, st,
-                             hitsDelivered, a.entOn ? a.entQ + (size_t)slot * kEntryCap : nullptr, nEnt);
+                             hitsDelivered, a.entOn ? a.entQ + (size_t)slot * kEntryCap : nullptr, nEnt,
+                             CNT ? &clk : nullptr);
             if (q == 0) {
                 if (a.counters) {
                     const unsigned long long dc = __builtin_amdgcn_s_memtime() - c0;
@@ -737,6 +795,18 @@ __global__ void __launch_bounds__(kBlock) sd_trace_queue_kernel(SDArgs a, const 
         atomicAdd(&a.counters[7], sumCycles);
         atomicMax(&a.counters[8], maxCycles);
         atomicAdd(&a.counters[9], (unsigned long long)(q == 0 ? st.leaves : 0u));
+        if (CNT && q == 0) {  // step clocks (rsd_counters.step_*): compute = own tests + the other branch
+            atomicAdd(&a.counters[14], clk.steps);
+            atomicAdd(&a.counters[16], clk.fetch);
+            atomicAdd(&a.counters[17], clk.total - clk.fetch - clk.stack);
+            atomicAdd(&a.counters[18], clk.stack);
+            atomicAdd(&a.counters[24], clk.tests);
+        }
+        if (CNT && blockIdx.x == 0 && lane == 0) {
+            const unsigned long long cal1 = __builtin_amdgcn_s_memtime(), calR1 = __builtin_amdgcn_s_memrealtime();
+            atomicMax(&a.counters[21], cal1 - cal0);
+            atomicMax(&a.counters[22], calR1 - calR0);
+        }
     }
 }
 
@@ -856,8 +926,12 @@ __global__ void __launch_bounds__(kBlock) sd_trace_ordered_kernel(SDArgs a, cons
     TraceStats st{0u, 0u, 0u};
     uint32_t active = 0, delivered = 0, maxNodes = 0, maxSteps = 0;
     uint32_t base = (blockIdx.x / kQueueParts) * (uint32_t)kQuadRays;
-    while (base < count) {
-        const uint32_t qi = base + (uint32_t)quad;
+    bool firstChunk = true;
+    while (base < count || (firstChunk && a.spread)) {
+        // the static first chunk (spread: quad q of the partition's wave w takes index q * waves + w)
+        const uint32_t qi = firstChunk && a.spread ? (uint32_t)quad * wavesPerPart + blockIdx.x / kQueueParts
+                                                   : base + (uint32_t)quad;
+        firstChunk = false;
         if (qi < count) {
             f3 d;
             float TMin, TMax, cosT;
@@ -1265,8 +1339,9 @@ __global__ void __launch_bounds__(kBlock) sd_trace_row_kernel(SDArgs a, const fl
         const bool fetching = phase == kFetch;
         if (phase == kFetch) {
             uint32_t qi;
-            if (first) {
-                qi = (blockIdx.x / kQueueParts) * (uint32_t)kRowRays + (uint32_t)row;  // static first ray
+            if (first) {  // the static first ray
+                qi = a.spread ? (uint32_t)row * wavesPerPart + blockIdx.x / kQueueParts
+                              : (blockIdx.x / kQueueParts) * (uint32_t)kRowRays + (uint32_t)row;
                 first = false;
             } else {
                 uint32_t h = 0;
@@ -1740,7 +1815,8 @@ static hipError_t launch_sd_kn(const SDArgs& a, dim3 grid, uint32_t persistentBl
         const char* specEnv = std::getenv("RSD_TRACE_SPEC");
         const bool spec = !(specEnv && std::string(specEnv) == "off") && !a.alphaTest && a.impl != 1u &&
                           a.impl != 3u && a.maxCount <= (uint32_t)K && !a.counters;
-        if (spec) hipLaunchKernelGGL((sd_trace_queue_kernel<K, N, true>), dim3(persistentBlocks), dim3(kBlock), 0, s, a, queue, qctl);
+        if (a.counters) hipLaunchKernelGGL((sd_trace_queue_kernel<K, N, false, true>), dim3(persistentBlocks), dim3(kBlock), 0, s, a, queue, qctl);
+        else if (spec) hipLaunchKernelGGL((sd_trace_queue_kernel<K, N, true>), dim3(persistentBlocks), dim3(kBlock), 0, s, a, queue, qctl);
         else hipLaunchKernelGGL((sd_trace_queue_kernel<K, N>), dim3(persistentBlocks), dim3(kBlock), 0, s, a, queue, qctl);
     }
     return hipGetLastError();
@@ -1967,6 +2043,11 @@ rsd_status sd_trace_impl(rsd_scene* scene, const rsd_camera* cam, const rsd_sd_p
     a.raster = 0u;
     a.lpt = 0u;
     a.lptLen = 0.0f;
+    {
+        // RSD_TRACE_SPREAD=on: the static first rays dealt row-major over the waves (SDArgs.spread; A/B)
+        const char* spreadEnv = std::getenv("RSD_TRACE_SPREAD");
+        a.spread = spreadEnv && std::string(spreadEnv) == "on" ? 1u : 0u;
+    }
     a.primRec = scene->d_prim_rec;
     a.entOn = 0u;
     a.entSlots = static_cast<const uint4*>(scene->d_entry);

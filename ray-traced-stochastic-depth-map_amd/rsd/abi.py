@@ -138,7 +138,8 @@ class BandStats(C.Structure):  # rsd_band_stats
                 ("halo_px", C.c_uint32), ("frames", C.c_uint64), ("blocked_waits", C.c_uint64),
                 ("resplits", C.c_uint64), ("bytes_intervals", C.c_uint64), ("bytes_sd", C.c_uint64),
                 ("bytes_ao", C.c_uint64), ("dense_intervals", C.c_uint64), ("dense_sd", C.c_uint64),
-                ("growth_syncs", C.c_uint64)]
+                ("growth_syncs", C.c_uint64), ("host_front_ns", C.c_uint64), ("host_back_ns", C.c_uint64),
+                ("host_wait_ns", C.c_uint64)]
 
 
 FRAME_INTERVALS_CLEAR = 4  # rsd.h RSD_FRAME_INTERVALS_CLEAR

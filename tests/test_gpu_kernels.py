@@ -141,6 +141,6 @@ def test_raytraced_refuses_bad_modes(oracle):
         r.pass2_raytraced()
     assert e.value.status == abi.ERR_INVALID_ARG
     svp.ao_kernel, svp.primary_depth_mode, svp.d_depth2 = 0, 1, None
-    with pytest.raises(abi.RsdError, match="DualDepth needs"):
+    with pytest.raises(abi.RsdError, match="d_depth2"):
         r.pass2_raytraced()
     r.close()

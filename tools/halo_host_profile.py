@@ -72,26 +72,47 @@ for rebalance in (False, True):
     print(s.getvalue())
 
 # ---- the native band frame (rsd_band_frame): front() + back() are one librsd call each; the null communicator
-#      (rsd_comm_null_create) stands in for RCCL, so this is librsd's host issue of one rank's frame
+#      (rsd_comm_null_create) stands in for RCCL, so this is librsd's host issue of one rank's frame.  Four frame
+#      slots in flight (back() of frame i after front() of frames i+1..i+3, as bench.py), so the count matrix a
+#      back() reads is normally complete; the stats split the host time into front, back and the count wait.
 from rsd.shard import NativeComm, NativeHaloFrame  # noqa: E402
 
+F = 4
 for rebalance in (False, True):
     comm = NativeComm.null(rank, world)
-    f = NativeHaloFrame(r, comm, rebalance=rebalance)
-    for _ in range(5):
-        f.front()
-        f.back()
+    rends = [r] + [r.frame_slot() for _ in range(F - 1)]
+    streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(F - 1)]
+    fs = [NativeHaloFrame(x, comm, rebalance=rebalance, throughput=True) for x in rends]
+
+    def run(n):
+        pending = []
+        for i in range(n):
+            with torch.cuda.stream(streams[i % F]):
+                fs[i % F].front()
+            pending.append(i)
+            if len(pending) > F - 1:
+                j = pending.pop(0)
+                with torch.cuda.stream(streams[j % F]):
+                    fs[j % F].back()
+        while pending:
+            j = pending.pop(0)
+            with torch.cuda.stream(streams[j % F]):
+                fs[j % F].back()
+
+    run(8)
     torch.cuda.synchronize()
+    s0 = [f.stats() for f in fs]
     t0 = time.perf_counter()
-    tf = 0.0
-    for _ in range(frames):
-        a = time.perf_counter()
-        f.front()
-        tf += time.perf_counter() - a
-        f.back()
+    run(frames)
     host = (time.perf_counter() - t0) / frames * 1e6
     torch.cuda.synchronize()
-    print(f"native rebalance={rebalance}: host {host:.1f} us per frame (front {tf / frames * 1e6:.1f} + back; "
-          f"collectives stubbed), blocked waits {f.blocked_waits} of {f.frames}")
-    f.close()
+    wall = (time.perf_counter() - t0) / frames * 1e6
+    s1 = [f.stats() for f in fs]
+    d = lambda k: sum(getattr(b, k) - getattr(a, k) for a, b in zip(s0, s1)) / frames / 1e3  # noqa: E731
+    blocked = sum(b.blocked_waits - a.blocked_waits for a, b in zip(s0, s1))
+    print(f"native rebalance={rebalance}: host {host:.1f} us per frame (Python loop), librsd front {d('host_front_ns'):.1f}"
+          f" + back {d('host_back_ns'):.1f} us (of which count wait {d('host_wait_ns'):.1f} us, {blocked} of {frames} "
+          f"back() calls blocked), wall {wall:.1f} us per frame; collectives stubbed, world {world} rank {rank}")
+    for f in fs:
+        f.close()
     comm.close()

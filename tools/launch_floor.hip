@@ -70,9 +70,17 @@ int main() {
     const double gle = per_call_us(s, [&] { (void)hipGetLastError(); });
     int dev = 0;
     const double gd = per_call_us(s, [&] { (void)hipGetDevice(&dev); });
+    // the band frame's count matrix to the host: an async copy into pinned memory vs a kernel writing it
+    long long* dsrc = nullptr;
+    long long* hpin = nullptr;
+    CHECK(hipMalloc(&dsrc, 9 * 8 * 8));
+    CHECK(hipHostMalloc((void**)&hpin, 9 * 8 * 8, hipHostMallocDefault));
+    const double d2h = per_call_us(s, [&] { (void)hipMemcpyAsync(hpin, dsrc, 9 * 8 * 8, hipMemcpyDeviceToHost, s); });
+    const double mset = per_call_us(s, [&] { (void)hipMemsetAsync(dsrc, 0, 9 * 8 * 8, s); });
     CHECK(hipStreamSynchronize(s));
     std::printf("{\"launch_us_args64\": %.2f, \"launch_us_args2048\": %.2f, \"event_record_us\": %.2f, "
-                "\"event_record_timing_us\": %.2f, \"get_last_error_us\": %.3f, \"get_device_us\": %.3f}\n",
-                small, big, rec, rect, gle, gd);
+                "\"event_record_timing_us\": %.2f, \"get_last_error_us\": %.3f, \"get_device_us\": %.3f, "
+                "\"memcpy_d2h_pinned_576B_us\": %.2f, \"memset_576B_us\": %.2f}\n",
+                small, big, rec, rect, gle, gd, d2h, mset);
     return 0;
 }
