@@ -57,8 +57,8 @@ for p in (str(ROOT), str(PKG)):
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8 TB/s (spec)
 DEFAULT_CONFIG = "suntemple_1080p_q"
 # committed rocprofv3 passes of the default bench (newest round first)
-PROFILE_DIRS = [ROOT / "profiles" / "round4", ROOT / "profiles" / "round3", ROOT / "profiles" / "round2",
-                ROOT / "profiles" / "round1"]
+PROFILE_DIRS = [ROOT / "profiles" / "round5", ROOT / "profiles" / "round4", ROOT / "profiles" / "round3",
+                ROOT / "profiles" / "round2", ROOT / "profiles" / "round1"]
 
 
 def parse():
@@ -173,7 +173,16 @@ def main():
     # N > 1 band frames issued from C++ (rsd_band_frame) over librsd's own RCCL communicators -- one per frame
     # slot, so every communicator's operations stay on one stream; the gloo rehearsal keeps HaloFrame
     native = shard == "band" and world > 1 and backend == "nccl" and args.frame_impl == "native"
-    comms = [NativeComm.rccl(rank, world, device=torch.device("cuda", local)) for _ in range(F)] if native else []
+    comms = []
+    if native:
+        try:
+            comms = [NativeComm.rccl(rank, world, device=torch.device("cuda", local)) for _ in range(F)]
+        except Exception as e:  # noqa: BLE001 -- librccl unusable here: the torch.distributed path, said on stderr
+            print(f"bench.py: librsd's RCCL communicator failed ({e}); falling back to rsd/shard.py HaloFrame",
+                  file=sys.stderr)
+            for c in comms:
+                c.close()
+            comms, native = [], False
 
     def make_frame(rend, throughput=False, slot=0):
         if shard == "band":

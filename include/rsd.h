@@ -204,6 +204,11 @@ typedef enum { RSD_NUMERICS_FAST = 0, RSD_NUMERICS_EXACT = 1 } rsd_numerics;
  * words, a 16-byte list header (two list counts: frames alternate between them, so no pass resets the
  * list on the device) and T list entries (8 T + 16 bytes; ABI v4 had T bytes). */
 uint32_t rsd_svao_tile_count(uint32_t width, uint32_t height, uint32_t guard_band);
+/* librsd keeps one generation counter per tile_flags buffer on the host (pass 1 / pass 2 alternate the list
+ * counts by it; pass 1 stamps a busy tile's flag with it, so a flag a pass 2 did not consume -- a pass 1
+ * whose rows no pass 2 covered -- never keeps its tile out of a later list).  An owner that frees the buffer
+ * calls this, so a new buffer at the same address starts from a fresh counter (with its zeroed memory). */
+void rsd_svao_tile_flags_release(const void* tile_flags);
 
 /* Traversal counters of the last instrumented trace (roofline bytes) */
 typedef struct {

@@ -427,6 +427,7 @@ public:
             // consumes; sized by the guard band of this frame, zeroed once per allocation
             const uint32_t n = rsd_svao_tile_count(width_, height_, (uint32_t)guard);
             if (n != flagsN_) {
+                rsd_svao_tile_flags_release(flags_);  // librsd's generation state of the old buffer
                 (void)hipFree(flags_);
                 flags_ = nullptr;
                 flagsN_ = 0;
@@ -472,7 +473,10 @@ public:
                              (uint8_t*)ao->ptr, ctx.stream),
               "SVAO AO 2");
     }
-    ~SVAOPass() override { (void)hipFree(flags_); }
+    ~SVAOPass() override {
+        rsd_svao_tile_flags_release(flags_);
+        (void)hipFree(flags_);
+    }
     RenderGraph* stochasticDepthGraph() { return sdGraph_.get(); }
 
 private:

@@ -2230,7 +2230,7 @@ rsd_status sd_trace_impl(rsd_scene* scene, const rsd_camera* cam, const rsd_sd_p
     // persistent waves: 8 per CU.  At 1080p/4 every row gets one of the ~22 K live rays in its
     // static first slot and the launch lasts as long as the slowest ray; 16 waves per CU (the
     // split walk holds < 128 VGPRs) measured no faster (tools/sd_time.py sweep)
-    static const char* wpcEnv = std::getenv("RSD_TRACE_WAVES_PER_CU");  // experiments only
+    const char* wpcEnv = std::getenv("RSD_TRACE_WAVES_PER_CU");  // experiments only (read per call: A/B runs)
     const uint32_t wavesPerCu = wpcEnv ? (uint32_t)std::max(1, std::atoi(wpcEnv)) : 8u;
     const uint32_t pb = ((uint32_t)std::max(1, scene->dev->cu_count) * wavesPerCu + kQueueParts - 1) / kQueueParts *
                         kQueueParts;

@@ -167,7 +167,7 @@ struct TileGen {
     bool appended = false;  // a pass 1 ran since the last pass 2
 };
 std::mutex g_tile_mutex;
-std::vector<std::pair<const void*, TileGen>> g_tile_gen;
+std::vector<std::pair<const void*, TileGen>> g_tile_gen;  // per buffer; rsd_svao_tile_flags_release forgets one
 
 TileGen& tile_gen_locked(const void* buf) {
     for (auto& e : g_tile_gen)
@@ -176,11 +176,14 @@ TileGen& tile_gen_locked(const void* buf) {
     return g_tile_gen.back().second;
 }
 
-uint32_t tile_gen_pass1(const void* buf) {
+// the list count pass 1 appends to (gen & 1) and its flag stamp (gen + 1, never 0)
+uint32_t tile_gen_pass1(const void* buf, uint32_t* stamp) {
+    *stamp = 1u;
     if (!buf) return 0u;
     std::lock_guard<std::mutex> lock(g_tile_mutex);
     TileGen& t = tile_gen_locked(buf);
     t.appended = true;
+    *stamp = t.gen % 0xfffffffeu + 1u;
     return t.gen & 1u;
 }
 
@@ -196,6 +199,16 @@ uint32_t tile_gen_pass2(const void* buf) {
     return g;
 }
 }  // namespace
+
+extern "C" void rsd_svao_tile_flags_release(const void* tile_flags) {
+    if (!tile_flags) return;
+    std::lock_guard<std::mutex> lock(g_tile_mutex);
+    for (size_t i = 0; i < g_tile_gen.size(); ++i)
+        if (g_tile_gen[i].first == tile_flags) {
+            g_tile_gen.erase(g_tile_gen.begin() + (long)i);
+            return;
+        }
+}
 
 extern "C" uint32_t rsd_svao_tile_count(uint32_t width, uint32_t height, uint32_t guard_band) {
     if (2 * guard_band >= width || 2 * guard_band >= height) return 0u;
@@ -280,7 +293,11 @@ rsd_status pass1_impl(const rsd_camera* cam, const rsd_vao_data* vao, const rsd_
     a.bandIndex = start;
     a.bandCount = step;
     if (bandGroups == 0) return RSD_OK;
-    a.tileGen = tile_gen_pass1(a.tileFlags);
+    a.tileGen = tile_gen_pass1(a.tileFlags, &a.tileStamp);
+    {
+        const char* xcdEnv = std::getenv("RSD_PASS1_XCD");  // A/B runs: workgroup chunks per XCD (0: off)
+        a.xcdChunk = xcdEnv ? (uint32_t)std::max(0, std::atoi(xcdEnv)) : 0u;
+    }
     // the specialised kernel for the StochasticDepth frame (every BASELINE config); RSD_PASS1=generic
     // forces the generic one (A/B runs)
     const char* p1Env = std::getenv("RSD_PASS1");

@@ -104,7 +104,17 @@ __device__ __forceinline__ void pass1_dir_generic(const SvaoArgs& a, float u, fl
 // ND > 0: NUM_DIRECTIONS known at compile time (the specialised kernel); 0: a.k.nd
 template <bool SPEC, int ND>
 __global__ void __launch_bounds__(256) svao_pass1_kernel(SvaoArgs a) {
-    const uint32_t bx = blockIdx.x, by = blockIdx.y;
+    uint32_t bx = blockIdx.x, by = blockIdx.y;
+    if (a.xcdChunk) {  // chunks of C workgroups dealt round-robin to the 8 XCD groups (bijective on the full chunks)
+        const uint32_t C = a.xcdChunk, gx = gridDim.x, n = gx * gridDim.y, L = by * gx + bx;
+        const uint32_t full = n / (8u * C) * (8u * C);
+        if (L < full) {
+            const uint32_t xcd = L % 8u, j = L / 8u;
+            const uint32_t T = ((j / C) * 8u + xcd) * C + j % C;
+            bx = T % gx;
+            by = T / gx;
+        }
+    }
     const uint32_t ox = (bx / 2u) * 32u + 2u * threadIdx.x + (bx % 2u);
     const uint32_t oy = ((by / 2u) * a.bandCount + a.bandIndex) * 32u + 2u * threadIdx.y + (by % 2u);
     const uint32_t px = ox + a.guard, py = oy + a.guard;
@@ -176,7 +186,8 @@ __global__ void __launch_bounds__(256) svao_pass1_kernel(SvaoArgs a) {
         if ((lane == 0u && mL) || (lane == 8u && mR)) {
             // the first wave to flag a tile appends it to the busy-tile list pass 2 walks
             const uint32_t t = (oy / kTileEdge) * a.tilesX + ox / kTileEdge;
-            if (atomicExch(&a.tileFlags[t], 1u) == 0u) a.tileList[atomicAdd(a.tileCount + a.tileGen, 1u)] = t;
+            if (atomicExch(&a.tileFlags[t], a.tileStamp) != a.tileStamp)
+                a.tileList[atomicAdd(a.tileCount + a.tileGen, 1u)] = t;
         }
         // the other list count (read by the previous frame's pass 2, earlier on this stream) starts the
         // next frame's list at zero: no workgroup of pass 2 has to reset anything (svao.hip tile_gen)

@@ -63,8 +63,14 @@ struct SvaoArgs {
     uint32_t* tileFlags;  // rsd_svao_params.tile_flags: one word per busy 16x16 tile (tile_layout), or nullptr
     uint32_t* tileCount;  // the two list counts (after the flags): frame generations alternate between them
     uint32_t tileGen;     // 0 / 1: the count this pass appends to (pass 1) or walks (pass 2), svao.hip tile_gen
+    uint32_t tileStamp;   // pass 1: the value it stores in a busy tile's flag (the generation + 1, never 0): a flag
+                          // left set by an earlier generation no pass 2 consumed does not keep its tile out of
+                          // this generation's list
     uint32_t* tileList;   // busy tiles in the order pass 1 found them (after the count)
     uint32_t tilesX;      // tiles per row of tileFlags
+    uint32_t xcdChunk;   // pass 1 (A/B, RSD_PASS1_XCD): > 0 deals chunks of this many workgroups to the XCDs
+                         // (workgroups b and b + 8 share an XCD, MI355X_MICROARCH.md "Workgroup dispatch"), so an
+                         // XCD's L2 serves neighbouring tiles; 0: the dispatch order as launched
     uint32_t dualDepth;  // PRIMARY_DEPTH_MODE == DualDepth: depth2 refines the raster samples
     const float* depth2; // gDepthTex2 (DualDepth), W x H linear depth
 };

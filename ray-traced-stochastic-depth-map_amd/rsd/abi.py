@@ -167,7 +167,7 @@ WALK_KERNELS = {WALK_QUAD: ("sd_setup_kernel", "sd_trace_queue_kernel"),
 
 
 # every symbol include/rsd.h declares (checked by tests/test_abi.py)
-EXPORTS = ["rsd_abi_version", "rsd_svao_tile_count", "rsd_last_error", "rsd_device_open", "rsd_device_close", "rsd_scene_upload",
+EXPORTS = ["rsd_abi_version", "rsd_svao_tile_count", "rsd_svao_tile_flags_release", "rsd_last_error", "rsd_device_open", "rsd_device_close", "rsd_scene_upload",
            "rsd_scene_info_get", "rsd_scene_release", "rsd_camera_look_at", "rsd_svao_make_vao_data",
            "rsd_gbuffer", "rsd_sd_trace", "rsd_svao_clear_intervals", "rsd_svao_pass1", "rsd_svao_pass2",
            "rsd_sd_trace_band", "rsd_svao_pass1_band", "rsd_svao_pass2_band", "rsd_gbuffer_raster",
@@ -217,6 +217,8 @@ def lib():
         L.rsd_abi_version.restype = u32
         L.rsd_svao_tile_count.restype = u32
         L.rsd_svao_tile_count.argtypes = [u32, u32, u32]
+        L.rsd_svao_tile_flags_release.restype = None
+        L.rsd_svao_tile_flags_release.argtypes = [vp]
         L.rsd_last_error.restype = C.c_char_p
         L.rsd_device_open.restype = st
         L.rsd_device_open.argtypes = [C.c_int, C.POINTER(vp)]

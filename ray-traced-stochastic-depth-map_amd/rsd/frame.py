@@ -18,6 +18,7 @@ from __future__ import annotations
 import ctypes as C
 import dataclasses
 import os
+import weakref
 
 import numpy as np
 
@@ -286,6 +287,9 @@ class Renderer:
         cfg = self.cfg
         n = abi.lib().rsd_svao_tile_count(cfg.fb_w, cfg.fb_h, cfg.guard_band)
         self.tile_flags = self.torch.zeros(max(1, n), dtype=self.torch.uint8, device=self.depth.device)
+        # librsd's generation counter of this buffer is forgotten when the tensor is freed: the caching
+        # allocator may hand the same address to the next (zeroed) flag buffer
+        weakref.finalize(self.tile_flags, abi.lib().rsd_svao_tile_flags_release, self.tile_flags.data_ptr())
         svp = abi.SVAOParams.from_buffer_copy(self.svp)
         # RSD_TILE_FLAGS=off: no flags (pass 2 visits every tile) -- A/B runs only
         svp.tile_flags = None if os.environ.get("RSD_TILE_FLAGS") == "off" else self.tile_flags.data_ptr()

@@ -614,3 +614,25 @@ def test_busy_tile_loop_matches_one_workgroup_per_tile(monkeypatch, torch_dev):
             assert not r.tile_flags.cpu().numpy().view(np.uint32)[:T].any(), (frame, loop)
         assert np.array_equal(aos[0], aos[1]), frame
         assert (aos[0] != aos[0].flat[0]).any()  # a non-trivial AO image
+
+
+def test_stale_tile_flags_do_not_hide_tiles(device):
+    """a pass 1 over some rows whose busy tiles no pass 2 consumed (a pass 2 over OTHER rows) leaves
+    their flags set; the next whole frame must still list those tiles (pass 1 stamps a flag with the buffer's
+    generation, svao.hip tile_gen_pass1) and equal a clean frame bit for bit."""
+    from rsd.frame import CONFIGS, FrameConfig, Renderer
+    from rsd.scenes import make_scene
+    kw, name = CONFIGS["suntemple_1080p_q"]
+    r = Renderer(make_scene(name), FrameConfig(**kw))
+    r.gbuffer()
+    r.frame()
+    ref = r.numpy()["ao"]
+    r.clear_intervals()
+    r.pass1_rows((0, 320))
+    r.sd_trace()
+    r.pass2_rows((640, 960))  # consumes only its own rows' flags
+    torch_ao = r.ao
+    torch_ao.zero_()
+    r.frame()
+    assert np.array_equal(r.numpy()["ao"], ref)
+    r.close()

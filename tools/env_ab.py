@@ -1,7 +1,8 @@
 """Same-process A/B of an SD-trace environment switch (diagnostics, GPU box): the trace of one frame's
 intervals (pass 1 once, the maps kept: no consume) timed with HIP events over `n` back-to-back launches,
 alternating the settings for `reps` rounds; the SD maps of every setting must be the same bits.
-usage: python tools/env_ab.py VAR value_a value_b [config] [--n 40] [--reps 6] [--walk fused|quad]"""
+usage: python tools/env_ab.py VAR value_a value_b [config] [--n 40] [--reps 6] [--walk fused|quad]
+       [--what trace|pass1|pass2] (pass1 / pass2: that pass alone, its outputs compared the same way)"""
 import json
 import os
 import sys
@@ -34,14 +35,21 @@ r.pass1()
 torch.cuda.synchronize()
 
 
+what = arg("--what", "trace")
+if what == "pass2":
+    r.sd_trace()
+call = {"trace": r.sd_trace, "pass1": r.pass1, "pass2": r.pass2}[what]
+out_of = {"trace": lambda: r.sd, "pass1": lambda: r.ray_minmax, "pass2": lambda: r.ao}[what]
+
+
 def run(v):
     os.environ[var] = v
-    r.sd_trace()
+    call()
     torch.cuda.synchronize()
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     s.record()
     for _ in range(n):
-        r.sd_trace()
+        call()
     e.record()
     torch.cuda.synchronize()
     return s.elapsed_time(e) / n * 1e3
@@ -52,8 +60,8 @@ maps = {}
 for _ in range(reps):
     for v in vals:
         times[v].append(run(v))
-        maps[v] = r.sd.cpu().numpy().view(np.uint32).copy()
+        maps[v] = out_of().cpu().numpy().view(np.uint8).copy()
 same = all(np.array_equal(maps[vals[0]], maps[v]) for v in vals[1:])
-print(json.dumps({"config": name, "var": var, "walk": os.environ.get("RSD_TRACE_WALK", "default"), "n": n,
+print(json.dumps({"config": name, "what": what, "var": var, "walk": os.environ.get("RSD_TRACE_WALK", "default"), "n": n,
                   "us": {v: [round(t, 2) for t in ts] for v, ts in times.items()},
                   "median_us": {v: round(float(np.median(ts)), 2) for v, ts in times.items()}, "same_bits": same}))
