@@ -367,10 +367,19 @@ struct QuadClk {
     unsigned long long fetch = 0, tests = 0, stack = 0, total = 0, steps = 0;
 };
 
+// the quad walk's key list: keys only (RSD_QUAD_RECIDX: with the record index, the round-4 layout, A/B builds)
+#ifdef RSD_QUAD_RECIDX
+template <int K>
+using QuadKeys = KList<K>;
+#else
+template <int K>
+using QuadKeys = KKeys<K>;
+#endif
+
 template <int K>
 __device__ __forceinline__ int trace_knearest_quad(const float4* __restrict__ bvh, uint32_t triOff, const RayCtx& r,
                                                    float tmin, float tmax, uint32_t cull, bool useLB, float lbT,
-                                                   uint32_t lbP, KList<K>& kl, uint32_t* __restrict__ sItem,
+                                                   uint32_t lbP, QuadKeys<K>& kl, uint32_t* __restrict__ sItem,
                                                    float* __restrict__ sT, int q, int quadBase, TraceStats& st,
                                                    const uint32_t* __restrict__ ent, uint32_t nEnt,
                                                    QuadClk* clk = nullptr) {
@@ -507,7 +516,7 @@ __device__ __forceinline__ void sd_resolve(const SDArgs& a, f3 d, float TMin, fl
     const rsd_camera& c = a.cam;
     RayCtx r;
     ray_setup(r, mk(c.posW[0], c.posW[1], c.posW[2]), d);
-    KList<K> kl;
+    QuadKeys<K> kl;
     uint32_t count = 0;
     bool commit = false, useLB = false;
     float lbT = 0.0f;
@@ -527,9 +536,17 @@ __device__ __forceinline__ void sd_resolve(const SDArgs& a, f3 d, float TMin, fl
             rngL[i] = 0.0f;
             zL[i] = 0.0f;
             uint32_t ti = 0u;
+#ifdef RSD_QUAD_RECIDX
 #pragma unroll
             for (int jj = 0; jj < K; ++jj)
                 if (jj == j) ti = kl.l[jj];
+#else
+            uint32_t pk = 0u;  // key j's primitive -> its triangle record
+#pragma unroll
+            for (int jj = 0; jj < K; ++jj)
+                if (jj == j) pk = kl.p[jj];
+            if (j < found) ti = a.primRec[pk];
+#endif
             if (j < found) {
                 float t, bu, bv, det;
                 const float4 v0 = a.tris[3 * ti], v1 = a.tris[3 * ti + 1], v2 = a.tris[3 * ti + 2];
@@ -2230,8 +2247,11 @@ rsd_status sd_trace_impl(rsd_scene* scene, const rsd_camera* cam, const rsd_sd_p
     // persistent waves: 8 per CU.  At 1080p/4 every row gets one of the ~22 K live rays in its
     // static first slot and the launch lasts as long as the slowest ray; 16 waves per CU (the
     // split walk holds < 128 VGPRs) measured no faster (tools/sd_time.py sweep)
+    // The quad walk with K = 16 (configs[4]'s N = 16) keeps its keys without record indices since round 5 (151
+    // instead of 177 VGPRs: three waves per SIMD fit), and it is throughput-bound there: 12 waves per CU, 827 ->
+    // 723 us at configs[4] (profiles/round5/trace_ab/wpc_*); at K = 8 (configs[2], [3]) 12 or 16 are neutral.
     const char* wpcEnv = std::getenv("RSD_TRACE_WAVES_PER_CU");  // experiments only (read per call: A/B runs)
-    const uint32_t wavesPerCu = wpcEnv ? (uint32_t)std::max(1, std::atoi(wpcEnv)) : 8u;
+    const uint32_t wavesPerCu = wpcEnv ? (uint32_t)std::max(1, std::atoi(wpcEnv)) : (walk == 0 && K == 16 ? 12u : 8u);
     const uint32_t pb = ((uint32_t)std::max(1, scene->dev->cu_count) * wavesPerCu + kQueueParts - 1) / kQueueParts *
                         kQueueParts;
     hipError_t e = hipSuccess;
