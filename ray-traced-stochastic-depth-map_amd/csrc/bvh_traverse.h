@@ -138,31 +138,6 @@ struct KList {
     }
 };
 
-// The K nearest keys without their record index (the quad walk: every lane holds the whole list, so the
-// index array was K more VGPRs per lane; the epilogue finds a key's record through the scene's primitive ->
-// record map, rsd_scene.d_prim_rec)
-template <int K>
-struct KKeys {
-    float t[K];
-    uint32_t p[K];
-    __device__ __forceinline__ void clear() {
-#pragma unroll
-        for (int j = 0; j < K; ++j) { t[j] = INFINITY; p[j] = 0xffffffffu; }
-    }
-    __device__ __forceinline__ void insert(float nt, uint32_t np, uint32_t) {
-#pragma unroll
-        for (int j = 0; j < K; ++j) {
-            const bool lt = key_less(nt, np, t[j], p[j]);
-            const float tt = t[j];
-            const uint32_t pp = p[j];
-            t[j] = lt ? nt : tt;
-            p[j] = lt ? np : pp;
-            nt = lt ? tt : nt;
-            np = lt ? pp : np;
-        }
-    }
-};
-
 struct TraceStats {
     uint32_t nodes, tris, leaves;
 };

@@ -367,14 +367,53 @@ struct QuadClk {
     unsigned long long fetch = 0, tests = 0, stack = 0, total = 0, steps = 0;
 };
 
-// the quad walk's key list: keys only (RSD_QUAD_RECIDX: with the record index, the round-4 layout, A/B builds)
-#ifdef RSD_QUAD_RECIDX
+// The quad walk's K nearest keys, distributed over the quad (round 5): lane q holds keys j = 4 s + q (slot s
+// of S = K / 4), so each lane keeps K / 4 keys instead of a copy of all K (at K = 16: 8 instead of 32 VGPRs,
+// and the record index is not kept at all -- the epilogue finds a key's triangle record through the scene's
+// primitive -> record map).  Lane q's slots are exactly the keys whose terms lane q prepares in the epilogue.
+// Every lane of the quad inserts the same key: its position is the quad-wide count of keys before it, and
+// each slot at or after it takes the key before it -- lane q - 1's same slot, or (lane 0) lane 3's previous
+// slot -- through one quad rotation per slot.  The K-th key is kept replicated for the pruning tests.
+constexpr int kDppQuadRotR = 0x93;  // quad_perm [3, 0, 1, 2]: lane q reads lane q - 1 (lane 0: lane 3)
 template <int K>
-using QuadKeys = KList<K>;
-#else
-template <int K>
-using QuadKeys = KKeys<K>;
-#endif
+struct QuadKeys {
+    static constexpr int S = K / 4;
+    float t[S];
+    uint32_t p[S];
+    float kthT;  // key K - 1 (every lane)
+    uint32_t kthP;
+    __device__ __forceinline__ void clear() {
+#pragma unroll
+        for (int i = 0; i < S; ++i) { t[i] = INFINITY; p[i] = 0xffffffffu; }
+        kthT = INFINITY;
+        kthP = 0xffffffffu;
+    }
+    __device__ __forceinline__ void insert(float nt, uint32_t np, int q) {
+        uint32_t c = 0u;
+#pragma unroll
+        for (int i = 0; i < S; ++i) c += key_less(t[i], p[i], nt, np) ? 1u : 0u;
+        c += dppu<kDppXor1>(c);
+        c += dppu<kDppXor2>(c);  // every lane: the keys before the new one
+        float rt[S];
+        uint32_t rp[S];
+#pragma unroll
+        for (int i = 0; i < S; ++i) {
+            rt[i] = dppf<kDppQuadRotR>(t[i]);
+            rp[i] = dppu<kDppQuadRotR>(p[i]);
+        }
+#pragma unroll
+        for (int i = 0; i < S; ++i) {
+            const uint32_t j = 4u * (uint32_t)i + (uint32_t)q;
+            const float prevT = q > 0 ? rt[i] : (i > 0 ? rt[i > 0 ? i - 1 : 0] : INFINITY);
+            const uint32_t prevP = q > 0 ? rp[i] : (i > 0 ? rp[i > 0 ? i - 1 : 0] : 0xffffffffu);
+            const bool put = j == c, shift = j > c;
+            t[i] = put ? nt : (shift ? prevT : t[i]);
+            p[i] = put ? np : (shift ? prevP : p[i]);
+        }
+        kthT = qbcf<3>(t[S - 1]);
+        kthP = qbcu<3>(p[S - 1]);
+    }
+};
 
 template <int K>
 __device__ __forceinline__ int trace_knearest_quad(const float4* __restrict__ bvh, uint32_t triOff, const RayCtx& r,
@@ -428,25 +467,24 @@ __device__ __forceinline__ int trace_knearest_quad(const float4* __restrict__ bv
                 if (intersect_tri(r, va, vb, vc, t, bu, bv, det) && t >= tmin && t <= tmax) {
                     prim = __float_as_uint(va.w);
                     acc = !culled(det, __float_as_uint(vb.w), cull) && (!useLB || key_less(lbT, lbP, t, prim)) &&
-                          key_less(t, prim, kl.t[K - 1], kl.p[K - 1]);
+                          key_less(t, prim, kl.kthT, kl.kthP);
                 }
             }
             uint32_t m = (uint32_t)(__ballot(acc) >> quadBase) & 0xfu;
-            const uint32_t first = (off - triOff) / 3u;
             while (m) {
                 const int j = __ffs(m) - 1;
                 m &= m - 1u;
                 const float tj = qself(t, j);
                 const uint32_t pj = qselu(prim, j);
-                if (key_less(tj, pj, kl.t[K - 1], kl.p[K - 1])) {
-                    kl.insert(tj, pj, first + (uint32_t)j);
+                if (key_less(tj, pj, kl.kthT, kl.kthP)) {
+                    kl.insert(tj, pj, q);
                     found = found < K ? found + 1 : K;
                 }
             }
             if (clk && q == 0) clk->tests += __builtin_amdgcn_s_memtime() - tF;
         } else {
             st.nodes++;
-            const float thi = fminf(tmax, kl.t[K - 1]);
+            const float thi = fminf(tmax, kl.kthT);
             const float* nb = bf + 4u * off;
             const float lox = nb[q], hix = nb[4 + q], loy = nb[8 + q], hiy = nb[12 + q], loz = nb[16 + q],
                         hiz = nb[20 + q];
@@ -483,7 +521,7 @@ __device__ __forceinline__ int trace_knearest_quad(const float4* __restrict__ bv
         }
         if (clk) tA = __builtin_amdgcn_s_memtime();  // the branches reconverged
         if (next == kNoItem) {
-            const float thi = fminf(tmax, kl.t[K - 1]);
+            const float thi = fminf(tmax, kl.kthT);
             while (sp > 0) {
                 --sp;
                 const float tt = sT[sp * kQuadRays];
@@ -536,17 +574,7 @@ __device__ __forceinline__ void sd_resolve(const SDArgs& a, f3 d, float TMin, fl
             rngL[i] = 0.0f;
             zL[i] = 0.0f;
             uint32_t ti = 0u;
-#ifdef RSD_QUAD_RECIDX
-#pragma unroll
-            for (int jj = 0; jj < K; ++jj)
-                if (jj == j) ti = kl.l[jj];
-#else
-            uint32_t pk = 0u;  // key j's primitive -> its triangle record
-#pragma unroll
-            for (int jj = 0; jj < K; ++jj)
-                if (jj == j) pk = kl.p[jj];
-            if (j < found) ti = a.primRec[pk];
-#endif
+            if (j < found) ti = a.primRec[kl.p[i]];  // key j = 4 i + q is this lane's slot i
             if (j < found) {
                 float t, bu, bv, det;
                 const float4 v0 = a.tris[3 * ti], v1 = a.tris[3 * ti + 1], v2 = a.tris[3 * ti + 2];
@@ -571,8 +599,8 @@ __device__ __forceinline__ void sd_resolve(const SDArgs& a, f3 d, float TMin, fl
         }
         if (SPEC || found < K) break;  // stream exhausted (SPEC: a commit by the K-th key)
         useLB = true;
-        lbT = kl.t[K - 1];
-        lbP = kl.p[K - 1];
+        lbT = kl.kthT;
+        lbP = kl.kthP;
     }
 }
 
@@ -2247,11 +2275,12 @@ rsd_status sd_trace_impl(rsd_scene* scene, const rsd_camera* cam, const rsd_sd_p
     // persistent waves: 8 per CU.  At 1080p/4 every row gets one of the ~22 K live rays in its
     // static first slot and the launch lasts as long as the slowest ray; 16 waves per CU (the
     // split walk holds < 128 VGPRs) measured no faster (tools/sd_time.py sweep)
-    // The quad walk with K = 16 (configs[4]'s N = 16) keeps its keys without record indices since round 5 (151
-    // instead of 177 VGPRs: three waves per SIMD fit), and it is throughput-bound there: 12 waves per CU, 827 ->
-    // 723 us at configs[4] (profiles/round5/trace_ab/wpc_*); at K = 8 (configs[2], [3]) 12 or 16 are neutral.
+    // The quad walk keeps its keys distributed over the quad since round 5 (QuadKeys: 177 -> 115 VGPRs at K = 16,
+    // 96 at K = 8), and the full-resolution maps it serves are throughput-bound: 12 waves per CU at K = 16
+    // (configs[4] 827 -> 713 us; 16 measured the same), 16 at K <= 8 (configs[2] 263 -> 257 us, configs[3] flat);
+    // profiles/round5/trace_ab/wpc_*.  The row walk stays at 8 (latency-bound: 10 / 12 / 16 measured no faster).
     const char* wpcEnv = std::getenv("RSD_TRACE_WAVES_PER_CU");  // experiments only (read per call: A/B runs)
-    const uint32_t wavesPerCu = wpcEnv ? (uint32_t)std::max(1, std::atoi(wpcEnv)) : (walk == 0 && K == 16 ? 12u : 8u);
+    const uint32_t wavesPerCu = wpcEnv ? (uint32_t)std::max(1, std::atoi(wpcEnv)) : (walk == 0 ? (K == 16 ? 12u : 16u) : 8u);
     const uint32_t pb = ((uint32_t)std::max(1, scene->dev->cu_count) * wavesPerCu + kQueueParts - 1) / kQueueParts *
                         kQueueParts;
     hipError_t e = hipSuccess;
