@@ -965,8 +965,9 @@ __global__ void __launch_bounds__(kBlock) sd_trace_ordered_kernel(SDArgs a, cons
     const int lane = threadIdx.x;
     const int q = lane & 3, quad = lane >> 2, quadBase = lane & ~3;
     const uint32_t part = blockIdx.x % kQueueParts, wavesPerPart = gridDim.x / kQueueParts;
-    const uint32_t count = __hip_atomic_load(&qctl[part], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const uint32_t slot0 = part * a.partCap;
+    const uint32_t nLong = __hip_atomic_load(&qctl[part], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t count = nLong + (a.lpt ? __hip_atomic_load(&qctl[kQctlShort + part], __ATOMIC_RELAXED,
+                                                               __HIP_MEMORY_SCOPE_AGENT) : 0u);
     const float DEFAULT = a.normalize ? 1.0f : 3.40282347e+37f;  // Common.slangh:16
     TraceStats st{0u, 0u, 0u};
     uint32_t active = 0, delivered = 0, maxNodes = 0, maxSteps = 0;
@@ -981,7 +982,7 @@ __global__ void __launch_bounds__(kBlock) sd_trace_ordered_kernel(SDArgs a, cons
             f3 d;
             float TMin, TMax, cosT;
             uint32_t idx;
-            ray_rec_load(queue, slot0 + qi, d, TMin, TMax, cosT, idx);
+            ray_rec_load(queue, queue_slot(a, part, qi, nLong), d, TMin, TMax, cosT, idx);
             float depths[N];
 #pragma unroll
             for (int i = 0; i < N; ++i) depths[i] = DEFAULT;
@@ -2230,7 +2231,9 @@ rsd_status sd_trace_impl(rsd_scene* scene, const rsd_camera* cam, const rsd_sd_p
     }
     if (walk == 1 || walk == 0) {
         // longest-first queue: rays whose interval exceeds 0.1 x TMin are dequeued first (configs[1]:
-        // 90 -> 84 us); RSD_TRACE_LPT = off | a threshold (> 0 absolute, < 0 relative to TMin)
+        // 90 -> 84 us); RSD_TRACE_LPT = off | a threshold (> 0 absolute, < 0 relative to TMin).  (The
+        // traversal-order walk reads the split queue too, but measured no gain from it: 150.7 vs 147.3 us at
+        // configs[1], profiles/round5/trace_ab/lpt_ordered_c1.json -- its rays start at the root.)
         const char* lptEnv = std::getenv("RSD_TRACE_LPT");
         const bool off = lptEnv && std::string(lptEnv) == "off";
         a.lpt = off ? 0u : 1u;
