@@ -69,6 +69,7 @@ typedef struct {
     uint64_t device_bytes;
     uint32_t build_threads;   /* host threads of the build (the process's CPU affinity, or RSD_BUILD_THREADS) */
     uint32_t entry_cells;     /* cells of the segment entry grid (RSD_ENTRY_CELLS bounds it, 0 = none) */
+    uint32_t wide_depth;      /* 4-wide nodes on the longest root-to-leaf path (sizes the walks' LDS stacks) */
 } rsd_scene_info;
 
 /* Alpha-masked materials (MaterialFactory.slang:124-151, AlphaTest.slang:54-84,

@@ -322,11 +322,19 @@ extern "C" rsd_status rsd_scene_upload_alpha(rsd_device* dev, const rsd_scene_de
 }
 
 extern "C" float rsd_ray_cone_spread(float focal_length, uint32_t height) {
+    // every SD trace asks for it with the frame's (focal length, height): keep the last answer per thread
+    // (the decimal round trip below costs about as much as a kernel launch on the host)
+    thread_local float lastF = -1.0f, lastS = 0.0f;
+    thread_local uint32_t lastH = 0;
+    if (focal_length == lastF && height == lastH) return lastS;
     const float fovY = 2.0f * std::atan(0.5f * 24.0f / focal_length);  // focalLengthToFovY(f, kDefaultFrameHeight)
     const float angle = std::atan(2.0f * std::tan(fovY * 0.5f) / (float)height);
     char buf[64];
     std::snprintf(buf, sizeof(buf), "%f", (double)angle);  // std::to_string(float)
-    return std::strtof(buf, nullptr);
+    lastS = std::strtof(buf, nullptr);
+    lastF = focal_length;
+    lastH = height;
+    return lastS;
 }
 
 extern "C" rsd_status rsd_scene_info_get(const rsd_scene* s, rsd_scene_info* out) {
@@ -337,6 +345,7 @@ extern "C" rsd_status rsd_scene_info_get(const rsd_scene* s, rsd_scene_info* out
     out->triangle_count = s->triangle_count;
     out->node_count = s->node_count;
     out->max_depth = s->stats.max_depth;
+    out->wide_depth = s->stats.wide_depth;
     out->leaf_count = s->stats.leaves;
     out->sah_cost = s->stats.sah_cost;
     out->build_ms = s->stats.build_ms + s->entry_build_ms;

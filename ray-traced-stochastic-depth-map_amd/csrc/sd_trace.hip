@@ -96,6 +96,7 @@ struct SDArgs {
     // the partition's waves (queue index i -> wave i % waves, row i / waves), so the longest-first rays land
     // one per wave instead of eight to a wave; 0: wave-major (index i -> wave i / rows, row i % rows)
     uint32_t spread;
+    uint32_t quadStack;  // entries of each ray's LDS stack in the quad walks (quad_stack_entries)
     // segment entry grid (entry_grid.h, canonical walks): the setup kernel looks up the frontier of
     // each live ray's segment and copies its items to entQ[slot * kEntryCap ..]
     uint32_t entOn;
@@ -322,7 +323,12 @@ __device__ __forceinline__ bool sd_any_hit(const SDArgs& a, float rng, float z, 
 // broadcast one by one and inserted by all 4 lanes.  A wave walks 16 rays.
 // ------------------------------------------------------------------------------------
 constexpr int kQuadRays = kBlock / 4;   // rays per wave
-constexpr int kQuadStack = 96;          // per-ray LDS stack depth (4-wide: <= 3 per level)
+// per-ray LDS stack of the quad walks, sized per scene at launch (dynamic LDS, SDArgs.quadStack): a
+// depth-first 4-wide walk holds <= 3 pushed siblings per level below its start, plus the entry items it
+// has not popped yet, so quad_stack_entries(wide depth) entries never overflow.  Sized to the tree, the
+// stack of configs[1]-[4]'s trees (4-wide depth 15-18: 56-64 entries) takes 7-8 KB per wave instead of round 4's fixed 96
+// entries (12 KB), and LDS no longer caps the persistent waves below their register limit (13 per CU).
+constexpr uint32_t quad_stack_entries(uint32_t wideDepth) { return (3u * wideDepth + 7u + 7u) & ~7u; }
 
 // Quad-local exchange through DPP quad_perm (a VALU modifier: no LDS round trip, unlike
 // __shfl / ds_bpermute).  CTRL = quad_perm(p0,p1,p2,p3) = p0 | p1<<2 | p2<<4 | p3<<6.
@@ -770,8 +776,9 @@ __global__ void __launch_bounds__(kSetupWaves * kBlock) sd_setup_kernel(SDArgs a
 template <int K, int N, bool SPEC = false, bool CNT = false>
 __global__ void __launch_bounds__(kBlock) sd_trace_queue_kernel(SDArgs a, const float4* __restrict__ queue,
                                                                 uint32_t* __restrict__ qctl) {
-    __shared__ uint32_t sItem[kQuadStack * kQuadRays];
-    __shared__ float sT[kQuadStack * kQuadRays];
+    extern __shared__ uint32_t sQuadStack[];  // a.quadStack entries per ray: items, then their entry distances
+    uint32_t* sItem = sQuadStack;
+    float* sT = reinterpret_cast<float*>(sQuadStack + a.quadStack * kQuadRays);
     const int lane = threadIdx.x;
     const int q = lane & 3, quad = lane >> 2, quadBase = lane & ~3;
     // wave w serves partition w % kQueueParts (gridDim.x is a multiple of kQueueParts)
@@ -960,8 +967,9 @@ __device__ __forceinline__ void sd_trace_ordered_ray(const SDArgs& a, f3 d, floa
 template <int N>
 __global__ void __launch_bounds__(kBlock) sd_trace_ordered_kernel(SDArgs a, const float4* __restrict__ queue,
                                                                   uint32_t* __restrict__ qctl) {
-    __shared__ uint32_t sItem[kQuadStack * kQuadRays];
-    __shared__ float sT[kQuadStack * kQuadRays];
+    extern __shared__ uint32_t sQuadStack[];  // a.quadStack entries per ray: items, then their entry distances
+    uint32_t* sItem = sQuadStack;
+    float* sT = reinterpret_cast<float*>(sQuadStack + a.quadStack * kQuadRays);
     const int lane = threadIdx.x;
     const int q = lane & 3, quad = lane >> 2, quadBase = lane & ~3;
     const uint32_t part = blockIdx.x % kQueueParts, wavesPerPart = gridDim.x / kQueueParts;
@@ -1824,6 +1832,8 @@ __global__ void __launch_bounds__(kBlock) gbuffer_kernel(GBArgs a) {
 // walk: 0 = quad (depth-first), 1 = row walk + in-kernel algorithm, 2 = split (row walk ->
 // keys -> resolve kernel), 3 = traversal-order any-hit stream (rsd_hit_order), 4 = raster (triangles
 // -> 64-bit key lists -> resolve kernel)
+static size_t quad_stack_bytes(const SDArgs& a) { return (size_t)a.quadStack * kQuadRays * 8u; }
+
 template <int K, int N>
 static hipError_t launch_sd_kn(const SDArgs& a, dim3 grid, uint32_t persistentBlocks, float4* queue, uint32_t* qctl,
                                uint2* keys, int walk, int pool, hipStream_t s) {
@@ -1841,7 +1851,7 @@ static hipError_t launch_sd_kn(const SDArgs& a, dim3 grid, uint32_t persistentBl
         if ((e = hipGetLastError()) != hipSuccess) return e;
         hipLaunchKernelGGL((sd_resolve_row_kernel<K, N, ROW>), pg, wb, 0, s, a, queue, qctl, keys);
     } else if (walk == 3) {
-        hipLaunchKernelGGL((sd_trace_ordered_kernel<N>), pg, wb, 0, s, a, queue, qctl);
+        hipLaunchKernelGGL((sd_trace_ordered_kernel<N>), pg, wb, quad_stack_bytes(a), s, a, queue, qctl);
     } else if (walk == 4) {
         hipLaunchKernelGGL((sd_raster_kernel<K>), dim3((a.nTris + kRasterBlock - 1) / kRasterBlock), dim3(kRasterBlock),
                            0, s, a, queue, qctl);
@@ -1861,9 +1871,10 @@ static hipError_t launch_sd_kn(const SDArgs& a, dim3 grid, uint32_t persistentBl
         const char* specEnv = std::getenv("RSD_TRACE_SPEC");
         const bool spec = !(specEnv && std::string(specEnv) == "off") && !a.alphaTest && a.impl != 1u &&
                           a.impl != 3u && a.maxCount <= (uint32_t)K && !a.counters;
-        if (a.counters) hipLaunchKernelGGL((sd_trace_queue_kernel<K, N, false, true>), dim3(persistentBlocks), dim3(kBlock), 0, s, a, queue, qctl);
-        else if (spec) hipLaunchKernelGGL((sd_trace_queue_kernel<K, N, true>), dim3(persistentBlocks), dim3(kBlock), 0, s, a, queue, qctl);
-        else hipLaunchKernelGGL((sd_trace_queue_kernel<K, N>), dim3(persistentBlocks), dim3(kBlock), 0, s, a, queue, qctl);
+        const size_t lds = quad_stack_bytes(a);
+        if (a.counters) hipLaunchKernelGGL((sd_trace_queue_kernel<K, N, false, true>), pg, wb, lds, s, a, queue, qctl);
+        else if (spec) hipLaunchKernelGGL((sd_trace_queue_kernel<K, N, true>), pg, wb, lds, s, a, queue, qctl);
+        else hipLaunchKernelGGL((sd_trace_queue_kernel<K, N>), pg, wb, lds, s, a, queue, qctl);
     }
     return hipGetLastError();
 }
@@ -2191,6 +2202,7 @@ rsd_status sd_trace_impl(rsd_scene* scene, const rsd_camera* cam, const rsd_sd_p
     // bound (kPoolCap >= poolSoft + 48 + 3 * depth), or RSD_TRACE_WALK=quad asks for the
     // depth-first quad walk (A/B measurements)
     const int depth = (int)std::max(1u, scene->stats.wide_depth);
+    a.quadStack = quad_stack_entries((uint32_t)depth);
     // the row walk's LDS pool: 128 entries per ray (8 KB per wave) wherever the tree depth allows it
     // (the pool bound above), else 256; with the specialised walk the smaller pool measured faster alone
     // (75.7 vs 78.3 us at configs[1]) and leaves more LDS to the other frames' passes
@@ -2279,11 +2291,13 @@ rsd_status sd_trace_impl(rsd_scene* scene, const rsd_camera* cam, const rsd_sd_p
     // static first slot and the launch lasts as long as the slowest ray; 16 waves per CU (the
     // split walk holds < 128 VGPRs) measured no faster (tools/sd_time.py sweep)
     // The quad walk keeps its keys distributed over the quad since round 5 (QuadKeys: 177 -> 115 VGPRs at K = 16,
-    // 96 at K = 8), and the full-resolution maps it serves are throughput-bound: 12 waves per CU at K = 16
-    // (configs[4] 827 -> 713 us; 16 measured the same), 16 at K <= 8 (configs[2] 263 -> 257 us, configs[3] flat);
-    // profiles/round5/trace_ab/wpc_*.  The row walk stays at 8 (latency-bound: 10 / 12 / 16 measured no faster).
+    // 96 at K = 8), and the full-resolution maps it serves are throughput-bound: 16 waves per CU, the register
+    // limit at K = 16 once its LDS stack is sized to the tree (quad_stack_entries: the fixed 96-entry stack held
+    // residency to 13; configs[4] 827 -> 713 us at 12, 699 -> 671 us from 12 to 16), and at K <= 8 (configs[2]
+    // 263 -> 257 us; 20 measured the same, as did configs[3]); profiles/round5/trace_ab/wpc_*, r5p/.  The row walk
+    // stays at 8 (latency-bound: 10 / 12 / 16 measured no faster).
     const char* wpcEnv = std::getenv("RSD_TRACE_WAVES_PER_CU");  // experiments only (read per call: A/B runs)
-    const uint32_t wavesPerCu = wpcEnv ? (uint32_t)std::max(1, std::atoi(wpcEnv)) : (walk == 0 ? (K == 16 ? 12u : 16u) : 8u);
+    const uint32_t wavesPerCu = wpcEnv ? (uint32_t)std::max(1, std::atoi(wpcEnv)) : (walk == 0 ? 16u : 8u);
     const uint32_t pb = ((uint32_t)std::max(1, scene->dev->cu_count) * wavesPerCu + kQueueParts - 1) / kQueueParts *
                         kQueueParts;
     hipError_t e = hipSuccess;

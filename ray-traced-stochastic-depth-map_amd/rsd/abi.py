@@ -53,7 +53,8 @@ class AlphaDesc(C.Structure):
 class SceneInfo(C.Structure):
     _fields_ = [("triangle_count", C.c_uint32), ("node_count", C.c_uint32), ("max_depth", C.c_uint32),
                 ("leaf_count", C.c_uint32), ("sah_cost", C.c_double), ("build_ms", C.c_double),
-                ("device_bytes", C.c_uint64), ("build_threads", C.c_uint32), ("entry_cells", C.c_uint32)]
+                ("device_bytes", C.c_uint64), ("build_threads", C.c_uint32), ("entry_cells", C.c_uint32),
+                ("wide_depth", C.c_uint32)]
 
 
 class Camera(C.Structure):

@@ -7,7 +7,9 @@
 #include <hip/hip_runtime.h>
 
 #include <chrono>
+#include <cmath>
 #include <cstdio>
+#include <cstdlib>
 
 struct Small {
     float v[16];
@@ -77,10 +79,22 @@ int main() {
     CHECK(hipHostMalloc((void**)&hpin, 9 * 8 * 8, hipHostMallocDefault));
     const double d2h = per_call_us(s, [&] { (void)hipMemcpyAsync(hpin, dsrc, 9 * 8 * 8, hipMemcpyDeviceToHost, s); });
     const double mset = per_call_us(s, [&] { (void)hipMemsetAsync(dsrc, 0, 9 * 8 * 8, s); });
+    // librsd's per-call host helpers: one getenv of a tuning variable, the "%f" round trip of RAY_CONE_SPREAD
+    volatile const char* sink = nullptr;
+    const double genv = per_call_us(s, [&] { sink = std::getenv("RSD_PASS2_LOOP"); });
+    volatile float fs = 0.0f;
+    const double spread = per_call_us(s, [&] {
+        char buf[64];
+        std::snprintf(buf, sizeof(buf), "%f", (double)std::atan(0.0012f));
+        fs = std::strtof(buf, nullptr);
+    });
+    (void)sink;
+    (void)fs;
     CHECK(hipStreamSynchronize(s));
     std::printf("{\"launch_us_args64\": %.2f, \"launch_us_args2048\": %.2f, \"event_record_us\": %.2f, "
                 "\"event_record_timing_us\": %.2f, \"get_last_error_us\": %.3f, \"get_device_us\": %.3f, "
-                "\"memcpy_d2h_pinned_576B_us\": %.2f, \"memset_576B_us\": %.2f}\n",
-                small, big, rec, rect, gle, gd, d2h, mset);
+                "\"memcpy_d2h_pinned_576B_us\": %.2f, \"memset_576B_us\": %.2f, \"getenv_us\": %.3f, "
+                "\"cone_spread_format_us\": %.3f}\n",
+                small, big, rec, rect, gle, gd, d2h, mset, genv, spread);
     return 0;
 }
