@@ -79,6 +79,9 @@ def parse():
                          "scaling, the north_star split); frame = every rank renders whole frames (weak scaling, "
                          "no per-frame collective); gather = interleaved bands with whole-map all-reduce / "
                          "all-gather (round-1 v1)")
+    ap.add_argument("--clean-tiles", choices=("on", "off"), default="on",
+                    help="SD traces skip rewriting 8x8 tiles they left at DEFAULT_DEPTH without a live ray "
+                         "(rsd_sd_params.d_tile_state; same bits; off: every texel every frame)")
     ap.add_argument("--frame-impl", choices=("native", "python"), default="native",
                     help="N > 1 band frames: native = rsd_band_frame (the frame's passes and exchanges issued from C++, "
                          "RCCL communicators driven by librsd: one per frame slot); python = rsd/shard.py HaloFrame "
@@ -167,6 +170,8 @@ def main():
     else:
         scene = make_scene(scene_name)
     r = Renderer(scene, cfg, device=local)
+    # clean tiles: band frames void the stamps on a re-split; the gather split all-reduces whole maps
+    r.keep_clean_tiles(args.clean_tiles == "on" and shard != "gather")
     bvh_build_s = r.gscene.info.build_ms * 1e-3
     bw = (rank, world) if shard == "gather" else (0, 1)
     F = max(1, args.frames_in_flight)
@@ -327,7 +332,13 @@ def main():
     # (+ the entry grid's lookups, which replace the top of the walk);
     # librsd's nodes are 4-wide (128 B per visit = two of SURVEY's 64-B BVH2 nodes).  Per launch =
     # per frame (band mode: the whole frame's bytes over the slowest rank's trace time).
-    alg_bytes = rays * (16 + 8 + 4 * N) + 128 * nodes_seq + 48 * tris_seq + entry_bytes
+    # (the store term counts only the texels written: clean tiles, --clean-tiles, are not rewritten)
+    texels_clean = mean_cnt(cnt_seq, "texels_clean")
+    if dist and shard != "frame":
+        t = torch.tensor([texels_clean], device="cuda", dtype=torch.float64)
+        dist.all_reduce(t)
+        texels_clean = float(t.item())
+    alg_bytes = rays * (16 + 8) + (rays - texels_clean) * 4 * N + 128 * nodes_seq + 48 * tris_seq + entry_bytes
     achieved = alg_bytes / (seq_sd_ms * 1e-3) / 1e9
     kernels_seq = abi.WALK_KERNELS[walk_seq]
     lat = latency_floor(cnt_seq, seq_sd_ms)

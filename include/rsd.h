@@ -126,6 +126,12 @@ typedef struct {
     uint32_t hit_order;      /* any-hit delivery order: rsd_hit_order (librsd extension) */
     uint32_t use_16bit;      /* Use16Bit (StochasticDepthMapRT.cpp:192-198): store R16F / RG16F / RGBA16F,
                                 N <= 4; d_sd_out then holds IEEE binary16 (round to nearest even) */
+    uint32_t* d_tile_state;  /* NULL, or rsd_sd_tile_state_count(sd_w, sd_h) device words owned with d_sd_out
+                                (librsd extension, DESIGN.md 4 "clean tiles"): the trace records per 8x8 SD tile
+                                whether it left every texel of the tile it wrote at DEFAULT_DEPTH, and does not
+                                rewrite such a tile while it has no live ray.  The caller zeroes the words when
+                                it allocates the map, writes the map itself, or changes which texels its traces
+                                own (a band split); the map's bits are those of a trace without it. */
 } rsd_sd_params;
 
 /* Any-hit order of the SD trace.  DXR calls any-hit in an implementation-defined traversal order
@@ -236,6 +242,7 @@ typedef struct {
     uint64_t step_pool_clocks;
     uint64_t row_steps;
     double shader_clock_mhz;
+    uint64_t texels_clean;   /* SD texels of clean tiles the setup did not rewrite (rsd_sd_params.d_tile_state) */
 } rsd_counters;
 /* rsd_counters.walk: which kernels an rsd_sd_trace launched (besides sd_setup_kernel) */
 #define RSD_WALK_QUAD 0u   /* sd_trace_queue_kernel: depth-first, 4 lanes per ray */
@@ -314,6 +321,8 @@ rsd_status rsd_sd_trace(rsd_scene* scene, const rsd_camera* cam, const rsd_sd_pa
                         rsd_counters* counters, rsd_stream stream);
 
 /* SVAO.cpp:330-341: rayMax <- 0, rayMin <- asuint(FLT_MAX) */
+/* Words of rsd_sd_params.d_tile_state for an sd_w x sd_h map: one per 8x8 tile. */
+uint32_t rsd_sd_tile_state_count(uint32_t sd_w, uint32_t sd_h);
 rsd_status rsd_svao_clear_intervals(uint32_t* d_ray_min, uint32_t* d_ray_max, uint32_t count, rsd_stream stream);
 
 /* "AO 1": SVAORaster.ps.slang:29-122, dispatched as SVAO.cpp:344-350.

@@ -258,6 +258,12 @@ rsd_status BandFrame::init(const rsd_svao_frame_desc& f, const rsd_band_params& 
 
 // rsd/shard.py HaloFrame._plan: pass bands, SD shares, windows, exchange regions, AO bands
 rsd_status BandFrame::plan(hipStream_t s) {
+    // a new split changes which SD texels this rank's traces write: its clean-tile stamps are void
+    if (sdp_.d_tile_state) {
+        const size_t b = (size_t)rsd_sd_tile_state_count(f_.sd_w, f_.sd_h) * sizeof(uint32_t);
+        const hipError_t e = s ? hipMemsetAsync(sdp_.d_tile_state, 0, b, s) : hipMemset(sdp_.d_tile_state, 0, b);
+        if (e != hipSuccess) return hip_fail(e, "rsd_band_frame (tile state)");
+    }
     const uint32_t sdh = f_.sd_h, sdw = f_.sd_w, g = guard_, fbh = f_.height;
     px_rows_.assign(world_, {0, 0});
     for (uint32_t r = 0; r < world_; ++r) px_rows_[r] = {32 * gb_[r], 32 * gb_[r + 1]};

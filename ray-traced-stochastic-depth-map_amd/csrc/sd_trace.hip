@@ -97,6 +97,10 @@ struct SDArgs {
     // one per wave instead of eight to a wave; 0: wave-major (index i -> wave i / rows, row i % rows)
     uint32_t spread;
     uint32_t quadStack;  // entries of each ray's LDS stack in the quad walks (quad_stack_entries)
+    // clean tiles (rsd_sd_params.d_tile_state): per 8x8 tile, tileSig when the last trace left every texel it
+    // wrote at DEFAULT_DEPTH (0: unknown); such a tile without a live ray is not rewritten
+    uint32_t* tileState;
+    uint32_t tileSig;
     // segment entry grid (entry_grid.h, canonical walks): the setup kernel looks up the frontier of
     // each live ray's segment and copies its items to entQ[slot * kEntryCap ..]
     uint32_t entOn;
@@ -659,6 +663,9 @@ __global__ void __launch_bounds__(kSetupWaves * kBlock) sd_setup_kernel(SDArgs a
         }
         return;  // uniform over the workgroup
     }
+    // the tile's clean stamp (one word per wave), loaded first so that its latency hides behind the texel's
+    const bool tileIn = tileX < tilesX;
+    const uint32_t tilePrev = a.tileState && tileIn ? a.tileState[(size_t)tileRow * tilesX + tileX] : 0u;
     bool live = false, culled = false;
     uint32_t ent = kEntryRoot, keep = 0u;  // keep: the frontier items the ray passes
     uint32_t code[kEntryCap];              // their item codes
@@ -703,15 +710,22 @@ __global__ void __launch_bounds__(kSetupWaves * kBlock) sd_setup_kernel(SDArgs a
                 culled = true;
             }
         }
-        if (!live) {
-            float depths[N];
-            const float DEFAULT = a.normalize ? 1.0f : 3.40282347e+37f;  // Common.slangh:16
-#pragma unroll
-            for (int i = 0; i < N; ++i) depths[i] = DEFAULT;
-            sd_store<N>(a, x, y, depths);
-        }
     }
     const unsigned long long m = __ballot(live);
+    // a tile without a live ray whose texels the previous trace of this map left at DEFAULT_DEPTH already
+    // holds this trace's bits (the full-resolution maps: most of the map, 64 B per texel at N = 16)
+    const bool clean = a.tileState && m == 0ull && tilePrev == a.tileSig;
+    if (inside && !live && !clean) {
+        float depths[N];
+        const float DEFAULT = a.normalize ? 1.0f : 3.40282347e+37f;  // Common.slangh:16
+#pragma unroll
+        for (int i = 0; i < N; ++i) depths[i] = DEFAULT;
+        sd_store<N>(a, x, y, depths);
+    }
+    if (a.tileState && tileIn && lane == 0) {  // a live ray may store anything: the tile is unknown again
+        const uint32_t now = m == 0ull ? a.tileSig : 0u;
+        if (now != tilePrev) a.tileState[(size_t)tileRow * tilesX + tileX] = now;
+    }
     const uint32_t n = (uint32_t)__popcll(m);
     // the queue is split in kQueueParts partitions (block b -> partition b % kQueueParts), each
     // with its own counter: one counter word serialises ~90 atomics/us.
@@ -766,6 +780,7 @@ __global__ void __launch_bounds__(kSetupWaves * kBlock) sd_setup_kernel(SDArgs a
     }
     const unsigned long long in = __ballot(inside);
     if (a.counters && lane == 0) atomicAdd(&a.counters[0], (unsigned long long)__popcll(in));
+    if (a.counters && clean && lane == 0) atomicAdd(&a.counters[25], (unsigned long long)__popcll(in));
 }
 
 // Phase 2: persistent waves pull 16 live rays (one per quad) at a time from the queue
@@ -2105,6 +2120,9 @@ rsd_status sd_trace_impl(rsd_scene* scene, const rsd_camera* cam, const rsd_sd_p
         const char* spreadEnv = std::getenv("RSD_TRACE_SPREAD");
         a.spread = spreadEnv && std::string(spreadEnv) == "on" ? 1u : 0u;
     }
+    // clean tiles: the stamp names what DEFAULT_DEPTH looks like in this map (value, storage, layers)
+    a.tileState = p->d_tile_state;
+    a.tileSig = 1u | (p->normalize ? 2u : 0u) | (p->use_16bit ? 4u : 0u) | ((uint32_t)N << 3);
     a.primRec = scene->d_prim_rec;
     a.entOn = 0u;
     a.entSlots = static_cast<const uint4*>(scene->d_entry);
@@ -2332,6 +2350,7 @@ rsd_status sd_trace_impl(rsd_scene* scene, const rsd_camera* cam, const rsd_sd_p
         counters->step_compute_clocks = h[17];
         counters->step_pool_clocks = h[18];
         counters->row_steps = h[14];
+        counters->texels_clean = h[25];
         counters->shader_clock_mhz = h[22] ? (double)h[21] / ((double)h[22] * 0.01) : 0.0;  // 100 MHz realtime
         if (const char* dbg = std::getenv("RSD_TRACE_PHASES"))
             if (*dbg) std::fprintf(stderr, "[rsd] row walk phase clocks: fetch %llu step %llu resolve %llu steps %llu loops %llu"
@@ -2395,6 +2414,10 @@ extern "C" rsd_status rsd_sd_trace_band(rsd_scene* scene, const rsd_camera* cam,
     return rsd_sd_trace_band_ex(scene, cam, p, d_linear_z, z_w, z_h, const_cast<uint32_t*>(d_ray_min),
                                 const_cast<uint32_t*>(d_ray_max), d_sd_out, sd_w, sd_h, band_index, band_count, 0u,
                                 counters, stream);
+}
+
+extern "C" uint32_t rsd_sd_tile_state_count(uint32_t sd_w, uint32_t sd_h) {
+    return ((sd_w + kTile - 1) / kTile) * ((sd_h + kTile - 1) / kTile);
 }
 
 extern "C" rsd_status rsd_sd_trace(rsd_scene* scene, const rsd_camera* cam, const rsd_sd_params* p,

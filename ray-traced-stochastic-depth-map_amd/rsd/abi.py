@@ -70,7 +70,8 @@ class SDParams(C.Structure):
     _fields_ = [("sample_count", C.c_uint32), ("implementation", C.c_uint32), ("max_count", C.c_uint32),
                 ("guard_band", C.c_int32), ("jitter", C.c_uint32), ("normalize", C.c_uint32),
                 ("ray_interval", C.c_uint32), ("cull_mode", C.c_uint32), ("alpha_test", C.c_uint32),
-                ("alpha", C.c_float), ("hit_order", C.c_uint32), ("use_16bit", C.c_uint32)]
+                ("alpha", C.c_float), ("hit_order", C.c_uint32), ("use_16bit", C.c_uint32),
+                ("d_tile_state", C.c_void_p)]
 
 
 class VAOData(C.Structure):
@@ -153,7 +154,8 @@ class Counters(C.Structure):
                 ("max_steps_per_ray", C.c_uint64), ("sum_ray_clocks", C.c_uint64), ("max_ray_clocks", C.c_uint64),
                 ("leaves_visited", C.c_uint64), ("walk", C.c_uint64), ("entry_lookups", C.c_uint64),
                 ("entry_items", C.c_uint64), ("step_fetch_clocks", C.c_uint64), ("step_compute_clocks", C.c_uint64),
-                ("step_pool_clocks", C.c_uint64), ("row_steps", C.c_uint64), ("shader_clock_mhz", C.c_double)]
+                ("step_pool_clocks", C.c_uint64), ("row_steps", C.c_uint64), ("shader_clock_mhz", C.c_double),
+                ("texels_clean", C.c_uint64)]
 
 
 WALK_QUAD, WALK_FUSED, WALK_SPLIT, WALK_ORDERED, WALK_RASTER = 0, 1, 2, 3, 4
@@ -168,7 +170,7 @@ WALK_KERNELS = {WALK_QUAD: ("sd_setup_kernel", "sd_trace_queue_kernel"),
 
 
 # every symbol include/rsd.h declares (checked by tests/test_abi.py)
-EXPORTS = ["rsd_abi_version", "rsd_svao_tile_count", "rsd_svao_tile_flags_release", "rsd_last_error", "rsd_device_open", "rsd_device_close", "rsd_scene_upload",
+EXPORTS = ["rsd_abi_version", "rsd_svao_tile_count", "rsd_sd_tile_state_count", "rsd_svao_tile_flags_release", "rsd_last_error", "rsd_device_open", "rsd_device_close", "rsd_scene_upload",
            "rsd_scene_info_get", "rsd_scene_release", "rsd_camera_look_at", "rsd_svao_make_vao_data",
            "rsd_gbuffer", "rsd_sd_trace", "rsd_svao_clear_intervals", "rsd_svao_pass1", "rsd_svao_pass2",
            "rsd_sd_trace_band", "rsd_svao_pass1_band", "rsd_svao_pass2_band", "rsd_gbuffer_raster",
@@ -218,6 +220,8 @@ def lib():
         L.rsd_abi_version.restype = u32
         L.rsd_svao_tile_count.restype = u32
         L.rsd_svao_tile_count.argtypes = [u32, u32, u32]
+        L.rsd_sd_tile_state_count.restype = u32
+        L.rsd_sd_tile_state_count.argtypes = [u32, u32]
         L.rsd_svao_tile_flags_release.restype = None
         L.rsd_svao_tile_flags_release.argtypes = [vp]
         L.rsd_last_error.restype = C.c_char_p

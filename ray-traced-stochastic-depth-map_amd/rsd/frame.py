@@ -296,6 +296,27 @@ class Renderer:
         svp.d_depth2 = self.depth2.data_ptr() if self.depth2 is not None else None
         self.svp = svp
 
+    def keep_clean_tiles(self, on: bool = True):
+        """Clean tiles (rsd_sd_params.d_tile_state): librsd's traces of this renderer's SD map skip rewriting the
+        8x8 tiles they left at DEFAULT_DEPTH and that have no live ray -- the same bits, a fraction of the
+        full-resolution maps' stores.  The map is then librsd's between traces: whoever writes it (or swaps it)
+        calls invalidate_sd_tiles().  A frame slot of this renderer gets a stamp buffer of its own."""
+        t = self.torch
+        sdp = abi.SDParams.from_buffer_copy(self.sdp)
+        if on:
+            n = abi.lib().rsd_sd_tile_state_count(self.sd_w, self.sd_h)
+            self.sd_tile_state = t.zeros(max(1, n), dtype=t.int32, device=self.depth.device)
+            sdp.d_tile_state = self.sd_tile_state.data_ptr()
+        else:
+            self.sd_tile_state = None
+            sdp.d_tile_state = None
+        self.sdp = sdp
+
+    def invalidate_sd_tiles(self):
+        """The SD map was written outside librsd's traces: forget which tiles hold DEFAULT_DEPTH."""
+        if getattr(self, "sd_tile_state", None) is not None:
+            self.sd_tile_state.zero_()
+
     def frame_slot(self, own_gbuffer: bool = False) -> "Renderer":
         """Another set of per-frame buffers (ao, stencil, intervals, SD map) over the same scene,
         camera and G-buffer: the state of one more frame in flight.  Frames of different slots
@@ -314,6 +335,8 @@ class Renderer:
         r.ray_min, r.ray_max = r.ray_minmax[0], r.ray_minmax[1]
         r.sd = t.empty_like(self.sd)
         r._bind_tile_flags()
+        if getattr(self, "sd_tile_state", None) is not None:
+            r.keep_clean_tiles()
         if own_gbuffer:
             r.cam = abi.Camera.from_buffer_copy(self.cam)
             r.depth = t.empty_like(self.depth)

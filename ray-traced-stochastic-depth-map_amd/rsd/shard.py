@@ -382,6 +382,10 @@ class HaloFrame:
     # ---- the partition implied by self.gb
     def _plan(self):
         b, world, me = self.b, self.world, self.rank
+        # a new split changes which SD texels this rank's traces write (and the SD replies it scatters): the
+        # renderer's clean-tile stamps are void (Renderer.keep_clean_tiles)
+        if hasattr(b, "invalidate_sd_tiles"):
+            b.invalidate_sd_tiles()
         cfg = b.cfg
         g, div, sdg, sdh = cfg.guard_band, cfg.divisor, int(b.vao.sdGuard), b.sd_h
         gb, V = self.gb, self.V
