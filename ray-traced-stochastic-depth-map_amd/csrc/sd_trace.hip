@@ -657,7 +657,9 @@ __global__ void __launch_bounds__(kSetupWaves * kBlock) sd_setup_kernel(SDArgs a
     const bool inside = x < a.sdW && y < a.sdH;
     if (a.consume && (tileRow < a.bandStart || (tileRow - a.bandStart) % a.bandStep != 0 ||
                       (tileRow - a.bandStart) / a.bandStep >= a.bandN)) {
-        if (inside) {
+        // only texels whose words are not at their reset values (8 B read instead of 8 B written: HBM reads
+        // are the cheaper direction, and most texels were never touched)
+        if (inside && (a.rayMinW[(size_t)y * a.sdW + x] != 0x7f7fffffu || a.rayMaxW[(size_t)y * a.sdW + x] != 0u)) {
             a.rayMinW[(size_t)y * a.sdW + x] = 0x7f7fffffu;  // asuint(FLT_MAX)
             a.rayMaxW[(size_t)y * a.sdW + x] = 0u;
         }
@@ -674,9 +676,12 @@ __global__ void __launch_bounds__(kSetupWaves * kBlock) sd_setup_kernel(SDArgs a
     if (inside) {
         // rayMin never lowered by pass 1 (still asuint(FLT_MAX)): TMin >= FLT_MAX > TMax, the
         // texel is dead without evaluating its ray (a.deadFast: the host proved TMax < FLT_MAX)
-        const bool untouched = a.deadFast && a.rayMin[(size_t)y * a.sdW + x] == 0x7f7fffffu;
+        const uint32_t rmin = a.rayMin[(size_t)y * a.sdW + x];
+        const bool untouched = a.deadFast && rmin == 0x7f7fffffu;
+        // consume: words already at their reset values are not rewritten (both read here, one round trip)
+        const bool atReset = a.consume && rmin == 0x7f7fffffu && a.rayMax[(size_t)y * a.sdW + x] == 0u;
         live = !untouched && sd_ray(a, x, y, d, TMin, TMax, cosT);
-        if (a.consume) {  // after the last read of this texel's interval
+        if (a.consume && !atReset) {  // after the last read of this texel's interval
             a.rayMinW[(size_t)y * a.sdW + x] = 0x7f7fffffu;
             a.rayMaxW[(size_t)y * a.sdW + x] = 0u;
         }
