@@ -516,14 +516,21 @@ def latency_floor(cnts, trace_ms):
     pool = sum(x.step_pool_clocks for x in c) / steps / mhz
     ms = max(x.max_steps_per_ray for x in c)
     floor = ms * (fetch + comp + pool)
-    return {"latency_floor_us": round(floor, 2), "latency_frac": round(floor / (trace_ms * 1e3), 3),
+    # latency-bound: the floor explains most of the trace.  Below 0.6 the launch outlasts its longest chain (the
+    # summed work sets it); above 1.05 the floor model fails the other way -- the mean step of a fully loaded launch
+    # overstates the longest rays' late steps, which run on a draining machine -- again a throughput-bound walk
+    lf = floor / (trace_ms * 1e3)
+    return {"latency_floor_us": round(floor, 2), "latency_frac": round(lf, 3),
             "latency_floor_fetch_only_us": round(ms * fetch, 2),
+            "walk_bound": "latency" if 0.6 <= lf <= 1.05 else "throughput",
             "step_us": {"fetch": round(fetch, 3), "tests_merge": round(comp, 3), "pool": round(pool, 3)},
             "max_steps_per_ray": int(ms), "shader_clock_mhz": round(mhz, 1),
             "latency_note": "floor = max_steps_per_ray x mean step time of the instrumented walk (row walk: one row "
                             "step = fetch wait + tests/merge + LDS pool; quad walk, maps above 0.6 M texels: one quad "
                             "iteration = own fetch wait + own tests and the wave's other branch + stack); "
-                            "latency_frac = floor / trace duration"}
+                            "latency_frac = floor / trace duration; walk_bound = latency for 0.6 <= latency_frac <= 1.05 (the "
+                            "longest chain sets the launch), else throughput (below: the summed work outlasts it; "
+                            "above: the loaded mean step overstates the longest rays' late steps)"}
 
 
 def pmc_traffic(csv_paths, kernel_substrs):

@@ -24,4 +24,5 @@ timeout -k 10 600 python3 -u bench.py --config "$CFG" --steps "$STEPS" --warmup 
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
     python3 bench.py --config "$CFG" --steps "$STEPS" --warmup "$WARM" --cpu-baseline-seconds 0 --hit-order-record 0 \
     > "$OUT/prof.log" 2>&1 &&
-cp "$(find "$OUT/prof" -name '*kernel_stats.csv' -print -quit)" "$OUT/kernel_stats.csv"
+cp "$(find "$OUT/prof" -name '*kernel_stats.csv' -print -quit)" "$OUT/kernel_stats.csv" &&
+cp "$(find "$OUT/prof" -name '*kernel_trace.csv' -print -quit)" "$OUT/kernel_trace.csv"
