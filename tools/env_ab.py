@@ -3,7 +3,7 @@ intervals (pass 1 once, the maps kept: no consume) timed with HIP events over `n
 alternating the settings for `reps` rounds; the SD maps of every setting must be the same bits.
 usage: python tools/env_ab.py VAR value_a value_b [config] [--n 40] [--reps 6] [--walk fused|quad]
        [--what trace|pass1|pass2] (pass1 / pass2: that pass alone, its outputs compared the same way)
-       [--hit-order canonical|traversal]"""
+       [--hit-order canonical|traversal] [--clean-tiles] (Renderer.keep_clean_tiles: the bench's SD maps)"""
 import json
 import os
 import sys
@@ -33,6 +33,8 @@ if arg("--hit-order", "canonical") == "traversal":  # the DXR-like any-hit strea
     from rsd import abi
     kw = dict(kw, hit_order=abi.HIT_ORDER_TRAVERSAL)
 r = Renderer(make_scene(sc), FrameConfig(**kw))
+if "--clean-tiles" in sys.argv:
+    r.keep_clean_tiles()
 r.gbuffer()
 r.clear_intervals()
 r.pass1()
