@@ -20,6 +20,9 @@ with L_coll = 12 us per small collective / point-to-point round (--coll-us) and 
 per xGMI peer link (--link-gbs); with F frames in flight the GPU part overlaps across frames as at
 N = 1 (factor --overlap = ms_per_step(F = 4) / one-frame GPU time, measured at N = 1 here), and the
 frame rate is bounded by max(overlapped GPU time, host issue time).
+Round 5: the product's clean SD tiles are on (Renderer.keep_clean_tiles; --no-clean-tiles: off), and the host issue
+is also measured for the native band frame (rsd_band_frame over the null communicator, librsd's own accounting:
+front + back minus the wait for the counts), the N > 1 path bench.py runs.
 usage: python tools/scaling_model.py [config] [--worlds 2,4,8] [--reps 15] [--pose i] [--sd-split auto|tiles|rows]"""
 import json
 import statistics
@@ -34,7 +37,7 @@ import torch.distributed as dist  # noqa: E402
 
 from rsd.frame import CONFIGS, DEFAULT_CAMERA_PATH, FrameConfig, Renderer, camera_path  # noqa: E402
 from rsd.scenes import make_scene  # noqa: E402
-from rsd.shard import FLT_MAX_BITS, HaloFrame  # noqa: E402
+from rsd.shard import FLT_MAX_BITS, HaloFrame, NativeComm, NativeHaloFrame  # noqa: E402
 from rsd.timing import TimingEvent  # noqa: E402
 
 
@@ -50,6 +53,8 @@ coll_us, link_gbs = float(arg("--coll-us", "12")), float(arg("--link-gbs", "50")
 sd_split = arg("--sd-split", "auto")  # HaloFrame's SD trace split: auto (its default), tiles or rows
 kw, sc = CONFIGS[name]
 r = Renderer(make_scene(sc), FrameConfig(**kw))
+if "--no-clean-tiles" not in sys.argv:
+    r.keep_clean_tiles()
 poses = camera_path(DEFAULT_CAMERA_PATH.get(name, "static"))
 if poses:
     r.set_pose(*poses[pose % len(poses)])
@@ -117,8 +122,10 @@ for world in worlds:
     for k, p in enumerate(plans):
         t1 = timed(lambda: r.pass1_rows(p.px_rows[k]), r.clear_intervals)
         r.sd.copy_(sd_full)
+        r.invalidate_sd_tiles()
         t2 = timed(p.trace, lambda: r.ray_minmax.copy_(union))  # its SD tiles (or rows)
         r.sd.copy_(sd_full)
+        r.invalidate_sd_tiles()
         t3 = timed(lambda: r.pass2_rows(p.px_rows[k]), lambda: (r.clear_intervals(), r.pass1()))
         iv = 12 * sum(touched[k])
         sdb = 4 * N * sum(touched[j][k] for j in range(world))
@@ -141,14 +148,31 @@ for world in worlds:
             f.back()
         host.append((time.perf_counter() - t0) / n * 1e6)
         torch.cuda.synchronize()
+    # the native band frame of the same ranks (bench.py's N > 1 path): librsd's host issue per frame, the time
+    # its front() / back() calls spent minus their wait for the count matrix
+    native = []
+    for k in sorted({0, world // 2}):
+        c = NativeComm.null(k, world)
+        f = NativeHaloFrame(r, c, rebalance=False, sd_split=sd_split)
+        for _ in range(23):
+            f.front()
+            f.back()
+        torch.cuda.synchronize()
+        st = f.stats()
+        native.append((st.host_front_ns + st.host_back_ns - st.host_wait_ns) / st.frames * 1e-3)
+        f.close()
+        c.close()
+    r.invalidate_sd_tiles()
     gpu = max(x["gpu_us"] for x in ranks)
     xfer = max(x["bytes"] for x in ranks) / (link_gbs * 1e3)  # bytes / (GB/s) in us
     lat = gpu + 4 * coll_us + xfer
     out["worlds"][str(world)] = {
         "ranks": ranks, "max_rank_gpu_us": round(gpu, 2), "max_rank_bytes": max(x["bytes"] for x in ranks),
         "host_issue_us_per_frame": round(max(host), 1),
+        "host_issue_native_us_per_frame": round(max(native), 1),
         "predicted_latency_us": round(lat, 1),
         "predicted_speedup_latency": round((one["gpu_us"]) / lat, 2),
         "note": "latency = max-rank GPU time + 4 collective latencies + max-rank bytes / link bandwidth; with "
-                "frames in flight the frame interval is bounded below by host_issue_us_per_frame"}
+                "frames in flight the frame interval is bounded below by the host issue (Python HaloFrame: "
+                "host_issue_us_per_frame; the native band frame bench.py runs: host_issue_native_us_per_frame)"}
 print(json.dumps(out))
