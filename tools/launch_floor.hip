@@ -25,6 +25,12 @@ __global__ void k_big(Big s, float* out) {
     if (threadIdx.x == 0 && blockIdx.x == 0 && s.v[0] < -1.0f) out[0] = s.v[511];
 }
 
+// four distinct kernels with 2 KB arguments, launched round robin (a frame's pass 1 / setup / walk / pass 2)
+template <int I>
+__global__ void k_big_n(Big s, float* out) {
+    if (threadIdx.x == 0 && blockIdx.x == 0 && s.v[0] < -1.0f) out[I] = s.v[511];
+}
+
 #define CHECK(x)                                                              \
     do {                                                                      \
         hipError_t e_ = (x);                                                  \
@@ -79,6 +85,32 @@ int main() {
     CHECK(hipHostMalloc((void**)&hpin, 9 * 8 * 8, hipHostMallocDefault));
     const double d2h = per_call_us(s, [&] { (void)hipMemcpyAsync(hpin, dsrc, 9 * 8 * 8, hipMemcpyDeviceToHost, s); });
     const double mset = per_call_us(s, [&] { (void)hipMemsetAsync(dsrc, 0, 9 * 8 * 8, s); });
+    // 4 distinct kernels round robin (per launch), and the same through hipModuleLaunchKernel on function handles
+    // looked up once (hipGetFuncBySymbol), the arguments passed as one buffer (HIP_LAUNCH_PARAM_BUFFER_POINTER)
+    int rr = 0;
+    const double rr4 = per_call_us(s, [&] {
+        switch (rr++ & 3) {
+            case 0: hipLaunchKernelGGL(k_big_n<0>, dim3(8160), dim3(256), 0, s, bg, out); break;
+            case 1: hipLaunchKernelGGL(k_big_n<1>, dim3(8160), dim3(256), 0, s, bg, out); break;
+            case 2: hipLaunchKernelGGL(k_big_n<2>, dim3(8160), dim3(256), 0, s, bg, out); break;
+            default: hipLaunchKernelGGL(k_big_n<3>, dim3(8160), dim3(256), 0, s, bg, out); break;
+        }
+    });
+    hipFunction_t fh[4];
+    CHECK(hipGetFuncBySymbol(&fh[0], reinterpret_cast<const void*>(&k_big_n<0>)));
+    CHECK(hipGetFuncBySymbol(&fh[1], reinterpret_cast<const void*>(&k_big_n<1>)));
+    CHECK(hipGetFuncBySymbol(&fh[2], reinterpret_cast<const void*>(&k_big_n<2>)));
+    CHECK(hipGetFuncBySymbol(&fh[3], reinterpret_cast<const void*>(&k_big_n<3>)));
+    struct {
+        Big b;
+        float* o;
+    } argbuf{bg, out};
+    size_t argsz = sizeof(argbuf);
+    void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &argbuf, HIP_LAUNCH_PARAM_BUFFER_SIZE, &argsz, HIP_LAUNCH_PARAM_END};
+    rr = 0;
+    const double mod4 = per_call_us(s, [&] {
+        (void)hipModuleLaunchKernel(fh[rr++ & 3], 8160, 1, 1, 256, 1, 1, 0, s, nullptr, cfg);
+    });
     // librsd's per-call host helpers: one getenv of a tuning variable, the "%f" round trip of RAY_CONE_SPREAD
     volatile const char* sink = nullptr;
     const double genv = per_call_us(s, [&] { sink = std::getenv("RSD_PASS2_LOOP"); });
@@ -94,7 +126,8 @@ int main() {
     std::printf("{\"launch_us_args64\": %.2f, \"launch_us_args2048\": %.2f, \"event_record_us\": %.2f, "
                 "\"event_record_timing_us\": %.2f, \"get_last_error_us\": %.3f, \"get_device_us\": %.3f, "
                 "\"memcpy_d2h_pinned_576B_us\": %.2f, \"memset_576B_us\": %.2f, \"getenv_us\": %.3f, "
-                "\"cone_spread_format_us\": %.3f}\n",
-                small, big, rec, rect, gle, gd, d2h, mset, genv, spread);
+                "\"cone_spread_format_us\": %.3f, \"launch_us_4kernels_args2048\": %.2f, "
+                "\"module_launch_us_4kernels_args2048\": %.2f}\n",
+                small, big, rec, rect, gle, gd, d2h, mset, genv, spread, rr4, mod4);
     return 0;
 }
