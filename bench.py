@@ -362,10 +362,13 @@ def main():
     # DXR-like any-hit order (rsd_hit_order TRAVERSAL): the same latency region with
     # the traversal-order hit stream -- the mode closest to the reference's DXR semantics
     # (Common.slangh:137-151: the reservoir samples among the hits in traversal order)
-    hit_trav = None
+    hit_trav = hit_wave = None
     if world == 1 and args.hit_order_record:
         hit_trav = hit_order_record(r, HaloFrame, new_ev, min(args.steps, 50), min(args.warmup, 5), pose,
                                     rays, rays_active)
+        # the wavefront order (round 5): the same stochastic semantics on the row walk's traversal
+        hit_wave = hit_order_record(r, HaloFrame, new_ev, min(args.steps, 50), min(args.warmup, 5), pose,
+                                    rays, rays_active, order=abi.HIT_ORDER_WAVEFRONT)
 
     if rank != 0:
         close_frames([seq] + slots, comms)
@@ -441,6 +444,7 @@ def main():
                                          final_split_groups=list(seq.gb))
         if shard == "band" and world > 1 else None,
         "hit_order_traversal": hit_trav,
+        "hit_order_wavefront": hit_wave,
         "bvh_build_s": round(bvh_build_s, 3),
         "bvh_build_threads": int(r.gscene.info.build_threads),
         "cpu_baseline": cpu,
@@ -460,18 +464,20 @@ def close_frames(frames, comms):
         c.close()
 
 
-def hit_order_record(r, frame_cls, new_ev, steps, warmup, pose, rays, rays_active):
-    """The latency region with the traversal-order hit stream (rsd.h RSD_HIT_ORDER_TRAVERSAL: a
-    depth-first walk of the 4-wide BVH delivering each triangle once in leaf order, a commit shrinking
-    TMax -- DXR's any-hit semantics, StochasticDepthMapRT.rt.slang:83-88): SD-trace time, dispatched /
-    active Mrays/s and the AO span over `steps` frames, one in flight."""
+def hit_order_record(r, frame_cls, new_ev, steps, warmup, pose, rays, rays_active, order=None):
+    """The latency region with a DXR-like hit stream (rsd.h RSD_HIT_ORDER_TRAVERSAL: a depth-first walk of the
+    4-wide BVH delivering each triangle once in leaf order, a commit shrinking TMax -- DXR's any-hit semantics,
+    StochasticDepthMapRT.rt.slang:83-88; or RSD_HIT_ORDER_WAVEFRONT: the same semantics over the 8-wide
+    wavefront traversal of the row walk): SD-trace time, dispatched / active Mrays/s and the AO span over
+    `steps` frames, one in flight."""
     import numpy as np
     import torch
 
     from rsd import abi
+    order = abi.HIT_ORDER_TRAVERSAL if order is None else order
     keep = r.sdp
     sdp = abi.SDParams.from_buffer_copy(keep)
-    sdp.hit_order = abi.HIT_ORDER_TRAVERSAL
+    sdp.hit_order = order
     r.sdp = sdp
     try:
         fr = frame_cls(r)
@@ -490,12 +496,14 @@ def hit_order_record(r, frame_cls, new_ev, steps, warmup, pose, rays, rays_activ
         ao_ms = float(np.mean([a.elapsed_time(b) for a, b in ev_ao]))
     finally:
         r.sdp = keep
-    return {"frames": steps, "walk": "ordered", "sd_kernel_ms": round(sd_ms, 4),
+    name = {abi.HIT_ORDER_TRAVERSAL: ("ordered", "RSD_HIT_ORDER_TRAVERSAL", "sd_trace_ordered_kernel"),
+            abi.HIT_ORDER_WAVEFRONT: ("wavefront", "RSD_HIT_ORDER_WAVEFRONT", "sd_trace_wavefront_kernel")}[order]
+    return {"frames": steps, "walk": name[0], "sd_kernel_ms": round(sd_ms, 4),
             "mrays_per_s": round(rays / (sd_ms * 1e-3) / 1e6, 1),
             "active_mrays_per_s": round(rays_active / (sd_ms * 1e-3) / 1e6, 2),
             "ao_span_ms": round(ao_ms, 4), "ao_frames_per_s": round(1e3 / ao_ms, 1),
-            "note": "latency region with rsd_sd_params.hit_order = RSD_HIT_ORDER_TRAVERSAL (DXR-like any-hit "
-                    "order, sd_trace_ordered_kernel); the headline value keeps the canonical order"}
+            "note": f"latency region with rsd_sd_params.hit_order = {name[1]} (DXR-like any-hit order, {name[2]}); "
+                    "the headline value keeps the canonical order"}
 
 
 def latency_floor(cnts, trace_ms):

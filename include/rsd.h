@@ -136,7 +136,7 @@ typedef struct {
 
 /* Any-hit order of the SD trace.  DXR calls any-hit in an implementation-defined traversal order
  * (Common.slangh:136-153 under RAY_FLAG_FORCE_NON_OPAQUE, StochasticDepthMapRT.rt.slang:83-88),
- * so two orders are defined:
+ * so three orders are defined:
  *   CANONICAL  ascending (t, primitive id), each triangle once -- independent of the BVH; the
  *              result depends only on the MAX_COUNT nearest hits (Default == KBuffer on opaque
  *              geometry: the reservoir never replaces a slot).
@@ -145,8 +145,16 @@ typedef struct {
  *              once; a committed hit (algorithm returns true = DXR AcceptHit) shrinks the ray's
  *              TMax to its t and later hits must be nearer (t < TMax), like DXR's RayTCurrent().
  *              The reservoir samples stochastically; the result depends on the BVH
- *              (rsd_scene_export_bvh gives the oracle the same tree). */
-typedef enum { RSD_HIT_ORDER_CANONICAL = 0, RSD_HIT_ORDER_TRAVERSAL = 1 } rsd_hit_order;
+ *              (rsd_scene_export_bvh gives the oracle the same tree).
+ *   WAVEFRONT  the order of an 8-wide wavefront walk of the same tree (round 5, the canonical row walk's
+ *              traversal): per step up to 8 items, each tested by its own lane against the TMax of the
+ *              step's start; the step's leaf hits go to any-hit in lane order, a leaf's triangles in
+ *              record order, with the same commit rule (t < TMax after a commit); surviving children
+ *              are pushed nearest-on-top per lane (lanes in order) onto a LIFO pool, from which the next
+ *              step pops up to 8 items (one while the pool holds more than min(208 - 3 depth, 160) items,
+ *              depth = rsd_scene_info.wide_depth).  Stochastic like TRAVERSAL; about the canonical
+ *              walk's speed instead of half of it. */
+typedef enum { RSD_HIT_ORDER_CANONICAL = 0, RSD_HIT_ORDER_TRAVERSAL = 1, RSD_HIT_ORDER_WAVEFRONT = 2 } rsd_hit_order;
 
 /* VAOData.slang:33-45 mirror */
 typedef struct {
@@ -249,6 +257,7 @@ typedef struct {
 #define RSD_WALK_FUSED 1u  /* sd_trace_row_kernel with the algorithm in-kernel */
 #define RSD_WALK_SPLIT 2u  /* sd_trace_row_kernel (K nearest keys) + sd_resolve_row_kernel */
 #define RSD_WALK_ORDERED 3u /* sd_trace_ordered_kernel: RSD_HIT_ORDER_TRAVERSAL */
+#define RSD_WALK_WAVEFRONT 5u /* sd_trace_wavefront_kernel: RSD_HIT_ORDER_WAVEFRONT */
 #define RSD_WALK_RASTER 4u  /* sd_raster_kernel (triangles -> K nearest keys per texel) + sd_resolve_row_kernel */
 
 /* --- library / device ------------------------------------------------------------ */

@@ -82,6 +82,8 @@ def lib():
         L.ocpu_sd_trace_band.argtypes = [vp, vp, vp, vp, u32, u32, vp, vp, vp, u32, u32, u32, u32, u32, u32, i32, vp]
         L.ocpu_sd_trace_ordered.argtypes = [vp, vp, u32, vp, vp, vp, u32, u32, vp, vp, vp, u32, u32, u32, u32, u32, u32,
                                             i32, vp]
+        L.ocpu_sd_trace_wavefront.argtypes = [vp, vp, u32, u32, vp, vp, vp, u32, u32, vp, vp, vp, u32, u32, u32, u32, u32,
+                                              u32, i32, vp]
         L.ocpu_svao_pass1_band.argtypes = [vp, vp, vp, vp, vp, u32, u32, vp, vp, vp, vp, u32, u32, u32, u32]
         L.ocpu_svao_pass1_rows.argtypes = [vp, vp, vp, vp, vp, u32, u32, vp, vp, vp, vp, u32, u32, u32, u32]
         L.ocpu_svao_pass2_rows.argtypes = [vp, vp, vp, vp, vp, u32, u32, vp, vp, u32, u32, vp, u32, u32, i32]
@@ -261,6 +263,23 @@ def sd_trace_ordered(scene: Scene, bvh, tri_offset, cam: Camera, params: SDParam
     lib().ocpu_sd_trace_ordered(scene.h, _p(b), int(tri_offset), C.byref(cam), C.byref(params), _p(lz), lz.shape[1],
                                 lz.shape[0], _p(rayMin), _p(rayMax), _p(sd), sdW, sdH, r0, r1, band[0], band[1],
                                 _threads(threads), _p(stats))
+    return sd, stats
+
+
+def sd_trace_wavefront(scene: Scene, bvh, tri_offset, pool_soft, cam: Camera, params: SDParams, linearZ, rayMin, rayMax,
+                       sdW, sdH, rows=None, band=(0, 1), threads=None):
+    """The SD trace over librsd's wavefront any-hit stream (rsd.h RSD_HIT_ORDER_WAVEFRONT) of librsd's own BVH;
+    pool_soft = min(208 - 3 wide_depth, 160) (rsd_scene_info.wide_depth), the pool bound its order depends on."""
+    N = params.sample_count
+    ch, layers = min(N, 4), (N + 3) // 4
+    sd = np.zeros((layers, sdH, sdW, ch), np.float32)
+    r0, r1 = rows if rows else (0, sdH)
+    stats = np.zeros(2, np.uint64)
+    lz = np.ascontiguousarray(linearZ, np.float32)
+    b = np.ascontiguousarray(bvh, np.float32)
+    lib().ocpu_sd_trace_wavefront(scene.h, _p(b), int(tri_offset), int(pool_soft), C.byref(cam), C.byref(params), _p(lz),
+                                  lz.shape[1], lz.shape[0], _p(rayMin), _p(rayMax), _p(sd), sdW, sdH, r0, r1, band[0],
+                                  band[1], _threads(threads), _p(stats))
     return sd, stats
 
 

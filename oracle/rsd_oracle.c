@@ -1154,6 +1154,121 @@ static uint64_t o_ordered_walk(const oscene* s, const float* bvh, uint32_t triOf
     return delivered;
 }
 
+/* ---- wavefront any-hit stream (rsd.h RSD_HIT_ORDER_WAVEFRONT) -------------------------------
+ * The other order librsd defines (librsd csrc/sd_trace.hip sd_trace_wavefront_kernel): the canonical row walk's
+ * traversal of the exported 4-wide BVH, 8 work items per step.  Per step every held item is tested against the
+ * TMax of the step's start (a node's 4 children, sorted by entry distance with the 5-exchange network; a leaf's
+ * triangles); the step's candidate hits go to any-hit in lane order, a leaf's triangles in record order, each
+ * against the current TMax with the commit rule of o_ordered_walk; then each lane's children with entry
+ * distance <= TMax are pushed, lane after lane, nearest on top of its own group, onto a LIFO pool, and the next
+ * step pops min(pool, pool <= soft ? 8 : 1) entries into lanes 0.. (an entry beyond TMax pops as nothing).
+ * The walk starts with the root in lane 0 and ends when the pool and the lanes are empty. */
+static uint64_t o_wavefront_walk(const oscene* s, const float* bvh, uint32_t triOff, uint32_t soft, const ocam* c,
+                                 const osd_params* p, const float d[3], float TMin, float TMax, float cosT,
+                                 float spread, const int32_t* lutIdx, const uint32_t* lut, float* depths,
+                                 uint32_t* count)
+{
+    enum { LANES = 8, POOL = 256 };
+    const uint32_t LEAF = 0x80000000u, OFF = 0x1fffffffu, NONE = 0xffffffffu;
+    const uint32_t N = p->sample_count;
+    oray r;
+    o_ray_setup(&r, c->posW, d);
+    obox_ray b;
+    o_box_setup(&b, c->posW, d);
+    uint32_t poolItem[POOL];
+    float poolT[POOL];
+    int pool = 0, committed = 0;
+    float tCur = TMax;
+    uint64_t delivered = 0;
+    uint32_t item[LANES];
+    for (int l = 0; l < LANES; ++l) item[l] = NONE;
+    item[0] = 0; /* root */
+    for (;;) {
+        const float thi0 = tCur;
+        float ck[LANES][4];
+        uint32_t ci[LANES][4];
+        int nc[LANES];
+        for (int l = 0; l < LANES; ++l) {
+            nc[l] = 0;
+            for (int j = 0; j < 4; ++j) { ck[l][j] = INFINITY; ci[l][j] = NONE; }
+            if (item[l] == NONE || (item[l] & LEAF)) continue;
+            const float* nb = bvh + 4u * (item[l] & OFF);
+            for (int q = 0; q < 4; ++q) {
+                const uint32_t ref = o_asuint(nb[24 + q]), cnt = o_asuint(nb[28 + q]);
+                float tn = 0.0f;
+                const int hit = ref != NONE && o_box4(&b, nb[q], nb[4 + q], nb[8 + q], nb[12 + q], nb[16 + q],
+                                                      nb[20 + q], TMin, thi0, &tn);
+                ck[l][q] = hit ? tn : INFINITY;
+                ci[l][q] = hit ? (cnt ? (LEAF | ((cnt - 1u) << 29) | (triOff + 3u * ref)) : 8u * ref) : NONE;
+                nc[l] += hit;
+            }
+            o_cswap4(ck[l], ci[l], 0, 1); o_cswap4(ck[l], ci[l], 2, 3);
+            o_cswap4(ck[l], ci[l], 0, 2); o_cswap4(ck[l], ci[l], 1, 3);
+            o_cswap4(ck[l], ci[l], 1, 2);
+        }
+        /* the step's leaf candidates, tested against thi0, delivered lane by lane */
+        for (int l = 0; l < LANES; ++l) {
+            if (item[l] == NONE || !(item[l] & LEAF)) continue;
+            const uint32_t off = item[l] & OFF, n = ((item[l] >> 29) & 3u) + 1u;
+            float ct[4], cr[4], cz[4];
+            int cv[4], caf[4];
+            for (uint32_t q = 0; q < 4; ++q) {
+                cv[q] = 0;
+                if (q >= n) continue;
+                const float* tp = bvh + 4u * (off + 3u * q);
+                float t, bu, bv, det;
+                if (!o_intersect_tri(&r, tp, tp + 4, tp + 8, &t, &bu, &bv, &det)) continue;
+                if (!(t >= TMin) || !(t <= thi0)) continue;
+                const uint32_t prim = o_asuint(tp[3]), flags = o_asuint(tp[7]);
+                if (o_culled(det, flags, p->cull_mode)) continue; /* ray flags: before any-hit */
+                cv[q] = 1;
+                ct[q] = t;
+                cr[q] = ocpu_hash(bu, bv);
+                float z = t * cosT; /* RayToViewDepth */
+                if (p->normalize) z = o_saturate((z - c->nearZ) / (c->farZ - c->nearZ));
+                cz[q] = z;
+                caf[q] = p->alpha_test && o_alpha_masked(s, prim) && ocpu_alpha_fails(s, prim, bu, bv, 1, t, d, spread);
+            }
+            for (uint32_t q = 0; q < 4; ++q) {
+                if (!cv[q] || (committed ? !(ct[q] < tCur) : !(ct[q] <= tCur))) continue;
+                delivered++;
+                if (o_any_hit(p, N, lutIdx, lut, depths, count, cr[q], cz[q], caf[q])) {
+                    tCur = ct[q]; /* AcceptHit: TMax = t */
+                    committed = 1;
+                }
+            }
+        }
+        /* push: lane l's kept children above lanes 0..l-1's, its nearest child on top of its group */
+        const float thi = tCur;
+        int pre = 0;
+        for (int l = 0; l < LANES; ++l) {
+            int keep = 0;
+            for (int j = 0; j < 4; ++j) keep += (j < nc[l] && ck[l][j] <= thi) ? 1 : 0;
+            if (pool + pre + keep > POOL) abort(); /* librsd's pool bound makes this unreachable */
+            for (int j = 0; j < keep; ++j) {
+                poolItem[pool + pre + (keep - 1 - j)] = ci[l][j];
+                poolT[pool + pre + (keep - 1 - j)] = ck[l][j];
+            }
+            pre += keep;
+        }
+        pool += pre;
+        /* pop */
+        const int lim = pool <= (int)soft ? LANES : 1, take = pool < lim ? pool : lim;
+        int any = 0;
+        for (int l = 0; l < LANES; ++l) {
+            item[l] = NONE;
+            if (l < take) {
+                const uint32_t it = poolItem[pool - 1 - l];
+                item[l] = poolT[pool - 1 - l] <= thi ? it : NONE;
+            }
+            any |= item[l] != NONE;
+        }
+        pool -= take;
+        if (pool == 0 && !any) break;
+    }
+    return delivered;
+}
+
 typedef struct {
     const oscene* s; const ocam* c; const osd_params* p;
     const float* z; uint32_t zW, zH;
@@ -1162,7 +1277,8 @@ typedef struct {
     uint32_t y0, y1;
     uint32_t bi, bc; /* band: 8-row tile rows t with t % bc == bi */
     uint64_t active, hits;
-    const float* bvh; uint32_t triOff; /* p->hit_order == 1: librsd's exported BVH */
+    const float* bvh; uint32_t triOff; /* p->hit_order 1 / 2: librsd's exported BVH */
+    uint32_t soft;                      /* p->hit_order 2: librsd's pool bound (rsd.h WAVEFRONT) */
 } osd_job;
 
 static void* o_sd_rows(void* arg)
@@ -1193,7 +1309,11 @@ static void* o_sd_rows(void* arg)
             for (uint32_t i = 0; i < N; ++i) depths[i] = DEFAULT;
             uint32_t count = 0;
 
-            if (TMin <= TMax && p->hit_order == 1) {
+            if (TMin <= TMax && p->hit_order == 2) {
+                j->active++;
+                j->hits += o_wavefront_walk(j->s, j->bvh, j->triOff, j->soft, c, p, d, TMin, TMax, cosT, spread, lutIdx,
+                                            lut, depths, &count);
+            } else if (TMin <= TMax && p->hit_order == 1) {
                 j->active++;
                 j->hits += o_ordered_walk(j->s, j->bvh, j->triOff, c, p, d, TMin, TMax, cosT, spread, lutIdx, lut,
                                           depths, &count);
@@ -1242,7 +1362,7 @@ void ocpu_sd_trace(const oscene* s, const ocam* cam, const osd_params* p,
     ocpu_sd_trace_band(s, cam, p, linearZ, zW, zH, rayMin, rayMax, sd, sdW, sdH, row0, row1, 0, 1, nthreads, stats);
 }
 
-static void o_sd_trace_impl(const oscene* s, const float* bvh, uint32_t triOff, const ocam* cam,
+static void o_sd_trace_impl(const oscene* s, const float* bvh, uint32_t triOff, uint32_t soft, const ocam* cam,
                             const osd_params* p, const float* linearZ, uint32_t zW, uint32_t zH,
                             const uint32_t* rayMin, const uint32_t* rayMax, float* sd, uint32_t sdW, uint32_t sdH,
                             uint32_t row0, uint32_t row1, uint32_t band_index, uint32_t band_count, int nthreads,
@@ -1257,7 +1377,7 @@ void ocpu_sd_trace_band(const oscene* s, const ocam* cam, const osd_params* p,
 {
     osd_params q = *p;
     q.hit_order = 0; /* the canonical stream (ocpu_sd_trace_ordered for the traversal order) */
-    o_sd_trace_impl(s, NULL, 0, cam, &q, linearZ, zW, zH, rayMin, rayMax, sd, sdW, sdH, row0, row1, band_index,
+    o_sd_trace_impl(s, NULL, 0, 0, cam, &q, linearZ, zW, zH, rayMin, rayMax, sd, sdW, sdH, row0, row1, band_index,
                     band_count, nthreads, stats);
 }
 
@@ -1269,11 +1389,23 @@ void ocpu_sd_trace_ordered(const oscene* s, const float* bvh, uint32_t tri_offse
 {
     osd_params q = *p;
     q.hit_order = 1;
-    o_sd_trace_impl(s, bvh, tri_offset, cam, &q, linearZ, zW, zH, rayMin, rayMax, sd, sdW, sdH, row0, row1,
+    o_sd_trace_impl(s, bvh, tri_offset, 0, cam, &q, linearZ, zW, zH, rayMin, rayMax, sd, sdW, sdH, row0, row1,
                     band_index, band_count, nthreads, stats);
 }
 
-static void o_sd_trace_impl(const oscene* s, const float* bvh, uint32_t triOff, const ocam* cam,
+void ocpu_sd_trace_wavefront(const oscene* s, const float* bvh, uint32_t tri_offset, uint32_t pool_soft,
+                             const ocam* cam, const osd_params* p, const float* linearZ, uint32_t zW, uint32_t zH,
+                             const uint32_t* rayMin, const uint32_t* rayMax, float* sd, uint32_t sdW, uint32_t sdH,
+                             uint32_t row0, uint32_t row1, uint32_t band_index, uint32_t band_count, int nthreads,
+                             uint64_t* stats)
+{
+    osd_params q = *p;
+    q.hit_order = 2;
+    o_sd_trace_impl(s, bvh, tri_offset, pool_soft, cam, &q, linearZ, zW, zH, rayMin, rayMax, sd, sdW, sdH, row0, row1,
+                    band_index, band_count, nthreads, stats);
+}
+
+static void o_sd_trace_impl(const oscene* s, const float* bvh, uint32_t triOff, uint32_t soft, const ocam* cam,
                             const osd_params* p, const float* linearZ, uint32_t zW, uint32_t zH,
                             const uint32_t* rayMin, const uint32_t* rayMax, float* sd, uint32_t sdW, uint32_t sdH,
                             uint32_t row0, uint32_t row1, uint32_t band_index, uint32_t band_count, int nthreads,
@@ -1287,7 +1419,7 @@ static void o_sd_trace_impl(const oscene* s, const float* bvh, uint32_t triOff, 
         jobs[i].rmin = rayMin; jobs[i].rmax = rayMax;
         jobs[i].sd = sd; jobs[i].sdW = sdW; jobs[i].sdH = sdH;
         jobs[i].bi = band_index; jobs[i].bc = band_count ? band_count : 1;
-        jobs[i].bvh = bvh; jobs[i].triOff = triOff;
+        jobs[i].bvh = bvh; jobs[i].triOff = triOff; jobs[i].soft = soft;
     }
     if (row1 > sdH) row1 = sdH;
     o_run_rows(o_sd_rows, jobs, sizeof(osd_job), row0, row1, nthreads, o_sd_setrows);

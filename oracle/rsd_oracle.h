@@ -58,7 +58,8 @@ typedef struct {
     uint32_t cull_mode;      /* 0 None, 1 Back, 2 Front */
     uint32_t alpha_test;     /* USE_ALPHA_TEST (opaque scenes: no-op) */
     float    alpha;          /* ALPHA (coverage mask) */
-    uint32_t hit_order;      /* rsd_hit_order: 0 canonical (ocpu_sd_trace), 1 traversal (ocpu_sd_trace_ordered) */
+    uint32_t hit_order;      /* rsd_hit_order: 0 canonical (ocpu_sd_trace), 1 traversal (ocpu_sd_trace_ordered),
+                                2 wavefront (ocpu_sd_trace_wavefront) */
     uint32_t use_16bit;      /* not read by the oracle (tests round the f32 map to binary16 in numpy) */
 } osd_params;
 
@@ -144,6 +145,13 @@ void ocpu_sd_trace_ordered(const oscene* s, const float* bvh, uint32_t tri_offse
                            const uint32_t* rayMin, const uint32_t* rayMax, float* sd, uint32_t sdW, uint32_t sdH,
                            uint32_t row0, uint32_t row1, uint32_t band_index, uint32_t band_count, int nthreads,
                            uint64_t* stats);
+/* The wavefront any-hit stream (rsd.h RSD_HIT_ORDER_WAVEFRONT) over librsd's exported BVH; pool_soft =
+ * min(208 - 3 wide_depth, 160) as librsd computes it (rsd_scene_info.wide_depth). */
+void ocpu_sd_trace_wavefront(const oscene* s, const float* bvh, uint32_t tri_offset, uint32_t pool_soft,
+                             const ocam* cam, const osd_params* p, const float* linearZ, uint32_t zW, uint32_t zH,
+                             const uint32_t* rayMin, const uint32_t* rayMax, float* sd, uint32_t sdW, uint32_t sdH,
+                             uint32_t row0, uint32_t row1, uint32_t band_index, uint32_t band_count, int nthreads,
+                             uint64_t* stats);
 
 /* the SD ray of texel (x, y): origin+direction, TMin, TMax and cosT (for tests) */
 void ocpu_sd_ray(const ocam* c, const osd_params* p, const float* z, uint32_t zW, uint32_t zH,

@@ -62,7 +62,7 @@ const std::initializer_list<const char*> kDepthModeNames = {"SingleDepth", "Dual
                                                             "Raytraced"};  // VAO/DepthMode.h
 const std::initializer_list<const char*> kImplNames = {"Default", "CoverageMask", "ReservoirSampling",
                                                        "KBuffer"};  // StochasticDepthImplementation.h
-const std::initializer_list<const char*> kHitOrderNames = {"Canonical", "Traversal"};  // rsd.h rsd_hit_order
+const std::initializer_list<const char*> kHitOrderNames = {"Canonical", "Traversal", "Wavefront"};  // rsd.h rsd_hit_order
 const std::initializer_list<const char*> kNumericsNames = {"Fast", "Exact"};  // rsd.h rsd_numerics
 const std::initializer_list<const char*> kAoKernelNames = {"VAO", "HBAO"};    // AOKernel.h -> rsd_ao_kernel
 
@@ -234,7 +234,7 @@ public:
         prm_.guard_band = (int32_t)p.getInt("GuardBand", 0);
         prm_.max_count = (uint32_t)p.getInt("MaxCount", 8);
         prm_.use_16bit = p.getBool("Use16Bit", false);
-        // librsd extension: "HitOrder" = "Canonical" (default) | "Traversal" (rsd.h rsd_hit_order)
+        // librsd extension: "HitOrder" = "Canonical" (default) | "Traversal" | "Wavefront" (rsd.h rsd_hit_order)
         prm_.hit_order = enumProp(p, "HitOrder", kHitOrderNames, 0);
         if (p.getBool("StoreNormals", false))  // StochasticDepthMapRT.cpp:198-203
             throw Unsupported("StochasticDepthMapRT: Storing normals is not supported yet");

@@ -1723,6 +1723,209 @@ __global__ void __launch_bounds__(kBlock) sd_trace_row_kernel(SDArgs a, const fl
     }
 }
 
+// Wavefront traversal-order any-hit stream (rsd_sd_params.hit_order = RSD_HIT_ORDER_WAVEFRONT, rsd.h): the
+// canonical row walk's traversal -- a row of 8 lanes per ray, each lane one work item per step, the surviving
+// children pushed nearest-on-top onto the ray's LIFO pool in LDS and up to 8 popped per step (1 while the pool
+// is above poolSoft) -- but every candidate hit goes to any-hit as the walk finds it: per step the lanes' leaves
+// in lane order, a leaf's triangles in record order; a committed hit sets TMax = t (AcceptHit), later
+// candidates need t < TMax, and boxes are tested against the TMax of the step's start.  Like the depth-first
+// order (sd_trace_ordered_kernel) it is one definition of DXR's implementation-defined order, walked from the
+// root (no entry grid: the frontier would reorder the stream); the oracle restates it step for step
+// (oracle/rsd_oracle.c o_wavefront_walk) over the exported BVH.  Rows stride over the live-ray queue as the
+// canonical row walk does (longest-first partitions).
+template <int N>
+__global__ void __launch_bounds__(kBlock) sd_trace_wavefront_kernel(SDArgs a, const float4* __restrict__ queue,
+                                                                    uint32_t* __restrict__ qctl) {
+    constexpr int kRow = 8, kRowRays = kBlock / kRow, POOL = kPoolCap;
+    __shared__ uint32_t sItem[kRowRays * POOL];
+    __shared__ float sT[kRowRays * POOL];
+    const int lane = threadIdx.x;
+    const int l = lane & (kRow - 1), base = lane & ~(kRow - 1), row = lane / kRow;
+    uint32_t* pItem = sItem + row * POOL;
+    float* pT = sT + row * POOL;
+    const uint32_t part = blockIdx.x % kQueueParts, wavesPerPart = gridDim.x / kQueueParts;
+    const uint32_t nLong = __hip_atomic_load(&qctl[part], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t count = nLong + (a.lpt ? __hip_atomic_load(&qctl[kQctlShort + part], __ATOMIC_RELAXED,
+                                                               __HIP_MEMORY_SCOPE_AGENT) : 0u);
+    const rsd_camera& c = a.cam;
+    const float DEFAULT = a.normalize ? 1.0f : 3.40282347e+37f;  // Common.slangh:16
+    const int soft = a.poolSoft;
+    constexpr int kFetch = 0, kTrace = 1, kExit = 2;
+    int phase = kFetch;
+    bool first = true;
+    int x = 0, y = 0, pool = 0;
+    RayCtx r;
+    float TMin = 0.0f, TMax = 0.0f, cosT = 0.0f, tCur = 0.0f;
+    bool committed = false;
+    float depths[N];
+    uint32_t cnt = 0, item = kNoItem;
+    TraceStats st{0u, 0u, 0u};
+    uint32_t active = 0, delivered = 0, raySteps = 0, maxSteps = 0;
+    while (__ballot(phase != kExit) != 0ull) {
+        if (phase == kFetch) {
+            uint32_t qi;
+            if (first) {
+                qi = (blockIdx.x / kQueueParts) * (uint32_t)kRowRays + (uint32_t)row;
+                first = false;
+            } else {
+                uint32_t h = 0;
+                if (l == 0) h = atomicAdd(&qctl[kQueueParts + part], 1u);
+                qi = wavesPerPart * (uint32_t)kRowRays + __shfl(h, base);
+            }
+            if (qi >= count) {
+                phase = kExit;
+            } else {
+                f3 d;
+                uint32_t idx;
+                ray_rec_load(queue, queue_slot(a, part, qi, nLong), d, TMin, TMax, cosT, idx);
+                x = (int)(idx % (uint32_t)a.sdW);
+                y = (int)(idx / (uint32_t)a.sdW);
+                ray_setup(r, mk(c.posW[0], c.posW[1], c.posW[2]), d);
+#pragma unroll
+                for (int i = 0; i < N; ++i) depths[i] = DEFAULT;
+                cnt = 0u;
+                tCur = TMax;  // RayTCurrent()
+                committed = false;
+                pool = 0;
+                item = l == 0 ? 0u : kNoItem;  // the root
+                phase = kTrace;
+                active += l == 0;
+                raySteps = 0;
+            }
+        }
+        if (phase != kTrace) continue;
+
+        // ---- one step of this row: every box against the TMax of the step's start
+        const float thi0 = tCur;
+        float ck[4];
+        uint32_t ci[4];
+        int nc = 0;
+        const float4* p = a.nodes + (item & kOffMask);
+        float4 q[12];
+        const bool isLeaf = item != kNoItem && (item & kLeafBit);
+        if (item != kNoItem) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) q[j] = p[j];
+            if (isLeaf && (item >> 29 & 3u) >= 2u) {
+#pragma unroll
+                for (int j = 8; j < 12; ++j) q[j] = p[j];
+            }
+        }
+        if (item != kNoItem && !isLeaf) {
+            st.nodes++;
+            const uint32_t rf[4] = {__float_as_uint(q[6].x), __float_as_uint(q[6].y), __float_as_uint(q[6].z),
+                                    __float_as_uint(q[6].w)};
+            const uint32_t cn[4] = {__float_as_uint(q[7].x), __float_as_uint(q[7].y), __float_as_uint(q[7].z),
+                                    __float_as_uint(q[7].w)};
+            const float lox[4] = {q[0].x, q[0].y, q[0].z, q[0].w}, hix[4] = {q[1].x, q[1].y, q[1].z, q[1].w};
+            const float loy[4] = {q[2].x, q[2].y, q[2].z, q[2].w}, hiy[4] = {q[3].x, q[3].y, q[3].z, q[3].w};
+            const float loz[4] = {q[4].x, q[4].y, q[4].z, q[4].w}, hiz[4] = {q[5].x, q[5].y, q[5].z, q[5].w};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                float tn;
+                const bool h = rf[j] != kNoItem && box_hit(r, lox[j], hix[j], loy[j], hiy[j], loz[j], hiz[j], TMin,
+                                                          thi0, tn);
+                ck[j] = h ? tn : INFINITY;
+                ci[j] = h ? (cn[j] ? (kLeafBit | ((cn[j] - 1u) << 29) | (a.triOff + 3u * rf[j])) : 8u * rf[j])
+                          : kNoItem;
+                nc += h;
+            }
+            cswap(ck[0], ci[0], ck[1], ci[1]);
+            cswap(ck[2], ci[2], ck[3], ci[3]);
+            cswap(ck[0], ci[0], ck[2], ci[2]);
+            cswap(ck[1], ci[1], ck[3], ci[3]);
+            cswap(ck[1], ci[1], ck[2], ci[2]);
+        }
+        // ---- leaves: every triangle test of the step first, then the row delivers the candidates in lane
+        //      order, a leaf's triangles in record order, each against the current TMax
+        const uint32_t lc = isLeaf ? ((item >> 29) & 3u) + 1u : 0u;
+        if (isLeaf) st.leaves++;
+        if (__ballot(lc != 0u) != 0ull) {
+            float tj[4], rj[4], zj[4];
+            uint32_t cand = 0u, afm = 0u;  // bit j: triangle j is a candidate / fails the alpha test
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                tj[j] = 0.0f; rj[j] = 0.0f; zj[j] = 0.0f;
+                if ((uint32_t)j < lc) {
+                    st.tris++;
+                    const float4 v0 = q[3 * j], v1 = q[3 * j + 1], v2 = q[3 * j + 2];
+                    float det, t, bu, bv;
+                    if (intersect_tri(r, v0, v1, v2, t, bu, bv, det) && t >= TMin && t <= thi0 &&
+                        !culled(det, __float_as_uint(v1.w), a.cull)) {  // ray flags: before any-hit
+                        cand |= 1u << j;
+                        tj[j] = t;
+                        rj[j] = sd_hash(bu, bv);
+                        float z = t * cosT;  // RayToViewDepth
+                        if (a.normalize) z = saturate((z - c.nearZ) / (c.farZ - c.nearZ));
+                        zj[j] = z;
+                        if (a.alphaTest && (__float_as_uint(v1.w) & 4u) &&
+                            alpha_test_fails(a.alphaData, __float_as_uint(v0.w), v0, v1, v2, bu, bv, true, t, r.d))
+                            afm |= 1u << j;
+                    }
+                }
+            }
+            for (uint32_t m = row_bits<kRow>(cand != 0u, base); m; m &= m - 1u) {
+                const int src = base + __ffs(m) - 1;
+                const uint32_t cs = (uint32_t)__shfl((int)cand, src), as = (uint32_t)__shfl((int)afm, src);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const float bt = __shfl(tj[j], src), br = __shfl(rj[j], src), bz = __shfl(zj[j], src);
+                    if (!((cs >> j) & 1u) || (committed ? !(bt < tCur) : !(bt <= tCur))) continue;
+                    delivered += l == 0;
+                    if (sd_any_hit<N>(a, br, bz, ((as >> j) & 1u) != 0u, depths, cnt)) {
+                        tCur = bt;  // AcceptHit: TMax = t
+                        committed = true;
+                    }
+                }
+            }
+        }
+        const float thi = tCur;
+        // ---- push the surviving children, nearest on top; pop the next items
+        int keep = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) keep += (j < nc && ck[j] <= thi) ? 1 : 0;  // ck ascending: a prefix
+        int total;
+        const int pre = row_prefix<kRow>(keep, l, base, total);
+        if (pool + total > POOL) {  // unreachable by the pool bound; never write out of range
+            if (a.counters && l == 0) atomicAdd(&a.counters[10], 1ull);
+            keep = max(0, min(keep, POOL - pool - pre));
+            total = POOL - pool;
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            if (j < keep) {
+                const int slot = pool + pre + (keep - 1 - j);
+                pItem[slot] = ci[j];
+                pT[slot] = ck[j];
+            }
+        }
+        pool += total;
+        __builtin_amdgcn_wave_barrier();
+        const int take = min(pool, pool <= soft ? kRow : 1);
+        item = kNoItem;
+        if (l < take) {
+            const uint32_t it = pItem[pool - 1 - l];
+            const float tt = pT[pool - 1 - l];
+            item = tt <= thi ? it : kNoItem;
+        }
+        pool -= take;
+        __builtin_amdgcn_wave_barrier();
+        raySteps++;
+        if (pool > 0 || row_bits<kRow>(item != kNoItem, base) != 0u) continue;
+        if (l == 0) sd_store<N>(a, x, y, depths);
+        maxSteps = max(maxSteps, raySteps);
+        phase = kFetch;
+    }
+    if (a.counters) {
+        atomicAdd(&a.counters[1], (unsigned long long)active);
+        atomicAdd(&a.counters[2], (unsigned long long)st.nodes);
+        atomicAdd(&a.counters[3], (unsigned long long)st.tris);
+        atomicAdd(&a.counters[4], (unsigned long long)delivered);
+        atomicMax(&a.counters[6], (unsigned long long)maxSteps);
+        atomicAdd(&a.counters[9], (unsigned long long)st.leaves);
+    }
+}
+
 // Phase 3 of the split trace: anyHit -> algorithm over the K nearest keys of every live ray
 // (one row of ROW lanes per ray, lane j prepares key j), then the SD texel store
 // (StochasticDepthMapRT.rt.slang:90-104).  Persistent rows stride over the queue partitions.
@@ -1872,6 +2075,8 @@ static hipError_t launch_sd_kn(const SDArgs& a, dim3 grid, uint32_t persistentBl
         hipLaunchKernelGGL((sd_resolve_row_kernel<K, N, ROW>), pg, wb, 0, s, a, queue, qctl, keys);
     } else if (walk == 3) {
         hipLaunchKernelGGL((sd_trace_ordered_kernel<N>), pg, wb, quad_stack_bytes(a), s, a, queue, qctl);
+    } else if (walk == 5) {
+        hipLaunchKernelGGL((sd_trace_wavefront_kernel<N>), pg, wb, 0, s, a, queue, qctl);
     } else if (walk == 4) {
         hipLaunchKernelGGL((sd_raster_kernel<K>), dim3((a.nTris + kRasterBlock - 1) / kRasterBlock), dim3(kRasterBlock),
                            0, s, a, queue, qctl);
@@ -2028,8 +2233,8 @@ rsd_status sd_trace_impl(rsd_scene* scene, const rsd_camera* cam, const rsd_sd_p
         set_error("rsd_sd_trace: ReservoirSampling is a raster-only implementation");
         return RSD_ERR_UNSUPPORTED;
     }
-    if (p->hit_order > RSD_HIT_ORDER_TRAVERSAL) {
-        set_error("rsd_sd_trace: hit_order must be RSD_HIT_ORDER_CANONICAL or RSD_HIT_ORDER_TRAVERSAL");
+    if (p->hit_order > RSD_HIT_ORDER_WAVEFRONT) {
+        set_error("rsd_sd_trace: hit_order must be RSD_HIT_ORDER_CANONICAL, _TRAVERSAL or _WAVEFRONT");
         return RSD_ERR_INVALID_ARG;
     }
     if (p->use_16bit && N > 4) {
@@ -2232,7 +2437,9 @@ rsd_status sd_trace_impl(rsd_scene* scene, const rsd_camera* cam, const rsd_sd_p
     // (profiles/round3/ab/trace_pool/).  RSD_TRACE_POOL=256 forces the large pool (A/B runs); the
     // instrumented (counters) walk always uses 256.
     static const char* poolEnv = std::getenv("RSD_TRACE_POOL");
-    int pool = (poolEnv && std::atoi(poolEnv) == 256) || counters ? kPoolCap : 128;
+    // (the wavefront stream's order depends on the pool bound: always the 256-entry pool, soft bound below)
+    int pool = (poolEnv && std::atoi(poolEnv) == 256) || counters || p->hit_order == RSD_HIT_ORDER_WAVEFRONT
+                   ? kPoolCap : 128;
     if (pool - 48 - 3 * depth < 16) pool = kPoolCap;
     a.poolSoft = std::min(pool - 48 - 3 * depth, 160);
     const char* walkEnv = std::getenv("RSD_TRACE_WALK");  // read per call: tests cover every walk
@@ -2256,7 +2463,12 @@ rsd_status sd_trace_impl(rsd_scene* scene, const rsd_camera* cam, const rsd_sd_p
     const bool raster = rasterOk && walkName == "raster";
     // the fused row walk carries every key's hit terms from its leaf test, so it needs no resolve
     // pass; RSD_TRACE_WALK=split keeps the key-list + resolve-kernel variant for A/B runs
-    const int walk = p->hit_order == RSD_HIT_ORDER_TRAVERSAL ? 3 : raster ? 4 : !rowWalk ? 0
+    if (p->hit_order == RSD_HIT_ORDER_WAVEFRONT && a.poolSoft < 16) {
+        set_error("rsd_sd_trace: the BVH is too deep for the wavefront order's LDS pool");
+        return RSD_ERR_UNSUPPORTED;
+    }
+    const int walk = p->hit_order == RSD_HIT_ORDER_TRAVERSAL ? 3 : p->hit_order == RSD_HIT_ORDER_WAVEFRONT ? 5
+                     : raster ? 4 : !rowWalk ? 0
                      : (split && walkName == "split") ? 2 : 1;
     // segment entry grid: canonical walks (row, quad, split) start from the frontier of each ray's
     // segment; RSD_TRACE_ENTRY=off walks every ray from the root (A/B runs)
@@ -2264,7 +2476,7 @@ rsd_status sd_trace_impl(rsd_scene* scene, const rsd_camera* cam, const rsd_sd_p
         const char* entEnv = std::getenv("RSD_TRACE_ENTRY");
         a.entOn = entEnv && std::string(entEnv) == "off" ? 0u : 1u;
     }
-    if (walk == 1 || walk == 0) {
+    if (walk == 1 || walk == 0 || walk == 5) {
         // longest-first queue: rays whose interval exceeds 0.1 x TMin are dequeued first (configs[1]:
         // 90 -> 84 us); RSD_TRACE_LPT = off | a threshold (> 0 absolute, < 0 relative to TMin).  (The
         // traversal-order walk reads the split queue too, but measured no gain from it: 150.7 vs 147.3 us at

@@ -1,5 +1,5 @@
-"""GPU parity of the traversal-order any-hit stream (rsd.h RSD_HIT_ORDER_TRAVERSAL) and of the
-Use16Bit SD map (StochasticDepthMapRT.cpp:192-198).
+"""GPU parity of the traversal-order any-hit streams (rsd.h RSD_HIT_ORDER_TRAVERSAL, the depth-first order, and
+RSD_HIT_ORDER_WAVEFRONT, the row walk's 8-wide order) and of the Use16Bit SD map (StochasticDepthMapRT.cpp:192-198).
 
 The traversal order depends on the BVH, so the oracle walks librsd's own tree: the GPU scene's
 rsd_scene_export_bvh bytes (ocpu_sd_trace_ordered).  Bit-exact, like test_gpu_parity.py."""
@@ -33,8 +33,13 @@ def _run(scene_name, cfg, oracle, band=(0, 1), consume=False):
     bvh, off = r.gscene.export_bvh()
     osc = oracle.Scene(scene.positions, scene.indices, scene.flags, scene.alpha)
     cam, sdp = to_oracle(r.cam, oracle.Camera), to_oracle(r.sdp, oracle.SDParams)
-    sd, stats = oracle.sd_trace_ordered(osc, bvh, off, cam, sdp, g0["depth"], g0["ray_min"], g0["ray_max"], r.sd_w,
-                                        r.sd_h, band=band)
+    if cfg.hit_order == 2:  # the wavefront order: librsd's pool bound from the tree depth (rsd.h)
+        soft = min(208 - 3 * int(r.gscene.info.wide_depth), 160)
+        sd, stats = oracle.sd_trace_wavefront(osc, bvh, off, soft, cam, sdp, g0["depth"], g0["ray_min"], g0["ray_max"],
+                                              r.sd_w, r.sd_h, band=band)
+    else:
+        sd, stats = oracle.sd_trace_ordered(osc, bvh, off, cam, sdp, g0["depth"], g0["ray_min"], g0["ray_max"], r.sd_w,
+                                            r.sd_h, band=band)
     r.close()
     return g, g0, sd, stats
 
@@ -154,3 +159,43 @@ def test_use16bit_refuses_n8():
                                 None)
     assert st == abi.ERR_UNSUPPORTED
     r.close()
+
+
+# ---- the wavefront order (RSD_HIT_ORDER_WAVEFRONT, sd_trace_wavefront_kernel vs oracle o_wavefront_walk)
+@pytest.mark.parametrize("N,impl,max_count", [(1, 0, 8), (4, 0, 8), (8, 0, 8), (16, 0, 16), (4, 3, 8), (4, 1, 8),
+                                              (4, 0, 2), (4, 0, 32)])
+def test_wavefront_order_parity(oracle, N, impl, max_count):
+    cfg = small_frame_config(visible=(256, 144), guard=32, divisor=2, N=N, max_count=max_count, impl=impl)
+    cfg.hit_order = 2
+    g, _, sd, stats = _run("arcade_tiny", cfg, oracle)
+    assert stats[0] > 100
+    assert bits_equal(g["sd"], sd)
+
+
+def test_wavefront_order_alpha_cull_band(oracle):
+    cfg = small_frame_config(visible=(256, 144), guard=32, divisor=2, N=4)
+    cfg.hit_order = 2
+    g, _, sd, _ = _run("foliage_small", cfg, oracle)
+    assert bits_equal(g["sd"], sd)
+    cfg = small_frame_config(visible=(160, 96), guard=0, divisor=1, N=4)
+    cfg.hit_order, cfg.cull_mode, cfg.ray_interval, cfg.sd_guard_px = 2, 2, False, 0
+    g, _, sd, _ = _run("arcade_tiny", cfg, oracle)
+    assert bits_equal(g["sd"], sd)
+    cfg = small_frame_config(visible=(256, 144), guard=32, divisor=2, N=4)
+    cfg.hit_order = 2
+    g, g0, sd, _ = _run("arcade_tiny", cfg, oracle, band=(1, 3), consume=True)
+    rows = np.array([y for y in range(g["sd"].shape[1]) if (y // 8) % 3 == 1])
+    assert bits_equal(g["sd"][:, rows], sd[:, rows])
+    assert (g["ray_max"] == 0).all()
+
+
+@pytest.mark.timeout(600)
+def test_wavefront_order_config1_whole_map(oracle):
+    """configs[1]: the whole SD map bit for bit, and the stream is its own (not the depth-first order's map)."""
+    from rsd.frame import CONFIGS, FrameConfig
+    kw, name = CONFIGS["suntemple_1080p_q"]
+    g, _, sd, stats = _run(name, FrameConfig(**kw, hit_order=2), oracle)
+    assert stats[0] > 10000
+    assert bits_equal(g["sd"], sd)
+    g1, _, _, _ = _run(name, FrameConfig(**kw, hit_order=1), oracle)
+    assert not bits_equal(g["sd"], g1["sd"])

@@ -37,7 +37,30 @@ def frame(oracle):
     def canonical(**kw):
         return oracle.sd_trace(osc, cam, params(**kw), z, None, None, sd_w, sd_h, threads=8)[0]
 
-    return dict(scene=scene, bvh=bvh, off=off, ordered=ordered, canonical=canonical, sd=(sd_w, sd_h))
+    soft = min(208 - 3 * wide_depth(bvh), 160)  # librsd's pool bound for the wavefront order (rsd.h)
+
+    def wavefront(**kw):
+        return oracle.sd_trace_wavefront(osc, bvh, off, soft, cam, params(hit_order=abi.HIT_ORDER_WAVEFRONT, **kw), z,
+                                         None, None, sd_w, sd_h, threads=8)[0]
+
+    return dict(scene=scene, bvh=bvh, off=off, ordered=ordered, canonical=canonical, wavefront=wavefront,
+                sd=(sd_w, sd_h))
+
+
+def wide_depth(bvh):
+    """Inner 4-wide nodes on the longest root-to-leaf path of librsd's exported BVH (rsd_scene_info.wide_depth)."""
+    u = bvh.view(np.uint32)
+
+    def depth(node):
+        nb = u[32 * node: 32 * node + 32]
+        d = 0
+        for c in range(4):
+            ref, cnt = int(nb[24 + c]), int(nb[28 + c])
+            if ref != 0xFFFFFFFF and cnt == 0:
+                d = max(d, depth(ref))
+        return 1 + d
+
+    return depth(0)
 
 
 def test_host_bvh_layout(frame):
@@ -98,3 +121,26 @@ def test_oracle_refuses_silent_canonical(frame, oracle):
     p.hit_order = abi.HIT_ORDER_TRAVERSAL
     with pytest.raises(ValueError):
         oracle.sd_trace(None, None, p, np.zeros((1, 1), np.float32), None, None, 1, 1)
+
+
+def test_wavefront_nearest_hit_is_order_independent(frame):
+    """The wavefront order (rsd.h RSD_HIT_ORDER_WAVEFRONT) delivers every hit nearer than the committed one too:
+    KBuffer with N = 1 keeps the nearest hit, equal to both other orders."""
+    from rsd import abi
+    w = frame["wavefront"](sd_samples=1, implementation=abi.SD_KBUFFER, max_count=64)
+    c = frame["canonical"](sd_samples=1, implementation=abi.SD_KBUFFER, max_count=64)
+    assert np.array_equal(w.view(np.uint32), c.view(np.uint32))
+
+
+def test_wavefront_default_samples_its_own_order(frame):
+    """Under the wavefront order the Default reservoir samples (slots replaced) and the stream is not the
+    depth-first one: the maps differ from the KBuffer's and from the depth-first order's."""
+    from rsd import abi
+    w = frame["wavefront"](sd_samples=4, implementation=abi.SD_DEFAULT)
+    k = frame["wavefront"](sd_samples=4, implementation=abi.SD_KBUFFER)
+    o = frame["ordered"](sd_samples=4, implementation=abi.SD_DEFAULT)
+    assert (w.view(np.uint32) != k.view(np.uint32)).any(axis=-1).mean() > 0.005
+    assert not np.array_equal(w.view(np.uint32), o.view(np.uint32))
+    c = frame["canonical"](sd_samples=4, implementation=abi.SD_DEFAULT)
+    hit = c[0, :, :, 0] < 1.0
+    assert (w[0][hit] < 1.0).any(axis=-1).all()

@@ -3,7 +3,7 @@ intervals (pass 1 once, the maps kept: no consume) timed with HIP events over `n
 alternating the settings for `reps` rounds; the SD maps of every setting must be the same bits.
 usage: python tools/env_ab.py VAR value_a value_b [config] [--n 40] [--reps 6] [--walk fused|quad]
        [--what trace|pass1|pass2] (pass1 / pass2: that pass alone, its outputs compared the same way)
-       [--hit-order canonical|traversal] [--clean-tiles] (Renderer.keep_clean_tiles: the bench's SD maps)"""
+       [--hit-order canonical|traversal|wavefront] [--clean-tiles] (Renderer.keep_clean_tiles: the bench's SD maps)"""
 import json
 import os
 import sys
@@ -29,9 +29,9 @@ n, reps = int(arg("--n", "40")), int(arg("--reps", "6"))
 if "--walk" in sys.argv:
     os.environ["RSD_TRACE_WALK"] = arg("--walk", "fused")
 kw, sc = CONFIGS[name]
-if arg("--hit-order", "canonical") == "traversal":  # the DXR-like any-hit stream (sd_trace_ordered_kernel)
+if arg("--hit-order", "canonical") in ("traversal", "wavefront"):  # the DXR-like any-hit streams
     from rsd import abi
-    kw = dict(kw, hit_order=abi.HIT_ORDER_TRAVERSAL)
+    kw = dict(kw, hit_order=abi.HIT_ORDER_TRAVERSAL if arg("--hit-order", "") == "traversal" else abi.HIT_ORDER_WAVEFRONT)
 r = Renderer(make_scene(sc), FrameConfig(**kw))
 if "--clean-tiles" in sys.argv:
     r.keep_clean_tiles()
