@@ -6,7 +6,8 @@ then pass 2 on each SD map.  Reports the SD-map differences over the live texels
 difference over the visible region against SURVEY 8(c)'s image tolerance (mean |dAO| <= 1/255,
 |dAO| <= 2/255 on >= 99.5 % of the pixels), plus the same for KBuffer (whose N nearest hits do
 not depend on the order unless MAX_COUNT truncates the stream).
-usage: python tools/hit_order_study.py > profiles/round2/hit_order_study.json"""
+usage: python tools/hit_order_study.py [--order traversal|wavefront] > profiles/roundN/hit_order_study.json
+(--order wavefront: RSD_HIT_ORDER_WAVEFRONT, round 5, instead of the depth-first order)"""
 import json
 import sys
 from pathlib import Path
@@ -30,13 +31,15 @@ def frame(scene, kw, impl, order):
 
 
 def main():
-    out = {"tolerance": {"ao_mae_max": 1 / 255, "ao_abs_le_2_over_255_min_frac": 0.995}}
+    order = 2 if "wavefront" in sys.argv else 1
+    out = {"tolerance": {"ao_mae_max": 1 / 255, "ao_abs_le_2_over_255_min_frac": 0.995},
+           "order": {1: "traversal (depth-first)", 2: "wavefront"}[order]}
     for config in ("suntemple_1080p_q", "bistro_1080p_full"):
         kw, name = CONFIGS[config]
         scene = make_scene(name)
         for impl, iname in ((0, "Default"), (3, "KBuffer")):
             a, cfg = frame(scene, kw, impl, 0)
-            b, _ = frame(scene, kw, impl, 1)
+            b, _ = frame(scene, kw, impl, order)
             live = a["ray_max"] != 0
             da, db = a["sd"].view(np.uint32), b["sd"].view(np.uint32)
             texel_diff = (da != db).any(axis=-1).any(axis=0)  # [sdH, sdW]
