@@ -40,7 +40,8 @@ namespace rsd {
 // ------------------------------------------------------------------------------------
 // queue-control words of one trace: {count[32], head[32]} of the live-ray queue partitions, the
 // raster walk's live-tile count, spare
-constexpr int kQctlWords = 3 * (int)kQueueParts + 32;
+constexpr int kQctlWords = 4 * (int)kQueueParts + 32;
+constexpr int kQctlHead2 = 3 * (int)kQueueParts + 32;  // hybrid walk: the row walk's own dequeue heads
 constexpr int kQctlLiveTiles = 2 * (int)kQueueParts;
 constexpr int kQctlShort = 2 * (int)kQueueParts + 32;  // lpt: short-ray counts (filled from the partition's end)
 constexpr int kSetupWaves = 4;  // sd_setup_kernel: tiles (waves) per workgroup
@@ -97,6 +98,8 @@ struct SDArgs {
     // one per wave instead of eight to a wave; 0: wave-major (index i -> wave i / rows, row i % rows)
     uint32_t spread;
     uint32_t quadStack;  // entries of each ray's LDS stack in the quad walks (quad_stack_entries)
+    uint32_t qrange;     // diagnostics (RSD_TRACE_QRANGE): 0 every ray, 1 the longest-first rays only, 2 the others
+    uint32_t hybridRowBlocks;  // hybrid walk: its first blocks run the row walk (sd_trace_hybrid_kernel)
     // clean tiles (rsd_sd_params.d_tile_state): per 8x8 tile, tileSig when the last trace left every texel it
     // wrote at DEFAULT_DEPTH (0: unknown); such a tile without a live ray is not rewritten
     uint32_t* tileState;
@@ -794,18 +797,22 @@ __global__ void __launch_bounds__(kSetupWaves * kBlock) sd_setup_kernel(SDArgs a
 // that starts after the static range, so a wave with no static chunk exits without an
 // atomic (one head word serialises ~90 dequeues/us, MI355X_MICROARCH.md "dequeue").
 template <int K, int N, bool SPEC = false, bool CNT = false>
-__global__ void __launch_bounds__(kBlock) sd_trace_queue_kernel(SDArgs a, const float4* __restrict__ queue,
-                                                                uint32_t* __restrict__ qctl) {
-    extern __shared__ uint32_t sQuadStack[];  // a.quadStack entries per ray: items, then their entry distances
+__device__ __forceinline__ void sd_trace_queue_body(const SDArgs& a, const float4* __restrict__ queue,
+                                                    uint32_t* __restrict__ qctl, uint32_t* sQuadStack, uint32_t bid,
+                                                    uint32_t nb, uint32_t qr) {
+    // sQuadStack: a.quadStack entries per ray, items then their entry distances; (bid, nb): this wave's block
+    // among the walk's blocks (the hybrid kernel's quad blocks follow its row blocks); qr: the queue range
     uint32_t* sItem = sQuadStack;
     float* sT = reinterpret_cast<float*>(sQuadStack + a.quadStack * kQuadRays);
     const int lane = threadIdx.x;
     const int q = lane & 3, quad = lane >> 2, quadBase = lane & ~3;
-    // wave w serves partition w % kQueueParts (gridDim.x is a multiple of kQueueParts)
-    const uint32_t part = blockIdx.x % kQueueParts, wavesPerPart = gridDim.x / kQueueParts;
+    // wave w serves partition w % kQueueParts (nb is a multiple of kQueueParts)
+    const uint32_t part = bid % kQueueParts, wavesPerPart = nb / kQueueParts;
     const uint32_t nLong = __hip_atomic_load(&qctl[part], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const uint32_t count = nLong + (a.lpt ? __hip_atomic_load(&qctl[kQctlShort + part], __ATOMIC_RELAXED,
-                                                               __HIP_MEMORY_SCOPE_AGENT) : 0u);
+    // (RSD_TRACE_QRANGE, diagnostics: only the longest-first rays, or only the others)
+    const uint32_t q0 = qr == 2u ? nLong : 0u;
+    const uint32_t count = (qr == 1u ? nLong : nLong + (a.lpt ? __hip_atomic_load(&qctl[kQctlShort + part],
+                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u)) - q0;
     TraceStats st{0u, 0u, 0u};
     uint32_t active = 0, hitsDelivered = 0, maxNodes = 0, maxSteps = 0;
     unsigned long long sumCycles = 0, maxCycles = 0;
@@ -813,22 +820,22 @@ __global__ void __launch_bounds__(kBlock) sd_trace_queue_kernel(SDArgs a, const 
     // the first wave (s_memtime ticks against the 100 MHz s_memrealtime), as the row walk's
     QuadClk clk;
     unsigned long long cal0 = 0, calR0 = 0;
-    if (CNT && blockIdx.x == 0) {
+    if (CNT && bid == 0) {
         cal0 = __builtin_amdgcn_s_memtime();
         calR0 = __builtin_amdgcn_s_memrealtime();
     }
-    uint32_t base = (blockIdx.x / kQueueParts) * (uint32_t)kQuadRays;
+    uint32_t base = (bid / kQueueParts) * (uint32_t)kQuadRays;
     bool firstChunk = true;
     while (base < count || (firstChunk && a.spread)) {
         // the static first chunk (spread: quad q of the partition's wave w takes index q * waves + w)
-        const uint32_t qi = firstChunk && a.spread ? (uint32_t)quad * wavesPerPart + blockIdx.x / kQueueParts
+        const uint32_t qi = firstChunk && a.spread ? (uint32_t)quad * wavesPerPart + bid / kQueueParts
                                                    : base + (uint32_t)quad;
         firstChunk = false;
         if (qi < count) {
             f3 d;
             float TMin, TMax, cosT;
             uint32_t idx, nEnt;
-            const uint32_t slot = queue_slot(a, part, qi, nLong);
+            const uint32_t slot = queue_slot(a, part, qi + q0, nLong);
             ray_rec_load(queue, slot, d, TMin, TMax, cosT, idx, nEnt);
             const int x = (int)(idx % (uint32_t)a.sdW), y = (int)(idx / (uint32_t)a.sdW);
             float depths[N];
@@ -874,12 +881,19 @@ __global__ void __launch_bounds__(kBlock) sd_trace_queue_kernel(SDArgs a, const 
             atomicAdd(&a.counters[18], clk.stack);
             atomicAdd(&a.counters[24], clk.tests);
         }
-        if (CNT && blockIdx.x == 0 && lane == 0) {
+        if (CNT && bid == 0 && lane == 0) {
             const unsigned long long cal1 = __builtin_amdgcn_s_memtime(), calR1 = __builtin_amdgcn_s_memrealtime();
             atomicMax(&a.counters[21], cal1 - cal0);
             atomicMax(&a.counters[22], calR1 - calR0);
         }
     }
+}
+
+template <int K, int N, bool SPEC = false, bool CNT = false>
+__global__ void __launch_bounds__(kBlock) sd_trace_queue_kernel(SDArgs a, const float4* __restrict__ queue,
+                                                                uint32_t* __restrict__ qctl) {
+    extern __shared__ uint32_t sQuadStack[];
+    sd_trace_queue_body<K, N, SPEC, CNT>(a, queue, qctl, sQuadStack, blockIdx.x, gridDim.x, a.qrange);
 }
 
 // ------------------------------------------------------------------------------------
@@ -1353,21 +1367,23 @@ __device__ __forceinline__ void sd_hit_terms(const SDArgs& a, const RayCtx& r, f
 // commit by the K-th key, so no second chunk of keys) and no alpha-tested triangles: the lower-bound
 // (useLB) tests, the alpha test, the other implementations and the chunk continuation compile away.
 template <int K, int N, int ROW, bool SPLIT, bool CNT, int POOL = kPoolCap, bool SPEC = false>
-__global__ void __launch_bounds__(kBlock) sd_trace_row_kernel(SDArgs a, const float4* __restrict__ queue,
-                                                              uint32_t* __restrict__ qctl, uint2* __restrict__ keys) {
+__device__ __forceinline__ void sd_trace_row_body(const SDArgs& a, const float4* __restrict__ queue,
+                                                  uint32_t* __restrict__ qctl, uint2* __restrict__ keys,
+                                                  uint32_t* sItem, float* sT, uint32_t bid, uint32_t nb, uint32_t qr) {
+    // sItem / sT: the rows' LDS pools (kBlock / ROW x POOL entries each); (bid, nb, qr) as sd_trace_queue_body's
     static_assert(K <= ROW, "one key per lane");
     static_assert(kEntryCap <= (uint32_t)ROW, "entry items start one per lane");
     constexpr int kRow = ROW, kRowRays = kBlock / ROW;
-    __shared__ uint32_t sItem[kRowRays * POOL];
-    __shared__ float sT[kRowRays * POOL];
     const int lane = threadIdx.x;
     const int l = lane & (kRow - 1), base = lane & ~(kRow - 1), row = lane / kRow;
     uint32_t* pItem = sItem + row * POOL;
     float* pT = sT + row * POOL;
-    const uint32_t part = blockIdx.x % kQueueParts, wavesPerPart = gridDim.x / kQueueParts;
+    const uint32_t part = bid % kQueueParts, wavesPerPart = nb / kQueueParts;
     const uint32_t nLong = __hip_atomic_load(&qctl[part], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const uint32_t count = nLong + (a.lpt ? __hip_atomic_load(&qctl[kQctlShort + part], __ATOMIC_RELAXED,
-                                                               __HIP_MEMORY_SCOPE_AGENT) : 0u);
+    // (RSD_TRACE_QRANGE, diagnostics: only the longest-first rays, or only the others)
+    const uint32_t q0 = qr == 2u ? nLong : 0u;
+    const uint32_t count = (qr == 1u ? nLong : nLong + (a.lpt ? __hip_atomic_load(&qctl[kQctlShort + part],
+                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u)) - q0;
     const rsd_camera& c = a.cam;
     const float DEFAULT = a.normalize ? 1.0f : 3.40282347e+37f;  // Common.slangh:16
     const int soft = a.poolSoft;
@@ -1403,7 +1419,7 @@ __global__ void __launch_bounds__(kBlock) sd_trace_row_kernel(SDArgs a, const fl
     // 100 MHz s_memrealtime ticks converts the step clocks to microseconds (rsd_counters.shader_clock_mhz)
     unsigned long long cal0 = 0, calR0 = 0;
     if constexpr (CNT) {
-        if (blockIdx.x == 0) {
+        if (bid == 0) {
             cal0 = __builtin_amdgcn_s_memtime();
             calR0 = __builtin_amdgcn_s_memrealtime();
         }
@@ -1414,18 +1430,18 @@ __global__ void __launch_bounds__(kBlock) sd_trace_row_kernel(SDArgs a, const fl
         if (phase == kFetch) {
             uint32_t qi;
             if (first) {  // the static first ray
-                qi = a.spread ? (uint32_t)row * wavesPerPart + blockIdx.x / kQueueParts
-                              : (blockIdx.x / kQueueParts) * (uint32_t)kRowRays + (uint32_t)row;
+                qi = a.spread ? (uint32_t)row * wavesPerPart + bid / kQueueParts
+                              : (bid / kQueueParts) * (uint32_t)kRowRays + (uint32_t)row;
                 first = false;
             } else {
                 uint32_t h = 0;
-                if (l == 0) h = atomicAdd(&qctl[kQueueParts + part], 1u);
+                if (l == 0) h = atomicAdd(&qctl[(qr == 1u ? kQctlHead2 : kQueueParts) + part], 1u);
                 qi = wavesPerPart * (uint32_t)kRowRays + __shfl(h, base);
             }
             if (qi >= count) {
                 phase = kExit;
             } else {
-                slot = queue_slot(a, part, qi, nLong);
+                slot = queue_slot(a, part, qi + q0, nLong);
                 f3 d;
                 uint32_t idx;
                 // the entry items load with the record (the setup kernel wrote both)
@@ -1715,12 +1731,37 @@ __global__ void __launch_bounds__(kBlock) sd_trace_row_kernel(SDArgs a, const fl
         atomicAdd(&a.counters[18], tPool);
         atomicAdd(&a.counters[23], tBox);
         atomicAdd(&a.counters[24], tTri);
-        if (blockIdx.x == 0 && lane == 0) {
+        if (bid == 0 && lane == 0) {
             const unsigned long long cal1 = __builtin_amdgcn_s_memtime(), calR1 = __builtin_amdgcn_s_memrealtime();
             atomicMax(&a.counters[21], cal1 - cal0);
             atomicMax(&a.counters[22], calR1 - calR0);
         }
     }
+}
+
+template <int K, int N, int ROW, bool SPLIT, bool CNT, int POOL = kPoolCap, bool SPEC = false>
+__global__ void __launch_bounds__(kBlock) sd_trace_row_kernel(SDArgs a, const float4* __restrict__ queue,
+                                                              uint32_t* __restrict__ qctl, uint2* __restrict__ keys) {
+    constexpr int kRowRays = kBlock / ROW;
+    __shared__ uint32_t sItem[kRowRays * POOL];
+    __shared__ float sT[kRowRays * POOL];
+    sd_trace_row_body<K, N, ROW, SPLIT, CNT, POOL, SPEC>(a, queue, qctl, keys, sItem, sT, blockIdx.x, gridDim.x, a.qrange);
+}
+
+// The hybrid walk (walk 6): one launch whose first a.hybridRowBlocks blocks walk the longest-first rays with the
+// specialised row walk and whose other blocks walk the remaining rays with the specialised quad walk, so the long
+// rays' chains (which set a quad-walk launch) take 8 items per step while the bulk keeps the quad walk's lane use.
+// One dynamic LDS allocation serves either role (max of the two).
+template <int K, int N, int ROW, int POOL>
+__global__ void __launch_bounds__(kBlock) sd_trace_hybrid_kernel(SDArgs a, const float4* __restrict__ queue,
+                                                                 uint32_t* __restrict__ qctl, uint2* __restrict__ keys) {
+    extern __shared__ uint32_t sDyn[];
+    const uint32_t rb = a.hybridRowBlocks;
+    if (blockIdx.x < rb)
+        sd_trace_row_body<K, N, ROW, false, false, POOL, true>(
+            a, queue, qctl, keys, sDyn, reinterpret_cast<float*>(sDyn + (kBlock / ROW) * POOL), blockIdx.x, rb, 1u);
+    else
+        sd_trace_queue_body<K, N, true>(a, queue, qctl, sDyn, blockIdx.x - rb, gridDim.x - rb, 2u);
 }
 
 // Wavefront traversal-order any-hit stream (rsd_sd_params.hit_order = RSD_HIT_ORDER_WAVEFRONT, rsd.h): the
@@ -2057,6 +2098,12 @@ __global__ void __launch_bounds__(kBlock) gbuffer_kernel(GBArgs a) {
 // -> 64-bit key lists -> resolve kernel)
 static size_t quad_stack_bytes(const SDArgs& a) { return (size_t)a.quadStack * kQuadRays * 8u; }
 
+// RSD_TRACE_SPEC=off: the generic walks (A/B runs)
+static bool specEnvOff() {
+    const char* e = std::getenv("RSD_TRACE_SPEC");
+    return e && std::string(e) == "off";
+}
+
 template <int K, int N>
 static hipError_t launch_sd_kn(const SDArgs& a, dim3 grid, uint32_t persistentBlocks, float4* queue, uint32_t* qctl,
                                uint2* keys, int walk, int pool, hipStream_t s) {
@@ -2077,6 +2124,10 @@ static hipError_t launch_sd_kn(const SDArgs& a, dim3 grid, uint32_t persistentBl
         hipLaunchKernelGGL((sd_trace_ordered_kernel<N>), pg, wb, quad_stack_bytes(a), s, a, queue, qctl);
     } else if (walk == 5) {
         hipLaunchKernelGGL((sd_trace_wavefront_kernel<N>), pg, wb, 0, s, a, queue, qctl);
+    } else if (walk == 6) {
+        const size_t rowLds = (size_t)(kBlock / ROW) * pool * 8u, lds = std::max(rowLds, quad_stack_bytes(a));
+        if (pool == 128) hipLaunchKernelGGL((sd_trace_hybrid_kernel<K, N, ROW, 128>), pg, wb, lds, s, a, queue, qctl, keys);
+        else hipLaunchKernelGGL((sd_trace_hybrid_kernel<K, N, ROW, kPoolCap>), pg, wb, lds, s, a, queue, qctl, keys);
     } else if (walk == 4) {
         hipLaunchKernelGGL((sd_raster_kernel<K>), dim3((a.nTris + kRasterBlock - 1) / kRasterBlock), dim3(kRasterBlock),
                            0, s, a, queue, qctl);
@@ -2329,6 +2380,8 @@ rsd_status sd_trace_impl(rsd_scene* scene, const rsd_camera* cam, const rsd_sd_p
         // RSD_TRACE_SPREAD=on: the static first rays dealt row-major over the waves (SDArgs.spread; A/B)
         const char* spreadEnv = std::getenv("RSD_TRACE_SPREAD");
         a.spread = spreadEnv && std::string(spreadEnv) == "on" ? 1u : 0u;
+        const char* qrEnv = std::getenv("RSD_TRACE_QRANGE");
+        a.qrange = qrEnv && std::string(qrEnv) == "long" ? 1u : qrEnv && std::string(qrEnv) == "short" ? 2u : 0u;
     }
     // clean tiles: the stamp names what DEFAULT_DEPTH looks like in this map (value, storage, layers)
     a.tileState = p->d_tile_state;
@@ -2467,7 +2520,7 @@ rsd_status sd_trace_impl(rsd_scene* scene, const rsd_camera* cam, const rsd_sd_p
         set_error("rsd_sd_trace: the BVH is too deep for the wavefront order's LDS pool");
         return RSD_ERR_UNSUPPORTED;
     }
-    const int walk = p->hit_order == RSD_HIT_ORDER_TRAVERSAL ? 3 : p->hit_order == RSD_HIT_ORDER_WAVEFRONT ? 5
+    int walk = p->hit_order == RSD_HIT_ORDER_TRAVERSAL ? 3 : p->hit_order == RSD_HIT_ORDER_WAVEFRONT ? 5
                      : raster ? 4 : !rowWalk ? 0
                      : (split && walkName == "split") ? 2 : 1;
     // segment entry grid: canonical walks (row, quad, split) start from the frontier of each ray's
@@ -2533,8 +2586,27 @@ rsd_status sd_trace_impl(rsd_scene* scene, const rsd_camera* cam, const rsd_sd_p
     // stays at 8 (latency-bound: 10 / 12 / 16 measured no faster).
     const char* wpcEnv = std::getenv("RSD_TRACE_WAVES_PER_CU");  // experiments only (read per call: A/B runs)
     const uint32_t wavesPerCu = wpcEnv ? (uint32_t)std::max(1, std::atoi(wpcEnv)) : (walk == 0 ? 16u : 8u);
-    const uint32_t pb = ((uint32_t)std::max(1, scene->dev->cu_count) * wavesPerCu + kQueueParts - 1) / kQueueParts *
-                        kQueueParts;
+    uint32_t pb = ((uint32_t)std::max(1, scene->dev->cu_count) * wavesPerCu + kQueueParts - 1) / kQueueParts *
+                  kQueueParts;
+    // The hybrid walk (round 5): a quad-walk trace (full-resolution maps) whose longest-first rays -- the ones whose
+    // chains set the quad walk's launch: configs[3]'s trace over them alone is 261 of its 268 us -- take the row walk
+    // (8 items per step) in the same launch (sd_trace_hybrid_kernel: its first blocks run the row walk over the
+    // longest-first end of each queue partition, the others the quad walk over the rest).  Only for 8-lane rows
+    // (K <= 8: with K = 16 the 16-lane row walk is the slower one) and one frame in flight: with frames in flight
+    // (RSD_SD_THROUGHPUT) the machine is already full of other frames' work.  RSD_TRACE_HYBRID=off disables it;
+    // RSD_TRACE_HYBRID_ROWWPC / RSD_TRACE_WAVES_PER_CU set the row / quad blocks per CU (A/B runs).
+    const char* hyEnv = std::getenv("RSD_TRACE_HYBRID");
+    const bool hybridOk = walk == 0 && K <= 8 && a.lpt && a.poolSoft >= 16 && !throughput &&
+                          !(hyEnv && std::string(hyEnv) == "off") && !a.alphaTest && a.impl != 1u && a.impl != 3u &&
+                          a.maxCount <= (uint32_t)K && !(specEnvOff());
+    if (hybridOk && !counters) {
+        const char* rwEnv = std::getenv("RSD_TRACE_HYBRID_ROWWPC");
+        const uint32_t rw = rwEnv ? (uint32_t)std::max(1, std::atoi(rwEnv)) : 4u, qw = wpcEnv ? wavesPerCu : 8u;
+        const uint32_t cus = (uint32_t)std::max(1, scene->dev->cu_count);
+        a.hybridRowBlocks = (cus * rw + kQueueParts - 1) / kQueueParts * kQueueParts;
+        pb = a.hybridRowBlocks + (cus * qw + kQueueParts - 1) / kQueueParts * kQueueParts;
+        walk = 6;
+    }
     hipError_t e = hipSuccess;
     if (grid.y == 0) {}
     else if (K == 4) e = launch_sd_k<4>(a, N, grid, pb, queue, qctl, keys, walk, pool, s);
@@ -2559,7 +2631,9 @@ rsd_status sd_trace_impl(rsd_scene* scene, const rsd_camera* cam, const rsd_sd_p
         counters->sum_ray_clocks = h[7];
         counters->max_ray_clocks = h[8];
         counters->leaves_visited = h[9];
-        counters->walk = (uint64_t)walk;
+        // (an instrumented trace walks the quad kernel alone; walk reports the hybrid the same trace takes without
+        // counters, so that a caller prices the kernels that ran in its timed traces)
+        counters->walk = (uint64_t)(walk == 0 && hybridOk ? 6 : walk);
         counters->entry_lookups = h[19];
         counters->entry_items = h[20];
         // row walk (instrumented): per-step clock sums and the clock of the instrumented launch

@@ -158,9 +158,9 @@ class Counters(C.Structure):
                 ("texels_clean", C.c_uint64)]
 
 
-WALK_QUAD, WALK_FUSED, WALK_SPLIT, WALK_ORDERED, WALK_RASTER, WALK_WAVEFRONT = 0, 1, 2, 3, 4, 5
+WALK_QUAD, WALK_FUSED, WALK_SPLIT, WALK_ORDERED, WALK_RASTER, WALK_WAVEFRONT, WALK_HYBRID = 0, 1, 2, 3, 4, 5, 6
 WALK_NAMES = {WALK_QUAD: "quad", WALK_FUSED: "fused", WALK_SPLIT: "split", WALK_ORDERED: "ordered", WALK_RASTER: "raster",
-              WALK_WAVEFRONT: "wavefront"}
+              WALK_WAVEFRONT: "wavefront", WALK_HYBRID: "hybrid"}
 HIT_ORDER_CANONICAL, HIT_ORDER_TRAVERSAL, HIT_ORDER_WAVEFRONT = 0, 1, 2
 # kernels of one rsd_sd_trace per walk (rsd_counters.walk)
 WALK_KERNELS = {WALK_QUAD: ("sd_setup_kernel", "sd_trace_queue_kernel"),
@@ -168,7 +168,8 @@ WALK_KERNELS = {WALK_QUAD: ("sd_setup_kernel", "sd_trace_queue_kernel"),
                 WALK_SPLIT: ("sd_setup_kernel", "sd_trace_row_kernel", "sd_resolve_row_kernel"),
                 WALK_ORDERED: ("sd_setup_kernel", "sd_trace_ordered_kernel"),
                 WALK_RASTER: ("sd_setup_kernel", "sd_raster_kernel", "sd_resolve_row_kernel"),
-                WALK_WAVEFRONT: ("sd_setup_kernel", "sd_trace_wavefront_kernel")}
+                WALK_WAVEFRONT: ("sd_setup_kernel", "sd_trace_wavefront_kernel"),
+                WALK_HYBRID: ("sd_setup_kernel", "sd_trace_row_kernel", "sd_trace_queue_kernel")}
 
 
 # every symbol include/rsd.h declares (checked by tests/test_abi.py)

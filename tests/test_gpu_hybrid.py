@@ -1,0 +1,57 @@
+"""The hybrid SD walk (rsd.h RSD_WALK_HYBRID, csrc/sd_trace.hip walk 6): on a full-resolution map with one frame in
+flight the longest-first rays take the row walk on a side stream while the quad walk takes the others.  Canonical hit
+stream, so the bits must be the quad walk's (and the oracle's, which test_gpu_configs.py checks at every config)."""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def bits(t):
+    return np.ascontiguousarray(t.cpu().numpy()).view(np.uint32)
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("config", ["emerald_4k_q", "bistro_1080p_full"])
+def test_hybrid_walk_equals_quad_walk(config):
+    import torch
+    from rsd import abi
+    from rsd.frame import CONFIGS, FrameConfig, Renderer
+    from rsd.scenes import make_scene
+    kw, name = CONFIGS[config]
+    r = Renderer(make_scene(name), FrameConfig(**kw))
+    r.keep_clean_tiles()
+    r.gbuffer()
+    r.clear_intervals()
+    r.pass1()
+    torch.cuda.synchronize()
+    saved = r.ray_minmax.clone()
+    maps = {}
+    try:
+        for mode in ("off", "on"):
+            os.environ["RSD_TRACE_HYBRID"] = mode
+            for rep in range(2):  # the second trace of the map runs over clean tiles
+                r.ray_minmax.copy_(saved)
+                r.sd_trace()
+            torch.cuda.synchronize()
+            maps[mode] = bits(r.sd)
+            c = r.sd_trace(counters=True)
+            assert int(c.walk) == (abi.WALK_HYBRID if mode == "on" else abi.WALK_QUAD), (mode, int(c.walk))
+            # with frames in flight (RSD_SD_THROUGHPUT) the quad walk runs alone
+            c = r.sd_trace(counters=True, throughput=True)
+            assert int(c.walk) == abi.WALK_QUAD
+        # band split by SD rows (the band frame's full-resolution split): the same rows, the same bits
+        r.ray_minmax.copy_(saved)
+        r.invalidate_sd_tiles()
+        r.sd.zero_()
+        h = r.sd_h // 16 * 8  # a multiple of 8 rows
+        r.sd_trace_rows((0, h))
+        torch.cuda.synchronize()
+        half = bits(r.sd)[:, :h]
+    finally:
+        os.environ.pop("RSD_TRACE_HYBRID", None)
+    assert np.array_equal(maps["on"], maps["off"])
+    assert np.array_equal(half, maps["off"][:, :h])
+    r.close()
