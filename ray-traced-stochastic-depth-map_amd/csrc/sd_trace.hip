@@ -2593,10 +2593,13 @@ rsd_status sd_trace_impl(rsd_scene* scene, const rsd_camera* cam, const rsd_sd_p
     // (8 items per step) in the same launch (sd_trace_hybrid_kernel: its first blocks run the row walk over the
     // longest-first end of each queue partition, the others the quad walk over the rest).  Only for 8-lane rows
     // (K <= 8: with K = 16 the 16-lane row walk is the slower one) and one frame in flight: with frames in flight
-    // (RSD_SD_THROUGHPUT) the machine is already full of other frames' work.  RSD_TRACE_HYBRID=off disables it;
+    // (RSD_SD_THROUGHPUT) the machine is already full of other frames' work and the quad walk's lane use wins
+    // (RSD_TRACE_HYBRID=all: configs[2] 0.188-0.191 -> 0.202-0.206 ms per frame, configs[3] 0.308-0.317 ->
+    // 0.327-0.347; profiles/round5/hybrid/in_flight/).  RSD_TRACE_HYBRID=off disables it;
     // RSD_TRACE_HYBRID_ROWWPC / RSD_TRACE_WAVES_PER_CU set the row / quad blocks per CU (A/B runs).
     const char* hyEnv = std::getenv("RSD_TRACE_HYBRID");
-    const bool hybridOk = walk == 0 && K <= 8 && a.lpt && a.poolSoft >= 16 && !throughput &&
+    const bool hybridOk = walk == 0 && K <= 8 && a.lpt && a.poolSoft >= 16 &&
+                          (!throughput || (hyEnv && std::string(hyEnv) == "all")) &&
                           !(hyEnv && std::string(hyEnv) == "off") && !a.alphaTest && a.impl != 1u && a.impl != 3u &&
                           a.maxCount <= (uint32_t)K && !(specEnvOff());
     if (hybridOk && !counters) {
