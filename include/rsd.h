@@ -258,9 +258,9 @@ typedef struct {
 #define RSD_WALK_SPLIT 2u  /* sd_trace_row_kernel (K nearest keys) + sd_resolve_row_kernel */
 #define RSD_WALK_ORDERED 3u /* sd_trace_ordered_kernel: RSD_HIT_ORDER_TRAVERSAL */
 #define RSD_WALK_WAVEFRONT 5u /* sd_trace_wavefront_kernel: RSD_HIT_ORDER_WAVEFRONT */
-#define RSD_WALK_HYBRID 6u /* one frame in flight on a map above 0.6 M texels with K <= 8: the longest-first rays on
-                              sd_trace_row_kernel (a side stream), the others on sd_trace_queue_kernel, concurrently;
-                              an instrumented trace reports it but walks sd_trace_queue_kernel alone */
+#define RSD_WALK_HYBRID 6u /* one frame in flight with K <= 8 (the canonical stream): sd_trace_hybrid_kernel, whose
+                              first blocks row-walk the longest-first rays and whose others quad-walk the rest; an
+                              instrumented trace reports it but walks the single walk (fused or quad) */
 #define RSD_WALK_RASTER 4u  /* sd_raster_kernel (triangles -> K nearest keys per texel) + sd_resolve_row_kernel */
 
 /* --- library / device ------------------------------------------------------------ */

@@ -2588,17 +2588,18 @@ rsd_status sd_trace_impl(rsd_scene* scene, const rsd_camera* cam, const rsd_sd_p
     const uint32_t wavesPerCu = wpcEnv ? (uint32_t)std::max(1, std::atoi(wpcEnv)) : (walk == 0 ? 16u : 8u);
     uint32_t pb = ((uint32_t)std::max(1, scene->dev->cu_count) * wavesPerCu + kQueueParts - 1) / kQueueParts *
                   kQueueParts;
-    // The hybrid walk (round 5): a quad-walk trace (full-resolution maps) whose longest-first rays -- the ones whose
-    // chains set the quad walk's launch: configs[3]'s trace over them alone is 261 of its 268 us -- take the row walk
-    // (8 items per step) in the same launch (sd_trace_hybrid_kernel: its first blocks run the row walk over the
-    // longest-first end of each queue partition, the others the quad walk over the rest).  Only for 8-lane rows
+    // The hybrid walk (round 5): a trace whose longest-first rays -- the ones whose chains set the launch: configs[3]'s
+    // quad walk over them alone is 261 of its 268 us -- take the row walk (8 items per step) in the same launch
+    // (sd_trace_hybrid_kernel: its first blocks run the row walk over the longest-first end of each queue partition,
+    // the others the quad walk over the rest), where the fused row walk (configs[1]: 74 -> 66 us) or the quad walk
+    // (configs[3] 268 -> 195 us, configs[2] 236 -> 177 us) would walk every ray alike.  Only for 8-lane rows
     // (K <= 8: with K = 16 the 16-lane row walk is the slower one) and one frame in flight: with frames in flight
     // (RSD_SD_THROUGHPUT) the machine is already full of other frames' work and the quad walk's lane use wins
     // (RSD_TRACE_HYBRID=all: configs[2] 0.188-0.191 -> 0.202-0.206 ms per frame, configs[3] 0.308-0.317 ->
     // 0.327-0.347; profiles/round5/hybrid/in_flight/).  RSD_TRACE_HYBRID=off disables it;
     // RSD_TRACE_HYBRID_ROWWPC / RSD_TRACE_WAVES_PER_CU set the row / quad blocks per CU (A/B runs).
     const char* hyEnv = std::getenv("RSD_TRACE_HYBRID");
-    const bool hybridOk = walk == 0 && K <= 8 && a.lpt && a.poolSoft >= 16 &&
+    const bool hybridOk = (walk == 0 || walk == 1) && K <= 8 && a.lpt && a.poolSoft >= 16 &&
                           (!throughput || (hyEnv && std::string(hyEnv) == "all")) &&
                           !(hyEnv && std::string(hyEnv) == "off") && !a.alphaTest && a.impl != 1u && a.impl != 3u &&
                           a.maxCount <= (uint32_t)K && !(specEnvOff());
@@ -2636,7 +2637,7 @@ rsd_status sd_trace_impl(rsd_scene* scene, const rsd_camera* cam, const rsd_sd_p
         counters->leaves_visited = h[9];
         // (an instrumented trace walks the quad kernel alone; walk reports the hybrid the same trace takes without
         // counters, so that a caller prices the kernels that ran in its timed traces)
-        counters->walk = (uint64_t)(walk == 0 && hybridOk ? 6 : walk);
+        counters->walk = (uint64_t)((walk == 0 || walk == 1) && hybridOk ? 6 : walk);
         counters->entry_lookups = h[19];
         counters->entry_items = h[20];
         // row walk (instrumented): per-step clock sums and the clock of the instrumented launch

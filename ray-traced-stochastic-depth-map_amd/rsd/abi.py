@@ -169,7 +169,7 @@ WALK_KERNELS = {WALK_QUAD: ("sd_setup_kernel", "sd_trace_queue_kernel"),
                 WALK_ORDERED: ("sd_setup_kernel", "sd_trace_ordered_kernel"),
                 WALK_RASTER: ("sd_setup_kernel", "sd_raster_kernel", "sd_resolve_row_kernel"),
                 WALK_WAVEFRONT: ("sd_setup_kernel", "sd_trace_wavefront_kernel"),
-                WALK_HYBRID: ("sd_setup_kernel", "sd_trace_row_kernel", "sd_trace_queue_kernel")}
+                WALK_HYBRID: ("sd_setup_kernel", "sd_trace_hybrid_kernel")}
 
 
 # every symbol include/rsd.h declares (checked by tests/test_abi.py)

@@ -1,6 +1,6 @@
-"""The hybrid SD walk (rsd.h RSD_WALK_HYBRID, csrc/sd_trace.hip walk 6): on a full-resolution map with one frame in
-flight the longest-first rays take the row walk on a side stream while the quad walk takes the others.  Canonical hit
-stream, so the bits must be the quad walk's (and the oracle's, which test_gpu_configs.py checks at every config)."""
+"""The hybrid SD walk (rsd.h RSD_WALK_HYBRID, csrc/sd_trace.hip walk 6): with one frame in flight the longest-first rays
+take the row walk and the others the quad walk, in one launch.  Canonical hit stream, so the bits must be the single
+walk's (and the oracle's, which the parity / configs tests check at every config)."""
 import os
 
 import numpy as np
@@ -14,8 +14,9 @@ def bits(t):
 
 
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("config", ["emerald_4k_q", "bistro_1080p_full"])
-def test_hybrid_walk_equals_quad_walk(config):
+@pytest.mark.parametrize("config,alone", [("emerald_4k_q", "quad"), ("bistro_1080p_full", "quad"),
+                                          ("suntemple_1080p_q", "fused")])
+def test_hybrid_walk_equals_quad_walk(config, alone):
     import torch
     from rsd import abi
     from rsd.frame import CONFIGS, FrameConfig, Renderer
@@ -38,10 +39,11 @@ def test_hybrid_walk_equals_quad_walk(config):
             torch.cuda.synchronize()
             maps[mode] = bits(r.sd)
             c = r.sd_trace(counters=True)
-            assert int(c.walk) == (abi.WALK_HYBRID if mode == "on" else abi.WALK_QUAD), (mode, int(c.walk))
-            # with frames in flight (RSD_SD_THROUGHPUT) the quad walk runs alone
+            single = abi.WALK_QUAD if alone == "quad" else abi.WALK_FUSED
+            assert int(c.walk) == (abi.WALK_HYBRID if mode == "on" else single), (mode, int(c.walk))
+            # with frames in flight (RSD_SD_THROUGHPUT) the single walk runs alone
             c = r.sd_trace(counters=True, throughput=True)
-            assert int(c.walk) == abi.WALK_QUAD
+            assert int(c.walk) == single
         # band split by SD rows (the band frame's full-resolution split): the same rows, the same bits
         r.ray_minmax.copy_(saved)
         r.invalidate_sd_tiles()
