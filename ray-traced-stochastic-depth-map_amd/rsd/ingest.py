@@ -15,7 +15,7 @@ indices, `d`/`Tr` constant alpha, `map_d` / the alpha channel of `map_Kd` as the
 texture) and `read_image` (PNG via zlib, binary/ASCII PGM/PPM/PAM, .npy) for alpha textures.
 A material with an alpha texture or a constant alpha below 1 is AlphaMode::Mask (Falcor's
 importers mark such materials Mask; the threshold defaults to 0.5, MaterialData.slang:99).
-FBX, glTF, USD and PBRT are out of scope."""
+Binary FBX 7.x: rsd.fbx.load_fbx (the same SceneBuilder).  glTF, USD and PBRT are out of scope."""
 from __future__ import annotations
 
 import dataclasses

@@ -15,13 +15,13 @@ scope.  The bindings this module mirrors, with the geometry they produce:
   BasicMaterial.cpp:233-259,611-633): baseColor, doubleSided, alphaMode, alphaThreshold (stored as
   float16), loadTexture(MaterialTextureSlot.BaseColor, path); the alpha mode follows
   updateAlphaMode: Mask iff the conservative alpha range's minimum is below the threshold.
-* `sceneBuilder` (Scene/SceneBuilder.cpp:2877-2907): importScene (OBJ via rsd.ingest.load_obj),
+* `sceneBuilder` (Scene/SceneBuilder.cpp:2877-2907): importScene (OBJ via rsd.ingest.load_obj, binary FBX via rsd.fbx.load_fbx),
   addTriangleMesh, addMaterial, getMaterial, replaceMaterial, loadMaterialTexture, addNode
   (world = parent world * local), addMeshInstance, addCamera (the first camera is the scene's).
 
 What the SD trace cannot see is accepted and dropped: lights, env maps, grid volumes, animations
 and procedural geometry (SDF grids, custom primitives) -- the SD rays skip procedural primitives
-(StochasticDepthMapRT.rt.slang:85 RAY_FLAG_SKIP_PROCEDURAL_PRIMITIVES).  FBX / glTF / USD / PBRT
+(StochasticDepthMapRT.rt.slang:85 RAY_FLAG_SKIP_PROCEDURAL_PRIMITIVES).  glTF / USD / PBRT / ASCII FBX
 imports raise (no importer for them in this image)."""
 from __future__ import annotations
 
@@ -30,7 +30,7 @@ from pathlib import Path
 
 import numpy as np
 
-from . import ingest
+from . import fbx, ingest
 
 F32 = np.float32
 INVALID_ID = 0xFFFFFFFF  # NodeID::kInvalidID
@@ -300,13 +300,13 @@ class TriangleMesh:
 
     @staticmethod
     def createFromFile(path, smoothNormals=False):
-        """:195-273 (Assimp, pre-transformed, UVs flipped): OBJ files only here."""
+        """:195-273 (Assimp, pre-transformed, UVs flipped): OBJ (rsd.ingest) and binary FBX (rsd.fbx) files."""
         p = _resolve(path)
         if p is None:
             return None  # the reference logs a warning and returns nullptr
-        if p.suffix.lower() != ".obj":
-            raise NotImplementedError(f"TriangleMesh.createFromFile: {p.suffix} needs Assimp (OBJ only here)")
-        b = ingest.load_obj(p)
+        if p.suffix.lower() not in (".obj", ".fbx"):
+            raise NotImplementedError(f"TriangleMesh.createFromFile: {p.suffix} needs Assimp (OBJ / FBX here)")
+        b = ingest.load_obj(p) if p.suffix.lower() == ".obj" else fbx.load_fbx(p)
         m = TriangleMesh()
         for mesh_id, T in b.instances:
             mm = b.meshes[mesh_id]
@@ -539,15 +539,16 @@ class PySceneBuilder:
 
     # -- geometry
     def importScene(self, path, dict=None):
-        """SceneBuilder::import: OBJ through rsd.ingest.load_obj; its meshes are placed by the
-        importer itself (world space, like Assimp's pre-transformed nodes)."""
+        """SceneBuilder::import: OBJ through rsd.ingest.load_obj, binary FBX through rsd.fbx.load_fbx (the
+        reference's AssimpImporter); their meshes are placed by the importer itself (world space, like
+        Assimp's node transforms)."""
         p = _resolve(path)
         if p is None:
             raise FileNotFoundError(f"importScene: can't find '{path}'")
-        if p.suffix.lower() != ".obj":
-            raise NotImplementedError(f"importScene: no importer for '{p.suffix}' in this build (OBJ only)")
+        if p.suffix.lower() not in (".obj", ".fbx"):
+            raise NotImplementedError(f"importScene: no importer for '{p.suffix}' in this build (OBJ, FBX)")
         before = len(self._B.materials)
-        ingest.load_obj(p, builder=self._B)
+        (ingest.load_obj if p.suffix.lower() == ".obj" else fbx.load_fbx)(p, builder=self._B)
         for idx in range(before, len(self._B.materials)):
             w = StandardMaterial(_wrap=self._B.materials[idx])
             self._mat_ids[id(w)] = idx
@@ -653,10 +654,12 @@ def load_pyscene(path, builder: ingest.SceneBuilder | None = None) -> ingest.Sce
 
 
 def load_scene_file(path, **kw) -> ingest.SceneBuilder:
-    """.pyscene or .obj by extension."""
+    """.pyscene, .obj or .fbx by extension."""
     p = Path(path)
     if p.suffix.lower() == ".pyscene":
         return load_pyscene(p, **kw)
     if p.suffix.lower() == ".obj":
         return ingest.load_obj(p, **kw)
-    raise NotImplementedError(f"{p.suffix}: no importer in this build (.pyscene, .obj)")
+    if p.suffix.lower() == ".fbx":
+        return fbx.load_fbx(p, **kw)
+    raise NotImplementedError(f"{p.suffix}: no importer in this build (.pyscene, .obj, .fbx)")

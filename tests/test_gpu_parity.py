@@ -374,6 +374,44 @@ def test_pyscene_ingest_frame_parity(device, oracle):
     gs.release()
 
 
+def test_fbx_ingest_frame_parity(device, oracle):
+    """The reference's binary FBX fixture (data/framework/meshes/sphere.fbx) loaded by rsd.fbx -- twice, once
+    through a scaled, rotated and translated instance -- on a floor: G-buffer, pass-1 intervals, SD map and AO
+    bit-exact vs the oracle."""
+    from conftest import ROOT
+    from rsd.fbx import euler, load_fbx
+    from rsd.frame import GpuScene, Renderer
+    from rsd.ingest import Mesh
+    fx = ROOT / "tests" / "fixtures" / "sphere.fbx"
+    B = load_fbx(fx)
+    T = euler((0.0, 30.0, 10.0))
+    T[:3, :3] *= 0.6
+    T[:3, 3] = (1.4, 0.6, -0.5)
+    load_fbx(fx, transform=T, builder=B)
+    floor = Mesh(np.array([[-4, -1, 4], [4, -1, 4], [4, -1, -4], [-4, -1, -4]], np.float32),
+                 np.array([[0, 1, 2], [0, 2, 3]], np.uint32))
+    B.add_instance(B.add_mesh(floor))
+    B.set_camera((0.3, 1.2, 4.5), (0.4, -0.2, 0.0))
+    s = B.build("fbx_spheres")
+    assert len(s.indices) == 2 * 760 + 2
+    cfg = small_frame_config(visible=(160, 96), guard=16, divisor=2, N=4)
+    gs = GpuScene(device, s)
+    r = Renderer(s, cfg, dev=device, gpu_scene=gs)
+    r.gbuffer()
+    r.frame()
+    g = r.numpy()
+    osc = oracle.Scene(s.positions, s.indices, s.flags, s.alpha)
+    cam, vao, sdp, svp = oracle_structs(r, oracle)
+    z, n = oracle.gbuffer(osc, cam, cfg.fb_w, cfg.fb_h, cfg.cull_mode)
+    assert bits_equal(g["depth"], z) and np.array_equal(g["normals"], n)
+    ao1, st, rmin, rmax = oracle.svao_pass1(cam, vao, svp, z, n, r.sd_w, r.sd_h)
+    sd, _ = oracle.sd_trace(osc, cam, sdp, z, rmin, rmax, r.sd_w, r.sd_h)
+    assert (rmax != 0).sum() > 0
+    assert bits_equal(g["sd"], sd)
+    assert np.array_equal(g["ao"], oracle.svao_pass2(cam, vao, svp, z, n, st, sd, ao1))
+    gs.release()
+
+
 def test_consumed_intervals_frames_match_fresh_frames(device, oracle):
     """BandFrame folds the interval clear into the trace (RSD_SD_CONSUME_INTERVALS): after
     a consuming trace the maps are exactly the cleared state, and consecutive frames stay

@@ -1,6 +1,7 @@
 """CPU tests of the .pyscene importer (rsd/pyscene.py): Falcor's Transform
 and TriangleMesh factories, material alpha-mode rules, the node hierarchy and importScene of an
-OBJ, on the repository's own fixture scene (tests/fixtures/courtyard.pyscene)."""
+OBJ, on the repository's own fixture scene (tests/fixtures/courtyard.pyscene); importScene of the
+reference's binary FBX fixture (tests/fixtures/sphere.fbx)."""
 import numpy as np
 import pytest
 
@@ -115,13 +116,39 @@ def test_courtyard_scene():
 
 def test_pyscene_errors(tmp_path):
     from rsd.pyscene import load_pyscene
+    from rsd.fbx import FbxError
     (tmp_path / "a.pyscene").write_text("sceneBuilder.importScene('Bistro.fbx')\n")
-    (tmp_path / "Bistro.fbx").write_bytes(b"Kaydara FBX Binary  \x00")
-    with pytest.raises(NotImplementedError, match="fbx"):
+    (tmp_path / "Bistro.fbx").write_bytes(b"Kaydara FBX Binary  \x00")  # a truncated binary FBX
+    with pytest.raises(FbxError, match="malformed"):
         load_pyscene(tmp_path / "a.pyscene")
+    (tmp_path / "d.pyscene").write_text("sceneBuilder.importScene('Bistro.gltf')\n")
+    (tmp_path / "Bistro.gltf").write_text("{}")
+    with pytest.raises(NotImplementedError, match="gltf"):
+        load_pyscene(tmp_path / "d.pyscene")
     (tmp_path / "b.pyscene").write_text("sceneBuilder.importScene('missing.obj')\n")
     with pytest.raises(FileNotFoundError):
         load_pyscene(tmp_path / "b.pyscene")
     (tmp_path / "c.pyscene").write_text("sceneBuilder.addMeshInstance(3, 0)\n")
     with pytest.raises(ValueError):
         load_pyscene(tmp_path / "c.pyscene")
+
+
+def test_pyscene_imports_fbx(tmp_path):
+    """sceneBuilder.importScene('*.fbx') routes to rsd.fbx (AssimpImporter's role), and
+    TriangleMesh.createFromFile reads it too."""
+    import shutil
+    from rsd.pyscene import TriangleMesh, load_pyscene
+    shutil.copy(FIX / "sphere.fbx", tmp_path / "sphere.fbx")
+    (tmp_path / "s.pyscene").write_text(
+        "sceneBuilder.importScene('sphere.fbx')\n"
+        "m = TriangleMesh.createFromFile('sphere.fbx')\n"
+        "mat = StandardMaterial('m')\n"
+        "mid = sceneBuilder.addTriangleMesh(m, mat)\n"
+        "n = sceneBuilder.addNode('n', Transform(translation=float3(3, 0, 0)))\n"
+        "sceneBuilder.addMeshInstance(n, mid)\n")
+    s = load_pyscene(tmp_path / "s.pyscene").build("s")
+    assert len(s.indices) == 2 * 760
+    r0 = np.linalg.norm(s.positions[s.indices[:760].reshape(-1)].astype(np.float64), axis=1)
+    r1 = np.linalg.norm(s.positions[s.indices[760:].reshape(-1)].astype(np.float64) - [3, 0, 0], axis=1)
+    np.testing.assert_allclose(r0, 1.0, atol=2e-6)
+    np.testing.assert_allclose(r1, 1.0, atol=4e-6)
