@@ -95,6 +95,11 @@ def parse():
     ap.add_argument("--hit-order-record", type=int, default=1,
                     help="1: add the hit_order_traversal sub-record (the latency region again with the DXR-like "
                          "traversal-order any-hit stream, rsd_hit_order TRAVERSAL); 0: skip it")
+    ap.add_argument("--local-ranks", type=int, default=1,
+                    help="pre-flight of the N > 1 path on ONE GPU: run this many ranks as threads of this process over "
+                         "librsd's in-process communicator, through the same band-frame code as a torchrun launch "
+                         "(native frames, per-rank counter reductions, summed value / roofline, lag = F - 1 schedule); "
+                         "a rehearsal of the driver's multi-GPU run, not a measurement of N GPUs")
     ap.add_argument("--timing-events", choices=("hip", "torch", "off"), default="hip",
                     help="per-kernel timing events: hip = fence-free timing events (rsd.timing, default); "
                          "torch = torch.cuda.Event (a system-scope fence per record); off = none in the "
@@ -130,21 +135,91 @@ def host_cpus():
             "model": model}
 
 
+class SoloGroup:
+    """One rank (N = 1)."""
+    rank, world, native_ok, kind = 0, 1, False, "solo"
+
+    def barrier(self):
+        pass
+
+    def reduce(self, values, op):
+        return [float(v) for v in values]
+
+    def comms(self, n, device):
+        return [], "one rank"
+
+    def close(self):
+        pass
+
+
+class TorchGroup:
+    """One process per GPU under torchrun: torch.distributed (nccl = RCCL, or gloo for rehearsals); the band
+    frame's own communicators are librsd's RCCL ones, created collectively (NativeComm.rccl_group)."""
+    kind = "torch.distributed"
+
+    def __init__(self, rank, world, backend, device):
+        import torch.distributed as dist
+        self.dist, self.rank, self.world, self.backend, self.device = dist, rank, world, backend, device
+        self.native_ok = backend == "nccl"
+
+    def barrier(self):
+        self.dist.barrier()
+
+    def reduce(self, values, op):
+        import torch
+        t = torch.tensor([float(v) for v in values], dtype=torch.float64,
+                         device=self.device if self.backend == "nccl" else "cpu")
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX if op == "max" else self.dist.ReduceOp.SUM)
+        return [float(x) for x in t.tolist()]
+
+    def comms(self, n, device):
+        from rsd.shard import NativeComm
+        return NativeComm.rccl_group(self.rank, self.world, n, device=device)
+
+    def close(self):
+        self.dist.destroy_process_group()
+
+
+class ThreadGroup:
+    """--local-ranks N: rank k of N threads of this process sharing one GPU (the pre-flight of the N > 1 path):
+    barriers and reductions through host memory, the band frame's exchanges through librsd's in-process
+    communicator (one hub per frame slot, like one RCCL communicator per slot under torchrun)."""
+    kind = "threads (in-process communicator, one GPU)"
+    native_ok = True
+
+    def __init__(self, rank, shared):
+        self.rank, self.world, self.sh = rank, shared["world"], shared
+
+    def barrier(self):
+        self.sh["barrier"].wait()
+
+    def reduce(self, values, op):
+        sh = self.sh
+        sh["slots"][self.rank] = [float(v) for v in values]
+        sh["barrier"].wait()
+        cols = list(zip(*sh["slots"]))
+        out = [max(c) if op == "max" else math.fsum(c) for c in cols]
+        sh["barrier"].wait()  # every rank read the slots before the next reduction writes them
+        return out
+
+    def comms(self, n, device):
+        from rsd.shard import NativeComm
+        return [NativeComm.local(self.sh["hubs"][j], self.rank) for j in range(n)], None
+
+    def close(self):
+        pass
+
+
 def main():
     args = parse()
-    import numpy as np
+    if args.local_ranks > 1:
+        return run_threads(args)
     import torch
-
-    from rsd import abi
-    from rsd.frame import CONFIGS, DEFAULT_CAMERA_PATH, FrameConfig, Renderer, camera_path
-    from rsd.scenes import make_scene
-    from rsd.shard import BandFrame, HaloFrame, NativeComm, NativeHaloFrame
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    backend = None
+    grp = SoloGroup()
     if world > 1:
         import torch.distributed as dist
         # RSD_BENCH_BACKEND=gloo: rehearsal of the N > 1 code paths with several ranks on one GPU
@@ -157,37 +232,109 @@ def main():
             local = local % torch.cuda.device_count()
             torch.cuda.set_device(local)
             dist.init_process_group(backend)
+        grp = TorchGroup(rank, world, backend, torch.device("cuda", local))
+    run_rank(args, grp, local)
 
+
+def run_threads(args):
+    """--local-ranks N: N rank threads over one GPU through run_rank (the same N > 1 code as torchrun's ranks).
+    The scene, its BVH and the device handle are shared (one GPU); every rank has its own renderer, frame
+    buffers, G-buffer, streams and band frames."""
+    import threading
+
+    import torch
+
+    from rsd.frame import CONFIGS, Device, GpuScene
+    from rsd.scenes import make_scene
+    from rsd.shard import NativeHub
+    world = args.local_ranks
+    F = max(1, args.frames_in_flight)
+    torch.cuda.set_device(0)
+    _, scene_name = CONFIGS[args.config]
+    if args.scene_file:
+        from rsd.pyscene import load_scene_file
+        scene = load_scene_file(args.scene_file).build(os.path.basename(args.scene_file))
+    else:
+        scene = make_scene(scene_name)
+    dev = Device(0)
+    gs = GpuScene(dev, scene)
+    shared = {"world": world, "barrier": threading.Barrier(world), "slots": [None] * world,
+              "hubs": [NativeHub(world) for _ in range(F)], "scene": scene, "gscene": gs, "dev": dev}
+    errors = []
+
+    def rank_main(k):
+        try:
+            with torch.cuda.stream(torch.cuda.Stream()):  # this rank's own default stream (torch's is per thread)
+                run_rank(args, ThreadGroup(k, shared), 0, shared)
+        except BaseException:  # noqa: BLE001 -- reported below; the other ranks may then wait at a barrier
+            import traceback
+            errors.append((k, traceback.format_exc()))
+            shared["barrier"].abort()
+
+    threads = [threading.Thread(target=rank_main, args=(k,)) for k in range(world)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join()
+    torch.cuda.synchronize()
+    for h in shared["hubs"]:
+        h.close()
+    gs.release()
+    dev.close()
+    if errors:
+        for k, tb in errors:
+            print(f"bench.py: rank thread {k} failed:\n{tb}", file=sys.stderr)
+        raise SystemExit(1)
+
+
+def run_rank(args, grp, local, shared=None):
+    """One rank's bench (rank 0 prints the line): grp = SoloGroup (N = 1), TorchGroup (torchrun, one GPU per
+    rank) or ThreadGroup (--local-ranks: rank threads sharing one GPU)."""
+    import numpy as np
+    import torch
+
+    from rsd import abi
+    from rsd.frame import CONFIGS, DEFAULT_CAMERA_PATH, FrameConfig, Renderer, camera_path
+    from rsd.scenes import make_scene
+    from rsd.shard import BandFrame, HaloFrame, NativeHaloFrame
+
+    rank, world = grp.rank, grp.world
+    dist = grp if world > 1 else None
     kw, scene_name = CONFIGS[args.config]
     cfg = FrameConfig(**kw)
     shard = args.shard or "band"
     path_name = args.camera_path or DEFAULT_CAMERA_PATH.get(args.config, "static")
     poses = camera_path(path_name)
-    if args.scene_file:
-        from rsd.pyscene import load_scene_file
-        scene_name = os.path.basename(args.scene_file)
-        scene = load_scene_file(args.scene_file).build(scene_name)
+    if shared is not None:
+        scene = shared["scene"]
+        scene_name = scene.name
+        r = Renderer(scene, cfg, device=local, gpu_scene=shared["gscene"], dev=shared["dev"])
     else:
-        scene = make_scene(scene_name)
-    r = Renderer(scene, cfg, device=local)
+        if args.scene_file:
+            from rsd.pyscene import load_scene_file
+            scene_name = os.path.basename(args.scene_file)
+            scene = load_scene_file(args.scene_file).build(scene_name)
+        else:
+            scene = make_scene(scene_name)
+        r = Renderer(scene, cfg, device=local)
     # clean tiles: band frames void the stamps on a re-split; the gather split all-reduces whole maps
     r.keep_clean_tiles(args.clean_tiles == "on" and shard != "gather")
     bvh_build_s = r.gscene.info.build_ms * 1e-3
     bw = (rank, world) if shard == "gather" else (0, 1)
     F = max(1, args.frames_in_flight)
-    # N > 1 band frames issued from C++ (rsd_band_frame) over librsd's own RCCL communicators -- one per frame
-    # slot, so every communicator's operations stay on one stream; the gloo rehearsal keeps HaloFrame
-    native = shard == "band" and world > 1 and backend == "nccl" and args.frame_impl == "native"
+    # N > 1 band frames issued from C++ (rsd_band_frame) over librsd's own communicators -- one per frame slot,
+    # so every communicator's operations stay on one stream: RCCL under torchrun (created collectively: the ranks
+    # fall back to rsd/shard.py HaloFrame together when any rank cannot), in-process for rank threads; the gloo
+    # rehearsal keeps HaloFrame
+    native = shard == "band" and world > 1 and grp.native_ok and args.frame_impl == "native"
     comms = []
     if native:
-        try:
-            comms = [NativeComm.rccl(rank, world, device=torch.device("cuda", local)) for _ in range(F)]
-        except Exception as e:  # noqa: BLE001 -- librccl unusable here: the torch.distributed path, said on stderr
-            print(f"bench.py: librsd's RCCL communicator failed ({e}); falling back to rsd/shard.py HaloFrame",
-                  file=sys.stderr)
-            for c in comms:
-                c.close()
-            comms, native = [], False
+        comms, why = grp.comms(F, torch.device("cuda", local))
+        if not comms:
+            if rank == 0:
+                print(f"bench.py: librsd's RCCL communicators are not usable ({why}); every rank falls back to "
+                      "rsd/shard.py HaloFrame", file=sys.stderr)
+            native = False
 
     def make_frame(rend, throughput=False, slot=0):
         if shard == "band":
@@ -223,6 +370,7 @@ def main():
                 acc.append(r.sd_trace(counters=True, throughput=thr, band=bw))
     torch.cuda.synchronize()
     walk_seq, walk_thr = int(cnt_seq[0].walk), int(cnt_thr[0].walk)
+    walk_seq_inst = int(cnt_seq[0].walk_instrumented)
     mean_cnt = lambda cs, f: float(np.mean([getattr(c, f) for c in cs]))  # noqa: E731
     if dist:
         dist.barrier()
@@ -240,9 +388,7 @@ def main():
         torch.cuda.synchronize()
         wall = time.perf_counter() - t0
         if dist:
-            t = torch.tensor([wall], device="cuda")
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            wall = float(t.item())
+            wall = dist.reduce([wall], "max")[0]
         return wall
 
     # ---- latency region: one frame in flight, the latency-optimised trace walk
@@ -309,9 +455,25 @@ def main():
     thr_sd_ms = float(np.mean([a.elapsed_time(b) for a, b in ev_thr])) if thr_ev else float("nan")
 
     if dist:  # per-kernel times: the slowest rank
-        t = torch.tensor([seq_sd_ms, seq_ao_ms, thr_sd_ms], device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        seq_sd_ms, seq_ao_ms, thr_sd_ms = (float(x) for x in t.tolist())
+        seq_sd_ms, seq_ao_ms, thr_sd_ms = dist.reduce([seq_sd_ms, seq_ao_ms, thr_sd_ms], "max")
+
+    # N > 1 band frames (untimed): one more frame of the split, checked on rank 0 against the 1-GPU frame of the same
+    # pose (rsd_svao_frame on a frame slot of its own) -- every rank's gathered AO image must be those bits
+    band_check = None
+    if world > 1 and shard == "band":
+        pose(r, 0)
+        r.ao.zero_()
+        seq.frame()
+        torch.cuda.synchronize()
+        if rank == 0:
+            one = r.frame_slot(own_gbuffer=True)
+            one.gbuffer()
+            one.frame()
+            torch.cuda.synchronize()
+            band_check = {"ao_equals_one_gpu": bool(torch.equal(one.ao, r.ao)),
+                          "note": "rank 0's gathered AO image of one band frame vs rsd_svao_frame of the same pose"}
+        if dist:
+            dist.barrier()
 
     rays = r.sd_rays
     N = cfg.sd_samples
@@ -321,10 +483,8 @@ def main():
     # the segment entry grid's lookups: one 16-B hash slot + 32 B per frontier item tested
     entry_bytes = 16 * mean_cnt(cnt_seq, "entry_lookups") + 32 * mean_cnt(cnt_seq, "entry_items")
     if dist and shard != "frame":  # counters are per band: the frame's totals
-        t = torch.tensor([rays_active, mean_cnt(cnt_seq, "nodes_visited"), mean_cnt(cnt_seq, "tris_tested"),
-                          entry_bytes], device="cuda", dtype=torch.float64)
-        dist.all_reduce(t)
-        rays_active, nodes_seq, tris_seq, entry_bytes = t.tolist()
+        rays_active, nodes_seq, tris_seq, entry_bytes = dist.reduce(
+            [rays_active, mean_cnt(cnt_seq, "nodes_visited"), mean_cnt(cnt_seq, "tris_tested"), entry_bytes], "sum")
     else:
         nodes_seq, tris_seq = mean_cnt(cnt_seq, "nodes_visited"), mean_cnt(cnt_seq, "tris_tested")
     value = units * rays / (seq_sd_ms * 1e-3) / 1e6
@@ -335,13 +495,15 @@ def main():
     # (the store term counts only the texels written: clean tiles, --clean-tiles, are not rewritten)
     texels_clean = mean_cnt(cnt_seq, "texels_clean")
     if dist and shard != "frame":
-        t = torch.tensor([texels_clean], device="cuda", dtype=torch.float64)
-        dist.all_reduce(t)
-        texels_clean = float(t.item())
+        texels_clean = dist.reduce([texels_clean], "sum")[0]
     alg_bytes = rays * (16 + 8) + (rays - texels_clean) * 4 * N + 128 * nodes_seq + 48 * tris_seq + entry_bytes
     achieved = alg_bytes / (seq_sd_ms * 1e-3) / 1e9
     kernels_seq = abi.WALK_KERNELS[walk_seq]
     lat = latency_floor(cnt_seq, seq_sd_ms)
+    if lat.get("latency_floor_us") is not None:
+        # the step clocks come from the instrumented launch, which walks the row or quad walk alone -- for the hybrid
+        # launch (walk 6), the row walk its first blocks run over the longest-first rays
+        lat["latency_walk"] = abi.WALK_NAMES[walk_seq_inst]
     pmc = args.pmc_csv
     if pmc is None and not args.scene_file:
         # the committed passes of this config (tools/config_measure.sh -> profiles/roundN/configs/<config>/),
@@ -372,8 +534,7 @@ def main():
 
     if rank != 0:
         close_frames([seq] + slots, comms)
-        if dist:
-            dist.destroy_process_group()
+        grp.close()
         return
 
     cpu = None
@@ -443,16 +604,23 @@ def main():
         "exchange_bytes_per_frame": dict(seq.bytes_per_frame(), dense_halo_equivalent=seq.dense_bytes_per_frame(),
                                          final_split_groups=list(seq.gb))
         if shard == "band" and world > 1 else None,
+        "band_check": band_check,
         "hit_order_traversal": hit_trav,
         "hit_order_wavefront": hit_wave,
         "bvh_build_s": round(bvh_build_s, 3),
         "bvh_build_threads": int(r.gscene.info.build_threads),
         "cpu_baseline": cpu,
     }
+    if isinstance(grp, ThreadGroup):
+        line["n_gpus"] = 1
+        line["preflight"] = {"ranks": world, "group": grp.kind,
+                             "note": "--local-ranks: the N > 1 band-frame path run by N rank threads sharing ONE GPU "
+                                     "over librsd's in-process communicator -- the same bench.py code as a torchrun "
+                                     "launch, a rehearsal of the driver's multi-GPU run; its times are not those of "
+                                     "N GPUs (the ranks share one GPU and one Python interpreter)"}
     print(json.dumps(line))
     close_frames([seq] + slots, comms)
-    if dist:
-        dist.destroy_process_group()
+    grp.close()
 
 
 def close_frames(frames, comms):

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define RSD_ABI_VERSION 6
+#define RSD_ABI_VERSION 7
 
 typedef enum {
     RSD_OK = 0,
@@ -251,6 +251,10 @@ typedef struct {
     uint64_t row_steps;
     double shader_clock_mhz;
     uint64_t texels_clean;   /* SD texels of clean tiles the setup did not rewrite (rsd_sd_params.d_tile_state) */
+    /* ABI v7: the walk the instrumented launch itself ran (RSD_WALK_*).  `walk` names the walk an uninstrumented
+     * trace of the same call takes (the kernels a caller's timed traces ran); the step clocks above belong to
+     * walk_instrumented (the hybrid walk is instrumented through its row or quad walk alone). */
+    uint64_t walk_instrumented;
 } rsd_counters;
 /* rsd_counters.walk: which kernels an rsd_sd_trace launched (besides sd_setup_kernel) */
 #define RSD_WALK_QUAD 0u   /* sd_trace_queue_kernel: depth-first, 4 lanes per ray */
@@ -521,6 +525,9 @@ typedef struct rsd_comm_hub rsd_comm_hub;
 #define RSD_COMM_RCCL 1u
 #define RSD_COMM_LOCAL 2u
 #define RSD_COMM_NULL 3u   /* moves nothing: host-cost probes of one rank's frame (diagnostics only) */
+/* ABI v7: RSD_OK when librccl.so.1 loads with every symbol the RCCL communicator uses (no RCCL call, no
+ * socket: every rank may ask, so that the ranks can agree on the native path before the collective create) */
+rsd_status rsd_comm_rccl_available(void);
 rsd_status rsd_comm_rccl_unique_id(uint8_t id[RSD_COMM_UNIQUE_ID_BYTES]);
 rsd_status rsd_comm_rccl_create(const uint8_t id[RSD_COMM_UNIQUE_ID_BYTES], uint32_t world, uint32_t rank,
                                 rsd_comm** out);
@@ -559,7 +566,10 @@ rsd_status rsd_comm_exchange(rsd_comm* comm, const rsd_comm_xfer* sends, uint32_
  * Every SD texel and AO pixel is produced by exactly one rank with the same kernels: each rank's AO
  * image and its own SD share are bit-identical to the 1-GPU frame (rsd_svao_frame), whatever the split.
  * The split of the 32-row groups is re-balanced every fourth frame from the ranks' measured pass-1 +
- * trace + pass-2 times (same decision on every rank).  The count matrix reaches the host through pinned
+ * trace + pass-2 times (same decision on every rank): frame 4j + 1 is timed, its time is read in the back() of
+ * frame 4j + 2 (after that frame's counts arrived, so without waiting), travels with the counts of frame
+ * 4j + 3, whose back() decides, and front() of frame 4j + 4 applies the new split.  A camera whose focal
+ * length or frame height differs from the previous frame's re-plans the halo windows (the sample reach).  The count matrix reaches the host through pinned
  * memory written by a kernel (a sequence word the host polls): front and back of a frame must be issued on
  * the same stream.  The frame description's buffers are used in
  * place; its camera / params structs are copied (rsd_band_frame_front may pass a new camera).
@@ -576,6 +586,10 @@ typedef struct {
 typedef struct rsd_band_frame rsd_band_frame;
 rsd_status rsd_band_frame_create(const rsd_svao_frame_desc* frame, const rsd_band_params* params, rsd_comm* comm,
                                  rsd_band_frame** out);
+/* ABI v7: a split chosen by the caller (split[0] = 0 < split[1] < ... < split[world] = rsd_band_stats.groups;
+ * the same on every rank), applied by the next front(): e.g. a skewed start that the re-balancing corrects.
+ * It does not count as a re-split in rsd_band_stats.resplits. */
+rsd_status rsd_band_frame_set_split(rsd_band_frame* bf, const uint32_t* split, uint32_t n);
 /* cam: NULL or the camera of this frame (an animated camera; copied) */
 rsd_status rsd_band_frame_front(rsd_band_frame* bf, const rsd_camera* cam, rsd_stream stream);
 /* events: NULL or 2 hipEvent_t (each may be NULL) recorded before and after this rank's SD trace */

@@ -125,6 +125,7 @@ public:
     }
 
     rsd_status init(const rsd_svao_frame_desc& f, const rsd_band_params& bp, Comm* comm);
+    rsd_status set_split(const uint32_t* split, uint32_t n);
     rsd_status front(const rsd_camera* cam, hipStream_t s);
     rsd_status back(void* const* events, hipStream_t s);
     void stats(rsd_band_stats& o) const;
@@ -169,9 +170,17 @@ private:
     uint32_t evn_ = 0;
     bool prev_valid_ = false;
     uint32_t prev_set_ = 0;
-    // timed_: this frame records the six timing events -- only the frames whose cost a re-split reads (every
-    // fourth: frames 4j + 3; the back() of frames 4j decides from them), 1.5 event records per frame on average
+    // Re-split cadence (every fourth frame of this object): frame 4j + 1 records the six timing events (timed_;
+    // 1.5 event records per frame on average); the back() of frame 4j + 2 reads their time once its count matrix
+    // has arrived -- this object's frames run on one stream, so frame 4j + 1 has completed by then (cost_ready_,
+    // -1 if not); front() of frame 4j + 3 puts it in the count row, the back() of frame 4j + 3 decides from every
+    // rank's time (all ranks see the same matrix: all skip or all re-split) and front() of frame 4j + 4 applies it
     bool timed_ = false;
+    int64_t cost_ready_ = -1;
+    hipStream_t timed_stream_ = nullptr;
+    bool next_forced_ = false;  // next_gb_ came from rsd_band_frame_set_split
+    // the camera terms halo_px_ was computed from (a zoom changes the sample reach: re-plan)
+    float halo_focal_ = 0.0f, halo_frame_h_ = 0.0f;
     bool open_ = false;
     hipStream_t last_ = nullptr;
     // statistics
@@ -236,6 +245,8 @@ rsd_status BandFrame::init(const rsd_svao_frame_desc& f, const rsd_band_params& 
     consume_ = true;  // RayInterval: the trace resets the interval maps it read
     rebalance_ = bp.rebalance && world_ > 1;
     halo_px_ = halo_reach_px(f.width, f.height, cam_.focalLength, cam_.frameHeight, vao_.ssMaxRadius);
+    halo_focal_ = cam_.focalLength;
+    halo_frame_h_ = cam_.frameHeight;
     gb_.resize(world_ + 1);
     for (uint32_t r = 0; r <= world_; ++r) gb_[r] = (uint32_t)((uint64_t)G_ * r / world_);
     ao_row_bytes_ = (size_t)f.width * (svp_.dual_ao ? 2u : 1u);
@@ -414,6 +425,23 @@ std::vector<uint32_t> BandFrame::rebalanced(const std::vector<double>& costs) co
     return nw;
 }
 
+// a split chosen by the caller (every rank the same), applied by the next front(): a skewed start for tests of the
+// re-balancing, or a split carried over from an earlier run
+rsd_status BandFrame::set_split(const uint32_t* split, uint32_t n) {
+    if (!split || n != world_ + 1 || split[0] != 0 || split[world_] != G_) {
+        set_error("rsd_band_frame_set_split: need world + 1 group boundaries from 0 to the group count");
+        return RSD_ERR_INVALID_ARG;
+    }
+    for (uint32_t k = 0; k < world_; ++k)
+        if (split[k + 1] < split[k] || (G_ >= world_ && split[k + 1] == split[k])) {
+            set_error("rsd_band_frame_set_split: boundaries must increase (one group per rank at least)");
+            return RSD_ERR_INVALID_ARG;
+        }
+    next_gb_.assign(split, split + n);
+    next_forced_ = true;
+    return RSD_OK;
+}
+
 rsd_status BandFrame::front(const rsd_camera* cam, hipStream_t s) {
     if (open_) {
         set_error("rsd_band_frame_front: front() twice without back()");
@@ -421,21 +449,36 @@ rsd_status BandFrame::front(const rsd_camera* cam, hipStream_t s) {
     }
     last_ = s;
     if (cam) cam_ = *cam;
+    // a zoom (focal length) or a new sensor height changes how far a sample reaches (ssMaxRadius projected,
+    // VAOData.slang:44): the windows and exchange regions follow it -- every rank gets the same camera
+    bool replan = false;
+    if (cam_.focalLength != halo_focal_ || cam_.frameHeight != halo_frame_h_) {
+        halo_px_ = halo_reach_px(f_.width, f_.height, cam_.focalLength, cam_.frameHeight, vao_.ssMaxRadius);
+        halo_focal_ = cam_.focalLength;
+        halo_frame_h_ = cam_.frameHeight;
+        replan = true;
+    }
     if (!next_gb_.empty() && next_gb_ != gb_) {
         gb_ = next_gb_;
-        ++resplits_;
+        if (!next_forced_) ++resplits_;
+        replan = true;
+    }
+    next_gb_.clear();
+    next_forced_ = false;
+    if (replan) {
         rsd_status st = plan(s);
         if (st != RSD_OK) return st;
     }
-    next_gb_.clear();
     rsd_status st = RSD_OK;
     if (!(consume_ && intervals_clear_)) {
         st = rsd_svao_clear_intervals(f_.d_ray_min, f_.d_ray_max, f_.sd_w * f_.sd_h, s);
         if (st != RSD_OK) return st;
     }
-    // the cost entry of the count row: this object's last timed frame, read by the back() of frames 4j
-    const int64_t prev_us = frames_ % 4 == 0 ? prev_cost_us() : -1;
-    timed_ = rebalance_ && frames_ % 4 == 3;
+    // the cost entry of the count row: this object's frame 4j + 1, read by the back() of frame 4j + 2
+    const int64_t prev_us = frames_ % 4 == 3 ? cost_ready_ : -1;
+    if (frames_ % 4 == 3) cost_ready_ = -1;
+    timed_ = rebalance_ && frames_ % 4 == 1;
+    if (timed_) timed_stream_ = s;
     if ((st = mark(s)) != RSD_OK) return st;
     st = rsd_svao_pass1_rows(&cam_, &vao_, &svp_, f_.d_depth, f_.d_normals, f_.width, f_.height, f_.d_ao, f_.d_stencil,
                              f_.d_ray_min, f_.d_ray_max, f_.sd_w, f_.sd_h, px_rows_[me_].first, px_rows_[me_].second, s);
@@ -487,8 +530,10 @@ rsd_status BandFrame::back(void* const* events, hipStream_t s) {
     std::vector<int64_t> M((size_t)W * (W + 1));
     for (size_t i = 0; i < M.size(); ++i) M[i] = pub[1 + i];
     auto cnt = [&](uint32_t from, uint32_t to) { return (uint64_t)std::max<int64_t>(0, M[(size_t)from * (W + 1) + to]); };
-    // re-split on every second frame (every rank sees the same counts: all skip or all re-split)
-    if (rebalance_ && frames_ % 4 == 0) {
+    // frame 4j + 2: the timed frame 4j + 1 ran before this frame's counts on this stream -- its time is final
+    if (rebalance_ && frames_ % 4 == 2) cost_ready_ = s == timed_stream_ ? prev_cost_us() : -1;
+    // re-split every fourth frame (every rank sees the same counts: all skip or all re-split)
+    if (rebalance_ && frames_ % 4 == 3) {
         std::vector<double> costs(W);
         bool ok = true;
         for (uint32_t k = 0; k < W; ++k) {
@@ -653,6 +698,14 @@ extern "C" rsd_status rsd_band_frame_create(const rsd_svao_frame_desc* frame, co
     }
     *out = new rsd_band_frame{bf};
     return RSD_OK;
+}
+
+extern "C" rsd_status rsd_band_frame_set_split(rsd_band_frame* bf, const uint32_t* split, uint32_t n) {
+    if (!bf || !bf->impl) {
+        set_error("rsd_band_frame_set_split: null frame");
+        return RSD_ERR_INVALID_ARG;
+    }
+    return bf->impl->set_split(split, n);
 }
 
 extern "C" rsd_status rsd_band_frame_front(rsd_band_frame* bf, const rsd_camera* cam, rsd_stream stream) {

@@ -314,6 +314,11 @@ rsd_status check_comm(const rsd_comm* c, const char* who) {
 
 using namespace rsd;
 
+extern "C" rsd_status rsd_comm_rccl_available(void) {
+    const Rccl* r = nullptr;
+    return rccl_load(&r);
+}
+
 extern "C" rsd_status rsd_comm_rccl_unique_id(uint8_t id[RSD_COMM_UNIQUE_ID_BYTES]) {
     if (!id) {
         set_error("rsd_comm_rccl_unique_id: null output");

@@ -2593,14 +2593,16 @@ rsd_status sd_trace_impl(rsd_scene* scene, const rsd_camera* cam, const rsd_sd_p
     // (sd_trace_hybrid_kernel: its first blocks run the row walk over the longest-first end of each queue partition,
     // the others the quad walk over the rest), where the fused row walk (configs[1]: 74 -> 66 us) or the quad walk
     // (configs[3] 268 -> 195 us, configs[2] 236 -> 177 us) would walk every ray alike.  Only for 8-lane rows
-    // (K <= 8: with K = 16 the 16-lane row walk is the slower one) and one frame in flight: with frames in flight
-    // (RSD_SD_THROUGHPUT) the machine is already full of other frames' work and the quad walk's lane use wins
-    // (RSD_TRACE_HYBRID=all: configs[2] 0.188-0.191 -> 0.202-0.206 ms per frame, configs[3] 0.308-0.317 ->
-    // 0.327-0.347; profiles/round5/hybrid/in_flight/).  RSD_TRACE_HYBRID=off disables it;
+    // (K <= 8: with K = 16 the 16-lane row walk is the slower one).  With frames in flight (RSD_SD_THROUGHPUT) it
+    // replaces the fused row walk of the small maps (configs[1]: 0.0834-0.0860 -> 0.0815-0.0840 ms per frame, three
+    // alternating pairs, profiles/round6/hybrid_in_flight/), but not the quad walk of the full-resolution maps: there
+    // the machine is already full of other frames' work and the quad walk's lane use wins (RSD_TRACE_HYBRID=all:
+    // configs[2] 0.188-0.191 -> 0.202-0.206 ms per frame, configs[3] 0.308-0.317 -> 0.327-0.347;
+    // profiles/round5/hybrid/in_flight/).  RSD_TRACE_HYBRID=off disables it, =all takes it for every walk;
     // RSD_TRACE_HYBRID_ROWWPC / RSD_TRACE_WAVES_PER_CU set the row / quad blocks per CU (A/B runs).
     const char* hyEnv = std::getenv("RSD_TRACE_HYBRID");
     const bool hybridOk = (walk == 0 || walk == 1) && K <= 8 && a.lpt && a.poolSoft >= 16 &&
-                          (!throughput || (hyEnv && std::string(hyEnv) == "all")) &&
+                          (!throughput || walk == 1 || (hyEnv && std::string(hyEnv) == "all")) &&
                           !(hyEnv && std::string(hyEnv) == "off") && !a.alphaTest && a.impl != 1u && a.impl != 3u &&
                           a.maxCount <= (uint32_t)K && !(specEnvOff());
     if (hybridOk && !counters) {
@@ -2635,9 +2637,10 @@ rsd_status sd_trace_impl(rsd_scene* scene, const rsd_camera* cam, const rsd_sd_p
         counters->sum_ray_clocks = h[7];
         counters->max_ray_clocks = h[8];
         counters->leaves_visited = h[9];
-        // (an instrumented trace walks the quad kernel alone; walk reports the hybrid the same trace takes without
-        // counters, so that a caller prices the kernels that ran in its timed traces)
+        // walk: the hybrid an uninstrumented trace of this call takes (the kernels a caller's timed traces ran);
+        // walk_instrumented: the walk this instrumented launch ran (its step clocks), never the hybrid
         counters->walk = (uint64_t)((walk == 0 || walk == 1) && hybridOk ? 6 : walk);
+        counters->walk_instrumented = (uint64_t)walk;
         counters->entry_lookups = h[19];
         counters->entry_items = h[20];
         // row walk (instrumented): per-step clock sums and the clock of the instrumented launch

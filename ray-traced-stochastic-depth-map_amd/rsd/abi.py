@@ -155,7 +155,7 @@ class Counters(C.Structure):
                 ("leaves_visited", C.c_uint64), ("walk", C.c_uint64), ("entry_lookups", C.c_uint64),
                 ("entry_items", C.c_uint64), ("step_fetch_clocks", C.c_uint64), ("step_compute_clocks", C.c_uint64),
                 ("step_pool_clocks", C.c_uint64), ("row_steps", C.c_uint64), ("shader_clock_mhz", C.c_double),
-                ("texels_clean", C.c_uint64)]
+                ("texels_clean", C.c_uint64), ("walk_instrumented", C.c_uint64)]
 
 
 WALK_QUAD, WALK_FUSED, WALK_SPLIT, WALK_ORDERED, WALK_RASTER, WALK_WAVEFRONT, WALK_HYBRID = 0, 1, 2, 3, 4, 5, 6
@@ -181,10 +181,10 @@ EXPORTS = ["rsd_abi_version", "rsd_svao_tile_count", "rsd_sd_tile_state_count", 
            "rsd_scene_upload_alpha", "rsd_ray_cone_spread", "rsd_sd_trace_band_ex", "rsd_scene_export_bvh",
            "rsd_bvh_build", "rsd_svao_pass1_rows", "rsd_svao_pass2_rows", "rsd_sd_trace_rows", "rsd_svao_frame",
            "rsd_halo_compact", "rsd_halo_merge", "rsd_halo_sd_gather", "rsd_halo_sd_scatter",
-           "rsd_comm_rccl_unique_id", "rsd_comm_rccl_create", "rsd_comm_hub_create", "rsd_comm_hub_release",
+           "rsd_comm_rccl_available", "rsd_comm_rccl_unique_id", "rsd_comm_rccl_create", "rsd_comm_hub_create", "rsd_comm_hub_release",
            "rsd_comm_local_create", "rsd_comm_null_create", "rsd_comm_release", "rsd_comm_info", "rsd_comm_all_gather", "rsd_comm_exchange",
            "rsd_band_frame_create", "rsd_band_frame_front", "rsd_band_frame_back", "rsd_band_frame_stats",
-           "rsd_band_frame_release"]
+           "rsd_band_frame_release", "rsd_band_frame_set_split"]
 
 SD_CONSUME_INTERVALS = 1
 SD_THROUGHPUT = 2  # frames in flight: the work-efficient traversal (rsd.h RSD_SD_THROUGHPUT)
@@ -291,6 +291,8 @@ def lib():
         L.rsd_halo_sd_gather.argtypes = [vp, u32, u32, u32, u32, C.POINTER(HaloSdList), u32, vp]
         L.rsd_halo_sd_scatter.restype = st
         L.rsd_halo_sd_scatter.argtypes = [vp, u32, u32, u32, u32, C.POINTER(HaloSdList), u32, vp]
+        L.rsd_comm_rccl_available.restype = st
+        L.rsd_comm_rccl_available.argtypes = []
         L.rsd_comm_rccl_unique_id.restype = st
         L.rsd_comm_rccl_unique_id.argtypes = [vp]
         L.rsd_comm_rccl_create.restype = st
@@ -319,6 +321,8 @@ def lib():
         L.rsd_band_frame_back.argtypes = [vp, vp, vp]
         L.rsd_band_frame_stats.restype = st
         L.rsd_band_frame_stats.argtypes = [vp, C.POINTER(BandStats)]
+        L.rsd_band_frame_set_split.restype = st
+        L.rsd_band_frame_set_split.argtypes = [vp, C.POINTER(u32), u32]
         L.rsd_band_frame_release.restype = None
         L.rsd_band_frame_release.argtypes = [vp]
         L.rsd_svao_pass2_raytraced.restype = st
@@ -400,3 +404,8 @@ class RsdError(RuntimeError):
 def check(status, where):
     if status != RSD_OK:
         raise RsdError(status, where)
+
+
+def last_error() -> str:
+    """librsd's message of the last failed call on this thread."""
+    return lib().rsd_last_error().decode(errors="replace")

@@ -799,6 +799,65 @@ class NativeComm:
         return cls(h)
 
     @classmethod
+    def rccl_group(cls, rank: int, world: int, n: int = 1, pg=None, device=None):
+        """`n` RCCL communicators over torch.distributed's group, created COLLECTIVELY so that the ranks fall back
+        together: every rank first checks that librccl loads (rsd_comm_rccl_available) and the ranks
+        agree on it (all-reduce MIN); rank 0 then draws the n ids and broadcasts them with a success flag (a
+        failing rank 0 sends the flag, it does not raise before the broadcast); every rank creates its
+        communicators and the ranks agree again.  Returns (communicators, None), or ([], reason) on every rank
+        when any rank failed -- the caller takes the torch.distributed path.  (A rank failing INSIDE
+        ncclCommInitRank after its peers entered it cannot be recovered from here: RCCL's own init is the
+        collective.)"""
+        import ctypes as C
+
+        import torch
+        import torch.distributed as dist
+
+        from . import abi
+        L = abi.lib()
+        on_gpu = world > 1 and dist.get_backend(pg) == "nccl"
+        dev = device if on_gpu else "cpu"
+
+        def agree(ok: bool) -> bool:
+            if world == 1:
+                return ok
+            t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MIN, group=pg)
+            return bool(int(t.item()))
+
+        if not agree(L.rsd_comm_rccl_available() == 0):
+            return [], "librccl.so.1 is not usable on every rank: " + abi.last_error()
+        B = abi.COMM_UNIQUE_ID_BYTES
+        buf = bytearray(1 + n * B)
+        if rank == 0:
+            ok, uid = True, (C.c_uint8 * B)()
+            for j in range(n):
+                if L.rsd_comm_rccl_unique_id(uid) != 0:
+                    ok = False
+                    break
+                buf[1 + j * B:1 + (j + 1) * B] = bytes(uid)
+            buf[0] = 1 if ok else 0
+        if world > 1:
+            t = torch.tensor(list(buf), dtype=torch.uint8, device=dev)
+            dist.broadcast(t, src=0, group=pg)
+            buf = bytearray(t.cpu().tolist())
+        if not buf[0]:
+            return [], "rank 0 could not draw the RCCL unique ids"
+        comms, err = [], None
+        for j in range(n):
+            uid = (C.c_uint8 * B)(*buf[1 + j * B:1 + (j + 1) * B])
+            h = C.c_void_p()
+            if L.rsd_comm_rccl_create(uid, world, rank, C.byref(h)) != 0:
+                err = abi.last_error()
+                break
+            comms.append(cls(h))
+        if not agree(err is None):
+            for c in comms:
+                c.close()
+            return [], f"rsd_comm_rccl_create failed on some rank ({err or 'peer'})"
+        return comms, None
+
+    @classmethod
     def local(cls, hub: NativeHub, rank: int):
         import ctypes as C
 
@@ -849,8 +908,11 @@ class NativeHaloFrame:
     copy to the host (front); the count read, the interval triples' point-to-point transfer and merge, the
     trace of the rank's SD share, the SD replies, pass 2 of its rows and the AO all-gather (back) -- with the
     exchanges on `comm` (NativeComm: RCCL, or in-process threads).  Same kernels, same bits as HaloFrame
-    and as the 1-GPU frame; the re-balancing rule is HaloFrame._rebalanced's.  `backend` is a Renderer (or
-    a frame slot of one): its buffers are used in place, its current camera is passed on every front()."""
+    and as the 1-GPU frame; the re-balancing rule is HaloFrame._rebalanced's, its cadence is not: HaloFrame
+    re-splits every second frame from the previous frame's time, the native frame every fourth frame (frame
+    4j + 1 timed, decided at 4j + 3, applied at 4j + 4: the time is read without waiting, rsd.h).  A camera
+    whose focal length or frame height changes re-plans the halo windows.  `backend` is a Renderer (or a frame
+    slot of one): its buffers are used in place, its current camera is passed on every front()."""
 
     def __init__(self, backend, comm: NativeComm, throughput: bool = False, rebalance: bool = True,
                  sd_split: str = "auto"):
@@ -891,6 +953,14 @@ class NativeHaloFrame:
     def frame(self, sd_events=None):
         self.front()
         self.back(sd_events)
+
+    def set_split(self, groups):
+        """A split of the 32-row groups applied by the next front() (every rank the same; rsd_band_frame_set_split)."""
+        import ctypes as C
+
+        from . import abi
+        a = (C.c_uint32 * len(groups))(*[int(g) for g in groups])
+        abi.check(self._L.rsd_band_frame_set_split(self.h, a, len(groups)), "rsd_band_frame_set_split")
 
     def stats(self):
         import ctypes as C

@@ -178,6 +178,140 @@ def test_native_band_frame_camera_path_and_rebalance():
     r.close()
 
 
+def _rank_threads(world, run):
+    threads = [threading.Thread(target=run, args=(k,)) for k in range(world)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(timeout=250)
+    assert not any(t.is_alive() for t in threads)
+
+
+@pytest.mark.timeout(300)
+def test_native_band_frame_skewed_split_rebalances():
+    """A deliberately skewed first split (rsd_band_frame_set_split: three ranks with one 32-row group each) is
+    re-balanced from the measured per-rank times -- the re-split path on a live stream (tile-state voiding, region
+    and buffer re-sizing) -- while every frame stays equal to the 1-GPU frame and every rank holds the same split
+    (resplits > 0 asserted)."""
+    import torch
+    from rsd.shard import NativeComm, NativeHaloFrame, NativeHub
+    r, ref = _renderer("suntemple_1080p_q")
+    r.keep_clean_tiles()
+    world, frames = 4, 13
+    hub = NativeHub(world)
+    comms = [NativeComm.local(hub, k) for k in range(world)]
+    slots = []
+    for k in range(world):
+        rr = r.frame_slot()
+        st = torch.cuda.Stream()
+        st.wait_stream(torch.cuda.current_stream())
+        slots.append((rr, st, NativeHaloFrame(rr, comms[k])))
+    G = slots[0][2].stats().groups
+    skew = [0, 1, 2, 3, G]
+    for _, _, f in slots:
+        f.set_split(skew)
+    torch.cuda.synchronize()
+    out, errors, splits = {}, [], {}
+
+    def run(k):
+        try:
+            rr, st, f = slots[k]
+            with torch.cuda.stream(st):
+                for i in range(frames):
+                    rr.ao.zero_()
+                    f.frame()
+                    out[(k, i)] = rr.ao.clone()
+                    splits[(k, i)] = tuple(f.gb)
+        except Exception:  # noqa: BLE001
+            import traceback
+            errors.append((k, traceback.format_exc()))
+
+    _rank_threads(world, run)
+    torch.cuda.synchronize()
+    assert not errors, errors
+    for k in range(world):
+        for i in range(frames):
+            assert np.array_equal(out[(k, i)].cpu().numpy(), ref["ao"]), f"rank {k} frame {i}"
+        g = slots[k][0].numpy()
+        for lo, hi in slots[k][2].owned_sd_rows():
+            assert bits_equal(g["sd"][:, lo:hi], ref["sd"][:, lo:hi]), f"rank {k} SD rows {lo}-{hi}"
+    for i in range(frames):
+        assert len({splits[(k, i)] for k in range(world)}) == 1, f"frame {i}: ranks disagree on the split"
+    assert splits[(0, 0)] == tuple(skew)
+    st = [f.stats() for _, _, f in slots]
+    assert all(x.resplits >= 1 for x in st), [x.resplits for x in st]
+    # the last rank held 3/4 of the rows: the re-balancing moved boundaries towards it
+    assert splits[(0, frames - 1)][3] > 3
+    for _, _, f in slots:
+        f.close()
+    for c in comms:
+        c.close()
+    hub.close()
+    r.close()
+
+
+@pytest.mark.timeout(300)
+def test_native_band_frame_zoom_replans_halo():
+    """A camera whose focal length changes between frames (a zoom) changes how far a sample reaches on screen:
+    the band frame re-plans its windows and exchange regions, and every rank's frame of every pose
+    stays equal to the 1-GPU frame."""
+    import dataclasses
+
+    import torch
+    from rsd.frame import look_at
+    from rsd.shard import NativeComm, NativeHaloFrame, NativeHub
+    r, _ = _renderer("suntemple_1080p_q")
+    sc = r.scene.camera
+    poses = [dataclasses.replace(r.cfg, focal_length=f) for f in (21.0, 9.0, 35.0, 9.0, 14.0)]
+    cams = [look_at(sc["pos"], sc["target"], sc["up"], c) for c in poses]
+    refs = []
+    for cam in cams:
+        r.cam = cam
+        r.gbuffer()
+        r.frame()
+        refs.append(r.numpy()["ao"])
+    world = 4
+    hub = NativeHub(world)
+    comms = [NativeComm.local(hub, k) for k in range(world)]
+    slots = []
+    for k in range(world):
+        rr = r.frame_slot(own_gbuffer=True)
+        st = torch.cuda.Stream()
+        st.wait_stream(torch.cuda.current_stream())
+        slots.append((rr, st, NativeHaloFrame(rr, comms[k])))
+    torch.cuda.synchronize()
+    out, errors, halo = {}, [], {}
+
+    def run(k):
+        try:
+            rr, st, f = slots[k]
+            with torch.cuda.stream(st):
+                for i, cam in enumerate(cams):
+                    rr.cam = cam
+                    rr.gbuffer()
+                    rr.ao.zero_()
+                    f.frame()
+                    out[(k, i)] = rr.ao.clone()
+                    halo[(k, i)] = int(f.stats().halo_px)
+        except Exception:  # noqa: BLE001
+            import traceback
+            errors.append((k, traceback.format_exc()))
+
+    _rank_threads(world, run)
+    torch.cuda.synchronize()
+    assert not errors, errors
+    for k in range(world):
+        for i in range(len(cams)):
+            assert np.array_equal(out[(k, i)].cpu().numpy(), refs[i]), f"rank {k} pose {i}"
+    assert halo[(0, 1)] > halo[(0, 0)] > halo[(0, 2)] and halo[(0, 3)] == halo[(0, 1)]
+    for _, _, f in slots:
+        f.close()
+    for c in comms:
+        c.close()
+    hub.close()
+    r.close()
+
+
 @pytest.mark.timeout(300)
 def test_rccl_world1_collectives_and_band_frame():
     """RCCL executes: a one-rank communicator (ncclCommInitRank, nranks = 1), an all-gather and a

@@ -350,3 +350,94 @@ def test_halo_frames_in_flight_interleaved(oracle, tmp_path, world):
     for r in range(world):
         for j in range(5):
             assert np.array_equal(np.load(tmp_path / f"lag_{r}_{j}.npy"), ref.np_ao), f"rank {r} frame {j}"
+
+
+def _rccl_group_worker(rank, world, port, out_dir, fail):
+    """NativeComm.rccl_group over gloo with librsd's RCCL entry points replaced by fakes: a rank that cannot use
+    RCCL must make EVERY rank fall back (no rank left blocked in a broadcast or a collective create)."""
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parents[1]
+    for p in (str(root), str(root / "ray-traced-stochastic-depth-map_amd")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    import torch.distributed as dist
+
+    from rsd import abi
+    from rsd.shard import NativeComm
+
+    class FakeLib:
+        def __init__(self, real):
+            self.real = real
+
+        def rsd_comm_rccl_available(self):
+            return 1 if fail == ("available", rank) else 0
+
+        def rsd_comm_rccl_unique_id(self, uid):
+            if fail == ("unique_id", rank):
+                return 1
+            for i in range(abi.COMM_UNIQUE_ID_BYTES):
+                uid[i] = (i * 7 + 3) & 255
+            return 0
+
+        def rsd_comm_rccl_create(self, uid, w, r, out):
+            return 1 if fail == ("create", rank) else 0
+
+        def rsd_last_error(self):
+            return b"fake failure"
+
+        def __getattr__(self, k):
+            return getattr(self.real, k)
+
+    real = abi.lib()
+    abi._lib = FakeLib(real)
+    created = []
+    NativeComm.__init__ = lambda self, h: created.append(h)  # no rsd_comm_info on a fake handle
+    NativeComm.close = lambda self: None
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    comms, why = NativeComm.rccl_group(rank, world, n=3)
+    np.save(os.path.join(out_dir, f"rg_{rank}.npy"), np.array([len(comms), why is None]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("fail", [None, ("available", 1), ("unique_id", 0), ("create", 1)])
+def test_rccl_group_falls_back_together(tmp_path, fail):
+    world = 2
+    mp.start_processes(_rccl_group_worker, args=(world, _free_port(), str(tmp_path), fail), nprocs=world, join=True,
+                       start_method="spawn")
+    got = [tuple(np.load(tmp_path / f"rg_{r}.npy")) for r in range(world)]
+    want = (3, 1) if fail is None else (0, 0)
+    assert got == [want] * world, got
+
+
+def test_bench_thread_group_reductions():
+    """bench.py's ThreadGroup (--local-ranks): barriers and max / sum reductions across rank threads, repeated
+    back to back (the slots are reused only after every rank has read them)."""
+    import sys
+    import threading
+    from pathlib import Path
+    sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+    import bench
+    world = 5
+    shared = {"world": world, "barrier": threading.Barrier(world), "slots": [None] * world}
+    out = {}
+
+    def run(k):
+        g = bench.ThreadGroup(k, shared)
+        res = []
+        for i in range(20):
+            res.append(g.reduce([k + i, 2.0 * k], "max"))
+            res.append(g.reduce([1.0, k * i], "sum"))
+            g.barrier()
+        out[k] = res
+
+    ts = [threading.Thread(target=run, args=(k,)) for k in range(world)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=60)
+    for k in range(world):
+        for i in range(20):
+            assert out[k][2 * i] == [world - 1 + i, 2.0 * (world - 1)]
+            assert out[k][2 * i + 1] == [float(world), float(i * sum(range(world)))]
