@@ -116,6 +116,9 @@ struct SDArgs {
     // diagnostics (instrumented fused walk, RSD_TRACE_RAYLOG): 8 words per queue slot {texel, steps,
     // nodes, leaves, keys found, clocks, TMax - TMin, TMin}
     uint32_t* rayLog;
+    // diagnostics (RSD_SETUP_DIAG, results wrong by design): 1 the setup kernel returns at once (the launch floor of a
+    // trace with an empty queue), 2 no texel is live (the setup's streaming part without the live rays' chains)
+    uint32_t diag;
 };
 
 // entry_lookup results besides first << 4 | count
@@ -148,10 +151,19 @@ __device__ __forceinline__ uint32_t entry_lookup(const SDArgs& a, f3 o, f3 d, fl
     uint32_t h = (uint32_t)((key * 0x9E3779B97F4A7C15ull) >> (64 - a.entBits));
     const uint32_t mask = (1u << a.entBits) - 1u;
     const uint32_t klo = (uint32_t)key, khi = (uint32_t)(key >> 32);
-    for (uint32_t n = 0; n <= a.entProbe; ++n, h = (h + 1u) & mask) {
-        const uint4 s = a.entSlots[h];
-        if (s.x == klo && s.y == khi) return s.z;
-        if (s.x == 0u && s.y == 0u) break;
+    // linear probing, four slots per round trip (the same slots, checked in the same order, as one at a time: a
+    // lane's chain of dependent probe loads is a quarter as long; round 6: configs[2] 180 -> 178 us, configs[1] and
+    // [3] unchanged -- the setup's live-ray path is not bound by its probe chain)
+    for (uint32_t n = 0; n <= a.entProbe; n += 4u, h = (h + 4u) & mask) {
+        uint4 sl[4];
+#pragma unroll
+        for (uint32_t k = 0; k < 4u; ++k) sl[k] = a.entSlots[(h + k) & mask];
+#pragma unroll
+        for (uint32_t k = 0; k < 4u; ++k) {
+            if (n + k > a.entProbe) return kEntryDead;
+            if (sl[k].x == klo && sl[k].y == khi) return sl[k].z;
+            if (sl[k].x == 0u && sl[k].y == 0u) return kEntryDead;
+        }
     }
     return kEntryDead;  // the level is complete: an absent cell overlaps no BVH box
 }
@@ -648,6 +660,7 @@ __global__ void __launch_bounds__(kSetupWaves * kBlock) sd_setup_kernel(SDArgs a
                                                                         uint32_t* __restrict__ qctlNext) {
     if (blockIdx.x == 0 && blockIdx.y == 0)
         for (int w = threadIdx.x; w < kQctlWords; w += kSetupWaves * kBlock) qctlNext[w] = 0u;
+    if (a.diag == 1u) return;
     // one wave per 8x8 tile, kSetupWaves tiles of a tile row per workgroup
     const int lane = threadIdx.x & (kBlock - 1);
     const int tileX = (int)blockIdx.x * kSetupWaves + (int)(threadIdx.x / kBlock);
@@ -683,7 +696,7 @@ __global__ void __launch_bounds__(kSetupWaves * kBlock) sd_setup_kernel(SDArgs a
         const bool untouched = a.deadFast && rmin == 0x7f7fffffu;
         // consume: words already at their reset values are not rewritten (both read here, one round trip)
         const bool atReset = a.consume && rmin == 0x7f7fffffu && a.rayMax[(size_t)y * a.sdW + x] == 0u;
-        live = !untouched && sd_ray(a, x, y, d, TMin, TMax, cosT);
+        live = !untouched && sd_ray(a, x, y, d, TMin, TMax, cosT) && a.diag != 2u;
         if (a.consume && !atReset) {  // after the last read of this texel's interval
             a.rayMinW[(size_t)y * a.sdW + x] = 0x7f7fffffu;
             a.rayMaxW[(size_t)y * a.sdW + x] = 0u;
@@ -2382,6 +2395,8 @@ rsd_status sd_trace_impl(rsd_scene* scene, const rsd_camera* cam, const rsd_sd_p
         a.spread = spreadEnv && std::string(spreadEnv) == "on" ? 1u : 0u;
         const char* qrEnv = std::getenv("RSD_TRACE_QRANGE");
         a.qrange = qrEnv && std::string(qrEnv) == "long" ? 1u : qrEnv && std::string(qrEnv) == "short" ? 2u : 0u;
+        const char* dgEnv = std::getenv("RSD_SETUP_DIAG");  // diagnostics: skip / nolive (results wrong by design)
+        a.diag = dgEnv && std::string(dgEnv) == "skip" ? 1u : dgEnv && std::string(dgEnv) == "nolive" ? 2u : 0u;
     }
     // clean tiles: the stamp names what DEFAULT_DEPTH looks like in this map (value, storage, layers)
     a.tileState = p->d_tile_state;

@@ -102,6 +102,9 @@ __device__ __forceinline__ void pass1_dir_generic(const SvaoArgs& a, float u, fl
 // "lean" direction body -- host constants in SGPRs, predicated updates, one float ratio compare --
 // measured 74 vs 70 us at configs[1]: more VALU per direction and 64-73 VGPRs)
 // ND > 0: NUM_DIRECTIONS known at compile time (the specialised kernel); 0: a.k.nd
+// (A workgroup-wide LDS copy of the depth texels around the 32 x 32 pixels plus a 16-texel apron, 16 KB, serving the
+// gathers inside it was measured slower at configs[1]-[3]: 46 -> 52 us, the copy costs more than the gathers it
+// serves; round 6, profiles/round6/pass1_window/.)
 template <bool SPEC, int ND>
 __global__ void __launch_bounds__(256) svao_pass1_kernel(SvaoArgs a) {
     uint32_t bx = blockIdx.x, by = blockIdx.y;

@@ -23,7 +23,10 @@ frame rate is bounded by max(overlapped GPU time, host issue time).
 Round 5: the product's clean SD tiles are on (Renderer.keep_clean_tiles; --no-clean-tiles: off), and the host issue
 is also measured for the native band frame (rsd_band_frame over the null communicator, librsd's own accounting:
 front + back minus the wait for the counts), the N > 1 path bench.py runs.
-usage: python tools/scaling_model.py [config] [--worlds 2,4,8] [--reps 15] [--pose i] [--sd-split auto|tiles|rows]"""
+Round 6: the throughput region too: the 1-GPU ms_per_step (F frames in flight) and, per world, the
+slowest rank's time per frame in flight measured alone on this GPU -> predicted_ms_per_step_us.
+usage: python tools/scaling_model.py [config] [--worlds 2,4,8] [--reps 15] [--pose i] [--sd-split auto|tiles|rows]
+       [--frames-in-flight 4]"""
 import json
 import statistics
 import sys
@@ -90,6 +93,28 @@ one = {"pass1_us": timed(r.pass1, r.clear_intervals),
        "trace_us": timed(lambda: r.sd_trace(), lambda: r.ray_minmax.copy_(union)),
        "pass2_us": timed(r.pass2, lambda: (r.clear_intervals(), r.pass1()))}
 one["gpu_us"] = one["pass1_us"] + one["trace_us"] + one["pass2_us"]
+
+
+def one_gpu_throughput(F=4, n=60):
+    """bench.py's N = 1 throughput region: rsd_svao_frame on F frame slots / streams, time per frame."""
+    slots = []
+    for j in range(F):
+        rr = r if j == 0 else r.frame_slot()
+        st = torch.cuda.current_stream() if j == 0 else torch.cuda.Stream()
+        slots.append((rr, st))
+    torch.cuda.synchronize()
+    for rnd in (2 * F, n):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(rnd):
+            rr, st = slots[i % F]
+            with torch.cuda.stream(st):
+                rr.frame()
+        torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / n * 1e6
+
+
+one["ms_per_step_us"] = round(one_gpu_throughput(int(arg("--frames-in-flight", "4"))), 1)
 overlap = float(arg("--overlap", "0") or 0) or None
 
 dist.get_backend = lambda pg=None: "gloo"  # plans only: no process group
@@ -162,6 +187,50 @@ for world in worlds:
         native.append((st.host_front_ns + st.host_back_ns - st.host_wait_ns) / st.frames * 1e-3)
         f.close()
         c.close()
+    # round 6: the throughput region (bench.py's ms_per_step at N > 1), per rank ALONE on this GPU --
+    # rank k's native band frame over the null communicator (its pass 1 rows, compaction, the trace of its share,
+    # pass 2 of its rows; no exchange), F frame slots on F streams with back() lagging F - 1 fronts as bench.py
+    # issues them; the slowest rank's time per frame bounds ms_per_step from below, and the exchange bytes over
+    # one xGMI link (overlapped with the other frames' compute) from the side
+    F = int(arg("--frames-in-flight", "4"))
+    slowest = max(range(world), key=lambda k: ranks[k]["gpu_us"])
+    thr = {}
+    for k in sorted({0, world // 2, slowest}):
+        c = NativeComm.null(k, world)
+        slots = []
+        for j in range(F):
+            rr = r.frame_slot()
+            st = torch.cuda.Stream()
+            st.wait_stream(torch.cuda.current_stream())
+            slots.append((rr, st, NativeHaloFrame(rr, c, throughput=True, rebalance=False, sd_split=sd_split)))
+        torch.cuda.synchronize()
+
+        def run(n):
+            pending = []
+            for i in range(n):
+                rr, st, f = slots[i % F]
+                with torch.cuda.stream(st):
+                    f.front()
+                pending.append(i)
+                if len(pending) > F - 1:
+                    j = pending.pop(0)
+                    with torch.cuda.stream(slots[j % F][1]):
+                        slots[j % F][2].back()
+            while pending:
+                j = pending.pop(0)
+                with torch.cuda.stream(slots[j % F][1]):
+                    slots[j % F][2].back()
+
+        run(2 * F)
+        torch.cuda.synchronize()
+        n = 60
+        t0 = time.perf_counter()
+        run(n)
+        torch.cuda.synchronize()
+        thr[k] = (time.perf_counter() - t0) / n * 1e6
+        for _, _, f in slots:
+            f.close()
+        c.close()
     r.invalidate_sd_tiles()
     gpu = max(x["gpu_us"] for x in ranks)
     xfer = max(x["bytes"] for x in ranks) / (link_gbs * 1e3)  # bytes / (GB/s) in us
@@ -172,6 +241,12 @@ for world in worlds:
         "host_issue_native_us_per_frame": round(max(native), 1),
         "predicted_latency_us": round(lat, 1),
         "predicted_speedup_latency": round((one["gpu_us"]) / lat, 2),
+        "rank_alone_us_per_frame_in_flight": {str(k): round(v, 1) for k, v in thr.items()},
+        "predicted_ms_per_step_us": round(max(max(thr.values()), xfer), 1),
+        "throughput_note": f"frames in flight (F = {F}): max(the slowest measured rank's time per frame alone on one "
+                           "GPU -- its band frame over the null communicator, bench.py's lag schedule --, the "
+                           "largest rank's exchange bytes / link bandwidth); collective latencies overlap the other "
+                           "frames in flight",
         "note": "latency = max-rank GPU time + 4 collective latencies + max-rank bytes / link bandwidth; with "
                 "frames in flight the frame interval is bounded below by the host issue (Python HaloFrame: "
                 "host_issue_us_per_frame; the native band frame bench.py runs: host_issue_native_us_per_frame)"}
