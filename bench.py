@@ -429,20 +429,31 @@ def run_rank(args, grp, local, shared=None):
     # drains the frames in flight); 1 rank: one rsd_svao_frame call per frame
     lag = F - 1 if shard == "band" and world > 1 else 0
 
+    # native band frames without a camera path: librsd's calls take each slot's stream explicitly, without a torch
+    # stream context per call (~6 us of host time each; at N >= 4 a rank's frame is host-bound)
+    raw = [st.cuda_stream for st in streams]
+    direct = native and lag and not poses
+
     def run_thr(n, timed_ev=thr_ev):
         pending = []
 
         def finish(j):
+            if direct:
+                slots[j % F].back(sd_events=ev_thr[j] if timed_ev else None, stream=raw[j % F])
+                return
             with torch.cuda.stream(streams[j % F]):
                 slots[j % F].back(sd_events=ev_thr[j] if timed_ev else None)
 
         for i in range(n):
-            with torch.cuda.stream(streams[i % F]):
-                pose(slots[i % F].b, i)
-                if lag:
-                    slots[i % F].front()
-                else:
-                    slots[i % F].frame(sd_events=ev_thr[i] if timed_ev else None)
+            if direct:
+                slots[i % F].front(stream=raw[i % F])
+            else:
+                with torch.cuda.stream(streams[i % F]):
+                    pose(slots[i % F].b, i)
+                    if lag:
+                        slots[i % F].front()
+                    else:
+                        slots[i % F].frame(sd_events=ev_thr[i] if timed_ev else None)
             if lag:
                 pending.append(i)
                 if len(pending) > lag:

@@ -1379,6 +1379,10 @@ __device__ __forceinline__ void sd_hit_terms(const SDArgs& a, const RayCtx& r, f
 // SPEC: the specialised fused walk of the common trace -- the Default reservoir with MaxCount <= K (a
 // commit by the K-th key, so no second chunk of keys) and no alpha-tested triangles: the lower-bound
 // (useLB) tests, the alpha test, the other implementations and the chunk continuation compile away.
+// (Round 6, not kept: deferring a row's leaves to a second pool stack and giving the WAVE separate node steps and
+// leaf steps -- every row then tests up to ROW deferred leaves at once -- so that node steps run the box tests alone
+// instead of the union of the box and triangle paths of a wave's mixed items.  Same bits, slower at every config:
+// configs[1] 67.5 -> 69.1 us, configs[2] 179 -> 223, configs[3] 197 -> 216 (profiles/round6/trace_ab/defer_*).)
 template <int K, int N, int ROW, bool SPLIT, bool CNT, int POOL = kPoolCap, bool SPEC = false>
 __device__ __forceinline__ void sd_trace_row_body(const SDArgs& a, const float4* __restrict__ queue,
                                                   uint32_t* __restrict__ qctl, uint2* __restrict__ keys,

@@ -931,21 +931,23 @@ class NativeHaloFrame:
         self._ev = (C.c_void_p * 2)()
         self._L = abi.lib()
 
-    def front(self):
+    def front(self, stream=None):
+        """stream: a raw HIP stream handle (default: torch's current stream of the renderer's device) -- a caller that
+        keeps one stream per frame slot passes it and saves the torch stream context per call (~6 us of host time)."""
         import ctypes as C
         b = self.b
-        st = self._L.rsd_band_frame_front(self.h, C.byref(b.cam), b.stream)
+        st = self._L.rsd_band_frame_front(self.h, C.byref(b.cam), b.stream if stream is None else stream)
         if st:
             from . import abi
             abi.check(st, "rsd_band_frame_front")
 
-    def back(self, sd_events=None):
+    def back(self, sd_events=None, stream=None):
         ev = None
         if sd_events:
             ev = self._ev
             ev[0] = sd_events[0].h.value if sd_events[0] is not None else None
             ev[1] = sd_events[1].h.value if sd_events[1] is not None else None
-        st = self._L.rsd_band_frame_back(self.h, ev, self.b.stream)
+        st = self._L.rsd_band_frame_back(self.h, ev, self.b.stream if stream is None else stream)
         if st:
             from . import abi
             abi.check(st, "rsd_band_frame_back")

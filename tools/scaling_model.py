@@ -205,21 +205,18 @@ for world in worlds:
             slots.append((rr, st, NativeHaloFrame(rr, c, throughput=True, rebalance=False, sd_split=sd_split)))
         torch.cuda.synchronize()
 
-        def run(n):
+        def run(n):  # bench.py's native N > 1 loop: explicit streams, no torch stream contexts
             pending = []
             for i in range(n):
                 rr, st, f = slots[i % F]
-                with torch.cuda.stream(st):
-                    f.front()
+                f.front(stream=st.cuda_stream)
                 pending.append(i)
                 if len(pending) > F - 1:
                     j = pending.pop(0)
-                    with torch.cuda.stream(slots[j % F][1]):
-                        slots[j % F][2].back()
+                    slots[j % F][2].back(stream=slots[j % F][1].cuda_stream)
             while pending:
                 j = pending.pop(0)
-                with torch.cuda.stream(slots[j % F][1]):
-                    slots[j % F][2].back()
+                slots[j % F][2].back(stream=slots[j % F][1].cuda_stream)
 
         run(2 * F)
         torch.cuda.synchronize()
