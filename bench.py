@@ -57,7 +57,7 @@ for p in (str(ROOT), str(PKG)):
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8 TB/s (spec)
 DEFAULT_CONFIG = "suntemple_1080p_q"
 # committed rocprofv3 passes of the default bench (newest round first)
-PROFILE_DIRS = [ROOT / "profiles" / "round5", ROOT / "profiles" / "round4", ROOT / "profiles" / "round3",
+PROFILE_DIRS = [ROOT / "profiles" / "round6", ROOT / "profiles" / "round5", ROOT / "profiles" / "round4", ROOT / "profiles" / "round3",
                 ROOT / "profiles" / "round2", ROOT / "profiles" / "round1"]
 
 

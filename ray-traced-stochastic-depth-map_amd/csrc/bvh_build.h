@@ -24,6 +24,8 @@ struct BvhStats {
     uint32_t leaves = 0;
     uint32_t max_depth = 0;   // binary SAH tree
     uint32_t wide_depth = 0;  // inner 4-wide nodes on the longest root-to-leaf path (the root counts 1)
+    uint32_t references = 0;  // triangle records (> triangle count with spatial splits)
+    uint32_t spatial_splits = 0;
     double sah_cost = 0.0;
     double build_ms = 0.0;
 };
@@ -38,8 +40,24 @@ constexpr uint32_t kBvhMaxDepth = 60;   // traversal stack is 64 entries
 constexpr uint32_t kBvhMaxLeaf = 4;
 constexpr uint32_t kBvhWidth = 4;
 
+// Spatial splits (SBVH, Stich et al. 2009): where the two boxes of the best object split overlap
+// by more than `split_alpha` of the root's area, a split of the node's box at a bin plane that
+// clips straddling triangles into both children is also priced; the cheaper one is taken.  A
+// triangle then has several references (leaves whose clipped boxes cover parts of it), each
+// with its own triangle record: the canonical any-hit stream is unchanged (a walk keeps each
+// (t, prim) key once), traversal-order streams need a tree without splits.  `split_budget`
+// bounds the extra references (fraction of the triangle count; 0 = no spatial split).
+// Clipped boxes are computed in double, rounded outward and padded by `split_pad` x the
+// scene's largest coordinate magnitude, so that a hit within the slab test's rounding of a
+// split plane lies in both children.
+struct BvhOptions {
+    double split_budget = 0.0;
+    double split_alpha = 1e-5;
+    double split_pad = 1.0 / 65536.0;
+};
+
 // positions: float3[nv]; indices: uint32[3*nt]; flags: uint32[nt] or nullptr
 FlatBvh build_bvh(const float* positions, uint32_t nv, const uint32_t* indices, uint32_t nt,
-                  const uint32_t* flags, unsigned threads);
+                  const uint32_t* flags, unsigned threads, const BvhOptions& opt = BvhOptions());
 
 }  // namespace rsd

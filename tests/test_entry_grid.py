@@ -25,10 +25,18 @@ def exe(tmp_path_factory):
     return out
 
 
-@pytest.mark.parametrize("tris,offset", [(20000, 0.0), (20000, 1000.0), (5000, -3000.0)])
-def test_entry_grid_covers_every_crossed_triangle(exe, tris, offset):
-    out = subprocess.run([str(exe), str(tris), "3000", str(offset)], capture_output=True, text=True, timeout=300)
+@pytest.mark.parametrize("tris,offset,splits", [(20000, 0.0, 0.0), (20000, 1000.0, 0.0), (5000, -3000.0, 0.0),
+                                                (20000, 0.0, 0.5), (5000, -3000.0, 0.5)])
+def test_entry_grid_covers_every_crossed_triangle(exe, tris, offset, splits):
+    """splits > 0: the spatial-split BVH (bvh_build.h BvhOptions; tools/sbvh_study.cpp): the
+    leaves' clipped, padded boxes still contain every crossing point of their triangle."""
+    out = subprocess.run([str(exe), str(tris), "3000", str(offset), str(splits)], capture_output=True, text=True,
+                         timeout=300)
     assert out.returncode == 0, out.stdout + out.stderr
     last = out.stdout.strip().splitlines()[-1]
     fields = dict(zip(last.split()[0::2], last.split()[1::2]))
     assert int(fields["violations"]) == 0 and int(fields["hits"]) > 1000, last
+    if splits:
+        head = out.stdout.strip().splitlines()[0].split()
+        info = dict(zip(head[0::2], head[1::2]))
+        assert int(info["spatial_splits"]) > 0 and int(info["references"]) > tris, head

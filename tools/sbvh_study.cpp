@@ -1,0 +1,273 @@
+// sbvh_study.cpp -- does a spatial-split BVH shorten the SD row walk's slowest chains?  (host only, no GPU)
+//
+// Builds librsd's BVH (csrc/bvh_build.cpp) with and without spatial splits plus its segment entry grid
+// (csrc/entry_grid.cpp), and replays the live SD ray segments of a frame (tools/sbvh_rays.py) through a
+// model of the row walk (sd_trace.hip sd_trace_row_kernel): the segment's entry frontier as the first pool,
+// then per step up to 8 items popped from the top of the ray's pool, every child box tested against
+// [TMin, min(TMax, k-th key)], the surviving children pushed nearest-on-top lane after lane, leaf hits
+// merged into the K nearest (t, prim) keys (each key once).  Reports the step / node / leaf counts whose
+// maximum sets the trace (DESIGN.md section 7 latency floor).
+//
+// build: g++ -O2 -std=c++17 -pthread -I ray-traced-stochastic-depth-map_amd/csrc tools/sbvh_study.cpp \
+//          ray-traced-stochastic-depth-map_amd/csrc/bvh_build.cpp ray-traced-stochastic-depth-map_amd/csrc/entry_grid.cpp
+// usage: sbvh_study pos.bin ind.bin rays.bin K budget [alpha] [lanes] [expand]
+//   lanes: items popped per step (the row width, 8); expand 1: an inner child the ray enters is replaced by its
+//   own children in the same step (a 16-wide node: what a wider tree could give at most)
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "bvh_build.h"
+#include "entry_grid.h"
+
+using namespace rsd;
+
+static std::vector<char> slurp(const char* p) {
+    FILE* f = std::fopen(p, "rb");
+    if (!f) { std::perror(p); std::exit(1); }
+    std::fseek(f, 0, SEEK_END);
+    const long n = std::ftell(f);
+    std::fseek(f, 0, SEEK_SET);
+    std::vector<char> b((size_t)n);
+    if (std::fread(b.data(), 1, (size_t)n, f) != (size_t)n) std::exit(1);
+    std::fclose(f);
+    return b;
+}
+
+static uint32_t fb(float f) { uint32_t u; std::memcpy(&u, &f, 4); return u; }
+
+struct Ray {
+    float o[3], d[3], tmin, tmax;
+    float invd[3], oinvd[3];
+    int kx, ky, kz;
+    float Sx, Sy, Sz;
+};
+
+static void setup(Ray& r) {
+    float ax = std::fabs(r.d[0]), ay = std::fabs(r.d[1]), az = std::fabs(r.d[2]);
+    int axis = 0;
+    if (ay > ax && ay > az) axis = 1;
+    if (az > ax && az > ay) axis = 2;
+    r.kz = axis;
+    r.kx = axis == 2 ? 0 : axis + 1;
+    r.ky = r.kx == 2 ? 0 : r.kx + 1;
+    if (r.d[r.kz] < 0.0f) std::swap(r.kx, r.ky);
+    r.Sx = r.d[r.kx] / r.d[r.kz];
+    r.Sy = r.d[r.ky] / r.d[r.kz];
+    r.Sz = 1.0f / r.d[r.kz];
+    for (int k = 0; k < 3; ++k) {
+        float v = std::fabs(r.d[k]) > 1e-20f ? r.d[k] : std::copysign(1e-20f, r.d[k]);
+        r.invd[k] = 1.0f / v;
+        r.oinvd[k] = r.o[k] * r.invd[k];
+    }
+}
+
+static bool box_hit(const Ray& r, const float lo[3], const float hi[3], float tlo, float thi, float& tn) {
+    float t0[3], t1[3];
+    for (int k = 0; k < 3; ++k) {
+        t0[k] = std::fma(lo[k], r.invd[k], -r.oinvd[k]);
+        t1[k] = std::fma(hi[k], r.invd[k], -r.oinvd[k]);
+    }
+    float n = std::max(std::max(std::min(t0[0], t1[0]), std::min(t0[1], t1[1])), std::min(t0[2], t1[2]));
+    float f = std::min(std::min(std::max(t0[0], t1[0]), std::max(t0[1], t1[1])), std::max(t0[2], t1[2]));
+    const float m = 1e-5f * (std::fabs(n) + std::fabs(f));
+    n -= m;
+    f += m;
+    tn = n;
+    return std::max(n, tlo) <= std::min(f, thi);
+}
+
+// watertight test (bvh_traverse.h intersect_tri), t only
+static bool tri_hit(const Ray& r, const float* a, const float* b, const float* c, float& t) {
+    float A[3], B[3], C[3];
+    for (int k = 0; k < 3; ++k) { A[k] = a[k] - r.o[k]; B[k] = b[k] - r.o[k]; C[k] = c[k] - r.o[k]; }
+    const float Ax = A[r.kx] - r.Sx * A[r.kz], Ay = A[r.ky] - r.Sy * A[r.kz];
+    const float Bx = B[r.kx] - r.Sx * B[r.kz], By = B[r.ky] - r.Sy * B[r.kz];
+    const float Cx = C[r.kx] - r.Sx * C[r.kz], Cy = C[r.ky] - r.Sy * C[r.kz];
+    float U = Cx * By - Cy * Bx, V = Ax * Cy - Ay * Cx, W = Bx * Ay - By * Ax;
+    if (U == 0.0f || V == 0.0f || W == 0.0f) {
+        U = (float)((double)Cx * By - (double)Cy * Bx);
+        V = (float)((double)Ax * Cy - (double)Ay * Cx);
+        W = (float)((double)Bx * Ay - (double)By * Ax);
+    }
+    if ((U < 0.0f || V < 0.0f || W < 0.0f) && (U > 0.0f || V > 0.0f || W > 0.0f)) return false;
+    const float det = U + V + W;
+    if (det == 0.0f) return false;
+    const float T = U * (r.Sz * A[r.kz]) + V * (r.Sz * B[r.kz]) + W * (r.Sz * C[r.kz]);
+    t = T * (1.0f / det);
+    return true;
+}
+
+struct Stats { int steps = 0, nodes = 0, leaves = 0, tris = 0, keys = 0; };
+
+int main(int argc, char** argv) {
+    if (argc < 6) { std::fprintf(stderr, "usage: %s pos.bin ind.bin rays.bin K budget [alpha]\n", argv[0]); return 2; }
+    auto pb = slurp(argv[1]), ib = slurp(argv[2]), rb = slurp(argv[3]);
+    const int K = std::atoi(argv[4]);
+    BvhOptions opt;
+    opt.split_budget = std::atof(argv[5]);
+    if (argc > 6) opt.split_alpha = std::atof(argv[6]);
+    const int lanes = argc > 7 ? std::atoi(argv[7]) : 8;
+    const int expand = argc > 8 ? std::atoi(argv[8]) : 0;
+    const float* pos = reinterpret_cast<const float*>(pb.data());
+    const uint32_t* ind = reinterpret_cast<const uint32_t*>(ib.data());
+    const uint32_t nv = (uint32_t)(pb.size() / 12), nt = (uint32_t)(ib.size() / 12);
+    const float* rays = reinterpret_cast<const float*>(rb.data());
+    const size_t nr = rb.size() / 32;
+    FlatBvh bvh = build_bvh(pos, nv, ind, nt, nullptr, 8, opt);
+    const uint32_t triOff = (uint32_t)(bvh.nodes.size() / 4);
+    EntryGrid g = build_entry_grid(bvh.nodes, triOff, 1ull << 21, 8);
+    std::vector<float> all(bvh.nodes);
+    all.insert(all.end(), bvh.tris.begin(), bvh.tris.end());
+    all.resize(all.size() + 48, 0.0f);
+    const float* base = all.data();
+    uint32_t bits = 0;
+    while ((4ull << bits) < g.slots.size()) ++bits;
+
+    std::vector<Stats> st(nr);
+    size_t walked = 0, culled = 0, rootStart = 0;
+    for (size_t i = 0; i < nr; ++i) {
+        Ray r;
+        for (int k = 0; k < 3; ++k) { r.o[k] = rays[8 * i + k]; r.d[k] = rays[8 * i + 3 + k]; }
+        r.tmin = rays[8 * i + 6];
+        r.tmax = rays[8 * i + 7];
+        setup(r);
+        // entry lookup (sd_trace.hip entry_lookup)
+        std::vector<uint32_t> pool;
+        {
+            const float pad = 0x1p-14f * (std::fabs(r.o[0]) + std::fabs(r.o[1]) + std::fabs(r.o[2]) + r.tmax) + 1e-30f;
+            float lo[3], hi[3];
+            for (int k = 0; k < 3; ++k) {
+                const float p0 = r.o[k] + r.d[k] * r.tmin, p1 = r.o[k] + r.d[k] * r.tmax;
+                lo[k] = std::min(p0, p1) - pad;
+                hi[k] = std::max(p0, p1) + pad;
+            }
+            const float m = std::max({hi[0] - lo[0], hi[1] - lo[1], hi[2] - lo[2]});
+            uint32_t ent = 0;  // root
+            bool dead = false;
+            if (m <= g.extent) {
+                int R = std::min((int)g.rmax, std::ilogb(g.extent / m));
+                while (R > 0 && m > std::ldexp(g.extent, -R)) --R;
+                const float sc = std::ldexp(1.0f, R) / g.extent;
+                const int ci = (int)std::floor((0.5f * (lo[0] + hi[0]) - g.origin[0]) * sc);
+                const int cj = (int)std::floor((0.5f * (lo[1] + hi[1]) - g.origin[1]) * sc);
+                const int ck = (int)std::floor((0.5f * (lo[2] + hi[2]) - g.origin[2]) * sc);
+                const uint64_t key = entry_key((uint32_t)R, ci, cj, ck);
+                uint32_t h = entry_hash(key, bits);
+                const uint32_t mask = (1u << bits) - 1u;
+                dead = true;
+                for (uint32_t n = 0; n <= g.max_probe; ++n, h = (h + 1) & mask) {
+                    const uint32_t* s = &g.slots[4 * (size_t)h];
+                    if (s[0] == (uint32_t)key && s[1] == (uint32_t)(key >> 32)) { ent = s[2]; dead = false; break; }
+                    if (s[0] == 0 && s[1] == 0) break;
+                }
+            }
+            if (dead) { ++culled; continue; }
+            if (ent == 0) { pool.push_back(0u); ++rootStart; }
+            else {
+                const uint32_t first = ent >> 4, n = ent & 15u;
+                std::vector<uint32_t> keep;
+                for (uint32_t e = 0; e < n; ++e) {
+                    const float* it = &g.items[8 * (size_t)(first + e)];
+                    float tn;
+                    if (box_hit(r, it + 1, it + 4, r.tmin, r.tmax, tn)) keep.push_back(fb(it[0]));
+                }
+                if (keep.empty()) { ++culled; continue; }
+                // the walk's lanes take the items in order: the pool's top is the first item
+                for (size_t e = keep.size(); e-- > 0;) pool.push_back(keep[e]);
+            }
+        }
+        ++walked;
+        std::vector<float> kt(K, INFINITY);
+        std::vector<uint32_t> kp(K, 0xffffffffu);
+        Stats& s = st[i];
+        while (!pool.empty()) {
+            ++s.steps;
+            const float thi = std::min(r.tmax, kt[K - 1]);
+            std::vector<uint32_t> step;
+            for (int l = 0; l < lanes && !pool.empty(); ++l) { step.push_back(pool.back()); pool.pop_back(); }
+            std::vector<std::pair<float, uint32_t>> hits;
+            std::vector<std::vector<std::pair<float, uint32_t>>> kids(step.size());
+            for (size_t l = 0; l < step.size(); ++l) {
+                const uint32_t item = step[l];
+                const float* p = base + 4 * (size_t)(item & 0x1fffffffu);
+                if (item & 0x80000000u) {
+                    ++s.leaves;
+                    const uint32_t cnt = ((item >> 29) & 3u) + 1u;
+                    for (uint32_t j = 0; j < cnt; ++j) {
+                        ++s.tris;
+                        const float* q = p + 12 * j;
+                        float t;
+                        if (tri_hit(r, q, q + 4, q + 8, t) && t >= r.tmin && t <= r.tmax) hits.push_back({t, fb(q[3])});
+                    }
+                } else {
+                    ++s.nodes;
+                    for (int j = 0; j < 4; ++j) {
+                        const uint32_t ref = fb(p[24 + j]), cnt = fb(p[28 + j]);
+                        if (ref == 0xffffffffu) continue;
+                        const float lo[3] = {p[0 + j], p[8 + j], p[16 + j]}, hi[3] = {p[4 + j], p[12 + j], p[20 + j]};
+                        float tn;
+                        if (!box_hit(r, lo, hi, r.tmin, thi, tn)) continue;
+                        const uint32_t code = cnt ? (0x80000000u | ((cnt - 1u) << 29) | (triOff + 3u * ref)) : 8u * ref;
+                        if (expand && !cnt) {  // open the inner child in the same step
+                            const float* c = base + 4 * (size_t)code;
+                            for (int jj = 0; jj < 4; ++jj) {
+                                const uint32_t ref2 = fb(c[24 + jj]), cnt2 = fb(c[28 + jj]);
+                                if (ref2 == 0xffffffffu) continue;
+                                const float lo2[3] = {c[0 + jj], c[8 + jj], c[16 + jj]}, hi2[3] = {c[4 + jj], c[12 + jj], c[20 + jj]};
+                                float tn2;
+                                if (!box_hit(r, lo2, hi2, r.tmin, thi, tn2)) continue;
+                                kids[l].push_back({tn2, cnt2 ? (0x80000000u | ((cnt2 - 1u) << 29) | (triOff + 3u * ref2)) : 8u * ref2});
+                            }
+                            continue;
+                        }
+                        kids[l].push_back({tn, code});
+                    }
+                    std::sort(kids[l].begin(), kids[l].end());
+                }
+            }
+            for (auto& h : hits) {  // insert, each (t, prim) key once
+                bool dup = false;
+                for (int j = 0; j < K; ++j) dup |= kt[j] == h.first && kp[j] == h.second;
+                if (dup) continue;
+                int j = K - 1;
+                if (!(h.first < kt[j] || (h.first == kt[j] && h.second < kp[j]))) continue;
+                while (j > 0 && (h.first < kt[j - 1] || (h.first == kt[j - 1] && h.second < kp[j - 1]))) {
+                    kt[j] = kt[j - 1]; kp[j] = kp[j - 1]; --j;
+                }
+                kt[j] = h.first; kp[j] = h.second;
+            }
+            const float thi2 = std::min(r.tmax, kt[K - 1]);
+            for (size_t l = step.size(); l-- > 0;)  // lane after lane, the first lane's nearest child on top
+                for (size_t c = kids[l].size(); c-- > 0;)
+                    if (kids[l][c].first <= thi2) pool.push_back(kids[l][c].second);
+        }
+        for (int j = 0; j < K; ++j) s.keys += kt[j] < INFINITY;
+    }
+    std::vector<int> steps;
+    double sn = 0, sl = 0, stt = 0, ss = 0;
+    for (size_t i = 0; i < nr; ++i)
+        if (st[i].steps) { steps.push_back(st[i].steps); sn += st[i].nodes; sl += st[i].leaves; stt += st[i].tris; ss += st[i].steps; }
+    std::sort(steps.begin(), steps.end());
+    auto pct = [&](double q) { return steps.empty() ? 0 : steps[std::min(steps.size() - 1, (size_t)(q * steps.size()))]; };
+    // the top 1 % of the rays by steps
+    std::vector<size_t> idx;
+    for (size_t i = 0; i < nr; ++i) if (st[i].steps) idx.push_back(i);
+    std::sort(idx.begin(), idx.end(), [&](size_t a, size_t b) { return st[a].steps > st[b].steps; });
+    const size_t top = std::max<size_t>(1, idx.size() / 100);
+    double tn = 0, tl = 0, ts = 0;
+    for (size_t q = 0; q < top; ++q) { tn += st[idx[q]].nodes; tl += st[idx[q]].leaves; ts += st[idx[q]].steps; }
+    std::printf("{\"lanes\": %d, \"expand\": %d, \"budget\": %.3f, \"alpha\": %g, \"tris\": %u, \"references\": %u, \"spatial_splits\": %u, "
+                "\"wide_nodes\": %zu, \"wide_depth\": %u, \"build_ms\": %.0f, \"entry_cells\": %u, \"rays\": %zu, "
+                "\"walked\": %zu, \"culled\": %zu, \"root_start\": %zu, \"steps_mean\": %.3f, \"steps_p99\": %d, "
+                "\"steps_p999\": %d, \"steps_max\": %d, \"nodes_mean\": %.3f, \"leaves_mean\": %.3f, \"tris_mean\": %.3f, "
+                "\"top1pct\": {\"steps\": %.2f, \"nodes\": %.2f, \"leaves\": %.2f}}\n",
+                lanes, expand, opt.split_budget, opt.split_alpha, nt, bvh.stats.references, bvh.stats.spatial_splits,
+                bvh.nodes.size() / 32, bvh.stats.wide_depth, bvh.stats.build_ms, g.cells, nr, walked, culled, rootStart,
+                ss / walked, pct(0.99), pct(0.999), steps.empty() ? 0 : steps.back(), sn / walked, sl / walked,
+                stt / walked, ts / top, tn / top, tl / top);
+    return 0;
+}
