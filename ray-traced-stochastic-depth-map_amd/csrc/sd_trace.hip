@@ -100,6 +100,7 @@ struct SDArgs {
     uint32_t quadStack;  // entries of each ray's LDS stack in the quad walks (quad_stack_entries)
     uint32_t qrange;     // diagnostics (RSD_TRACE_QRANGE): 0 every ray, 1 the longest-first rays only, 2 the others
     uint32_t hybridRowBlocks;  // hybrid walk: its first blocks run the row walk (sd_trace_hybrid_kernel)
+    uint32_t rowPrio;          // hybrid walk: issue priority of the row blocks' waves (s_setprio; A/B, RSD_TRACE_ROWPRIO)
     // clean tiles (rsd_sd_params.d_tile_state): per 8x8 tile, tileSig when the last trace left every texel it
     // wrote at DEFAULT_DEPTH (0: unknown); such a tile without a live ray is not rewritten
     uint32_t* tileState;
@@ -1320,6 +1321,32 @@ __device__ __forceinline__ void row_insert(float& kt, uint32_t& kp, float& ku, f
     }
 }
 
+// two keys per lane (K = 2 ROW, the specialised walk at K = 16 on 8-lane rows): lane l holds keys 2l (slot 0) and
+// 2l + 1 (slot 1) of the sorted list; the insert counts the keys below the new one in both slots and shifts every key
+// at or above that position by one (slot 1 <- own slot 0, slot 0 <- the previous lane's slot 1)
+template <int ROW>
+__device__ __forceinline__ void row_insert2(float& kt0, uint32_t& kp0, float& ku0, float& kv0, float& kt1, uint32_t& kp1,
+                                            float& ku1, float& kv1, float nt, uint32_t np, float nu, float nv, int l,
+                                            int base) {
+    const int pos = __popc(row_bits<ROW>(key_less(kt0, kp0, nt, np), base)) +
+                    __popc(row_bits<ROW>(key_less(kt1, kp1, nt, np), base));
+    const float st = __uint_as_float(row_prev<ROW>(__float_as_uint(kt1), l, base));
+    const uint32_t sp = row_prev<ROW>(kp1, l, base);
+    const float su = __uint_as_float(row_prev<ROW>(__float_as_uint(ku1), l, base));
+    const float sv = __uint_as_float(row_prev<ROW>(__float_as_uint(kv1), l, base));
+    const int i0 = 2 * l, i1 = 2 * l + 1;
+    if (i1 == pos) {
+        kt1 = nt; kp1 = np; ku1 = nu; kv1 = nv;
+    } else if (i1 > pos) {
+        kt1 = kt0; kp1 = kp0; ku1 = ku0; kv1 = kv0;
+    }
+    if (i0 == pos) {
+        kt0 = nt; kp0 = np; ku0 = nu; kv0 = nv;
+    } else if (i0 > pos) {
+        kt0 = st; kp0 = sp; ku0 = su; kv0 = sv;
+    }
+}
+
 // exclusive prefix sum (and total) of v in [0, 7] over the lanes of a row
 template <int ROW>
 __device__ __forceinline__ int row_prefix(int v, int l, int base, int& total) {
@@ -1351,6 +1378,22 @@ __device__ __forceinline__ bool sd_algorithm_row(const SDArgs& a, float rng, flo
         if (commit || j >= found) continue;
         delivered++;
         commit = sd_any_hit_impl<N, IMPL>(a, rj, zj, af, depths, cnt);
+    }
+    return commit;
+}
+
+// the same with two keys per lane (row_insert2's layout: key j in lane j / 2, slot j % 2), no alpha-tested keys
+template <int K, int N, int IMPL = -1>
+__device__ __forceinline__ bool sd_algorithm_row2(const SDArgs& a, float rng0, float z0, float rng1, float z1, int found,
+                                                  int base, float (&depths)[N], uint32_t& cnt, uint32_t& delivered) {
+    bool commit = false;
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+        const float rj = __shfl((j & 1) ? rng1 : rng0, base + j / 2);
+        const float zj = __shfl((j & 1) ? z1 : z0, base + j / 2);
+        if (commit || j >= found) continue;
+        delivered++;
+        commit = sd_any_hit_impl<N, IMPL>(a, rj, zj, false, depths, cnt);
     }
     return commit;
 }
@@ -1388,7 +1431,10 @@ __device__ __forceinline__ void sd_trace_row_body(const SDArgs& a, const float4*
                                                   uint32_t* __restrict__ qctl, uint2* __restrict__ keys,
                                                   uint32_t* sItem, float* sT, uint32_t bid, uint32_t nb, uint32_t qr) {
     // sItem / sT: the rows' LDS pools (kBlock / ROW x POOL entries each); (bid, nb, qr) as sd_trace_queue_body's
-    static_assert(K <= ROW, "one key per lane");
+    // one key per lane, or (the specialised fused walk, K = 16 on 8-lane rows) two: row_insert2
+    static_assert(K <= ROW || (K == 2 * ROW && SPEC && !SPLIT), "one key per lane, or two in the specialised walk");
+    constexpr int KPL = K <= ROW ? 1 : 2;
+    constexpr int kKthLane = (K - 1) / KPL;  // the lane holding key K - 1 (slot KPL - 1)
     static_assert(kEntryCap <= (uint32_t)ROW, "entry items start one per lane");
     constexpr int kRow = ROW, kRowRays = kBlock / ROW;
     const int lane = threadIdx.x;
@@ -1424,6 +1470,8 @@ __device__ __forceinline__ void sd_trace_row_body(const SDArgs& a, const float4*
     float kt = INFINITY;  // per lane: key l of the row's sorted k-list
     uint32_t kp = kNoItem;
     float ku = 0.0f, kv = 0.0f;  // per lane: key l's barycentrics (fused walk: the hit terms' inputs)
+    float kt2 = INFINITY, ku2 = 0.0f, kv2 = 0.0f;  // KPL = 2: lane l holds keys 2l (kt ...) and 2l + 1 (kt2 ...)
+    uint32_t kp2 = kNoItem;
     // ---- statistics (counters build)
     TraceStats st{0u, 0u, 0u};
     uint32_t active = 0, hitsDelivered = 0, maxSteps = 0, raySteps = 0, maxNodes = 0, rayNodes = 0, rayLeaves = 0;
@@ -1475,6 +1523,7 @@ __device__ __forceinline__ void sd_trace_row_body(const SDArgs& a, const float4*
                 // the root node, or the segment's entry-grid frontier (one item per lane)
                 item = nEnt ? ((uint32_t)l < nEnt ? e : kNoItem) : (l == 0 ? 0u : kNoItem);
                 kt = INFINITY; kp = kNoItem; ku = kv = 0.0f;
+                kt2 = INFINITY; kp2 = kNoItem; ku2 = kv2 = 0.0f;
                 phase = kTrace;
                 if constexpr (CNT) {
                     active += l == 0;
@@ -1494,8 +1543,8 @@ __device__ __forceinline__ void sd_trace_row_body(const SDArgs& a, const float4*
         // ---- one traversal step of this row
         if constexpr (SPEC) useLB = false;
         const float tlo = useLB ? fmaxf(TMin, lbT) : TMin;
-        float kthT = row_bcastf<ROW, K - 1>(kt, l, base);
-        uint32_t kthP = row_bcast<ROW, K - 1>(kp, l, base);
+        float kthT = row_bcastf<ROW, kKthLane>(KPL == 2 ? kt2 : kt, l, base);
+        uint32_t kthP = row_bcast<ROW, kKthLane>(KPL == 2 ? kp2 : kp, l, base);
         float thi = fminf(TMax, kthT);
         float ck[4];
         uint32_t ci[4];
@@ -1590,9 +1639,10 @@ __device__ __forceinline__ void sd_trace_row_body(const SDArgs& a, const float4*
                     }
                     if (key_less(bt, bp, kthT, kthP)) {
                         if constexpr (SPLIT) row_insert<ROW>(kt, kp, bt, bp, l, base);
+                        else if constexpr (KPL == 2) row_insert2<ROW>(kt, kp, ku, kv, kt2, kp2, ku2, kv2, bt, bp, nu, nv, l, base);
                         else row_insert<ROW>(kt, kp, ku, kv, bt, bp, nu, nv, l, base);
-                        kthT = row_bcastf<ROW, K - 1>(kt, l, base);
-                        kthP = row_bcast<ROW, K - 1>(kp, l, base);
+                        kthT = row_bcastf<ROW, kKthLane>(KPL == 2 ? kt2 : kt, l, base);
+                        kthP = row_bcast<ROW, kKthLane>(KPL == 2 ? kp2 : kp, l, base);
                     }
                 }
             }
@@ -1670,11 +1720,31 @@ __device__ __forceinline__ void sd_trace_row_body(const SDArgs& a, const float4*
         }
         // TraceRay + anyHit -> algorithm (Common.slangh:102-254) over the found keys, in
         // ascending (t, prim) order; lane j prepares key j
-        const int found = min(K, __popc(row_bits<ROW>(kp != kNoItem, base)));
+        const int found = min(K, __popc(row_bits<ROW>(kp != kNoItem, base)) +
+                                     (KPL == 2 ? __popc(row_bits<ROW>(kp2 != kNoItem, base)) : 0));
         // lane j: key j's terms from the (t, barycentrics) its leaf test found -- sd_hit_terms'
         // values bit for bit; the alpha test (alpha scenes only) re-reads the triangle
         float rng = 0.0f, z = 0.0f;
         bool af = false;
+        uint32_t delivered = 0;
+        if constexpr (KPL == 2) {  // lane l: keys 2l and 2l + 1 (no alpha test: SPEC)
+            float rng2 = 0.0f, z2 = 0.0f;
+            if (2 * l < found) {
+                rng = sd_hash(ku, kv);
+                z = kt * cosT;
+                if (a.normalize) z = saturate((z - a.cam.nearZ) / (a.cam.farZ - a.cam.nearZ));
+            }
+            if (2 * l + 1 < found) {
+                rng2 = sd_hash(ku2, kv2);
+                z2 = kt2 * cosT;
+                if (a.normalize) z2 = saturate((z2 - a.cam.nearZ) / (a.cam.farZ - a.cam.nearZ));
+            }
+            sd_algorithm_row2<K, N, 0>(a, rng, z, rng2, z2, found, base, depths, cnt, delivered);
+            if (l == 0) hitsDelivered += delivered;
+            if (l == 0) sd_store<N>(a, x, y, depths);
+            phase = kFetch;
+            continue;
+        }
         if (l < found) {
             if (!SPEC && a.alphaTest) {
                 sd_hit_terms(a, r, cosT, a.primRec[kp], rng, z, af);
@@ -1684,7 +1754,6 @@ __device__ __forceinline__ void sd_trace_row_body(const SDArgs& a, const float4*
                 if (a.normalize) z = saturate((z - a.cam.nearZ) / (a.cam.farZ - a.cam.nearZ));
             }
         }
-        uint32_t delivered = 0;
         const bool commit = sd_algorithm_row<K, N, SPEC ? 0 : -1>(a, rng, z, af, found, base, depths, cnt, delivered);
         if (l == 0) hitsDelivered += delivered;
         if (CNT && l == 0) tResolve += __builtin_amdgcn_s_memtime() - tS1;
@@ -1774,6 +1843,7 @@ __global__ void __launch_bounds__(kBlock) sd_trace_hybrid_kernel(SDArgs a, const
                                                                  uint32_t* __restrict__ qctl, uint2* __restrict__ keys) {
     extern __shared__ uint32_t sDyn[];
     const uint32_t rb = a.hybridRowBlocks;
+    if (blockIdx.x < rb && a.rowPrio) __builtin_amdgcn_s_setprio(2);  // (neutral at configs[1]-[3]: trace_ab/prio_*)
     if (blockIdx.x < rb)
         sd_trace_row_body<K, N, ROW, false, false, POOL, true>(
             a, queue, qctl, keys, sDyn, reinterpret_cast<float*>(sDyn + (kBlock / ROW) * POOL), blockIdx.x, rb, 1u);
@@ -2142,9 +2212,10 @@ static hipError_t launch_sd_kn(const SDArgs& a, dim3 grid, uint32_t persistentBl
     } else if (walk == 5) {
         hipLaunchKernelGGL((sd_trace_wavefront_kernel<N>), pg, wb, 0, s, a, queue, qctl);
     } else if (walk == 6) {
-        const size_t rowLds = (size_t)(kBlock / ROW) * pool * 8u, lds = std::max(rowLds, quad_stack_bytes(a));
-        if (pool == 128) hipLaunchKernelGGL((sd_trace_hybrid_kernel<K, N, ROW, 128>), pg, wb, lds, s, a, queue, qctl, keys);
-        else hipLaunchKernelGGL((sd_trace_hybrid_kernel<K, N, ROW, kPoolCap>), pg, wb, lds, s, a, queue, qctl, keys);
+        // 8-lane rows at every K (K = 16: two keys per lane, row_insert2)
+        const size_t rowLds = (size_t)(kBlock / 8) * pool * 8u, lds = std::max(rowLds, quad_stack_bytes(a));
+        if (pool == 128) hipLaunchKernelGGL((sd_trace_hybrid_kernel<K, N, 8, 128>), pg, wb, lds, s, a, queue, qctl, keys);
+        else hipLaunchKernelGGL((sd_trace_hybrid_kernel<K, N, 8, kPoolCap>), pg, wb, lds, s, a, queue, qctl, keys);
     } else if (walk == 4) {
         hipLaunchKernelGGL((sd_raster_kernel<K>), dim3((a.nTris + kRasterBlock - 1) / kRasterBlock), dim3(kRasterBlock),
                            0, s, a, queue, qctl);
@@ -2336,7 +2407,7 @@ rsd_status sd_trace_impl(rsd_scene* scene, const rsd_camera* cam, const rsd_sd_p
         if (counters) { *counters = rsd_counters{}; counters->rays_dispatched = (uint64_t)sd_w * sd_h; }
         return RSD_OK;
     }
-    SDArgs a;
+    SDArgs a{};
     a.nodes = scene->d_nodes;
     a.tris = scene->d_tris;
     a.triOff = scene->tri_offset;
@@ -2620,7 +2691,14 @@ rsd_status sd_trace_impl(rsd_scene* scene, const rsd_camera* cam, const rsd_sd_p
     // profiles/round5/hybrid/in_flight/).  RSD_TRACE_HYBRID=off disables it, =all takes it for every walk;
     // RSD_TRACE_HYBRID_ROWWPC / RSD_TRACE_WAVES_PER_CU set the row / quad blocks per CU (A/B runs).
     const char* hyEnv = std::getenv("RSD_TRACE_HYBRID");
-    const bool hybridOk = (walk == 0 || walk == 1) && K <= 8 && a.lpt && a.poolSoft >= 16 &&
+    // K = 16 (round 6, RSD_TRACE_HYBRID16=on; off by default): the row blocks walk 8-lane rows holding two keys per lane
+    // (row_insert2).  Same bits, but slower at configs[4]: 555 -> 688 us static, 0.987 -> 1.597 ms along the orbit
+    // (profiles/round6/hybrid16/).  Its long rays are many (the quad walk over them alone takes 411 of its 547 us: the
+    // set is throughput-bound, where 8 lanes per ray lose to 4), and one launch gives every block the row walk's 191
+    // VGPRs: 8 waves per CU instead of the quad walk's 16 (the quad walk alone at 4 per CU: 972 us).
+    const char* hy16Env = std::getenv("RSD_TRACE_HYBRID16");
+    const bool hybridK = K <= 8 || (hy16Env && std::string(hy16Env) == "on");
+    const bool hybridOk = (walk == 0 || walk == 1) && hybridK && a.lpt && a.poolSoft >= 16 &&
                           (!throughput || walk == 1 || (hyEnv && std::string(hyEnv) == "all")) &&
                           !(hyEnv && std::string(hyEnv) == "off") && !a.alphaTest && a.impl != 1u && a.impl != 3u &&
                           a.maxCount <= (uint32_t)K && !(specEnvOff());
@@ -2629,6 +2707,8 @@ rsd_status sd_trace_impl(rsd_scene* scene, const rsd_camera* cam, const rsd_sd_p
         const uint32_t rw = rwEnv ? (uint32_t)std::max(1, std::atoi(rwEnv)) : 4u, qw = wpcEnv ? wavesPerCu : 8u;
         const uint32_t cus = (uint32_t)std::max(1, scene->dev->cu_count);
         a.hybridRowBlocks = (cus * rw + kQueueParts - 1) / kQueueParts * kQueueParts;
+        const char* prEnv = std::getenv("RSD_TRACE_ROWPRIO");
+        a.rowPrio = prEnv && std::string(prEnv) == "on" ? 1u : 0u;
         pb = a.hybridRowBlocks + (cus * qw + kQueueParts - 1) / kQueueParts * kQueueParts;
         walk = 6;
     }

@@ -10,9 +10,10 @@
 //
 // build: g++ -O2 -std=c++17 -pthread -I ray-traced-stochastic-depth-map_amd/csrc tools/sbvh_study.cpp \
 //          ray-traced-stochastic-depth-map_amd/csrc/bvh_build.cpp ray-traced-stochastic-depth-map_amd/csrc/entry_grid.cpp
-// usage: sbvh_study pos.bin ind.bin rays.bin K budget [alpha] [lanes] [expand]
+// usage: sbvh_study pos.bin ind.bin rays.bin K budget [alpha] [lanes] [expand] [steps_out.bin]
 //   lanes: items popped per step (the row width, 8); expand 1: an inner child the ray enters is replaced by its
-//   own children in the same step (a 16-wide node: what a wider tree could give at most)
+//   own children in the same step (a 16-wide node: what a wider tree could give at most); expand 2: only as many inner
+//   children are opened as the row has spare lanes this step (a block layout, see below)
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
@@ -191,6 +192,16 @@ int main(int argc, char** argv) {
             for (int l = 0; l < lanes && !pool.empty(); ++l) { step.push_back(pool.back()); pool.pop_back(); }
             std::vector<std::pair<float, uint32_t>> hits;
             std::vector<std::vector<std::pair<float, uint32_t>>> kids(step.size());
+            // expand 2: the row's spare lanes (lanes - popped items) fetch the k-th INNER child of a popped inner node
+            // in the same step (assigned round robin: inner child 0 of every popped item, then 1, ...); such a child is
+            // opened when its box is hit (a block layout: a node's record followed by its inner children's records)
+            std::vector<int> spare(step.size(), 0);
+            if (expand == 2) {
+                int free = lanes - (int)step.size();
+                for (int k = 0; k < 4 && free > 0; ++k)
+                    for (size_t l = 0; l < step.size() && free > 0; ++l)
+                        if (!(step[l] & 0x80000000u)) { spare[l]++; --free; }
+            }
             for (size_t l = 0; l < step.size(); ++l) {
                 const uint32_t item = step[l];
                 const float* p = base + 4 * (size_t)(item & 0x1fffffffu);
@@ -205,14 +216,16 @@ int main(int argc, char** argv) {
                     }
                 } else {
                     ++s.nodes;
+                    int innerSeen = 0;
                     for (int j = 0; j < 4; ++j) {
                         const uint32_t ref = fb(p[24 + j]), cnt = fb(p[28 + j]);
                         if (ref == 0xffffffffu) continue;
                         const float lo[3] = {p[0 + j], p[8 + j], p[16 + j]}, hi[3] = {p[4 + j], p[12 + j], p[20 + j]};
                         float tn;
+                        const int innerIdx = cnt ? -1 : innerSeen++;
                         if (!box_hit(r, lo, hi, r.tmin, thi, tn)) continue;
                         const uint32_t code = cnt ? (0x80000000u | ((cnt - 1u) << 29) | (triOff + 3u * ref)) : 8u * ref;
-                        if (expand && !cnt) {  // open the inner child in the same step
+                        if ((expand == 1 && !cnt) || (expand == 2 && !cnt && innerIdx < spare[l])) {  // open it now
                             const float* c = base + 4 * (size_t)code;
                             for (int jj = 0; jj < 4; ++jj) {
                                 const uint32_t ref2 = fb(c[24 + jj]), cnt2 = fb(c[28 + jj]);
@@ -246,6 +259,11 @@ int main(int argc, char** argv) {
                     if (kids[l][c].first <= thi2) pool.push_back(kids[l][c].second);
         }
         for (int j = 0; j < K; ++j) s.keys += kt[j] < INFINITY;
+    }
+    if (argc > 9) {  // per-ray steps (int32 each, 0 = culled in setup)
+        FILE* f = std::fopen(argv[9], "wb");
+        for (size_t i = 0; i < nr; ++i) std::fwrite(&st[i].steps, 4, 1, f);
+        std::fclose(f);
     }
     std::vector<int> steps;
     double sn = 0, sl = 0, stt = 0, ss = 0;

@@ -1,4 +1,5 @@
-"""Time one rsd_sd_trace of a BASELINE config (diagnostics; env vars select the walk)."""
+"""Time one rsd_sd_trace of a BASELINE config (diagnostics; env vars select the walk).
+usage: python tools/sd_time.py [config] [--clean-tiles]"""
 import sys
 from pathlib import Path
 ROOT = Path(__file__).resolve().parents[1]
@@ -7,9 +8,11 @@ import torch
 from rsd.frame import CONFIGS, FrameConfig, Renderer
 from rsd.scenes import make_scene
 
-name = sys.argv[1] if len(sys.argv) > 1 else "suntemple_1080p_q"
+name = next((a for a in sys.argv[1:] if not a.startswith("--")), "suntemple_1080p_q")
 kw, sc = CONFIGS[name]
 r = Renderer(make_scene(sc), FrameConfig(**kw))
+if "--clean-tiles" in sys.argv:  # the bench's SD maps (Renderer.keep_clean_tiles)
+    r.keep_clean_tiles()
 r.gbuffer()
 r.clear_intervals()
 r.pass1()

@@ -14,7 +14,8 @@ path = next(Path(sys.argv[1]).rglob("*kernel_trace.csv"))
 rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
 ks = [(r["Kernel_Name"], int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in rows]
 setup = [(s, e) for n, s, e in ks if "sd_setup_kernel" in n]
-walk = [(n, s, e) for n, s, e in ks if "sd_trace_row_kernel" in n or "sd_trace_queue_kernel" in n]
+walk = [(n, s, e) for n, s, e in ks if "sd_trace_row_kernel" in n or "sd_trace_queue_kernel" in n or
+        "sd_trace_hybrid_kernel" in n]
 pairs = []
 for s0, e0 in setup:
     nxt = next(((n, s, e) for n, s, e in walk if s >= e0), None)
