@@ -573,7 +573,8 @@ def run_rank(args, grp, local, shared=None):
                    "stoch_map_divisor": cfg.divisor, "camera_path": path_name,
                    "parallelism": {"band": f"screen-band+halo x{world}", "gather": f"screen-band+allgather x{world}",
                                    "frame": f"frame-parallel x{world}"}[shard],
-                   "frame_impl": ("native (rsd_band_frame, librsd RCCL communicators)" if native else
+                   "frame_impl": (("native (rsd_band_frame, librsd in-process communicator)" if args.local_ranks > 1
+                                   else "native (rsd_band_frame, librsd RCCL communicators)") if native else
                                   "python (rsd/shard.py)") if shard == "band" and world > 1 else "rsd_svao_frame",
                    "frames_in_flight": F},
         "value_definition": "dispatched SD rays / SD-kernel time (HIP events around every rsd_sd_trace of the "
