@@ -40,11 +40,15 @@ namespace rsd {
 // ------------------------------------------------------------------------------------
 // queue-control words of one trace: {count[32], head[32]} of the live-ray queue partitions, the
 // raster walk's live-tile count, spare
-constexpr int kQctlWords = 4 * (int)kQueueParts + 32;
+constexpr int kQctlWords = 5 * (int)kQueueParts + 32;
+constexpr int kQctlTouch = 4 * (int)kQueueParts + 32;  // two-pass setup: touched texels listed per partition
 constexpr int kQctlHead2 = 3 * (int)kQueueParts + 32;  // hybrid walk: the row walk's own dequeue heads
 constexpr int kQctlLiveTiles = 2 * (int)kQueueParts;
 constexpr int kQctlShort = 2 * (int)kQueueParts + 32;  // lpt: short-ray counts (filled from the partition's end)
-constexpr int kSetupWaves = 4;  // sd_setup_kernel: tiles (waves) per workgroup
+#ifndef RSD_SETUP_WAVES
+#define RSD_SETUP_WAVES 4
+#endif
+constexpr int kSetupWaves = RSD_SETUP_WAVES;  // sd_setup_kernel: tiles (waves) per workgroup (A/B: RSD_SETUP_WAVES)
 struct SDArgs {
     const float4* nodes;  // BVH base (wide nodes, then triangle records)
     const float4* tris;   // = nodes + triOff
@@ -100,6 +104,11 @@ struct SDArgs {
     uint32_t quadStack;  // entries of each ray's LDS stack in the quad walks (quad_stack_entries)
     uint32_t qrange;     // diagnostics (RSD_TRACE_QRANGE): 0 every ray, 1 the longest-first rays only, 2 the others
     uint32_t hybridRowBlocks;  // hybrid walk: its first blocks run the row walk (sd_trace_hybrid_kernel)
+    // two-pass setup (the full-resolution maps): sd_classify_kernel lists the texels pass 1 touched, partition p at
+    // touchList[p * touchCap ..), and sd_live_kernel evaluates only those
+    uint32_t* touchList;
+    uint32_t touchCap;
+    uint32_t liveBlocks;  // sd_live_kernel's grid (a multiple of kQueueParts)
     uint32_t rowPrio;          // hybrid walk: issue priority of the row blocks' waves (s_setprio; A/B, RSD_TRACE_ROWPRIO)
     // clean tiles (rsd_sd_params.d_tile_state): per 8x8 tile, tileSig when the last trace left every texel it
     // wrote at DEFAULT_DEPTH (0: unknown); such a tile without a live ray is not rewritten
@@ -648,6 +657,97 @@ __device__ __forceinline__ void ray_rec_load(const float4* __restrict__ q, uint3
     ray_rec_load(q, slot, d, TMin, TMax, cosT, texel, nEnt);
 }
 
+// The frontier of a live ray's segment (entry_grid.h) and the items whose boxes the ray passes (the walk's own child
+// test); false: the segment can hit nothing (a culled ray: DEFAULT_DEPTH, no walk).  keep = 0 with true: from the root.
+// B: frontier items loaded (and tested) per round trip -- kEntryCap (all at once: the one-pass setup, latency-bound),
+// or kEntryCap / 2 (sd_live_kernel: half the box registers, more waves resident; the second batch only for a segment
+// with more items)
+template <uint32_t B = kEntryCap>
+__device__ __forceinline__ bool entry_frontier(const SDArgs& a, f3 d, float TMin, float TMax, uint32_t& keep,
+                                               uint32_t (&code)[kEntryCap]) {
+    const f3 o = mk(a.cam.posW[0], a.cam.posW[1], a.cam.posW[2]);
+    uint32_t ent = entry_lookup(a, o, d, TMin, TMax);
+    if (a.counters) {  // roofline bytes of the lookup (rsd_counters.entry_*)
+        atomicAdd(&a.counters[19], 1ull);
+        if (ent != kEntryRoot && ent != kEntryDead) atomicAdd(&a.counters[20], (unsigned long long)(ent & 15u));
+    }
+    if (ent != kEntryRoot && ent != kEntryDead) {
+        RayCtx r;
+        ray_setup(r, o, d);
+        const uint32_t first = ent >> 4, n = ent & 15u;
+        if constexpr (B == kEntryCap) {
+            float4 b0[kEntryCap], b1[kEntryCap];
+#pragma unroll
+            for (uint32_t e = 0; e < kEntryCap; ++e)  // every load before the first test
+                if (e < n) { b0[e] = a.entItems[2u * (first + e)]; b1[e] = a.entItems[2u * (first + e) + 1u]; }
+#pragma unroll
+            for (uint32_t e = 0; e < kEntryCap; ++e) {
+                float tn;
+                code[e] = __float_as_uint(b0[e].x);
+                if (e < n && box_hit(r, b0[e].y, b1[e].x, b0[e].z, b1[e].y, b0[e].w, b1[e].z, TMin, TMax, tn))
+                    keep |= 1u << e;
+            }
+        } else {
+#pragma unroll
+        for (uint32_t e0 = 0; e0 < kEntryCap; e0 += B) {
+            if (e0 >= n) break;
+            float4 b0[B], b1[B];
+#pragma unroll
+            for (uint32_t k = 0; k < B; ++k)  // every load of the batch before its first test
+                if (e0 + k < n) { b0[k] = a.entItems[2u * (first + e0 + k)]; b1[k] = a.entItems[2u * (first + e0 + k) + 1u]; }
+#pragma unroll
+            for (uint32_t k = 0; k < B; ++k) {
+                float tn;
+                code[e0 + k] = __float_as_uint(b0[k].x);
+                if (e0 + k < n && box_hit(r, b0[k].y, b1[k].x, b0[k].z, b1[k].y, b0[k].w, b1[k].z, TMin, TMax, tn))
+                    keep |= 1u << (e0 + k);
+            }
+        }
+        }
+        if (keep == 0u) ent = kEntryDead;
+    }
+    return ent != kEntryDead;
+}
+
+// Queue slots of a wave's live rays in partition `part` (every lane calls it; the queue is split in kQueueParts
+// partitions, each with its own counters: one counter word serialises ~90 atomics/us) -- with a.lpt the rays
+// longer than lptLen from the partition's front, the others from its back -- and their records + entry items.
+__device__ __forceinline__ uint32_t queue_live(const SDArgs& a, float4* __restrict__ queue, uint32_t* __restrict__ qctl,
+                                               uint32_t part, int lane, bool live, f3 d, float TMin, float TMax,
+                                               float cosT, uint32_t texel, uint32_t keep,
+                                               const uint32_t (&code)[kEntryCap]) {
+    const unsigned long long m = __ballot(live);
+    uint32_t slot;
+    if (a.lpt) {
+        // lptLen > 0: absolute interval length; < 0: relative to TMin
+        const bool isLong = live && TMax - TMin > (a.lptLen >= 0.0f ? a.lptLen : -a.lptLen * TMin);
+        const unsigned long long ml = __ballot(isLong), ms = m & ~ml;
+        const uint32_t nl = (uint32_t)__popcll(ml), ns = (uint32_t)__popcll(ms);
+        uint32_t bl = 0, bs = 0;
+        if (lane == 0 && nl) bl = atomicAdd(&qctl[part], nl);
+        if (lane == 0 && ns) bs = atomicAdd(&qctl[kQctlShort + part], ns);
+        bl = __shfl(bl, 0);
+        bs = __shfl(bs, 0);
+        const unsigned long long below = (1ull << lane) - 1ull;
+        slot = isLong ? part * a.partCap + bl + (uint32_t)__popcll(ml & below)
+                      : part * a.partCap + a.partCap - 1u - (bs + (uint32_t)__popcll(ms & below));
+    } else {
+        uint32_t base = 0;
+        if (lane == 0 && m) base = atomicAdd(&qctl[part], (uint32_t)__popcll(m));
+        base = __shfl(base, 0);
+        slot = part * a.partCap + base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+    }
+    if (live) {
+        // record word 7: the number of entry items stored to entQ (0: walk from the root)
+        queue[2u * slot] = make_float4(d.x, d.y, d.z, TMin);
+        queue[2u * slot + 1u] = make_float4(TMax, cosT, __uint_as_float(texel), __uint_as_float(__popc(keep)));
+#pragma unroll
+        for (uint32_t e = 0; e < kEntryCap; ++e)
+            if ((keep >> e) & 1u) a.entQ[(size_t)slot * kEntryCap + __popc(keep & ((1u << e) - 1u))] = code[e];
+    }
+    return slot;
+}
+
 // Phase 1 (rayGen up to TraceRay): one lane per SD texel of the band.  Rays whose interval
 // is empty keep DEFAULT_DEPTH and are written here; the others are appended to a compact
 // queue of ray records (one atomic per wave) so that phase 2 runs full waves of live rays
@@ -686,7 +786,7 @@ __global__ void __launch_bounds__(kSetupWaves * kBlock) sd_setup_kernel(SDArgs a
     const bool tileIn = tileX < tilesX;
     const uint32_t tilePrev = a.tileState && tileIn ? a.tileState[(size_t)tileRow * tilesX + tileX] : 0u;
     bool live = false, culled = false;
-    uint32_t ent = kEntryRoot, keep = 0u;  // keep: the frontier items the ray passes
+    uint32_t keep = 0u;                    // keep: the frontier items the ray passes
     uint32_t code[kEntryCap];              // their item codes
     f3 d = mk(0.0f, 0.0f, 0.0f);
     float TMin = 0.0f, TMax = 0.0f, cosT = 0.0f;
@@ -702,35 +802,9 @@ __global__ void __launch_bounds__(kSetupWaves * kBlock) sd_setup_kernel(SDArgs a
             a.rayMinW[(size_t)y * a.sdW + x] = 0x7f7fffffu;
             a.rayMaxW[(size_t)y * a.sdW + x] = 0u;
         }
-        if (live && a.entOn) {
-            const f3 o = mk(a.cam.posW[0], a.cam.posW[1], a.cam.posW[2]);
-            ent = entry_lookup(a, o, d, TMin, TMax);
-            if (a.counters) {  // roofline bytes of the lookup (rsd_counters.entry_*)
-                atomicAdd(&a.counters[19], 1ull);
-                if (ent != kEntryRoot && ent != kEntryDead) atomicAdd(&a.counters[20], (unsigned long long)(ent & 15u));
-            }
-            if (ent != kEntryRoot && ent != kEntryDead) {
-                // the frontier items whose boxes the ray passes (the walk's own child test)
-                RayCtx r;
-                ray_setup(r, o, d);
-                const uint32_t first = ent >> 4, n = ent & 15u;
-                float4 b0[kEntryCap], b1[kEntryCap];
-#pragma unroll
-                for (uint32_t e = 0; e < kEntryCap; ++e)  // every load before the first test
-                    if (e < n) { b0[e] = a.entItems[2u * (first + e)]; b1[e] = a.entItems[2u * (first + e) + 1u]; }
-#pragma unroll
-                for (uint32_t e = 0; e < kEntryCap; ++e) {
-                    float tn;
-                    code[e] = __float_as_uint(b0[e].x);
-                    if (e < n && box_hit(r, b0[e].y, b1[e].x, b0[e].z, b1[e].y, b0[e].w, b1[e].z, TMin, TMax, tn))
-                        keep |= 1u << e;
-                }
-                if (keep == 0u) ent = kEntryDead;
-            }
-            if (ent == kEntryDead) {  // a live interval that can hit nothing: DEFAULT_DEPTH, no walk
-                live = false;
-                culled = true;
-            }
+        if (live && a.entOn && !entry_frontier(a, d, TMin, TMax, keep, code)) {
+            live = false;  // a live interval that can hit nothing: DEFAULT_DEPTH, no walk
+            culled = true;
         }
     }
     const unsigned long long m = __ballot(live);
@@ -753,35 +827,8 @@ __global__ void __launch_bounds__(kSetupWaves * kBlock) sd_setup_kernel(SDArgs a
     // with its own counter: one counter word serialises ~90 atomics/us.
     const uint32_t lin = blockIdx.y * (uint32_t)tilesX + (uint32_t)tileX;
     const uint32_t part = lin % kQueueParts;
-    uint32_t slot;
-    if (a.lpt) {
-        // lptLen > 0: absolute interval length; < 0: relative to TMin
-        const bool isLong = live && TMax - TMin > (a.lptLen >= 0.0f ? a.lptLen : -a.lptLen * TMin);
-        const unsigned long long ml = __ballot(isLong), ms = m & ~ml;
-        const uint32_t nl = (uint32_t)__popcll(ml), ns = (uint32_t)__popcll(ms);
-        uint32_t bl = 0, bs = 0;
-        if (lane == 0 && nl) bl = atomicAdd(&qctl[part], nl);
-        if (lane == 0 && ns) bs = atomicAdd(&qctl[kQctlShort + part], ns);
-        bl = __shfl(bl, 0);
-        bs = __shfl(bs, 0);
-        const unsigned long long below = (1ull << lane) - 1ull;
-        slot = isLong ? part * a.partCap + bl + (uint32_t)__popcll(ml & below)
-                      : part * a.partCap + a.partCap - 1u - (bs + (uint32_t)__popcll(ms & below));
-    } else {
-        uint32_t base = 0;
-        if (lane == 0 && n) base = atomicAdd(&qctl[part], n);
-        base = __shfl(base, 0);
-        slot = part * a.partCap + base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-    }
-    if (live) {
-        // record word 7: the number of entry items stored to entQ (0: walk from the root)
-        queue[2u * slot] = make_float4(d.x, d.y, d.z, TMin);
-        queue[2u * slot + 1u] =
-            make_float4(TMax, cosT, __uint_as_float((uint32_t)y * (uint32_t)a.sdW + x), __uint_as_float(__popc(keep)));
-#pragma unroll
-        for (uint32_t e = 0; e < kEntryCap; ++e)
-            if ((keep >> e) & 1u) a.entQ[(size_t)slot * kEntryCap + __popc(keep & ((1u << e) - 1u))] = code[e];
-    }
+    const uint32_t slot = queue_live(a, queue, qctl, part, lane, live, d, TMin, TMax, cosT,
+                                     (uint32_t)y * (uint32_t)a.sdW + x, keep, code);
     if (a.counters && culled) atomicAdd(&a.counters[1], 1ull);  // still an active ray (rsd_counters)
     if (a.raster) {
         // the raster walk's inputs: slot map, the tile's view-depth range, empty key lists
@@ -810,6 +857,156 @@ __global__ void __launch_bounds__(kSetupWaves * kBlock) sd_setup_kernel(SDArgs a
 // The first chunk of each wave is static (blockIdx); later ones come from one atomic head
 // that starts after the static range, so a wave with no static chunk exits without an
 // atomic (one head word serialises ~90 dequeues/us, MI355X_MICROARCH.md "dequeue").
+
+// Two-pass setup (round 6; the full-resolution maps).  The one-pass setup evaluates each texel's
+// ray in the lane of its texel, so every wave that holds a live ray carries its lookup chain (the ray, the entry-grid
+// probe, the frontier boxes, the queue atomics: ~5 dependent round trips), and at configs[4] 258 K such waves pass
+// through 24 slots per CU -- 42 rounds of that chain.  Here pass A streams over the map with one light lane per
+// texel (interval words, the tiles' clean stamps, DEFAULT_DEPTH where no texel of a tile was touched and the tile is
+// not clean) and lists the touched texels -- rayMin lowered by pass 1 -- per queue partition (one atomic per
+// workgroup); pass B gives every listed texel a lane, densely, for the chain.  Same records, same stores: the
+// bits of the map are the one-pass setup's (a tile with touched but dead texels is stamped unknown instead of
+// clean: it is rewritten once more on its next trace, conservatively).
+constexpr int kClassWaves = 4;   // sd_classify_kernel: waves per workgroup
+constexpr int kClassTiles = 4;   // sd_classify_kernel: 8x8 tiles per wave (their loads in one round trip)
+constexpr int kLiveBlock = 256;  // sd_live_kernel: lanes per workgroup (4 waves)
+
+template <int N>
+__global__ void __launch_bounds__(kClassWaves * kBlock) sd_classify_kernel(SDArgs a, uint32_t* __restrict__ qctl,
+                                                                           uint32_t* __restrict__ qctlNext) {
+    if (blockIdx.x == 0 && blockIdx.y == 0)
+        for (int w = threadIdx.x; w < kQctlWords; w += kClassWaves * kBlock) qctlNext[w] = 0u;
+    __shared__ uint32_t sCount[kClassWaves + 1];
+    const int lane = threadIdx.x & (kBlock - 1), wave = (int)(threadIdx.x / kBlock);
+    const int tilesX = (a.sdW + kTile - 1) / kTile;
+    const int tileX0 = ((int)blockIdx.x * kClassWaves + wave) * kClassTiles;  // the wave's kClassTiles tiles
+    const int tileRow = a.consume ? (int)blockIdx.y : (int)blockIdx.y * a.bandStep + a.bandStart;
+    const int y = tileRow * kTile + (lane / kTile);
+    const bool otherBand = a.consume && (tileRow < a.bandStart || (tileRow - a.bandStart) % a.bandStep != 0 ||
+                                         (tileRow - a.bandStart) / a.bandStep >= a.bandN);
+    // every load of the wave's texels and tile stamps first (one round trip for the kClassTiles tiles)
+    uint32_t rmin[kClassTiles], rmax[kClassTiles], prev[kClassTiles];
+#pragma unroll
+    for (int t = 0; t < kClassTiles; ++t) {
+        const int x = (tileX0 + t) * kTile + (lane & (kTile - 1));
+        const bool inside = x < a.sdW && y < a.sdH;
+        const size_t o = (size_t)y * a.sdW + x;
+        rmin[t] = inside ? a.rayMin[o] : 0x7f7fffffu;
+        rmax[t] = inside && a.consume ? a.rayMax[o] : 0u;
+        prev[t] = a.tileState && !otherBand && tileX0 + t < tilesX ? a.tileState[(size_t)tileRow * tilesX + tileX0 + t] : 0u;
+    }
+    if (otherBand) {
+        // other bands' rows: the intervals are reset only (sd_setup_kernel)
+#pragma unroll
+        for (int t = 0; t < kClassTiles; ++t) {
+            const int x = (tileX0 + t) * kTile + (lane & (kTile - 1));
+            const size_t o = (size_t)y * a.sdW + x;
+            if (x < a.sdW && y < a.sdH && (rmin[t] != 0x7f7fffffu || rmax[t] != 0u)) {
+                a.rayMinW[o] = 0x7f7fffffu;
+                a.rayMaxW[o] = 0u;
+            }
+        }
+        return;  // uniform over the workgroup
+    }
+    const float DEFAULT = a.normalize ? 1.0f : 3.40282347e+37f;  // Common.slangh:16
+    unsigned long long m[kClassTiles];
+    uint32_t waveCount = 0;
+#pragma unroll
+    for (int t = 0; t < kClassTiles; ++t) {
+        const int x = (tileX0 + t) * kTile + (lane & (kTile - 1));
+        const bool inside = x < a.sdW && y < a.sdH;
+        const size_t o = (size_t)y * a.sdW + x;
+        const bool touched = inside && rmin[t] != 0x7f7fffffu;  // (a.deadFast: an untouched texel's ray is dead)
+        // consume: untouched words not at their reset values are reset here; pass B resets the touched ones after
+        // reading them
+        if (a.consume && inside && !touched && rmax[t] != 0u) a.rayMaxW[o] = 0u;
+        m[t] = __ballot(touched);
+        waveCount += (uint32_t)__popcll(m[t]);
+        const bool clean = a.tileState && m[t] == 0ull && prev[t] == a.tileSig;
+        if (inside && !touched && !clean) {
+            float depths[N];
+#pragma unroll
+            for (int i = 0; i < N; ++i) depths[i] = DEFAULT;
+            sd_store<N>(a, x, y, depths);
+        }
+        if (a.tileState && tileX0 + t < tilesX && lane == 0) {  // a touched texel may turn live: the tile is unknown
+            const uint32_t now = m[t] == 0ull ? a.tileSig : 0u;
+            if (now != prev[t]) a.tileState[(size_t)tileRow * tilesX + tileX0 + t] = now;
+        }
+        if (a.counters) {
+            const unsigned long long in = __ballot(inside);
+            if (lane == 0) atomicAdd(&a.counters[0], (unsigned long long)__popcll(in));
+            if (clean && lane == 0) atomicAdd(&a.counters[25], (unsigned long long)__popcll(in));
+        }
+    }
+    // the touched texels of the workgroup: one atomic on its partition's list counter
+    if (lane == 0) sCount[wave] = waveCount;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t tot = 0;
+        for (int w = 0; w < kClassWaves; ++w) { const uint32_t c = sCount[w]; sCount[w] = tot; tot += c; }
+        const uint32_t part = (blockIdx.y * gridDim.x + blockIdx.x) % kQueueParts;
+        sCount[kClassWaves] = tot ? part * a.touchCap + atomicAdd(&qctl[kQctlTouch + part], tot) : 0u;
+    }
+    __syncthreads();
+    uint32_t at = sCount[kClassWaves] + sCount[wave];
+    const unsigned long long below = (1ull << lane) - 1ull;
+#pragma unroll
+    for (int t = 0; t < kClassTiles; ++t) {
+        if ((m[t] >> lane) & 1ull)
+            a.touchList[at + (uint32_t)__popcll(m[t] & below)] =
+                (uint32_t)y * (uint32_t)a.sdW + (uint32_t)((tileX0 + t) * kTile + (lane & (kTile - 1)));
+        at += (uint32_t)__popcll(m[t]);
+    }
+}
+
+// Pass B: lane i of list partition p's texels (blocks b with b % kQueueParts == p stride over them).  A list partition
+// holds whole classify workgroups (128 x 8-texel strips), so the rays of one cluster of long segments would share a
+// queue partition -- and the static rows of the walk that read it; the wave of 64 listed texels c therefore appends to
+// queue partition (p + c) % kQueueParts (one-pass setup: tile t -> t % kQueueParts), which holds at most
+// touchCap + 2 * 64 * kQueueParts rays (partCap covers that).
+template <int N>
+__global__ void __launch_bounds__(kLiveBlock) sd_live_kernel(SDArgs a, float4* __restrict__ queue,
+                                                             uint32_t* __restrict__ qctl) {
+    const uint32_t part = blockIdx.x % kQueueParts, blocksPerPart = gridDim.x / kQueueParts;
+    const uint32_t count = min(__hip_atomic_load(&qctl[kQctlTouch + part], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                               a.touchCap);
+    const int lane = threadIdx.x & (kBlock - 1);
+    const float DEFAULT = a.normalize ? 1.0f : 3.40282347e+37f;  // Common.slangh:16
+    for (uint32_t base = (blockIdx.x / kQueueParts) * kLiveBlock; base < count; base += blocksPerPart * kLiveBlock) {
+        const uint32_t i = base + threadIdx.x;  // (wave-uniform loop: every lane of a wave reaches the ballots)
+        bool live = false, culled = false;
+        uint32_t keep = 0u, code[kEntryCap];
+        f3 d = mk(0.0f, 0.0f, 0.0f);
+        float TMin = 0.0f, TMax = 0.0f, cosT = 0.0f;
+        uint32_t texel = 0u;
+        int x = 0, y = 0;
+        if (i < count) {
+            texel = a.touchList[part * a.touchCap + i];
+            x = (int)(texel % (uint32_t)a.sdW);
+            y = (int)(texel / (uint32_t)a.sdW);
+            live = sd_ray(a, x, y, d, TMin, TMax, cosT);
+            if (a.consume) {  // after the last read of this texel's interval
+                a.rayMinW[texel] = 0x7f7fffffu;
+                a.rayMaxW[texel] = 0u;
+            }
+            if (live && a.entOn && !entry_frontier<kEntryCap / 2>(a, d, TMin, TMax, keep, code)) {
+                live = false;
+                culled = true;
+            }
+            if (!live) {
+                float depths[N];
+#pragma unroll
+                for (int k = 0; k < N; ++k) depths[k] = DEFAULT;
+                sd_store<N>(a, x, y, depths);
+            }
+        }
+        const uint32_t qpart = (part + (base + threadIdx.x - (uint32_t)lane) / (uint32_t)kBlock) % kQueueParts;
+        queue_live(a, queue, qctl, qpart, lane, live, d, TMin, TMax, cosT, texel, keep, code);
+        if (a.counters && culled) atomicAdd(&a.counters[1], 1ull);  // still an active ray (rsd_counters)
+    }
+}
+
 template <int K, int N, bool SPEC = false, bool CNT = false>
 __device__ __forceinline__ void sd_trace_queue_body(const SDArgs& a, const float4* __restrict__ queue,
                                                     uint32_t* __restrict__ qctl, uint32_t* sQuadStack, uint32_t bid,
@@ -2196,8 +2393,16 @@ static hipError_t launch_sd_kn(const SDArgs& a, dim3 grid, uint32_t persistentBl
                                uint2* keys, int walk, int pool, hipStream_t s) {
     constexpr int ROW = K <= 8 ? 8 : 16;
     uint32_t* qctlNext = a.qctlNext;
-    const dim3 sgrid((grid.x + kSetupWaves - 1) / kSetupWaves, grid.y);
-    hipLaunchKernelGGL((sd_setup_kernel<N>), sgrid, dim3(kSetupWaves * kBlock), 0, s, a, queue, qctl, qctlNext);
+    if (a.touchList) {  // the two-pass setup
+        const dim3 cgrid((grid.x + kClassWaves * kClassTiles - 1) / (kClassWaves * kClassTiles), grid.y);
+        hipLaunchKernelGGL((sd_classify_kernel<N>), cgrid, dim3(kClassWaves * kBlock), 0, s, a, qctl, qctlNext);
+        hipError_t e0 = hipGetLastError();
+        if (e0 != hipSuccess) return e0;
+        hipLaunchKernelGGL((sd_live_kernel<N>), dim3(a.liveBlocks), dim3(kLiveBlock), 0, s, a, queue, qctl);
+    } else {
+        const dim3 sgrid((grid.x + kSetupWaves - 1) / kSetupWaves, grid.y);
+        hipLaunchKernelGGL((sd_setup_kernel<N>), sgrid, dim3(kSetupWaves * kBlock), 0, s, a, queue, qctl, qctlNext);
+    }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const dim3 pg(persistentBlocks), wb(kBlock);
@@ -2537,6 +2742,12 @@ rsd_status sd_trace_impl(rsd_scene* scene, const rsd_camera* cam, const rsd_sd_p
     const uint32_t need = p->implementation == RSD_SD_COVERAGE_MASK ? 8u : p->max_count;
     const uint32_t setupBlocks = grid.x * grid.y;
     a.partCap = (setupBlocks + kQueueParts - 1) / kQueueParts * (uint32_t)kBlock;
+    // the two-pass setup's touched-texel lists: a partition holds the texels of its classify workgroups (and its
+    // queue partition those texels' rays: partCap covers both)
+    constexpr uint32_t kClassTilesPerBlock = kClassWaves * kClassTiles;
+    const uint32_t classBlocks = (grid.x + kClassTilesPerBlock - 1) / kClassTilesPerBlock * grid.y;
+    const uint32_t touchCap = (classBlocks + kQueueParts - 1) / kQueueParts * (kClassTilesPerBlock * (uint32_t)kBlock);
+    a.partCap = std::max(a.partCap, touchCap + 2u * (uint32_t)kBlock * kQueueParts);
     // live-ray queue workspace (grow-only; the first call of a larger map allocates)
     const size_t need_q = std::max(((size_t)(sd_w + kTile - 1) / kTile * ((sd_h + kTile - 1) / kTile) + kQueueParts) * kBlock,
                                    (size_t)a.partCap * kQueueParts);
@@ -2545,14 +2756,16 @@ rsd_status sd_trace_impl(rsd_scene* scene, const rsd_camera* cam, const rsd_sd_p
     const bool split = p->implementation != RSD_SD_COVERAGE_MASK && p->max_count <= K;
     const size_t queueBytes = need_q * 32, keyBytes = split ? need_q * K * sizeof(uint2) : 0;
     const size_t entBytes = scene->d_entry ? need_q * kEntryCap * sizeof(uint32_t) : 0;
-    if (ws->queue_cap < queueBytes + keyBytes + entBytes) {
+    const size_t touchBytes = (size_t)touchCap * kQueueParts * sizeof(uint32_t);
+    if (ws->queue_cap < queueBytes + keyBytes + entBytes + touchBytes) {
         RSD_HIP(hipStreamSynchronize(s));
         (void)hipFree(ws->queue);
         ws->queue = nullptr;
         ws->queue_cap = 0;
-        RSD_HIP(hipMalloc(&ws->queue, queueBytes + keyBytes + entBytes));
-        ws->queue_cap = queueBytes + keyBytes + entBytes;
+        RSD_HIP(hipMalloc(&ws->queue, queueBytes + keyBytes + entBytes + touchBytes));
+        ws->queue_cap = queueBytes + keyBytes + entBytes + touchBytes;
     }
+    uint32_t* touchList = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(ws->queue) + queueBytes + keyBytes + entBytes);
     float4* queue = reinterpret_cast<float4*>(ws->queue);
     uint2* keys = reinterpret_cast<uint2*>(reinterpret_cast<char*>(ws->queue) + queueBytes);
     if (entBytes) a.entQ = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(ws->queue) + queueBytes + keyBytes);
@@ -2628,6 +2841,23 @@ rsd_status sd_trace_impl(rsd_scene* scene, const rsd_camera* cam, const rsd_sd_p
         const bool off = lptEnv && std::string(lptEnv) == "off";
         a.lpt = off ? 0u : 1u;
         a.lptLen = lptEnv && *lptEnv && !off ? (float)std::atof(lptEnv) : -0.1f;
+    }
+    // two-pass setup (sd_classify_kernel + sd_live_kernel) for the full-resolution maps, where the one-pass setup's
+    // live-ray chains pass through the machine in tens of rounds: configs[2] setup 66 -> 45 us, trace 177 -> 154 us;
+    // configs[4] 202 -> 152 us, 551 -> 487 us at the static pose, 0.989 -> 0.922 ms along the orbit
+    // (profiles/round6/setup_twopass/).  The 1/4-resolution maps keep the one-pass setup: configs[1] 67 -> 72 us (one
+    // round of the chain there: the second launch costs more than it saves), configs[3] (1.0 M texels) 197 -> 215 us
+    // (the setup flat, the hybrid walk slower with the listed order of its rays).  Above 2 M texels;
+    // RSD_SETUP_TWOPASS = on | off overrides (A/B runs, tests of small maps).
+    {
+        const char* tpEnv = std::getenv("RSD_SETUP_TWOPASS");
+        const bool force = tpEnv && std::string(tpEnv) == "on", never = tpEnv && std::string(tpEnv) == "off";
+        if (a.deadFast && walk != 4 && a.diag == 0u && !never && (force || bandTexels > 2000000u)) {
+            a.touchList = touchList;
+            a.touchCap = touchCap;
+            // the resident grid: 5 workgroups of 4 waves per CU (92-94 VGPRs: 5 waves per SIMD), rounded to the partitions
+            a.liveBlocks = ((uint32_t)std::max(1, scene->dev->cu_count) * 5u + kQueueParts - 1) / kQueueParts * kQueueParts;
+        }
     }
     if (walk == 4) {
         const uint32_t tilesW = (sd_w + kTile - 1) / kTile, tilesH = (sd_h + kTile - 1) / kTile;

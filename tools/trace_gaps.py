@@ -14,6 +14,18 @@ path = next(Path(sys.argv[1]).rglob("*kernel_trace.csv"))
 rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
 ks = [(r["Kernel_Name"], int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in rows]
 setup = [(s, e) for n, s, e in ks if "sd_setup_kernel" in n]
+# the two-pass setup (sd_classify_kernel + sd_live_kernel): one setup span from the classify start to the live end
+cls = [(s, e) for n, s, e in ks if "sd_classify_kernel" in n]
+live = [(s, e) for n, s, e in ks if "sd_live_kernel" in n]
+if cls:
+    setup = []
+    for s0, e0 in cls:
+        nl = next(((s, e) for s, e in live if s >= e0), None)
+        if nl:
+            setup.append((s0, nl[1]))
+    lk = [(e - s) / 1e3 for s, e in live][2:]
+    ck = [(e - s) / 1e3 for s, e in cls][2:]
+    print(json.dumps({"classify_us": round(statistics.median(ck), 2), "live_us": round(statistics.median(lk), 2)}))
 walk = [(n, s, e) for n, s, e in ks if "sd_trace_row_kernel" in n or "sd_trace_queue_kernel" in n or
         "sd_trace_hybrid_kernel" in n]
 pairs = []
