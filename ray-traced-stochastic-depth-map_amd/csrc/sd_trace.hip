@@ -110,6 +110,7 @@ struct SDArgs {
     uint32_t touchCap;
     uint32_t liveBlocks;  // sd_live_kernel's grid (a multiple of kQueueParts)
     uint32_t rowPrio;          // hybrid walk: issue priority of the row blocks' waves (s_setprio; A/B, RSD_TRACE_ROWPRIO)
+    uint32_t prio;             // issue priority of every setup and walk wave (s_setprio; A/B, RSD_TRACE_PRIO)
     // clean tiles (rsd_sd_params.d_tile_state): per 8x8 tile, tileSig when the last trace left every texel it
     // wrote at DEFAULT_DEPTH (0: unknown); such a tile without a live ray is not rewritten
     uint32_t* tileState;
@@ -759,6 +760,7 @@ template <int N>
 __global__ void __launch_bounds__(kSetupWaves * kBlock) sd_setup_kernel(SDArgs a, float4* __restrict__ queue,
                                                                         uint32_t* __restrict__ qctl,
                                                                         uint32_t* __restrict__ qctlNext) {
+    if (a.prio) __builtin_amdgcn_s_setprio(2);
     if (blockIdx.x == 0 && blockIdx.y == 0)
         for (int w = threadIdx.x; w < kQctlWords; w += kSetupWaves * kBlock) qctlNext[w] = 0u;
     if (a.diag == 1u) return;
@@ -868,7 +870,10 @@ __global__ void __launch_bounds__(kSetupWaves * kBlock) sd_setup_kernel(SDArgs a
 // bits of the map are the one-pass setup's (a tile with touched but dead texels is stamped unknown instead of
 // clean: it is rewritten once more on its next trace, conservatively).
 constexpr int kClassWaves = 4;   // sd_classify_kernel: waves per workgroup
-constexpr int kClassTiles = 4;   // sd_classify_kernel: 8x8 tiles per wave (their loads in one round trip)
+#ifndef RSD_CLASS_TILES
+#define RSD_CLASS_TILES 4
+#endif
+constexpr int kClassTiles = RSD_CLASS_TILES;  // sd_classify_kernel: 8x8 tiles per wave (their loads in one round trip)
 constexpr int kLiveBlock = 256;  // sd_live_kernel: lanes per workgroup (4 waves)
 
 template <int N>
@@ -923,7 +928,11 @@ __global__ void __launch_bounds__(kClassWaves * kBlock) sd_classify_kernel(SDArg
         m[t] = __ballot(touched);
         waveCount += (uint32_t)__popcll(m[t]);
         const bool clean = a.tileState && m[t] == 0ull && prev[t] == a.tileSig;
+#ifdef RSD_DIAG_CLASSIFY_NOSTORE
+        if (false) {  // diagnostics (results wrong by design): the classify pass without its DEFAULT_DEPTH stores
+#else
         if (inside && !touched && !clean) {
+#endif
             float depths[N];
 #pragma unroll
             for (int i = 0; i < N; ++i) depths[i] = DEFAULT;
@@ -965,8 +974,11 @@ __global__ void __launch_bounds__(kClassWaves * kBlock) sd_classify_kernel(SDArg
 // queue partition -- and the static rows of the walk that read it; the wave of 64 listed texels c therefore appends to
 // queue partition (p + c) % kQueueParts (one-pass setup: tile t -> t % kQueueParts), which holds at most
 // touchCap + 2 * 64 * kQueueParts rays (partCap covers that).
+#ifndef RSD_LIVE_WAVES
+#define RSD_LIVE_WAVES 1
+#endif
 template <int N>
-__global__ void __launch_bounds__(kLiveBlock) sd_live_kernel(SDArgs a, float4* __restrict__ queue,
+__global__ void __launch_bounds__(kLiveBlock) __attribute__((amdgpu_waves_per_eu(RSD_LIVE_WAVES))) sd_live_kernel(SDArgs a, float4* __restrict__ queue,
                                                              uint32_t* __restrict__ qctl) {
     const uint32_t part = blockIdx.x % kQueueParts, blocksPerPart = gridDim.x / kQueueParts;
     const uint32_t count = min(__hip_atomic_load(&qctl[kQctlTouch + part], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
@@ -2040,7 +2052,7 @@ __global__ void __launch_bounds__(kBlock) sd_trace_hybrid_kernel(SDArgs a, const
                                                                  uint32_t* __restrict__ qctl, uint2* __restrict__ keys) {
     extern __shared__ uint32_t sDyn[];
     const uint32_t rb = a.hybridRowBlocks;
-    if (blockIdx.x < rb && a.rowPrio) __builtin_amdgcn_s_setprio(2);  // (neutral at configs[1]-[3]: trace_ab/prio_*)
+    if ((blockIdx.x < rb && a.rowPrio) || a.prio) __builtin_amdgcn_s_setprio(2);  // (rowPrio: neutral, trace_ab/prio_*)
     if (blockIdx.x < rb)
         sd_trace_row_body<K, N, ROW, false, false, POOL, true>(
             a, queue, qctl, keys, sDyn, reinterpret_cast<float*>(sDyn + (kBlock / ROW) * POOL), blockIdx.x, rb, 1u);
@@ -2614,6 +2626,10 @@ rsd_status sd_trace_impl(rsd_scene* scene, const rsd_camera* cam, const rsd_sd_p
     }
     SDArgs a{};
     a.nodes = scene->d_nodes;
+    {
+        const char* pEnv = std::getenv("RSD_TRACE_PRIO");  // A/B runs: the trace's waves ahead of other frames' passes
+        a.prio = pEnv && std::string(pEnv) == "on" ? 1u : 0u;
+    }
     a.tris = scene->d_tris;
     a.triOff = scene->tri_offset;
     a.cam = *cam;
@@ -2856,7 +2872,8 @@ rsd_status sd_trace_impl(rsd_scene* scene, const rsd_camera* cam, const rsd_sd_p
             a.touchList = touchList;
             a.touchCap = touchCap;
             // the resident grid: 5 workgroups of 4 waves per CU (92-94 VGPRs: 5 waves per SIMD), rounded to the partitions
-            a.liveBlocks = ((uint32_t)std::max(1, scene->dev->cu_count) * 5u + kQueueParts - 1) / kQueueParts * kQueueParts;
+            const uint32_t perCu = RSD_LIVE_WAVES > 5 ? (uint32_t)RSD_LIVE_WAVES : 5u;
+            a.liveBlocks = ((uint32_t)std::max(1, scene->dev->cu_count) * perCu + kQueueParts - 1) / kQueueParts * kQueueParts;
         }
     }
     if (walk == 4) {
