@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define RSD_ABI_VERSION 7
+#define RSD_ABI_VERSION 8
 
 typedef enum {
     RSD_OK = 0,
@@ -128,8 +128,9 @@ typedef struct {
                                 N <= 4; d_sd_out then holds IEEE binary16 (round to nearest even) */
     uint32_t* d_tile_state;  /* NULL, or rsd_sd_tile_state_count(sd_w, sd_h) device words owned with d_sd_out
                                 (librsd extension, DESIGN.md 4 "clean tiles"): the trace records per 8x8 SD tile
-                                whether it left every texel of the tile it wrote at DEFAULT_DEPTH, and does not
-                                rewrite such a tile while it has no live ray.  The caller zeroes the words when
+                                whether it left every texel of the tile it wrote at DEFAULT_DEPTH -- since ABI v8
+                                also which texels (a 64-bit mask per tile after the tiles' stamps) -- and does not
+                                rewrite those texels while they have no live ray.  The caller zeroes the words when
                                 it allocates the map, writes the map itself, or changes which texels its traces
                                 own (a band split); the map's bits are those of a trace without it. */
 } rsd_sd_params;
@@ -337,7 +338,7 @@ rsd_status rsd_sd_trace(rsd_scene* scene, const rsd_camera* cam, const rsd_sd_pa
                         rsd_counters* counters, rsd_stream stream);
 
 /* SVAO.cpp:330-341: rayMax <- 0, rayMin <- asuint(FLT_MAX) */
-/* Words of rsd_sd_params.d_tile_state for an sd_w x sd_h map: one per 8x8 tile. */
+/* Words of rsd_sd_params.d_tile_state for an sd_w x sd_h map: three per 8x8 tile (a stamp; since ABI v8 a texel mask). */
 uint32_t rsd_sd_tile_state_count(uint32_t sd_w, uint32_t sd_h);
 rsd_status rsd_svao_clear_intervals(uint32_t* d_ray_min, uint32_t* d_ray_max, uint32_t count, rsd_stream stream);
 

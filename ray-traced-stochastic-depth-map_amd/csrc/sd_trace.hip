@@ -115,6 +115,7 @@ struct SDArgs {
     // wrote at DEFAULT_DEPTH (0: unknown); such a tile without a live ray is not rewritten
     uint32_t* tileState;
     uint32_t tileSig;
+    uint32_t tileCount;  // 8x8 tiles of the map: the texel masks follow the stamps in tileState (2 words per tile)
     // segment entry grid (entry_grid.h, canonical walks): the setup kernel looks up the frontier of
     // each live ray's segment and copies its items to entQ[slot * kEntryCap ..]
     uint32_t entOn;
@@ -131,6 +132,10 @@ struct SDArgs {
     // trace with an empty queue), 2 no texel is live (the setup's streaming part without the live rays' chains)
     uint32_t diag;
 };
+
+// tile stamp of a tile whose texel mask (the words after the stamps in tileState) names the texels the last trace left
+// at DEFAULT_DEPTH (sd_classify_kernel; the one-pass setup treats it as unknown and rewrites the tile)
+constexpr uint32_t kTileMaskSig = 0x100u;
 
 // entry_lookup results besides first << 4 | count
 constexpr uint32_t kEntryRoot = 0u;           // walk from the root
@@ -890,7 +895,7 @@ __global__ void __launch_bounds__(kClassWaves * kBlock) sd_classify_kernel(SDArg
     const bool otherBand = a.consume && (tileRow < a.bandStart || (tileRow - a.bandStart) % a.bandStep != 0 ||
                                          (tileRow - a.bandStart) / a.bandStep >= a.bandN);
     // every load of the wave's texels and tile stamps first (one round trip for the kClassTiles tiles)
-    uint32_t rmin[kClassTiles], rmax[kClassTiles], prev[kClassTiles];
+    uint32_t rmin[kClassTiles], rmax[kClassTiles], prev[kClassTiles], mlo[kClassTiles], mhi[kClassTiles];
 #pragma unroll
     for (int t = 0; t < kClassTiles; ++t) {
         const int x = (tileX0 + t) * kTile + (lane & (kTile - 1));
@@ -899,6 +904,10 @@ __global__ void __launch_bounds__(kClassWaves * kBlock) sd_classify_kernel(SDArg
         rmin[t] = inside ? a.rayMin[o] : 0x7f7fffffu;
         rmax[t] = inside && a.consume ? a.rayMax[o] : 0u;
         prev[t] = a.tileState && !otherBand && tileX0 + t < tilesX ? a.tileState[(size_t)tileRow * tilesX + tileX0 + t] : 0u;
+        // the tile's texel mask (stamp kSubSig: the texels the last trace left at DEFAULT_DEPTH), loaded with the stamp
+        const size_t mw = a.tileCount + 2u * ((size_t)tileRow * tilesX + tileX0 + t);
+        mlo[t] = a.tileState && !otherBand && tileX0 + t < tilesX ? a.tileState[mw] : 0u;
+        mhi[t] = a.tileState && !otherBand && tileX0 + t < tilesX ? a.tileState[mw + 1u] : 0u;
     }
     if (otherBand) {
         // other bands' rows: the intervals are reset only (sd_setup_kernel)
@@ -919,44 +928,61 @@ __global__ void __launch_bounds__(kClassWaves * kBlock) sd_classify_kernel(SDArg
 #pragma unroll
     for (int t = 0; t < kClassTiles; ++t) {
         const int x = (tileX0 + t) * kTile + (lane & (kTile - 1));
+        m[t] = __ballot(x < a.sdW && y < a.sdH && rmin[t] != 0x7f7fffffu);  // touched (a.deadFast: else dead)
+        waveCount += (uint32_t)__popcll(m[t]);
+    }
+    // the touched texels of the workgroup: one atomic on its partition's list counter, issued before the stores
+    // below so that its round trip overlaps them
+    if (lane == 0) sCount[wave] = waveCount;
+    __syncthreads();
+    uint32_t wgBase = 0, tot = 0;
+    if (threadIdx.x == 0) {
+        for (int w = 0; w < kClassWaves; ++w) { const uint32_t c = sCount[w]; sCount[w] = tot; tot += c; }
+        if (tot) wgBase = atomicAdd(&qctl[kQctlTouch + (blockIdx.y * gridDim.x + blockIdx.x) % kQueueParts], tot);
+    }
+#pragma unroll
+    for (int t = 0; t < kClassTiles; ++t) {
+        const int x = (tileX0 + t) * kTile + (lane & (kTile - 1));
         const bool inside = x < a.sdW && y < a.sdH;
         const size_t o = (size_t)y * a.sdW + x;
-        const bool touched = inside && rmin[t] != 0x7f7fffffu;  // (a.deadFast: an untouched texel's ray is dead)
+        const bool touched = (m[t] >> lane) & 1ull;
         // consume: untouched words not at their reset values are reset here; pass B resets the touched ones after
         // reading them
         if (a.consume && inside && !touched && rmax[t] != 0u) a.rayMaxW[o] = 0u;
-        m[t] = __ballot(touched);
-        waveCount += (uint32_t)__popcll(m[t]);
         const bool clean = a.tileState && m[t] == 0ull && prev[t] == a.tileSig;
+        // per-texel: the last trace left this texel at DEFAULT_DEPTH (a whole-tile stamp, or the tile's mask)
+        const uint64_t mask = ((uint64_t)mhi[t] << 32) | mlo[t];
+        const bool known = a.tileState && (prev[t] == a.tileSig || (prev[t] == (a.tileSig | kTileMaskSig) && ((mask >> lane) & 1ull)));
 #ifdef RSD_DIAG_CLASSIFY_NOSTORE
         if (false) {  // diagnostics (results wrong by design): the classify pass without its DEFAULT_DEPTH stores
 #else
-        if (inside && !touched && !clean) {
+        if (inside && !touched && !known) {
 #endif
             float depths[N];
 #pragma unroll
             for (int i = 0; i < N; ++i) depths[i] = DEFAULT;
             sd_store<N>(a, x, y, depths);
         }
-        if (a.tileState && tileX0 + t < tilesX && lane == 0) {  // a touched texel may turn live: the tile is unknown
-            const uint32_t now = m[t] == 0ull ? a.tileSig : 0u;
+        if (a.tileState && tileX0 + t < tilesX && lane == 0) {
+            // no touched texel: the whole tile is DEFAULT_DEPTH now; else its untouched texels are (a touched one may
+            // turn live: unknown), recorded in the tile's mask
+            const uint32_t now = m[t] == 0ull ? a.tileSig : (a.tileSig | kTileMaskSig);
             if (now != prev[t]) a.tileState[(size_t)tileRow * tilesX + tileX0 + t] = now;
+            if (m[t] != 0ull) {
+                const uint64_t nm = ~m[t];
+                const size_t mw = a.tileCount + 2u * ((size_t)tileRow * tilesX + tileX0 + t);
+                if (prev[t] != now || (uint32_t)nm != mlo[t]) a.tileState[mw] = (uint32_t)nm;
+                if (prev[t] != now || (uint32_t)(nm >> 32) != mhi[t]) a.tileState[mw + 1u] = (uint32_t)(nm >> 32);
+            }
         }
         if (a.counters) {
-            const unsigned long long in = __ballot(inside);
+            const unsigned long long in = __ballot(inside), kept = __ballot(inside && !touched && known);
             if (lane == 0) atomicAdd(&a.counters[0], (unsigned long long)__popcll(in));
-            if (clean && lane == 0) atomicAdd(&a.counters[25], (unsigned long long)__popcll(in));
+            if (lane == 0) atomicAdd(&a.counters[25], (unsigned long long)__popcll(kept));
         }
     }
-    // the touched texels of the workgroup: one atomic on its partition's list counter
-    if (lane == 0) sCount[wave] = waveCount;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t tot = 0;
-        for (int w = 0; w < kClassWaves; ++w) { const uint32_t c = sCount[w]; sCount[w] = tot; tot += c; }
-        const uint32_t part = (blockIdx.y * gridDim.x + blockIdx.x) % kQueueParts;
-        sCount[kClassWaves] = tot ? part * a.touchCap + atomicAdd(&qctl[kQctlTouch + part], tot) : 0u;
-    }
+    if (threadIdx.x == 0)
+        sCount[kClassWaves] = tot ? ((blockIdx.y * gridDim.x + blockIdx.x) % kQueueParts) * a.touchCap + wgBase : 0u;
     __syncthreads();
     uint32_t at = sCount[kClassWaves] + sCount[wave];
     const unsigned long long below = (1ull << lane) - 1ull;
@@ -2697,6 +2723,7 @@ rsd_status sd_trace_impl(rsd_scene* scene, const rsd_camera* cam, const rsd_sd_p
     // clean tiles: the stamp names what DEFAULT_DEPTH looks like in this map (value, storage, layers)
     a.tileState = p->d_tile_state;
     a.tileSig = 1u | (p->normalize ? 2u : 0u) | (p->use_16bit ? 4u : 0u) | ((uint32_t)N << 3);
+    a.tileCount = ((sd_w + kTile - 1) / kTile) * ((sd_h + kTile - 1) / kTile);
     a.primRec = scene->d_prim_rec;
     a.entOn = 0u;
     a.entSlots = static_cast<const uint4*>(scene->d_entry);
@@ -3061,7 +3088,8 @@ extern "C" rsd_status rsd_sd_trace_band(rsd_scene* scene, const rsd_camera* cam,
 }
 
 extern "C" uint32_t rsd_sd_tile_state_count(uint32_t sd_w, uint32_t sd_h) {
-    return ((sd_w + kTile - 1) / kTile) * ((sd_h + kTile - 1) / kTile);
+    // per 8x8 tile a stamp word, then (ABI v8) per tile the two words of its 64-texel DEFAULT mask
+    return 3u * ((sd_w + kTile - 1) / kTile) * ((sd_h + kTile - 1) / kTile);
 }
 
 extern "C" rsd_status rsd_sd_trace(rsd_scene* scene, const rsd_camera* cam, const rsd_sd_params* p,

@@ -40,7 +40,7 @@ def test_library_exports_every_header_symbol(abi):
     exported = set(re.findall(r"\bT (rsd_\w+)", out))
     missing = [f for f in header_functions() if f not in exported]
     assert not missing, missing
-    assert abi.lib().rsd_abi_version() == 7
+    assert abi.lib().rsd_abi_version() == 8
 
 
 def test_struct_layouts_match_header(abi, tmp_path):
