@@ -510,6 +510,10 @@ def run_rank(args, grp, local, shared=None):
     alg_bytes = rays * (16 + 8) + (rays - texels_clean) * 4 * N + 128 * nodes_seq + 48 * tris_seq + entry_bytes
     achieved = alg_bytes / (seq_sd_ms * 1e-3) / 1e9
     kernels_seq = abi.WALK_KERNELS[walk_seq]
+    if r.sd_w * r.sd_h > 2_000_000 and walk_seq != abi.WALK_RASTER:
+        # the full-resolution maps' two-pass setup (sd_trace.hip: sd_classify_kernel + sd_live_kernel above 2 M
+        # texels) in place of the one-pass setup kernel
+        kernels_seq = ("sd_classify_kernel", "sd_live_kernel") + tuple(k for k in kernels_seq if k != "sd_setup_kernel")
     lat = latency_floor(cnt_seq, seq_sd_ms)
     if lat.get("latency_floor_us") is not None:
         # the step clocks come from the instrumented launch, which walks the row or quad walk alone -- for the hybrid
